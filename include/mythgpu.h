@@ -1,0 +1,211 @@
+/*
+ * mythgpu.h — C-ABI of the MI355X batched bit-vector evaluation engine.
+ *
+ * This is the drop-in boundary for ONE hot path of the reference
+ * (strawberrylady99/mythril v0.22.7): the satisfiability queries LASER sends to
+ * z3 through `get_model` (mythril/support/model.py:15-49) and the model
+ * evaluation z3 performs for `Model.eval` (mythril/laser/smt/model.py:45-59).
+ * The reference reaches z3 through z3py/ctypes (libz3); this library is loaded
+ * the same way (ctypes) by `mythril_amd/native.py`.
+ *
+ * Entry points and the reference interface each one replaces:
+ *
+ *   mg_init / mg_shutdown     z3 context creation (implicit in z3py import,
+ *                             mythril/laser/smt/solver/__init__.py:1-9)
+ *   mg_program_load           Solver.add / Optimize.add of the constraint list
+ *                             (mythril/laser/smt/solver/solver.py:28-45,
+ *                             mythril/support/model.py:38-39): the flattened
+ *                             SSA program of the whole conjunction
+ *   mg_search                 Optimize.check() for SAT instances
+ *                             (mythril/support/model.py:44,
+ *                             solver.py:47-57): first satisfying candidate index
+ *   mg_eval / mg_eval_generated
+ *                             ModelRef.eval(expr, model_completion=True)
+ *                             (mythril/laser/smt/model.py:45-59) batched over
+ *                             N assignments; also Solver.model() materialisation
+ *                             (solver.py:59-64) of a search hit
+ *   mg_keccak256              ethereum.utils.sha3 used for concrete SHA3
+ *                             (mythril/laser/ethereum/keccak_function_manager.py:44-57,
+ *                             mythril/analysis/solver.py:146)
+ *   mg_stats                  SolverStatistics (laser/smt/solver/solver_statistics.py:8-43)
+ *   mg_last_error             z3 exceptions -> here: an error string; the host
+ *                             maps any error to "unknown" (never to unsat)
+ *
+ * Conventions: every function returns 0 on success and a negative MG_E_* code on
+ * failure (no C++ exception crosses the ABI). Host buffers are caller-owned.
+ * Functions with the `_dev` suffix take device pointers already resident in HBM
+ * (used by the benchmark so that the timed region excludes PCIe).
+ * One process drives one GPU (one process per GPU; multi-GPU sharding and the
+ * first-hit all-reduce are done by the caller over RCCL).
+ */
+#ifndef MYTHGPU_H
+#define MYTHGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes ---------------------------------------------------- */
+#define MG_OK 0
+#define MG_E_INVALID (-1)      /* malformed program / argument */
+#define MG_E_UNSUPPORTED (-2)  /* operator or width outside the engine: fall back to z3 */
+#define MG_E_HIP (-3)          /* HIP runtime error */
+#define MG_E_NODEVICE (-4)     /* no usable gfx950 device */
+#define MG_E_NOMEM (-5)
+#define MG_E_NOTINIT (-6)
+
+/* ---- program format v1 ---------------------------------------------- *
+ * Little-endian uint32 words:
+ *   header[16]  : MG_MAGIC, MG_VERSION, n_nodes, n_roots, n_coords, n_tables,
+ *                 n_const_words, n_watch, 0...
+ *   nodes       : n_nodes x 8 words {op, width, a, b, c, p0, p1, p2}
+ *                 operands a/b/c are indices of EARLIER nodes (SSA order)
+ *   roots       : n_roots node indices (Bool nodes; the query is their AND)
+ *   coords      : n_coords x 4 words {width, kind, node, table}
+ *   tables      : n_tables x 4 words {kind, key_width, val_width, 0}
+ *   watch       : n_watch node indices whose values mg_eval dumps
+ *   consts      : n_const_words (little-endian 32-bit limbs)
+ * A value of width w occupies ceil(w/32) limbs, limb 0 least significant,
+ * unused high bits zero.  Bool = width 1.
+ */
+#define MG_MAGIC 0x3150474Du /* "MGP1" */
+#define MG_VERSION 1u
+#define MG_NONE 0xFFFFFFFFu
+#define MG_MAX_WIDTH 32768u
+
+enum mg_op {
+  MG_OP_CONST = 0,      /* p0 = const word offset */
+  MG_OP_VAR = 1,        /* p0 = coord index */
+  MG_OP_ADD = 2,
+  MG_OP_SUB = 3,
+  MG_OP_MUL = 4,
+  MG_OP_UDIV = 5,
+  MG_OP_UREM = 6,
+  MG_OP_SDIV = 7,
+  MG_OP_SREM = 8,
+  MG_OP_SMOD = 9,
+  MG_OP_AND = 10,
+  MG_OP_OR = 11,
+  MG_OP_XOR = 12,
+  MG_OP_NOT = 13,
+  MG_OP_NEG = 14,
+  MG_OP_SHL = 15,
+  MG_OP_LSHR = 16,
+  MG_OP_ASHR = 17,
+  MG_OP_CONCAT = 18,    /* a = high part, b = low part */
+  MG_OP_EXTRACT = 19,   /* p0 = lo; width = hi-lo+1 */
+  MG_OP_ZEXT = 20,
+  MG_OP_SEXT = 21,
+  MG_OP_ITE = 22,       /* a = Bool condition */
+  MG_OP_EQ = 23,
+  MG_OP_ULT = 24,
+  MG_OP_ULE = 25,
+  MG_OP_SLT = 26,
+  MG_OP_SLE = 27,
+  MG_OP_UMUL_NOOVF = 28,
+  MG_OP_ARR_VAR = 29,   /* array-sorted: p0 = table */
+  MG_OP_ARR_K = 30,     /* array-sorted: a = default value */
+  MG_OP_ARR_STORE = 31, /* array-sorted: a = array, b = index, c = value */
+  MG_OP_SELECT = 32,    /* a = array, b = index, p0 = coord of the base read (or MG_NONE) */
+  MG_OP_UFAPP = 33,     /* a = argument, p0 = table, p1 = coord */
+  MG_OP_KECCAK = 34,    /* a = data (or MG_NONE), p0 = byte length */
+  MG_OP_EXP = 35,
+  MG_OP_COUNT = 36
+};
+
+enum mg_coord_kind { MG_COORD_SCALAR = 0, MG_COORD_ARRAY_SITE = 1, MG_COORD_UF_SITE = 2 };
+enum mg_table_kind { MG_TABLE_ARRAY = 0, MG_TABLE_UF = 1 };
+
+/* ---- candidate generator (search mode) -------------------------------- *
+ * blob: header[4] {MG_GEN_MAGIC, n_coords, n_const_words, 0}
+ *       specs: n_coords x 8 words {kind, p0, p1, p2, p3, p4, p5, p6}
+ *       consts: n_const_words
+ * Coordinate c of candidate i is a pure function of (seed, i, c).
+ */
+#define MG_GEN_MAGIC 0x314E4547u /* "GEN1" */
+enum mg_gen_kind {
+  MG_GEN_UNIFORM = 0,  /* uniform over [0, 2^w) */
+  MG_GEN_RANGE = 1,    /* p0 = const offset of lo, p1 = span (0 => 2^32): lo + r mod span */
+  MG_GEN_DICT = 2,     /* p0 = const offset of n entries (ceil(w/32) limbs each), p1 = n */
+  MG_GEN_MIXED = 3,    /* p0/p1 = dict, p2 = P(dict) / 65536, p3 = copy-from coord (MG_NONE: none),
+                          p4 = P(copy) / 65536, p5 = P(+/-small delta on dict) / 65536,
+                          p6 = P(uniform but small: < 2^(p6>>16)) / 65536 in low 16 bits */
+  MG_GEN_ALIGNED = 4,  /* p0 = const offset of lo, p1 = log2(align), p2 = count (0 => 2^32) */
+  MG_GEN_FIXED = 5,    /* p0 = const offset of the value */
+  MG_GEN_LAZY = 6      /* site coords only: p0 = node whose value is the default (must precede the site) */
+};
+
+/* search flags */
+#define MG_SEARCH_EARLY_EXIT 1u   /* stop lanes past the current first hit; skip waves whose roots all failed */
+
+typedef struct mg_program_info {
+  uint32_t n_nodes, n_instrs, n_coords, n_roots;
+  uint32_t value_words;      /* per-lane value-file words after liveness allocation */
+  uint32_t uses_lds;         /* 1 if the value file lives in LDS */
+  uint32_t n_watch;
+  uint32_t watch_words;      /* sum of ceil(w/32) over watch nodes */
+  uint32_t coord_words;      /* sum of ceil(w/32) over coords (SoA rows of mg_eval input) */
+  uint32_t reserved;
+  uint64_t limb_ops;         /* algorithmic 32-bit limb ops per candidate (fixed cost table) */
+} mg_program_info_t;
+
+typedef struct mg_stats {
+  uint64_t programs_loaded;
+  uint64_t launches;
+  uint64_t candidates;       /* candidates evaluated (eval + search) */
+  uint64_t hits;
+  double kernel_ms_total;    /* HIP-event time of engine kernels on the engine stream */
+  double last_kernel_ms;     /* HIP-event time of the last launch */
+  uint64_t last_candidates;
+  uint32_t device;
+  uint32_t cu_count;
+  uint32_t clock_mhz;
+  uint32_t reserved;
+} mg_stats_t;
+
+int mg_init(uint32_t device_mask);
+void mg_shutdown(void);
+const char* mg_last_error(void);
+int mg_version(void);
+
+/* host-only checks (no GPU needed) */
+int mg_program_check(const uint8_t* ssa, size_t len, mg_program_info_t* info);
+
+int mg_program_load(const uint8_t* ssa, size_t len, uint64_t* prog_handle);
+int mg_program_info(uint64_t prog, mg_program_info_t* info);
+int mg_program_free(uint64_t prog);
+
+int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* gen_handle);
+int mg_gen_free(uint64_t gen);
+
+/* soa_coords: coord_words rows of n uint32 (row r = limb of a coordinate, coords in order)
+ * verdict_out: n bytes (0/1); watch_out (nullable): watch_words rows of n uint32 */
+int mg_eval(uint64_t prog, const uint32_t* soa_coords, uint64_t n, uint8_t* verdict_out, uint32_t* watch_out);
+int mg_eval_dev(uint64_t prog, const uint32_t* d_soa_coords, uint64_t n, uint8_t* d_verdict_out,
+                uint32_t* d_watch_out);
+int mg_eval_generated(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64_t n,
+                      uint8_t* verdict_out, uint32_t* watch_out);
+
+/* first_hit: lowest satisfying candidate index in [start, start+count), UINT64_MAX if none */
+int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags,
+              uint64_t* first_hit, uint64_t* n_hits);
+
+/* msgs: concatenated messages; lens: n byte lengths; out32: n x 32 bytes */
+int mg_keccak256(const uint8_t* msgs, const uint32_t* lens, uint64_t n, uint8_t* out32);
+
+int mg_stats(mg_stats_t* out);
+int mg_stats_reset(void);
+
+/* device buffer helpers for callers that keep inputs resident in HBM */
+int mg_dev_alloc(size_t bytes, void** dptr);
+int mg_dev_free(void* dptr);
+int mg_dev_upload(void* dptr, const void* src, size_t bytes);
+int mg_dev_download(void* dst, const void* dptr, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MYTHGPU_H */

@@ -1,0 +1,56 @@
+"""Build the in-tree native library ``mythril_amd/libmythgpu.so`` for gfx950.
+
+``hipcc --offload-arch=gfx950`` cross-compiles here (no GPU needed); the built
+``.so`` is git-ignored but travels to the GPU box with the tree snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+INCLUDE = PKG.parent / "include"
+LIB = PKG / "libmythgpu.so"
+
+SOURCES = [CSRC / "engine.hip", CSRC / "program.cpp"]
+HEADERS = [CSRC / "bv_device.h", CSRC / "keccak_device.h", CSRC / "program.hpp", INCLUDE / "mythgpu.h"]
+
+ARCH = os.environ.get("MYTHGPU_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build libmythgpu.so)")
+
+
+def stale() -> bool:
+    if not LIB.exists():
+        return True
+    t = LIB.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in SOURCES + HEADERS)
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    if not force and not stale():
+        return LIB
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-unused-result", "-o", str(LIB)] + [str(s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd[cmd.index("-o") + 1] = str(tmp)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-4000:]}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

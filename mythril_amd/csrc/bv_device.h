@@ -1,0 +1,347 @@
+// 256-bit (8 x 32-bit limb) bit-vector arithmetic in VGPRs for gfx950.
+//
+// All arrays are indexed with compile-time constants only (fully unrolled
+// loops), so they stay in registers: a runtime-indexed private array is
+// demoted to scratch on AMDGPU.  Per-lane data-dependent amounts (shift
+// counts, exponent bits) are handled with barrel stages and predication, never
+// with runtime register indexing.
+//
+// Semantics follow SMT-LIB QF_BV (what z3 evaluates for LASER's terms,
+// SURVEY.md §2.3): total division (x/0 = ~0, x%0 = x), shifts >= w saturate.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mg {
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+struct W8 {
+  u32 w[8];
+};
+
+__device__ __forceinline__ u32 top_mask(u32 width) {
+  u32 r = width & 31u;
+  return r ? ((1u << r) - 1u) : 0xFFFFFFFFu;
+}
+
+// mask limbs above `width` (width <= 256) to zero
+__device__ __forceinline__ void canon8(W8& x, u32 width) {
+  const u32 L = (width + 31u) >> 5;
+  const u32 tm = top_mask(width);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u32 v = x.w[i];
+    v = (u32)i < L ? v : 0u;
+    v = (u32)i == L - 1 ? (v & tm) : v;
+    x.w[i] = v;
+  }
+}
+
+__device__ __forceinline__ W8 add8(const W8& a, const W8& b) {
+  W8 r;
+  u64 c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u64 t = (u64)a.w[i] + b.w[i] + c;
+    r.w[i] = (u32)t;
+    c = t >> 32;
+  }
+  return r;
+}
+
+__device__ __forceinline__ W8 sub8(const W8& a, const W8& b, u32* borrow_out = nullptr) {
+  W8 r;
+  u64 br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u64 t = (u64)a.w[i] - b.w[i] - br;
+    r.w[i] = (u32)t;
+    br = (t >> 32) & 1u;
+  }
+  if (borrow_out) *borrow_out = (u32)br;
+  return r;
+}
+
+__device__ __forceinline__ W8 neg8(const W8& a) {
+  W8 z;
+#pragma unroll
+  for (int i = 0; i < 8; i++) z.w[i] = 0;
+  return sub8(z, a);
+}
+
+// low 256 bits of a*b (schoolbook, 36 partial products)
+__device__ __forceinline__ W8 mul8(const W8& a, const W8& b) {
+  W8 r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.w[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u64 c = 0;
+#pragma unroll
+    for (int j = 0; j < 8 - i; j++) {
+      u64 t = (u64)a.w[i] * b.w[j] + r.w[i + j] + c;
+      r.w[i + j] = (u32)t;
+      c = t >> 32;
+    }
+  }
+  return r;
+}
+
+// high 256 bits of the 512-bit product
+__device__ __forceinline__ W8 mulhi8(const W8& a, const W8& b) {
+  u32 r[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) r[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u64 c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      u64 t = (u64)a.w[i] * b.w[j] + r[i + j] + c;
+      r[i + j] = (u32)t;
+      c = t >> 32;
+    }
+    r[i + 8] = (u32)c;
+  }
+  W8 h;
+#pragma unroll
+  for (int i = 0; i < 8; i++) h.w[i] = r[i + 8];
+  return h;
+}
+
+__device__ __forceinline__ bool is_zero8(const W8& a) {
+  u32 o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= a.w[i];
+  return o == 0;
+}
+
+// a >= b (unsigned)
+__device__ __forceinline__ bool uge8(const W8& a, const W8& b) {
+  u32 br;
+  (void)sub8(a, b, &br);
+  return br == 0;
+}
+
+// Restoring division, 256 steps over the 512-bit pair (rem:quo); uniform trip
+// count (no lane divergence).  Invariant rem < b, so 2*rem+bit needs 257 bits:
+// the bit shifted out of rem is kept in `c`.
+__device__ __forceinline__ void udivrem8(const W8& a, const W8& b, W8& q, W8& r) {
+  W8 rem, quo = a;
+#pragma unroll
+  for (int i = 0; i < 8; i++) rem.w[i] = 0;
+#pragma unroll 1
+  for (int it = 0; it < 256; it++) {
+    const u32 c = rem.w[7] >> 31;
+#pragma unroll
+    for (int i = 7; i > 0; i--) rem.w[i] = (rem.w[i] << 1) | (rem.w[i - 1] >> 31);
+    rem.w[0] = (rem.w[0] << 1) | (quo.w[7] >> 31);
+#pragma unroll
+    for (int i = 7; i > 0; i--) quo.w[i] = (quo.w[i] << 1) | (quo.w[i - 1] >> 31);
+    quo.w[0] <<= 1;
+    u32 br;
+    W8 d = sub8(rem, b, &br);
+    const bool ge = (c != 0) | (br == 0);
+#pragma unroll
+    for (int i = 0; i < 8; i++) rem.w[i] = ge ? d.w[i] : rem.w[i];
+    quo.w[0] |= ge ? 1u : 0u;
+  }
+  q = quo;
+  r = rem;
+}
+
+// SMT-LIB bvudiv / bvurem with the total-division convention
+__device__ __forceinline__ W8 bv_udiv(const W8& a, const W8& b, u32 width) {
+  W8 q, r;
+  udivrem8(a, b, q, r);
+  if (is_zero8(b)) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) q.w[i] = 0xFFFFFFFFu;
+  }
+  canon8(q, width);
+  return q;
+}
+
+__device__ __forceinline__ W8 bv_urem(const W8& a, const W8& b, u32 width) {
+  W8 q, r;
+  udivrem8(a, b, q, r);
+  if (is_zero8(b)) r = a;
+  canon8(r, width);
+  return r;
+}
+
+__device__ __forceinline__ u32 msb_of(const W8& a, u32 width) {
+  const u32 bit = width - 1;
+  u32 v = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) v = ((u32)i == (bit >> 5)) ? a.w[i] : v;
+  return (v >> (bit & 31)) & 1u;
+}
+
+__device__ __forceinline__ W8 negw(const W8& a, u32 width) {
+  W8 r = neg8(a);
+  canon8(r, width);
+  return r;
+}
+
+// bvsdiv: msb case split of the SMT-LIB definition
+__device__ __forceinline__ W8 bv_sdiv(const W8& a, const W8& b, u32 width) {
+  const u32 ma = msb_of(a, width), mb = msb_of(b, width);
+  W8 aa = ma ? negw(a, width) : a;
+  W8 bb = mb ? negw(b, width) : b;
+  W8 q = bv_udiv(aa, bb, width);
+  return (ma ^ mb) ? negw(q, width) : q;
+}
+
+// bvsrem: sign follows the dividend
+__device__ __forceinline__ W8 bv_srem(const W8& a, const W8& b, u32 width) {
+  const u32 ma = msb_of(a, width), mb = msb_of(b, width);
+  W8 aa = ma ? negw(a, width) : a;
+  W8 bb = mb ? negw(b, width) : b;
+  W8 r = bv_urem(aa, bb, width);
+  return ma ? negw(r, width) : r;
+}
+
+// bvsmod: sign follows the divisor
+__device__ __forceinline__ W8 bv_smod(const W8& a, const W8& b, u32 width) {
+  const u32 ma = msb_of(a, width), mb = msb_of(b, width);
+  W8 aa = ma ? negw(a, width) : a;
+  W8 bb = mb ? negw(b, width) : b;
+  W8 u = bv_urem(aa, bb, width);
+  if (is_zero8(u) || (!ma && !mb)) return u;
+  W8 r;
+  if (ma && !mb) {
+    r = add8(negw(u, width), b);
+  } else if (!ma && mb) {
+    r = add8(u, b);
+  } else {
+    r = negw(u, width);
+  }
+  canon8(r, width);
+  return r;
+}
+
+// shift amount as a saturated small integer: returns width if b >= width
+__device__ __forceinline__ u32 shamt(const W8& b, u32 width) {
+  u32 hi = 0;
+#pragma unroll
+  for (int i = 1; i < 8; i++) hi |= b.w[i];
+  return (hi != 0 || b.w[0] >= width) ? width : b.w[0];
+}
+
+// x << s (s < 256): barrel over whole limbs, then a funnel shift
+__device__ __forceinline__ W8 shl8(const W8& x, u32 s) {
+  W8 r = x;
+  const u32 q = s >> 5, b = s & 31u;
+#pragma unroll
+  for (int k = 1; k <= 4; k <<= 1) {
+    const bool on = (q & (u32)k) != 0;
+#pragma unroll
+    for (int i = 7; i >= 0; i--) {
+      u32 v = i - k >= 0 ? r.w[i - k] : 0u;
+      r.w[i] = on ? v : r.w[i];
+    }
+  }
+#pragma unroll
+  for (int i = 7; i >= 0; i--) {
+    u32 lo = i > 0 ? r.w[i - 1] : 0u;
+    r.w[i] = (u32)((((u64)r.w[i] << 32) | lo) >> (32 - b));
+  }
+  return r;
+}
+
+// x >> s with fill (0 or ~0) for the vacated bits
+__device__ __forceinline__ W8 shr8(const W8& x, u32 s, u32 fill) {
+  W8 r = x;
+  const u32 q = s >> 5, b = s & 31u;
+#pragma unroll
+  for (int k = 1; k <= 4; k <<= 1) {
+    const bool on = (q & (u32)k) != 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      u32 v = i + k < 8 ? r.w[i + k] : fill;
+      r.w[i] = on ? v : r.w[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u32 hi = i < 7 ? r.w[i + 1] : fill;
+    r.w[i] = (u32)((((u64)hi << 32) | r.w[i]) >> b);
+  }
+  return r;
+}
+
+__device__ __forceinline__ W8 bv_shl(const W8& a, const W8& b, u32 width) {
+  const u32 s = shamt(b, width);
+  W8 r;
+  if (s >= width) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.w[i] = 0;
+    return r;
+  }
+  r = shl8(a, s);
+  canon8(r, width);
+  return r;
+}
+
+__device__ __forceinline__ W8 bv_lshr(const W8& a, const W8& b, u32 width) {
+  const u32 s = shamt(b, width);
+  W8 r;
+  if (s >= width) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.w[i] = 0;
+    return r;
+  }
+  return shr8(a, s, 0u);
+}
+
+__device__ __forceinline__ W8 bv_ashr(const W8& a, const W8& b, u32 width) {
+  const u32 s = shamt(b, width);
+  const u32 neg = msb_of(a, width);
+  // sign-extend a to 256 bits, shift with sign fill, re-mask
+  W8 x = a;
+  if (neg) {
+    const u32 L = (width + 31u) >> 5;
+    const u32 tm = top_mask(width);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      if ((u32)i == L - 1) x.w[i] |= ~tm;
+      else if ((u32)i >= L) x.w[i] = 0xFFFFFFFFu;
+    }
+  }
+  W8 r;
+  if (s >= width) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.w[i] = neg ? 0xFFFFFFFFu : 0u;
+  } else {
+    r = shr8(x, s, neg ? 0xFFFFFFFFu : 0u);
+  }
+  canon8(r, width);
+  return r;
+}
+
+// EVM EXP (mod 2^width): square-and-multiply over the exponent bits, MSB first
+__device__ __forceinline__ W8 bv_exp(const W8& base, const W8& e, u32 width) {
+  W8 r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.w[i] = 0;
+  r.w[0] = 1;
+  W8 ex = e;
+#pragma unroll 1
+  for (int it = 0; it < 256; it++) {
+    const u32 bit = ex.w[7] >> 31;
+#pragma unroll
+    for (int i = 7; i > 0; i--) ex.w[i] = (ex.w[i] << 1) | (ex.w[i - 1] >> 31);
+    ex.w[0] <<= 1;
+    r = mul8(r, r);
+    W8 m = mul8(r, base);
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.w[i] = bit ? m.w[i] : r.w[i];
+  }
+  canon8(r, width);
+  return r;
+}
+
+}  // namespace mg

@@ -1,0 +1,1046 @@
+// MI355X batched bit-vector evaluation engine: kernels + C-ABI (libmythgpu.so).
+//
+// One lane evaluates one candidate assignment.  The lowered program
+// (program.cpp) is wave-uniform: each 32-byte instruction is fetched with scalar
+// loads and dispatched with scalar branches; values live in a per-lane value
+// file laid out [word][lane] (LDS when it fits, else an HBM/L2 scratch slab), so
+// every value-file access is a conflict-free / fully coalesced 4-byte-per-lane
+// access.  256-bit arithmetic (MUL/DIV/shift/EXP) is done in VGPRs
+// (bv_device.h); linear ops (ADD/SUB/logic/compare/concat/extract) stream words.
+//
+// Modes: EVAL (coordinates from a SoA buffer in HBM), GEN (coordinates from the
+// counter-based generator, for model materialisation), SEARCH (generator + wave
+// ballot + atomicMin first hit).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mythgpu.h"
+#include "bv_device.h"
+#include "keccak_device.h"
+#include "program.hpp"
+
+namespace mg {
+
+constexpr int kWave = 64;
+constexpr uint32_t kLdsWordsMax = 160;  // value file in LDS up to 160 words (40 KiB per wave)
+
+__device__ __constant__ static const uint32_t kEmptyKeccak[8] = {
+    0x5d85a470u, 0xfad8045du, 0x82273b7bu, 0xe500b653u, 0xdcc703c0u, 0x927e7db2u, 0x86f7233cu, 0xc5d24601u};
+
+enum Mode : int { MODE_EVAL = 0, MODE_GEN = 1, MODE_SEARCH = 2 };
+
+struct KArgs {
+  const Instr* code;
+  const uint32_t* consts;
+  const uint32_t* aux;
+  const GenSpec* specs;
+  const uint32_t* gconsts;
+  const uint32_t* coord_width;
+  const uint32_t* soa;       // EVAL: [row][n]
+  uint8_t* verdict;          // EVAL/GEN: [n]
+  uint32_t* watch;           // EVAL/GEN: [row][n] (nullable)
+  uint32_t* scratch;         // global value file [word][stride]
+  unsigned long long* first_hit;
+  unsigned long long* hits;
+  uint64_t start, count, seed, stride;
+  uint32_t n_instr, value_words, flags, pad;
+};
+
+// ---------------------------------------------------------------------------
+// value file policies
+// ---------------------------------------------------------------------------
+struct VFLds {
+  uint32_t* base;
+  __device__ VFLds(uint32_t* lds, const KArgs&) : base(lds) {}
+  __device__ __forceinline__ uint32_t& at(uint32_t w) const { return base[w * kWave + threadIdx.x]; }
+};
+
+struct VFGlobal {
+  uint32_t* base;
+  uint64_t stride;
+  __device__ VFGlobal(uint32_t*, const KArgs& k)
+      : base(k.scratch + (uint64_t)blockIdx.x * kWave + threadIdx.x), stride(k.stride) {}
+  __device__ __forceinline__ uint32_t& at(uint32_t w) const { return base[(uint64_t)w * stride]; }
+};
+
+// ---------------------------------------------------------------------------
+// counter-based candidate generator (pure function of seed, index, coordinate)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t cand_key(uint64_t idx, uint64_t seed) {
+  return mix32((uint32_t)idx ^ mix32((uint32_t)(idx >> 32) ^ (uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + 0x632BE5ABu)));
+}
+
+__device__ __forceinline__ uint32_t rnd(uint32_t key, uint32_t c, uint32_t j) {
+  return mix32(key + c * 0x9E3779B9u + j * 0x85EBCA6Bu + 0x27D4EB2Fu);
+}
+
+template <class VF>
+__device__ __forceinline__ void write_masked(const VF& vf, uint32_t dst, uint32_t L, uint32_t width) {
+  vf.at(dst + L - 1) &= top_mask(width);
+}
+
+// Value of coordinate c for a candidate (key = cand_key(index, seed)).
+// MIXED may copy another coordinate: the copy regenerates the source with the
+// source's own spec and index (one level, no recursion), truncated/zero-extended.
+template <class VF>
+__device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c, uint32_t width, uint32_t key) {
+  const uint32_t L = (width + 31) >> 5;
+  uint32_t cc = c;  // coordinate whose spec/randomness is used
+  GenSpec s = k.specs[c];
+  uint32_t Lg = L;  // limbs to generate
+  bool allow_copy = true;
+  for (int level = 0; level < 2; level++) {
+    if (s.kind != MG_GEN_MIXED) break;
+    const uint32_t sel = rnd(key, cc, 0xFFFFu) & 0xFFFFu;
+    const uint32_t pc = (allow_copy && s.p[3] != MG_NONE) ? s.p[4] : 0u;
+    const uint32_t pd = s.p[1] ? s.p[2] : 0u;
+    const uint32_t ps = s.p[6] & 0xFFFFu;
+    if (sel < pc) {
+      cc = s.p[3];
+      s = k.specs[cc];
+      Lg = min(L, (k.coord_width[cc] + 31) >> 5);
+      allow_copy = false;
+      continue;  // re-decide with the source's spec
+    }
+    if (sel < pc + pd) {
+      s.kind = MG_GEN_DICT;  // dictionary draw, keeps p5 (delta) below
+      s.p[6] = 1;            // marks "came from MIXED" so the delta option applies
+    } else if (sel < pc + pd + ps) {
+      const uint32_t bits = min(width, s.p[6] >> 16);
+      for (uint32_t j = 0; j < L; j++) {
+        uint32_t v = rnd(key, cc, j);
+        const uint32_t lo = j * 32;
+        v = lo >= bits ? 0u : (bits - lo >= 32 ? v : (v & ((1u << (bits - lo)) - 1u)));
+        vf.at(dst + j) = v;
+      }
+      write_masked(vf, dst, L, width);
+      return;
+    } else {
+      s.kind = MG_GEN_UNIFORM;
+    }
+    break;
+  }
+  const uint32_t Ls = s.kind == MG_GEN_DICT || s.kind == MG_GEN_RANGE || s.kind == MG_GEN_ALIGNED ||
+                              s.kind == MG_GEN_FIXED
+                          ? ((k.coord_width[cc] + 31) >> 5)
+                          : Lg;  // limb stride of the source's constants
+  switch (s.kind) {
+    case MG_GEN_DICT: {
+      const uint32_t n = s.p[1];
+      const uint32_t e = (uint32_t)(((uint64_t)rnd(key, cc, 0xFFFEu) * n) >> 32);
+      const uint32_t* src = k.gconsts + s.p[0] + e * Ls;
+      for (uint32_t j = 0; j < Lg; j++) vf.at(dst + j) = src[j];
+      if (s.p[6] == 1 && s.p[5]) {
+        const uint32_t r = rnd(key, cc, 0xFFFDu);
+        if ((r & 0xFFFFu) < s.p[5]) {
+          // +/- 1 or 2 (wrapping)
+          const uint32_t mag = ((r >> 16) & 1u) + 1u;
+          const bool sub = (r >> 17) & 1u;
+          uint64_t carry = mag;
+          for (uint32_t j = 0; j < Lg; j++) {
+            uint64_t t = sub ? ((uint64_t)vf.at(dst + j) - carry) : ((uint64_t)vf.at(dst + j) + carry);
+            vf.at(dst + j) = (uint32_t)t;
+            carry = sub ? ((t >> 32) & 1u) : (t >> 32);
+          }
+        }
+      }
+      break;
+    }
+    case MG_GEN_RANGE: {
+      const uint32_t span = s.p[1];
+      const uint32_t r = rnd(key, cc, 0);
+      const uint32_t off = span ? (uint32_t)(((uint64_t)r * span) >> 32) : r;
+      uint64_t carry = off;
+      for (uint32_t j = 0; j < Lg; j++) {
+        uint64_t t = (uint64_t)k.gconsts[s.p[0] + j] + carry;
+        vf.at(dst + j) = (uint32_t)t;
+        carry = t >> 32;
+      }
+      break;
+    }
+    case MG_GEN_ALIGNED: {
+      const uint32_t cnt = s.p[2];
+      const uint32_t r = rnd(key, cc, 0);
+      const uint64_t m = cnt ? (((uint64_t)r * cnt) >> 32) : r;
+      const uint32_t sh = s.p[1];
+      uint64_t carry = 0;
+      for (uint32_t j = 0; j < Lg; j++) {
+        const int32_t bit0 = (int32_t)(j * 32) - (int32_t)sh;  // word j of (m << sh)
+        uint32_t mw;
+        if (bit0 <= -32 || bit0 >= 64) mw = 0;
+        else if (bit0 < 0) mw = (uint32_t)(m << (-bit0));
+        else mw = (uint32_t)(m >> bit0);
+        uint64_t t = (uint64_t)k.gconsts[s.p[0] + j] + mw + carry;
+        vf.at(dst + j) = (uint32_t)t;
+        carry = t >> 32;
+      }
+      break;
+    }
+    case MG_GEN_FIXED: {
+      for (uint32_t j = 0; j < Lg; j++) vf.at(dst + j) = k.gconsts[s.p[0] + j];
+      break;
+    }
+    default: {  // UNIFORM (and LAZY coordinates, which the program never reads)
+      for (uint32_t j = 0; j < Lg; j++) vf.at(dst + j) = rnd(key, cc, j);
+      break;
+    }
+  }
+  for (uint32_t j = Lg; j < L; j++) vf.at(dst + j) = 0;
+  write_masked(vf, dst, L, width);
+}
+
+// ---------------------------------------------------------------------------
+// value-file helpers
+// ---------------------------------------------------------------------------
+template <class VF>
+__device__ __forceinline__ W8 ld8(const VF& vf, uint32_t off, uint32_t L) {
+  W8 x;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x.w[i] = (uint32_t)i < L ? vf.at(off + i) : 0u;
+  return x;
+}
+
+template <class VF>
+__device__ __forceinline__ void st8(const VF& vf, uint32_t off, uint32_t L, const W8& x) {
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if ((uint32_t)i < L) vf.at(off + i) = x.w[i];
+}
+
+// 32 bits of value (slot off, width w) starting at bit position p (zero beyond w)
+template <class VF>
+__device__ __forceinline__ uint32_t bits32(const VF& vf, uint32_t off, uint32_t w, uint32_t p) {
+  if (p >= w) return 0u;
+  const uint32_t L = (w + 31) >> 5;
+  const uint32_t q = p >> 5, r = p & 31u;
+  const uint32_t lo = vf.at(off + q);
+  const uint32_t hi = (q + 1 < L) ? vf.at(off + q + 1) : 0u;
+  return r ? ((lo >> r) | (hi << (32 - r))) : lo;
+}
+
+template <class VF>
+__device__ __forceinline__ uint32_t keccak_byte(const VF& vf, uint32_t off, uint32_t len, uint32_t m) {
+  // message byte m (big-endian value of 8*len bits)
+  const uint32_t bitpos = 8u * (len - 1u - m);
+  return (vf.at(off + (bitpos >> 5)) >> (bitpos & 31u)) & 0xFFu;
+}
+
+template <class VF>
+__device__ void do_keccak(const VF& vf, const Instr& in) {
+  uint64_t st[25];
+#pragma unroll
+  for (int i = 0; i < 25; i++) st[i] = 0;
+  const uint32_t len = in.p0;
+  const uint32_t nblocks = len / 136u + 1u;
+  for (uint32_t b = 0; b < nblocks; b++) {
+    for (uint32_t t = 0; t < 17; t++) {
+      uint64_t lane = 0;
+      for (uint32_t k = 0; k < 8; k++) {
+        const uint32_t m = b * 136u + t * 8u + k;
+        uint32_t byte = m < len ? keccak_byte(vf, in.a, len, m) : 0u;
+        if (m == len) byte |= 0x01u;
+        if (m == nblocks * 136u - 1u) byte |= 0x80u;
+        lane |= (uint64_t)byte << (8 * k);
+      }
+      // st[t] ^= lane with a compile-time index (t is uniform; unrolled select)
+#pragma unroll
+      for (int i = 0; i < 17; i++)
+        if ((uint32_t)i == t) st[i] ^= lane;
+    }
+    keccak_f1600(st);
+  }
+  // value limb j = bswap32(digest dword 7-j); digest dword 2t / 2t+1 = low / high of st[t]
+  uint32_t dw[8];
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    dw[2 * t] = (uint32_t)st[t];
+    dw[2 * t + 1] = (uint32_t)(st[t] >> 32);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; j++) vf.at(in.dst + j) = __builtin_bswap32(dw[7 - j]);
+}
+
+// ---------------------------------------------------------------------------
+// interpreter
+// ---------------------------------------------------------------------------
+template <class VF, int MODE>
+__device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, uint64_t i, uint32_t key,
+                                                bool early) {
+  uint32_t verdict = 1;
+  const Instr* code = k.code;
+  const uint32_t n_instr = k.n_instr;
+  for (uint32_t pc = 0; pc < n_instr; pc++) {
+    const Instr in = code[pc];
+    const uint32_t W = in.wd;
+    const uint32_t L = (W + 31) >> 5;
+    switch (in.op) {
+      case K_CONST: {
+        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = k.consts[in.p0 + j];
+        break;
+      }
+      case K_COORD: {
+        if (MODE == MODE_EVAL) {
+          for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = k.soa[(uint64_t)(in.p1 + j) * k.count + i];
+        } else {
+          gen_coord<VF>(k, vf, in.dst, in.p0, W, key);
+        }
+        break;
+      }
+      case K_COPY: {
+        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = vf.at(in.a + j);
+        break;
+      }
+      case K_ADD:
+      case K_SUB: {
+        uint64_t c = 0;
+        const bool sub = in.op == K_SUB;
+        for (uint32_t j = 0; j < L; j++) {
+          const uint64_t x = vf.at(in.a + j), y = vf.at(in.b + j);
+          const uint64_t t = sub ? (x - y - c) : (x + y + c);
+          vf.at(in.dst + j) = (uint32_t)t;
+          c = sub ? ((t >> 32) & 1u) : (t >> 32);
+        }
+        write_masked(vf, in.dst, L, W);
+        break;
+      }
+      case K_NEG: {
+        uint64_t c = 0;
+        for (uint32_t j = 0; j < L; j++) {
+          const uint64_t t = 0ull - (uint64_t)vf.at(in.a + j) - c;
+          vf.at(in.dst + j) = (uint32_t)t;
+          c = (t >> 32) & 1u;
+        }
+        write_masked(vf, in.dst, L, W);
+        break;
+      }
+      case K_AND:
+        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = vf.at(in.a + j) & vf.at(in.b + j);
+        break;
+      case K_OR:
+        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = vf.at(in.a + j) | vf.at(in.b + j);
+        break;
+      case K_XOR:
+        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = vf.at(in.a + j) ^ vf.at(in.b + j);
+        break;
+      case K_NOT:
+        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = ~vf.at(in.a + j);
+        write_masked(vf, in.dst, L, W);
+        break;
+      case K_ITE: {
+        const bool c = vf.at(in.a) != 0;
+        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = c ? vf.at(in.b + j) : vf.at(in.c + j);
+        break;
+      }
+      case K_EQ: {
+        const uint32_t La = (in.p1 + 31) >> 5;
+        uint32_t d = 0;
+        for (uint32_t j = 0; j < La; j++) d |= vf.at(in.a + j) ^ vf.at(in.b + j);
+        vf.at(in.dst) = d == 0;
+        break;
+      }
+      case K_ULT:
+      case K_ULE:
+      case K_SLT:
+      case K_SLE: {
+        const uint32_t wa = in.p1, La = (wa + 31) >> 5;
+        // a - b borrow chain; for signed compare flip the sign bits first
+        const uint32_t sflip = (in.op == K_SLT || in.op == K_SLE) ? (1u << ((wa - 1) & 31)) : 0u;
+        uint64_t br = 0;
+        uint32_t nz = 0;
+        for (uint32_t j = 0; j < La; j++) {
+          uint32_t x = vf.at(in.a + j), y = vf.at(in.b + j);
+          if (j == La - 1) {
+            x ^= sflip;
+            y ^= sflip;
+          }
+          const uint64_t t = (uint64_t)x - y - br;
+          br = (t >> 32) & 1u;
+          nz |= (uint32_t)t;
+        }
+        const bool lt = br != 0;
+        const bool le = lt || nz == 0;
+        vf.at(in.dst) = (in.op == K_ULT || in.op == K_SLT) ? (uint32_t)lt : (uint32_t)le;
+        break;
+      }
+      case K_CONCAT: {
+        // dst = a:b, width(b) = p1
+        const uint32_t wb = in.p1, wa = W - wb;
+        for (uint32_t j = 0; j < L; j++) {
+          const uint32_t p = j * 32;
+          uint32_t v = bits32(vf, in.b, wb, p);
+          if (p + 32 > wb) {
+            v |= (p >= wb) ? bits32(vf, in.a, wa, p - wb) : (bits32(vf, in.a, wa, 0) << (wb - p));
+          }
+          vf.at(in.dst + j) = v;
+        }
+        write_masked(vf, in.dst, L, W);
+        break;
+      }
+      case K_EXTRACT: {
+        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = bits32(vf, in.a, in.p1, in.p0 + j * 32);
+        write_masked(vf, in.dst, L, W);
+        break;
+      }
+      case K_ZEXT:
+      case K_SEXT: {
+        const uint32_t wa = in.p1, La = (wa + 31) >> 5;
+        uint32_t fill = 0;
+        if (in.op == K_SEXT) fill = ((vf.at(in.a + La - 1) >> ((wa - 1) & 31)) & 1u) ? 0xFFFFFFFFu : 0u;
+        for (uint32_t j = 0; j < L; j++) {
+          uint32_t v;
+          if (j < La) {
+            v = vf.at(in.a + j);
+            if (j == La - 1) v = (v & top_mask(wa)) | (fill & ~top_mask(wa));
+          } else {
+            v = fill;
+          }
+          vf.at(in.dst + j) = v;
+        }
+        write_masked(vf, in.dst, L, W);
+        break;
+      }
+      case K_MUL: {
+        W8 r = mul8(ld8(vf, in.a, L), ld8(vf, in.b, L));
+        canon8(r, W);
+        st8(vf, in.dst, L, r);
+        break;
+      }
+      case K_UMUL_NOOVF: {
+        const uint32_t wa = in.p1, La = (wa + 31) >> 5;
+        const W8 x = ld8(vf, in.a, La), y = ld8(vf, in.b, La);
+        const W8 lo = mul8(x, y);
+        const W8 hi = mulhi8(x, y);
+        // no overflow <=> bits >= wa of the 512-bit product are all zero
+        uint32_t ov = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          ov |= hi.w[q];
+          const uint32_t lw = lo.w[q];
+          const uint32_t bit0 = q * 32;
+          uint32_t m;
+          if (bit0 + 32 <= wa) m = 0u;
+          else if (bit0 >= wa) m = 0xFFFFFFFFu;
+          else m = ~((1u << (wa - bit0)) - 1u);
+          ov |= lw & m;
+        }
+        vf.at(in.dst) = ov == 0;
+        break;
+      }
+      case K_UDIV: st8(vf, in.dst, L, bv_udiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
+      case K_UREM: st8(vf, in.dst, L, bv_urem(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
+      case K_SDIV: st8(vf, in.dst, L, bv_sdiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
+      case K_SREM: st8(vf, in.dst, L, bv_srem(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
+      case K_SMOD: st8(vf, in.dst, L, bv_smod(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
+      case K_SHL: st8(vf, in.dst, L, bv_shl(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
+      case K_LSHR: st8(vf, in.dst, L, bv_lshr(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
+      case K_ASHR: st8(vf, in.dst, L, bv_ashr(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
+      case K_EXP: st8(vf, in.dst, L, bv_exp(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
+      case K_LOOKUP: {
+        const uint32_t Lk = (in.b + 31) >> 5;
+        uint32_t src = in.p0;
+        bool found = false;
+        for (uint32_t p = 0; p < in.c; p++) {
+          const uint32_t ko = k.aux[in.p1 + 2 * p], vo = k.aux[in.p1 + 2 * p + 1];
+          uint32_t d = 0;
+          for (uint32_t j = 0; j < Lk; j++) d |= vf.at(in.a + j) ^ vf.at(ko + j);
+          const bool hit = !found && d == 0;
+          src = hit ? vo : src;
+          found = found || hit;
+        }
+        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = vf.at(src + j);
+        break;
+      }
+      case K_KECCAK: {
+        if (in.a == MG_NONE) {
+          // keccak256("") — the constant of keccak_function_manager.py:75-81
+          for (uint32_t j = 0; j < 8; j++) vf.at(in.dst + j) = kEmptyKeccak[j];
+        } else {
+          do_keccak(vf, in);
+        }
+        break;
+      }
+      case K_ASSERT: {
+        verdict &= vf.at(in.a);
+        if (early && __ballot(verdict != 0) == 0ull) return 0u;
+        break;
+      }
+      case K_WATCH: {
+        if (MODE != MODE_SEARCH && k.watch) {
+          for (uint32_t j = 0; j < L; j++) k.watch[(uint64_t)(in.p0 + j) * k.count + i] = vf.at(in.a + j);
+        }
+        break;
+      }
+      default:
+        break;
+    }
+  }
+  return verdict;
+}
+
+template <class VF, int MODE>
+__global__ void __launch_bounds__(kWave) k_run(KArgs k) {
+  extern __shared__ uint32_t lds[];
+  VF vf(lds, k);
+  const uint64_t total = k.count;
+  const uint64_t step = (uint64_t)gridDim.x * kWave;
+  const bool early = (MODE == MODE_SEARCH) && (k.flags & MG_SEARCH_EARLY_EXIT);
+  for (uint64_t base = (uint64_t)blockIdx.x * kWave; base < total; base += step) {
+    const uint64_t i_raw = base + threadIdx.x;
+    const bool active = i_raw < total;
+    const uint64_t i = active ? i_raw : (total - 1);
+    const uint64_t idx = k.start + i;
+    if (early) {
+      // every candidate below the current first hit is still evaluated, so the
+      // final minimum is exact; waves entirely above it stop
+      const unsigned long long cur = __hip_atomic_load(k.first_hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t cur_u = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) |
+                             __builtin_amdgcn_readfirstlane((uint32_t)cur);
+      if (k.start + base >= cur_u) break;
+    }
+    const uint32_t key = (MODE == MODE_EVAL) ? 0u : cand_key(idx, k.seed);
+    uint32_t v = run_program<VF, MODE>(k, vf, i, key, early);
+    v = active ? v : 0u;
+    if (MODE == MODE_SEARCH) {
+      const unsigned long long m = __ballot(v != 0);
+      if (m) {
+        if (threadIdx.x == (unsigned)__ffsll((long long)m) - 1) {
+          atomicMin(k.first_hit, (unsigned long long)idx);
+          atomicAdd(k.hits, (unsigned long long)__popcll(m));
+        }
+      }
+    } else if (active) {
+      k.verdict[i] = (uint8_t)v;
+    }
+  }
+}
+
+// batched concrete Keccak-256: one lane per message
+__global__ void __launch_bounds__(256) k_keccak(const uint8_t* msgs, const uint64_t* offs, const uint32_t* lens,
+                                                 uint64_t n, uint8_t* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* m = msgs + offs[i];
+  const uint32_t len = lens[i];
+  uint64_t st[25];
+#pragma unroll
+  for (int q = 0; q < 25; q++) st[q] = 0;
+  const uint32_t nblocks = len / 136u + 1u;
+  for (uint32_t b = 0; b < nblocks; b++) {
+#pragma unroll
+    for (int t = 0; t < 17; t++) {
+      uint64_t lane = 0;
+      for (int kb = 0; kb < 8; kb++) {
+        const uint32_t pos = b * 136u + t * 8u + kb;
+        uint32_t byte = pos < len ? m[pos] : 0u;
+        if (pos == len) byte |= 0x01u;
+        if (pos == nblocks * 136u - 1u) byte |= 0x80u;
+        lane |= (uint64_t)byte << (8 * kb);
+      }
+      st[t] ^= lane;
+    }
+    keccak_f1600(st);
+  }
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+#pragma unroll
+    for (int kb = 0; kb < 8; kb++) out[i * 32 + t * 8 + kb] = (uint8_t)(st[t] >> (8 * kb));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+thread_local std::string g_err;
+
+struct DevProgram {
+  Lowered low;
+  Instr* d_code = nullptr;
+  uint32_t* d_consts = nullptr;
+  uint32_t* d_aux = nullptr;
+  uint32_t* d_coord_width = nullptr;
+  bool lds = false;
+};
+
+struct DevGen {
+  uint64_t prog = 0;
+  GenSpec* d_specs = nullptr;
+  uint32_t* d_consts = nullptr;
+};
+
+struct Engine {
+  std::mutex mu;
+  bool init = false;
+  int device = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int cu_count = 0, clock_mhz = 0;
+  uint64_t next_handle = 1;
+  std::unordered_map<uint64_t, std::unique_ptr<DevProgram>> progs;
+  std::unordered_map<uint64_t, std::unique_ptr<DevGen>> gens;
+  unsigned long long* d_hit = nullptr;  // [0] first hit, [1] hit count
+  uint32_t* d_scratch = nullptr;
+  size_t scratch_bytes = 0;
+  mg_stats_t stats{};
+};
+
+Engine& E() {
+  static Engine e;
+  return e;
+}
+
+#define HIPCHK(x)                                                                  \
+  do {                                                                             \
+    hipError_t _e = (x);                                                           \
+    if (_e != hipSuccess) {                                                        \
+      g_err = std::string(#x) + ": " + hipGetErrorString(_e);                      \
+      return MG_E_HIP;                                                             \
+    }                                                                              \
+  } while (0)
+
+static int set_err(int code, const std::string& m) {
+  g_err = m;
+  return code;
+}
+
+template <class T>
+static int upload(T** d, const T* h, size_t n) {
+  *d = nullptr;
+  if (n == 0) n = 1;
+  HIPCHK(hipMalloc((void**)d, n * sizeof(T)));
+  if (h) HIPCHK(hipMemcpy(*d, h, n * sizeof(T), hipMemcpyHostToDevice));
+  return MG_OK;
+}
+
+static int ensure_scratch(Engine& e, size_t bytes) {
+  if (bytes <= e.scratch_bytes) return MG_OK;
+  if (e.d_scratch) (void)hipFree(e.d_scratch);
+  e.d_scratch = nullptr;
+  e.scratch_bytes = 0;
+  HIPCHK(hipMalloc((void**)&e.d_scratch, bytes));
+  e.scratch_bytes = bytes;
+  return MG_OK;
+}
+
+// grid: enough waves to fill 256 CUs several times over, never more than needed
+static uint32_t grid_for(const Engine& e, uint64_t count, bool lds, uint32_t value_words) {
+  uint64_t want = (count + kWave - 1) / kWave;
+  uint32_t waves_per_cu = 8;
+  if (lds) {
+    const uint32_t bytes = value_words * kWave * 4;
+    waves_per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (160u * 1024u) / std::max<uint32_t>(bytes, 1)));
+  }
+  uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * waves_per_cu * 4;
+  return (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+}
+
+template <int MODE>
+static int launch(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
+  if (count == 0) return MG_OK;
+  const uint32_t grid = grid_for(e, count, p.lds, p.low.value_words);
+  k.code = p.d_code;
+  k.consts = p.d_consts;
+  k.aux = p.d_aux;
+  k.coord_width = p.d_coord_width;
+  k.count = count;
+  k.n_instr = (uint32_t)p.low.code.size();
+  k.value_words = p.low.value_words;
+  k.stride = (uint64_t)grid * kWave;
+  if (!p.lds) {
+    const size_t need = (size_t)p.low.value_words * k.stride * 4;
+    int rc = ensure_scratch(e, need);
+    if (rc) return rc;
+    k.scratch = e.d_scratch;
+  }
+  const size_t shmem = p.lds ? (size_t)p.low.value_words * kWave * 4 : 0;
+  HIPCHK(hipEventRecord(e.ev0, e.stream));
+  if (p.lds)
+    hipLaunchKernelGGL((k_run<VFLds, MODE>), dim3(grid), dim3(kWave), shmem, e.stream, k);
+  else
+    hipLaunchKernelGGL((k_run<VFGlobal, MODE>), dim3(grid), dim3(kWave), 0, e.stream, k);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e.ev1, e.stream));
+  HIPCHK(hipEventSynchronize(e.ev1));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e.ev0, e.ev1));
+  e.stats.launches++;
+  e.stats.last_kernel_ms = ms;
+  e.stats.kernel_ms_total += ms;
+  e.stats.candidates += count;
+  e.stats.last_candidates = count;
+  return MG_OK;
+}
+
+}  // namespace mg
+
+using namespace mg;
+
+extern "C" {
+
+int mg_version(void) { return 1; }
+
+const char* mg_last_error(void) { return g_err.c_str(); }
+
+int mg_init(uint32_t device_mask) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (e.init) return MG_OK;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return set_err(MG_E_NODEVICE, "no HIP device");
+  int dev = -1;
+  for (int d = 0; d < n && d < 32; d++)
+    if (device_mask & (1u << d)) {
+      dev = d;
+      break;
+    }
+  if (dev < 0) dev = 0;
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, dev));
+  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+    return set_err(MG_E_NODEVICE, std::string("device is ") + prop.gcnArchName + ", engine is built for gfx950");
+  HIPCHK(hipSetDevice(dev));
+  HIPCHK(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreate(&e.ev0));
+  HIPCHK(hipEventCreate(&e.ev1));
+  HIPCHK(hipMalloc((void**)&e.d_hit, 2 * sizeof(unsigned long long)));
+  e.device = dev;
+  e.cu_count = prop.multiProcessorCount;
+  e.clock_mhz = prop.clockRate / 1000;
+  e.stats.device = dev;
+  e.stats.cu_count = e.cu_count;
+  e.stats.clock_mhz = e.clock_mhz;
+  e.init = true;
+  return MG_OK;
+}
+
+void mg_shutdown(void) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.init) return;
+  for (auto& kv : e.progs) {
+    (void)hipFree(kv.second->d_code);
+    (void)hipFree(kv.second->d_consts);
+    (void)hipFree(kv.second->d_aux);
+    (void)hipFree(kv.second->d_coord_width);
+  }
+  e.progs.clear();
+  for (auto& kv : e.gens) {
+    (void)hipFree(kv.second->d_specs);
+    (void)hipFree(kv.second->d_consts);
+  }
+  e.gens.clear();
+  if (e.d_scratch) (void)hipFree(e.d_scratch);
+  e.d_scratch = nullptr;
+  e.scratch_bytes = 0;
+  (void)hipFree(e.d_hit);
+  (void)hipEventDestroy(e.ev0);
+  (void)hipEventDestroy(e.ev1);
+  (void)hipStreamDestroy(e.stream);
+  e.init = false;
+}
+
+int mg_program_check(const uint8_t* ssa, size_t len, mg_program_info_t* info) {
+  Lowered low;
+  std::string err;
+  int rc = lower_program(ssa, len, low, err);
+  if (rc) return set_err(rc, err);
+  if (info) {
+    std::memset(info, 0, sizeof(*info));
+    info->n_nodes = low.n_nodes;
+    info->n_instrs = (uint32_t)low.code.size();
+    info->n_coords = low.n_coords;
+    info->n_roots = low.n_roots;
+    info->value_words = low.value_words;
+    info->uses_lds = low.value_words <= kLdsWordsMax;
+    info->n_watch = low.n_watch;
+    info->watch_words = low.watch_words;
+    info->coord_words = low.coord_words;
+    info->limb_ops = low.limb_ops;
+  }
+  return MG_OK;
+}
+
+int mg_program_load(const uint8_t* ssa, size_t len, uint64_t* handle) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.init) return set_err(MG_E_NOTINIT, "mg_init not called");
+  auto p = std::make_unique<DevProgram>();
+  std::string err;
+  int rc = lower_program(ssa, len, p->low, err);
+  if (rc) return set_err(rc, err);
+  p->lds = p->low.value_words <= kLdsWordsMax;
+  if ((rc = upload(&p->d_code, p->low.code.data(), p->low.code.size()))) return rc;
+  if ((rc = upload(&p->d_consts, p->low.consts.data(), p->low.consts.size()))) return rc;
+  if ((rc = upload(&p->d_aux, p->low.aux.data(), p->low.aux.size()))) return rc;
+  if ((rc = upload(&p->d_coord_width, p->low.coord_width.data(), p->low.coord_width.size()))) return rc;
+  const uint64_t h = e.next_handle++;
+  e.progs[h] = std::move(p);
+  e.stats.programs_loaded++;
+  *handle = h;
+  return MG_OK;
+}
+
+static DevProgram* find_prog(Engine& e, uint64_t h) {
+  auto it = e.progs.find(h);
+  return it == e.progs.end() ? nullptr : it->second.get();
+}
+
+int mg_program_info(uint64_t prog, mg_program_info_t* info) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  DevProgram* p = find_prog(e, prog);
+  if (!p) return set_err(MG_E_INVALID, "bad program handle");
+  std::memset(info, 0, sizeof(*info));
+  info->n_nodes = p->low.n_nodes;
+  info->n_instrs = (uint32_t)p->low.code.size();
+  info->n_coords = p->low.n_coords;
+  info->n_roots = p->low.n_roots;
+  info->value_words = p->low.value_words;
+  info->uses_lds = p->lds;
+  info->n_watch = p->low.n_watch;
+  info->watch_words = p->low.watch_words;
+  info->coord_words = p->low.coord_words;
+  info->limb_ops = p->low.limb_ops;
+  return MG_OK;
+}
+
+int mg_program_free(uint64_t prog) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  auto it = e.progs.find(prog);
+  if (it == e.progs.end()) return set_err(MG_E_INVALID, "bad program handle");
+  (void)hipFree(it->second->d_code);
+  (void)hipFree(it->second->d_consts);
+  (void)hipFree(it->second->d_aux);
+  (void)hipFree(it->second->d_coord_width);
+  e.progs.erase(it);
+  return MG_OK;
+}
+
+int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* gen_handle) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  DevProgram* p = find_prog(e, prog);
+  if (!p) return set_err(MG_E_INVALID, "bad program handle");
+  std::vector<GenSpec> specs;
+  std::vector<uint32_t> consts;
+  std::string err;
+  int rc = parse_gen(p->low, blob, n_words, specs, consts, err);
+  if (rc) return set_err(rc, err);
+  auto gg = std::make_unique<DevGen>();
+  gg->prog = prog;
+  if ((rc = upload(&gg->d_specs, specs.data(), specs.size()))) return rc;
+  if ((rc = upload(&gg->d_consts, consts.data(), consts.size()))) return rc;
+  const uint64_t h = e.next_handle++;
+  e.gens[h] = std::move(gg);
+  *gen_handle = h;
+  return MG_OK;
+}
+
+int mg_gen_free(uint64_t gen) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  auto it = e.gens.find(gen);
+  if (it == e.gens.end()) return set_err(MG_E_INVALID, "bad generator handle");
+  (void)hipFree(it->second->d_specs);
+  (void)hipFree(it->second->d_consts);
+  e.gens.erase(it);
+  return MG_OK;
+}
+
+int mg_eval_dev(uint64_t prog, const uint32_t* d_soa, uint64_t n, uint8_t* d_verdict, uint32_t* d_watch) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  DevProgram* p = find_prog(e, prog);
+  if (!p) return set_err(MG_E_INVALID, "bad program handle");
+  KArgs k{};
+  k.soa = d_soa;
+  k.verdict = d_verdict;
+  k.watch = d_watch;
+  k.start = 0;
+  return launch<MODE_EVAL>(e, *p, k, n);
+}
+
+int mg_eval(uint64_t prog, const uint32_t* soa, uint64_t n, uint8_t* verdict_out, uint32_t* watch_out) {
+  Engine& e = E();
+  DevProgram* p;
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!e.init) return set_err(MG_E_NOTINIT, "mg_init not called");
+    p = find_prog(e, prog);
+    if (!p) return set_err(MG_E_INVALID, "bad program handle");
+  }
+  if (n == 0) return MG_OK;
+  const size_t soa_bytes = (size_t)std::max<uint32_t>(p->low.coord_words, 1) * n * 4;
+  const size_t watch_bytes = (size_t)p->low.watch_words * n * 4;
+  uint32_t *d_soa = nullptr, *d_watch = nullptr;
+  uint8_t* d_ver = nullptr;
+  HIPCHK(hipMalloc((void**)&d_soa, soa_bytes));
+  HIPCHK(hipMalloc((void**)&d_ver, n));
+  if (watch_out && watch_bytes) HIPCHK(hipMalloc((void**)&d_watch, watch_bytes));
+  if (p->low.coord_words) HIPCHK(hipMemcpy(d_soa, soa, (size_t)p->low.coord_words * n * 4, hipMemcpyHostToDevice));
+  int rc = mg_eval_dev(prog, d_soa, n, d_ver, d_watch);
+  if (rc == MG_OK) {
+    HIPCHK(hipMemcpy(verdict_out, d_ver, n, hipMemcpyDeviceToHost));
+    if (d_watch) HIPCHK(hipMemcpy(watch_out, d_watch, watch_bytes, hipMemcpyDeviceToHost));
+  }
+  (void)hipFree(d_soa);
+  (void)hipFree(d_ver);
+  if (d_watch) (void)hipFree(d_watch);
+  return rc;
+}
+
+int mg_eval_generated(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64_t n, uint8_t* verdict_out,
+                      uint32_t* watch_out) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  DevProgram* p = find_prog(e, prog);
+  if (!p) return set_err(MG_E_INVALID, "bad program handle");
+  auto it = e.gens.find(gen);
+  if (it == e.gens.end() || it->second->prog != prog) return set_err(MG_E_INVALID, "bad generator handle");
+  if (n == 0) return MG_OK;
+  const size_t watch_bytes = (size_t)p->low.watch_words * n * 4;
+  uint32_t* d_watch = nullptr;
+  uint8_t* d_ver = nullptr;
+  HIPCHK(hipMalloc((void**)&d_ver, n));
+  if (watch_out && watch_bytes) HIPCHK(hipMalloc((void**)&d_watch, watch_bytes));
+  KArgs k{};
+  k.specs = it->second->d_specs;
+  k.gconsts = it->second->d_consts;
+  k.verdict = d_ver;
+  k.watch = d_watch;
+  k.start = start;
+  k.seed = seed;
+  int rc = launch<MODE_GEN>(e, *p, k, n);
+  if (rc == MG_OK) {
+    HIPCHK(hipMemcpy(verdict_out, d_ver, n, hipMemcpyDeviceToHost));
+    if (d_watch) HIPCHK(hipMemcpy(watch_out, d_watch, watch_bytes, hipMemcpyDeviceToHost));
+  }
+  (void)hipFree(d_ver);
+  if (d_watch) (void)hipFree(d_watch);
+  return rc;
+}
+
+int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags,
+              uint64_t* first_hit, uint64_t* n_hits) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  DevProgram* p = find_prog(e, prog);
+  if (!p) return set_err(MG_E_INVALID, "bad program handle");
+  auto it = e.gens.find(gen);
+  if (it == e.gens.end() || it->second->prog != prog) return set_err(MG_E_INVALID, "bad generator handle");
+  unsigned long long init[2] = {~0ull, 0ull};
+  HIPCHK(hipMemcpyAsync(e.d_hit, init, sizeof(init), hipMemcpyHostToDevice, e.stream));
+  KArgs k{};
+  k.specs = it->second->d_specs;
+  k.gconsts = it->second->d_consts;
+  k.first_hit = e.d_hit;
+  k.hits = e.d_hit + 1;
+  k.start = start;
+  k.seed = seed;
+  k.flags = flags;
+  int rc = launch<MODE_SEARCH>(e, *p, k, count);
+  if (rc) return rc;
+  unsigned long long res[2];
+  HIPCHK(hipMemcpy(res, e.d_hit, sizeof(res), hipMemcpyDeviceToHost));
+  if (first_hit) *first_hit = res[0];
+  if (n_hits) *n_hits = res[1];
+  e.stats.hits += res[1];
+  return MG_OK;
+}
+
+int mg_keccak256(const uint8_t* msgs, const uint32_t* lens, uint64_t n, uint8_t* out32) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.init) return set_err(MG_E_NOTINIT, "mg_init not called");
+  if (n == 0) return MG_OK;
+  std::vector<uint64_t> offs(n);
+  uint64_t tot = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    offs[i] = tot;
+    tot += lens[i];
+  }
+  uint8_t *d_msgs = nullptr, *d_out = nullptr;
+  uint64_t* d_offs = nullptr;
+  uint32_t* d_lens = nullptr;
+  HIPCHK(hipMalloc((void**)&d_msgs, std::max<uint64_t>(tot, 1)));
+  HIPCHK(hipMalloc((void**)&d_offs, n * 8));
+  HIPCHK(hipMalloc((void**)&d_lens, n * 4));
+  HIPCHK(hipMalloc((void**)&d_out, n * 32));
+  if (tot) HIPCHK(hipMemcpy(d_msgs, msgs, tot, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_offs, offs.data(), n * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_lens, lens, n * 4, hipMemcpyHostToDevice));
+  const uint32_t block = 256;
+  const uint32_t grid = (uint32_t)((n + block - 1) / block);
+  HIPCHK(hipEventRecord(e.ev0, e.stream));
+  hipLaunchKernelGGL(k_keccak, dim3(grid), dim3(block), 0, e.stream, d_msgs, d_offs, d_lens, n, d_out);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e.ev1, e.stream));
+  HIPCHK(hipEventSynchronize(e.ev1));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e.ev0, e.ev1));
+  e.stats.launches++;
+  e.stats.last_kernel_ms = ms;
+  e.stats.kernel_ms_total += ms;
+  HIPCHK(hipMemcpy(out32, d_out, n * 32, hipMemcpyDeviceToHost));
+  (void)hipFree(d_msgs);
+  (void)hipFree(d_offs);
+  (void)hipFree(d_lens);
+  (void)hipFree(d_out);
+  return MG_OK;
+}
+
+int mg_stats(mg_stats_t* out) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  *out = e.stats;
+  return MG_OK;
+}
+
+int mg_stats_reset(void) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  mg_stats_t keep = e.stats;
+  std::memset(&e.stats, 0, sizeof(e.stats));
+  e.stats.device = keep.device;
+  e.stats.cu_count = keep.cu_count;
+  e.stats.clock_mhz = keep.clock_mhz;
+  return MG_OK;
+}
+
+int mg_dev_alloc(size_t bytes, void** dptr) {
+  HIPCHK(hipMalloc(dptr, std::max<size_t>(bytes, 1)));
+  return MG_OK;
+}
+int mg_dev_free(void* dptr) {
+  HIPCHK(hipFree(dptr));
+  return MG_OK;
+}
+int mg_dev_upload(void* dptr, const void* src, size_t bytes) {
+  HIPCHK(hipMemcpy(dptr, src, bytes, hipMemcpyHostToDevice));
+  return MG_OK;
+}
+int mg_dev_download(void* dst, const void* dptr, size_t bytes) {
+  HIPCHK(hipMemcpy(dst, dptr, bytes, hipMemcpyDeviceToHost));
+  return MG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,571 @@
+// Program v1 parser, validator and lowering (host C++).
+//
+// Lowering does three things the kernels rely on:
+//  1. arrays/UFs -> per-lane canonicalising lookups: a Select over
+//     Store(...Store(A, i1, v1)..., ik, vk) at index j becomes
+//     ite(j==ik, vk, ... ite(j==i1, v1, LOOKUP_A(j)) ...), and LOOKUP_A returns
+//     the value of the first earlier site of A whose key equals j, else the
+//     site's own coordinate (z3 array/UF semantics under a finite model,
+//     mythril/laser/smt/array.py:16-63, function.py:7-25);
+//  2. a liveness pass + first-fit allocator over 32-bit words gives every value a
+//     slot in the per-lane value file (destinations never alias live operands);
+//  3. roots become K_ASSERT right after they are computed, so the verdict is a
+//     running AND and a wave can stop once all its lanes failed.
+#include "program.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+
+namespace mg {
+
+static inline uint32_t L_of(uint32_t w) { return (w + 31) / 32; }
+
+uint64_t op_cost(uint32_t k, uint32_t w, uint32_t wa) {
+  // SURVEY.md §8(d) fixed cost table, in 32-bit limb operations.
+  const uint64_t L = L_of(w), La = L_of(wa);
+  switch (k) {
+    case K_ADD: case K_SUB: case K_NEG: case K_AND: case K_OR: case K_XOR: case K_NOT:
+    case K_ITE: case K_EXTRACT: case K_CONCAT: case K_ZEXT: case K_SEXT:
+      return L;
+    case K_EQ: case K_ULT: case K_ULE: case K_SLT: case K_SLE:
+      return 2 * La;
+    case K_SHL: case K_LSHR: case K_ASHR:
+      return 4 * L;
+    case K_MUL:
+      return L * (L + 1) / 2 + L * (L - 1) / 2 + L * L;
+    case K_UMUL_NOOVF:
+      return 4 * La * La;
+    case K_UDIV: case K_UREM: case K_SDIV: case K_SREM: case K_SMOD:
+      return 4 * L * L + 16 * L;
+    case K_EXP:
+      // 128 x (bits + popcount) with the mean popcount of a w-bit exponent
+      return 128ull * (uint64_t)(w + w / 2);
+    default:
+      return 0;
+  }
+}
+
+namespace {
+
+struct Node {
+  uint32_t op, width, a, b, c, p0, p1, p2;
+};
+
+struct ArrInfo {
+  bool is_table = false;
+  uint32_t table = MG_NONE;     // table index when based on an array variable
+  uint32_t default_node = MG_NONE;  // K() default node
+  std::vector<std::pair<uint32_t, uint32_t>> stores;  // (index node, value node), oldest first
+  uint32_t dom = 0, rng = 0;
+};
+
+struct VInstr {
+  uint32_t op, wd, dst, a, b, c, p0, p1;
+  std::vector<uint32_t> prior;  // LOOKUP: flattened (key vid, val vid) pairs
+};
+
+struct Fail {
+  int code;
+  std::string msg;
+};
+
+[[noreturn]] void fail(int code, const std::string& m) { throw Fail{code, m}; }
+
+class Alloc {
+ public:
+  uint32_t alloc(uint32_t n) {
+    for (auto it = free_.begin(); it != free_.end(); ++it) {
+      if (it->second >= n) {
+        uint32_t s = it->first;
+        if (it->second == n) {
+          free_.erase(it);
+        } else {
+          uint32_t ns = it->first + n, nl = it->second - n;
+          free_.erase(it);
+          free_.emplace(ns, nl);
+        }
+        return s;
+      }
+    }
+    uint32_t s = top_;
+    top_ += n;
+    return s;
+  }
+  void release(uint32_t s, uint32_t n) {
+    auto it = free_.emplace(s, n).first;
+    // merge with next
+    auto nx = std::next(it);
+    if (nx != free_.end() && it->first + it->second == nx->first) {
+      it->second += nx->second;
+      free_.erase(nx);
+    }
+    if (it != free_.begin()) {
+      auto pv = std::prev(it);
+      if (pv->first + pv->second == it->first) {
+        pv->second += it->second;
+        free_.erase(it);
+      }
+    }
+  }
+  uint32_t high() const { return top_; }
+
+ private:
+  std::map<uint32_t, uint32_t> free_;
+  uint32_t top_ = 0;
+};
+
+}  // namespace
+
+int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& err) {
+  try {
+    if (blob == nullptr || len < 64 || (len % 4) != 0) fail(MG_E_INVALID, "program blob too short");
+    std::vector<uint32_t> w(len / 4);
+    std::memcpy(w.data(), blob, len);
+    if (w[0] != MG_MAGIC) fail(MG_E_INVALID, "bad magic");
+    if (w[1] != MG_VERSION) fail(MG_E_INVALID, "unsupported program version");
+    const uint64_t n_nodes = w[2], n_roots = w[3], n_coords = w[4], n_tables = w[5], n_consts = w[6],
+                   n_watch = w[7];
+    const uint64_t need = 16 + n_nodes * 8 + n_roots + n_coords * 4 + n_tables * 4 + n_watch + n_consts;
+    if (need != w.size()) fail(MG_E_INVALID, "program length does not match header");
+    if (n_nodes == 0) fail(MG_E_INVALID, "empty program");
+    size_t pos = 16;
+    std::vector<Node> nodes(n_nodes);
+    for (uint64_t i = 0; i < n_nodes; i++, pos += 8) std::memcpy(&nodes[i], &w[pos], 32);
+    std::vector<uint32_t> roots(w.begin() + pos, w.begin() + pos + n_roots);
+    pos += n_roots;
+    struct C4 { uint32_t width, kind, node, table; };
+    std::vector<C4> coords(n_coords);
+    for (uint64_t i = 0; i < n_coords; i++, pos += 4) std::memcpy(&coords[i], &w[pos], 16);
+    struct T4 { uint32_t kind, kw, vw, z; };
+    std::vector<T4> tables(n_tables);
+    for (uint64_t i = 0; i < n_tables; i++, pos += 4) std::memcpy(&tables[i], &w[pos], 16);
+    std::vector<uint32_t> watch(w.begin() + pos, w.begin() + pos + n_watch);
+    pos += n_watch;
+    std::vector<uint32_t> consts(w.begin() + pos, w.begin() + pos + n_consts);
+
+    out = Lowered();
+    out.n_nodes = (uint32_t)n_nodes;
+    out.n_roots = (uint32_t)n_roots;
+    out.n_coords = (uint32_t)n_coords;
+    out.n_watch = (uint32_t)n_watch;
+    out.consts = consts;
+
+    // coordinates
+    out.coord_width.resize(n_coords);
+    out.coord_row.resize(n_coords);
+    out.coord_kind.resize(n_coords);
+    out.coord_lazy.assign(n_coords, MG_NONE);
+    uint32_t row = 0;
+    for (uint64_t c = 0; c < n_coords; c++) {
+      if (coords[c].width == 0 || coords[c].width > MG_MAX_WIDTH) fail(MG_E_UNSUPPORTED, "coordinate width");
+      if (coords[c].kind > MG_COORD_UF_SITE) fail(MG_E_INVALID, "coordinate kind");
+      if (coords[c].node >= n_nodes) fail(MG_E_INVALID, "coordinate node");
+      out.coord_width[c] = coords[c].width;
+      out.coord_kind[c] = coords[c].kind;
+      out.coord_row[c] = row;
+      row += L_of(coords[c].width);
+    }
+    out.coord_words = row;
+    for (auto& t : tables) {
+      if (t.kind > MG_TABLE_UF || t.kw == 0 || t.vw == 0 || t.kw > MG_MAX_WIDTH || t.vw > MG_MAX_WIDTH)
+        fail(MG_E_INVALID, "table descriptor");
+    }
+
+    // ---- validate nodes + lower to virtual instructions ---------------
+    const uint32_t NONE = MG_NONE;
+    std::vector<uint32_t> vid(n_nodes, NONE);
+    std::vector<uint32_t> vwidth;  // width per vid
+    std::vector<ArrInfo> arr(n_nodes);
+    std::vector<char> is_arr(n_nodes, 0);
+    std::vector<VInstr> code;
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> table_sites(n_tables);
+    std::vector<uint32_t> site_base_vid(n_coords, NONE);
+    std::vector<char> root_of(n_nodes, 0), watch_of(n_nodes, 0);
+    for (uint32_t r : roots) {
+      if (r >= n_nodes) fail(MG_E_INVALID, "root index");
+      root_of[r] = 1;
+    }
+    std::vector<uint32_t> watch_row(n_watch);
+    uint32_t wrow = 0;
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> watch_at(n_nodes);  // node -> (watch idx, row)
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> watch_site(n_coords);
+    uint32_t max_w = 0;
+
+    auto new_vid = [&](uint32_t width) {
+      vwidth.push_back(width);
+      return (uint32_t)(vwidth.size() - 1);
+    };
+    auto emit = [&](uint32_t op, uint32_t wd, uint32_t dst, uint32_t a = NONE, uint32_t b = NONE, uint32_t c = NONE,
+                    uint32_t p0 = 0, uint32_t p1 = 0) {
+      VInstr v{op, wd, dst, a, b, c, p0, p1, {}};
+      code.push_back(v);
+      return code.size() - 1;
+    };
+    auto val = [&](uint32_t i, uint32_t cur) -> uint32_t {
+      if (i >= cur) fail(MG_E_INVALID, "operand does not precede its use");
+      if (is_arr[i]) fail(MG_E_INVALID, "array used as a value");
+      return vid[i];
+    };
+    auto wid = [&](uint32_t i) { return nodes[i].width; };
+
+    for (uint32_t i = 0; i < n_nodes; i++) {
+      const Node& n = nodes[i];
+      const uint32_t W = n.width;
+      if (n.op >= MG_OP_COUNT) fail(MG_E_UNSUPPORTED, "unknown operator");
+      const bool array_op = n.op == MG_OP_ARR_VAR || n.op == MG_OP_ARR_K || n.op == MG_OP_ARR_STORE;
+      if (!array_op) {
+        if (W == 0 || W > MG_MAX_WIDTH) fail(MG_E_UNSUPPORTED, "value width");
+        max_w = std::max(max_w, W);
+      }
+      auto need_same = [&](uint32_t a, uint32_t b) {
+        if (wid(a) != wid(b)) fail(MG_E_INVALID, "operand width mismatch");
+      };
+      auto need_le256 = [&](uint32_t width) {
+        if (width > 256) fail(MG_E_UNSUPPORTED, "arithmetic wider than 256 bits");
+      };
+      switch (n.op) {
+        case MG_OP_CONST: {
+          if ((uint64_t)n.p0 + L_of(W) > n_consts) fail(MG_E_INVALID, "constant out of range");
+          vid[i] = new_vid(W);
+          emit(K_CONST, W, vid[i], NONE, NONE, NONE, n.p0);
+          break;
+        }
+        case MG_OP_VAR: {
+          if (n.p0 >= n_coords || coords[n.p0].kind != MG_COORD_SCALAR || coords[n.p0].width != W)
+            fail(MG_E_INVALID, "VAR coordinate");
+          vid[i] = new_vid(W);
+          emit(K_COORD, W, vid[i], NONE, NONE, NONE, n.p0, out.coord_row[n.p0]);
+          break;
+        }
+        case MG_OP_ADD: case MG_OP_SUB: case MG_OP_AND: case MG_OP_OR: case MG_OP_XOR:
+        case MG_OP_MUL: case MG_OP_UDIV: case MG_OP_UREM: case MG_OP_SDIV: case MG_OP_SREM:
+        case MG_OP_SMOD: case MG_OP_SHL: case MG_OP_LSHR: case MG_OP_ASHR: case MG_OP_EXP: {
+          uint32_t a = val(n.a, i), b = val(n.b, i);
+          need_same(n.a, n.b);
+          if (wid(n.a) != W) fail(MG_E_INVALID, "result width");
+          static const uint32_t map[] = {0, 0, K_ADD, K_SUB, K_MUL, K_UDIV, K_UREM, K_SDIV, K_SREM, K_SMOD,
+                                         K_AND, K_OR, K_XOR, 0, 0, K_SHL, K_LSHR, K_ASHR};
+          uint32_t k = n.op == MG_OP_EXP ? (uint32_t)K_EXP : map[n.op];
+          if (k != K_ADD && k != K_SUB && k != K_AND && k != K_OR && k != K_XOR) need_le256(W);
+          vid[i] = new_vid(W);
+          emit(k, W, vid[i], a, b, NONE, 0, W);
+          break;
+        }
+        case MG_OP_NOT: case MG_OP_NEG: {
+          uint32_t a = val(n.a, i);
+          if (wid(n.a) != W) fail(MG_E_INVALID, "result width");
+          vid[i] = new_vid(W);
+          emit(n.op == MG_OP_NOT ? K_NOT : K_NEG, W, vid[i], a, NONE, NONE, 0, W);
+          break;
+        }
+        case MG_OP_CONCAT: {
+          uint32_t a = val(n.a, i), b = val(n.b, i);
+          if ((uint64_t)wid(n.a) + wid(n.b) != W) fail(MG_E_INVALID, "concat width");
+          vid[i] = new_vid(W);
+          emit(K_CONCAT, W, vid[i], a, b, NONE, 0, wid(n.b));
+          break;
+        }
+        case MG_OP_EXTRACT: {
+          uint32_t a = val(n.a, i);
+          if ((uint64_t)n.p0 + W > wid(n.a)) fail(MG_E_INVALID, "extract range");
+          vid[i] = new_vid(W);
+          emit(K_EXTRACT, W, vid[i], a, NONE, NONE, n.p0, wid(n.a));
+          break;
+        }
+        case MG_OP_ZEXT: case MG_OP_SEXT: {
+          uint32_t a = val(n.a, i);
+          if (wid(n.a) >= W) fail(MG_E_INVALID, "extend width");
+          vid[i] = new_vid(W);
+          emit(n.op == MG_OP_ZEXT ? K_ZEXT : K_SEXT, W, vid[i], a, NONE, NONE, 0, wid(n.a));
+          break;
+        }
+        case MG_OP_ITE: {
+          uint32_t a = val(n.a, i), b = val(n.b, i), c = val(n.c, i);
+          if (wid(n.a) != 1 || wid(n.b) != W || wid(n.c) != W) fail(MG_E_INVALID, "ite widths");
+          vid[i] = new_vid(W);
+          emit(K_ITE, W, vid[i], a, b, c, 0, W);
+          break;
+        }
+        case MG_OP_EQ: case MG_OP_ULT: case MG_OP_ULE: case MG_OP_SLT: case MG_OP_SLE:
+        case MG_OP_UMUL_NOOVF: {
+          uint32_t a = val(n.a, i), b = val(n.b, i);
+          need_same(n.a, n.b);
+          if (W != 1) fail(MG_E_INVALID, "predicate width");
+          static const uint32_t map[] = {K_EQ, K_ULT, K_ULE, K_SLT, K_SLE, K_UMUL_NOOVF};
+          uint32_t k = map[n.op - MG_OP_EQ];
+          if (k == K_UMUL_NOOVF) need_le256(wid(n.a));
+          vid[i] = new_vid(1);
+          emit(k, 1, vid[i], a, b, NONE, 0, wid(n.a));
+          break;
+        }
+        case MG_OP_ARR_VAR: {
+          if (n.p0 >= n_tables || tables[n.p0].kind != MG_TABLE_ARRAY) fail(MG_E_INVALID, "array table");
+          is_arr[i] = 1;
+          arr[i].is_table = true;
+          arr[i].table = n.p0;
+          arr[i].dom = tables[n.p0].kw;
+          arr[i].rng = tables[n.p0].vw;
+          break;
+        }
+        case MG_OP_ARR_K: {
+          if (n.a >= i || is_arr[n.a]) fail(MG_E_INVALID, "K default");
+          is_arr[i] = 1;
+          arr[i].default_node = n.a;
+          arr[i].rng = wid(n.a);
+          arr[i].dom = 0;  // any
+          break;
+        }
+        case MG_OP_ARR_STORE: {
+          if (n.a >= i || !is_arr[n.a]) fail(MG_E_INVALID, "store base");
+          if (n.b >= i || n.c >= i || is_arr[n.b] || is_arr[n.c]) fail(MG_E_INVALID, "store operands");
+          is_arr[i] = 1;
+          arr[i] = arr[n.a];
+          if (arr[i].dom == 0) arr[i].dom = wid(n.b);
+          if (wid(n.b) != arr[i].dom || wid(n.c) != arr[i].rng) fail(MG_E_INVALID, "store sorts");
+          arr[i].stores.emplace_back(n.b, n.c);
+          break;
+        }
+        case MG_OP_SELECT: {
+          if (n.a >= i || !is_arr[n.a]) fail(MG_E_INVALID, "select array");
+          const ArrInfo& A = arr[n.a];
+          uint32_t key = val(n.b, i);
+          if (A.dom && wid(n.b) != A.dom) fail(MG_E_INVALID, "select index width");
+          if (A.rng != W) fail(MG_E_INVALID, "select width");
+          uint32_t cur;
+          if (A.is_table) {
+            if (n.p0 >= n_coords || coords[n.p0].kind != MG_COORD_ARRAY_SITE || coords[n.p0].table != A.table ||
+                coords[n.p0].width != W)
+              fail(MG_E_INVALID, "select site coordinate");
+            uint32_t dflt = new_vid(W);
+            emit(K_COORD, W, dflt, NONE, NONE, NONE, n.p0, out.coord_row[n.p0]);
+            cur = new_vid(W);
+            size_t at = emit(K_LOOKUP, W, cur, key, wid(n.b), 0, dflt, 0);
+            auto& prior = table_sites[A.table];
+            for (auto& pr : prior) {
+              if (vwidth[pr.first] != wid(n.b)) continue;  // same name, other sort: separate table
+              code[at].prior.push_back(pr.first);
+              code[at].prior.push_back(pr.second);
+            }
+            code[at].c = (uint32_t)(code[at].prior.size() / 2);
+            prior.emplace_back(key, cur);
+            site_base_vid[n.p0] = cur;
+          } else {
+            if (n.p0 != NONE) fail(MG_E_INVALID, "select over K() has no site");
+            cur = vid[A.default_node];
+          }
+          for (auto& st : A.stores) {
+            uint32_t e = new_vid(1);
+            emit(K_EQ, 1, e, key, vid[st.first], NONE, 0, wid(n.b));
+            uint32_t nv = new_vid(W);
+            emit(K_ITE, W, nv, e, vid[st.second], cur, 0, W);
+            cur = nv;
+          }
+          vid[i] = cur;
+          break;
+        }
+        case MG_OP_UFAPP: {
+          uint32_t key = val(n.a, i);
+          if (n.p0 >= n_tables || tables[n.p0].kind != MG_TABLE_UF) fail(MG_E_INVALID, "uf table");
+          if (tables[n.p0].kw != wid(n.a) || tables[n.p0].vw != W) fail(MG_E_INVALID, "uf sorts");
+          if (n.p1 >= n_coords || coords[n.p1].kind != MG_COORD_UF_SITE || coords[n.p1].width != W)
+            fail(MG_E_INVALID, "uf site coordinate");
+          uint32_t dflt;
+          if (n.p2 != NONE) {
+            dflt = val(n.p2, i);
+            if (wid(n.p2) != W) fail(MG_E_INVALID, "lazy default width");
+            out.coord_lazy[n.p1] = n.p2;
+          } else {
+            dflt = new_vid(W);
+            emit(K_COORD, W, dflt, NONE, NONE, NONE, n.p1, out.coord_row[n.p1]);
+          }
+          uint32_t v = new_vid(W);
+          size_t at = emit(K_LOOKUP, W, v, key, wid(n.a), 0, dflt, 0);
+          auto& prior = table_sites[n.p0];
+          for (auto& pr : prior) {
+            code[at].prior.push_back(pr.first);
+            code[at].prior.push_back(pr.second);
+          }
+          code[at].c = (uint32_t)(code[at].prior.size() / 2);
+          prior.emplace_back(key, v);
+          site_base_vid[n.p1] = v;
+          vid[i] = v;
+          break;
+        }
+        case MG_OP_KECCAK: {
+          if (W != 256) fail(MG_E_INVALID, "keccak width");
+          uint32_t a = NONE;
+          if (n.a == NONE) {
+            if (n.p0 != 0) fail(MG_E_INVALID, "keccak empty input");
+          } else {
+            a = val(n.a, i);
+            if ((uint64_t)wid(n.a) != 8ull * n.p0 || n.p0 == 0) fail(MG_E_INVALID, "keccak length");
+          }
+          vid[i] = new_vid(256);
+          emit(K_KECCAK, 256, vid[i], a, NONE, NONE, n.p0, 0);
+          break;
+        }
+        default:
+          fail(MG_E_UNSUPPORTED, "operator");
+      }
+      if (root_of[i]) {
+        if (is_arr[i] || W != 1) fail(MG_E_INVALID, "root is not Bool");
+        emit(K_ASSERT, 1, NONE, vid[i]);
+      }
+    }
+    // watch list (after all nodes: watch entries refer to nodes or site bases)
+    for (uint64_t j = 0; j < n_watch; j++) {
+      uint32_t wv = watch[j];
+      uint32_t v, width;
+      if (wv & 0x80000000u) {
+        uint32_t c = wv & 0x7FFFFFFFu;
+        if (c >= n_coords || site_base_vid[c] == NONE) fail(MG_E_INVALID, "watch site");
+        v = site_base_vid[c];
+        width = vwidth[v];
+      } else {
+        if (wv >= n_nodes || is_arr[wv]) fail(MG_E_INVALID, "watch node");
+        v = vid[wv];
+        width = nodes[wv].width;
+      }
+      watch_row[j] = wrow;
+      // insert the K_WATCH right after the instruction defining v
+      VInstr wi{K_WATCH, width, NONE, v, NONE, NONE, wrow, 0, {}};
+      size_t def = 0;
+      for (size_t k = 0; k < code.size(); k++)
+        if (code[k].dst == v) { def = k; break; }
+      code.insert(code.begin() + def + 1, wi);
+      wrow += L_of(width);
+    }
+    out.watch_row = watch_row;
+    out.watch_words = wrow;
+    out.max_width = max_w;
+
+    // ---- liveness + allocation ----------------------------------------
+    const size_t nv = vwidth.size();
+    std::vector<int64_t> last(nv, -1), def(nv, -1);
+    for (size_t k = 0; k < code.size(); k++) {
+      const VInstr& c = code[k];
+      auto use = [&](uint32_t v) {
+        if (v != NONE && v < nv) last[v] = (int64_t)k;
+      };
+      if (c.op == K_LOOKUP) {
+        use(c.a);
+        use(c.p0);
+        for (uint32_t v : c.prior) use(v);
+      } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT ||
+                 c.op == K_KECCAK || c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
+        use(c.a);
+        use(c.b);
+      } else if (c.op != K_CONST && c.op != K_COORD) {
+        use(c.a);
+        use(c.b);
+        use(c.c);
+      }
+      if (c.dst != NONE && def[c.dst] < 0) def[c.dst] = (int64_t)k;
+    }
+    std::vector<uint32_t> slot(nv, NONE);
+    std::vector<std::vector<uint32_t>> dies(code.size());
+    for (size_t v = 0; v < nv; v++) {
+      if (def[v] < 0) continue;
+      int64_t d = std::max(last[v], def[v]);
+      dies[(size_t)d].push_back((uint32_t)v);
+    }
+    Alloc al;
+    out.code.clear();
+    out.aux.clear();
+    for (size_t k = 0; k < code.size(); k++) {
+      VInstr c = code[k];
+      if (c.dst != NONE && slot[c.dst] == NONE) slot[c.dst] = al.alloc(L_of(vwidth[c.dst]));
+      auto S = [&](uint32_t v) -> uint32_t {
+        if (v == NONE) return NONE;
+        if (slot[v] == NONE) fail(MG_E_INVALID, "internal: use before definition");
+        return slot[v];
+      };
+      Instr in{c.op, c.wd, c.dst == NONE ? NONE : slot[c.dst], 0, 0, 0, c.p0, c.p1};
+      if (c.op == K_LOOKUP) {
+        in.a = S(c.a);
+        in.b = c.b;
+        in.c = c.c;
+        in.p0 = S(c.p0);
+        in.p1 = (uint32_t)out.aux.size();
+        for (uint32_t v : c.prior) out.aux.push_back(S(v));
+      } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT || c.op == K_KECCAK ||
+                 c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
+        in.a = S(c.a);
+        in.b = S(c.b);
+        in.c = NONE;
+      } else if (c.op == K_CONST || c.op == K_COORD) {
+        in.a = in.b = in.c = NONE;
+      } else {
+        in.a = S(c.a);
+        in.b = S(c.b);
+        in.c = S(c.c);
+      }
+      out.code.push_back(in);
+      // cost
+      uint32_t wa = c.p1;
+      if (c.op == K_LOOKUP) {
+        out.limb_ops += 3ull * L_of(c.b) * c.c + L_of(c.wd);
+      } else if (c.op == K_KECCAK) {
+        out.limb_ops += 7500ull * (c.p0 / 136 + 1);
+      } else {
+        out.limb_ops += op_cost(c.op, c.wd, wa ? wa : c.wd);
+      }
+      for (uint32_t v : dies[k]) al.release(slot[v], L_of(vwidth[v]));
+    }
+    out.value_words = std::max<uint32_t>(al.high(), 1);
+    return MG_OK;
+  } catch (const Fail& f) {
+    err = f.msg;
+    return f.code;
+  } catch (const std::exception& e) {
+    err = e.what();
+    return MG_E_INVALID;
+  }
+}
+
+int parse_gen(const Lowered& prog, const uint32_t* blob, size_t n_words, std::vector<GenSpec>& specs,
+              std::vector<uint32_t>& consts, std::string& err) {
+  if (blob == nullptr || n_words < 4 || blob[0] != MG_GEN_MAGIC) {
+    err = "bad generator blob";
+    return MG_E_INVALID;
+  }
+  const uint32_t nc = blob[1], ncw = blob[2];
+  if (nc != prog.n_coords || 4ull + 8ull * nc + ncw != n_words) {
+    err = "generator does not match program";
+    return MG_E_INVALID;
+  }
+  specs.resize(nc);
+  for (uint32_t c = 0; c < nc; c++) std::memcpy(&specs[c], blob + 4 + 8 * c, 32);
+  consts.assign(blob + 4 + 8 * nc, blob + n_words);
+  for (uint32_t c = 0; c < nc; c++) {
+    const GenSpec& s = specs[c];
+    const uint32_t L = L_of(prog.coord_width[c]);
+    auto in_range = [&](uint64_t off, uint64_t n) { return off + n <= ncw; };
+    switch (s.kind) {
+      case MG_GEN_UNIFORM:
+        break;
+      case MG_GEN_RANGE:
+      case MG_GEN_FIXED:
+        if (!in_range(s.p[0], L)) { err = "generator constant out of range"; return MG_E_INVALID; }
+        break;
+      case MG_GEN_ALIGNED:
+        if (!in_range(s.p[0], L) || s.p[1] > 255) { err = "aligned generator"; return MG_E_INVALID; }
+        break;
+      case MG_GEN_DICT:
+      case MG_GEN_MIXED:
+        if (s.p[1] == 0 && s.kind == MG_GEN_DICT) { err = "empty dictionary"; return MG_E_INVALID; }
+        if (!in_range(s.p[0], (uint64_t)s.p[1] * L)) { err = "dictionary out of range"; return MG_E_INVALID; }
+        if (s.kind == MG_GEN_MIXED && s.p[3] != MG_NONE && s.p[3] >= nc) { err = "copy source"; return MG_E_INVALID; }
+        break;
+      case MG_GEN_LAZY:
+        break;  // default comes from the program (UFAPP p2); the coordinate is unused
+      default:
+        err = "unknown generator kind";
+        return MG_E_INVALID;
+    }
+  }
+  return MG_OK;
+}
+
+}  // namespace mg

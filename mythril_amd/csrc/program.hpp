@@ -1,0 +1,75 @@
+// Program v1 parser + lowering to the device instruction stream.
+//
+// Host-only C++ (no HIP); compiled into libmythgpu.so and also testable on a
+// CPU-only machine through mg_program_check().
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/mythgpu.h"
+
+namespace mg {
+
+// Device instruction ops (after lowering). Arrays and UF applications are gone:
+// SELECT-over-store-chains become EQ/ITE chains over a canonicalising LOOKUP.
+enum KOp : uint32_t {
+  K_CONST = 0,   // dst <- consts[p0 ..]
+  K_COORD,       // dst <- coordinate p0 (eval: SoA row p1; search: generator)
+  K_ADD, K_SUB, K_MUL, K_UDIV, K_UREM, K_SDIV, K_SREM, K_SMOD,
+  K_AND, K_OR, K_XOR, K_NOT, K_NEG,
+  K_SHL, K_LSHR, K_ASHR,
+  K_CONCAT,      // dst <- a:b ; p1 = width(b)
+  K_EXTRACT,     // dst <- a[lo +: wd] ; p0 = lo, p1 = width(a)
+  K_ZEXT,        // p1 = width(a)
+  K_SEXT,        // p1 = width(a)
+  K_ITE,         // dst <- a ? b : c
+  K_EQ, K_ULT, K_ULE, K_SLT, K_SLE,   // p1 = operand width
+  K_UMUL_NOOVF,  // p1 = operand width
+  K_EXP,
+  K_LOOKUP,      // dst <- first prior (key==a) value, else slot p0 ; b = key width, c = n_prior, p1 = aux offset
+  K_KECCAK,      // dst <- keccak256(bytes of a) ; p0 = byte length, a = MG_NONE for empty input
+  K_ASSERT,      // verdict &= a ; may early-exit the wave
+  K_WATCH,       // watch rows [p0 .. p0+L) <- a  (eval only)
+  K_COPY,        // dst <- a
+  K_COUNT
+};
+
+struct Instr {
+  uint32_t op, wd, dst, a, b, c, p0, p1;
+};
+static_assert(sizeof(Instr) == 32, "Instr must be 8 words");
+
+struct Lowered {
+  std::vector<Instr> code;
+  std::vector<uint32_t> consts;
+  std::vector<uint32_t> aux;          // LOOKUP prior lists: pairs (key slot, value slot)
+  uint32_t value_words = 0;
+  uint32_t n_nodes = 0, n_roots = 0, n_coords = 0, n_watch = 0;
+  std::vector<uint32_t> coord_width;
+  std::vector<uint32_t> coord_row;    // SoA row offset of each coordinate
+  std::vector<uint32_t> coord_kind;
+  std::vector<uint32_t> coord_lazy;   // node providing a lazy default (MG_NONE if none)
+  uint32_t coord_words = 0;
+  std::vector<uint32_t> watch_row;
+  uint32_t watch_words = 0;
+  uint64_t limb_ops = 0;              // fixed cost table, per candidate
+  uint32_t max_width = 0;
+};
+
+// Parse + validate + lower. Returns MG_OK or an MG_E_* code with `err` set.
+int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& err);
+
+// Fixed algorithmic cost table (32-bit limb ops), SURVEY.md §8(d).
+uint64_t op_cost(uint32_t node_op, uint32_t width, uint32_t operand_width);
+
+struct GenSpec {
+  uint32_t kind, p[7];
+};
+
+// Validate a generator blob against a lowered program; fills specs/consts.
+int parse_gen(const Lowered& prog, const uint32_t* blob, size_t n_words, std::vector<GenSpec>& specs,
+              std::vector<uint32_t>& consts, std::string& err);
+
+}  // namespace mg

@@ -1,0 +1,240 @@
+"""ctypes binding of ``libmythgpu.so`` (C-ABI in ``include/mythgpu.h``).
+
+The reference reaches its solver through z3py's ctypes binding of libz3; this
+module is the same kind of binding for the GPU engine.  There is no CPU
+fallback: if the library or a gfx950 device is missing, the calls raise
+:class:`EngineError` (the ``get_model`` hook then leaves the query to z3).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "libmythgpu.so"
+
+MG_OK = 0
+MG_E_INVALID = -1
+MG_E_UNSUPPORTED = -2
+MG_E_HIP = -3
+MG_E_NODEVICE = -4
+MG_E_NOMEM = -5
+MG_E_NOTINIT = -6
+MG_SEARCH_EARLY_EXIT = 1
+NO_HIT = (1 << 64) - 1
+
+EXPORTS = [
+    "mg_init", "mg_shutdown", "mg_last_error", "mg_version", "mg_program_check", "mg_program_load",
+    "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_free", "mg_eval", "mg_eval_dev",
+    "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
+    "mg_dev_free", "mg_dev_upload", "mg_dev_download",
+]
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mythgpu error {code}: {msg}")
+        self.code = code
+
+
+class EngineUnsupported(EngineError):
+    pass
+
+
+class ProgramInfo(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_uint32), ("n_instrs", C.c_uint32), ("n_coords", C.c_uint32), ("n_roots", C.c_uint32),
+        ("value_words", C.c_uint32), ("uses_lds", C.c_uint32), ("n_watch", C.c_uint32),
+        ("watch_words", C.c_uint32), ("coord_words", C.c_uint32), ("reserved", C.c_uint32),
+        ("limb_ops", C.c_uint64),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("programs_loaded", C.c_uint64), ("launches", C.c_uint64), ("candidates", C.c_uint64),
+        ("hits", C.c_uint64), ("kernel_ms_total", C.c_double), ("last_kernel_ms", C.c_double),
+        ("last_candidates", C.c_uint64), ("device", C.c_uint32), ("cu_count", C.c_uint32),
+        ("clock_mhz", C.c_uint32), ("reserved", C.c_uint32),
+    ]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: Optional[Path] = None) -> C.CDLL:
+    """Load (and type) the shared library.  Loading needs no GPU."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        p = Path(path or LIB_PATH)
+        if not p.exists():
+            raise EngineError(MG_E_NODEVICE, f"{p} is not built (run mythril_amd.build.build())")
+        lib = C.CDLL(str(p))
+        u8p, u32p, u64p = C.POINTER(C.c_uint8), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
+        sig = {
+            "mg_init": (C.c_int, [C.c_uint32]),
+            "mg_shutdown": (None, []),
+            "mg_last_error": (C.c_char_p, []),
+            "mg_version": (C.c_int, []),
+            "mg_program_check": (C.c_int, [u8p, C.c_size_t, C.POINTER(ProgramInfo)]),
+            "mg_program_load": (C.c_int, [u8p, C.c_size_t, u64p]),
+            "mg_program_info": (C.c_int, [C.c_uint64, C.POINTER(ProgramInfo)]),
+            "mg_program_free": (C.c_int, [C.c_uint64]),
+            "mg_gen_load": (C.c_int, [C.c_uint64, u32p, C.c_size_t, u64p]),
+            "mg_gen_free": (C.c_int, [C.c_uint64]),
+            "mg_eval": (C.c_int, [C.c_uint64, u32p, C.c_uint64, u8p, u32p]),
+            "mg_eval_dev": (C.c_int, [C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+            "mg_eval_generated": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, u8p, u32p]),
+            "mg_search": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32,
+                                    u64p, u64p]),
+            "mg_keccak256": (C.c_int, [u8p, u32p, C.c_uint64, u8p]),
+            "mg_stats": (C.c_int, [C.POINTER(Stats)]),
+            "mg_stats_reset": (C.c_int, []),
+            "mg_dev_alloc": (C.c_int, [C.c_size_t, C.POINTER(C.c_void_p)]),
+            "mg_dev_free": (C.c_int, [C.c_void_p]),
+            "mg_dev_upload": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+            "mg_dev_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def _check(rc: int):
+    if rc != MG_OK:
+        msg = (_lib.mg_last_error() or b"").decode(errors="replace")
+        if rc == MG_E_UNSUPPORTED:
+            raise EngineUnsupported(rc, msg)
+        raise EngineError(rc, msg)
+
+
+def _u8(buf: bytes):
+    arr = (C.c_uint8 * len(buf)).from_buffer_copy(buf)
+    return arr
+
+
+def _ptr(a: np.ndarray, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def check_program(blob: bytes) -> ProgramInfo:
+    """Validate + lower a program on the host (no GPU)."""
+    lib = load_library()
+    info = ProgramInfo()
+    _check(lib.mg_program_check(_u8(blob), len(blob), C.byref(info)))
+    return info
+
+
+class Engine:
+    """Process-wide handle on one GPU (one process per GPU)."""
+
+    _instance = None
+    _ilock = threading.Lock()
+
+    @classmethod
+    def get(cls) -> "Engine":
+        with cls._ilock:
+            if cls._instance is None:
+                cls._instance = Engine()
+            return cls._instance
+
+    def __init__(self, device: Optional[int] = None):
+        self.lib = load_library()
+        if device is None:
+            device = int(os.environ.get("MYTHGPU_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+        _check(self.lib.mg_init(1 << device))
+        self.device = device
+
+    # programs -------------------------------------------------------
+    def load(self, blob: bytes) -> int:
+        h = C.c_uint64()
+        _check(self.lib.mg_program_load(_u8(blob), len(blob), C.byref(h)))
+        return h.value
+
+    def info(self, prog: int) -> ProgramInfo:
+        info = ProgramInfo()
+        _check(self.lib.mg_program_info(prog, C.byref(info)))
+        return info
+
+    def free(self, prog: int):
+        _check(self.lib.mg_program_free(prog))
+
+    def load_gen(self, prog: int, blob: np.ndarray) -> int:
+        blob = np.ascontiguousarray(blob, dtype=np.uint32)
+        h = C.c_uint64()
+        _check(self.lib.mg_gen_load(prog, _ptr(blob, C.c_uint32), blob.size, C.byref(h)))
+        return h.value
+
+    def free_gen(self, gen: int):
+        _check(self.lib.mg_gen_free(gen))
+
+    # evaluation -----------------------------------------------------
+    def eval(self, prog: int, soa: np.ndarray, n: int, watch_words: int = 0):
+        """Evaluate n candidates given as a [coord_words][n] uint32 SoA."""
+        soa = np.ascontiguousarray(soa, dtype=np.uint32)
+        ver = np.zeros(n, dtype=np.uint8)
+        watch = np.zeros((max(watch_words, 1), n), dtype=np.uint32) if watch_words else None
+        _check(self.lib.mg_eval(prog, _ptr(soa, C.c_uint32), n, _ptr(ver, C.c_uint8),
+                                _ptr(watch, C.c_uint32) if watch is not None else None))
+        return ver, watch
+
+    def eval_generated(self, prog: int, gen: int, seed: int, start: int, n: int, watch_words: int = 0):
+        ver = np.zeros(n, dtype=np.uint8)
+        watch = np.zeros((max(watch_words, 1), n), dtype=np.uint32) if watch_words else None
+        _check(self.lib.mg_eval_generated(prog, gen, seed, start, n, _ptr(ver, C.c_uint8),
+                                          _ptr(watch, C.c_uint32) if watch is not None else None))
+        return ver, watch
+
+    def search(self, prog: int, gen: int, seed: int, start: int, count: int, early_exit: bool = True):
+        fh, nh = C.c_uint64(), C.c_uint64()
+        flags = MG_SEARCH_EARLY_EXIT if early_exit else 0
+        _check(self.lib.mg_search(prog, gen, seed, start, count, flags, C.byref(fh), C.byref(nh)))
+        return (None if fh.value == NO_HIT else fh.value), nh.value
+
+    def keccak256(self, msgs):
+        msgs = [bytes(m) for m in msgs]
+        n = len(msgs)
+        if n == 0:
+            return []
+        cat = b"".join(msgs) or b"\0"
+        lens = np.array([len(m) for m in msgs], dtype=np.uint32)
+        out = np.zeros(n * 32, dtype=np.uint8)
+        _check(self.lib.mg_keccak256(_u8(cat), _ptr(lens, C.c_uint32), n, _ptr(out, C.c_uint8)))
+        return [out[32 * i:32 * i + 32].tobytes() for i in range(n)]
+
+    def stats(self) -> Stats:
+        s = Stats()
+        _check(self.lib.mg_stats(C.byref(s)))
+        return s
+
+    def reset_stats(self):
+        _check(self.lib.mg_stats_reset())
+
+    # device buffers (inputs resident in HBM) ------------------------
+    def dev_alloc(self, nbytes: int) -> int:
+        p = C.c_void_p()
+        _check(self.lib.mg_dev_alloc(nbytes, C.byref(p)))
+        return p.value
+
+    def dev_free(self, p: int):
+        _check(self.lib.mg_dev_free(p))
+
+    def dev_upload(self, p: int, arr: np.ndarray):
+        arr = np.ascontiguousarray(arr)
+        _check(self.lib.mg_dev_upload(p, arr.ctypes.data, arr.nbytes))
+
+    def dev_download(self, arr: np.ndarray, p: int):
+        _check(self.lib.mg_dev_download(arr.ctypes.data, p, arr.nbytes))
+
+    def eval_dev(self, prog: int, d_soa: int, n: int, d_ver: int, d_watch: int = 0):
+        _check(self.lib.mg_eval_dev(prog, d_soa, n, d_ver, d_watch or None))

@@ -1,0 +1,273 @@
+"""Candidate generation, GPU search and model materialisation.
+
+This is the engine's answer to ``Optimize.check()`` for SAT instances
+(``mythril/support/model.py:44``): sweep candidate indices on the GPU until one
+satisfies every constraint, then read the winning candidate back as a finite
+model (``Solver.model()``, ``laser/smt/solver/solver.py:59-64``).
+
+Generator heuristics (per coordinate, all on device, pure functions of
+``(seed, index, coordinate)`` so the first hit is the same on any GPU count):
+
+* scalars: a MIXED draw over a dictionary of the query's own literals of that
+  width (plus 0, 1, 2^w-1, the three LASER actor addresses of
+  ``transaction/symbolic.py:22-33``), +/-1/2 around them, copies of another
+  coordinate of the same width (equalities between symbols are common),
+  small values (calldatasize, loop counters), and uniform bits;
+* keccak UF sites: multiples of 64 inside the interval the side condition
+  pins (``keccak_function_manager.py:121-149``), read from the query's own
+  constants (never recomputed);
+* inverse-UF sites: lazily equal to the forward argument (set in ``ssa.py``).
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import ssa
+from .smt import terms as T
+
+GEN_MAGIC = 0x314E4547
+GEN_UNIFORM, GEN_RANGE, GEN_DICT, GEN_MIXED, GEN_ALIGNED, GEN_FIXED, GEN_LAZY = range(7)
+NONE = ssa.MG_NONE
+
+ACTORS = [
+    0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE,  # CREATOR  (transaction/symbolic.py:22-33)
+    0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF,  # ATTACKER
+    0xAAAAAAAABBBBBBBBCCCCCCCCDDDDDDDDEEEEEEEE,  # SOMEGUY
+]
+
+P16 = 65536
+
+
+class GenBuilder:
+    """Assemble a generator blob (``include/mythgpu.h`` MG_GEN_MAGIC layout)."""
+
+    def __init__(self, P: ssa.Program):
+        self.P = P
+        self.specs: List[List[int]] = [[GEN_UNIFORM, 0, 0, 0, 0, 0, 0, 0] for _ in P.coords]
+        self.consts: List[int] = []
+
+    def _push(self, values: Sequence[int], w: int) -> int:
+        off = len(self.consts)
+        for v in values:
+            self.consts.extend(ssa.int_to_limbs(int(v) % (1 << w), w))
+        return off
+
+    def uniform(self, c: int):
+        self.specs[c] = [GEN_UNIFORM, 0, 0, 0, 0, 0, 0, 0]
+
+    def fixed(self, c: int, v: int):
+        w = self.P.coords[c].width
+        self.specs[c] = [GEN_FIXED, self._push([v], w), 0, 0, 0, 0, 0, 0]
+
+    def range(self, c: int, lo: int, span: int):
+        w = self.P.coords[c].width
+        self.specs[c] = [GEN_RANGE, self._push([lo], w), span & 0xFFFFFFFF, 0, 0, 0, 0, 0]
+
+    def dict(self, c: int, values: Sequence[int]):
+        w = self.P.coords[c].width
+        self.specs[c] = [GEN_DICT, self._push(values, w), len(values), 0, 0, 0, 0, 0]
+
+    def aligned(self, c: int, lo: int, log2_align: int, count: int):
+        w = self.P.coords[c].width
+        self.specs[c] = [GEN_ALIGNED, self._push([lo], w), log2_align, min(count, 1 << 32) & 0xFFFFFFFF,
+                         0, 0, 0, 0]
+
+    def lazy(self, c: int):
+        self.specs[c] = [GEN_LAZY, 0, 0, 0, 0, 0, 0, 0]
+
+    def mixed(self, c: int, values: Sequence[int], p_dict: float, copy_from: Optional[int] = None,
+              p_copy: float = 0.0, p_delta: float = 0.0, small_bits: int = 0, p_small: float = 0.0):
+        w = self.P.coords[c].width
+        values = list(values)
+        off = self._push(values, w) if values else 0
+        self.specs[c] = [
+            GEN_MIXED, off, len(values), int(p_dict * P16) if values else 0,
+            NONE if copy_from is None else copy_from, int(p_copy * P16), int(p_delta * P16),
+            ((small_bits & 0xFFFF) << 16) | (int(p_small * P16) & 0xFFFF),
+        ]
+
+    def blob(self) -> np.ndarray:
+        words = [GEN_MAGIC, len(self.specs), len(self.consts), 0]
+        for s in self.specs:
+            words.extend(int(x) & 0xFFFFFFFF for x in s)
+        words.extend(self.consts)
+        return np.array(words, dtype=np.uint32)
+
+
+def _interval_bounds(P: ssa.Program):
+    """For each UF-site coordinate, the [lo, hi) literal bounds the query puts on
+    the application (ULE(lo, f(x)) / ULT(f(x), hi), keccak_function_manager.py:138-143)."""
+    out: Dict[int, list] = {}
+    site_of_node = {P.site_val_node[c.index]: c.index for c in P.sites}
+    for n, node in enumerate(P.nodes):
+        op = node[0]
+        if op not in (ssa.OPS["ULT"], ssa.OPS["ULE"]):
+            continue
+        a, b = node[2], node[3]
+        ta, tb = P.node_term[a], P.node_term[b]
+        if b in site_of_node and ta is not None and ta.op == "bvconst":
+            lo = ta.params[0]
+            out.setdefault(site_of_node[b], [None, None])[0] = lo if op == ssa.OPS["ULE"] else lo + 1
+        if a in site_of_node and tb is not None and tb.op == "bvconst":
+            hi = tb.params[0]
+            out.setdefault(site_of_node[a], [None, None])[1] = hi if op == ssa.OPS["ULT"] else hi + 1
+    return out
+
+
+def default_generator(P: ssa.Program, extra_dict: Sequence[int] = ()) -> GenBuilder:
+    g = GenBuilder(P)
+    by_width: Dict[int, set] = {}
+    for v, w in P.const_values:
+        by_width.setdefault(w, set()).add(v)
+    bounds = _interval_bounds(P)
+    last_of_width: Dict[int, int] = {}
+    for c in P.coords:
+        w = c.width
+        if c.kind == ssa.COORD_UF_SITE and P.nodes[c.node][7] != NONE:
+            g.lazy(c.index)
+            continue
+        if c.kind == ssa.COORD_UF_SITE and c.index in bounds and None not in bounds[c.index]:
+            lo, hi = bounds[c.index]
+            lo = (lo + 63) // 64 * 64
+            if hi > lo:
+                g.aligned(c.index, lo, 6, max(1, (hi - lo) // 64))
+                continue
+        if w == 1:
+            g.uniform(c.index)
+            last_of_width[w] = c.index
+            continue
+        vals = set(by_width.get(w, ()))
+        mask = (1 << w) - 1
+        vals |= {0, 1, mask}
+        for a in list(ACTORS) + list(extra_dict):
+            vals.add(a & mask)
+        for v in list(vals):
+            if v and v < mask:
+                pass
+        vals = sorted(vals)[:4096]
+        copy = last_of_width.get(w)
+        g.mixed(c.index, vals, p_dict=0.45, copy_from=copy, p_copy=0.10 if copy is not None else 0.0,
+                p_delta=0.25, small_bits=min(w, 8), p_small=0.20)
+        last_of_width[w] = c.index
+    return g
+
+
+class SearchResult:
+    def __init__(self, index, hits, scanned, seconds, model=None):
+        self.index, self.hits, self.scanned, self.seconds, self.model = index, hits, scanned, seconds, model
+
+
+def model_watch(P: ssa.Program):
+    """Watch entries that read a whole model back: scalar VAR nodes, site keys and
+    site base values (0x80000000 | coord).  Returns (entries, widths)."""
+    entries, widths = [], []
+    for c in P.scalar_coords():
+        entries.append(c.node)
+        widths.append(c.width)
+    for c in P.sites:
+        k = P.site_key_node[c.index]
+        entries.append(k)
+        widths.append(P.node_width[k])
+        entries.append(0x80000000 | c.index)
+        widths.append(c.width)
+    return entries, widths
+
+
+def read_rows(watch: np.ndarray, widths: Sequence[int], col: int) -> List[int]:
+    out, r = [], 0
+    for w in widths:
+        L = ssa.limbs(w)
+        out.append(ssa.limbs_to_int(watch[r:r + L, col]))
+        r += L
+    return out
+
+
+def materialize(engine, P: ssa.Program, gen_blob: np.ndarray, seed: int, index: int):
+    """Re-run candidate ``index`` with the model watch list; returns (verdict, scalars, arrays, funcs)."""
+    entries, widths = model_watch(P)
+    P.set_watch(entries)
+    prog = engine.load(P.to_bytes())
+    try:
+        gen = engine.load_gen(prog, gen_blob)
+        try:
+            ver, watch = engine.eval_generated(prog, gen, seed, index, 1, watch_words=sum(ssa.limbs(w) for w in widths))
+        finally:
+            engine.free_gen(gen)
+    finally:
+        engine.free(prog)
+        P.set_watch([])
+    vals = read_rows(watch, widths, 0) if watch is not None else []
+    scal, keys, bases = {}, {}, {}
+    it = iter(vals)
+    for c in P.scalar_coords():
+        scal[c.index] = next(it)
+    for c in P.sites:
+        keys[c.index] = next(it)
+        bases[c.index] = next(it)
+    scalars, arrays, funcs = ssa.model_from_sites(P, scal, keys, bases)
+    return int(ver[0]), scalars, arrays, funcs
+
+
+def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int = 1 << 22,
+           max_candidates: int = 1 << 26, timeout_s: float = 10.0, gen: Optional[GenBuilder] = None,
+           want_model: bool = True) -> SearchResult:
+    """Find the lowest-index satisfying candidate (or give up: None)."""
+    P = ssa.flatten(roots)
+    g = gen or default_generator(P)
+    blob = g.blob()
+    prog = engine.load(P.to_bytes())
+    t0 = time.perf_counter()
+    scanned = 0
+    hit = None
+    hits = 0
+    try:
+        gh = engine.load_gen(prog, blob)
+        try:
+            start = 0
+            while scanned < max_candidates and time.perf_counter() - t0 < timeout_s:
+                n = min(chunk, max_candidates - scanned)
+                idx, nh = engine.search(prog, gh, seed, start, n, early_exit=True)
+                scanned += n
+                start += n
+                if idx is not None:
+                    hit, hits = idx, nh
+                    break
+                chunk = min(chunk * 2, 1 << 28)
+        finally:
+            engine.free_gen(gh)
+    finally:
+        engine.free(prog)
+    dt = time.perf_counter() - t0
+    res = SearchResult(hit, hits, scanned, dt)
+    if hit is not None and want_model:
+        res.model = materialize(engine, P, blob, seed, hit) + (P,)
+    return res
+
+
+def eval_with_models(engine, P: ssa.Program, assigns: Sequence[Sequence[int]]):
+    """Batched eval of explicit assignments; also reads every candidate back as a
+    finite model ``(scalars, arrays, funcs)`` (site canonicalisation applied)."""
+    entries, widths = model_watch(P)
+    P.set_watch(entries)
+    soa = ssa.soa_from_assignments(P, assigns)
+    prog = engine.load(P.to_bytes())
+    try:
+        ww = sum(ssa.limbs(w) for w in widths)
+        ver, watch = engine.eval(prog, soa, len(assigns), watch_words=ww)
+    finally:
+        engine.free(prog)
+        P.set_watch([])
+    models = []
+    for i in range(len(assigns)):
+        vals = iter(read_rows(watch, widths, i)) if watch is not None else iter(())
+        scal, keys, bases = {}, {}, {}
+        for c in P.scalar_coords():
+            scal[c.index] = next(vals)
+        for c in P.sites:
+            keys[c.index] = next(vals)
+            bases[c.index] = next(vals)
+        models.append(ssa.model_from_sites(P, scal, keys, bases))
+    return ver, models

@@ -1,0 +1,186 @@
+"""Shared test infrastructure: golden-vector loaders, a random term-DAG
+generator and the GPU-vs-oracle comparison used by the parity tests."""
+from __future__ import annotations
+
+import json
+import random
+from pathlib import Path
+from typing import Dict, List, Sequence
+
+import numpy as np
+
+from mythril_amd import ssa
+from mythril_amd.replay import ExceptionalHalt, ReplayUnsupported, replay, replay_assignment
+from mythril_amd.smt import terms as T
+from oracle.bv import OracleModel, evaluate_many
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def load_json(name):
+    return json.loads((GOLDEN / name).read_text())
+
+
+def vmtest_cases():
+    """(name, vector, ReplayResult) for every VMTests vector the replay subset covers
+    and whose outcome is a post-state (not ignored by the reference)."""
+    out = []
+    for name, v in sorted(load_json("vmtests.json").items()):
+        if v["reference_ignored"] or v["post_storage"] is None:
+            continue
+        pre = {int(k, 16): int(x, 16) for k, x in v["pre_storage"].items()}
+        try:
+            r = replay(v["code"], bytes.fromhex(v["data"]), pre)
+        except (ReplayUnsupported, ExceptionalHalt):
+            continue
+        out.append((name, v, r))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# random programs
+# ---------------------------------------------------------------------------
+EDGE_256 = [0, 1, 2, 3, 31, 32, 255, 256, 257, (1 << 255), (1 << 255) - 1, (1 << 256) - 1, (1 << 256) - 2,
+            (1 << 128), (1 << 160) - 1, (1 << 64) + 1]
+
+BIN_OPS = ["bvadd", "bvsub", "bvmul", "bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod", "bvand", "bvor",
+           "bvxor", "bvshl", "bvlshr", "bvashr"]
+CMP_OPS = ["bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge", "bvumul_noovfl"]
+
+
+def edge_value(rng: random.Random, w: int) -> int:
+    m = (1 << w) - 1
+    r = rng.random()
+    if r < 0.35:
+        return rng.choice(EDGE_256) & m
+    if r < 0.5:
+        return rng.choice([0, 1, m, m - 1, 1 << (w - 1), (1 << (w - 1)) - 1]) & m
+    if r < 0.65:
+        return rng.getrandbits(min(w, rng.choice([4, 8, 16, 64])))
+    return rng.getrandbits(w)
+
+
+class RandomProgram:
+    """A random constraint DAG over scalars, one array and one UF, with a list of
+    'interesting' terms to compare value-by-value."""
+
+    def __init__(self, seed: int, n_ops: int = 40, widths=(256, 256, 256, 160, 64, 32, 8, 1 + 7, 257, 512)):
+        rng = random.Random(seed)
+        self.rng = rng
+        self.vars: Dict[int, List[T.Term]] = {}
+        pool: Dict[int, List[T.Term]] = {}
+
+        def add(t):
+            pool.setdefault(t.width, []).append(t)
+            return t
+
+        for i, w in enumerate(widths):
+            v = T.BitVecVar(f"v{i}_{w}", w)
+            self.vars.setdefault(w, []).append(v)
+            add(v)
+            add(T.BitVecVal(edge_value(rng, w), w))
+        bools: List[T.Term] = [T.BoolVar("flag")]
+        arr = T.ArrayVar("Storage", 256, 256)
+        fn = T.FuncDecl("keccak256_512", 512, 256)
+        terms: List[T.Term] = []
+        for _ in range(n_ops):
+            kind = rng.random()
+            w = rng.choice([256, 256, 256, 64, 160, 8, 32])
+            src = pool.get(w) or [T.BitVecVal(0, w)]
+            a, b = rng.choice(src), rng.choice(src)
+            if kind < 0.45:
+                op = rng.choice(BIN_OPS)
+                if op in ("bvmul", "bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod", "bvshl", "bvlshr", "bvashr") and w > 256:
+                    op = "bvadd"
+                t = T.bvbin(op, a, b)
+            elif kind < 0.55:
+                t = T.bvun(rng.choice(["bvnot", "bvneg"]), a)
+            elif kind < 0.65:
+                c = T.bvcmp(rng.choice(CMP_OPS), a, b) if w <= 256 else T.eq(a, b)
+                bools.append(c)
+                terms.append(c)
+                continue
+            elif kind < 0.72:
+                c = rng.choice(bools)
+                t = T.ite(c, a, b)
+            elif kind < 0.80:
+                hi = rng.randrange(w)
+                lo = rng.randrange(hi + 1)
+                t = T.extract(hi, lo, a)
+            elif kind < 0.86:
+                w2 = rng.choice([8, 32, 96, 160, 256])
+                b2 = rng.choice(pool.get(w2) or [T.BitVecVal(1, w2)])
+                t = T.concat(a, b2) if a.width + w2 <= 1024 else a
+            elif kind < 0.90:
+                k = rng.choice([1, 8, 96, 256])
+                t = T.zero_extend(k, a) if rng.random() < 0.5 else T.sign_extend(k, a)
+            elif kind < 0.95:
+                idx = rng.choice(pool.get(256) or [T.BitVecVal(0, 256)])
+                if rng.random() < 0.5:
+                    st = T.store(arr, rng.choice(pool[256]), rng.choice(pool[256]))
+                    t = T.select(st, idx)
+                else:
+                    t = T.select(arr, idx)
+            else:
+                x = rng.choice(pool.get(256))
+                y = rng.choice(pool.get(256))
+                t = T.app(fn, T.concat(x, y))
+            add(t)
+            terms.append(t)
+        # logical glue
+        for _ in range(4):
+            x, y = rng.choice(bools), rng.choice(bools)
+            c = rng.choice([T.and_(x, y), T.or_(x, y), T.not_(x), T.xor_(x, y), T.eq(x, y)])
+            bools.append(c)
+            terms.append(c)
+        self.terms = terms
+        self.bools = bools
+        self.root = T.or_(*bools[-3:]) if len(bools) >= 3 else T.BoolVal(True)
+
+
+def random_assignments(P: ssa.Program, n: int, seed: int):
+    rng = random.Random(seed)
+    return [[edge_value(rng, c.width) for c in P.coords] for _ in range(n)]
+
+
+def gpu_eval_terms(engine, roots: Sequence[T.Term], watch_terms: Sequence[T.Term], assigns=None, n=64, seed=0):
+    """Evaluate on the GPU; returns (P, assigns, verdicts, per-candidate dict term-id -> value,
+    per-candidate oracle models)."""
+    P = ssa.flatten(list(roots) + [t for t in watch_terms if t.is_bool and False])
+    # watch every requested term that the program contains, plus the model read-back entries
+    from mythril_amd.search import model_watch
+
+    for t in watch_terms:
+        if t.id not in P.term_node:
+            raise KeyError("watch term not in program")
+    term_entries = [P.term_node[t.id] for t in watch_terms]
+    m_entries, m_widths = model_watch(P)
+    entries = term_entries + m_entries
+    widths = [P.node_width[e] for e in term_entries] + m_widths
+    P.set_watch(entries)
+    if assigns is None:
+        assigns = random_assignments(P, n, seed)
+    soa = ssa.soa_from_assignments(P, assigns)
+    prog = engine.load(P.to_bytes())
+    try:
+        info = engine.info(prog)
+        ver, watch = engine.eval(prog, soa, len(assigns), watch_words=info.watch_words)
+    finally:
+        engine.free(prog)
+    from mythril_amd.search import read_rows
+
+    results, models = [], []
+    for i in range(len(assigns)):
+        vals = read_rows(watch, widths, i)
+        tv = {t.id: vals[j] for j, t in enumerate(watch_terms)}
+        rest = iter(vals[len(watch_terms):])
+        scal, keys, bases = {}, {}, {}
+        for c in P.scalar_coords():
+            scal[c.index] = next(rest)
+        for c in P.sites:
+            keys[c.index] = next(rest)
+            bases[c.index] = next(rest)
+        s, a, f = ssa.model_from_sites(P, scal, keys, bases)
+        results.append(tv)
+        models.append(OracleModel(s, a, f))
+    return P, assigns, ver, results, models

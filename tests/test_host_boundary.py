@@ -1,0 +1,121 @@
+"""Host-side checks of the C-ABI boundary and the flattener — CPU only (no compute
+call needs a GPU here)."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+from mythril_amd import native, ssa
+from mythril_amd.smt import (Array, BVAddNoOverflow, BVMulNoOverflow, BVSubNoUnderflow, Concat, Function, If, K,
+                             Not, UDiv, UGE, UGT, ULT, symbol_factory)
+from mythril_amd.smt import terms as T
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = (ROOT / "include" / "mythgpu.h").read_text()
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from mythril_amd import build
+
+    build.build()
+    return native.load_library()
+
+
+def test_header_opcodes_match_flattener():
+    enum = dict(re.findall(r"MG_OP_([A-Z_]+) = (\d+)", HEADER))
+    enum.pop("COUNT")
+    assert {k: int(v) for k, v in enum.items()} == ssa.OPS
+
+
+def test_library_exports_every_declared_symbol(lib):
+    declared = set(re.findall(r"^\s*(?:int|void|const char\*)\s+(mg_\w+)\(", HEADER, re.M))
+    assert declared == set(native.EXPORTS)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.mg_version() == 1
+
+
+def test_init_without_device_fails_loudly(lib):
+    if Path("/dev/kfd").exists():
+        pytest.skip("a GPU is present")
+    with pytest.raises(native.EngineError):
+        native.Engine(0)
+
+
+def _bec_constraints():
+    """BECToken batchOverflow shape."""
+    cnt = symbol_factory.BitVecSym("cnt", 256)
+    value = symbol_factory.BitVecSym("value", 256)
+    sender = symbol_factory.BitVecSym("sender_1", 256)
+    storage = Array("Storage", 256, 256)
+    keccak = Function("keccak256_512", 512, 256)
+    slot = keccak(Concat(sender, symbol_factory.BitVecVal(0, 256)))
+    amount = cnt * value
+    return [
+        Not(BVMulNoOverflow(cnt, value, False)),
+        UGT(cnt, symbol_factory.BitVecVal(0, 256)),
+        ULT(cnt, symbol_factory.BitVecVal(21, 256)),
+        UGT(value, symbol_factory.BitVecVal(0, 256)),
+        UGE(storage[slot], amount),
+    ]
+
+
+def test_program_check_and_cost(lib):
+    cs = _bec_constraints()
+    P = ssa.flatten([c.raw for c in cs])
+    info = native.check_program(P.to_bytes())
+    assert info.n_roots == 5
+    assert info.n_coords == len(P.coords) == 5  # cnt, value, sender, keccak site, storage site
+    assert info.coord_words == 8 * 4 + 8
+    # MUL 128 + UMUL_NOOVF 256 + 4 compares ... : cost table is deterministic
+    assert info.limb_ops > 128 + 256
+    assert info.value_words < 160
+
+
+def test_unsupported_wide_arithmetic(lib):
+    x = T.BitVecVar("x", 512)
+    t = T.eq(T.bvbin("bvmul", x, x), x)
+    P = ssa.flatten([t])
+    with pytest.raises(native.EngineUnsupported):
+        native.check_program(P.to_bytes())
+
+
+def test_malformed_program_rejected(lib):
+    x = symbol_factory.BitVecSym("x", 256)
+    blob = bytearray(ssa.flatten([(x == 1).raw]).to_bytes())
+    blob[0] ^= 0xFF
+    with pytest.raises(native.EngineError):
+        native.check_program(bytes(blob))
+    with pytest.raises(native.EngineError):
+        native.check_program(bytes(ssa.flatten([(x == 1).raw]).to_bytes())[:-4])
+
+
+def test_flatten_sites_and_lazy_inverse():
+    x = symbol_factory.BitVecSym("x", 256)
+    f = Function("keccak256_256", 256, 256)
+    inv = Function("keccak256_256-1", 256, 256)
+    c = inv(f(x)) == x
+    P = ssa.flatten([c.raw])
+    kinds = [co.kind for co in P.coords]
+    assert kinds == [ssa.COORD_SCALAR, ssa.COORD_UF_SITE, ssa.COORD_UF_SITE]
+    inv_node = P.coords[2].node
+    assert P.nodes[inv_node][7] == P.coords[0].node  # lazy default = x
+
+
+def test_flatten_select_over_store_chain():
+    s = K(256, 256, 0)
+    a = symbol_factory.BitVecSym("a", 256)
+    s[a] = symbol_factory.BitVecVal(5, 256)
+    c = s[symbol_factory.BitVecVal(3, 256)] == 5
+    P = ssa.flatten([c.raw])
+    assert all(co.kind == ssa.COORD_SCALAR for co in P.coords)  # K() base: no site
+
+
+def test_addnooverflow_expands_like_z3():
+    a = symbol_factory.BitVecSym("a", 256)
+    b = symbol_factory.BitVecSym("b", 256)
+    t = BVAddNoOverflow(a, b, False).raw
+    assert t.op == "eq" and t.args[0].op == "extract" and t.args[0].params == (256, 256)
+    assert BVSubNoUnderflow(a, b, False).raw.op == "bvule"
