@@ -35,7 +35,7 @@ constexpr int kWave = 64;
 constexpr uint32_t kLdsWordsMax = 160;  // value file in LDS up to 160 words (40 KiB per wave)
 
 __device__ __constant__ static const uint32_t kEmptyKeccak[8] = {
-    0x5d85a470u, 0xfad8045du, 0x82273b7bu, 0xe500b653u, 0xdcc703c0u, 0x927e7db2u, 0x86f7233cu, 0xc5d24601u};
+    0x5d85a470u, 0x7bfad804u, 0xca82273bu, 0xe500b653u, 0xdcc703c0u, 0x927e7db2u, 0x86f7233cu, 0xc5d24601u};
 
 enum Mode : int { MODE_EVAL = 0, MODE_GEN = 1, MODE_SEARCH = 2 };
 

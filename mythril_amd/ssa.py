@@ -174,8 +174,9 @@ def _base_of(arr: T.Term) -> T.Term:
     return arr
 
 
-def flatten(roots: Sequence[T.Term], lazy_inverse: bool = True) -> Program:
-    """Flatten Bool roots (terms) into a :class:`Program`."""
+def flatten(roots: Sequence[T.Term], lazy_inverse: bool = True, extra: Sequence[T.Term] = ()) -> Program:
+    """Flatten Bool roots (terms) into a :class:`Program`.  ``extra`` terms are
+    flattened too (so they can be watched) without becoming constraints."""
     P = Program()
     roots = list(roots)
     for r in roots:
@@ -215,7 +216,7 @@ def flatten(roots: Sequence[T.Term], lazy_inverse: bool = True) -> Program:
         P.coords.append(c)
         return c
 
-    order = T.postorder(roots)
+    order = T.postorder(list(roots) + list(extra))
     # pre-pass: forward UF apps (for lazy inverse defaults)
     if lazy_inverse:
         for t in order:

@@ -146,7 +146,7 @@ def random_assignments(P: ssa.Program, n: int, seed: int):
 def gpu_eval_terms(engine, roots: Sequence[T.Term], watch_terms: Sequence[T.Term], assigns=None, n=64, seed=0):
     """Evaluate on the GPU; returns (P, assigns, verdicts, per-candidate dict term-id -> value,
     per-candidate oracle models)."""
-    P = ssa.flatten(list(roots) + [t for t in watch_terms if t.is_bool and False])
+    P = ssa.flatten(list(roots), extra=list(watch_terms))
     # watch every requested term that the program contains, plus the model read-back entries
     from mythril_amd.search import model_watch
 
