@@ -1,0 +1,209 @@
+"""Benchmark: candidate assignments evaluated / s on LASER path-constraint queries.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1
+it is launched by torch.distributed.run, one rank per GPU.  Rank 0 prints ONE
+JSON line.
+
+A *step* is one full sweep of the hot path over one batch of candidates: every
+rank evaluates C candidates of the workload's constraint program (no early exit:
+every candidate is evaluated to its verdict) in the search kernel, then the ranks
+agree on the lowest satisfying index with one RCCL all-reduce(MIN) over xGMI —
+the only exchange step the path has.  Candidate shards are disjoint index ranges
+(weak scaling).  Inputs are generated on the device (nothing crosses PCIe inside
+the timed region).
+
+roofline: achieved = limb_ops/candidate (fixed cost table, program.cpp op_cost)
+x C / the search kernel's mean duration (HIP events on the engine's own stream);
+peak = INT32 VALU lane-ops/s of MI355X (256 CU x 4 SIMD x 32 lanes x 2.4 GHz).
+cpu_baseline: the plain-C restatement (oracle/bveval.c, OpenMP) timed on the
+host cores over a bounded sample of the same candidates (rank 0, N == 1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.6 T int32 lane-ops/s
+METRIC = "candidate assignments evaluated/sec (node) + time-to-first-model vs z3"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="token_transfer_underflow")
+    ap.add_argument("--candidates", type=int, default=1 << 24, help="candidates per GPU per step")
+    ap.add_argument("--seed", type=int, default=0x6D797468)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # torch first: its HIP runtime is the one process-wide runtime the engine then shares
+    import torch
+    import torch.distributed as dist
+
+    distributed = world > 1
+    torch.cuda.set_device(local_rank)
+    if distributed:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from mythril_amd import build, native, search, ssa, workloads
+
+    if rank == 0 and not native.LIB_PATH.exists():
+        build.build()
+    if distributed:
+        dist.barrier()
+    os.environ["MYTHGPU_DEVICE"] = str(local_rank)
+    eng = native.Engine.get()
+
+    cs = workloads.WORKLOADS[args.workload]()
+    roots = [c.raw for c in cs]
+    P = ssa.flatten(roots)
+    gen = search.default_generator(P)
+    blob = gen.blob()
+    prog = eng.load(P.to_bytes())
+    info = eng.info(prog)
+    gh = eng.load_gen(prog, blob)
+    C = args.candidates
+
+    hit_t = torch.full((1,), (1 << 63) - 1, dtype=torch.int64, device="cuda")
+
+    def step(s):
+        start = (s * world + rank) * C
+        idx, nh = eng.search(prog, gh, args.seed, start, C, early_exit=False)
+        if distributed:
+            hit_t.fill_(idx if idx is not None else (1 << 63) - 1)
+            dist.all_reduce(hit_t, op=dist.ReduceOp.MIN)
+        return idx, nh
+
+    for s in range(args.warmup):
+        step(s)
+    eng.reset_stats()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    total_hits = 0
+    for s in range(args.warmup, args.warmup + args.steps):
+        _, nh = step(s)
+        total_hits += nh
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    st = eng.stats()
+    kernel_ms = st.kernel_ms_total / max(st.launches, 1)
+    dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    km_t = torch.tensor([kernel_ms], dtype=torch.float64, device="cuda")
+    if distributed:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(km_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    kernel_ms = float(km_t.item())
+
+    # time to first model (early-exit search from index 0 + model read-back), rank 0 only
+    ttfm_ms = None
+    if rank == 0:
+        t1 = time.perf_counter()
+        res = search.search(eng, roots, seed=args.seed, chunk=1 << 20, max_candidates=1 << 30, timeout_s=30)
+        ttfm_ms = (time.perf_counter() - t1) * 1e3 if res.index is not None else None
+
+    # CPU baseline: the C restatement over a bounded sample of the same candidates
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(P, blob, args, eng, prog, gh)
+
+    if rank == 0:
+        total = world * C * args.steps
+        value = total / dt
+        achieved = info.limb_ops * C / (kernel_ms * 1e-3) / 1e12
+        traffic = None
+        tj = Path(args.traffic_json)
+        if tj.exists():
+            try:
+                t = json.loads(tj.read_text())
+                if t.get("workload") == args.workload and t.get("candidates") == C:
+                    traffic = t.get("hbm_bytes_per_launch")
+            except (ValueError, OSError):
+                traffic = None
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "candidate assignments/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (device-generated candidates of a LASER-shaped query; no solc/z3 in image)",
+            "config": {
+                "workload": f"C2 {args.workload} (BASELINE.json configs[1])",
+                "candidates_per_gpu_step": C,
+                "limb_ops_per_candidate": int(info.limb_ops),
+                "program_instrs": int(info.n_instrs),
+                "value_file_words": int(info.value_words),
+                "value_file": "lds" if info.uses_lds else "hbm",
+                "parallelism": f"shard{world}",
+            },
+            "roofline": {
+                "bound": "valu",
+                "achieved": achieved,
+                "peak": VALU_PEAK_TOPS,
+                "unit": "TOP/s (int32 lane-ops)",
+                "frac": achieved / VALU_PEAK_TOPS,
+                "traffic": traffic,
+                "kernel_ms": kernel_ms,
+            },
+            "cpu_baseline": cpu,
+            "time_to_first_model_ms": ttfm_ms,
+            "hits_in_timed_region": int(total_hits),
+        }
+        print(json.dumps(out), flush=True)
+    eng.free_gen(gh)
+    eng.free(prog)
+    if distributed:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(P, blob, args, eng, prog, gh):
+    from oracle import cport
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    start = 1 << 40  # a window the GPU also evaluates below
+    n = 4096
+    t = time.perf_counter()
+    cport.search(P.to_bytes(), blob, args.seed, start, n, threads=threads)
+    dt = time.perf_counter() - t
+    n = int(min(max(n, n * args.cpu_seconds / max(dt, 1e-6)), 1 << 26))
+    t = time.perf_counter()
+    first, hits, _ = cport.search(P.to_bytes(), blob, args.seed, start, n, threads=threads)
+    dt = time.perf_counter() - t
+    g_first, g_hits = eng.search(prog, gh, args.seed, start, n, early_exit=False)
+    return {
+        "value": n / dt,
+        "unit": "candidate assignments/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n} candidates [{start}, {start + n}) of the same workload/seed; {dt:.1f} s",
+        "agrees_with_gpu": bool(first == g_first and hits == g_hits),
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -16,6 +16,8 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <cstdio>
+#include <cstdlib>
 
 namespace mg {
 
@@ -192,9 +194,18 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
     std::vector<std::vector<std::pair<uint32_t, uint32_t>>> watch_site(n_coords);
     uint32_t max_w = 0;
 
+    std::vector<uint32_t> vconst;  // const-pool offset when the vid is a literal, else NONE
     auto new_vid = [&](uint32_t width) {
       vwidth.push_back(width);
+      vconst.push_back(NONE);
       return (uint32_t)(vwidth.size() - 1);
+    };
+    // two keys that are distinct literals can never select the same table entry:
+    // such priors are dropped from a lookup's candidate list at load time
+    auto distinct_literals = [&](uint32_t x, uint32_t y) {
+      if (vconst[x] == NONE || vconst[y] == NONE || vwidth[x] != vwidth[y]) return false;
+      const uint32_t L = L_of(vwidth[x]);
+      return std::memcmp(&consts[vconst[x]], &consts[vconst[y]], 4 * L) != 0;
     };
     auto emit = [&](uint32_t op, uint32_t wd, uint32_t dst, uint32_t a = NONE, uint32_t b = NONE, uint32_t c = NONE,
                     uint32_t p0 = 0, uint32_t p1 = 0) {
@@ -202,9 +213,18 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
       code.push_back(v);
       return code.size() - 1;
     };
+    // literals are rematerialised at every use (a scalar-load K_CONST right before
+    // the consumer) instead of occupying value-file words from first to last use
+    std::vector<uint32_t> node_const(n_nodes, NONE);
     auto val = [&](uint32_t i, uint32_t cur) -> uint32_t {
       if (i >= cur) fail(MG_E_INVALID, "operand does not precede its use");
       if (is_arr[i]) fail(MG_E_INVALID, "array used as a value");
+      if (node_const[i] != NONE) {
+        uint32_t v = new_vid(nodes[i].width);
+        vconst[v] = node_const[i];
+        emit(K_CONST, nodes[i].width, v, NONE, NONE, NONE, node_const[i]);
+        return v;
+      }
       return vid[i];
     };
     auto wid = [&](uint32_t i) { return nodes[i].width; };
@@ -227,8 +247,7 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
       switch (n.op) {
         case MG_OP_CONST: {
           if ((uint64_t)n.p0 + L_of(W) > n_consts) fail(MG_E_INVALID, "constant out of range");
-          vid[i] = new_vid(W);
-          emit(K_CONST, W, vid[i], NONE, NONE, NONE, n.p0);
+          node_const[i] = n.p0;  // materialised lazily by val()
           break;
         }
         case MG_OP_VAR: {
@@ -344,6 +363,7 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
             auto& prior = table_sites[A.table];
             for (auto& pr : prior) {
               if (vwidth[pr.first] != wid(n.b)) continue;  // same name, other sort: separate table
+              if (distinct_literals(key, pr.first)) continue;
               code[at].prior.push_back(pr.first);
               code[at].prior.push_back(pr.second);
             }
@@ -352,13 +372,15 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
             site_base_vid[n.p0] = cur;
           } else {
             if (n.p0 != NONE) fail(MG_E_INVALID, "select over K() has no site");
-            cur = vid[A.default_node];
+            cur = val(A.default_node, i);
           }
           for (auto& st : A.stores) {
             uint32_t e = new_vid(1);
-            emit(K_EQ, 1, e, key, vid[st.first], NONE, 0, wid(n.b));
+            uint32_t si = val(st.first, i);
+            emit(K_EQ, 1, e, key, si, NONE, 0, wid(n.b));
+            uint32_t sv = val(st.second, i);
             uint32_t nv = new_vid(W);
-            emit(K_ITE, W, nv, e, vid[st.second], cur, 0, W);
+            emit(K_ITE, W, nv, e, sv, cur, 0, W);
             cur = nv;
           }
           vid[i] = cur;
@@ -383,6 +405,7 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
           size_t at = emit(K_LOOKUP, W, v, key, wid(n.a), 0, dflt, 0);
           auto& prior = table_sites[n.p0];
           for (auto& pr : prior) {
+            if (distinct_literals(key, pr.first)) continue;
             code[at].prior.push_back(pr.first);
             code[at].prior.push_back(pr.second);
           }
@@ -410,7 +433,7 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
       }
       if (root_of[i]) {
         if (is_arr[i] || W != 1) fail(MG_E_INVALID, "root is not Bool");
-        emit(K_ASSERT, 1, NONE, vid[i]);
+        emit(K_ASSERT, 1, NONE, val(i, i + 1));
       }
     }
     // watch list (after all nodes: watch entries refer to nodes or site bases)
@@ -424,7 +447,12 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
         width = vwidth[v];
       } else {
         if (wv >= n_nodes || is_arr[wv]) fail(MG_E_INVALID, "watch node");
-        v = vid[wv];
+        if (node_const[wv] != NONE) {
+          v = new_vid(nodes[wv].width);
+          emit(K_CONST, nodes[wv].width, v, NONE, NONE, NONE, node_const[wv]);
+        } else {
+          v = vid[wv];
+        }
         width = nodes[wv].width;
       }
       watch_row[j] = wrow;
@@ -471,6 +499,7 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
       dies[(size_t)d].push_back((uint32_t)v);
     }
     Alloc al;
+    uint32_t dbg_high = 0;
     out.code.clear();
     out.aux.clear();
     for (size_t k = 0; k < code.size(); k++) {
@@ -512,6 +541,18 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
         out.limb_ops += op_cost(c.op, c.wd, wa ? wa : c.wd);
       }
       for (uint32_t v : dies[k]) al.release(slot[v], L_of(vwidth[v]));
+      if (getenv("MYTHGPU_DEBUG_ALLOC") && al.high() > dbg_high) {
+        dbg_high = al.high();
+        size_t live = 0;
+        std::string s;
+        for (size_t v = 0; v < nv; v++)
+          if (def[v] >= 0 && def[v] <= (int64_t)k && std::max(last[v], def[v]) > (int64_t)k) {
+            live += L_of(vwidth[v]);
+            s += " " + std::to_string(v) + ":" + std::to_string(vwidth[v]) + "@" + std::to_string(code[def[v]].op) +
+                 "-" + std::to_string(last[v]);
+          }
+        fprintf(stderr, "instr %zu high %u live %zu:%s\n", k, al.high(), live, s.c_str());
+      }
     }
     out.value_words = std::max<uint32_t>(al.high(), 1);
     return MG_OK;

@@ -254,3 +254,28 @@ def _eval_node(t, model: OracleModel, memo):
         w = t.args[0].width
         return keccak256_int(a[0].to_bytes(w // 8, "big"))
     raise NotImplementedError(f"oracle: operator {op}")
+
+
+def model_from_coordinates(P, assignment):
+    """The finite model a candidate denotes: scalars from their coordinates; each
+    array/UF site, in SSA order, adds ``key -> coordinate`` (or its lazy default)
+    unless an earlier site of the same table already holds that key.  This is the
+    z3-model reading of a candidate that the engine's canonicalisation implements
+    (mythril_amd/ssa.py docstring); restated here independently for the tests."""
+    def mask(v, w):
+        return v & ((1 << w) - 1)
+
+    scal = {c.name: mask(assignment[c.index], c.width) for c in P.scalar_coords()}
+    arrays, funcs = {}, {}
+    for c in P.sites:
+        m = OracleModel(scal, arrays, funcs)
+        key = evaluate(P.node_term[P.site_key_node[c.index]], m)
+        lazy = P.nodes[c.node][7] if c.kind == 2 else 0xFFFFFFFF
+        if lazy != 0xFFFFFFFF:
+            dflt = evaluate(P.node_term[lazy], m)
+        else:
+            dflt = mask(assignment[c.index], c.width)
+        tables = arrays if c.kind == 1 else funcs
+        table, _ = tables.setdefault(c.name, ({}, 0))
+        table.setdefault(key, dflt)
+    return OracleModel(scal, arrays, funcs)

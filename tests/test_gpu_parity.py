@@ -259,3 +259,40 @@ def test_eval_dev_resident_inputs(engine):
     assert (ver_h == ver_d).all()
     for i in range(0, n, 97):
         assert ver_h[i] == evaluate(c.raw, OracleModel({"x": assigns[i][0], "y": assigns[i][1]}))
+
+
+@pytest.mark.parametrize("name", ["token_transfer_underflow", "etherstore_reentrancy", "bectoken_batch_overflow"])
+def test_workload_verdicts_match_c_restatement(engine, name):
+    """Every candidate verdict of the benchmark workloads (search-mode generator,
+    full evaluation) equals the C restatement's, and the search first hit/count agree."""
+    from mythril_amd import workloads
+    from oracle import cport
+
+    roots = [c.raw for c in workloads.WORKLOADS[name]()]
+    P = ssa.flatten(roots)
+    blob = search.default_generator(P).blob()
+    n, start, seed = 1 << 14, 12345, 0x6D797468
+    prog = engine.load(P.to_bytes())
+    gh = engine.load_gen(prog, blob)
+    try:
+        gver, _ = engine.eval_generated(prog, gh, seed, start, n)
+        gfirst, ghits = engine.search(prog, gh, seed, start, n, early_exit=False)
+    finally:
+        engine.free_gen(gh)
+        engine.free(prog)
+    cfirst, chits, cver = cport.search(P.to_bytes(), blob, seed, start, n, threads=8, verdicts=True)
+    assert (gver == cver).all(), int((gver != cver).sum())
+    assert (gfirst, ghits) == (cfirst, chits)
+
+
+@pytest.mark.parametrize("name", ["token_transfer_underflow", "etherstore_reentrancy", "bectoken_batch_overflow"])
+def test_workload_models_verified(engine, name):
+    """The GPU finds a model of each workload query and the oracle accepts it."""
+    from mythril_amd import workloads
+
+    roots = [c.raw for c in workloads.WORKLOADS[name]()]
+    res = search.search(engine, roots, max_candidates=1 << 28, timeout_s=60)
+    assert res.index is not None, name
+    ver, scalars, arrays, funcs, P = res.model
+    m = OracleModel(scalars, arrays, funcs)
+    assert ver == 1 and all(evaluate(r, m) == 1 for r in roots)
