@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=0x6D797468)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--engine", choices=["jit", "interp"], default="jit",
+                    help="jit: hipRTC-specialised search kernel; interp: the generic interpreter kernel")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
     return ap.parse_args()
 
@@ -78,12 +80,20 @@ def main():
     info = eng.info(prog)
     gh = eng.load_gen(prog, blob)
     C = args.candidates
+    jit = None
+    compile_ms = None
+    if args.engine == "jit":
+        jit = eng.jit_compile(prog, gh)
+        compile_ms = eng.jit_info(jit)[0]
 
     hit_t = torch.full((1,), (1 << 63) - 1, dtype=torch.int64, device="cuda")
 
     def step(s):
         start = (s * world + rank) * C
-        idx, nh = eng.search(prog, gh, args.seed, start, C, early_exit=False)
+        if jit is not None:
+            idx, nh = eng.jit_search(jit, args.seed, start, C, early_exit=False)
+        else:
+            idx, nh = eng.search(prog, gh, args.seed, start, C, early_exit=False)
         if distributed:
             hit_t.fill_(idx if idx is not None else (1 << 63) - 1)
             dist.all_reduce(hit_t, op=dist.ReduceOp.MIN)
@@ -124,7 +134,7 @@ def main():
     # CPU baseline: the C restatement over a bounded sample of the same candidates
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(P, blob, args, eng, prog, gh)
+        cpu = cpu_baseline(P, blob, args, eng, prog, gh, jit)
 
     if rank == 0:
         total = world * C * args.steps
@@ -158,7 +168,9 @@ def main():
                 "limb_ops_per_candidate": int(info.limb_ops),
                 "program_instrs": int(info.n_instrs),
                 "value_file_words": int(info.value_words),
-                "value_file": "lds" if info.uses_lds else "hbm",
+                "value_file": "vgpr (jit)" if jit is not None else ("lds" if info.uses_lds else "hbm"),
+                "engine": args.engine,
+                "jit_compile_ms": compile_ms,
                 "parallelism": f"shard{world}",
             },
             "roofline": {
@@ -175,13 +187,15 @@ def main():
             "hits_in_timed_region": int(total_hits),
         }
         print(json.dumps(out), flush=True)
+    if jit is not None:
+        eng.jit_free(jit)
     eng.free_gen(gh)
     eng.free(prog)
     if distributed:
         dist.destroy_process_group()
 
 
-def cpu_baseline(P, blob, args, eng, prog, gh):
+def cpu_baseline(P, blob, args, eng, prog, gh, jit=None):
     from oracle import cport
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
@@ -195,6 +209,8 @@ def cpu_baseline(P, blob, args, eng, prog, gh):
     first, hits, _ = cport.search(P.to_bytes(), blob, args.seed, start, n, threads=threads)
     dt = time.perf_counter() - t
     g_first, g_hits = eng.search(prog, gh, args.seed, start, n, early_exit=False)
+    if jit is not None:
+        assert eng.jit_search(jit, args.seed, start, n, early_exit=False) == (g_first, g_hits)
     return {
         "value": n / dt,
         "unit": "candidate assignments/s",

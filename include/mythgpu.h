@@ -193,6 +193,23 @@ int mg_eval_generated(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start
 int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags,
               uint64_t* first_hit, uint64_t* n_hits);
 
+/* ---- JIT specialisation (hipRTC) ------------------------------------
+ * mg_jit_compile turns a loaded program into straight-line gfx950 code: with a
+ * generator handle, the search kernel (mg_jit_search) specialised on it; with
+ * gen = 0, the eval kernel (mg_jit_eval*).  It emits straight-line code (values in VGPRs, literals as immediates,
+ * generator inlined).  Same semantics as mg_search / mg_eval. */
+/* host-only: the specialised source (search kernel if gen_blob, else eval kernel), optionally hipRTC-compiled */
+int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words, int compile,
+                          char* buf, size_t cap, size_t* out_len);
+int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle);
+int mg_jit_info(uint64_t jit, double* compile_ms, int* blocks_per_cu);
+int mg_jit_free(uint64_t jit);
+int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags, uint64_t* first_hit,
+                  uint64_t* n_hits);
+int mg_jit_eval(uint64_t jit, const uint32_t* soa_coords, uint64_t n, uint8_t* verdict_out, uint32_t* watch_out);
+int mg_jit_eval_dev(uint64_t jit, const uint32_t* d_soa_coords, uint64_t n, uint8_t* d_verdict_out,
+                    uint32_t* d_watch_out);
+
 /* msgs: concatenated messages; lens: n byte lengths; out32: n x 32 bytes */
 int mg_keccak256(const uint8_t* msgs, const uint32_t* lens, uint64_t n, uint8_t* out32);
 

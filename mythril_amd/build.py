@@ -16,8 +16,26 @@ CSRC = PKG / "csrc"
 INCLUDE = PKG.parent / "include"
 LIB = PKG / "libmythgpu.so"
 
-SOURCES = [CSRC / "engine.hip", CSRC / "program.cpp"]
-HEADERS = [CSRC / "bv_device.h", CSRC / "keccak_device.h", CSRC / "program.hpp", INCLUDE / "mythgpu.h"]
+SOURCES = [CSRC / "engine.hip", CSRC / "program.cpp", CSRC / "jit.cpp"]
+HEADERS = [CSRC / "bv_device.h", CSRC / "keccak_device.h", CSRC / "jit_device.h", CSRC / "program.hpp",
+           CSRC / "jit.hpp", INCLUDE / "mythgpu.h"]
+PRELUDE_PARTS = [CSRC / "bv_device.h", CSRC / "keccak_device.h", CSRC / "jit_device.h"]
+PRELUDE_INC = CSRC / "jit_prelude.inc"
+
+
+def write_prelude() -> None:
+    """Embed the device headers the JIT kernels need as one raw string literal
+    (hipRTC gets no include path; #include / #pragma once lines are dropped)."""
+    body = []
+    for p in PRELUDE_PARTS:
+        for line in p.read_text().splitlines():
+            t = line.strip()
+            if t.startswith("#include") or t == "#pragma once":
+                continue
+            body.append(line)
+    text = "R\"MGJ(\n" + "\n".join(body) + "\n)MGJ\"\n"
+    if not PRELUDE_INC.exists() or PRELUDE_INC.read_text() != text:
+        PRELUDE_INC.write_text(text)
 
 ARCH = os.environ.get("MYTHGPU_ARCH", "gfx950")
 
@@ -33,14 +51,15 @@ def stale() -> bool:
     if not LIB.exists():
         return True
     t = LIB.stat().st_mtime
-    return any(p.stat().st_mtime > t for p in SOURCES + HEADERS)
+    return any(p.stat().st_mtime > t for p in SOURCES + HEADERS + [PRELUDE_INC])
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
+    write_prelude()
     if not force and not stale():
         return LIB
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-o", str(LIB)] + [str(s) for s in SOURCES]
+           "-Wno-unused-result", "-o", str(LIB), "-ldl"] + [str(s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     tmp = LIB.with_suffix(".so.tmp")

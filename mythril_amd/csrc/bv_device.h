@@ -345,3 +345,32 @@ __device__ __forceinline__ W8 bv_exp(const W8& base, const W8& e, u32 width) {
 }
 
 }  // namespace mg
+
+namespace mg {
+
+// low `width` bits of a*b
+__device__ __forceinline__ W8 mul8w(const W8& a, const W8& b, u32 width) {
+  W8 r = mul8(a, b);
+  canon8(r, width);
+  return r;
+}
+
+// bvumul_noovfl: the full 2w-bit product of two w-bit values fits in w bits
+__device__ __forceinline__ u32 umul_noovf8(const W8& x, const W8& y, u32 wa) {
+  const W8 lo = mul8(x, y);
+  const W8 hi = mulhi8(x, y);
+  u32 ov = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    ov |= hi.w[q];
+    const u32 bit0 = q * 32;
+    u32 m;
+    if (bit0 + 32 <= wa) m = 0u;
+    else if (bit0 >= wa) m = 0xFFFFFFFFu;
+    else m = ~((1u << (wa - bit0)) - 1u);
+    ov |= lo.w[q] & m;
+  }
+  return ov == 0;
+}
+
+}  // namespace mg

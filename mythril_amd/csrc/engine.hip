@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -27,6 +28,7 @@
 #include "../../include/mythgpu.h"
 #include "bv_device.h"
 #include "keccak_device.h"
+#include "jit.hpp"
 #include "program.hpp"
 
 namespace mg {
@@ -582,12 +584,24 @@ struct DevProgram {
 
 struct DevGen {
   uint64_t prog = 0;
+  std::vector<GenSpec> specs;     // host copies: the JIT specialises on them
+  std::vector<uint32_t> consts;
   GenSpec* d_specs = nullptr;
   uint32_t* d_consts = nullptr;
 };
 
+struct DevJit {
+  hipModule_t mod = nullptr;
+  hipFunction_t fsearch = nullptr, feval = nullptr;
+  uint64_t prog = 0, gen = 0;
+  int nb_search = 1, nb_eval = 1;
+  double compile_ms = 0;
+};
+
 struct Engine {
   std::mutex mu;
+  std::unordered_map<uint64_t, std::unique_ptr<DevJit>> jits;
+  std::unordered_map<std::string, std::vector<char>> code_cache;  // JIT source -> code object
   bool init = false;
   int device = -1;
   hipStream_t stream = nullptr;
@@ -847,6 +861,8 @@ int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* g
   if (rc) return set_err(rc, err);
   auto gg = std::make_unique<DevGen>();
   gg->prog = prog;
+  gg->specs = specs;
+  gg->consts = consts;
   if ((rc = upload(&gg->d_specs, specs.data(), specs.size()))) return rc;
   if ((rc = upload(&gg->d_consts, consts.data(), consts.size()))) return rc;
   const uint64_t h = e.next_handle++;
@@ -1041,6 +1057,196 @@ int mg_dev_upload(void* dptr, const void* src, size_t bytes) {
 int mg_dev_download(void* dst, const void* dptr, size_t bytes) {
   HIPCHK(hipMemcpy(dst, dptr, bytes, hipMemcpyDeviceToHost));
   return MG_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// JIT-specialised kernels
+// ---------------------------------------------------------------------------
+namespace mg {
+
+static int jit_launch(Engine& e, hipFunction_t f, int nb, uint64_t count, void** args) {
+  const uint64_t want = (count + 255) / 256;
+  const uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * std::max(nb, 1) * 2;
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+  HIPCHK(hipEventRecord(e.ev0, e.stream));
+  HIPCHK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, e.stream, args, nullptr));
+  HIPCHK(hipEventRecord(e.ev1, e.stream));
+  HIPCHK(hipEventSynchronize(e.ev1));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e.ev0, e.ev1));
+  e.stats.launches++;
+  e.stats.last_kernel_ms = ms;
+  e.stats.kernel_ms_total += ms;
+  e.stats.candidates += count;
+  e.stats.last_candidates = count;
+  return MG_OK;
+}
+
+}  // namespace mg
+
+extern "C" {
+
+int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words, int compile,
+                          char* buf, size_t cap, size_t* out_len) {
+  Lowered low;
+  std::string err;
+  int rc = lower_program(ssa, len, low, err);
+  if (rc) return set_err(rc, err);
+  std::vector<GenSpec> specs;
+  std::vector<uint32_t> consts;
+  if (gen_blob) {
+    rc = parse_gen(low, gen_blob, gen_words, specs, consts, err);
+    if (rc) return set_err(rc, err);
+  }
+  const std::string src = gen_blob ? jit_source(low, &specs, &consts, true, false)
+                                   : jit_source(low, nullptr, nullptr, false, true);
+  if (out_len) *out_len = src.size();
+  if (buf && cap) {
+    const size_t n = std::min(cap - 1, src.size());
+    std::memcpy(buf, src.data(), n);
+    buf[n] = 0;
+  }
+  if (compile) {
+    std::vector<char> code;
+    std::string log;
+    rc = jit_compile(src, code, log);
+    if (rc) return set_err(rc, "JIT compile failed: " + log.substr(0, 4000));
+  }
+  return MG_OK;
+}
+
+int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  DevProgram* p = find_prog(e, prog);
+  if (!p) return set_err(MG_E_INVALID, "bad program handle");
+  DevGen* gp = nullptr;
+  if (gen) {
+    auto it = e.gens.find(gen);
+    if (it == e.gens.end() || it->second->prog != prog) return set_err(MG_E_INVALID, "bad generator handle");
+    gp = it->second.get();
+  }
+  // with a generator: the search kernel specialised on it; without: the eval kernel
+  const std::string src =
+      gp ? jit_source(p->low, &gp->specs, &gp->consts, true, false) : jit_source(p->low, nullptr, nullptr, false, true);
+  auto t0 = std::chrono::steady_clock::now();
+  auto hit = e.code_cache.find(src);
+  if (hit == e.code_cache.end()) {
+    std::vector<char> code;
+    std::string log;
+    int rc = jit_compile(src, code, log);
+    if (rc) return set_err(rc, "JIT compile failed: " + log.substr(0, 4000));
+    hit = e.code_cache.emplace(src, std::move(code)).first;
+  }
+  auto j = std::make_unique<DevJit>();
+  HIPCHK(hipModuleLoadData(&j->mod, hit->second.data()));
+  int nb = 0;
+  if (gp) {
+    HIPCHK(hipModuleGetFunction(&j->fsearch, j->mod, "mgj_search"));
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, j->fsearch, 256, 0) == hipSuccess && nb > 0)
+      j->nb_search = nb;
+  } else {
+    HIPCHK(hipModuleGetFunction(&j->feval, j->mod, "mgj_eval"));
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, j->feval, 256, 0) == hipSuccess && nb > 0)
+      j->nb_eval = nb;
+  }
+  j->prog = prog;
+  j->gen = gen;
+  j->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const uint64_t h = e.next_handle++;
+  e.jits[h] = std::move(j);
+  *jit_handle = h;
+  return MG_OK;
+}
+
+int mg_jit_info(uint64_t jit, double* compile_ms, int* blocks_per_cu) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  auto it = e.jits.find(jit);
+  if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
+  if (compile_ms) *compile_ms = it->second->compile_ms;
+  if (blocks_per_cu) *blocks_per_cu = it->second->nb_search;
+  return MG_OK;
+}
+
+int mg_jit_free(uint64_t jit) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  auto it = e.jits.find(jit);
+  if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
+  (void)hipModuleUnload(it->second->mod);
+  e.jits.erase(it);
+  return MG_OK;
+}
+
+int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags, uint64_t* first_hit,
+                  uint64_t* n_hits) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  auto it = e.jits.find(jit);
+  if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
+  DevJit& j = *it->second;
+  DevProgram* p = find_prog(e, j.prog);
+  auto git = e.gens.find(j.gen);
+  if (!p || git == e.gens.end() || !j.fsearch) return set_err(MG_E_INVALID, "jit was not compiled for search");
+  unsigned long long init[2] = {~0ull, 0ull};
+  HIPCHK(hipMemcpyAsync(e.d_hit, init, sizeof(init), hipMemcpyHostToDevice, e.stream));
+  const uint32_t* gconsts = git->second->d_consts;
+  const GenSpec* specs = git->second->d_specs;
+  const uint32_t* cw = p->d_coord_width;
+  unsigned long long* hitp = e.d_hit;
+  void* args[] = {&gconsts, &specs, &cw, &start, &count, &seed, &hitp, &flags};
+  int rc = jit_launch(e, j.fsearch, j.nb_search, count, args);
+  if (rc) return rc;
+  unsigned long long res[2];
+  HIPCHK(hipMemcpy(res, e.d_hit, sizeof(res), hipMemcpyDeviceToHost));
+  if (first_hit) *first_hit = res[0];
+  if (n_hits) *n_hits = res[1];
+  e.stats.hits += res[1];
+  return MG_OK;
+}
+
+int mg_jit_eval_dev(uint64_t jit, const uint32_t* d_soa, uint64_t n, uint8_t* d_verdict, uint32_t* d_watch) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  auto it = e.jits.find(jit);
+  if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
+  DevJit& j = *it->second;
+  if (!j.feval) return set_err(MG_E_INVALID, "jit was not compiled for eval (compile with gen = 0)");
+  void* args[] = {&d_soa, &n, &d_verdict, &d_watch};
+  return jit_launch(e, j.feval, j.nb_eval, n, args);
+}
+
+int mg_jit_eval(uint64_t jit, const uint32_t* soa, uint64_t n, uint8_t* verdict_out, uint32_t* watch_out) {
+  Engine& e = E();
+  DevProgram* p;
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    auto it = e.jits.find(jit);
+    if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
+    p = find_prog(e, it->second->prog);
+    if (!p) return set_err(MG_E_INVALID, "jit program was freed");
+  }
+  if (n == 0) return MG_OK;
+  const size_t soa_bytes = (size_t)std::max<uint32_t>(p->low.coord_words, 1) * n * 4;
+  const size_t watch_bytes = (size_t)p->low.watch_words * n * 4;
+  uint32_t *d_soa = nullptr, *d_watch = nullptr;
+  uint8_t* d_ver = nullptr;
+  HIPCHK(hipMalloc((void**)&d_soa, soa_bytes));
+  HIPCHK(hipMalloc((void**)&d_ver, n));
+  if (watch_out && watch_bytes) HIPCHK(hipMalloc((void**)&d_watch, watch_bytes));
+  if (p->low.coord_words) HIPCHK(hipMemcpy(d_soa, soa, (size_t)p->low.coord_words * n * 4, hipMemcpyHostToDevice));
+  int rc = mg_jit_eval_dev(jit, d_soa, n, d_ver, d_watch);
+  if (rc == MG_OK) {
+    HIPCHK(hipMemcpy(verdict_out, d_ver, n, hipMemcpyDeviceToHost));
+    if (d_watch) HIPCHK(hipMemcpy(watch_out, d_watch, watch_bytes, hipMemcpyDeviceToHost));
+  }
+  (void)hipFree(d_soa);
+  (void)hipFree(d_ver);
+  if (d_watch) (void)hipFree(d_watch);
+  return rc;
 }
 
 }  // extern "C"

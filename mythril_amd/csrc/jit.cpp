@@ -1,0 +1,513 @@
+// JIT specialisation: one lowered program -> straight-line HIP source ->
+// hipRTC -> code object.  Every SSA value becomes scalar u32 limbs (v<id>_<j>) so
+// LLVM allocates VGPRs; literals become immediates; the candidate generator is
+// inlined per coordinate.  This removes the interpreter's per-instruction fetch,
+// dispatch and value-file traffic (the dominant cost of k_run).
+#include "jit.hpp"
+
+#include <dlfcn.h>
+
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+
+namespace mg {
+
+namespace {
+
+const char* kPrelude =
+#include "jit_prelude.inc"
+    ;
+
+inline uint32_t Lw(uint32_t w) { return (w + 31) / 32; }
+
+struct Gen {
+  const Lowered& P;
+  const std::vector<GenSpec>* specs;
+  const std::vector<uint32_t>* gconsts;
+  std::ostringstream o;
+  Gen(const Lowered& p, const std::vector<GenSpec>* s, const std::vector<uint32_t>* g) : P(p), specs(s), gconsts(g) {}
+
+  // Branch-free, spec-specialised generator for coordinate c (same function of
+  // (key, c) as gen_coord in engine.hip / gen_regs in jit_device.h): every
+  // alternative is computed and the winner picked with selects, so the kernel
+  // keeps a tiny CFG (hipRTC compile time is dominated by register coalescing
+  // over basic blocks otherwise).  Writes limbs into `out` names.
+  void gen_value(uint32_t c, uint32_t width, const std::string& out, bool allow_copy, int depth) {
+    const GenSpec& sp = (*specs)[c];
+    const uint32_t L = Lw(width);
+    const uint32_t Lc = Lw(P.coord_width[c]);  // limb stride of this coordinate's constants
+    const uint32_t Lg = std::min(L, Lc);
+    const std::string C = std::to_string(c) + "u";
+    auto lim = [&](const std::string& base, uint32_t j) { return base + "_" + std::to_string(j); };
+    o << "  {\n";
+    switch (sp.kind) {
+      case MG_GEN_MIXED: {
+        const uint32_t pc = (allow_copy && sp.p[3] != MG_NONE) ? sp.p[4] : 0u;
+        const uint32_t pd = sp.p[1] ? sp.p[2] : 0u;
+        const uint32_t ps = sp.p[6] & 0xFFFFu;
+        const uint32_t bits = std::min(width, sp.p[6] >> 16);
+        o << "  const uint32_t sel" << depth << " = rnd(key, " << C << ", 0xFFFFu) & 0xFFFFu;\n";
+        // uniform / small
+        for (uint32_t j = 0; j < L; j++) o << "  const uint32_t u" << depth << "_" << j << " = rnd(key, " << C << ", " << j << "u);\n";
+        // dictionary (+ delta)
+        if (pd) {
+          o << "  const uint32_t de" << depth << " = (uint32_t)(((uint64_t)rnd(key, " << C << ", 0xFFFEu) * " << sp.p[1]
+            << "ull) >> 32);\n";
+          for (uint32_t j = 0; j < L; j++)
+            o << "  uint32_t d" << depth << "_" << j << " = " << (j < Lg ? ("gconsts[" + std::to_string(sp.p[0] + j) + "u + de" + std::to_string(depth) + " * " + std::to_string(Lc) + "u]") : std::string("0u")) << ";\n";
+          if (sp.p[5]) {
+            o << "  { const uint32_t rr = rnd(key, " << C << ", 0xFFFDu); const bool on = (rr & 0xFFFFu) < " << sp.p[5]
+              << "u; const uint64_t mag = on ? (((rr >> 16) & 1u) + 1u) : 0u; const bool sb = (rr >> 17) & 1u; uint64_t cy = mag, t;";
+            for (uint32_t j = 0; j < Lg; j++)
+              o << " t = sb ? ((uint64_t)d" << depth << "_" << j << " - cy) : ((uint64_t)d" << depth << "_" << j
+                << " + cy); d" << depth << "_" << j << " = (uint32_t)t; cy = sb ? ((t >> 32) & 1u) : (t >> 32);";
+            o << " (void)cy; }\n";
+          }
+        }
+        // copy of another coordinate (its own spec, no further copy)
+        if (pc) {
+          const uint32_t src = sp.p[3];
+          const uint32_t sw = P.coord_width[src];
+          const uint32_t Ls = Lw(sw);
+          for (uint32_t j = 0; j < L; j++) o << "  uint32_t k" << depth << "_" << j << " = 0u;\n";
+          o << "  uint32_t";
+          for (uint32_t j = 0; j < Ls; j++) o << (j ? ", " : " ") << "kk" << depth << "_" << j;
+          o << ";\n";
+          gen_value(src, sw, "kk" + std::to_string(depth), false, depth + 1);
+          for (uint32_t j = 0; j < L && j < Ls; j++)
+            o << "  k" << depth << "_" << j << " = kk" << depth << "_" << j << ";\n";
+        }
+        for (uint32_t j = 0; j < L; j++) {
+          const uint32_t lo = 32 * j;
+          uint32_t smask = lo >= bits ? 0u : (bits - lo >= 32 ? 0xFFFFFFFFu : ((1u << (bits - lo)) - 1u));
+          std::string e = "u" + std::to_string(depth) + "_" + std::to_string(j);
+          if (ps) e = "(sel" + std::to_string(depth) + " < " + std::to_string(pc + pd + ps) + "u ? (" + e + " & " + hex(smask) + ") : " + e + ")";
+          if (pd) e = "(sel" + std::to_string(depth) + " < " + std::to_string(pc + pd) + "u ? d" + std::to_string(depth) + "_" + std::to_string(j) + " : " + e + ")";
+          if (pc) e = "(sel" + std::to_string(depth) + " < " + std::to_string(pc) + "u ? k" + std::to_string(depth) + "_" + std::to_string(j) + " : " + e + ")";
+          o << "  " << lim(out, j) << " = " << e << ";\n";
+        }
+        break;
+      }
+      case MG_GEN_DICT: {
+        o << "  const uint32_t de = (uint32_t)(((uint64_t)rnd(key, " << C << ", 0xFFFEu) * " << sp.p[1] << "ull) >> 32);\n";
+        for (uint32_t j = 0; j < L; j++)
+          o << "  " << lim(out, j) << " = " << (j < Lg ? ("gconsts[" + std::to_string(sp.p[0] + j) + "u + de * " + std::to_string(Lc) + "u]") : std::string("0u")) << ";\n";
+        break;
+      }
+      case MG_GEN_RANGE: {
+        o << "  const uint32_t r = rnd(key, " << C << ", 0u); uint64_t cy = "
+          << (sp.p[1] ? ("(uint32_t)(((uint64_t)r * " + std::to_string(sp.p[1]) + "ull) >> 32)") : std::string("r"))
+          << ", t;\n";
+        for (uint32_t j = 0; j < L; j++) {
+          if (j < Lg)
+            o << "  t = (uint64_t)" << hex((*gconsts)[sp.p[0] + j]) << " + cy; " << lim(out, j) << " = (uint32_t)t; cy = t >> 32;\n";
+          else
+            o << "  " << lim(out, j) << " = 0u;\n";
+        }
+        o << "  (void)cy;\n";
+        break;
+      }
+      case MG_GEN_ALIGNED: {
+        o << "  const uint32_t r = rnd(key, " << C << ", 0u); const uint64_t m = "
+          << (sp.p[2] ? ("(((uint64_t)r * " + std::to_string(sp.p[2]) + "ull) >> 32)") : std::string("(uint64_t)r"))
+          << "; uint64_t cy = 0, t;\n";
+        const int32_t sh = (int32_t)sp.p[1];
+        for (uint32_t j = 0; j < L; j++) {
+          if (j >= Lg) {
+            o << "  " << lim(out, j) << " = 0u;\n";
+            continue;
+          }
+          const int32_t bit0 = (int32_t)(j * 32) - sh;
+          std::string mw;
+          if (bit0 <= -32 || bit0 >= 64) mw = "0u";
+          else if (bit0 < 0) mw = "(uint32_t)(m << " + std::to_string(-bit0) + ")";
+          else mw = "(uint32_t)(m >> " + std::to_string(bit0) + ")";
+          o << "  t = (uint64_t)" << hex((*gconsts)[sp.p[0] + j]) << " + " << mw << " + cy; " << lim(out, j)
+            << " = (uint32_t)t; cy = t >> 32;\n";
+        }
+        o << "  (void)cy;\n";
+        break;
+      }
+      case MG_GEN_FIXED:
+        for (uint32_t j = 0; j < L; j++)
+          o << "  " << lim(out, j) << " = " << (j < Lg ? hex((*gconsts)[sp.p[0] + j]) : std::string("0u")) << ";\n";
+        break;
+      default:  // UNIFORM / LAZY
+        for (uint32_t j = 0; j < L; j++)
+          o << "  " << lim(out, j) << " = " << (j < Lg ? ("rnd(key, " + C + ", " + std::to_string(j) + "u)") : std::string("0u")) << ";\n";
+        break;
+    }
+    if (width & 31) o << "  " << lim(out, L - 1) << " &= " << hex(topmask(width)) << ";\n";
+    o << "  }\n";
+  }
+
+  std::string v(uint32_t id, uint32_t j) const {
+    if (j >= Lw(P.vwidth[id])) return "0u";
+    return "v" + std::to_string(id) + "_" + std::to_string(j);
+  }
+  static std::string hex(uint32_t x) {
+    char b[16];
+    snprintf(b, sizeof b, "0x%08xu", x);
+    return b;
+  }
+  static uint32_t topmask(uint32_t w) { return (w & 31) ? ((1u << (w & 31)) - 1u) : 0xFFFFFFFFu; }
+
+  // 32 bits of value id starting at bit p (zero above width w)
+  std::string bits(uint32_t id, uint32_t w, uint32_t p) const {
+    if (p >= w) return "0u";
+    const uint32_t q = p >> 5, r = p & 31;
+    const uint32_t L = Lw(w);
+    if (r == 0) return v(id, q);
+    std::string lo = "(" + v(id, q) + " >> " + std::to_string(r) + ")";
+    if (q + 1 < L) lo = "(" + lo + " | (" + v(id, q + 1) + " << " + std::to_string(32 - r) + "))";
+    return lo;
+  }
+
+  void mask_top(uint32_t id) {
+    const uint32_t w = P.vwidth[id];
+    if (w & 31) o << "  " << v(id, Lw(w) - 1) << " &= " << hex(topmask(w)) << ";\n";
+  }
+
+  std::string w8(uint32_t id) const {
+    std::string s = "{{";
+    for (uint32_t j = 0; j < 8; j++) s += (j ? "," : "") + v(id, j);
+    return s + "}}";
+  }
+
+  void emit(const Instr& in, bool search, bool eval_watch) {
+    const uint32_t d = in.dst, W = in.wd, L = Lw(W);
+    switch (in.op) {
+      case K_CONST:
+        for (uint32_t j = 0; j < L; j++) o << "  " << v(d, j) << " = " << hex(P.consts[in.p0 + j]) << ";\n";
+        break;
+      case K_COORD:
+        if (search && specs) {
+          gen_value(in.p0, W, "v" + std::to_string(d), true, 0);
+        } else if (search) {
+          o << "  { uint32_t t[" << L << "]; gen_regs<" << L << ">(t, gconsts, specs, cw, " << in.p0 << "u, " << W
+            << "u, key);";
+          for (uint32_t j = 0; j < L; j++) o << " " << v(d, j) << " = t[" << j << "];";
+          o << " }\n";
+        } else {
+          for (uint32_t j = 0; j < L; j++)
+            o << "  " << v(d, j) << " = soa[(uint64_t)" << (in.p1 + j) << "u * n + i];\n";
+        }
+        break;
+      case K_ADD:
+      case K_SUB: {
+        const bool sub = in.op == K_SUB;
+        o << "  { uint64_t c = 0, t;";
+        for (uint32_t j = 0; j < L; j++) {
+          if (sub)
+            o << " t = (uint64_t)" << v(in.a, j) << " - " << v(in.b, j) << " - c; " << v(d, j)
+              << " = (uint32_t)t; c = (t >> 32) & 1u;";
+          else
+            o << " t = (uint64_t)" << v(in.a, j) << " + " << v(in.b, j) << " + c; " << v(d, j)
+              << " = (uint32_t)t; c = t >> 32;";
+        }
+        o << " (void)c; }\n";
+        mask_top(d);
+        break;
+      }
+      case K_NEG: {
+        o << "  { uint64_t c = 0, t;";
+        for (uint32_t j = 0; j < L; j++)
+          o << " t = 0ull - (uint64_t)" << v(in.a, j) << " - c; " << v(d, j) << " = (uint32_t)t; c = (t >> 32) & 1u;";
+        o << " (void)c; }\n";
+        mask_top(d);
+        break;
+      }
+      case K_AND: case K_OR: case K_XOR: {
+        const char* op = in.op == K_AND ? " & " : in.op == K_OR ? " | " : " ^ ";
+        for (uint32_t j = 0; j < L; j++) o << "  " << v(d, j) << " = " << v(in.a, j) << op << v(in.b, j) << ";\n";
+        break;
+      }
+      case K_NOT:
+        for (uint32_t j = 0; j < L; j++) o << "  " << v(d, j) << " = ~" << v(in.a, j) << ";\n";
+        mask_top(d);
+        break;
+      case K_ITE:
+        for (uint32_t j = 0; j < L; j++)
+          o << "  " << v(d, j) << " = " << v(in.a, 0) << " ? " << v(in.b, j) << " : " << v(in.c, j) << ";\n";
+        break;
+      case K_EQ: {
+        const uint32_t La = Lw(in.p1);
+        o << "  " << v(d, 0) << " = (0u";
+        for (uint32_t j = 0; j < La; j++) o << " | (" << v(in.a, j) << " ^ " << v(in.b, j) << ")";
+        o << ") == 0u;\n";
+        break;
+      }
+      case K_ULT: case K_ULE: case K_SLT: case K_SLE: {
+        const uint32_t wa = in.p1, La = Lw(wa);
+        const bool sgn = in.op == K_SLT || in.op == K_SLE;
+        const std::string flip = sgn ? hex(1u << ((wa - 1) & 31)) : "0u";
+        o << "  { uint64_t br = 0, t; uint32_t nz = 0;";
+        for (uint32_t j = 0; j < La; j++) {
+          std::string x = v(in.a, j), y = v(in.b, j);
+          if (j == La - 1 && sgn) {
+            x = "(" + x + " ^ " + flip + ")";
+            y = "(" + y + " ^ " + flip + ")";
+          }
+          o << " t = (uint64_t)" << x << " - " << y << " - br; br = (t >> 32) & 1u; nz |= (uint32_t)t;";
+        }
+        if (in.op == K_ULT || in.op == K_SLT)
+          o << " " << v(d, 0) << " = (uint32_t)br; (void)nz; }\n";
+        else
+          o << " " << v(d, 0) << " = (uint32_t)(br != 0 || nz == 0); }\n";
+        break;
+      }
+      case K_CONCAT: {
+        const uint32_t wb = in.p1, wa = W - wb;
+        for (uint32_t j = 0; j < L; j++) {
+          const uint32_t p = 32 * j;
+          std::string e = bits(in.b, wb, p);
+          if (p + 32 > wb) {
+            std::string hi = p >= wb ? bits(in.a, wa, p - wb) : "(" + bits(in.a, wa, 0) + " << " + std::to_string(wb - p) + ")";
+            e = "(" + e + " | " + hi + ")";
+          }
+          o << "  " << v(d, j) << " = " << e << ";\n";
+        }
+        mask_top(d);
+        break;
+      }
+      case K_EXTRACT:
+        for (uint32_t j = 0; j < L; j++) o << "  " << v(d, j) << " = " << bits(in.a, in.p1, in.p0 + 32 * j) << ";\n";
+        mask_top(d);
+        break;
+      case K_ZEXT: {
+        const uint32_t La = Lw(in.p1);
+        for (uint32_t j = 0; j < L; j++) o << "  " << v(d, j) << " = " << (j < La ? v(in.a, j) : "0u") << ";\n";
+        break;
+      }
+      case K_SEXT: {
+        const uint32_t wa = in.p1, La = Lw(wa);
+        const uint32_t tm = topmask(wa);
+        o << "  { const uint32_t f = ((" << v(in.a, La - 1) << " >> " << ((wa - 1) & 31) << ") & 1u) ? 0xFFFFFFFFu : 0u;";
+        for (uint32_t j = 0; j < L; j++) {
+          if (j < La - 1) o << " " << v(d, j) << " = " << v(in.a, j) << ";";
+          else if (j == La - 1)
+            o << " " << v(d, j) << " = (" << v(in.a, j) << " & " << hex(tm) << ") | (f & " << hex(~tm) << ");";
+          else o << " " << v(d, j) << " = f;";
+        }
+        o << " }\n";
+        mask_top(d);
+        break;
+      }
+      case K_MUL: case K_UDIV: case K_UREM: case K_SDIV: case K_SREM: case K_SMOD:
+      case K_SHL: case K_LSHR: case K_ASHR: case K_EXP: {
+        const char* fn = nullptr;
+        switch (in.op) {
+          case K_MUL: fn = "mul8w"; break;
+          case K_UDIV: fn = "bv_udiv"; break;
+          case K_UREM: fn = "bv_urem"; break;
+          case K_SDIV: fn = "bv_sdiv"; break;
+          case K_SREM: fn = "bv_srem"; break;
+          case K_SMOD: fn = "bv_smod"; break;
+          case K_SHL: fn = "bv_shl"; break;
+          case K_LSHR: fn = "bv_lshr"; break;
+          case K_ASHR: fn = "bv_ashr"; break;
+          default: fn = "bv_exp"; break;
+        }
+        o << "  { const W8 x = " << w8(in.a) << ", y = " << w8(in.b) << "; const W8 r = " << fn << "(x, y, " << W
+          << "u);";
+        for (uint32_t j = 0; j < L; j++) o << " " << v(d, j) << " = r.w[" << j << "];";
+        o << " }\n";
+        break;
+      }
+      case K_UMUL_NOOVF: {
+        const uint32_t wa = in.p1;
+        o << "  { const W8 x = " << w8(in.a) << ", y = " << w8(in.b) << "; " << v(d, 0) << " = umul_noovf8(x, y, "
+          << wa << "u); }\n";
+        break;
+      }
+      case K_LOOKUP: {
+        const uint32_t Lk = Lw(in.b), n = in.c;
+        for (uint32_t j = 0; j < L; j++) o << "  " << v(d, j) << " = " << v(in.p0, j) << ";\n";
+        // first match wins: apply the priors from last to first
+        for (int32_t p = (int32_t)n - 1; p >= 0; p--) {
+          const uint32_t kv = P.vaux[in.p1 + 2 * p], vv = P.vaux[in.p1 + 2 * p + 1];
+          o << "  { const bool h = (0u";
+          for (uint32_t j = 0; j < Lk; j++) o << " | (" << v(in.a, j) << " ^ " << v(kv, j) << ")";
+          o << ") == 0u;";
+          for (uint32_t j = 0; j < L; j++) o << " " << v(d, j) << " = h ? " << v(vv, j) << " : " << v(d, j) << ";";
+          o << " }\n";
+        }
+        break;
+      }
+      case K_KECCAK: {
+        if (in.a == MG_NONE) {
+          static const uint32_t e[8] = {0x5d85a470u, 0x7bfad804u, 0xca82273bu, 0xe500b653u,
+                                        0xdcc703c0u, 0x927e7db2u, 0x86f7233cu, 0xc5d24601u};
+          for (uint32_t j = 0; j < 8; j++) o << "  " << v(d, j) << " = " << hex(e[j]) << ";\n";
+        } else {
+          const uint32_t La = Lw(P.vwidth[in.a]);
+          o << "  { uint32_t in_[" << La << "] = {";
+          for (uint32_t j = 0; j < La; j++) o << (j ? "," : "") << v(in.a, j);
+          o << "}; uint32_t out_[8]; keccak_value<" << La << ", " << in.p0 << ">(in_, out_);";
+          for (uint32_t j = 0; j < 8; j++) o << " " << v(d, j) << " = out_[" << j << "];";
+          o << " }\n";
+        }
+        break;
+      }
+      case K_ASSERT:
+        o << "  verdict &= " << v(in.a, 0) << ";\n";
+        if (search) o << "  if (early && __ballot(verdict != 0u) == 0ull) goto mg_next;\n";
+        break;
+      case K_WATCH:
+        if (eval_watch)
+          for (uint32_t j = 0; j < L; j++)
+            o << "  if (watch) watch[(uint64_t)" << (in.p0 + j) << "u * n + i] = " << v(in.a, j) << ";\n";
+        break;
+      case K_COPY:
+        for (uint32_t j = 0; j < L; j++) o << "  " << v(d, j) << " = " << v(in.a, j) << ";\n";
+        break;
+      default:
+        break;
+    }
+  }
+
+  void decls() {
+    // declare every limb of every value up front (gotos may jump over the body)
+    size_t n = 0;
+    for (uint32_t id = 0; id < P.vwidth.size(); id++) {
+      for (uint32_t j = 0; j < Lw(P.vwidth[id]); j++) {
+        o << (n % 16 == 0 ? "  uint32_t " : ", ") << v(id, j);
+        if (n % 16 == 15) o << ";\n";
+        n++;
+      }
+    }
+    if (n % 16) o << ";\n";
+  }
+
+  void body(bool search) {
+    for (const Instr& in : P.vcode) emit(in, search, !search);
+  }
+};
+
+}  // namespace
+
+std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
+                       bool want_search, bool want_eval) {
+  Gen g(P, specs, gconsts);
+  auto& o = g.o;
+  o << "typedef unsigned int uint32_t;\ntypedef int int32_t;\ntypedef unsigned long long uint64_t;\n"
+    << "typedef unsigned char uint8_t;\n";
+  o << kPrelude << "\nusing namespace mg;\n";
+  if (want_search) {
+  // search kernel
+  o << "extern \"C\" __global__ void __launch_bounds__(256) mgj_search(const uint32_t* __restrict__ gconsts, "
+       "const GenSpec* __restrict__ specs, const uint32_t* __restrict__ cw, uint64_t start, uint64_t count, "
+       "uint64_t seed, unsigned long long* hit, uint32_t flags) {\n"
+       "  const bool early = (flags & 1u) != 0u;\n"
+       "  const uint32_t lane = threadIdx.x & 63u;\n"
+       "  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;\n"
+       "  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < count; base += stride) {\n"
+       "  if (early) {\n"
+       "    const unsigned long long cur = __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+       "    const uint64_t cu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) | "
+       "__builtin_amdgcn_readfirstlane((uint32_t)cur);\n"
+       "    if (start + base >= cu) break;\n"
+       "  }\n"
+       "  const uint64_t i = base + lane;\n"
+       "  const bool active = i < count;\n"
+       "  const uint64_t idx = start + (active ? i : count - 1);\n"
+       "  const uint32_t key = cand_key(idx, seed);\n"
+       "  uint32_t verdict = 1u;\n";
+  g.decls();
+  g.body(true);
+  o << "  mg_next:\n"
+       "  verdict = active ? verdict : 0u;\n"
+       "  { const unsigned long long m = __ballot(verdict != 0u);\n"
+       "    if (m && lane == (uint32_t)(__ffsll((long long)m) - 1)) {\n"
+       "      atomicMin(hit, (unsigned long long)idx);\n"
+       "      atomicAdd(hit + 1, (unsigned long long)__popcll(m));\n"
+       "    } }\n"
+       "  }\n}\n\n";
+  }
+  if (want_eval) {
+  // eval kernel (explicit SoA coordinates, verdicts, optional watch rows)
+  o << "extern \"C\" __global__ void __launch_bounds__(256) mgj_eval(const uint32_t* __restrict__ soa, uint64_t n, "
+       "uint8_t* __restrict__ verdict_out, uint32_t* __restrict__ watch) {\n"
+       "  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;\n"
+       "  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {\n"
+       "  uint32_t verdict = 1u;\n";
+  g.decls();
+  g.body(false);
+  o << "  verdict_out[i] = (uint8_t)verdict;\n  }\n}\n";
+  }
+  return o.str();
+}
+
+// ---------------------------------------------------------------------------
+// hipRTC, loaded at run time (no link-time dependency of libmythgpu.so on it)
+// ---------------------------------------------------------------------------
+namespace {
+typedef int (*pCreate)(void**, const char*, const char*, int, const char**, const char**);
+typedef int (*pCompile)(void*, int, const char**);
+typedef int (*pSize)(void*, size_t*);
+typedef int (*pGet)(void*, char*);
+typedef int (*pDestroy)(void**);
+struct Rtc {
+  void* h = nullptr;
+  pCreate create = nullptr;
+  pCompile compile = nullptr;
+  pSize log_size = nullptr, code_size = nullptr;
+  pGet log = nullptr, code = nullptr;
+  pDestroy destroy = nullptr;
+  bool ok = false;
+};
+Rtc& rtc() {
+  static Rtc r;
+  if (r.h) return r;
+  const char* names[] = {"libhiprtc.so.7", "/opt/rocm/lib/libhiprtc.so.7", "libhiprtc.so"};
+  for (const char* n : names) {
+    r.h = dlopen(n, RTLD_NOW | RTLD_LOCAL);
+    if (r.h) break;
+  }
+  if (!r.h) return r;
+  r.create = (pCreate)dlsym(r.h, "hiprtcCreateProgram");
+  r.compile = (pCompile)dlsym(r.h, "hiprtcCompileProgram");
+  r.log_size = (pSize)dlsym(r.h, "hiprtcGetProgramLogSize");
+  r.log = (pGet)dlsym(r.h, "hiprtcGetProgramLog");
+  r.code_size = (pSize)dlsym(r.h, "hiprtcGetCodeSize");
+  r.code = (pGet)dlsym(r.h, "hiprtcGetCode");
+  r.destroy = (pDestroy)dlsym(r.h, "hiprtcDestroyProgram");
+  r.ok = r.create && r.compile && r.log_size && r.log && r.code_size && r.code && r.destroy;
+  return r;
+}
+}  // namespace
+
+int jit_compile(const std::string& src, std::vector<char>& code, std::string& log) {
+  Rtc& r = rtc();
+  if (!r.ok) {
+    log = "hipRTC not available";
+    return MG_E_UNSUPPORTED;
+  }
+  void* prog = nullptr;
+  if (r.create(&prog, src.c_str(), "mythgpu_jit.hip", 0, nullptr, nullptr) != 0) {
+    log = "hiprtcCreateProgram failed";
+    return MG_E_HIP;
+  }
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-variable",
+                        "-Wno-uninitialized", "-Wno-sometimes-uninitialized"};
+  int rc = r.compile(prog, (int)(sizeof(opts) / sizeof(opts[0])), opts);
+  size_t ls = 0;
+  r.log_size(prog, &ls);
+  if (ls > 1) {
+    log.resize(ls);
+    r.log(prog, &log[0]);
+  }
+  if (rc != 0) {
+    r.destroy(&prog);
+    return MG_E_HIP;
+  }
+  size_t cs = 0;
+  r.code_size(prog, &cs);
+  code.resize(cs);
+  r.code(prog, code.data());
+  r.destroy(&prog);
+  return MG_OK;
+}
+
+}  // namespace mg

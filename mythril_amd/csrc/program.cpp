@@ -531,6 +531,14 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
         in.c = S(c.c);
       }
       out.code.push_back(in);
+      {
+        Instr vi{c.op, c.wd, c.dst, c.a, c.b, c.c, c.p0, c.p1};
+        if (c.op == K_LOOKUP) {
+          vi.p1 = (uint32_t)out.vaux.size();
+          for (uint32_t v : c.prior) out.vaux.push_back(v);
+        }
+        out.vcode.push_back(vi);
+      }
       // cost
       uint32_t wa = c.p1;
       if (c.op == K_LOOKUP) {
@@ -555,6 +563,7 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
       }
     }
     out.value_words = std::max<uint32_t>(al.high(), 1);
+    out.vwidth = vwidth;
     return MG_OK;
   } catch (const Fail& f) {
     err = f.msg;
@@ -597,7 +606,11 @@ int parse_gen(const Lowered& prog, const uint32_t* blob, size_t n_words, std::ve
       case MG_GEN_MIXED:
         if (s.p[1] == 0 && s.kind == MG_GEN_DICT) { err = "empty dictionary"; return MG_E_INVALID; }
         if (!in_range(s.p[0], (uint64_t)s.p[1] * L)) { err = "dictionary out of range"; return MG_E_INVALID; }
-        if (s.kind == MG_GEN_MIXED && s.p[3] != MG_NONE && s.p[3] >= nc) { err = "copy source"; return MG_E_INVALID; }
+        if (s.kind == MG_GEN_MIXED && s.p[3] != MG_NONE &&
+            (s.p[3] >= nc || prog.coord_width[s.p[3]] != prog.coord_width[c])) {
+          err = "copy source must be a coordinate of the same width";
+          return MG_E_INVALID;
+        }
         break;
       case MG_GEN_LAZY:
         break;  // default comes from the program (UFAPP p2); the coordinate is unused

@@ -56,6 +56,10 @@ struct Lowered {
   uint32_t watch_words = 0;
   uint64_t limb_ops = 0;              // fixed cost table, per candidate
   uint32_t max_width = 0;
+  // SSA form of the same code (operands are value ids, not slots) for the JIT
+  std::vector<Instr> vcode;           // LOOKUP: p0 = default vid, p1 = offset into vaux
+  std::vector<uint32_t> vaux;         // LOOKUP prior lists: pairs (key vid, value vid)
+  std::vector<uint32_t> vwidth;       // width of each value id
 };
 
 // Parse + validate + lower. Returns MG_OK or an MG_E_* code with `err` set.

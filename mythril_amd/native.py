@@ -31,7 +31,8 @@ EXPORTS = [
     "mg_init", "mg_shutdown", "mg_last_error", "mg_version", "mg_program_check", "mg_program_load",
     "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_free", "mg_eval", "mg_eval_dev",
     "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
-    "mg_dev_free", "mg_dev_upload", "mg_dev_download",
+    "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_jit_compile", "mg_jit_info",
+    "mg_jit_free", "mg_jit_search", "mg_jit_eval", "mg_jit_eval_dev",
 ]
 
 
@@ -101,6 +102,14 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_dev_free": (C.c_int, [C.c_void_p]),
             "mg_dev_upload": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
             "mg_dev_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+            "mg_program_jit_source": (C.c_int, [u8p, C.c_size_t, u32p, C.c_size_t, C.c_int, C.c_char_p,
+                                                C.c_size_t, C.POINTER(C.c_size_t)]),
+            "mg_jit_compile": (C.c_int, [C.c_uint64, C.c_uint64, u64p]),
+            "mg_jit_info": (C.c_int, [C.c_uint64, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+            "mg_jit_free": (C.c_int, [C.c_uint64]),
+            "mg_jit_search": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u64p, u64p]),
+            "mg_jit_eval": (C.c_int, [C.c_uint64, u32p, C.c_uint64, u8p, u32p]),
+            "mg_jit_eval_dev": (C.c_int, [C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -133,6 +142,21 @@ def check_program(blob: bytes) -> ProgramInfo:
     info = ProgramInfo()
     _check(lib.mg_program_check(_u8(blob), len(blob), C.byref(info)))
     return info
+
+
+def jit_source(blob: bytes, gen_blob: Optional[np.ndarray] = None, compile: bool = False) -> str:
+    """Host-only: the specialised HIP source of a program — the search kernel when a
+    generator blob is given, else the eval kernel — optionally hipRTC-compiled (no GPU)."""
+    lib = load_library()
+    g = None if gen_blob is None else np.ascontiguousarray(gen_blob, dtype=np.uint32)
+    gp = _ptr(g, C.c_uint32) if g is not None else None
+    gn = 0 if g is None else g.size
+    n = C.c_size_t()
+    _check(lib.mg_program_jit_source(_u8(blob), len(blob), gp, gn, 0, None, 0, C.byref(n)))
+    buf = C.create_string_buffer(n.value + 1)
+    _check(lib.mg_program_jit_source(_u8(blob), len(blob), gp, gn, 1 if compile else 0, buf, n.value + 1,
+                                     C.byref(n)))
+    return buf.value.decode()
 
 
 class Engine:
@@ -200,6 +224,34 @@ class Engine:
         flags = MG_SEARCH_EARLY_EXIT if early_exit else 0
         _check(self.lib.mg_search(prog, gen, seed, start, count, flags, C.byref(fh), C.byref(nh)))
         return (None if fh.value == NO_HIT else fh.value), nh.value
+
+    # JIT-specialised kernels --------------------------------------
+    def jit_compile(self, prog: int, gen: int = 0) -> int:
+        h = C.c_uint64()
+        _check(self.lib.mg_jit_compile(prog, gen, C.byref(h)))
+        return h.value
+
+    def jit_info(self, jit: int):
+        ms, nb = C.c_double(), C.c_int()
+        _check(self.lib.mg_jit_info(jit, C.byref(ms), C.byref(nb)))
+        return ms.value, nb.value
+
+    def jit_free(self, jit: int):
+        _check(self.lib.mg_jit_free(jit))
+
+    def jit_search(self, jit: int, seed: int, start: int, count: int, early_exit: bool = True):
+        fh, nh = C.c_uint64(), C.c_uint64()
+        flags = MG_SEARCH_EARLY_EXIT if early_exit else 0
+        _check(self.lib.mg_jit_search(jit, seed, start, count, flags, C.byref(fh), C.byref(nh)))
+        return (None if fh.value == NO_HIT else fh.value), nh.value
+
+    def jit_eval(self, jit: int, soa: np.ndarray, n: int, watch_words: int = 0):
+        soa = np.ascontiguousarray(soa, dtype=np.uint32)
+        ver = np.zeros(n, dtype=np.uint8)
+        watch = np.zeros((max(watch_words, 1), n), dtype=np.uint32) if watch_words else None
+        _check(self.lib.mg_jit_eval(jit, _ptr(soa, C.c_uint32), n, _ptr(ver, C.c_uint8),
+                                    _ptr(watch, C.c_uint32) if watch is not None else None))
+        return ver, watch
 
     def keccak256(self, msgs):
         msgs = [bytes(m) for m in msgs]
