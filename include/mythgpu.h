@@ -123,7 +123,14 @@ enum mg_table_kind { MG_TABLE_ARRAY = 0, MG_TABLE_UF = 1 };
  * blob: header[4] {MG_GEN_MAGIC, n_coords, n_const_words, 0}
  *       specs: n_coords x 8 words {kind, p0, p1, p2, p3, p4, p5, p6}
  *       consts: n_const_words
- * Coordinate c of candidate i is a pure function of (seed, i, c).
+ * Coordinate c of candidate i is a pure function of (seed, i, c):
+ *   key        = mix32(i_lo ^ mix32(i_hi ^ seed_lo ^ mix32(seed_hi + 0x632BE5AB)))
+ *                (mix32: xorshift-multiply finaliser, multipliers 0x7FEB352D, 0x846CA68B)
+ *   rnd(c, j)  = fin(key ^ (c*0x9E3779B9 + j*0x85EBCA6B + 0x27D4EB2F)),
+ *                fin(x) = x ^= x>>16; x *= 0x7FEB352D; x ^= x>>15
+ *   uniform limb j = rnd(c, j); selector h = rnd(c, 0xFFFF): MIXED branch = h & 0xFFFF,
+ *   dictionary entry = ((h >> 16) * n) >> 16 (n <= 65535); the +/- delta of a
+ *   MIXED dictionary draw reads its bits from rnd(c, 0) (unused by that branch).
  */
 #define MG_GEN_MAGIC 0x314E4547u /* "GEN1" */
 enum mg_gen_kind {

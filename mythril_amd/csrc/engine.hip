@@ -92,7 +92,12 @@ __device__ __forceinline__ uint32_t cand_key(uint64_t idx, uint64_t seed) {
 }
 
 __device__ __forceinline__ uint32_t rnd(uint32_t key, uint32_t c, uint32_t j) {
-  return mix32(key + c * 0x9E3779B9u + j * 0x85EBCA6Bu + 0x27D4EB2Fu);
+  /* one-multiply finaliser of the (well mixed) candidate key; see MG_GEN_* in mythgpu.h */
+  uint32_t x = key ^ (c * 0x9E3779B9u + j * 0x85EBCA6Bu + 0x27D4EB2Fu);
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  return x;
 }
 
 template <class VF>
@@ -148,11 +153,11 @@ __device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c
   switch (s.kind) {
     case MG_GEN_DICT: {
       const uint32_t n = s.p[1];
-      const uint32_t e = (uint32_t)(((uint64_t)rnd(key, cc, 0xFFFEu) * n) >> 32);
+      const uint32_t e = (((rnd(key, cc, 0xFFFFu) >> 16) * n) >> 16);
       const uint32_t* src = k.gconsts + s.p[0] + e * Ls;
       for (uint32_t j = 0; j < Lg; j++) vf.at(dst + j) = src[j];
       if (s.p[6] == 1 && s.p[5]) {
-        const uint32_t r = rnd(key, cc, 0xFFFDu);
+        const uint32_t r = rnd(key, cc, 0u);
         if ((r & 0xFFFFu) < s.p[5]) {
           // +/- 1 or 2 (wrapping)
           const uint32_t mag = ((r >> 16) & 1u) + 1u;

@@ -8,6 +8,7 @@
 #include <dlfcn.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <sstream>
 
@@ -26,7 +27,19 @@ struct Gen {
   const std::vector<GenSpec>* specs;
   const std::vector<uint32_t>* gconsts;
   std::ostringstream o;
-  Gen(const Lowered& p, const std::vector<GenSpec>* s, const std::vector<uint32_t>* g) : P(p), specs(s), gconsts(g) {}
+  std::vector<int32_t> def;  // value id -> index of its defining instruction in P.vcode (-1: none)
+  Gen(const Lowered& p, const std::vector<GenSpec>* s, const std::vector<uint32_t>* g)
+      : P(p), specs(s), gconsts(g), def(p.vwidth.size(), -1) {
+    for (size_t k = 0; k < P.vcode.size(); k++)
+      if (P.vcode[k].dst != MG_NONE && P.vcode[k].dst < def.size() && def[P.vcode[k].dst] < 0)
+        def[P.vcode[k].dst] = (int32_t)k;
+  }
+  const Instr* def_of(uint32_t id) const { return def[id] >= 0 ? &P.vcode[def[id]] : nullptr; }
+  // literal limbs of a value defined by K_CONST (else nullptr)
+  const uint32_t* lit(uint32_t id) const {
+    const Instr* d = def_of(id);
+    return (d && d->op == K_CONST) ? &P.consts[d->p0] : nullptr;
+  }
 
   // Branch-free, spec-specialised generator for coordinate c (same function of
   // (key, c) as gen_coord in engine.hip / gen_regs in jit_device.h): every
@@ -47,17 +60,17 @@ struct Gen {
         const uint32_t pd = sp.p[1] ? sp.p[2] : 0u;
         const uint32_t ps = sp.p[6] & 0xFFFFu;
         const uint32_t bits = std::min(width, sp.p[6] >> 16);
-        o << "  const uint32_t sel" << depth << " = rnd(key, " << C << ", 0xFFFFu) & 0xFFFFu;\n";
+        o << "  const uint32_t h" << depth << " = rnd(key, " << C << ", 0xFFFFu);\n";
+        o << "  const uint32_t sel" << depth << " = h" << depth << " & 0xFFFFu;\n";
         // uniform / small
         for (uint32_t j = 0; j < L; j++) o << "  const uint32_t u" << depth << "_" << j << " = rnd(key, " << C << ", " << j << "u);\n";
         // dictionary (+ delta)
         if (pd) {
-          o << "  const uint32_t de" << depth << " = (uint32_t)(((uint64_t)rnd(key, " << C << ", 0xFFFEu) * " << sp.p[1]
-            << "ull) >> 32);\n";
+          o << "  const uint32_t de" << depth << " = ((h" << depth << " >> 16) * " << sp.p[1] << "u) >> 16;\n";
           for (uint32_t j = 0; j < L; j++)
             o << "  uint32_t d" << depth << "_" << j << " = " << (j < Lg ? ("gconsts[" + std::to_string(sp.p[0] + j) + "u + de" + std::to_string(depth) + " * " + std::to_string(Lc) + "u]") : std::string("0u")) << ";\n";
           if (sp.p[5]) {
-            o << "  { const uint32_t rr = rnd(key, " << C << ", 0xFFFDu); const bool on = (rr & 0xFFFFu) < " << sp.p[5]
+            o << "  { const uint32_t rr = u" << depth << "_0; const bool on = (rr & 0xFFFFu) < " << sp.p[5]
               << "u; const uint64_t mag = on ? (((rr >> 16) & 1u) + 1u) : 0u; const bool sb = (rr >> 17) & 1u; uint64_t cy = mag, t;";
             for (uint32_t j = 0; j < Lg; j++)
               o << " t = sb ? ((uint64_t)d" << depth << "_" << j << " - cy) : ((uint64_t)d" << depth << "_" << j
@@ -90,7 +103,7 @@ struct Gen {
         break;
       }
       case MG_GEN_DICT: {
-        o << "  const uint32_t de = (uint32_t)(((uint64_t)rnd(key, " << C << ", 0xFFFEu) * " << sp.p[1] << "ull) >> 32);\n";
+        o << "  const uint32_t de = ((rnd(key, " << C << ", 0xFFFFu) >> 16) * " << sp.p[1] << "u) >> 16;\n";
         for (uint32_t j = 0; j < L; j++)
           o << "  " << lim(out, j) << " = " << (j < Lg ? ("gconsts[" + std::to_string(sp.p[0] + j) + "u + de * " + std::to_string(Lc) + "u]") : std::string("0u")) << ";\n";
         break;
@@ -154,14 +167,72 @@ struct Gen {
   static uint32_t topmask(uint32_t w) { return (w & 31) ? ((1u << (w & 31)) - 1u) : 0xFFFFFFFFu; }
 
   // 32 bits of value id starting at bit p (zero above width w)
-  std::string bits(uint32_t id, uint32_t w, uint32_t p) const {
-    if (p >= w) return "0u";
+  // Expression for bits [p, p+need) of value `id` (width w) in its low bits.
+  // Bits of the expression at k >= need are either the value's bit p+k or 0, and
+  // are 0 above the value's width; need = 32 therefore gives an exact limb.
+  // Looks through CONCAT / ZEXT / EXTRACT definitions down to their operands, so
+  // a left-folded Concat of 32 calldata bytes costs O(32) shifts, not O(32^2).
+  std::string bits(uint32_t id, uint32_t w, uint32_t p, int need = 32, int depth = 0) const {
+    if (p >= w || need <= 0) return "0u";
+    const Instr* d = def_of(id);
+    if (d && depth < 96) {
+      if (d->op == K_CONCAT) {
+        const uint32_t wb = d->p1, wa = w - wb;
+        if (p >= wb) return bits(d->a, wa, p - wb, need, depth + 1);
+        if (p + (uint32_t)need <= wb) return bits(d->b, wb, p, need, depth + 1);
+        const uint32_t sft = wb - p;
+        const std::string lo = bits(d->b, wb, p, (int)sft, depth + 1);
+        const std::string hi = bits(d->a, wa, 0, need - (int)sft, depth + 1);
+        if (hi == "0u") return lo;
+        return "(" + lo + " | (" + hi + " << " + std::to_string(sft) + "))";
+      }
+      if (d->op == K_ZEXT) return bits(d->a, d->p1, p, need, depth + 1);
+      if (d->op == K_EXTRACT) {
+        std::string e = bits(d->a, d->p1, d->p0 + p, need, depth + 1);
+        if (p + 32 > w && e != "0u") e = "(" + e + " & " + hex(topmask(w - p)) + ")";
+        return e;
+      }
+    }
     const uint32_t q = p >> 5, r = p & 31;
     const uint32_t L = Lw(w);
     if (r == 0) return v(id, q);
     std::string lo = "(" + v(id, q) + " >> " + std::to_string(r) + ")";
-    if (q + 1 < L) lo = "(" + lo + " | (" + v(id, q + 1) + " << " + std::to_string(32 - r) + "))";
+    if (q + 1 < L && need > (int)(32 - r)) lo = "(" + lo + " | (" + v(id, q + 1) + " << " + std::to_string(32 - r) + "))";
     return lo;
+  }
+
+  // x <op> c / c <op> x with a literal c that fits in limb 0 (and, for signed
+  // compares, is non-negative): only limb 0 is compared; the upper limbs enter
+  // through one OR-reduction written identically everywhere so LLVM CSEs it
+  // across all compares of the same value (e.g. every `i < calldatasize`).
+  bool emit_small_literal_compare(const Instr& in, uint32_t d, uint32_t wa, uint32_t La, bool sgn) {
+    if (La < 2 || wa <= 32) return false;
+    const uint32_t* la = lit(in.a);
+    const uint32_t* lb = lit(in.b);
+    if ((la == nullptr) == (lb == nullptr)) return false;
+    const uint32_t* c = la ? la : lb;
+    for (uint32_t j = 1; j < La; j++)
+      if (c[j]) return false;
+    const uint32_t x = la ? in.b : in.a;  // the non-literal operand
+    const bool lit_left = la != nullptr;
+    std::string hz = "((0u";
+    for (uint32_t j = 1; j < La; j++) hz += " | " + v(x, j);
+    hz += ") == 0u)";
+    const std::string c0 = hex(c[0]);
+    const std::string neg = "((" + v(x, La - 1) + " >> " + std::to_string((wa - 1) & 31) + ") & 1u)";
+    const bool strict = in.op == K_ULT || in.op == K_SLT;
+    std::string e;
+    if (!lit_left) {
+      // x < c  |  x <= c
+      e = "(" + hz + " && " + v(x, 0) + (strict ? " < " : " <= ") + c0 + ")";
+      if (sgn) e = "(" + neg + " || " + e + ")";
+    } else {
+      // c < x  = !(x <= c)  |  c <= x = !(x < c)
+      e = "!(" + hz + " && " + v(x, 0) + (strict ? " <= " : " < ") + c0 + ")";
+      if (sgn) e = "(!" + neg + " && " + e + ")";
+    }
+    o << "  " << v(d, 0) << " = (uint32_t)(" << e << ");\n";
+    return true;
   }
 
   void mask_top(uint32_t id) {
@@ -241,6 +312,7 @@ struct Gen {
       case K_ULT: case K_ULE: case K_SLT: case K_SLE: {
         const uint32_t wa = in.p1, La = Lw(wa);
         const bool sgn = in.op == K_SLT || in.op == K_SLE;
+        if (emit_small_literal_compare(in, d, wa, La, sgn)) break;
         const std::string flip = sgn ? hex(1u << ((wa - 1) & 31)) : "0u";
         o << "  { uint64_t br = 0, t; uint32_t nz = 0;";
         for (uint32_t j = 0; j < La; j++) {
@@ -394,9 +466,12 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   o << "typedef unsigned int uint32_t;\ntypedef int int32_t;\ntypedef unsigned long long uint64_t;\n"
     << "typedef unsigned char uint8_t;\n";
   o << kPrelude << "\nusing namespace mg;\n";
+  // optional occupancy target (min waves per SIMD) for the search kernel
+  std::string lb = "256";
+  if (const char* wv = getenv("MYTHGPU_JIT_WAVES")) lb += std::string(", ") + std::to_string(atoi(wv));
   if (want_search) {
   // search kernel
-  o << "extern \"C\" __global__ void __launch_bounds__(256) mgj_search(const uint32_t* __restrict__ gconsts, "
+  o << "extern \"C\" __global__ void __launch_bounds__(" << lb << ") mgj_search(const uint32_t* __restrict__ gconsts, "
        "const GenSpec* __restrict__ specs, const uint32_t* __restrict__ cw, uint64_t start, uint64_t count, "
        "uint64_t seed, unsigned long long* hit, uint32_t flags) {\n"
        "  const bool early = (flags & 1u) != 0u;\n"

@@ -28,7 +28,12 @@ __device__ __forceinline__ uint32_t cand_key(uint64_t idx, uint64_t seed) {
 }
 
 __device__ __forceinline__ uint32_t rnd(uint32_t key, uint32_t c, uint32_t j) {
-  return mix32(key + c * 0x9E3779B9u + j * 0x85EBCA6Bu + 0x27D4EB2Fu);
+  /* one-multiply finaliser of the (well mixed) candidate key; see MG_GEN_* in mythgpu.h */
+  uint32_t x = key ^ (c * 0x9E3779B9u + j * 0x85EBCA6Bu + 0x27D4EB2Fu);
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  return x;
 }
 
 // MG_GEN_* kinds (include/mythgpu.h)
@@ -80,12 +85,12 @@ __device__ __forceinline__ void gen_regs(uint32_t (&o)[L], const uint32_t* __res
     case 0xFFu:
       break;
     case G_DICT: {
-      const uint32_t e = (uint32_t)(((uint64_t)rnd(key, cc, 0xFFFEu) * s.p[1]) >> 32);
+      const uint32_t e = (((rnd(key, cc, 0xFFFFu) >> 16) * s.p[1]) >> 16);
       const uint32_t* src = gconsts + s.p[0] + e * Ls;
 #pragma unroll
       for (int j = 0; j < L; j++) o[j] = (uint32_t)j < Lg ? src[j] : 0u;
       if (from_mixed && s.p[5]) {
-        const uint32_t r = rnd(key, cc, 0xFFFDu);
+        const uint32_t r = rnd(key, cc, 0u);
         if ((r & 0xFFFFu) < s.p[5]) {
           const uint32_t mag = ((r >> 16) & 1u) + 1u;
           const bool sub = (r >> 17) & 1u;

@@ -213,6 +213,25 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
       code.push_back(v);
       return code.size() - 1;
     };
+    // index of the single set bit of a literal (power of two), else -1
+    auto pow2_literal = [&](uint32_t off, uint32_t width) -> int {
+      int bit = -1;
+      for (uint32_t j = 0; j < L_of(width); j++) {
+        const uint32_t x = consts[off + j];
+        if (!x) continue;
+        if ((x & (x - 1)) || bit >= 0) return -1;
+        bit = (int)(32 * j + __builtin_ctz(x));
+      }
+      return bit;
+    };
+    // a fresh all-zero literal of the given width (appended to the constant pool)
+    auto zero_literal = [&](uint32_t width) -> uint32_t {
+      const uint32_t off = (uint32_t)out.consts.size();
+      out.consts.insert(out.consts.end(), L_of(width), 0u);
+      uint32_t v = new_vid(width);
+      emit(K_CONST, width, v, NONE, NONE, NONE, off);
+      return v;
+    };
     // literals are rematerialised at every use (a scalar-load K_CONST right before
     // the consumer) instead of occupying value-file words from first to last use
     std::vector<uint32_t> node_const(n_nodes, NONE);
@@ -260,9 +279,50 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
         case MG_OP_ADD: case MG_OP_SUB: case MG_OP_AND: case MG_OP_OR: case MG_OP_XOR:
         case MG_OP_MUL: case MG_OP_UDIV: case MG_OP_UREM: case MG_OP_SDIV: case MG_OP_SREM:
         case MG_OP_SMOD: case MG_OP_SHL: case MG_OP_LSHR: case MG_OP_ASHR: case MG_OP_EXP: {
-          uint32_t a = val(n.a, i), b = val(n.b, i);
           need_same(n.a, n.b);
           if (wid(n.a) != W) fail(MG_E_INVALID, "result width");
+          // Strength reduction by a literal power of two (the rewrite z3's simplifier
+          // applies too; exact for every operand value):
+          //   a udiv 2^k = zext(extract(w-1, k, a)),  a urem 2^k = zext(extract(k-1, 0, a)),
+          //   a * 2^k    = extract(w-k-1, 0, a) ++ 0_k
+          if ((n.op == MG_OP_UDIV || n.op == MG_OP_UREM || n.op == MG_OP_MUL) && node_const[n.b] != NONE) {
+            const int k2 = pow2_literal(node_const[n.b], W);
+            if (k2 >= 0 && (uint32_t)k2 < W) {
+              const uint32_t k = (uint32_t)k2;
+              const uint32_t a = val(n.a, i);
+              if (n.op == MG_OP_UDIV) {
+                if (k == 0) {
+                  vid[i] = a;
+                } else {
+                  uint32_t t = new_vid(W - k);
+                  emit(K_EXTRACT, W - k, t, a, NONE, NONE, k, W);
+                  vid[i] = new_vid(W);
+                  emit(K_ZEXT, W, vid[i], t, NONE, NONE, 0, W - k);
+                }
+              } else if (n.op == MG_OP_UREM) {
+                if (k == 0) {
+                  vid[i] = zero_literal(W);
+                } else {
+                  uint32_t t = new_vid(k);
+                  emit(K_EXTRACT, k, t, a, NONE, NONE, 0, W);
+                  vid[i] = new_vid(W);
+                  emit(K_ZEXT, W, vid[i], t, NONE, NONE, 0, k);
+                }
+              } else {  // MUL
+                if (k == 0) {
+                  vid[i] = a;
+                } else {
+                  uint32_t t = new_vid(W - k);
+                  emit(K_EXTRACT, W - k, t, a, NONE, NONE, 0, W);
+                  uint32_t z = zero_literal(k);
+                  vid[i] = new_vid(W);
+                  emit(K_CONCAT, W, vid[i], t, z, NONE, 0, k);
+                }
+              }
+              break;
+            }
+          }
+          uint32_t a = val(n.a, i), b = val(n.b, i);
           static const uint32_t map[] = {0, 0, K_ADD, K_SUB, K_MUL, K_UDIV, K_UREM, K_SDIV, K_SREM, K_SMOD,
                                          K_AND, K_OR, K_XOR, 0, 0, K_SHL, K_LSHR, K_ASHR};
           uint32_t k = n.op == MG_OP_EXP ? (uint32_t)K_EXP : map[n.op];
@@ -605,6 +665,7 @@ int parse_gen(const Lowered& prog, const uint32_t* blob, size_t n_words, std::ve
       case MG_GEN_DICT:
       case MG_GEN_MIXED:
         if (s.p[1] == 0 && s.kind == MG_GEN_DICT) { err = "empty dictionary"; return MG_E_INVALID; }
+        if (s.p[1] > 65535) { err = "dictionary larger than 65535 entries"; return MG_E_INVALID; }
         if (!in_range(s.p[0], (uint64_t)s.p[1] * L)) { err = "dictionary out of range"; return MG_E_INVALID; }
         if (s.kind == MG_GEN_MIXED && s.p[3] != MG_NONE &&
             (s.p[3] >= nc || prog.coord_width[s.p[3]] != prog.coord_width[c])) {

@@ -7,7 +7,7 @@
  * Used by tests/ (hit counts / first hit must equal the GPU's) and by
  * bench.py's cpu_baseline leg ("port": timed on the host cores with OpenMP).
  * Never linked into the product.  Semantics restated (SMT-LIB QF_ABV, what z3
- * evaluates for mythril/laser/smt/*.py terms):
+ * evaluates for mythril/laser/smt terms):
  *   bvudiv x 0 = ~0, bvurem x 0 = x, bvsdiv/bvsrem/bvsmod by the msb case
  *   split, shifts >= w saturate, bvumul_noovfl = product fits in w bits;
  *   arrays/UFs under a finite model with per-candidate first-occurrence
@@ -186,13 +186,17 @@ static uint32_t cand_key(uint64_t idx, uint64_t seed) {
   return mix32((uint32_t)idx ^ mix32((uint32_t)(idx >> 32) ^ (uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + 0x632BE5ABu)));
 }
 static uint32_t rnd(uint32_t key, uint32_t c, uint32_t j) {
-  return mix32(key + c * 0x9E3779B9u + j * 0x85EBCA6Bu + 0x27D4EB2Fu);
+  /* one-multiply finaliser of the (well mixed) candidate key; see MG_GEN_* in mythgpu.h */
+  uint32_t x = key ^ (c * 0x9E3779B9u + j * 0x85EBCA6Bu + 0x27D4EB2Fu);
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  return x;
 }
 
 static void set_limb32(val_t* v, uint32_t j, uint32_t x) {
   v->w[j / 2] |= (uint64_t)x << (32 * (j % 2));
 }
-static uint32_t get_limb32(const val_t* v, uint32_t j) { return (uint32_t)(v->w[j / 2] >> (32 * (j % 2))); }
 
 static void from_limbs32(val_t* v, const uint32_t* src, uint32_t L) {
   vzero(v);
@@ -245,11 +249,11 @@ static void gen_coord(const prog_t* P, uint32_t c, uint32_t key, val_t* out) {
   switch (s[0]) {
     case 2: { /* DICT */
       uint32_t n = s[2];
-      uint32_t e = (uint32_t)(((uint64_t)rnd(key, cc, 0xFFFEu) * n) >> 32);
+      uint32_t e = (((rnd(key, cc, 0xFFFFu) >> 16) * n) >> 16);
       const uint32_t* src = P->gconsts + s[1] + e * Lsrc;
       for (uint32_t j = 0; j < Lg; j++) limb[j] = src[j];
       if (from_mixed && s[6]) {
-        uint32_t r = rnd(key, cc, 0xFFFDu);
+        uint32_t r = rnd(key, cc, 0u);
         if ((r & 0xFFFFu) < s[6]) {
           uint32_t mag = ((r >> 16) & 1u) + 1u;
           int sub = (r >> 17) & 1u;

@@ -296,3 +296,36 @@ def test_workload_models_verified(engine, name):
     ver, scalars, arrays, funcs, P = res.model
     m = OracleModel(scalars, arrays, funcs)
     assert ver == 1 and all(evaluate(r, m) == 1 for r in roots)
+
+
+def test_power_of_two_strength_reduction(engine):
+    """udiv/urem/mul by a literal 2^k are lowered to extract/zext/concat; exact vs the oracle,
+    in both the interpreter and the JIT kernels."""
+    a = T.BitVecVar("a", 256)
+    terms = []
+    for k in (0, 1, 5, 31, 32, 33, 64, 200, 224, 255):
+        c = T.BitVecVal(1 << k, 256)
+        terms += [T.bvbin("bvudiv", a, c), T.bvbin("bvurem", a, c), T.bvbin("bvmul", a, c)]
+    a8 = T.BitVecVar("a8", 8)
+    terms += [T.bvbin(op, a8, T.BitVecVal(1 << k, 8)) for op in ("bvudiv", "bvurem", "bvmul") for k in (0, 3, 7)]
+    rng = random.Random(11)
+    assigns = [[rng.getrandbits(256), rng.getrandbits(8)] for _ in range(200)] + [[(1 << 256) - 1, 255], [0, 0]]
+    P, _, ver, got, models = gpu_eval_terms(engine, [T.BoolVal(True)], terms, assigns)
+    for i, (x, y) in enumerate(assigns):
+        want = evaluate_many(terms, OracleModel({"a": x, "a8": y}))
+        for t, w in zip(terms, want):
+            assert got[i][t.id] == w, (t.op, T.to_sexpr(t.args[1]), hex(x))
+    # the JIT path on the same program
+    P2 = ssa.flatten([T.BoolVal(True)], extra=terms)
+    P2.set_watch([P2.term_node[t.id] for t in terms])
+    soa = ssa.soa_from_assignments(P2, assigns)
+    prog = engine.load(P2.to_bytes())
+    try:
+        info = engine.info(prog)
+        vi, wi = engine.eval(prog, soa, len(assigns), watch_words=info.watch_words)
+        jit = engine.jit_compile(prog, 0)
+        vj, wj = engine.jit_eval(jit, soa, len(assigns), watch_words=info.watch_words)
+        engine.jit_free(jit)
+    finally:
+        engine.free(prog)
+    assert (wi == wj).all()
