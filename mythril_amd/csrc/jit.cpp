@@ -468,7 +468,8 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   o << kPrelude << "\nusing namespace mg;\n";
   // optional occupancy target (min waves per SIMD) for the search kernel
   std::string lb = "256";
-  if (const char* wv = getenv("MYTHGPU_JIT_WAVES")) lb += std::string(", ") + std::to_string(atoi(wv));
+  if (const char* wv = getenv("MYTHGPU_JIT_WAVES"))
+    if (atoi(wv) > 0) lb += std::string(", ") + std::to_string(atoi(wv));
   if (want_search) {
   // search kernel
   o << "extern \"C\" __global__ void __launch_bounds__(" << lb << ") mgj_search(const uint32_t* __restrict__ gconsts, "
