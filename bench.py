@@ -74,7 +74,7 @@ def main():
     cs = workloads.WORKLOADS[args.workload]()
     roots = [c.raw for c in cs]
     P = ssa.flatten(roots)
-    gen = search.default_generator(P)
+    gen = search.default_generator(P, roots=roots)
     blob = gen.blob()
     prog = eng.load(P.to_bytes())
     info = eng.info(prog)

@@ -145,6 +145,12 @@ enum mg_gen_kind {
   MG_GEN_LAZY = 6      /* site coords only: p0 = node whose value is the default (must precede the site) */
 };
 
+/* spec.kind bits 8..31: 0, or 1 + the const offset of a fixed-bit record
+ * {mask limbs[L], value limbs[L]} (L = limbs of the coordinate) applied after
+ * generation: v = (v & ~mask) | value.  When MIXED copies another coordinate, the
+ * source's record is applied to the copy first. */
+#define MG_GEN_KIND(kind) ((kind) & 0xFFu)
+
 /* search flags */
 #define MG_SEARCH_EARLY_EXIT 1u   /* stop lanes past the current first hit; skip waves whose roots all failed */
 

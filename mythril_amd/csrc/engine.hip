@@ -113,6 +113,9 @@ __device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c
   const uint32_t L = (width + 31) >> 5;
   uint32_t cc = c;  // coordinate whose spec/randomness is used
   GenSpec s = k.specs[c];
+  const uint32_t fix_dst = s.kind >> 8;  // 1 + const offset of a (mask, value) fix, 0: none
+  uint32_t fix_src = 0;
+  s.kind &= 0xFFu;
   uint32_t Lg = L;  // limbs to generate
   bool allow_copy = true;
   for (int level = 0; level < 2; level++) {
@@ -124,6 +127,8 @@ __device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c
     if (sel < pc) {
       cc = s.p[3];
       s = k.specs[cc];
+      fix_src = s.kind >> 8;
+      s.kind &= 0xFFu;
       Lg = min(L, (k.coord_width[cc] + 31) >> 5);
       allow_copy = false;
       continue;  // re-decide with the source's spec
@@ -139,8 +144,7 @@ __device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c
         v = lo >= bits ? 0u : (bits - lo >= 32 ? v : (v & ((1u << (bits - lo)) - 1u)));
         vf.at(dst + j) = v;
       }
-      write_masked(vf, dst, L, width);
-      return;
+      s.kind = 0xFFu;  // value complete
     } else {
       s.kind = MG_GEN_UNIFORM;
     }
@@ -151,6 +155,8 @@ __device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c
                           ? ((k.coord_width[cc] + 31) >> 5)
                           : Lg;  // limb stride of the source's constants
   switch (s.kind) {
+    case 0xFFu:
+      break;
     case MG_GEN_DICT: {
       const uint32_t n = s.p[1];
       const uint32_t e = (((rnd(key, cc, 0xFFFFu) >> 16) * n) >> 16);
@@ -213,6 +219,16 @@ __device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c
   }
   for (uint32_t j = Lg; j < L; j++) vf.at(dst + j) = 0;
   write_masked(vf, dst, L, width);
+  // fixed bits: v = (v & ~mask) | value — the copied source's fix first, then this coordinate's
+  if (cc != c && fix_src) {
+    const uint32_t* f = k.gconsts + (fix_src - 1);
+    const uint32_t Ls = (k.coord_width[cc] + 31) >> 5;
+    for (uint32_t j = 0; j < Lg; j++) vf.at(dst + j) = (vf.at(dst + j) & ~f[j]) | f[Ls + j];
+  }
+  if (fix_dst) {
+    const uint32_t* f = k.gconsts + (fix_dst - 1);
+    for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = (vf.at(dst + j) & ~f[j]) | f[L + j];
+  }
 }
 
 // ---------------------------------------------------------------------------

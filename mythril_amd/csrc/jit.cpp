@@ -47,7 +47,9 @@ struct Gen {
   // keeps a tiny CFG (hipRTC compile time is dominated by register coalescing
   // over basic blocks otherwise).  Writes limbs into `out` names.
   void gen_value(uint32_t c, uint32_t width, const std::string& out, bool allow_copy, int depth) {
-    const GenSpec& sp = (*specs)[c];
+    GenSpec sp = (*specs)[c];
+    const uint32_t fix = sp.kind >> 8;  // 1 + const offset of (mask, value) limbs, 0: none
+    sp.kind &= 0xFFu;
     const uint32_t L = Lw(width);
     const uint32_t Lc = Lw(P.coord_width[c]);  // limb stride of this coordinate's constants
     const uint32_t Lg = std::min(L, Lc);
@@ -152,6 +154,15 @@ struct Gen {
         break;
     }
     if (width & 31) o << "  " << lim(out, L - 1) << " &= " << hex(topmask(width)) << ";\n";
+    if (fix) {
+      // fixed bits are literals here: (v & ~mask) | value
+      const uint32_t f = fix - 1, Lf = Lw(P.coord_width[c]);
+      for (uint32_t j = 0; j < L && j < Lf; j++) {
+        const uint32_t m = (*gconsts)[f + j], val = (*gconsts)[f + Lf + j];
+        if (m == 0xFFFFFFFFu) o << "  " << lim(out, j) << " = " << hex(val) << ";\n";
+        else if (m) o << "  " << lim(out, j) << " = (" << lim(out, j) << " & " << hex(~m) << ") | " << hex(val) << ";\n";
+      }
+    }
     o << "  }\n";
   }
 

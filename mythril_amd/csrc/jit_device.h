@@ -45,6 +45,9 @@ __device__ __forceinline__ void gen_regs(uint32_t (&o)[L], const uint32_t* __res
                                          uint32_t c, uint32_t width, uint32_t key) {
   uint32_t cc = c;
   GenSpec s = specs[c];
+  const uint32_t fix_dst = s.kind >> 8;
+  uint32_t fix_src = 0;
+  s.kind &= 0xFFu;
   uint32_t Lg = L;
   bool allow_copy = true;
   bool from_mixed = false;
@@ -58,6 +61,8 @@ __device__ __forceinline__ void gen_regs(uint32_t (&o)[L], const uint32_t* __res
     if (sel < pc) {
       cc = s.p[3];
       s = specs[cc];
+      fix_src = s.kind >> 8;
+      s.kind &= 0xFFu;
       const uint32_t Ls = (cw[cc] + 31) >> 5;
       Lg = Ls < (uint32_t)L ? Ls : (uint32_t)L;
       allow_copy = false;
@@ -160,6 +165,17 @@ __device__ __forceinline__ void gen_regs(uint32_t (&o)[L], const uint32_t* __res
   }
   const uint32_t r = width & 31u;
   if (r) o[L - 1] &= (1u << r) - 1u;
+  if (cc != c && fix_src) {
+    const uint32_t* f = gconsts + (fix_src - 1);
+#pragma unroll
+    for (int j = 0; j < L; j++)
+      if ((uint32_t)j < Lg) o[j] = (o[j] & ~f[j]) | f[Ls + j];
+  }
+  if (fix_dst) {
+    const uint32_t* f = gconsts + (fix_dst - 1);
+#pragma unroll
+    for (int j = 0; j < L; j++) o[j] = (o[j] & ~f[j]) | f[L + j];
+  }
 }
 
 // Keccak-256 of the LEN big-endian bytes of an L-limb value (LEN >= 1)

@@ -652,7 +652,12 @@ int parse_gen(const Lowered& prog, const uint32_t* blob, size_t n_words, std::ve
     const GenSpec& s = specs[c];
     const uint32_t L = L_of(prog.coord_width[c]);
     auto in_range = [&](uint64_t off, uint64_t n) { return off + n <= ncw; };
-    switch (s.kind) {
+    const uint32_t fix = s.kind >> 8;
+    if (fix && !in_range(fix - 1, 2ull * L)) {
+      err = "fixed-bit record out of range";
+      return MG_E_INVALID;
+    }
+    switch (s.kind & 0xFFu) {
       case MG_GEN_UNIFORM:
         break;
       case MG_GEN_RANGE:
@@ -664,10 +669,10 @@ int parse_gen(const Lowered& prog, const uint32_t* blob, size_t n_words, std::ve
         break;
       case MG_GEN_DICT:
       case MG_GEN_MIXED:
-        if (s.p[1] == 0 && s.kind == MG_GEN_DICT) { err = "empty dictionary"; return MG_E_INVALID; }
+        if (s.p[1] == 0 && (s.kind & 0xFFu) == MG_GEN_DICT) { err = "empty dictionary"; return MG_E_INVALID; }
         if (s.p[1] > 65535) { err = "dictionary larger than 65535 entries"; return MG_E_INVALID; }
         if (!in_range(s.p[0], (uint64_t)s.p[1] * L)) { err = "dictionary out of range"; return MG_E_INVALID; }
-        if (s.kind == MG_GEN_MIXED && s.p[3] != MG_NONE &&
+        if ((s.kind & 0xFFu) == MG_GEN_MIXED && s.p[3] != MG_NONE &&
             (s.p[3] >= nc || prog.coord_width[s.p[3]] != prog.coord_width[c])) {
           err = "copy source must be a coordinate of the same width";
           return MG_E_INVALID;

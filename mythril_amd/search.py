@@ -89,6 +89,17 @@ class GenBuilder:
             ((small_bits & 0xFFFF) << 16) | (int(p_small * P16) & 0xFFFF),
         ]
 
+    def fix(self, c: int, mask: int, value: int):
+        """Fixed bits applied after generation: v = (v & ~mask) | value (call last)."""
+        w = self.P.coords[c].width
+        mask &= (1 << w) - 1
+        if not mask:
+            return
+        off = len(self.consts)
+        self.consts.extend(ssa.int_to_limbs(mask, w))
+        self.consts.extend(ssa.int_to_limbs(value & mask, w))
+        self.specs[c][0] = (self.specs[c][0] & 0xFF) | ((off + 1) << 8)
+
     def blob(self) -> np.ndarray:
         words = [GEN_MAGIC, len(self.specs), len(self.consts), 0]
         for s in self.specs:
@@ -117,7 +128,13 @@ def _interval_bounds(P: ssa.Program):
     return out
 
 
-def default_generator(P: ssa.Program, extra_dict: Sequence[int] = ()) -> GenBuilder:
+def default_generator(P: ssa.Program, extra_dict: Sequence[int] = (), roots: Optional[Sequence[T.Term]] = None
+                      ) -> GenBuilder:
+    """Per-coordinate generator specs.  With ``roots`` the propagation pass
+    (``propagate.py``) first shapes each coordinate's domain."""
+    from .propagate import propagate
+
+    doms = propagate(P, roots) if roots is not None else {}
     g = GenBuilder(P)
     by_width: Dict[int, set] = {}
     for v, w in P.const_values:
@@ -126,10 +143,15 @@ def default_generator(P: ssa.Program, extra_dict: Sequence[int] = ()) -> GenBuil
     last_of_width: Dict[int, int] = {}
     for c in P.coords:
         w = c.width
+        mask = (1 << w) - 1
         if c.kind == ssa.COORD_UF_SITE and P.nodes[c.node][7] != NONE:
             g.lazy(c.index)
             continue
-        if c.kind == ssa.COORD_UF_SITE and c.index in bounds and None not in bounds[c.index]:
+        dom = doms.get(c.index)
+        if dom is not None and _apply_domain(g, P, c.index, dom):
+            last_of_width[w] = c.index
+            continue
+        if dom is None and c.kind == ssa.COORD_UF_SITE and c.index in bounds and None not in bounds[c.index]:
             lo, hi = bounds[c.index]
             lo = (lo + 63) // 64 * 64
             if hi > lo:
@@ -139,20 +161,60 @@ def default_generator(P: ssa.Program, extra_dict: Sequence[int] = ()) -> GenBuil
             g.uniform(c.index)
             last_of_width[w] = c.index
             continue
-        vals = set(by_width.get(w, ()))
-        mask = (1 << w) - 1
-        vals |= {0, 1, mask}
+        vals = set(by_width.get(w, ())) | {0, 1, mask}
         for a in list(ACTORS) + list(extra_dict):
             vals.add(a & mask)
-        for v in list(vals):
-            if v and v < mask:
-                pass
+        small_bits, p_small = min(w, 8), 0.20
+        if dom is not None:
+            # a huge interval is only a hint: keep the broad draw, steer the dictionary
+            if dom.intervals:
+                for a_, b_ in dom.intervals[:4]:
+                    vals |= {a_, (a_ + 1) & mask, b_, (b_ - 1) & mask}
+            vals = {v for v in vals if dom.admissible(v)} or vals
         vals = sorted(vals)[:4096]
         copy = last_of_width.get(w)
         g.mixed(c.index, vals, p_dict=0.45, copy_from=copy, p_copy=0.10 if copy is not None else 0.0,
-                p_delta=0.25, small_bits=min(w, 8), p_small=0.20)
+                p_delta=0.25, small_bits=small_bits, p_small=p_small)
+        if dom is not None and dom.fmask:
+            g.fix(c.index, dom.fmask, dom.fval)
         last_of_width[w] = c.index
     return g
+
+
+def _apply_domain(g: GenBuilder, P: ssa.Program, c: int, dom) -> bool:
+    """Give coordinate c a spec drawn from its propagated domain when the domain is
+    narrow enough to enumerate; False leaves it to the broad default draw."""
+    w = P.coords[c].width
+    full = (1 << w) - 1
+    if dom.choices:
+        ok = [v for v in dom.choices if dom.admissible(v)]
+        if ok:
+            g.dict(c, ok)
+            return True
+    if dom.fmask == full:
+        g.fixed(c, dom.fval)
+        return True
+    if dom.intervals:
+        a, b = dom.intervals[0]
+        # low zero bits fixed (keccak outputs: URem(f(x), 64) == 0) -> aligned sweep
+        k = 0
+        while k < w and (dom.fmask >> k) & 1 and not (dom.fval >> k) & 1:
+            k += 1
+        if k:
+            lo = (a + (1 << k) - 1) >> k << k
+            if lo <= b:
+                g.aligned(c, lo, k, min(((b - lo) >> k) + 1, 1 << 32) % (1 << 32))
+                rest = dom.fmask & ~((1 << k) - 1)
+                if rest:
+                    g.fix(c, rest, dom.fval)
+                return True
+        span = sum(y - x + 1 for x, y in dom.intervals)
+        if span < (1 << 32) and len(dom.intervals) == 1:
+            g.range(c, a, span)
+            if dom.fmask:
+                g.fix(c, dom.fmask, dom.fval)
+            return True
+    return False
 
 
 class SearchResult:
@@ -216,7 +278,7 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
            want_model: bool = True) -> SearchResult:
     """Find the lowest-index satisfying candidate (or give up: None)."""
     P = ssa.flatten(roots)
-    g = gen or default_generator(P)
+    g = gen or default_generator(P, roots=roots)
     blob = g.blob()
     prog = engine.load(P.to_bytes())
     t0 = time.perf_counter()

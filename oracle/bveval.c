@@ -209,8 +209,11 @@ static void gen_coord(const prog_t* P, uint32_t c, uint32_t key, val_t* out) {
   uint32_t cc = c;
   uint32_t s[8];
   memcpy(s, P->specs + 8 * c, 32);
+  const uint32_t fix_dst = s[0] >> 8; /* 1 + const offset of a (mask, value) fix */
+  uint32_t fix_src = 0;
+  s[0] &= 0xFFu;
   uint32_t Lg = L;
-  int allow_copy = 1, from_mixed = 0;
+  int allow_copy = 1, from_mixed = 0, done = 0;
   vzero(out);
   for (int level = 0; level < 2; level++) {
     if (s[0] != 3) break;
@@ -221,6 +224,8 @@ static void gen_coord(const prog_t* P, uint32_t c, uint32_t key, val_t* out) {
     if (sel < pc) {
       cc = s[4];
       memcpy(s, P->specs + 8 * cc, 32);
+      fix_src = s[0] >> 8;
+      s[0] &= 0xFFu;
       uint32_t Ls = (P->coords[4 * cc] + 31) / 32;
       Lg = Ls < L ? Ls : L;
       allow_copy = 0;
@@ -237,7 +242,7 @@ static void gen_coord(const prog_t* P, uint32_t c, uint32_t key, val_t* out) {
         set_limb32(out, j, v);
       }
       vmask(out, width);
-      return;
+      done = 1;
     } else {
       s[0] = 0;
     }
@@ -245,6 +250,7 @@ static void gen_coord(const prog_t* P, uint32_t c, uint32_t key, val_t* out) {
   }
   const uint32_t Lsrc = (P->coords[4 * cc] + 31) / 32;
   uint32_t limb[64];
+  if (done) goto fixes;
   memset(limb, 0, sizeof(limb));
   switch (s[0]) {
     case 2: { /* DICT */
@@ -304,6 +310,24 @@ static void gen_coord(const prog_t* P, uint32_t c, uint32_t key, val_t* out) {
   }
   from_limbs32(out, limb, Lg);
   vmask(out, width);
+fixes:
+  /* fixed bits (v & ~mask) | value: the copied source's fix, then this coordinate's */
+  if (cc != c && fix_src) {
+    const uint32_t* f = P->gconsts + (fix_src - 1);
+    for (uint32_t j = 0; j < Lg; j++) {
+      uint32_t x = (uint32_t)(out->w[j / 2] >> (32 * (j % 2)));
+      x = (x & ~f[j]) | f[Lsrc + j];
+      out->w[j / 2] = (out->w[j / 2] & ~(0xFFFFFFFFull << (32 * (j % 2)))) | ((uint64_t)x << (32 * (j % 2)));
+    }
+  }
+  if (fix_dst) {
+    const uint32_t* f = P->gconsts + (fix_dst - 1);
+    for (uint32_t j = 0; j < L; j++) {
+      uint32_t x = (uint32_t)(out->w[j / 2] >> (32 * (j % 2)));
+      x = (x & ~f[j]) | f[L + j];
+      out->w[j / 2] = (out->w[j / 2] & ~(0xFFFFFFFFull << (32 * (j % 2)))) | ((uint64_t)x << (32 * (j % 2)));
+    }
+  }
 }
 
 /* ---- evaluation ---- */
