@@ -125,6 +125,8 @@ def _fold(t: T.Term, memo) -> T.Term:
             res = args[1] if vals[0] else args[2]
     elif t.op == "ite" and T.const_value(args[0]) is not None:
         res = args[1] if T.const_value(args[0]) else args[2]
+    elif t.op == "eq" and args[0] is args[1]:
+        res = T.BoolVal(True)  # hash-consed: structurally equal (z3 simplify does the same)
     if res is None:
         res = t if args == t.args else T.mk(t.op, t.sort, args, t.params)
     memo[t.id] = res

@@ -1,0 +1,180 @@
+"""The solver mirror on the GPU, written after the reference's own tests:
+tests/laser/smt/model_test.py, tests/laser/state/calldata_test.py,
+tests/laser/keccak_tests.py.  Verdict mapping: where the reference expects
+``sat`` the engine must return a model the oracle verifies; where it expects
+``unsat`` the engine must never return a model the oracle rejects (the engine
+answers ``unknown``, which get_model turns into UnsatError exactly like z3's
+unsat/unknown)."""
+import pytest
+
+from mythril_amd import solver
+from mythril_amd.keccak_model import KeccakFunctionManager
+from mythril_amd.smt import And, Array, If, symbol_factory
+from mythril_amd.solver import Solver, sat, unknown
+from oracle.bv import OracleModel, evaluate
+
+pytestmark = pytest.mark.gpu
+BVV = symbol_factory.BitVecVal
+BVS = symbol_factory.BitVecSym
+
+
+def _verified(s: Solver):
+    m = s.model()
+    om = OracleModel(m.scalars, m.arrays, m.funcs)
+    return all(evaluate(c, om) == 1 for c in s.constraints)
+
+
+def _check(s: Solver, expected):
+    r = s.check()
+    if expected is sat:
+        assert r == sat and _verified(s)
+    elif r == sat:
+        assert _verified(s), "engine returned a model the oracle rejects"
+    return r
+
+
+# -- tests/laser/smt/model_test.py -------------------------------------------
+def test_decls(engine):
+    s = Solver()
+    x = BVS("x", 256)
+    s.add(x == BVV(2, 256))
+    assert s.check() == sat
+    assert "x" in s.model().decls()
+
+
+def test_get_item(engine):
+    s = Solver()
+    x = BVS("x", 256)
+    s.add(x == BVV(2, 256))
+    assert s.check() == sat
+    assert s.model()[x.raw] == 2
+
+
+def test_as_long(engine):
+    s = Solver()
+    x = BVS("x", 256)
+    s.add(x == BVV(2, 256))
+    assert s.check() == sat
+    assert s.model().eval(x.raw).as_long() == 2
+
+
+def test_model_eval_on_gpu_with_arrays(engine):
+    s = Solver()
+    x = BVS("x", 256)
+    st = Array("Storage", 256, 256)
+    s.add(st[x] == BVV(7, 256), x == BVV(3, 256))
+    assert s.check() == sat and _verified(s)
+    m = s.model()
+    assert m.eval((st[x] + 1).raw, model_completion=True).as_long() == 8
+    assert m.eval(st[BVV(3, 256)].raw, model_completion=True).as_long() == 7
+
+
+# -- tests/laser/state/calldata_test.py --------------------------------------
+def _load(tx_calldata, size, item):
+    return If(item < size, tx_calldata[item], BVV(0, 8))  # calldata.py:217-231
+
+
+def test_symbolic_calldata_constrain_index(engine):
+    cd, size = Array("0_calldata", 256, 8), BVS("0_calldatasize", 256)
+    s = Solver()
+    s.set_timeout(500)
+    s.add(_load(cd, size, BVV(51, 256)) == BVV(1, 8), size == BVV(50, 256))
+    assert _check(s, "unsat") == unknown
+
+
+def test_symbolic_calldata_equal_indices(engine):
+    cd, size = Array("0_calldata", 256, 8), BVS("0_calldatasize", 256)
+    ia, ib = BVS("index_a", 256), BVS("index_b", 256)
+    s = Solver()
+    s.set_timeout(500)
+    s.append(ia == ib)
+    s.append(_load(cd, size, ia) != _load(cd, size, ib))
+    assert _check(s, "unsat") == unknown
+
+
+def test_symbolic_calldata_sat_read(engine):
+    cd, size = Array("0_calldata", 256, 8), BVS("0_calldatasize", 256)
+    s = Solver()
+    s.add(_load(cd, size, BVV(3, 256)) == BVV(0xAB, 8), size == BVV(7, 256))
+    _check(s, sat)
+    assert s.model().eval(size.raw).as_long() == 7
+
+
+# -- tests/laser/keccak_tests.py ---------------------------------------------
+@pytest.mark.parametrize(
+    "in1, in2, expected",
+    [
+        (lambda: BVV(100, 8), lambda: BVV(101, 8), "unsat"),
+        (lambda: BVV(100, 8), lambda: BVV(100, 16), "unsat"),
+        (lambda: BVV(100, 8), lambda: BVV(100, 8), sat),
+        (lambda: BVS("N1", 256), lambda: BVS("N2", 256), sat),
+        (lambda: BVV(100, 256), lambda: BVS("N1", 256), sat),
+        (lambda: BVV(100, 8), lambda: BVS("N1", 256), "unsat"),
+    ],
+)
+def test_keccak_basic(engine, in1, in2, expected):
+    km = KeccakFunctionManager()
+    s = Solver()
+    s.set_timeout(2000)
+    o1, c1 = km.create_keccak(in1())
+    o2, c2 = km.create_keccak(in2())
+    s.add(And(c1, c2))
+    s.add(o1 == o2)
+    _check(s, expected)
+
+
+def test_keccak_symbol_and_val(engine):
+    km = KeccakFunctionManager()
+    s = Solver()
+    s.set_timeout(500)
+    hundred, n = BVV(100, 256), BVS("n", 256)
+    o1, c1 = km.create_keccak(hundred)
+    o2, c2 = km.create_keccak(n)
+    s.add(And(c1, c2), o1 == o2, n == BVV(10, 256))
+    assert _check(s, "unsat") == unknown
+
+
+def test_keccak_complex_eq2(engine):
+    km = KeccakFunctionManager()
+    s = Solver()
+    s.set_timeout(5000)
+    a, b = BVS("a", 160), BVS("b", 160)
+    o1, c1 = km.create_keccak(a)
+    o2, c2 = km.create_keccak(b)
+    s.add(And(c1, c2))
+    two = BVV(2, 256)
+    o1, c1 = km.create_keccak(two * o1)
+    o2, c2 = km.create_keccak(two * o2)
+    s.add(And(c1, c2), o1 == o2)
+    _check(s, sat)
+
+
+def test_keccak_simple_number(engine):
+    km = KeccakFunctionManager()
+    s = Solver()
+    s.set_timeout(500)
+    a = BVS("a", 160)
+    o, c = km.create_keccak(a)
+    s.add(c, BVV(10, 256) == o)
+    assert _check(s, "unsat") == unknown
+
+
+def test_keccak_other_num(engine):
+    km = KeccakFunctionManager()
+    s = Solver()
+    s.set_timeout(5000)
+    a, b = BVS("a", 160), BVS("b", 256)
+    o, c = km.create_keccak(a)
+    s.add(c)
+    o, c = km.create_keccak(BVV(2, 256) * o)
+    s.add(c, b == o)
+    _check(s, sat)
+
+
+# -- support/model.py get_model contract ---------------------------------------
+def test_get_model_contract(engine):
+    x = BVS("x", 256)
+    m = solver.get_model((x == BVV(5, 256), x != BVV(6, 256)))
+    assert m.eval(x.raw).as_long() == 5
+    with pytest.raises(solver.UnsatError):
+        solver.get_model((x == BVV(5, 256), x == BVV(6, 256)), enforce_execution_time=False)
