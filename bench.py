@@ -86,17 +86,16 @@ def main():
         jit = eng.jit_compile(prog, gh)
         compile_ms = eng.jit_info(jit)[0]
 
-    hit_t = torch.full((1,), (1 << 63) - 1, dtype=torch.int64, device="cuda")
+    from mythril_amd.distributed import chunk_start, first_hit_allreduce
 
     def step(s):
-        start = (s * world + rank) * C
+        start = chunk_start(s, rank, world, C)
         if jit is not None:
             idx, nh = eng.jit_search(jit, args.seed, start, C, early_exit=False)
         else:
             idx, nh = eng.search(prog, gh, args.seed, start, C, early_exit=False)
-        if distributed:
-            hit_t.fill_(idx if idx is not None else (1 << 63) - 1)
-            dist.all_reduce(hit_t, op=dist.ReduceOp.MIN)
+        if distributed:  # the path's one exchange step: all-reduce(MIN) of the first hit over RCCL
+            idx = first_hit_allreduce(idx, device="cuda")
         return idx, nh
 
     for s in range(args.warmup):
