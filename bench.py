@@ -57,7 +57,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    distributed = world > 1
+    # launched by torch.distributed.run (even at one rank): use the RCCL exchange path
+    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
     torch.cuda.set_device(local_rank)
     if distributed:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))

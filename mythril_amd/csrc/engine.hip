@@ -526,6 +526,7 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
   const uint64_t total = k.count;
   const uint64_t step = (uint64_t)gridDim.x * kWave;
   const bool early = (MODE == MODE_SEARCH) && (k.flags & MG_SEARCH_EARLY_EXIT);
+  uint64_t wave_best = ~0ull, wave_hits = 0;  // wave-uniform; published once per wave
   for (uint64_t base = (uint64_t)blockIdx.x * kWave; base < total; base += step) {
     const uint64_t i_raw = base + threadIdx.x;
     const bool active = i_raw < total;
@@ -545,14 +546,20 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
     if (MODE == MODE_SEARCH) {
       const unsigned long long m = __ballot(v != 0);
       if (m) {
-        if (threadIdx.x == (unsigned)__ffsll((long long)m) - 1) {
-          atomicMin(k.first_hit, (unsigned long long)idx);
-          atomicAdd(k.hits, (unsigned long long)__popcll(m));
+        const uint64_t first = k.start + base + (uint64_t)(__ffsll((long long)m) - 1);
+        wave_hits += (uint64_t)__popcll(m);
+        if (first < wave_best) {
+          wave_best = first;
+          if (early && threadIdx.x == 0) atomicMin(k.first_hit, (unsigned long long)first);
         }
       }
     } else if (active) {
       k.verdict[i] = (uint8_t)v;
     }
+  }
+  if (MODE == MODE_SEARCH && threadIdx.x == 0) {
+    if (wave_best != ~0ull) atomicMin(k.first_hit, (unsigned long long)wave_best);
+    if (wave_hits) atomicAdd(k.hits, (unsigned long long)wave_hits);
   }
 }
 

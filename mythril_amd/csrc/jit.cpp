@@ -489,6 +489,7 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  const bool early = (flags & 1u) != 0u;\n"
        "  const uint32_t lane = threadIdx.x & 63u;\n"
        "  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;\n"
+       "  uint64_t wave_best = ~0ull, wave_hits = 0;  // per-wave, wave-uniform\n"
        "  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < count; base += stride) {\n"
        "  if (early) {\n"
        "    const unsigned long long cur = __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
@@ -506,10 +507,19 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   o << "  mg_next:\n"
        "  verdict = active ? verdict : 0u;\n"
        "  { const unsigned long long m = __ballot(verdict != 0u);\n"
-       "    if (m && lane == (uint32_t)(__ffsll((long long)m) - 1)) {\n"
-       "      atomicMin(hit, (unsigned long long)idx);\n"
-       "      atomicAdd(hit + 1, (unsigned long long)__popcll(m));\n"
+       "    if (m) {\n"
+       "      const uint64_t first = start + base + (uint64_t)(__ffsll((long long)m) - 1);\n"
+       "      wave_hits += (uint64_t)__popcll(m);\n"
+       "      if (first < wave_best) {\n"
+       "        wave_best = first;\n"
+       "        // publish at once when waves stop early on it; else once per wave at the end\n"
+       "        if (early && lane == 0u) atomicMin(hit, (unsigned long long)first);\n"
+       "      }\n"
        "    } }\n"
+       "  }\n"
+       "  if (lane == 0u) {\n"
+       "    if (wave_best != ~0ull) atomicMin(hit, (unsigned long long)wave_best);\n"
+       "    if (wave_hits) atomicAdd(hit + 1, (unsigned long long)wave_hits);\n"
        "  }\n}\n\n";
   }
   if (want_eval) {
