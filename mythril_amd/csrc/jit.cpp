@@ -604,6 +604,18 @@ int jit_compile(const std::string& src, std::vector<char>& code, std::string& lo
   code.resize(cs);
   r.code(prog, code.data());
   r.destroy(&prog);
+  // MYTHGPU_JIT_DUMP=<prefix>: keep the source and code object for offline disassembly
+  if (const char* dump = getenv("MYTHGPU_JIT_DUMP")) {
+    const std::string base(dump);
+    if (FILE* f = fopen((base + ".hip").c_str(), "wb")) {
+      fwrite(src.data(), 1, src.size(), f);
+      fclose(f);
+    }
+    if (FILE* f = fopen((base + ".co").c_str(), "wb")) {
+      fwrite(code.data(), 1, code.size(), f);
+      fclose(f);
+    }
+  }
   return MG_OK;
 }
 

@@ -172,9 +172,9 @@ def default_generator(P: ssa.Program, extra_dict: Sequence[int] = (), roots: Opt
                     vals |= {a_, (a_ + 1) & mask, b_, (b_ - 1) & mask}
             vals = {v for v in vals if dom.admissible(v)} or vals
         vals = sorted(vals)[:4096]
-        copy = last_of_width.get(w)
+        copy = last_of_width.get(w) if w >= 32 else None
         g.mixed(c.index, vals, p_dict=0.45, copy_from=copy, p_copy=0.10 if copy is not None else 0.0,
-                p_delta=0.25, small_bits=small_bits, p_small=p_small)
+                p_delta=0.25 if w > 8 else 0.0, small_bits=small_bits, p_small=p_small)
         if dom is not None and dom.fmask:
             g.fix(c.index, dom.fmask, dom.fval)
         last_of_width[w] = c.index
