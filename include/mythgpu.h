@@ -131,8 +131,11 @@ enum mg_table_kind { MG_TABLE_ARRAY = 0, MG_TABLE_UF = 1 };
  *   uniform limb j = rnd(c, j); selector h = rnd(c, 0xFFFF): MIXED branch = h & 0xFFFF,
  *   dictionary entry = ((h >> 16) * n) >> 16 (n <= 65535); the +/- delta of a
  *   MIXED dictionary draw reads its bits from rnd(c, 0) (unused by that branch).
+ *   Narrow coordinates (width <= MG_GEN_NARROW_BITS) under MIXED take their
+ *   uniform and small values from h >> 16 instead of rnd(c, 0): one hash each.
  */
 #define MG_GEN_MAGIC 0x314E4547u /* "GEN1" */
+#define MG_GEN_NARROW_BITS 16u
 enum mg_gen_kind {
   MG_GEN_UNIFORM = 0,  /* uniform over [0, 2^w) */
   MG_GEN_RANGE = 1,    /* p0 = const offset of lo, p1 = span (0 => 2^32): lo + r mod span */

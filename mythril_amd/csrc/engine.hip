@@ -120,7 +120,10 @@ __device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c
   bool allow_copy = true;
   for (int level = 0; level < 2; level++) {
     if (s.kind != MG_GEN_MIXED) break;
-    const uint32_t sel = rnd(key, cc, 0xFFFFu) & 0xFFFFu;
+    const uint32_t h = rnd(key, cc, 0xFFFFu);
+    const uint32_t sel = h & 0xFFFFu;
+    // narrow coordinates (<= 16 bits) draw their uniform / small value from h >> 16
+    const bool narrow = k.coord_width[cc] <= MG_GEN_NARROW_BITS;
     const uint32_t pc = (allow_copy && s.p[3] != MG_NONE) ? s.p[4] : 0u;
     const uint32_t pd = s.p[1] ? s.p[2] : 0u;
     const uint32_t ps = s.p[6] & 0xFFFFu;
@@ -139,11 +142,14 @@ __device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c
     } else if (sel < pc + pd + ps) {
       const uint32_t bits = min(width, s.p[6] >> 16);
       for (uint32_t j = 0; j < L; j++) {
-        uint32_t v = rnd(key, cc, j);
+        uint32_t v = narrow ? (j == 0 ? h >> 16 : 0u) : rnd(key, cc, j);
         const uint32_t lo = j * 32;
         v = lo >= bits ? 0u : (bits - lo >= 32 ? v : (v & ((1u << (bits - lo)) - 1u)));
         vf.at(dst + j) = v;
       }
+      s.kind = 0xFFu;  // value complete
+    } else if (narrow) {
+      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = j == 0 ? h >> 16 : 0u;
       s.kind = 0xFFu;  // value complete
     } else {
       s.kind = MG_GEN_UNIFORM;
@@ -217,6 +223,8 @@ __device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c
       break;
     }
   }
+  // a copy is the source's value: masked to the source width, then truncated / zero-extended
+  if (cc != c && Lg == ((k.coord_width[cc] + 31) >> 5)) vf.at(dst + Lg - 1) &= top_mask(k.coord_width[cc]);
   for (uint32_t j = Lg; j < L; j++) vf.at(dst + j) = 0;
   write_masked(vf, dst, L, width);
   // fixed bits: v = (v & ~mask) | value — the copied source's fix first, then this coordinate's

@@ -65,14 +65,21 @@ struct Gen {
         o << "  const uint32_t h" << depth << " = rnd(key, " << C << ", 0xFFFFu);\n";
         o << "  const uint32_t sel" << depth << " = h" << depth << " & 0xFFFFu;\n";
         // uniform / small
-        for (uint32_t j = 0; j < L; j++) o << "  const uint32_t u" << depth << "_" << j << " = rnd(key, " << C << ", " << j << "u);\n";
+        // narrow coordinates (MG_GEN_NARROW_BITS) take their uniform / small value from h >> 16
+        const bool narrow = P.coord_width[c] <= MG_GEN_NARROW_BITS;
+        for (uint32_t j = 0; j < L; j++)
+          o << "  const uint32_t u" << depth << "_" << j << " = "
+            << (narrow ? (j ? std::string("0u") : "(h" + std::to_string(depth) + " >> 16)")
+                       : "rnd(key, " + C + ", " + std::to_string(j) + "u)")
+            << ";\n";
         // dictionary (+ delta)
         if (pd) {
           o << "  const uint32_t de" << depth << " = ((h" << depth << " >> 16) * " << sp.p[1] << "u) >> 16;\n";
           for (uint32_t j = 0; j < L; j++)
             o << "  uint32_t d" << depth << "_" << j << " = " << (j < Lg ? ("gconsts[" + std::to_string(sp.p[0] + j) + "u + de" + std::to_string(depth) + " * " + std::to_string(Lc) + "u]") : std::string("0u")) << ";\n";
           if (sp.p[5]) {
-            o << "  { const uint32_t rr = u" << depth << "_0; const bool on = (rr & 0xFFFFu) < " << sp.p[5]
+            o << "  { const uint32_t rr = " << (narrow ? "rnd(key, " + C + ", 0u)" : "u" + std::to_string(depth) + "_0")
+            << "; const bool on = (rr & 0xFFFFu) < " << sp.p[5]
               << "u; const uint64_t mag = on ? (((rr >> 16) & 1u) + 1u) : 0u; const bool sb = (rr >> 17) & 1u; uint64_t cy = mag, t;";
             for (uint32_t j = 0; j < Lg; j++)
               o << " t = sb ? ((uint64_t)d" << depth << "_" << j << " - cy) : ((uint64_t)d" << depth << "_" << j

@@ -54,7 +54,9 @@ __device__ __forceinline__ void gen_regs(uint32_t (&o)[L], const uint32_t* __res
 #pragma unroll
   for (int level = 0; level < 2; level++) {
     if (s.kind != G_MIXED) break;
-    const uint32_t sel = rnd(key, cc, 0xFFFFu) & 0xFFFFu;
+    const uint32_t h = rnd(key, cc, 0xFFFFu);
+    const uint32_t sel = h & 0xFFFFu;
+    const bool narrow = cw[cc] <= 16u;  // MG_GEN_NARROW_BITS: uniform / small value from h >> 16
     const uint32_t pc = (allow_copy && s.p[3] != 0xFFFFFFFFu) ? s.p[4] : 0u;
     const uint32_t pd = s.p[1] ? s.p[2] : 0u;
     const uint32_t ps = s.p[6] & 0xFFFFu;
@@ -75,10 +77,14 @@ __device__ __forceinline__ void gen_regs(uint32_t (&o)[L], const uint32_t* __res
       const uint32_t bits = (s.p[6] >> 16) < width ? (s.p[6] >> 16) : width;
 #pragma unroll
       for (int j = 0; j < L; j++) {
-        uint32_t v = rnd(key, cc, j);
+        uint32_t v = narrow ? (j == 0 ? h >> 16 : 0u) : rnd(key, cc, j);
         const uint32_t lo = j * 32;
         o[j] = lo >= bits ? 0u : (bits - lo >= 32 ? v : (v & ((1u << (bits - lo)) - 1u)));
       }
+      s.kind = 0xFFu;  // done
+    } else if (narrow) {
+#pragma unroll
+      for (int j = 0; j < L; j++) o[j] = j == 0 ? h >> 16 : 0u;
       s.kind = 0xFFu;  // done
     } else {
       s.kind = G_UNIFORM;
@@ -162,6 +168,12 @@ __device__ __forceinline__ void gen_regs(uint32_t (&o)[L], const uint32_t* __res
       for (int j = 0; j < L; j++) o[j] = (uint32_t)j < Lg ? rnd(key, cc, j) : 0u;
       break;
     }
+  }
+  // a copy is the source's value: masked to the source width, then truncated / zero-extended
+  if (cc != c && Lg == Ls && (cw[cc] & 31u)) {
+#pragma unroll
+    for (int j = 0; j < L; j++)
+      if ((uint32_t)j == Lg - 1) o[j] &= (1u << (cw[cc] & 31u)) - 1u;
   }
   const uint32_t r = width & 31u;
   if (r) o[L - 1] &= (1u << r) - 1u;

@@ -217,7 +217,9 @@ static void gen_coord(const prog_t* P, uint32_t c, uint32_t key, val_t* out) {
   vzero(out);
   for (int level = 0; level < 2; level++) {
     if (s[0] != 3) break;
-    uint32_t sel = rnd(key, cc, 0xFFFFu) & 0xFFFFu;
+    uint32_t h = rnd(key, cc, 0xFFFFu), sel = h & 0xFFFFu;
+    /* narrow coordinates (<= 16 bits, MG_GEN_NARROW_BITS): uniform / small value = h >> 16 */
+    int narrow = P->coords[4 * cc] <= 16;
     uint32_t pc = (allow_copy && s[4] != NONE) ? s[5] : 0;
     uint32_t pd = s[2] ? s[3] : 0;
     uint32_t ps = s[7] & 0xFFFFu;
@@ -236,13 +238,16 @@ static void gen_coord(const prog_t* P, uint32_t c, uint32_t key, val_t* out) {
       from_mixed = 1;
     } else if (sel < pc + pd + ps) {
       uint32_t bits = (s[7] >> 16) < width ? (s[7] >> 16) : width;
+      if (P->coords[4 * cc] < bits) bits = P->coords[4 * cc]; /* a copy keeps the source width */
       for (uint32_t j = 0; j < L; j++) {
-        uint32_t v = rnd(key, cc, j), lo = j * 32;
+        uint32_t v = narrow ? (j == 0 ? h >> 16 : 0u) : rnd(key, cc, j), lo = j * 32;
         v = lo >= bits ? 0u : (bits - lo >= 32 ? v : (v & ((1u << (bits - lo)) - 1u)));
         set_limb32(out, j, v);
       }
       vmask(out, width);
       done = 1;
+    } else if (narrow) {
+      s[0] = 0xFFu; /* value complete: h >> 16 */
     } else {
       s[0] = 0;
     }
@@ -253,6 +258,9 @@ static void gen_coord(const prog_t* P, uint32_t c, uint32_t key, val_t* out) {
   if (done) goto fixes;
   memset(limb, 0, sizeof(limb));
   switch (s[0]) {
+    case 0xFFu: /* narrow MIXED draw */
+      limb[0] = rnd(key, cc, 0xFFFFu) >> 16;
+      break;
     case 2: { /* DICT */
       uint32_t n = s[2];
       uint32_t e = (((rnd(key, cc, 0xFFFFu) >> 16) * n) >> 16);
@@ -308,6 +316,8 @@ static void gen_coord(const prog_t* P, uint32_t c, uint32_t key, val_t* out) {
       for (uint32_t j = 0; j < Lg; j++) limb[j] = rnd(key, cc, j);
       break;
   }
+  /* a copy is the source's value: masked to the source width, then truncated / zero-extended */
+  if (cc != c && Lg == Lsrc && (P->coords[4 * cc] & 31u)) limb[Lg - 1] &= (1u << (P->coords[4 * cc] & 31u)) - 1u;
   from_limbs32(out, limb, Lg);
   vmask(out, width);
 fixes:
