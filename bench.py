@@ -30,6 +30,14 @@ sys.path.insert(0, str(ROOT))
 
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.6 T int32 lane-ops/s
 METRIC = "candidate assignments evaluated/sec (node) + time-to-first-model vs z3"
+# workload -> the BASELINE.json config it stands for
+CONFIG_OF = {
+    "token_transfer_underflow": "C2 token_transfer_underflow (BASELINE.json configs[1])",
+    "etherstore_reentrancy": "C2 etherstore_reentrancy (BASELINE.json configs[1])",
+    "bectoken_batch_overflow": "C3 bectoken_batch_overflow (BASELINE.json configs[2])",
+    "walletlibrary_kill": "C4 walletlibrary_kill -t 3 (BASELINE.json configs[3])",
+    "sha3_keyed_mapping": "C5 sha3_keyed_mapping (BASELINE.json configs[4])",
+}
 
 
 def parse():
@@ -163,7 +171,7 @@ def main():
             "dtype": "u32",
             "data": "synthetic (device-generated candidates of a LASER-shaped query; no solc/z3 in image)",
             "config": {
-                "workload": f"C2 {args.workload} (BASELINE.json configs[1])",
+                "workload": CONFIG_OF[args.workload],
                 "candidates_per_gpu_step": C,
                 "limb_ops_per_candidate": int(info.limb_ops),
                 "program_instrs": int(info.n_instrs),

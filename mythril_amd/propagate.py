@@ -120,8 +120,11 @@ class Propagator:
     def __init__(self, P: ssa.Program):
         self.P = P
         self.dom: Dict[int, Domain] = {}
+        self.term_ivs: Dict[int, List[Tuple[int, int]]] = {}  # interval facts on non-coordinate terms
         # term id -> coordinate index, for terms that ARE a coordinate's value
         self.coord_of: Dict[int, int] = {}
+        self.base_read_of: Dict[int, int] = {}
+        self.hints: List[T.Term] = []  # terms a symbolic comparison wants small
         for c in P.coords:
             t = c.term
             if c.kind == ssa.COORD_SCALAR:
@@ -129,6 +132,8 @@ class Propagator:
             elif c.kind == ssa.COORD_ARRAY_SITE:
                 if t.args[0].op == "array_var":  # a store chain would override the value
                     self.coord_of[t.id] = c.index
+                else:  # the base read a store-chain select falls through to when no index matches
+                    self.base_read_of[t.id] = c.index
             else:
                 if P.nodes[c.node][7] == ssa.MG_NONE:  # lazily-defaulted sites are not free
                     self.coord_of[t.id] = c.index
@@ -153,6 +158,8 @@ class Propagator:
             n = w - lo
         value &= _mask(n)
         c = self.coord_of.get(t.id)
+        if c is None:
+            c = self.base_read_of.get(t.id)
         if c is not None:
             return self.d(c).fix_bits(lo, n, value)
         op = t.op
@@ -212,6 +219,8 @@ class Propagator:
                 return self.eq_bits(x, lo, n, value, depth + 1)
             if xv is not None and y.op != "bvconst":
                 return self.eq_bits(y, lo, n, value, depth + 1)
+            if xv is None and yv is None:
+                return self.eq_bits(x, lo, n, value, depth + 1) | self.eq_bits(y, lo, n, value, depth + 1)
             return False
         if lo == 0 and n == w:
             if op in ("bvadd", "bvsub", "bvxor"):
@@ -229,6 +238,8 @@ class Propagator:
     def bound(self, t: T.Term, ivs: List[Tuple[int, int]], depth=0) -> bool:
         """Assume t (unsigned) lies in the interval union."""
         c = self.coord_of.get(t.id)
+        if c is None:
+            c = self.base_read_of.get(t.id)
         w = t.width
         if c is not None:
             return self.d(c).restrict(ivs)
@@ -242,7 +253,25 @@ class Propagator:
         if t.op == "zero_extend":
             inner = _intersect(ivs, [(0, _mask(t.args[0].width))])
             return bool(inner) and self.bound(t.args[0], inner, depth + 1)
-        return False
+        if t.op == "ite":
+            # bound both arms: the fact then holds whichever way the condition goes
+            # (yetNeeded = If(pending == 0, m_required, pending) <= 1)
+            ok = False
+            for arm in t.args[1:]:
+                if arm.op != "bvconst":
+                    ok |= self.bound(arm, ivs, depth + 1)
+            return ok
+        # any other term: intersect with what earlier facts said about it, and fix the
+        # high bits every admissible value shares (a calldata word bounded to [1, 1] by
+        # a loop's two JUMPI conditions becomes 32 fixed bytes)
+        prev = self.term_ivs.get(t.id)
+        ivs = _norm(ivs) if prev is None else _intersect(prev, ivs)
+        if not ivs:
+            return False
+        self.term_ivs[t.id] = ivs
+        lo, hi = ivs[0][0], ivs[-1][1]
+        k = (lo ^ hi).bit_length()
+        return k < w and self.eq_bits(t, k, w - k, lo >> k, depth + 1)
 
     # -- boolean facts ----------------------------------------------
     def assume(self, b: T.Term, truth: bool, depth=0) -> bool:
@@ -316,6 +345,13 @@ class Propagator:
         if a.op == "bvconst" and b.op != "bvconst":
             a, b, op = b, a, flip[op]
         if b.op != "bvconst":
+            # symbolic on both sides: hint that the smaller side is small, applied after
+            # every literal fact (so it never displaces one): newRequired <= m_numOwners
+            if not truth:
+                op = {"bvult": "bvuge", "bvule": "bvugt", "bvugt": "bvule", "bvuge": "bvult",
+                      "bvslt": "bvsge", "bvsle": "bvsgt", "bvsgt": "bvsle", "bvsge": "bvslt"}[op]
+            small = a if op in ("bvult", "bvule", "bvslt", "bvsle") else b
+            self.hints.append(small)
             return False
         if not truth:
             op = {"bvult": "bvuge", "bvule": "bvugt", "bvugt": "bvule", "bvuge": "bvult",
@@ -356,4 +392,7 @@ def propagate(P: ssa.Program, roots: Sequence[T.Term]) -> Dict[int, Domain]:
     pr = Propagator(P)
     for r in roots:
         pr.assume(r, True)
+    for t in pr.hints:
+        if t.op != "bvconst" and t.width > 8:
+            pr.bound(t, [(0, 255)])
     return pr.dom

@@ -125,6 +125,20 @@ def _fold(t: T.Term, memo) -> T.Term:
             res = args[1] if vals[0] else args[2]
     elif t.op == "ite" and T.const_value(args[0]) is not None:
         res = args[1] if T.const_value(args[0]) else args[2]
+    elif t.op == "select" and T.const_value(args[1]) is not None:
+        # z3 simplify's array rewrite: Select(Store(a, i, v), j) with literal i, j is v
+        # when i == j and Select(a, j) when i != j; K(v) reads v.  It stops at the first
+        # symbolic store index (account.py:61 returns simplify(storage[item])).
+        j = T.const_value(args[1])
+        arr = args[0]
+        while arr.op == "store" and T.const_value(arr.args[1]) is not None and T.const_value(arr.args[1]) != j:
+            arr = arr.args[0]
+        if arr.op == "store" and T.const_value(arr.args[1]) == j:
+            res = arr.args[2]
+        elif arr.op == "const_array":
+            res = arr.args[0]
+        elif arr is not args[0]:
+            res = T.mk("select", t.sort, (arr, args[1]))
     elif t.op == "eq" and args[0] is args[1]:
         res = T.BoolVal(True)  # hash-consed: structurally equal (z3 simplify does the same)
     if res is None:

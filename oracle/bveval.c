@@ -78,6 +78,72 @@ static int viszero(const val_t* a) {
   return 1;
 }
 
+/* Keccak-256 (0x01 padding, rate 136), FIPS-202 Keccak-f[1600] on 64-bit lanes,
+ * as _pysha3 / ethereum.utils.sha3 (keccak_function_manager.py:44-57).  Pinned by
+ * the KATs in tests/golden/keccak_kat.json through tests/test_cport.py. */
+static const uint64_t KRC[24] = {
+  0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
+  0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+  0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
+  0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
+  0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+  0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+
+static uint64_t rotl64(uint64_t x, unsigned r) { return r ? (x << r) | (x >> (64 - r)) : x; }
+
+static void keccak_f1600(uint64_t a[25]) {
+  for (int round = 0; round < 24; round++) {
+    uint64_t c[5], d, b[25];
+    for (int x = 0; x < 5; x++) c[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
+    for (int x = 0; x < 5; x++) {
+      d = c[(x + 4) % 5] ^ rotl64(c[(x + 1) % 5], 1);
+      for (int y = 0; y < 25; y += 5) a[y + x] ^= d;
+    }
+    /* rho + pi: lane (x, y) moves to (y, 2x + 3y), rotated by the triangular offsets */
+    unsigned x = 1, y = 0, r = 0;
+    b[0] = a[0];
+    for (int t = 0; t < 24; t++) {
+      r += (unsigned)t + 1;
+      unsigned nx = y, ny = (2 * x + 3 * y) % 5;
+      b[nx + 5 * ny] = rotl64(a[x + 5 * y], r % 64);
+      x = nx;
+      y = ny;
+    }
+    for (int yy = 0; yy < 25; yy += 5)
+      for (int xx = 0; xx < 5; xx++) a[yy + xx] = b[yy + xx] ^ (~b[yy + (xx + 1) % 5] & b[yy + (xx + 2) % 5]);
+    a[0] ^= KRC[round];
+  }
+}
+
+/* keccak256 of the nbytes big-endian bytes of v, as a 256-bit big-endian value */
+static void vkeccak(val_t* r, const val_t* v, uint32_t nbytes) {
+  uint8_t msg[MAXW * 8 + 136];
+  for (uint32_t m = 0; m < nbytes; m++) {
+    uint32_t bit = 8 * (nbytes - 1 - m);
+    msg[m] = (uint8_t)(v->w[bit / 64] >> (bit % 64));
+  }
+  uint32_t nblk = nbytes / 136 + 1, tot = nblk * 136;
+  memset(msg + nbytes, 0, tot - nbytes);
+  msg[nbytes] |= 0x01;
+  msg[tot - 1] |= 0x80;
+  uint64_t st[25];
+  memset(st, 0, sizeof(st));
+  for (uint32_t blk = 0; blk < nblk; blk++) {
+    for (int i = 0; i < 17; i++) {
+      uint64_t lane = 0;
+      for (int k = 0; k < 8; k++) lane |= (uint64_t)msg[blk * 136 + 8 * i + k] << (8 * k);
+      st[i] ^= lane;
+    }
+    keccak_f1600(st);
+  }
+  vzero(r);
+  for (int m = 0; m < 32; m++) { /* digest byte m is value byte 31 - m */
+    uint8_t byte = (uint8_t)(st[m / 8] >> (8 * (m % 8)));
+    uint32_t bit = 8 * (31 - m);
+    r->w[bit / 64] |= (uint64_t)byte << (bit % 64);
+  }
+}
+
 static void vadd(val_t* r, const val_t* a, const val_t* b, uint32_t width) {
   unsigned __int128 c = 0;
   for (int i = 0; i < MAXW; i++) {
@@ -522,8 +588,12 @@ static int eval_candidate(ctx_t* X) {
         *r = acc;
         break;
       }
+      case OP_KECCAK:
+        if (A) vkeccak(r, A, n->p0);
+        else { val_t z; vzero(&z); vkeccak(r, &z, 0); }
+        break;
       default:
-        return -1; /* KECCAK not restated here (tests use oracle/keccak.py) */
+        return -1;
     }
   }
   for (uint32_t k = 0; k < P->n_roots; k++)

@@ -72,13 +72,14 @@ def test_jit_eval_vmtests_sample(engine):
             row += 8
 
 
+@pytest.mark.parametrize("shaped", [False, True])
 @pytest.mark.parametrize("name", sorted(workloads.WORKLOADS))
-def test_jit_search_matches_interpreter_and_c(engine, name):
+def test_jit_search_matches_interpreter_and_c(engine, name, shaped):
     from oracle import cport
 
     roots = [c.raw for c in workloads.WORKLOADS[name]()]
     P = ssa.flatten(roots)
-    blob = search.default_generator(P).blob()
+    blob = search.default_generator(P, roots=roots if shaped else None).blob()
     prog = engine.load(P.to_bytes())
     gh = engine.load_gen(prog, blob)
     jit = engine.jit_compile(prog, gh)

@@ -261,16 +261,22 @@ def test_eval_dev_resident_inputs(engine):
         assert ver_h[i] == evaluate(c.raw, OracleModel({"x": assigns[i][0], "y": assigns[i][1]}))
 
 
-@pytest.mark.parametrize("name", ["token_transfer_underflow", "etherstore_reentrancy", "bectoken_batch_overflow"])
-def test_workload_verdicts_match_c_restatement(engine, name):
-    """Every candidate verdict of the benchmark workloads (search-mode generator,
-    full evaluation) equals the C restatement's, and the search first hit/count agree."""
+WORKLOAD_NAMES = ["token_transfer_underflow", "etherstore_reentrancy", "bectoken_batch_overflow",
+                  "walletlibrary_kill", "sha3_keyed_mapping"]
+
+
+@pytest.mark.parametrize("shaped", [False, True])
+@pytest.mark.parametrize("name", WORKLOAD_NAMES)
+def test_workload_verdicts_match_c_restatement(engine, name, shaped):
+    """Every candidate verdict of the benchmark workloads (search-mode generator, broad
+    or propagation-shaped; full evaluation) equals the C restatement's, and the search
+    first hit/count agree."""
     from mythril_amd import workloads
     from oracle import cport
 
     roots = [c.raw for c in workloads.WORKLOADS[name]()]
     P = ssa.flatten(roots)
-    blob = search.default_generator(P).blob()
+    blob = search.default_generator(P, roots=roots if shaped else None).blob()
     n, start, seed = 1 << 14, 12345, 0x6D797468
     prog = engine.load(P.to_bytes())
     gh = engine.load_gen(prog, blob)
@@ -285,7 +291,7 @@ def test_workload_verdicts_match_c_restatement(engine, name):
     assert (gfirst, ghits) == (cfirst, chits)
 
 
-@pytest.mark.parametrize("name", ["token_transfer_underflow", "etherstore_reentrancy", "bectoken_batch_overflow"])
+@pytest.mark.parametrize("name", WORKLOAD_NAMES)
 def test_workload_models_verified(engine, name):
     """The GPU finds a model of each workload query and the oracle accepts it."""
     from mythril_amd import workloads
