@@ -115,7 +115,7 @@ def _try_gpu(constraints, enforce_execution_time):
 
     from . import z3bridge
     from .native import Engine
-    from .search import search
+    from .search import search_partitioned
 
     if any(type(c) == bool and not c for c in constraints):
         return None  # the original raises UnsatError for this
@@ -128,7 +128,7 @@ def _try_gpu(constraints, enforce_execution_time):
     if budget <= 0:
         return None
     terms = z3bridge.to_terms(cs)
-    res = search(Engine.get(), terms, timeout_s=budget / 1000.0, max_candidates=1 << 34)
+    res = search_partitioned(Engine.get(), terms, timeout_s=budget / 1000.0, max_candidates=1 << 34)
     if res.index is None:
         return None
     ver, scalars, arrays, funcs, _ = res.model

@@ -220,6 +220,8 @@ def _apply_domain(g: GenBuilder, P: ssa.Program, c: int, dom) -> bool:
 class SearchResult:
     def __init__(self, index, hits, scanned, seconds, model=None):
         self.index, self.hits, self.scanned, self.seconds, self.model = index, hits, scanned, seconds, model
+        self.engine = "interp"
+        self.buckets = 1
 
 
 def model_watch(P: ssa.Program):
@@ -275,8 +277,16 @@ def materialize(engine, P: ssa.Program, gen_blob: np.ndarray, seed: int, index: 
 
 def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int = 1 << 22,
            max_candidates: int = 1 << 26, timeout_s: float = 10.0, gen: Optional[GenBuilder] = None,
-           want_model: bool = True) -> SearchResult:
-    """Find the lowest-index satisfying candidate (or give up: None)."""
+           want_model: bool = True, jit: str = "auto", jit_cost_s: float = 0.5) -> SearchResult:
+    """Find the lowest-index satisfying candidate (or give up: None).
+
+    ``jit``: "never" keeps the generic interpreter (``k_run``, no compile
+    latency); "always" compiles the query-specialised kernel first; "auto"
+    starts on the interpreter, and when the first chunk has no hit and more than
+    ``jit_cost_s`` of the budget is left, compiles the JIT kernel (~0.35 s of
+    hipRTC, ~10x the interpreter's candidates/s) and continues the SAME index
+    stream on it.  Both kernels compute identical verdicts for every index
+    (``tests/test_gpu_jit.py``), so the first hit does not depend on the mode."""
     P = ssa.flatten(roots)
     g = gen or default_generator(P, roots=roots)
     blob = g.blob()
@@ -285,27 +295,83 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
     scanned = 0
     hit = None
     hits = 0
+    used = "interp"
     try:
         gh = engine.load_gen(prog, blob)
+        jh = None
         try:
             start = 0
             while scanned < max_candidates and time.perf_counter() - t0 < timeout_s:
+                left = timeout_s - (time.perf_counter() - t0)
+                if jh is None and (jit == "always" or (jit == "auto" and scanned > 0 and left > jit_cost_s)):
+                    try:
+                        jh = engine.jit_compile(prog, gh)
+                        used = "jit"
+                    except Exception:  # JIT unavailable for this program: stay on the interpreter
+                        jit = "never"
+                    continue
                 n = min(chunk, max_candidates - scanned)
-                idx, nh = engine.search(prog, gh, seed, start, n, early_exit=True)
+                if jh is not None:
+                    idx, nh = engine.jit_search(jh, seed, start, n, early_exit=True)
+                else:
+                    idx, nh = engine.search(prog, gh, seed, start, n, early_exit=True)
                 scanned += n
                 start += n
                 if idx is not None:
                     hit, hits = idx, nh
                     break
-                chunk = min(chunk * 2, 1 << 28)
+                chunk = min(chunk * 2, 1 << 28 if jh is None else 1 << 30)
         finally:
+            if jh is not None:
+                engine.jit_free(jh)
             engine.free_gen(gh)
     finally:
         engine.free(prog)
     dt = time.perf_counter() - t0
     res = SearchResult(hit, hits, scanned, dt)
+    res.engine = used
     if hit is not None and want_model:
         res.model = materialize(engine, P, blob, seed, hit) + (P,)
+    return res
+
+
+def search_partitioned(engine, roots: Sequence[T.Term], timeout_s: float = 10.0, **kw) -> SearchResult:
+    """Search each variable-disjoint bucket (``partition.py``) on its own and merge
+    the bucket models (``independence_solver.py:119-140``).  ``index`` is the
+    tuple of per-bucket first hits; the model tuple is
+    ``(verdict, scalars, arrays, funcs, [programs])``."""
+    from .partition import partition
+
+    buckets = partition(roots)
+    if len(buckets) <= 1:
+        return search(engine, roots, timeout_s=timeout_s, **kw)
+    t0 = time.perf_counter()
+    idx, hits, scanned = [], 0, 0
+    ver, scalars, arrays, funcs, progs = 1, {}, {}, {}, []
+    engines = set()
+    for b in buckets:
+        left = timeout_s - (time.perf_counter() - t0)
+        r = search(engine, b, timeout_s=max(left, 1e-3), **kw)
+        scanned += r.scanned
+        engines.add(getattr(r, "engine", "interp"))
+        if r.index is None:
+            res = SearchResult(None, 0, scanned, time.perf_counter() - t0)
+            res.buckets = len(buckets)
+            return res
+        idx.append(r.index)
+        hits += r.hits
+        if r.model is not None:
+            v, s_, a_, f_, p_ = r.model
+            ver &= int(v)
+            scalars.update(s_)
+            arrays.update(a_)
+            funcs.update(f_)
+            progs.append(p_)
+    res = SearchResult(tuple(idx), hits, scanned, time.perf_counter() - t0)
+    res.buckets = len(buckets)
+    res.engine = "+".join(sorted(engines))
+    if kw.get("want_model", True):
+        res.model = (ver, scalars, arrays, funcs, progs)
     return res
 
 

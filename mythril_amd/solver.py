@@ -234,8 +234,8 @@ def _solve(constraints: Sequence[T.Term], timeout_ms: float) -> Optional[Model]:
 
     st = SolverStatistics()
     eng = Engine.get()
-    res = search.search(eng, list(constraints), timeout_s=max(timeout_ms, 1.0) / 1000.0,
-                        max_candidates=1 << 34)
+    res = search.search_partitioned(eng, list(constraints), timeout_s=max(timeout_ms, 1.0) / 1000.0,
+                                    max_candidates=1 << 34)
     st.candidates += res.scanned
     if res.index is None:
         st.gpu_unknown += 1
@@ -290,6 +290,14 @@ class Solver(BaseSolver):
 
     def pop(self, num: int) -> None:
         self.constraints = self.constraints[: max(0, len(self.constraints) - num)]
+
+
+class IndependenceSolver(Solver):
+    """``mythril/laser/smt/solver/independence_solver.py:85-153``: every
+    :class:`BaseSolver` here already splits its constraints into
+    variable-disjoint buckets before the GPU search (``search_partitioned``)
+    and returns the merged model, so this is the same solver under the
+    reference's name."""
 
 
 class Optimize(BaseSolver):

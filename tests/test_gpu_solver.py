@@ -178,3 +178,51 @@ def test_get_model_contract(engine):
     assert m.eval(x.raw).as_long() == 5
     with pytest.raises(solver.UnsatError):
         solver.get_model((x == BVV(5, 256), x == BVV(6, 256)), enforce_execution_time=False)
+
+
+# -- independence partitioning (independence_solver.py) -----------------------
+def _two_independent_needles():
+    x, y = BVS("x", 256), BVS("y", 256)
+    k1, k2 = BVV(0x9E3779B97F4A7C15F39CC0605CEDC835, 256), BVV(0xC2B2AE3D27D4EB4F165667B19E3779F9, 256)
+    from mythril_amd.smt import Extract
+
+    return [(Extract(15, 0, x * k1) == BVV(0x1234, 16)).raw, (Extract(15, 0, y * k2) == BVV(0xBEEF, 16)).raw]
+
+
+def test_partitioned_search_turns_product_into_sum(engine):
+    from mythril_amd import search
+
+    cs = _two_independent_needles()
+    joint = search.search(engine, cs, max_candidates=1 << 24, timeout_s=30, jit="never")
+    assert joint.index is None  # ~2^-32 per candidate jointly
+    res = search.search_partitioned(engine, cs, max_candidates=1 << 24, timeout_s=30, jit="never")
+    assert res.buckets == 2 and res.index is not None
+    ver, scalars, arrays, funcs, _ = res.model
+    om = OracleModel(scalars, arrays, funcs)
+    assert ver == 1 and all(evaluate(c, om) == 1 for c in cs)
+
+
+def test_independence_solver(engine):
+    x, y, z, a, b = (BVS(n, 256) for n in "xyzab")
+    from mythril_amd.smt import UGT
+
+    s = solver.IndependenceSolver()
+    s.add(UGT(x, y), y == z, a == b)
+    _check(s, sat)
+    s = solver.IndependenceSolver()
+    s.set_timeout(300)
+    s.add(UGT(x, y), y == z, a == b, a != b)
+    assert _check(s, "unsat") == unknown
+
+
+# -- interpreter -> JIT escalation -------------------------------------------
+def test_jit_escalation_same_first_hit(engine):
+    from mythril_amd import search
+
+    cs = _two_independent_needles()[:1]
+    r_i = search.search(engine, cs, timeout_s=30, jit="never", chunk=1 << 12)
+    r_j = search.search(engine, cs, timeout_s=30, jit="always", chunk=1 << 12)
+    r_a = search.search(engine, cs, timeout_s=30, jit="auto", chunk=1 << 12, jit_cost_s=0.0)
+    assert r_i.engine == "interp" and r_j.engine == "jit" and r_a.engine == "jit"
+    assert r_i.index is not None and r_i.index == r_j.index == r_a.index
+    assert r_i.model[1:4] == r_j.model[1:4]
