@@ -322,23 +322,78 @@ __device__ __forceinline__ W8 bv_ashr(const W8& a, const W8& b, u32 width) {
   return r;
 }
 
-// EVM EXP (mod 2^width): square-and-multiply over the exponent bits, MSB first
+// low 256 bits of a*a: 16 doubled cross products + 4 squares (mul8 needs 36)
+__device__ __forceinline__ W8 sqr8(const W8& a) {
+  W8 r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.w[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    u64 c = 0;
+#pragma unroll
+    for (int j = i + 1; j < 8 - i; j++) {
+      u64 t = (u64)a.w[i] * a.w[j] + r.w[i + j] + c;
+      r.w[i + j] = (u32)t;
+      c = t >> 32;
+    }
+  }
+#pragma unroll
+  for (int i = 7; i > 0; i--) r.w[i] = (r.w[i] << 1) | (r.w[i - 1] >> 31);
+  r.w[0] <<= 1;
+  W8 d;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const u64 q = (u64)a.w[i] * a.w[i];
+    d.w[2 * i] = (u32)q;
+    d.w[2 * i + 1] = (u32)(q >> 32);
+  }
+  return add8(r, d);
+}
+
+// EVM EXP (mod 2^width): left-to-right 2-bit fixed-window exponentiation.
+// Exponent limbs that are zero in every active lane of the wave are skipped
+// (wave-uniform, so no divergence); per 2 exponent bits: two squarings and at
+// most one multiply by base^{1,2,3}.
 __device__ __forceinline__ W8 bv_exp(const W8& base, const W8& e, u32 width) {
   W8 r;
 #pragma unroll
   for (int i = 0; i < 8; i++) r.w[i] = 0;
   r.w[0] = 1;
+  u32 live = 0;  // wave-uniform count of low limbs that are non-zero somewhere
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if (__ballot(e.w[i] != 0u) != 0ull) live = i + 1;
   W8 ex = e;
+  const u32 sh = 8u - live;  // move the top live limb to limb 7 (uniform barrel stages)
+  if (sh & 4u) {
+#pragma unroll
+    for (int i = 7; i >= 0; i--) ex.w[i] = i >= 4 ? ex.w[i - 4] : 0u;
+  }
+  if (sh & 2u) {
+#pragma unroll
+    for (int i = 7; i >= 0; i--) ex.w[i] = i >= 2 ? ex.w[i - 2] : 0u;
+  }
+  if (sh & 1u) {
+#pragma unroll
+    for (int i = 7; i >= 0; i--) ex.w[i] = i >= 1 ? ex.w[i - 1] : 0u;
+  }
+  const W8 b2 = sqr8(base);
+  const W8 b3 = mul8(b2, base);
 #pragma unroll 1
-  for (int it = 0; it < 256; it++) {
-    const u32 bit = ex.w[7] >> 31;
+  for (u32 it = 0; it < live * 16u; it++) {
+    const u32 dg = ex.w[7] >> 30;
 #pragma unroll
-    for (int i = 7; i > 0; i--) ex.w[i] = (ex.w[i] << 1) | (ex.w[i - 1] >> 31);
-    ex.w[0] <<= 1;
-    r = mul8(r, r);
-    W8 m = mul8(r, base);
+    for (int i = 7; i > 0; i--) ex.w[i] = (ex.w[i] << 2) | (ex.w[i - 1] >> 30);
+    ex.w[0] <<= 2;
+    r = sqr8(sqr8(r));
+    if (__ballot(dg != 0u) != 0ull) {
+      W8 f;
 #pragma unroll
-    for (int i = 0; i < 8; i++) r.w[i] = bit ? m.w[i] : r.w[i];
+      for (int i = 0; i < 8; i++) f.w[i] = dg == 1u ? base.w[i] : (dg == 2u ? b2.w[i] : b3.w[i]);
+      const W8 m = mul8(r, f);
+#pragma unroll
+      for (int i = 0; i < 8; i++) r.w[i] = dg ? m.w[i] : r.w[i];
+    }
   }
   canon8(r, width);
   return r;

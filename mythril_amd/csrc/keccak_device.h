@@ -16,18 +16,46 @@ __device__ __constant__ static const uint64_t kKeccakRC[24] = {
     0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
     0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
 
-__device__ __forceinline__ uint64_t rol64(uint64_t v, int n) { return (v << n) | (v >> (64 - n)); }
+// 64-bit lanes as (lo, hi) 32-bit halves.  gfx950 has no 64-bit rotate; a
+// rotate is two v_alignbit_b32 (funnel shifts), 3-input XOR / chi's
+// a ^ (~b & c) are single v_bitop3_b32 (truth tables 0x96 / 0xD2).
+__device__ __forceinline__ uint32_t lo32(uint64_t v) { return (uint32_t)v; }
+__device__ __forceinline__ uint32_t hi32(uint64_t v) { return (uint32_t)(v >> 32); }
+__device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+__device__ __forceinline__ uint64_t rol64(uint64_t v, int n) {
+  const uint32_t l = lo32(v), h = hi32(v);
+  if (n == 32) return mk64(h, l);
+  if (n < 32)
+    return mk64(__builtin_amdgcn_alignbit(l, h, 32 - n), __builtin_amdgcn_alignbit(h, l, 32 - n));
+  return mk64(__builtin_amdgcn_alignbit(h, l, 64 - n), __builtin_amdgcn_alignbit(l, h, 64 - n));
+}
+
+__device__ __forceinline__ uint32_t xor3_32(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ uint64_t xor5(uint64_t a, uint64_t b, uint64_t c, uint64_t d, uint64_t e) {
+  return mk64(xor3_32(xor3_32(lo32(a), lo32(b), lo32(c)), lo32(d), lo32(e)),
+              xor3_32(xor3_32(hi32(a), hi32(b), hi32(c)), hi32(d), hi32(e)));
+}
+
+// a ^ (~b & c)
+__device__ __forceinline__ uint64_t chi64(uint64_t a, uint64_t b, uint64_t c) {
+  return mk64(__builtin_amdgcn_bitop3_b32(lo32(a), lo32(b), lo32(c), 0xD2),
+              __builtin_amdgcn_bitop3_b32(hi32(a), hi32(b), hi32(c), 0xD2));
+}
 
 __device__ __forceinline__ void keccak_f1600(uint64_t (&a)[25]) {
 #pragma unroll 1
   for (int round = 0; round < 24; ++round) {
-    uint64_t c0 = a[0] ^ a[5] ^ a[10] ^ a[15] ^ a[20];
-    uint64_t c1 = a[1] ^ a[6] ^ a[11] ^ a[16] ^ a[21];
-    uint64_t c2 = a[2] ^ a[7] ^ a[12] ^ a[17] ^ a[22];
-    uint64_t c3 = a[3] ^ a[8] ^ a[13] ^ a[18] ^ a[23];
-    uint64_t c4 = a[4] ^ a[9] ^ a[14] ^ a[19] ^ a[24];
-    uint64_t d0 = c4 ^ rol64(c1, 1), d1 = c0 ^ rol64(c2, 1), d2 = c1 ^ rol64(c3, 1), d3 = c2 ^ rol64(c4, 1),
-             d4 = c3 ^ rol64(c0, 1);
+    const uint64_t c0 = xor5(a[0], a[5], a[10], a[15], a[20]);
+    const uint64_t c1 = xor5(a[1], a[6], a[11], a[16], a[21]);
+    const uint64_t c2 = xor5(a[2], a[7], a[12], a[17], a[22]);
+    const uint64_t c3 = xor5(a[3], a[8], a[13], a[18], a[23]);
+    const uint64_t c4 = xor5(a[4], a[9], a[14], a[19], a[24]);
+    const uint64_t d0 = c4 ^ rol64(c1, 1), d1 = c0 ^ rol64(c2, 1), d2 = c1 ^ rol64(c3, 1),
+                   d3 = c2 ^ rol64(c4, 1), d4 = c3 ^ rol64(c0, 1);
 #pragma unroll
     for (int y = 0; y < 25; y += 5) {
       a[y + 0] ^= d0; a[y + 1] ^= d1; a[y + 2] ^= d2; a[y + 3] ^= d3; a[y + 4] ^= d4;
@@ -61,12 +89,12 @@ __device__ __forceinline__ void keccak_f1600(uint64_t (&a)[25]) {
     // chi
 #pragma unroll
     for (int y = 0; y < 25; y += 5) {
-      uint64_t b0 = a[y], b1 = a[y + 1], b2 = a[y + 2], b3 = a[y + 3], b4 = a[y + 4];
-      a[y + 0] = b0 ^ (~b1 & b2);
-      a[y + 1] = b1 ^ (~b2 & b3);
-      a[y + 2] = b2 ^ (~b3 & b4);
-      a[y + 3] = b3 ^ (~b4 & b0);
-      a[y + 4] = b4 ^ (~b0 & b1);
+      const uint64_t b0 = a[y], b1 = a[y + 1], b2 = a[y + 2], b3 = a[y + 3], b4 = a[y + 4];
+      a[y + 0] = chi64(b0, b1, b2);
+      a[y + 1] = chi64(b1, b2, b3);
+      a[y + 2] = chi64(b2, b3, b4);
+      a[y + 3] = chi64(b3, b4, b0);
+      a[y + 4] = chi64(b4, b0, b1);
     }
     a[0] ^= kKeccakRC[round];
   }
