@@ -564,10 +564,16 @@ struct Rtc {
 Rtc& rtc() {
   static Rtc r;
   if (r.h) return r;
-  const char* names[] = {"libhiprtc.so.7", "/opt/rocm/lib/libhiprtc.so.7", "libhiprtc.so"};
+  // the image's ROCm hipRTC first: a process that imported torch already has torch's bundled (older)
+  // libhiprtc loaded under the same soname, and its code for these kernels is measurably slower
+  // hipRTC dlopens its compiler (libamd_comgr.so.3) by soname, which would bind to torch's copy;
+  // a fresh link namespace makes it resolve the image's own comgr next to it.
+  const char* env = getenv("MYTHGPU_HIPRTC");
+  if (!env || std::strcmp(env, "shared") != 0) r.h = dlmopen(LM_ID_NEWLM, "/opt/rocm/lib/libhiprtc.so.7", RTLD_NOW | RTLD_LOCAL);
+  const char* names[] = {"/opt/rocm/lib/libhiprtc.so.7", "libhiprtc.so.7", "libhiprtc.so"};
   for (const char* n : names) {
-    r.h = dlopen(n, RTLD_NOW | RTLD_LOCAL);
     if (r.h) break;
+    r.h = dlopen(n, RTLD_NOW | RTLD_LOCAL);
   }
   if (!r.h) return r;
   r.create = (pCreate)dlsym(r.h, "hiprtcCreateProgram");
