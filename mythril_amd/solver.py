@@ -208,6 +208,32 @@ class Model:
             memo[n.id] = r
         return memo[t.id]
 
+    def eval_many(self, expressions, model_completion: bool = True) -> List["Value"]:
+        """Batched :meth:`eval`: every ground term is watched in ONE program and
+        evaluated by one ``mg_eval`` launch (terms with unbound symbols come back
+        symbolic, as in :meth:`eval`)."""
+        from .native import Engine
+
+        subs = [self.substitute(_raw(e), model_completion) for e in expressions]
+        ground = [t for t in subs if not T.free_symbols([t])]
+        out: Dict[int, Value] = {}
+        if ground:
+            P = ssa.flatten([T.BoolVal(True)], extra=ground)
+            P.set_watch([P.term_node[t.id] for t in ground])
+            eng = Engine.get()
+            prog = eng.load(P.to_bytes())
+            try:
+                info = eng.info(prog)
+                _, watch = eng.eval(prog, ssa.soa_from_assignments(P, [[]]), 1, watch_words=info.watch_words)
+            finally:
+                eng.free(prog)
+            r = 0
+            for t in ground:
+                L = ssa.limbs(t.width)
+                out[t.id] = Value(ssa.limbs_to_int(watch[r:r + L, 0]), t.width, t.is_bool)
+                r += L
+        return [out.get(t.id, t) for t in subs]
+
     def eval(self, expression, model_completion: bool = False):
         """Evaluate on the GPU (``mg_eval`` of the ground, substituted term)."""
         from .native import Engine
