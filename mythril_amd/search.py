@@ -40,6 +40,9 @@ ACTORS = [
 
 P16 = 65536
 
+# prefix-incremental flattening shared by every search (LASER's sibling queries share prefixes)
+FLATTEN_CACHE = ssa.FlattenCache()
+
 
 class GenBuilder:
     """Assemble a generator blob (``include/mythgpu.h`` MG_GEN_MAGIC layout)."""
@@ -287,7 +290,7 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
     hipRTC, ~10x the interpreter's candidates/s) and continues the SAME index
     stream on it.  Both kernels compute identical verdicts for every index
     (``tests/test_gpu_jit.py``), so the first hit does not depend on the mode."""
-    P = ssa.flatten(roots)
+    P = FLATTEN_CACHE.flatten(roots)
     g = gen or default_generator(P, roots=roots)
     blob = g.blob()
     prog = engine.load(P.to_bytes())

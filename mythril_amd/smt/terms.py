@@ -316,9 +316,10 @@ def bvexp(a: Term, b: Term) -> Term:
 # traversal helpers
 # ----------------------------------------------------------------------------
 
-def postorder(roots: Iterable[Term]):
-    """Yield every distinct term reachable from ``roots`` children-first."""
-    seen = set()
+def postorder(roots: Iterable[Term], skip=None):
+    """Yield every distinct term reachable from ``roots`` children-first.  Terms
+    whose id is in ``skip`` (a set or dict) are neither yielded nor expanded."""
+    seen = set(skip) if skip is not None else set()
     out = []
     stack = [(r, False) for r in reversed(list(roots))]
     while stack:

@@ -174,19 +174,10 @@ def _base_of(arr: T.Term) -> T.Term:
     return arr
 
 
-def flatten(roots: Sequence[T.Term], lazy_inverse: bool = True, extra: Sequence[T.Term] = ()) -> Program:
-    """Flatten Bool roots (terms) into a :class:`Program`.  ``extra`` terms are
-    flattened too (so they can be watched) without becoming constraints."""
-    P = Program()
-    roots = list(roots)
-    for r in roots:
-        if not r.is_bool:
-            raise TypeError("constraint roots must be Bool terms")
-
-    scalar_coord: Dict[str, int] = {}
-    table_of: Dict[tuple, int] = {}
-    # inverse-UF laziness: inverse app of f(x) defaults to x
-    fwd_arg: Dict[int, int] = {}   # term id of f(x) app -> term id of x
+def _extend(st: "_FlatState", terms: Sequence[T.Term], lazy_inverse: bool) -> None:
+    """Flatten the not-yet-flattened subterms of ``terms`` into ``st.P``."""
+    P = st.P
+    scalar_coord, table_of, fwd_arg = st.scalar_coord, st.table_of, st.fwd_arg
 
     def new_node(op, width, a=MG_NONE, b=MG_NONE, c=MG_NONE, p0=0, p1=0, p2=0, term=None):
         if width > MG_MAX_WIDTH:
@@ -216,13 +207,12 @@ def flatten(roots: Sequence[T.Term], lazy_inverse: bool = True, extra: Sequence[
         P.coords.append(c)
         return c
 
-    order = T.postorder(list(roots) + list(extra))
-    # pre-pass: forward UF apps (for lazy inverse defaults)
-    if lazy_inverse:
-        for t in order:
-            if t.op == "app":
-                fwd_arg[t.id] = t.args[0].id
-
+    order = T.postorder(terms, skip=P.term_node) if P.term_node else T.postorder(terms)
+    for t in order:
+        if lazy_inverse and t.op == "app":
+            # forward UF apps, for lazy inverse defaults; the argument of an inverse
+            # app is visited before it (children first), so one pass suffices
+            fwd_arg[t.id] = t.args[0].id
     for t in order:
         n = None
         op = t.op
@@ -317,8 +307,99 @@ def flatten(roots: Sequence[T.Term], lazy_inverse: bool = True, extra: Sequence[
             raise Unsupported(f"operator {op}")
         P.term_node[t.id] = n
 
-    P.roots = [P.term_node[r.id] for r in roots]
-    return P
+    P._blob = None
+
+
+def flatten(roots: Sequence[T.Term], lazy_inverse: bool = True, extra: Sequence[T.Term] = ()) -> Program:
+    """Flatten Bool roots (terms) into a :class:`Program`.  ``extra`` terms are
+    flattened too (so they can be watched) without becoming constraints."""
+    roots = list(roots)
+    for r in roots:
+        if not r.is_bool:
+            raise TypeError("constraint roots must be Bool terms")
+    st = _FlatState()
+    _extend(st, list(roots) + list(extra), lazy_inverse)
+    st.P.roots = [st.P.term_node[r.id] for r in roots]
+    return st.P
+
+
+class _FlatState:
+    """A Program under construction plus the flattener's lookup tables."""
+
+    def __init__(self):
+        self.P = Program()
+        self.scalar_coord: Dict[str, int] = {}
+        self.table_of: Dict[tuple, int] = {}
+        self.fwd_arg: Dict[int, int] = {}   # term id of f(x) app -> term id of x
+
+    def copy(self) -> "_FlatState":
+        c = _FlatState()
+        P, Q = self.P, c.P
+        Q.nodes = [list(n) for n in P.nodes]
+        Q.node_width = list(P.node_width)
+        Q.roots = list(P.roots)
+        Q.coords = list(P.coords)
+        Q.tables = list(P.tables)
+        Q.consts = list(P.consts)
+        Q.term_node = dict(P.term_node)
+        Q.node_term = list(P.node_term)
+        Q.sites = list(P.sites)
+        Q.site_key_node = dict(P.site_key_node)
+        Q.site_val_node = dict(P.site_val_node)
+        Q.const_values = list(P.const_values)
+        c.scalar_coord = dict(self.scalar_coord)
+        c.table_of = dict(self.table_of)
+        c.fwd_arg = dict(self.fwd_arg)
+        return c
+
+
+class FlattenCache:
+    """Prefix-incremental flattening.
+
+    LASER's states share constraint prefixes: ``Constraints.__copy__`` /
+    ``WorldState.__copy__`` (``constraints.py:61-98``, ``world_state.py:58-74``)
+    hand each successor its parent's list, and ``svm.py:252-257`` then appends
+    one JUMPI condition.  The flattened state after every root prefix is kept
+    (keyed by the root term ids, LRU); a query extends the longest cached prefix
+    with its remaining roots only.  Terms are hash-consed, so the program built
+    this way is byte-identical to :func:`flatten` of the whole tuple
+    (``tests/test_host_boundary.py``)."""
+
+    def __init__(self, capacity: int = 4096, lazy_inverse: bool = True):
+        from collections import OrderedDict
+
+        self.capacity, self.lazy_inverse = capacity, lazy_inverse
+        self._lru: "OrderedDict[tuple, _FlatState]" = OrderedDict()
+        self.hits = self.misses = 0
+
+    def flatten(self, roots: Sequence[T.Term]) -> Program:
+        roots = list(roots)
+        for r in roots:
+            if not r.is_bool:
+                raise TypeError("constraint roots must be Bool terms")
+        ids = tuple(r.id for r in roots)
+        k = len(ids)
+        while k > 0 and ids[:k] not in self._lru:
+            k -= 1
+        if k:
+            self.hits += 1
+            self._lru.move_to_end(ids[:k])
+            st = self._lru[ids[:k]].copy()
+        else:
+            self.misses += 1
+            st = _FlatState()
+        if k == len(ids):
+            return st.P
+        _extend(st, roots[k:], self.lazy_inverse)
+        st.P.roots.extend(st.P.term_node[r.id] for r in roots[k:])
+        self._put(ids, st.copy())  # a query's successors extend its own tuple (svm.py:252-257)
+        return st.P
+
+    def _put(self, key, st):
+        self._lru[key] = st
+        self._lru.move_to_end(key)
+        while len(self._lru) > self.capacity:
+            self._lru.popitem(last=False)
 
 
 # ---------------------------------------------------------------------------

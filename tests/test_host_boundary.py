@@ -119,3 +119,24 @@ def test_addnooverflow_expands_like_z3():
     t = BVAddNoOverflow(a, b, False).raw
     assert t.op == "eq" and t.args[0].op == "extract" and t.args[0].params == (256, 256)
     assert BVSubNoUnderflow(a, b, False).raw.op == "bvule"
+
+
+def test_prefix_incremental_flatten_is_byte_identical():
+    """FlattenCache (SURVEY §8(f) rank 4) extends the longest cached root prefix;
+    the program must equal a fresh flatten of the whole tuple, byte for byte."""
+    import random
+
+    from mythril_amd import workloads
+
+    fc = ssa.FlattenCache(capacity=64)
+    rng = random.Random(3)
+    for name, fn in workloads.WORKLOADS.items():
+        roots = [c.raw for c in fn()]
+        for _ in range(4):  # a random walk of prefixes, as sibling states produce
+            k = rng.randint(1, len(roots))
+            assert fc.flatten(roots[:k]).to_bytes() == ssa.flatten(roots[:k]).to_bytes(), name
+        P = fc.flatten(roots)
+        assert P.to_bytes() == ssa.flatten(roots).to_bytes(), name
+        P.set_watch([0])  # callers may mutate what they get; the cache must not see it
+        assert fc.flatten(roots).watch == []
+    assert fc.hits > 0
