@@ -226,3 +226,18 @@ def test_jit_escalation_same_first_hit(engine):
     assert r_i.engine == "interp" and r_j.engine == "jit" and r_a.engine == "jit"
     assert r_i.index is not None and r_i.index == r_j.index == r_a.index
     assert r_i.model[1:4] == r_j.model[1:4]
+
+
+def test_partitioned_search_with_ground_bucket(engine):
+    from mythril_amd import search
+    from mythril_amd.smt import Not
+
+    x = BVS("x", 256)
+    ground_true = Not(BVV(1, 256) == BVV(2, 256)).raw
+    cs = [(x == BVV(5, 256)).raw, ground_true]
+    res = search.search_partitioned(engine, cs, timeout_s=10)
+    assert res.buckets == 2 and res.index is not None
+    assert res.model[1]["x"] == 5
+    ground_false = (BVV(1, 256) == BVV(2, 256)).raw
+    assert search.search_partitioned(engine, [cs[0], ground_false], timeout_s=0.2,
+                                     max_candidates=1 << 22).index is None
