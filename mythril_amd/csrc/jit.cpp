@@ -41,6 +41,21 @@ struct Gen {
     return (d && d->op == K_CONST) ? &P.consts[d->p0] : nullptr;
   }
 
+  // A dictionary of n entries of a coordinate at most 32 bits wide whose n*width bits fit in 64 is
+  // packed into one 64-bit literal: entry `idx` is a shift and a mask in VGPRs instead of a per-lane
+  // gather from gconsts (one VMEM instruction per coordinate and candidate; the C2 query has 124
+  // such byte coordinates).  Returns "" when the dictionary does not fit.
+  std::string packed_dict(uint32_t off, uint32_t n, uint32_t w, const std::string& idx) const {
+    if (w > 32 || n == 0 || (uint64_t)n * w > 64) return "";
+    uint64_t pack = 0;
+    const uint64_t m = w == 64 ? ~0ull : ((1ull << w) - 1ull);
+    for (uint32_t e = 0; e < n; e++) pack |= ((uint64_t)(*gconsts)[off + e] & m) << (e * w);
+    std::ostringstream t;
+    t << "(uint32_t)((0x" << std::hex << pack << "ull >> (" << idx << " * " << std::dec << w << "u)) & 0x" << std::hex
+      << m << "ull)";
+    return t.str();
+  }
+
   // Branch-free, spec-specialised generator for coordinate c (same function of
   // (key, c) as gen_coord in engine.hip / gen_regs in jit_device.h): every
   // alternative is computed and the winner picked with selects, so the kernel
@@ -75,8 +90,13 @@ struct Gen {
         // dictionary (+ delta)
         if (pd) {
           o << "  const uint32_t de" << depth << " = ((h" << depth << " >> 16) * " << sp.p[1] << "u) >> 16;\n";
+          const std::string packed = packed_dict(sp.p[0], sp.p[1], P.coord_width[c], "de" + std::to_string(depth));
           for (uint32_t j = 0; j < L; j++)
-            o << "  uint32_t d" << depth << "_" << j << " = " << (j < Lg ? ("gconsts[" + std::to_string(sp.p[0] + j) + "u + de" + std::to_string(depth) + " * " + std::to_string(Lc) + "u]") : std::string("0u")) << ";\n";
+            o << "  uint32_t d" << depth << "_" << j << " = "
+              << (j < Lg ? (!packed.empty() ? (j ? std::string("0u") : packed)
+                                            : ("gconsts[" + std::to_string(sp.p[0] + j) + "u + de" + std::to_string(depth) + " * " + std::to_string(Lc) + "u]"))
+                         : std::string("0u"))
+              << ";\n";
           if (sp.p[5]) {
             o << "  { const uint32_t rr = " << (narrow ? "rnd(key, " + C + ", 0u)" : "u" + std::to_string(depth) + "_0")
             << "; const bool on = (rr & 0xFFFFu) < " << sp.p[5]
@@ -113,8 +133,13 @@ struct Gen {
       }
       case MG_GEN_DICT: {
         o << "  const uint32_t de = ((rnd(key, " << C << ", 0xFFFFu) >> 16) * " << sp.p[1] << "u) >> 16;\n";
+        const std::string packed = packed_dict(sp.p[0], sp.p[1], P.coord_width[c], "de");
         for (uint32_t j = 0; j < L; j++)
-          o << "  " << lim(out, j) << " = " << (j < Lg ? ("gconsts[" + std::to_string(sp.p[0] + j) + "u + de * " + std::to_string(Lc) + "u]") : std::string("0u")) << ";\n";
+          o << "  " << lim(out, j) << " = "
+            << (j < Lg ? (!packed.empty() ? (j ? std::string("0u") : packed)
+                                          : ("gconsts[" + std::to_string(sp.p[0] + j) + "u + de * " + std::to_string(Lc) + "u]"))
+                       : std::string("0u"))
+            << ";\n";
         break;
       }
       case MG_GEN_RANGE: {
