@@ -140,3 +140,18 @@ def test_prefix_incremental_flatten_is_byte_identical():
         P.set_watch([0])  # callers may mutate what they get; the cache must not see it
         assert fc.flatten(roots).watch == []
     assert fc.hits > 0
+
+
+def test_flatten_cache_survives_unsupported_extension():
+    """A query that fails to flatten (ssa.Unsupported) must leave the cached
+    prefix untouched: the next extension of that prefix is still byte-identical."""
+    from mythril_amd import workloads
+
+    roots = [c.raw for c in workloads.WORKLOADS["bectoken_batch_overflow"]()]
+    fc = ssa.FlattenCache()
+    fc.flatten(roots[:-1])
+    wide = T.BitVecVar("too_wide", ssa.MG_MAX_WIDTH + 8)
+    bad = T.eq(wide, T.BitVecVal(1, ssa.MG_MAX_WIDTH + 8))
+    with pytest.raises(ssa.Unsupported):
+        fc.flatten(roots[:-1] + [bad])
+    assert fc.flatten(roots).to_bytes() == ssa.flatten(roots).to_bytes()
