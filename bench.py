@@ -32,6 +32,7 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.6 T int32 lane-ops/s
 METRIC = "candidate assignments evaluated/sec (node) + time-to-first-model vs z3"
 # workload -> the BASELINE.json config it stands for
 CONFIG_OF = {
+    "suicide_kill": "C1 suicide_kill -t 2 (BASELINE.json configs[0] query shape; GPU stand-in for the z3 run)",
     "token_transfer_underflow": "C2 token_transfer_underflow (BASELINE.json configs[1])",
     "etherstore_reentrancy": "C2 etherstore_reentrancy (BASELINE.json configs[1])",
     "bectoken_batch_overflow": "C3 bectoken_batch_overflow (BASELINE.json configs[2])",

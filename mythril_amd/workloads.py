@@ -94,6 +94,24 @@ def mapping_slot(km: KeccakFunctionManager, key, slot: int, conds: List[Bool]):
     return h
 
 
+def suicide_kill() -> List[Bool]:
+    """C1 stand-in (``myth analyze solidity_examples/suicide.sol -t 2``; no solc/z3 here, so the
+    SURVEY §8(d) fallback shape): tx 1 calls ``kill(addr)`` with ``addr != 0`` (the ``if`` is not
+    taken and the call returns), and tx 2 calls ``kill(0)``, which reaches SELFDESTRUCT.  The suicide
+    module then asks for a sequence in which every caller is the attacker and the origin
+    (``modules/suicide.py:68-81``).  Each symbolic call also carries the balance precondition
+    ``UGE(balance[sender], call_value)`` (``transaction/symbolic.py``)."""
+    balance = Array("balance", 256, 256)
+    conds: List[Bool] = []
+    for tx in (Tx(1), Tx(2)):
+        conds += tx.dispatch(SEL_KILL, 1)
+        addr = tx.arg(0) & BVV(MASK160, 256)
+        conds.append(UGE(balance[tx.sender], tx.value))
+        conds.append(addr == 0 if tx.id == 2 else addr != 0)
+        conds += [tx.sender == BVV(ATTACKER, 256), tx.sender == BVS(f"origin{tx.id}", 256)]
+    return conds
+
+
 def token_transfer_underflow() -> List[Bool]:
     """C2 (token.sol ``transfer``, -t 2): tx 1 transfers, tx 2's
     ``balances[msg.sender] -= _value`` can underflow (integer module, SWC-101)."""
@@ -259,6 +277,7 @@ def sha3_keyed_mapping() -> List[Bool]:
 
 
 WORKLOADS = {
+    "suicide_kill": suicide_kill,
     "token_transfer_underflow": token_transfer_underflow,
     "etherstore_reentrancy": etherstore_reentrancy,
     "bectoken_batch_overflow": bectoken_batch_overflow,

@@ -3,7 +3,7 @@
 set -o pipefail
 out=gpurun_out/bench_workloads.jsonl
 : > $out
-for w in token_transfer_underflow etherstore_reentrancy bectoken_batch_overflow walletlibrary_kill sha3_keyed_mapping; do
+for w in suicide_kill token_transfer_underflow etherstore_reentrancy bectoken_batch_overflow walletlibrary_kill sha3_keyed_mapping; do
   timeout -k 10 150 python bench.py --workload $w --cpu-seconds ${CPU_SECONDS:-4} > gpurun_out/bench_$w.log 2>&1 || exit $?
   tail -1 gpurun_out/bench_$w.log >> $out
 done
