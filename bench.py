@@ -141,6 +141,30 @@ def main():
         res = search.search(eng, roots, seed=args.seed, chunk=1 << 20, max_candidates=1 << 30, timeout_s=30)
         ttfm_ms = (time.perf_counter() - t1) * 1e3 if res.index is not None else None
 
+    # time to first model on ALL ranks: the compiled kernel sweeps epochs of `chunk` candidates per
+    # rank from index 0, one all-reduce(MIN) per epoch (distributed.sharded_first_hit); the index found
+    # is the global lowest, identical at every GPU count
+    from mythril_amd.distributed import sharded_first_hit
+
+    def first_hit(start, count):
+        if jit is not None:
+            return eng.jit_search(jit, args.seed, start, count, early_exit=True)[0]
+        return eng.search(prog, gh, args.seed, start, count, early_exit=True)[0]
+
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if distributed:
+        ttfm_index, _ = sharded_first_hit(first_hit, rank, world, 1 << 20, max_epochs=1024, device="cuda")
+    else:
+        ttfm_index = None
+        for e in range(1024):
+            ttfm_index = first_hit(e << 20, 1 << 20)
+            if ttfm_index is not None:
+                break
+    ttfm_sharded_ms = (time.perf_counter() - t1) * 1e3 if ttfm_index is not None else None
+
     # CPU baseline: the C restatement over a bounded sample of the same candidates
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -194,6 +218,8 @@ def main():
             },
             "cpu_baseline": cpu,
             "time_to_first_model_ms": ttfm_ms,
+            "time_to_first_model_sharded_ms": ttfm_sharded_ms,
+            "first_model_index": ttfm_index,
             "hits_in_timed_region": int(total_hits),
         }
         print(json.dumps(out), flush=True)
