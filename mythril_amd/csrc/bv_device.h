@@ -39,28 +39,22 @@ __device__ __forceinline__ void canon8(W8& x, u32 width) {
   }
 }
 
+// carry / borrow chains through __builtin_addc/__builtin_subc: one v_add_co/v_addc_co
+// (v_sub_co/v_subb_co) per limb, no 64-bit temporaries
 __device__ __forceinline__ W8 add8(const W8& a, const W8& b) {
   W8 r;
-  u64 c = 0;
+  u32 c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    u64 t = (u64)a.w[i] + b.w[i] + c;
-    r.w[i] = (u32)t;
-    c = t >> 32;
-  }
+  for (int i = 0; i < 8; i++) r.w[i] = __builtin_addc(a.w[i], b.w[i], c, &c);
   return r;
 }
 
 __device__ __forceinline__ W8 sub8(const W8& a, const W8& b, u32* borrow_out = nullptr) {
   W8 r;
-  u64 br = 0;
+  u32 br = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    u64 t = (u64)a.w[i] - b.w[i] - br;
-    r.w[i] = (u32)t;
-    br = (t >> 32) & 1u;
-  }
-  if (borrow_out) *borrow_out = (u32)br;
+  for (int i = 0; i < 8; i++) r.w[i] = __builtin_subc(a.w[i], b.w[i], br, &br);
+  if (borrow_out) *borrow_out = br;
   return r;
 }
 
