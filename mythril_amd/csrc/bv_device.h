@@ -91,21 +91,30 @@ __device__ __forceinline__ W8 mul8(const W8& a, const W8& b) {
   return r;
 }
 
-// high 256 bits of the 512-bit product
+// high 256 bits of the 512-bit product.  Row i adds its low halves at limbs i..i+7
+// (the chain's carry lands in limb i+8, still zero before this row) and its high
+// halves at limbs i+1..i+8; the partial sum after row i fits in i+9 limbs, so the
+// high chain's final carry is zero.
 __device__ __forceinline__ W8 mulhi8(const W8& a, const W8& b) {
   u32 r[16];
 #pragma unroll
   for (int i = 0; i < 16; i++) r[i] = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    u64 c = 0;
+    u32 lo[8], hi[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      u64 t = (u64)a.w[i] * b.w[j] + r[i + j] + c;
-      r[i + j] = (u32)t;
-      c = t >> 32;
+      const u64 p = (u64)a.w[i] * b.w[j];
+      lo[j] = (u32)p;
+      hi[j] = (u32)(p >> 32);
     }
-    r[i + 8] = (u32)c;
+    u32 c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) r[i + j] = __builtin_addc(r[i + j], lo[j], c, &c);
+    r[i + 8] = c;
+    c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) r[i + 1 + j] = __builtin_addc(r[i + 1 + j], hi[j], c, &c);
   }
   W8 h;
 #pragma unroll
