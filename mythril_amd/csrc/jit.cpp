@@ -311,23 +311,18 @@ struct Gen {
       case K_ADD:
       case K_SUB: {
         const bool sub = in.op == K_SUB;
-        o << "  { uint64_t c = 0, t;";
-        for (uint32_t j = 0; j < L; j++) {
-          if (sub)
-            o << " t = (uint64_t)" << v(in.a, j) << " - " << v(in.b, j) << " - c; " << v(d, j)
-              << " = (uint32_t)t; c = (t >> 32) & 1u;";
-          else
-            o << " t = (uint64_t)" << v(in.a, j) << " + " << v(in.b, j) << " + c; " << v(d, j)
-              << " = (uint32_t)t; c = t >> 32;";
-        }
+        // carry / borrow chain: one v_add_co / v_addc_co (v_sub_co / v_subb_co) per limb
+        o << "  { uint32_t c = 0u;";
+        for (uint32_t j = 0; j < L; j++)
+          o << " " << v(d, j) << " = " << (sub ? "__builtin_subc(" : "__builtin_addc(") << v(in.a, j) << ", "
+            << v(in.b, j) << ", c, &c);";
         o << " (void)c; }\n";
         mask_top(d);
         break;
       }
       case K_NEG: {
-        o << "  { uint64_t c = 0, t;";
-        for (uint32_t j = 0; j < L; j++)
-          o << " t = 0ull - (uint64_t)" << v(in.a, j) << " - c; " << v(d, j) << " = (uint32_t)t; c = (t >> 32) & 1u;";
+        o << "  { uint32_t c = 0u;";
+        for (uint32_t j = 0; j < L; j++) o << " " << v(d, j) << " = __builtin_subc(0u, " << v(in.a, j) << ", c, &c);";
         o << " (void)c; }\n";
         mask_top(d);
         break;
@@ -357,14 +352,14 @@ struct Gen {
         const bool sgn = in.op == K_SLT || in.op == K_SLE;
         if (emit_small_literal_compare(in, d, wa, La, sgn)) break;
         const std::string flip = sgn ? hex(1u << ((wa - 1) & 31)) : "0u";
-        o << "  { uint64_t br = 0, t; uint32_t nz = 0;";
+        o << "  { uint32_t br = 0u, nz = 0u;";
         for (uint32_t j = 0; j < La; j++) {
           std::string x = v(in.a, j), y = v(in.b, j);
           if (j == La - 1 && sgn) {
             x = "(" + x + " ^ " + flip + ")";
             y = "(" + y + " ^ " + flip + ")";
           }
-          o << " t = (uint64_t)" << x << " - " << y << " - br; br = (t >> 32) & 1u; nz |= (uint32_t)t;";
+          o << " nz |= __builtin_subc(" << x << ", " << y << ", br, &br);";
         }
         if (in.op == K_ULT || in.op == K_SLT)
           o << " " << v(d, 0) << " = (uint32_t)br; (void)nz; }\n";
