@@ -100,11 +100,13 @@ struct Gen {
           if (sp.p[5]) {
             o << "  { const uint32_t rr = " << (narrow ? "rnd(key, " + C + ", 0u)" : "u" + std::to_string(depth) + "_0")
             << "; const bool on = (rr & 0xFFFFu) < " << sp.p[5]
-              << "u; const uint64_t mag = on ? (((rr >> 16) & 1u) + 1u) : 0u; const bool sb = (rr >> 17) & 1u; uint64_t cy = mag, t;";
+              << "u; const uint32_t mag = on ? (((rr >> 16) & 1u) + 1u) : 0u; const bool sb = (rr >> 17) & 1u;"
+              // d -/+ mag (mod 2^(32 Lg)) as ONE carry chain: add the sign-extended +/-mag
+              << " const uint32_t a0 = sb ? 0u - mag : mag, ah = (sb && mag) ? 0xFFFFFFFFu : 0u; uint32_t cy = 0u;";
             for (uint32_t j = 0; j < Lg; j++)
-              o << " t = sb ? ((uint64_t)d" << depth << "_" << j << " - cy) : ((uint64_t)d" << depth << "_" << j
-                << " + cy); d" << depth << "_" << j << " = (uint32_t)t; cy = sb ? ((t >> 32) & 1u) : (t >> 32);";
-            o << " (void)cy; }\n";
+              o << " d" << depth << "_" << j << " = __builtin_addc(d" << depth << "_" << j << ", " << (j ? "ah" : "a0")
+                << ", cy, &cy);";
+            o << " (void)cy; (void)ah; }\n";
           }
         }
         // copy of another coordinate (its own spec, no further copy)
