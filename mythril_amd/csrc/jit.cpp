@@ -145,12 +145,13 @@ struct Gen {
         break;
       }
       case MG_GEN_RANGE: {
-        o << "  const uint32_t r = rnd(key, " << C << ", 0u); uint64_t cy = "
+        o << "  const uint32_t r = rnd(key, " << C << ", 0u); const uint32_t off = "
           << (sp.p[1] ? ("(uint32_t)(((uint64_t)r * " + std::to_string(sp.p[1]) + "ull) >> 32)") : std::string("r"))
-          << ", t;\n";
+          << "; uint32_t cy = 0u;\n";
         for (uint32_t j = 0; j < L; j++) {
           if (j < Lg)
-            o << "  t = (uint64_t)" << hex((*gconsts)[sp.p[0] + j]) << " + cy; " << lim(out, j) << " = (uint32_t)t; cy = t >> 32;\n";
+            o << "  " << lim(out, j) << " = __builtin_addc(" << hex((*gconsts)[sp.p[0] + j]) << ", " << (j ? "0u" : "off")
+              << ", cy, &cy);\n";
           else
             o << "  " << lim(out, j) << " = 0u;\n";
         }
@@ -160,7 +161,7 @@ struct Gen {
       case MG_GEN_ALIGNED: {
         o << "  const uint32_t r = rnd(key, " << C << ", 0u); const uint64_t m = "
           << (sp.p[2] ? ("(((uint64_t)r * " + std::to_string(sp.p[2]) + "ull) >> 32)") : std::string("(uint64_t)r"))
-          << "; uint64_t cy = 0, t;\n";
+          << "; uint32_t cy = 0u;\n";
         const int32_t sh = (int32_t)sp.p[1];
         for (uint32_t j = 0; j < L; j++) {
           if (j >= Lg) {
@@ -172,8 +173,7 @@ struct Gen {
           if (bit0 <= -32 || bit0 >= 64) mw = "0u";
           else if (bit0 < 0) mw = "(uint32_t)(m << " + std::to_string(-bit0) + ")";
           else mw = "(uint32_t)(m >> " + std::to_string(bit0) + ")";
-          o << "  t = (uint64_t)" << hex((*gconsts)[sp.p[0] + j]) << " + " << mw << " + cy; " << lim(out, j)
-            << " = (uint32_t)t; cy = t >> 32;\n";
+          o << "  " << lim(out, j) << " = __builtin_addc(" << hex((*gconsts)[sp.p[0] + j]) << ", " << mw << ", cy, &cy);\n";
         }
         o << "  (void)cy;\n";
         break;
