@@ -12,13 +12,19 @@ the only exchange step the path has.  Candidate shards are disjoint index ranges
 (weak scaling).  Inputs are generated on the device (nothing crosses PCIe inside
 the timed region).
 
-roofline: achieved = limb_ops/candidate (fixed cost table, program.cpp op_cost)
-x C / the search kernel's mean duration (HIP events on the engine's own stream);
-peak = INT32 VALU lane-ops/s of MI355X (256 CU x 4 SIMD x 32 lanes x 2.4 GHz).
+roofline: achieved = VALU lane-instructions per candidate MEASURED by rocprofv3
+(SQ_INSTS_VALU x 64 / candidates, committed under profiles/ by tools/profile.sh and
+matched to this exact kernel by the SHA of its JIT source) x C / the search kernel's
+mean duration (HIP events on the engine's own stream); peak = INT32 VALU lane-ops/s
+of MI355X (256 CU x 4 SIMD x 32 lanes x 2.4 GHz), so frac <= 1 by construction.  The
+SURVEY §8(d) cost-table figure (program.cpp op_cost) is reported beside it as
+``algorithmic``: it prices work the JIT folds away, so it is not a roofline.
 cpu_baseline: the plain-C restatement (oracle/bveval.c, OpenMP) timed on the
 host cores over a bounded sample of the same candidates (rank 0, N == 1).
 """
 import argparse
+import glob
+import hashlib
 import json
 import os
 import sys
@@ -52,10 +58,26 @@ def parse():
     ap.add_argument("--seed", type=int, default=0x6D797468)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ttfm", action="store_true",
+                    help="skip the time-to-first-model searches (profiling passes: full launches only)")
     ap.add_argument("--engine", choices=["jit", "interp"], default="jit",
                     help="jit: hipRTC-specialised search kernel; interp: the generic interpreter kernel")
-    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
+    ap.add_argument("--pmc-dir", default=str(ROOT / "profiles"),
+                    help="where tools/profile.sh summaries (pmc_<workload>*.json) are looked up by kernel SHA")
     return ap.parse_args()
+
+
+def load_pmc(pmc_dir: str, workload: str, sha: str, candidates: int):
+    """The committed rocprofv3 summary of THIS kernel (same JIT source SHA, same launch size)."""
+    for f in sorted(glob.glob(os.path.join(pmc_dir, f"*pmc*{workload}*.json")), reverse=True):
+        try:
+            d = json.loads(Path(f).read_text())
+        except (OSError, ValueError):
+            continue
+        if d.get("jit_source_sha16") == sha and d.get("candidates_per_launch") == candidates:
+            d["_file"] = os.path.relpath(f, ROOT)
+            return d
+    return None
 
 
 def main():
@@ -84,17 +106,26 @@ def main():
 
     cs = workloads.WORKLOADS[args.workload]()
     roots = [c.raw for c in cs]
-    P = ssa.flatten(roots)
-    gen = search.default_generator(P, roots=roots)
-    blob = gen.blob()
+    # the program and generator the product path (search.search / the get_model hook) runs
+    P, blob = search.prepare(roots)
     prog = eng.load(P.to_bytes())
     info = eng.info(prog)
     gh = eng.load_gen(prog, blob)
     C = args.candidates
     jit = None
     compile_ms = None
+    sha = None
     if args.engine == "jit":
+        sha = hashlib.sha256(native.jit_source(P.to_bytes(), blob).encode()).hexdigest()[:16]
+        # cold compile: comgr's on-disk cache off, so a kernel compiled by an earlier process
+        # (tests, a previous bench) is not reported as a compile cost
+        prev = os.environ.get("AMD_COMGR_CACHE")
+        os.environ["AMD_COMGR_CACHE"] = "0"
         jit = eng.jit_compile(prog, gh)
+        if prev is None:
+            os.environ.pop("AMD_COMGR_CACHE")
+        else:
+            os.environ["AMD_COMGR_CACHE"] = prev
         compile_ms = eng.jit_info(jit)[0]
 
     from mythril_amd.distributed import chunk_start, first_hit_allreduce
@@ -136,7 +167,7 @@ def main():
 
     # time to first model (early-exit search from index 0 + model read-back), rank 0 only
     ttfm_ms = None
-    if rank == 0:
+    if rank == 0 and not args.no_ttfm:
         t1 = time.perf_counter()
         res = search.search(eng, roots, seed=args.seed, chunk=1 << 20, max_candidates=1 << 30, timeout_s=30)
         ttfm_ms = (time.perf_counter() - t1) * 1e3 if res.index is not None else None
@@ -155,7 +186,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    if distributed:
+    if args.no_ttfm:
+        ttfm_index = None
+    elif distributed:
         ttfm_index, _ = sharded_first_hit(first_hit, rank, world, 1 << 20, max_epochs=1024, device="cuda")
     else:
         ttfm_index = None
@@ -173,16 +206,23 @@ def main():
     if rank == 0:
         total = world * C * args.steps
         value = total / dt
-        achieved = info.limb_ops * C / (kernel_ms * 1e-3) / 1e12
-        traffic = None
-        tj = Path(args.traffic_json)
-        if tj.exists():
-            try:
-                t = json.loads(tj.read_text())
-                if t.get("workload") == args.workload and t.get("candidates") == C:
-                    traffic = t.get("hbm_bytes_per_launch")
-            except (ValueError, OSError):
-                traffic = None
+        kernel_s = kernel_ms * 1e-3
+        pmc = load_pmc(args.pmc_dir, args.workload, sha, C) if sha else None
+        roofline = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_TOPS, "unit": "TOP/s (int32 lane-ops)",
+                    "frac": None, "traffic": None, "kernel_ms": kernel_ms,
+                    "basis": "no rocprofv3 summary for this kernel under profiles/ (run tools/profile.sh)"}
+        if pmc is not None:
+            n_instr = pmc["derived"]["valu_wave_instructions_per_candidate"]
+            achieved = n_instr * C / kernel_s / 1e12
+            roofline.update(achieved=achieved, frac=achieved / VALU_PEAK_TOPS,
+                            traffic=pmc["derived"].get("hbm_bytes_per_launch"),
+                            valu_instructions_per_candidate=n_instr,
+                            basis=f"measured VALU lane-instructions per candidate ({pmc['_file']}, "
+                                  f"rocprofv3 SQ_INSTS_VALU) x candidates / kernel time")
+        algorithmic = {"limb_ops_per_candidate": int(info.limb_ops),
+                       "achieved_T": info.limb_ops * C / kernel_s / 1e12,
+                       "note": "SURVEY §8(d) fixed cost table; prices work the JIT folds (Concat/Extract look-through, "
+                               "range-decided compares), so it is not a roofline fraction"}
         out = {
             "metric": METRIC,
             "value": value,
@@ -199,23 +239,15 @@ def main():
             "config": {
                 "workload": CONFIG_OF[args.workload],
                 "candidates_per_gpu_step": C,
-                "limb_ops_per_candidate": int(info.limb_ops),
                 "program_instrs": int(info.n_instrs),
-                "value_file_words": int(info.value_words),
-                "value_file": "vgpr (jit)" if jit is not None else ("lds" if info.uses_lds else "hbm"),
+                "coords": int(info.n_coords),
                 "engine": args.engine,
-                "jit_compile_ms": compile_ms,
+                "jit_source_sha16": sha,
+                "jit_compile_ms_cold": compile_ms,
                 "parallelism": f"shard{world}",
             },
-            "roofline": {
-                "bound": "valu",
-                "achieved": achieved,
-                "peak": VALU_PEAK_TOPS,
-                "unit": "TOP/s (int32 lane-ops)",
-                "frac": achieved / VALU_PEAK_TOPS,
-                "traffic": traffic,
-                "kernel_ms": kernel_ms,
-            },
+            "roofline": roofline,
+            "algorithmic": algorithmic,
             "cpu_baseline": cpu,
             "time_to_first_model_ms": ttfm_ms,
             "time_to_first_model_sharded_ms": ttfm_sharded_ms,

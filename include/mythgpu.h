@@ -72,7 +72,7 @@ extern "C" {
  * unused high bits zero.  Bool = width 1.
  */
 #define MG_MAGIC 0x3150474Du /* "MGP1" */
-#define MG_VERSION 1u
+#define MG_VERSION 2u  /* v2: SELECT p1 = lazy default node, AUX coordinates */
 #define MG_NONE 0xFFFFFFFFu
 #define MG_MAX_WIDTH 32768u
 
@@ -109,49 +109,80 @@ enum mg_op {
   MG_OP_ARR_VAR = 29,   /* array-sorted: p0 = table */
   MG_OP_ARR_K = 30,     /* array-sorted: a = default value */
   MG_OP_ARR_STORE = 31, /* array-sorted: a = array, b = index, c = value */
-  MG_OP_SELECT = 32,    /* a = array, b = index, p0 = coord of the base read (or MG_NONE) */
+  MG_OP_SELECT = 32,    /* a = array, b = index, p0 = coord of the base read (or MG_NONE),
+                           p1 = node giving the base read's default (MG_NONE: the coordinate) */
   MG_OP_UFAPP = 33,     /* a = argument, p0 = table, p1 = coord */
   MG_OP_KECCAK = 34,    /* a = data (or MG_NONE), p0 = byte length */
   MG_OP_EXP = 35,
   MG_OP_COUNT = 36
 };
 
-enum mg_coord_kind { MG_COORD_SCALAR = 0, MG_COORD_ARRAY_SITE = 1, MG_COORD_UF_SITE = 2 };
+/* AUX: a generator-only scalar (no symbol of the query; e.g. one 256-bit calldata
+ * word whose bytes are the lazy defaults of 32 calldata sites) */
+enum mg_coord_kind { MG_COORD_SCALAR = 0, MG_COORD_ARRAY_SITE = 1, MG_COORD_UF_SITE = 2, MG_COORD_AUX = 3 };
 enum mg_table_kind { MG_TABLE_ARRAY = 0, MG_TABLE_UF = 1 };
 
-/* ---- candidate generator (search mode) -------------------------------- *
+/* ---- candidate generator (search mode), format GEN2 -------------------- *
  * blob: header[4] {MG_GEN_MAGIC, n_coords, n_const_words, 0}
  *       specs: n_coords x 8 words {kind, p0, p1, p2, p3, p4, p5, p6}
  *       consts: n_const_words
- * Coordinate c of candidate i is a pure function of (seed, i, c):
- *   key        = mix32(i_lo ^ mix32(i_hi ^ seed_lo ^ mix32(seed_hi + 0x632BE5AB)))
- *                (mix32: xorshift-multiply finaliser, multipliers 0x7FEB352D, 0x846CA68B)
- *   rnd(c, j)  = fin(key ^ (c*0x9E3779B9 + j*0x85EBCA6B + 0x27D4EB2F)),
- *                fin(x) = x ^= x>>16; x *= 0x7FEB352D; x ^= x>>15
- *   uniform limb j = rnd(c, j); selector h = rnd(c, 0xFFFF): MIXED branch = h & 0xFFFF,
- *   dictionary entry = ((h >> 16) * n) >> 16 (n <= 65535); the +/- delta of a
- *   MIXED dictionary draw reads its bits from rnd(c, 0) (unused by that branch).
- *   Narrow coordinates (width <= MG_GEN_NARROW_BITS) under MIXED take their
- *   uniform and small values from h >> 16 instead of rnd(c, 0): one hash each.
+ *
+ * Coordinate c of candidate i is a pure function of (seed, i, c).  Two keys:
+ *   fmix64(x)   = x ^= x>>33; x *= 0xFF51AFD7ED558CCD; x ^= x>>33;
+ *                 x *= 0xC4CEB9FE1A85EC53; x ^= x>>33        (a bijection of u64)
+ *   lane key    K = fmix64(i ^ fmix64(seed ^ 0x6A09E667F3BCC908))        (K_lo, K_hi)
+ *   group key   G = fmix64((i >> 6) ^ fmix64(seed ^ 0xBB67AE8584CAA73B)) (G_lo, G_hi)
+ * K is distinct for every index, so no two indices of one seed draw the same
+ * candidate (all 2^64 indices are usable).  G is shared by the 64 consecutive
+ * indices of one aligned group — exactly one wave of the search kernels — so a
+ * choice made from G is wave-uniform (a scalar branch, not a per-lane select).
+ *   salt(c, j)  = c*0x9E3779B9 + j*0x85EBCA6B + 0x27D4EB2F           (mod 2^32)
+ *   fin(x)      = x ^= x>>16; x *= 0x7FEB352D; x ^= x>>15
+ *   rnd(c, j)   = fin(K_lo ^ salt(c, j)) + K_hi      per-lane 32 random bits
+ *   h(c)        = rnd(c, 0xFFFF)                     per-lane index / delta bits
+ *   wsel(c)     = fin(G_lo ^ salt(c, 0xFFFE)) + G_hi per-group choice bits
+ *
+ * Kinds (L = ceil(w/32) limbs; every value is masked to its width w):
+ *   UNIFORM  limb j = rnd(c, j)
+ *   RANGE    lo + (((u64)rnd(c,0) * span) >> 32) (span 0: + rnd(c,0)), carried over L limbs
+ *   DICT     entry ((h(c) >> 16) * n) >> 16 of the n-entry table
+ *   ALIGNED  lo + (m << p1), m = ((u64)rnd(c,0) * count) >> 32 (count 0: m = rnd(c,0))
+ *   FIXED    the value
+ *   LAZY     never generated (a site whose default is a program node)
+ *   MIXED    one alternative per aligned group, chosen by s = wsel(c) & 0xFFFF:
+ *              pc = P(copy) if p3 != MG_NONE else 0, pd = P(dict) if n else 0, ps = P(small)
+ *              s < pc            COPY     the FINAL value of coordinate p3 (p3 < c, same width)
+ *              s < pc+pd         DICT     entry ((h(c) >> 16) * n) >> 16
+ *              s < pc+pd+ps      SMALL    UNIFORM masked to min(w, small_bits) bits
+ *              otherwise         UNIFORM
+ *            narrow coordinates (w <= MG_GEN_NARROW_BITS) take UNIFORM / SMALL from
+ *            h(c) & 0xFFFF (one hash each);
+ *            COPY and DICT add a per-lane delta when (wsel(c) >> 16) < P(delta):
+ *              +/-(1 + (h & 1)), minus when (h >> 1) & 1, modulo 2^(32 L);
+ *            then mask to w, then the clamp record (if any): v stays if
+ *              lo <= v < lo + span, else v = lo + (((u64)limb0(v) * span) >> 32)
+ *              (span 0 = 2^32; lo + span <= 2^w is checked at load).
+ * Finally every kind applies its fixed-bit record (kind bits 8..31).
+ * Probabilities are 16-bit fixed point (/65536).
  */
-#define MG_GEN_MAGIC 0x314E4547u /* "GEN1" */
+#define MG_GEN_MAGIC 0x324E4547u /* "GEN2" */
 #define MG_GEN_NARROW_BITS 16u
+#define MG_GEN_MAX_COPY_DEPTH 64u  /* longest static COPY chain a generator may hold */
 enum mg_gen_kind {
   MG_GEN_UNIFORM = 0,  /* uniform over [0, 2^w) */
   MG_GEN_RANGE = 1,    /* p0 = const offset of lo, p1 = span (0 => 2^32): lo + r mod span */
   MG_GEN_DICT = 2,     /* p0 = const offset of n entries (ceil(w/32) limbs each), p1 = n */
-  MG_GEN_MIXED = 3,    /* p0/p1 = dict, p2 = P(dict) / 65536, p3 = copy-from coord (MG_NONE: none),
-                          p4 = P(copy) / 65536, p5 = P(+/-small delta on dict) / 65536,
-                          p6 = P(uniform but small: < 2^(p6>>16)) / 65536 in low 16 bits */
+  MG_GEN_MIXED = 3,    /* p0/p1 = dict, p2 = P(copy) | P(dict) << 16, p3 = copy-from coord (MG_NONE: none),
+                          p4 = P(small) | small_bits << 16, p5 = P(delta on COPY/DICT),
+                          p6 = 0 or 1 + const offset of a clamp record {lo limbs[L], span} */
   MG_GEN_ALIGNED = 4,  /* p0 = const offset of lo, p1 = log2(align), p2 = count (0 => 2^32) */
   MG_GEN_FIXED = 5,    /* p0 = const offset of the value */
   MG_GEN_LAZY = 6      /* site coords only: p0 = node whose value is the default (must precede the site) */
 };
 
 /* spec.kind bits 8..31: 0, or 1 + the const offset of a fixed-bit record
- * {mask limbs[L], value limbs[L]} (L = limbs of the coordinate) applied after
- * generation: v = (v & ~mask) | value.  When MIXED copies another coordinate, the
- * source's record is applied to the copy first. */
+ * {mask limbs[L], value limbs[L]} (L = limbs of the coordinate) applied last:
+ * v = (v & ~mask) | value. */
 #define MG_GEN_KIND(kind) ((kind) & 0xFFu)
 
 /* search flags */

@@ -17,9 +17,9 @@ INCLUDE = PKG.parent / "include"
 LIB = PKG / "libmythgpu.so"
 
 SOURCES = [CSRC / "engine.hip", CSRC / "program.cpp", CSRC / "jit.cpp"]
-HEADERS = [CSRC / "bv_device.h", CSRC / "keccak_device.h", CSRC / "jit_device.h", CSRC / "program.hpp",
+HEADERS = [CSRC / "bv_device.h", CSRC / "keccak_device.h", CSRC / "gen_device.h", CSRC / "jit_device.h", CSRC / "program.hpp",
            CSRC / "jit.hpp", INCLUDE / "mythgpu.h"]
-PRELUDE_PARTS = [CSRC / "bv_device.h", CSRC / "keccak_device.h", CSRC / "jit_device.h"]
+PRELUDE_PARTS = [CSRC / "bv_device.h", CSRC / "keccak_device.h", CSRC / "gen_device.h", CSRC / "jit_device.h"]
 PRELUDE_INC = CSRC / "jit_prelude.inc"
 
 

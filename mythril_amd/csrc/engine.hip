@@ -28,6 +28,7 @@
 #include "../../include/mythgpu.h"
 #include "bv_device.h"
 #include "keccak_device.h"
+#include "gen_device.h"
 #include "jit.hpp"
 #include "program.hpp"
 
@@ -55,6 +56,7 @@ struct KArgs {
   unsigned long long* first_hit;
   unsigned long long* hits;
   uint64_t start, count, seed, stride;
+  uint64_t sk, sg;           // GEN2 seed keys (seed_lane_key / seed_group_key of seed)
   uint32_t n_instr, value_words, flags, pad;
 };
 
@@ -76,172 +78,155 @@ struct VFGlobal {
 };
 
 // ---------------------------------------------------------------------------
-// counter-based candidate generator (pure function of seed, index, coordinate)
+// candidate generator, GEN2 (include/mythgpu.h): a pure function of (seed, index,
+// coordinate); the same function as oracle/bveval.c gen_value and the JIT's
+// straight-line gen_value (jit.cpp), checked candidate by candidate by the tests
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x7FEB352Du;
-  x ^= x >> 15;
-  x *= 0x846CA68Bu;
-  x ^= x >> 16;
-  return x;
+enum : uint32_t { ALT_NONE = 0, ALT_COPY = 1, ALT_DICT = 2, ALT_SMALL = 3, ALT_UNIFORM = 4 };
+
+__device__ __forceinline__ uint32_t mixed_alt(const GenSpec& s, uint32_t ws) {
+  const uint32_t sel = ws & 0xFFFFu;
+  const uint32_t pc = s.p[3] != MG_NONE ? (s.p[2] & 0xFFFFu) : 0u;
+  const uint32_t pd = s.p[1] ? (s.p[2] >> 16) : 0u;
+  const uint32_t ps = s.p[4] & 0xFFFFu;
+  return sel < pc ? ALT_COPY : sel < pc + pd ? ALT_DICT : sel < pc + pd + ps ? ALT_SMALL : ALT_UNIFORM;
 }
 
-__device__ __forceinline__ uint32_t cand_key(uint64_t idx, uint64_t seed) {
-  return mix32((uint32_t)idx ^ mix32((uint32_t)(idx >> 32) ^ (uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + 0x632BE5ABu)));
-}
-
-__device__ __forceinline__ uint32_t rnd(uint32_t key, uint32_t c, uint32_t j) {
-  /* one-multiply finaliser of the (well mixed) candidate key; see MG_GEN_* in mythgpu.h */
-  uint32_t x = key ^ (c * 0x9E3779B9u + j * 0x85EBCA6Bu + 0x27D4EB2Fu);
-  x ^= x >> 16;
-  x *= 0x7FEB352Du;
-  x ^= x >> 15;
-  return x;
-}
-
+// value of coordinate c before its finish (MIXED: the chosen non-COPY alternative)
 template <class VF>
-__device__ __forceinline__ void write_masked(const VF& vf, uint32_t dst, uint32_t L, uint32_t width) {
-  vf.at(dst + L - 1) &= top_mask(width);
-}
-
-// Value of coordinate c for a candidate (key = cand_key(index, seed)).
-// MIXED may copy another coordinate: the copy regenerates the source with the
-// source's own spec and index (one level, no recursion), truncated/zero-extended.
-template <class VF>
-__device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c, uint32_t width, uint32_t key) {
+__device__ void gen_base(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c, uint32_t width, const GKeys& ky,
+                         const GenSpec& s, uint32_t alt) {
   const uint32_t L = (width + 31) >> 5;
-  uint32_t cc = c;  // coordinate whose spec/randomness is used
-  GenSpec s = k.specs[c];
-  const uint32_t fix_dst = s.kind >> 8;  // 1 + const offset of a (mask, value) fix, 0: none
-  uint32_t fix_src = 0;
-  s.kind &= 0xFFu;
-  uint32_t Lg = L;  // limbs to generate
-  bool allow_copy = true;
-  for (int level = 0; level < 2; level++) {
-    if (s.kind != MG_GEN_MIXED) break;
-    const uint32_t h = rnd(key, cc, 0xFFFFu);
-    const uint32_t sel = h & 0xFFFFu;
-    // narrow coordinates (<= 16 bits) draw their uniform / small value from h >> 16
-    const bool narrow = k.coord_width[cc] <= MG_GEN_NARROW_BITS;
-    const uint32_t pc = (allow_copy && s.p[3] != MG_NONE) ? s.p[4] : 0u;
-    const uint32_t pd = s.p[1] ? s.p[2] : 0u;
-    const uint32_t ps = s.p[6] & 0xFFFFu;
-    if (sel < pc) {
-      cc = s.p[3];
-      s = k.specs[cc];
-      fix_src = s.kind >> 8;
-      s.kind &= 0xFFu;
-      Lg = min(L, (k.coord_width[cc] + 31) >> 5);
-      allow_copy = false;
-      continue;  // re-decide with the source's spec
-    }
-    if (sel < pc + pd) {
-      s.kind = MG_GEN_DICT;  // dictionary draw, keeps p5 (delta) below
-      s.p[6] = 1;            // marks "came from MIXED" so the delta option applies
-    } else if (sel < pc + pd + ps) {
-      const uint32_t bits = min(width, s.p[6] >> 16);
-      for (uint32_t j = 0; j < L; j++) {
-        uint32_t v = narrow ? (j == 0 ? h >> 16 : 0u) : rnd(key, cc, j);
-        const uint32_t lo = j * 32;
-        v = lo >= bits ? 0u : (bits - lo >= 32 ? v : (v & ((1u << (bits - lo)) - 1u)));
-        vf.at(dst + j) = v;
-      }
-      s.kind = 0xFFu;  // value complete
-    } else if (narrow) {
-      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = j == 0 ? h >> 16 : 0u;
-      s.kind = 0xFFu;  // value complete
-    } else {
-      s.kind = MG_GEN_UNIFORM;
-    }
-    break;
-  }
-  const uint32_t Ls = s.kind == MG_GEN_DICT || s.kind == MG_GEN_RANGE || s.kind == MG_GEN_ALIGNED ||
-                              s.kind == MG_GEN_FIXED
-                          ? ((k.coord_width[cc] + 31) >> 5)
-                          : Lg;  // limb stride of the source's constants
-  switch (s.kind) {
-    case 0xFFu:
-      break;
-    case MG_GEN_DICT: {
-      const uint32_t n = s.p[1];
-      const uint32_t e = (((rnd(key, cc, 0xFFFFu) >> 16) * n) >> 16);
-      const uint32_t* src = k.gconsts + s.p[0] + e * Ls;
-      for (uint32_t j = 0; j < Lg; j++) vf.at(dst + j) = src[j];
-      if (s.p[6] == 1 && s.p[5]) {
-        const uint32_t r = rnd(key, cc, 0u);
-        if ((r & 0xFFFFu) < s.p[5]) {
-          // +/- 1 or 2 (wrapping)
-          const uint32_t mag = ((r >> 16) & 1u) + 1u;
-          const bool sub = (r >> 17) & 1u;
-          uint64_t carry = mag;
-          for (uint32_t j = 0; j < Lg; j++) {
-            uint64_t t = sub ? ((uint64_t)vf.at(dst + j) - carry) : ((uint64_t)vf.at(dst + j) + carry);
-            vf.at(dst + j) = (uint32_t)t;
-            carry = sub ? ((t >> 32) & 1u) : (t >> 32);
-          }
-        }
-      }
-      break;
-    }
+  switch (MG_GEN_KIND(s.kind)) {
     case MG_GEN_RANGE: {
-      const uint32_t span = s.p[1];
-      const uint32_t r = rnd(key, cc, 0);
-      const uint32_t off = span ? (uint32_t)(((uint64_t)r * span) >> 32) : r;
-      uint64_t carry = off;
-      for (uint32_t j = 0; j < Lg; j++) {
-        uint64_t t = (uint64_t)k.gconsts[s.p[0] + j] + carry;
-        vf.at(dst + j) = (uint32_t)t;
-        carry = t >> 32;
+      const uint32_t span = s.p[1], r = grnd(ky, c, 0);
+      uint32_t off = span ? (uint32_t)(((uint64_t)r * span) >> 32) : r, cy = 0;
+      for (uint32_t j = 0; j < L; j++) {
+        vf.at(dst + j) = __builtin_addc(k.gconsts[s.p[0] + j], j ? 0u : off, cy, &cy);
       }
+      break;
+    }
+    case MG_GEN_DICT: {
+      const uint32_t e = ((grnd(ky, c, 0xFFFFu) >> 16) * s.p[1]) >> 16;
+      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = k.gconsts[s.p[0] + e * L + j];
       break;
     }
     case MG_GEN_ALIGNED: {
-      const uint32_t cnt = s.p[2];
-      const uint32_t r = rnd(key, cc, 0);
+      const uint32_t cnt = s.p[2], r = grnd(ky, c, 0);
       const uint64_t m = cnt ? (((uint64_t)r * cnt) >> 32) : r;
       const uint32_t sh = s.p[1];
-      uint64_t carry = 0;
-      for (uint32_t j = 0; j < Lg; j++) {
-        const int32_t bit0 = (int32_t)(j * 32) - (int32_t)sh;  // word j of (m << sh)
+      uint32_t cy = 0;
+      for (uint32_t j = 0; j < L; j++) {
+        const int32_t bit0 = (int32_t)(j * 32) - (int32_t)sh;
         uint32_t mw;
         if (bit0 <= -32 || bit0 >= 64) mw = 0;
         else if (bit0 < 0) mw = (uint32_t)(m << (-bit0));
         else mw = (uint32_t)(m >> bit0);
-        uint64_t t = (uint64_t)k.gconsts[s.p[0] + j] + mw + carry;
-        vf.at(dst + j) = (uint32_t)t;
-        carry = t >> 32;
+        vf.at(dst + j) = __builtin_addc(k.gconsts[s.p[0] + j], mw, cy, &cy);
       }
       break;
     }
-    case MG_GEN_FIXED: {
-      for (uint32_t j = 0; j < Lg; j++) vf.at(dst + j) = k.gconsts[s.p[0] + j];
+    case MG_GEN_FIXED:
+      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = k.gconsts[s.p[0] + j];
+      break;
+    case MG_GEN_MIXED: {
+      const uint32_t h = grnd(ky, c, 0xFFFFu);
+      if (alt == ALT_DICT) {
+        const uint32_t e = ((h >> 16) * s.p[1]) >> 16;
+        for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = k.gconsts[s.p[0] + e * L + j];
+      } else {  // SMALL / UNIFORM
+        const bool narrow = width <= MG_GEN_NARROW_BITS;
+        const uint32_t bits = alt == ALT_SMALL ? min(width, s.p[4] >> 16) : width;
+        for (uint32_t j = 0; j < L; j++) {
+          const uint32_t v = narrow ? (j == 0 ? (h & 0xFFFFu) : 0u) : grnd(ky, c, j);
+          const uint32_t lo = j * 32;
+          vf.at(dst + j) = lo >= bits ? 0u : (bits - lo >= 32 ? v : (v & ((1u << (bits - lo)) - 1u)));
+        }
+      }
       break;
     }
-    default: {  // UNIFORM (and LAZY coordinates, which the program never reads)
-      for (uint32_t j = 0; j < Lg; j++) vf.at(dst + j) = rnd(key, cc, j);
+    default:  // UNIFORM (and LAZY coordinates, which the program never reads)
+      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = grnd(ky, c, j);
       break;
+  }
+}
+
+// MIXED: per-lane delta on COPY/DICT, width mask, clamp; every kind: width mask, fixed bits
+template <class VF>
+__device__ void gen_finish(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c, uint32_t width,
+                           const GKeys& ky, const GenSpec& s, uint32_t alt, uint32_t ws) {
+  const uint32_t L = (width + 31) >> 5;
+  if (MG_GEN_KIND(s.kind) == MG_GEN_MIXED) {
+    if ((alt == ALT_COPY || alt == ALT_DICT) && (ws >> 16) < s.p[5]) {
+      const uint32_t h = grnd(ky, c, 0xFFFFu);
+      const uint32_t mag = 1u + (h & 1u);
+      const bool sub = (h >> 1) & 1u;
+      const uint32_t a0 = sub ? 0u - mag : mag, ah = sub ? 0xFFFFFFFFu : 0u;  // +/-mag sign-extended
+      uint32_t cy = 0;
+      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = __builtin_addc(vf.at(dst + j), j ? ah : a0, cy, &cy);
+    }
+    vf.at(dst + L - 1) &= top_mask(width);
+    if (s.p[6]) {  // clamp into [lo, lo + span)
+      const uint32_t* lo = k.gconsts + (s.p[6] - 1);
+      const uint32_t span = lo[L];
+      uint32_t br = 0, hi_or = 0, t0 = 0;
+      for (uint32_t j = 0; j < L; j++) {
+        const uint32_t t = __builtin_subc(vf.at(dst + j), lo[j], br, &br);
+        if (j == 0) t0 = t;
+        else hi_or |= t;
+      }
+      if (br || hi_or || (span && t0 >= span)) {
+        const uint32_t v0 = vf.at(dst);
+        const uint32_t off = span ? (uint32_t)(((uint64_t)v0 * span) >> 32) : v0;
+        uint32_t cy = 0;
+        for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = __builtin_addc(lo[j], j ? 0u : off, cy, &cy);
+      }
     }
   }
-  // a copy is the source's value: masked to the source width, then truncated / zero-extended
-  if (cc != c && Lg == ((k.coord_width[cc] + 31) >> 5)) vf.at(dst + Lg - 1) &= top_mask(k.coord_width[cc]);
-  for (uint32_t j = Lg; j < L; j++) vf.at(dst + j) = 0;
-  write_masked(vf, dst, L, width);
-  // fixed bits: v = (v & ~mask) | value — the copied source's fix first, then this coordinate's
-  if (cc != c && fix_src) {
-    const uint32_t* f = k.gconsts + (fix_src - 1);
-    const uint32_t Ls = (k.coord_width[cc] + 31) >> 5;
-    for (uint32_t j = 0; j < Lg; j++) vf.at(dst + j) = (vf.at(dst + j) & ~f[j]) | f[Ls + j];
-  }
-  if (fix_dst) {
-    const uint32_t* f = k.gconsts + (fix_dst - 1);
+  vf.at(dst + L - 1) &= top_mask(width);
+  if (const uint32_t fix = s.kind >> 8) {
+    const uint32_t* f = k.gconsts + (fix - 1);
     for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = (vf.at(dst + j) & ~f[j]) | f[L + j];
+  }
+}
+
+// Final value of coordinate c.  A MIXED COPY is the source's final value; the chain
+// c -> p3 -> ... ends at the first link whose group choice is not COPY (sources have
+// smaller indices, so it ends; parse_gen bounds its static length).  The root is
+// generated, then every link's finish is applied from the root back to c.
+template <class VF>
+__device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c, uint32_t width, const GKeys& ky) {
+  uint32_t m = 0, root = c;
+  GenSpec s = k.specs[c];
+  uint32_t ws = 0, alt = ALT_NONE;
+  for (;;) {
+    alt = ALT_NONE;
+    if (MG_GEN_KIND(s.kind) != MG_GEN_MIXED) break;
+    ws = gwsel(ky, root);
+    alt = mixed_alt(s, ws);
+    if (alt != ALT_COPY) break;
+    root = s.p[3];
+    s = k.specs[root];
+    m++;
+  }
+  gen_base(k, vf, dst, root, width, ky, s, alt);
+  gen_finish(k, vf, dst, root, width, ky, s, alt, ws);
+  while (m-- > 0) {  // link m: m steps from c
+    uint32_t l = c;
+    for (uint32_t t = 0; t < m; t++) l = k.specs[l].p[3];
+    const GenSpec sl = k.specs[l];
+    gen_finish(k, vf, dst, l, width, ky, sl, ALT_COPY, gwsel(ky, l));
   }
 }
 
 // ---------------------------------------------------------------------------
 // value-file helpers
 // ---------------------------------------------------------------------------
+template <class VF>
+__device__ __forceinline__ void write_masked(const VF& vf, uint32_t dst, uint32_t L, uint32_t width) {
+  vf.at(dst + L - 1) &= top_mask(width);
+}
+
 template <class VF>
 __device__ __forceinline__ W8 ld8(const VF& vf, uint32_t off, uint32_t L) {
   W8 x;
@@ -314,8 +299,8 @@ __device__ void do_keccak(const VF& vf, const Instr& in) {
 // interpreter
 // ---------------------------------------------------------------------------
 template <class VF, int MODE>
-__device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, uint64_t i, uint32_t key,
-                                                bool early) {
+__device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, uint64_t i, const GKeys& key,
+                                                bool early, bool active) {
   uint32_t verdict = 1;
   const Instr* code = k.code;
   const uint32_t n_instr = k.n_instr;
@@ -515,7 +500,7 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
         break;
       }
       case K_WATCH: {
-        if (MODE != MODE_SEARCH && k.watch) {
+        if (MODE != MODE_SEARCH && k.watch && active) {
           for (uint32_t j = 0; j < L; j++) k.watch[(uint64_t)(in.p0 + j) * k.count + i] = vf.at(in.a + j);
         }
         break;
@@ -531,30 +516,36 @@ template <class VF, int MODE>
 __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
   extern __shared__ uint32_t lds[];
   VF vf(lds, k);
-  const uint64_t total = k.count;
+  // EVAL sweeps rows [0, count); GEN / SEARCH sweep the aligned 64-index groups that
+  // cover [start, start + count), one group per wave (the GEN2 group key is per wave)
+  const uint64_t a0 = (MODE == MODE_EVAL) ? 0ull : (k.start & ~63ull);
+  const uint64_t end = k.start + k.count;
+  const uint64_t total = (MODE == MODE_EVAL) ? k.count : (end - a0);
   const uint64_t step = (uint64_t)gridDim.x * kWave;
   const bool early = (MODE == MODE_SEARCH) && (k.flags & MG_SEARCH_EARLY_EXIT);
   uint64_t wave_best = ~0ull, wave_hits = 0;  // wave-uniform; published once per wave
   for (uint64_t base = (uint64_t)blockIdx.x * kWave; base < total; base += step) {
-    const uint64_t i_raw = base + threadIdx.x;
-    const bool active = i_raw < total;
-    const uint64_t i = active ? i_raw : (total - 1);
-    const uint64_t idx = k.start + i;
+    const uint64_t off = base + threadIdx.x;
+    const uint64_t idx = a0 + off;  // candidate index (GEN / SEARCH)
+    const bool active = (MODE == MODE_EVAL) ? off < total : (idx >= k.start && idx < end);
+    // EVAL: SoA row; GEN: output row (only written by active lanes)
+    const uint64_t i = (MODE == MODE_EVAL) ? (active ? off : total - 1) : (idx - k.start);
     if (early) {
       // every candidate below the current first hit is still evaluated, so the
       // final minimum is exact; waves entirely above it stop
       const unsigned long long cur = __hip_atomic_load(k.first_hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint64_t cur_u = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) |
                              __builtin_amdgcn_readfirstlane((uint32_t)cur);
-      if (k.start + base >= cur_u) break;
+      if (a0 + base >= cur_u) break;
     }
-    const uint32_t key = (MODE == MODE_EVAL) ? 0u : cand_key(idx, k.seed);
-    uint32_t v = run_program<VF, MODE>(k, vf, i, key, early);
+    GKeys key{};
+    if (MODE != MODE_EVAL) key = gen_keys(idx, k.sk, k.sg);
+    uint32_t v = run_program<VF, MODE>(k, vf, i, key, early, active);
     v = active ? v : 0u;
     if (MODE == MODE_SEARCH) {
       const unsigned long long m = __ballot(v != 0);
       if (m) {
-        const uint64_t first = k.start + base + (uint64_t)(__ffsll((long long)m) - 1);
+        const uint64_t first = a0 + base + (uint64_t)(__ffsll((long long)m) - 1);
         wave_hits += (uint64_t)__popcll(m);
         if (first < wave_best) {
           wave_best = first;
@@ -705,7 +696,11 @@ static uint32_t grid_for(const Engine& e, uint64_t count, bool lds, uint32_t val
 template <int MODE>
 static int launch(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   if (count == 0) return MG_OK;
-  const uint32_t grid = grid_for(e, count, p.lds, p.low.value_words);
+  // GEN / SEARCH sweep whole aligned 64-index groups (k_run)
+  const uint64_t lanes = MODE == MODE_EVAL ? count : (k.start + count) - (k.start & ~63ull);
+  const uint32_t grid = grid_for(e, lanes, p.lds, p.low.value_words);
+  k.sk = seed_lane_key(k.seed);
+  k.sg = seed_group_key(k.seed);
   k.code = p.d_code;
   k.consts = p.d_consts;
   k.aux = p.d_aux;
@@ -745,7 +740,7 @@ using namespace mg;
 
 extern "C" {
 
-int mg_version(void) { return 1; }
+int mg_version(void) { return 2; }
 
 const char* mg_last_error(void) { return g_err.c_str(); }
 
@@ -1230,11 +1225,12 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
   unsigned long long init[2] = {~0ull, 0ull};
   HIPCHK(hipMemcpyAsync(e.d_hit, init, sizeof(init), hipMemcpyHostToDevice, e.stream));
   const uint32_t* gconsts = git->second->d_consts;
-  const GenSpec* specs = git->second->d_specs;
-  const uint32_t* cw = p->d_coord_width;
   unsigned long long* hitp = e.d_hit;
-  void* args[] = {&gconsts, &specs, &cw, &start, &count, &seed, &hitp, &flags};
-  int rc = jit_launch(e, j.fsearch, j.nb_search, count, args);
+  uint64_t sk = seed_lane_key(seed), sg = seed_group_key(seed);
+  void* args[] = {&gconsts, &start, &count, &sk, &sg, &hitp, &flags};
+  // one wave per aligned 64-index group
+  const uint64_t lanes = (start + count) - (start & ~63ull);
+  int rc = jit_launch(e, j.fsearch, j.nb_search, lanes, args);
   if (rc) return rc;
   unsigned long long res[2];
   HIPCHK(hipMemcpy(res, e.d_hit, sizeof(res), hipMemcpyDeviceToHost));

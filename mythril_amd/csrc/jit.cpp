@@ -8,6 +8,7 @@
 #include <dlfcn.h>
 
 #include <cstdio>
+#include <map>
 #include <cstdlib>
 #include <cstring>
 #include <sstream>
@@ -34,11 +35,392 @@ struct Gen {
       if (P.vcode[k].dst != MG_NONE && P.vcode[k].dst < def.size() && def[P.vcode[k].dst] < 0)
         def[P.vcode[k].dst] = (int32_t)k;
   }
-  const Instr* def_of(uint32_t id) const { return def[id] >= 0 ? &P.vcode[def[id]] : nullptr; }
+  const Instr* def_of(uint32_t id) const {
+    id = res(id);
+    return def[id] >= 0 ? &P.vcode[def[id]] : nullptr;
+  }
   // literal limbs of a value defined by K_CONST (else nullptr)
   const uint32_t* lit(uint32_t id) const {
     const Instr* d = def_of(id);
     return (d && d->op == K_CONST) ? &P.consts[d->p0] : nullptr;
+  }
+
+  // ---- value ranges, folding and aliases (analyze) ---------------------------
+  // rng[id]: when known, the value lies in [lo, hi] (so it fits in 64 bits).  In the
+  // search kernel a coordinate's range comes from its generator spec, which bounds
+  // EVERY candidate the kernel evaluates (clamp records, dictionaries, fixed bits), so a
+  // comparison decided by the ranges is decided for every candidate: it folds to a
+  // literal, an ITE on it becomes an alias of the chosen arm, and bits() then looks
+  // through it (e.g. the calldata guard If(k < size, calldata[k], 0) with size drawn
+  // from [68, 2^32) collapses to the byte, and a CALLDATALOAD to its AUX word).
+  struct Rng {
+    bool k = false;
+    uint64_t lo = 0, hi = 0;
+  };
+  std::vector<Rng> rng;
+  std::vector<int8_t> fold;       // per id: -1, or the folded Bool value
+  std::vector<uint32_t> alias;    // per id: the id it equals (itself if none)
+  std::vector<char> skip;         // per instruction: defines an alias / a decided assert
+  std::vector<Rng> crng;          // per coordinate (search mode)
+
+  uint32_t res(uint32_t id) const {
+    if (alias.empty() || id >= alias.size()) return id;
+    while (alias[id] != id) id = alias[id];
+    return id;
+  }
+  static Rng full(uint32_t w) {
+    Rng r;
+    if (w <= 64) {
+      r.k = true;
+      r.hi = w == 64 ? ~0ull : ((1ull << w) - 1ull);
+    }
+    return r;
+  }
+  static Rng exact(uint64_t v) {
+    Rng r;
+    r.k = true;
+    r.lo = r.hi = v;
+    return r;
+  }
+  static Rng hull(const Rng& a, const Rng& b) {
+    Rng r;
+    if (!a.k || !b.k) return r;
+    r.k = true;
+    r.lo = std::min(a.lo, b.lo);
+    r.hi = std::max(a.hi, b.hi);
+    return r;
+  }
+  // limbs [0, L) as one u64 if every limb >= 2 is zero
+  static bool fits64(const uint32_t* x, uint32_t L, uint64_t* v) {
+    for (uint32_t j = 2; j < L; j++)
+      if (x[j]) return false;
+    *v = (uint64_t)x[0] | (L > 1 ? (uint64_t)x[1] << 32 : 0ull);
+    return true;
+  }
+
+  // range of a generated coordinate's final value (include/mythgpu.h GEN2)
+  Rng coord_range(uint32_t c) const {
+    const GenSpec& sp = (*specs)[c];
+    const uint32_t w = P.coord_width[c], L = Lw(w), kind = sp.kind & 0xFFu;
+    const auto& G = *gconsts;
+    const unsigned __int128 wlim = w >= 128 ? ~(unsigned __int128)0 : (((unsigned __int128)1 << w) - 1);
+    Rng r;
+    switch (kind) {
+      case MG_GEN_FIXED: {
+        uint64_t v;
+        if (fits64(&G[sp.p[0]], L, &v)) r = exact(v);
+        break;
+      }
+      case MG_GEN_DICT:
+      case MG_GEN_MIXED: {
+        Rng d;  // dictionary hull
+        bool ok = sp.p[1] > 0;
+        for (uint32_t e = 0; ok && e < sp.p[1]; e++) {
+          uint64_t v;
+          if (!fits64(&G[sp.p[0] + e * L], L, &v)) ok = false;
+          else d = d.k ? hull(d, exact(v)) : exact(v);
+        }
+        if (kind == MG_GEN_DICT) {
+          if (ok) r = d;
+          break;
+        }
+        if (sp.p[6]) {  // clamp record: the final value is inside [lo, lo + span)
+          uint64_t lo;
+          const uint32_t rec = sp.p[6] - 1;
+          if (fits64(&G[rec], L, &lo)) {
+            const uint64_t span = G[rec + L] ? G[rec + L] : (1ull << 32);
+            if ((unsigned __int128)lo + span - 1 <= (unsigned __int128)~0ull) {
+              r.k = true;
+              r.lo = lo;
+              r.hi = lo + span - 1;
+            }
+          }
+          break;
+        }
+        const uint32_t pc = sp.p[3] != MG_NONE ? (sp.p[2] & 0xFFFFu) : 0u;
+        const uint32_t pd = sp.p[1] ? (sp.p[2] >> 16) : 0u;
+        const uint32_t ps = sp.p[4] & 0xFFFFu;
+        Rng u;
+        bool have = false, unknown = false;
+        auto add = [&](const Rng& x) {
+          if (!x.k) unknown = true;
+          else u = have ? hull(u, x) : x;
+          have = true;
+        };
+        Rng cd;  // COPY / DICT part, before the delta
+        bool cd_have = false, cd_unknown = false;
+        if (pc) {
+          const Rng s = crng[sp.p[3]];
+          if (!s.k) cd_unknown = true;
+          else cd = s;
+          cd_have = true;
+        }
+        if (pd) {
+          if (!ok) cd_unknown = true;
+          else cd = cd_have && cd.k ? hull(cd, d) : d;
+          cd_have = true;
+        }
+        if (cd_have) {
+          if (cd_unknown) add(Rng{});
+          else if (sp.p[5]) {  // +/-2 at most, no wrap
+            if (cd.lo >= 2 && (unsigned __int128)cd.hi + 2 <= wlim && cd.hi + 2 > cd.hi) {
+              Rng x;
+              x.k = true;
+              x.lo = cd.lo - 2;
+              x.hi = cd.hi + 2;
+              add(x);
+            } else {
+              add(full(w));
+            }
+          } else {
+            add(cd);
+          }
+        }
+        const uint32_t sb = std::min(w, sp.p[4] >> 16);
+        if (ps) add(full(sb));
+        if (pc + pd + ps < 65536u) add(full(w));
+        if (have && !unknown) r = u;
+        break;
+      }
+      case MG_GEN_RANGE: {
+        uint64_t lo;
+        if (fits64(&G[sp.p[0]], L, &lo)) {
+          const uint64_t span = sp.p[1] ? sp.p[1] : (1ull << 32);
+          if ((unsigned __int128)lo + span - 1 <= wlim && (unsigned __int128)lo + span - 1 <= (unsigned __int128)~0ull) {
+            r.k = true;
+            r.lo = lo;
+            r.hi = lo + span - 1;
+          }
+        }
+        break;
+      }
+      case MG_GEN_ALIGNED: {
+        uint64_t lo;
+        if (fits64(&G[sp.p[0]], L, &lo) && sp.p[1] < 64) {
+          const unsigned __int128 cnt = sp.p[2] ? sp.p[2] : (1ull << 32);
+          const unsigned __int128 top = (unsigned __int128)lo + ((cnt - 1) << sp.p[1]);
+          if (top <= wlim && top <= (unsigned __int128)~0ull) {
+            r.k = true;
+            r.lo = lo;
+            r.hi = (uint64_t)top;
+          }
+        }
+        break;
+      }
+      default:  // UNIFORM / LAZY
+        r = full(w);
+        break;
+    }
+    if (!r.k) r = full(w);
+    if (const uint32_t fix = sp.kind >> 8) {  // (v & ~m) | val lies in [val, val | ~m]
+      const uint32_t f = fix - 1;
+      uint64_t m, val;
+      std::vector<uint32_t> nm(L);
+      for (uint32_t j = 0; j < L; j++) nm[j] = ~G[f + j];
+      if (w & 31) nm[L - 1] &= (1u << (w & 31)) - 1u;
+      if (fits64(&G[f + L], L, &val) && fits64(nm.data(), L, &m)) {
+        r.k = true;
+        r.lo = val;
+        r.hi = val | m;
+      } else {
+        r = Rng{};
+      }
+    }
+    return r;
+  }
+
+  // decide a comparison from operand ranges: -1 undecided, else 0 / 1
+  static int decide(uint32_t op, const Rng& a, const Rng& b, uint32_t wa) {
+    if (!a.k || !b.k) return -1;
+    if (op == K_SLT || op == K_SLE) {
+      const uint64_t sign = wa >= 65 ? 0ull : (1ull << (wa - 1));
+      if (sign && (a.hi >= sign || b.hi >= sign)) return -1;  // a negative value may be inside
+      op = op == K_SLT ? K_ULT : K_ULE;
+    }
+    switch (op) {
+      case K_ULT:
+        if (a.hi < b.lo) return 1;
+        if (a.lo >= b.hi) return 0;
+        return -1;
+      case K_ULE:
+        if (a.hi <= b.lo) return 1;
+        if (a.lo > b.hi) return 0;
+        return -1;
+      case K_EQ:
+        if (a.lo == a.hi && b.lo == b.hi && a.lo == b.lo) return 1;
+        if (a.hi < b.lo || b.hi < a.lo) return 0;
+        return -1;
+      default:
+        return -1;
+    }
+  }
+
+  void analyze(bool search) {
+    const size_t nv = P.vwidth.size();
+    rng.assign(nv, Rng{});
+    fold.assign(nv, -1);
+    alias.resize(nv);
+    for (size_t i = 0; i < nv; i++) alias[i] = (uint32_t)i;
+    skip.assign(P.vcode.size(), 0);
+    if (search && specs) {
+      crng.assign(P.n_coords, Rng{});
+      for (uint32_t c = 0; c < P.n_coords; c++) crng[c] = coord_range(c);
+    }
+    for (size_t k = 0; k < P.vcode.size(); k++) {
+      const Instr& in = P.vcode[k];
+      const uint32_t d = in.dst, W = in.wd;
+      auto R = [&](uint32_t id) { return rng[res(id)]; };
+      auto F = [&](uint32_t id) { return (int)fold[res(id)]; };
+      auto alias_to = [&](uint32_t src) {
+        alias[d] = res(src);
+        rng[d] = rng[res(src)];
+        fold[d] = fold[res(src)];
+        skip[k] = 1;
+      };
+      auto set_fold = [&](int v) {
+        fold[d] = (int8_t)v;
+        rng[d] = exact((uint64_t)v);
+      };
+      if (d == MG_NONE || d >= nv) {
+        if (in.op == K_ASSERT && F(in.a) == 1) skip[k] = 1;
+        continue;
+      }
+      Rng r = full(W);
+      switch (in.op) {
+        case K_CONST: {
+          uint64_t v;
+          if (fits64(&P.consts[in.p0], Lw(W), &v)) r = exact(v);
+          break;
+        }
+        case K_COORD:
+          if (search && specs) r = crng[in.p0];
+          break;
+        case K_COPY:
+          alias_to(in.a);
+          continue;
+        case K_ZEXT:
+          if (R(in.a).k) r = R(in.a);
+          break;
+        case K_EXTRACT: {
+          const Rng a = R(in.a);
+          if (a.k && in.p0 < 64 && (W >= 64 || (a.hi >> in.p0) < (1ull << W))) {
+            r.k = true;
+            r.lo = a.lo >> in.p0;
+            r.hi = a.hi >> in.p0;
+          } else if (a.k && in.p0 >= 64) {
+            r = exact(0);
+          }
+          break;
+        }
+        case K_CONCAT: {
+          const Rng a = R(in.a), b = R(in.b);
+          const uint32_t wb = in.p1;
+          if (a.k && b.k && wb < 64 && (a.hi >> (64 - wb)) == 0) {
+            r.k = true;
+            r.lo = (a.lo << wb) | b.lo;
+            r.hi = (a.hi << wb) | b.hi;
+          }
+          break;
+        }
+        case K_AND:
+        case K_OR:
+        case K_XOR: {
+          const int fa = F(in.a), fb = F(in.b);
+          if (W == 1) {
+            if (in.op == K_AND) {
+              if (fa == 0 || fb == 0) { set_fold(0); continue; }
+              if (fa == 1) { alias_to(in.b); continue; }
+              if (fb == 1) { alias_to(in.a); continue; }
+            } else if (in.op == K_OR) {
+              if (fa == 1 || fb == 1) { set_fold(1); continue; }
+              if (fa == 0) { alias_to(in.b); continue; }
+              if (fb == 0) { alias_to(in.a); continue; }
+            } else if (fa >= 0 && fb >= 0) {
+              set_fold(fa ^ fb);
+              continue;
+            }
+            break;
+          }
+          const Rng a = R(in.a), b = R(in.b);
+          if (in.op == K_AND) {
+            if (a.k || b.k) {
+              r.k = true;
+              r.lo = 0;
+              r.hi = std::min(a.k ? a.hi : ~0ull, b.k ? b.hi : ~0ull);
+            }
+          } else if (a.k && b.k) {
+            const uint64_t m = std::max(a.hi, b.hi);
+            r.k = true;
+            r.lo = 0;
+            r.hi = m ? (~0ull >> __builtin_clzll(m)) : 0ull;
+          }
+          break;
+        }
+        case K_NOT:
+          if (W == 1 && F(in.a) >= 0) {
+            set_fold(1 - F(in.a));
+            continue;
+          }
+          break;
+        case K_ITE: {
+          const int fc = F(in.a);
+          if (fc >= 0) {
+            alias_to(fc ? in.b : in.c);
+            continue;
+          }
+          const Rng h = hull(R(in.b), R(in.c));
+          if (h.k) r = h;
+          break;
+        }
+        case K_ADD: {
+          const Rng a = R(in.a), b = R(in.b);
+          if (a.k && b.k && (unsigned __int128)a.hi + b.hi <= (unsigned __int128)full(std::min(W, 64u)).hi) {
+            r.k = true;
+            r.lo = a.lo + b.lo;
+            r.hi = a.hi + b.hi;
+          }
+          break;
+        }
+        case K_SUB: {
+          const Rng a = R(in.a), b = R(in.b);
+          if (a.k && b.k && a.lo >= b.hi) {
+            r.k = true;
+            r.lo = a.lo - b.hi;
+            r.hi = a.hi - b.lo;
+          }
+          break;
+        }
+        case K_EQ:
+        case K_ULT:
+        case K_ULE:
+        case K_SLT:
+        case K_SLE: {
+          const int v = decide(in.op, R(in.a), R(in.b), in.p1);
+          if (v >= 0) {
+            set_fold(v);
+            continue;
+          }
+          break;
+        }
+        case K_LOOKUP: {
+          if (in.c == 0) {  // no earlier site can share the key: the default
+            alias_to(in.p0);
+            continue;
+          }
+          Rng h = R(in.p0);
+          for (uint32_t p = 0; p < in.c && h.k; p++) h = hull(h, R(P.vaux[in.p1 + 2 * p + 1]));
+          if (h.k) r = h;
+          break;
+        }
+        default:
+          break;
+      }
+      if (r.k && W < 64) {  // intersect with the width
+        const uint64_t m = (1ull << W) - 1ull;
+        if (r.hi > m) r = full(W);
+      }
+      rng[d] = r;
+    }
   }
 
   // A dictionary of n entries of a coordinate at most 32 bits wide whose n*width bits fit in 64 is
@@ -56,151 +438,175 @@ struct Gen {
     return t.str();
   }
 
-  // Branch-free, spec-specialised generator for coordinate c (same function of
-  // (key, c) as gen_coord in engine.hip / gen_regs in jit_device.h): every
-  // alternative is computed and the winner picked with selects, so the kernel
-  // keeps a tiny CFG (hipRTC compile time is dominated by register coalescing
-  // over basic blocks otherwise).  Writes limbs into `out` names.
-  void gen_value(uint32_t c, uint32_t width, const std::string& out, bool allow_copy, int depth) {
-    GenSpec sp = (*specs)[c];
+  // Spec-specialised GEN2 generator for coordinate c (the same function of (seed, index, c)
+  // as gen_coord in engine.hip and gen_value in oracle/bveval.c).  Writes L limbs into
+  // `out`_j.  A MIXED coordinate's alternative comes from the group key (SGPRs), so the
+  // alternatives are scalar branches: a lane computes only the one its wave chose.
+  std::map<uint32_t, std::string> coord_var;  // coordinate -> prefix of its generated (final) limbs
+  int tmp_id = 0;
+
+  std::string gen_coord_value(uint32_t c) {
+    auto it = coord_var.find(c);
+    if (it != coord_var.end()) return it->second;
+    // a copy source with no K_COORD of its own: generate it into temporaries
+    const std::string pre = "cg" + std::to_string(c) + "_" + std::to_string(tmp_id++);
+    const uint32_t L = Lw(P.coord_width[c]);
+    o << "  uint32_t";
+    for (uint32_t j = 0; j < L; j++) o << (j ? ", " : " ") << pre << "_" << j;
+    o << ";\n";
+    gen_value(c, pre);
+    return pre;
+  }
+
+  void gen_value(uint32_t c, const std::string& out) {
+    const GenSpec sp = (*specs)[c];
     const uint32_t fix = sp.kind >> 8;  // 1 + const offset of (mask, value) limbs, 0: none
-    sp.kind &= 0xFFu;
+    const uint32_t kind = sp.kind & 0xFFu;
+    const uint32_t width = P.coord_width[c];
     const uint32_t L = Lw(width);
-    const uint32_t Lc = Lw(P.coord_width[c]);  // limb stride of this coordinate's constants
-    const uint32_t Lg = std::min(L, Lc);
     const std::string C = std::to_string(c) + "u";
-    auto lim = [&](const std::string& base, uint32_t j) { return base + "_" + std::to_string(j); };
+    auto lim = [&](uint32_t j) { return out + "_" + std::to_string(j); };
+    const auto& G = *gconsts;
+    if (kind == MG_GEN_MIXED && sp.p[3] != MG_NONE && (sp.p[2] & 0xFFFFu)) gen_coord_value(sp.p[3]);
     o << "  {\n";
-    switch (sp.kind) {
+    switch (kind) {
       case MG_GEN_MIXED: {
-        const uint32_t pc = (allow_copy && sp.p[3] != MG_NONE) ? sp.p[4] : 0u;
-        const uint32_t pd = sp.p[1] ? sp.p[2] : 0u;
-        const uint32_t ps = sp.p[6] & 0xFFFFu;
-        const uint32_t bits = std::min(width, sp.p[6] >> 16);
-        o << "  const uint32_t h" << depth << " = rnd(key, " << C << ", 0xFFFFu);\n";
-        o << "  const uint32_t sel" << depth << " = h" << depth << " & 0xFFFFu;\n";
-        // uniform / small
-        // narrow coordinates (MG_GEN_NARROW_BITS) take their uniform / small value from h >> 16
-        const bool narrow = P.coord_width[c] <= MG_GEN_NARROW_BITS;
-        for (uint32_t j = 0; j < L; j++)
-          o << "  const uint32_t u" << depth << "_" << j << " = "
-            << (narrow ? (j ? std::string("0u") : "(h" + std::to_string(depth) + " >> 16)")
-                       : "rnd(key, " + C + ", " + std::to_string(j) + "u)")
-            << ";\n";
-        // dictionary (+ delta)
-        if (pd) {
-          o << "  const uint32_t de" << depth << " = ((h" << depth << " >> 16) * " << sp.p[1] << "u) >> 16;\n";
-          const std::string packed = packed_dict(sp.p[0], sp.p[1], P.coord_width[c], "de" + std::to_string(depth));
-          for (uint32_t j = 0; j < L; j++)
-            o << "  uint32_t d" << depth << "_" << j << " = "
-              << (j < Lg ? (!packed.empty() ? (j ? std::string("0u") : packed)
-                                            : ("gconsts[" + std::to_string(sp.p[0] + j) + "u + de" + std::to_string(depth) + " * " + std::to_string(Lc) + "u]"))
-                         : std::string("0u"))
-              << ";\n";
-          if (sp.p[5]) {
-            o << "  { const uint32_t rr = " << (narrow ? "rnd(key, " + C + ", 0u)" : "u" + std::to_string(depth) + "_0")
-            << "; const bool on = (rr & 0xFFFFu) < " << sp.p[5]
-              << "u; const uint32_t mag = on ? (((rr >> 16) & 1u) + 1u) : 0u; const bool sb = (rr >> 17) & 1u;"
-              // d -/+ mag (mod 2^(32 Lg)) as ONE carry chain: add the sign-extended +/-mag
-              << " const uint32_t a0 = sb ? 0u - mag : mag, ah = (sb && mag) ? 0xFFFFFFFFu : 0u; uint32_t cy = 0u;";
-            for (uint32_t j = 0; j < Lg; j++)
-              o << " d" << depth << "_" << j << " = __builtin_addc(d" << depth << "_" << j << ", " << (j ? "ah" : "a0")
-                << ", cy, &cy);";
-            o << " (void)cy; (void)ah; }\n";
+        const uint32_t pc = sp.p[3] != MG_NONE ? (sp.p[2] & 0xFFFFu) : 0u;
+        const uint32_t pd = sp.p[1] ? (sp.p[2] >> 16) : 0u;
+        const uint32_t ps = sp.p[4] & 0xFFFFu;
+        const uint32_t small_bits = std::min(width, sp.p[4] >> 16);
+        const bool narrow = width <= MG_GEN_NARROW_BITS;
+        o << "  const uint32_t ws = gwsel(ky, " << C << "), sel = ws & 0xFFFFu;\n";
+        o << "  const uint32_t h = grnd(ky, " << C << ", 0xFFFFu);\n";
+        // uniform / small limbs (one draw per limb; narrow: from h)
+        auto uni = [&](uint32_t bits) {
+          for (uint32_t j = 0; j < L; j++) {
+            const uint32_t lo = 32 * j;
+            const uint32_t m = lo >= bits ? 0u : (bits - lo >= 32 ? 0xFFFFFFFFu : ((1u << (bits - lo)) - 1u));
+            std::string e = narrow ? (j ? std::string("0u") : std::string("(h & 0xFFFFu)"))
+                                   : "grnd(ky, " + C + ", " + std::to_string(j) + "u)";
+            if (m == 0) e = "0u";
+            else if (m != 0xFFFFFFFFu) e = "(" + e + " & " + hex(m) + ")";
+            o << "    " << lim(j) << " = " << e << ";\n";
           }
-        }
-        // copy of another coordinate (its own spec, no further copy)
+        };
+        bool first = true;
+        auto branch = [&](const std::string& cond) {
+          o << (first ? "  if (" : "  } else if (") << cond << ") {\n";
+          first = false;
+        };
         if (pc) {
-          const uint32_t src = sp.p[3];
-          const uint32_t sw = P.coord_width[src];
-          const uint32_t Ls = Lw(sw);
-          for (uint32_t j = 0; j < L; j++) o << "  uint32_t k" << depth << "_" << j << " = 0u;\n";
-          o << "  uint32_t";
-          for (uint32_t j = 0; j < Ls; j++) o << (j ? ", " : " ") << "kk" << depth << "_" << j;
-          o << ";\n";
-          gen_value(src, sw, "kk" + std::to_string(depth), false, depth + 1);
-          for (uint32_t j = 0; j < L && j < Ls; j++)
-            o << "  k" << depth << "_" << j << " = kk" << depth << "_" << j << ";\n";
+          branch("sel < " + std::to_string(pc) + "u");
+          const std::string src = coord_var.at(sp.p[3]);
+          for (uint32_t j = 0; j < L; j++) o << "    " << lim(j) << " = " << src << "_" << j << ";\n";
         }
-        for (uint32_t j = 0; j < L; j++) {
-          const uint32_t lo = 32 * j;
-          uint32_t smask = lo >= bits ? 0u : (bits - lo >= 32 ? 0xFFFFFFFFu : ((1u << (bits - lo)) - 1u));
-          std::string e = "u" + std::to_string(depth) + "_" + std::to_string(j);
-          if (ps) e = "(sel" + std::to_string(depth) + " < " + std::to_string(pc + pd + ps) + "u ? (" + e + " & " + hex(smask) + ") : " + e + ")";
-          if (pd) e = "(sel" + std::to_string(depth) + " < " + std::to_string(pc + pd) + "u ? d" + std::to_string(depth) + "_" + std::to_string(j) + " : " + e + ")";
-          if (pc) e = "(sel" + std::to_string(depth) + " < " + std::to_string(pc) + "u ? k" + std::to_string(depth) + "_" + std::to_string(j) + " : " + e + ")";
-          o << "  " << lim(out, j) << " = " << e << ";\n";
+        if (pd) {
+          branch("sel < " + std::to_string(pc + pd) + "u");
+          o << "    const uint32_t e = ((h >> 16) * " << sp.p[1] << "u) >> 16;\n";
+          const std::string packed = packed_dict(sp.p[0], sp.p[1], width, "e");
+          for (uint32_t j = 0; j < L; j++)
+            o << "    " << lim(j) << " = "
+              << (!packed.empty() ? (j ? std::string("0u") : packed)
+                                  : "gconsts[" + std::to_string(sp.p[0] + j) + "u + e * " + std::to_string(L) + "u]")
+              << ";\n";
+        }
+        if (ps) {
+          branch("sel < " + std::to_string(pc + pd + ps) + "u");
+          uni(small_bits);
+        }
+        if (first) {
+          uni(width);
+        } else {
+          o << "  } else {\n";
+          uni(width);
+          o << "  }\n";
+        }
+        if (sp.p[5] && (pc || pd)) {
+          // +/-(1 + (h & 1)) on COPY / DICT as ONE carry chain over the sign-extended step
+          o << "  if ((ws >> 16) < " << sp.p[5] << "u && sel < " << (pc + pd) << "u) {"
+            << " const uint32_t mag = 1u + (h & 1u); const bool sb = (h >> 1) & 1u;"
+            << " const uint32_t a0 = sb ? 0u - mag : mag, ah = sb ? 0xFFFFFFFFu : 0u; uint32_t cy = 0u;";
+          for (uint32_t j = 0; j < L; j++)
+            o << " " << lim(j) << " = __builtin_addc(" << lim(j) << ", " << (j ? "ah" : "a0") << ", cy, &cy);";
+          o << " (void)cy; (void)ah; }\n";
+        }
+        if (width & 31) o << "  " << lim(L - 1) << " &= " << hex(topmask(width)) << ";\n";
+        if (sp.p[6]) {
+          const uint32_t r = sp.p[6] - 1;
+          const uint32_t span = G[r + L];
+          o << "  { uint32_t br = 0u, hz = 0u, t0;";
+          for (uint32_t j = 0; j < L; j++) {
+            if (j == 0) o << " t0 = __builtin_subc(" << lim(0) << ", " << hex(G[r]) << ", br, &br);";
+            else o << " hz |= __builtin_subc(" << lim(j) << ", " << hex(G[r + j]) << ", br, &br);";
+          }
+          o << " if (br | hz" << (span ? " | (uint32_t)(t0 >= " + hex(span) + ")" : std::string("")) << ") {"
+            << " const uint32_t off = " << (span ? "(uint32_t)(((uint64_t)" + lim(0) + " * " + std::to_string(span) + "ull) >> 32)" : lim(0))
+            << "; uint32_t cy = 0u;";
+          for (uint32_t j = 0; j < L; j++)
+            o << " " << lim(j) << " = __builtin_addc(" << hex(G[r + j]) << ", " << (j ? "0u" : "off") << ", cy, &cy);";
+          o << " (void)cy; } }\n";
         }
         break;
       }
       case MG_GEN_DICT: {
-        o << "  const uint32_t de = ((rnd(key, " << C << ", 0xFFFFu) >> 16) * " << sp.p[1] << "u) >> 16;\n";
-        const std::string packed = packed_dict(sp.p[0], sp.p[1], P.coord_width[c], "de");
+        o << "  const uint32_t e = ((grnd(ky, " << C << ", 0xFFFFu) >> 16) * " << sp.p[1] << "u) >> 16;\n";
+        const std::string packed = packed_dict(sp.p[0], sp.p[1], width, "e");
         for (uint32_t j = 0; j < L; j++)
-          o << "  " << lim(out, j) << " = "
-            << (j < Lg ? (!packed.empty() ? (j ? std::string("0u") : packed)
-                                          : ("gconsts[" + std::to_string(sp.p[0] + j) + "u + de * " + std::to_string(Lc) + "u]"))
-                       : std::string("0u"))
+          o << "  " << lim(j) << " = "
+            << (!packed.empty() ? (j ? std::string("0u") : packed)
+                                : "gconsts[" + std::to_string(sp.p[0] + j) + "u + e * " + std::to_string(L) + "u]")
             << ";\n";
         break;
       }
       case MG_GEN_RANGE: {
-        o << "  const uint32_t r = rnd(key, " << C << ", 0u); const uint32_t off = "
+        o << "  const uint32_t r = grnd(ky, " << C << ", 0u); const uint32_t off = "
           << (sp.p[1] ? ("(uint32_t)(((uint64_t)r * " + std::to_string(sp.p[1]) + "ull) >> 32)") : std::string("r"))
           << "; uint32_t cy = 0u;\n";
-        for (uint32_t j = 0; j < L; j++) {
-          if (j < Lg)
-            o << "  " << lim(out, j) << " = __builtin_addc(" << hex((*gconsts)[sp.p[0] + j]) << ", " << (j ? "0u" : "off")
-              << ", cy, &cy);\n";
-          else
-            o << "  " << lim(out, j) << " = 0u;\n";
-        }
+        for (uint32_t j = 0; j < L; j++)
+          o << "  " << lim(j) << " = __builtin_addc(" << hex(G[sp.p[0] + j]) << ", " << (j ? "0u" : "off")
+            << ", cy, &cy);\n";
         o << "  (void)cy;\n";
         break;
       }
       case MG_GEN_ALIGNED: {
-        o << "  const uint32_t r = rnd(key, " << C << ", 0u); const uint64_t m = "
+        o << "  const uint32_t r = grnd(ky, " << C << ", 0u); const uint64_t m = "
           << (sp.p[2] ? ("(((uint64_t)r * " + std::to_string(sp.p[2]) + "ull) >> 32)") : std::string("(uint64_t)r"))
           << "; uint32_t cy = 0u;\n";
         const int32_t sh = (int32_t)sp.p[1];
         for (uint32_t j = 0; j < L; j++) {
-          if (j >= Lg) {
-            o << "  " << lim(out, j) << " = 0u;\n";
-            continue;
-          }
           const int32_t bit0 = (int32_t)(j * 32) - sh;
           std::string mw;
           if (bit0 <= -32 || bit0 >= 64) mw = "0u";
           else if (bit0 < 0) mw = "(uint32_t)(m << " + std::to_string(-bit0) + ")";
           else mw = "(uint32_t)(m >> " + std::to_string(bit0) + ")";
-          o << "  " << lim(out, j) << " = __builtin_addc(" << hex((*gconsts)[sp.p[0] + j]) << ", " << mw << ", cy, &cy);\n";
+          o << "  " << lim(j) << " = __builtin_addc(" << hex(G[sp.p[0] + j]) << ", " << mw << ", cy, &cy);\n";
         }
         o << "  (void)cy;\n";
         break;
       }
       case MG_GEN_FIXED:
-        for (uint32_t j = 0; j < L; j++)
-          o << "  " << lim(out, j) << " = " << (j < Lg ? hex((*gconsts)[sp.p[0] + j]) : std::string("0u")) << ";\n";
+        for (uint32_t j = 0; j < L; j++) o << "  " << lim(j) << " = " << hex(G[sp.p[0] + j]) << ";\n";
         break;
       default:  // UNIFORM / LAZY
-        for (uint32_t j = 0; j < L; j++)
-          o << "  " << lim(out, j) << " = " << (j < Lg ? ("rnd(key, " + C + ", " + std::to_string(j) + "u)") : std::string("0u")) << ";\n";
+        for (uint32_t j = 0; j < L; j++) o << "  " << lim(j) << " = grnd(ky, " << C << ", " << j << "u);\n";
         break;
     }
-    if (width & 31) o << "  " << lim(out, L - 1) << " &= " << hex(topmask(width)) << ";\n";
+    if (width & 31) o << "  " << lim(L - 1) << " &= " << hex(topmask(width)) << ";\n";
     if (fix) {
       // fixed bits are literals here: (v & ~mask) | value
-      const uint32_t f = fix - 1, Lf = Lw(P.coord_width[c]);
-      for (uint32_t j = 0; j < L && j < Lf; j++) {
-        const uint32_t m = (*gconsts)[f + j], val = (*gconsts)[f + Lf + j];
-        if (m == 0xFFFFFFFFu) o << "  " << lim(out, j) << " = " << hex(val) << ";\n";
-        else if (m) o << "  " << lim(out, j) << " = (" << lim(out, j) << " & " << hex(~m) << ") | " << hex(val) << ";\n";
+      const uint32_t f = fix - 1;
+      for (uint32_t j = 0; j < L; j++) {
+        const uint32_t m = G[f + j], val = G[f + L + j];
+        if (m == 0xFFFFFFFFu) o << "  " << lim(j) << " = " << hex(val) << ";\n";
+        else if (m) o << "  " << lim(j) << " = (" << lim(j) << " & " << hex(~m) << ") | " << hex(val) << ";\n";
       }
     }
     o << "  }\n";
+    coord_var[c] = out;
   }
 
   std::string v(uint32_t id, uint32_t j) const {
+    id = res(id);
     if (j >= Lw(P.vwidth[id])) return "0u";
     return "v" + std::to_string(id) + "_" + std::to_string(j);
   }
@@ -298,13 +704,8 @@ struct Gen {
         for (uint32_t j = 0; j < L; j++) o << "  " << v(d, j) << " = " << hex(P.consts[in.p0 + j]) << ";\n";
         break;
       case K_COORD:
-        if (search && specs) {
-          gen_value(in.p0, W, "v" + std::to_string(d), true, 0);
-        } else if (search) {
-          o << "  { uint32_t t[" << L << "]; gen_regs<" << L << ">(t, gconsts, specs, cw, " << in.p0 << "u, " << W
-            << "u, key);";
-          for (uint32_t j = 0; j < L; j++) o << " " << v(d, j) << " = t[" << j << "];";
-          o << " }\n";
+        if (search) {
+          gen_value(in.p0, "v" + std::to_string(d));
         } else {
           for (uint32_t j = 0; j < L; j++)
             o << "  " << v(d, j) << " = soa[(uint64_t)" << (in.p1 + j) << "u * n + i];\n";
@@ -493,7 +894,16 @@ struct Gen {
   }
 
   void body(bool search) {
-    for (const Instr& in : P.vcode) emit(in, search, !search);
+    analyze(search);
+    for (size_t k = 0; k < P.vcode.size(); k++) {
+      const Instr& in = P.vcode[k];
+      if (skip[k]) continue;  // an alias of an earlier value, or an assert decided true
+      if (in.dst != MG_NONE && in.dst < fold.size() && fold[in.dst] >= 0 && in.op != K_COORD && in.op != K_CONST) {
+        o << "  " << v(in.dst, 0) << " = " << (int)fold[in.dst] << "u;  // decided by value ranges\n";
+        continue;
+      }
+      emit(in, search, !search);
+    }
   }
 };
 
@@ -513,23 +923,29 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   if (want_search) {
   // search kernel
   o << "extern \"C\" __global__ void __launch_bounds__(" << lb << ") mgj_search(const uint32_t* __restrict__ gconsts, "
-       "const GenSpec* __restrict__ specs, const uint32_t* __restrict__ cw, uint64_t start, uint64_t count, "
-       "uint64_t seed, unsigned long long* hit, uint32_t flags) {\n"
+       "uint64_t start, uint64_t count, uint64_t sk, uint64_t sg, unsigned long long* hit, uint32_t flags) {\n"
        "  const bool early = (flags & 1u) != 0u;\n"
        "  const uint32_t lane = threadIdx.x & 63u;\n"
-       "  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;\n"
+       "  // one aligned group of 64 candidate indices per wave (GEN2 group key, mythgpu.h)\n"
+       "  const uint64_t a0 = start & ~63ull, end = start + count;\n"
+       "  const uint64_t ngroups = (end - a0 + 63ull) >> 6;\n"
+       "  const uint64_t gstride = (uint64_t)gridDim.x * (blockDim.x >> 6);\n"
        "  uint64_t wave_best = ~0ull, wave_hits = 0;  // per-wave, wave-uniform\n"
-       "  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < count; base += stride) {\n"
+       "  for (uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); g < ngroups; g += gstride) {\n"
+       "  const uint64_t gb = a0 + (g << 6);\n"
+       "  const uint64_t gbase = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32)) << 32) | "
+       "__builtin_amdgcn_readfirstlane((uint32_t)gb);\n"
        "  if (early) {\n"
        "    const unsigned long long cur = __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
        "    const uint64_t cu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) | "
        "__builtin_amdgcn_readfirstlane((uint32_t)cur);\n"
-       "    if (start + base >= cu) break;\n"
+       "    if (gbase >= cu) break;\n"
        "  }\n"
-       "  const uint64_t i = base + lane;\n"
-       "  const bool active = i < count;\n"
-       "  const uint64_t idx = start + (active ? i : count - 1);\n"
-       "  const uint32_t key = cand_key(idx, seed);\n"
+       "  const uint64_t idx = gbase + lane;\n"
+       "  const bool active = idx >= start && idx < end;\n"
+       "  GKeys ky;\n"
+       "  { const uint64_t K = fmix64(idx ^ sk), G = fmix64((gbase >> 6) ^ sg);\n"
+       "    ky.klo = (uint32_t)K; ky.khi = (uint32_t)(K >> 32); ky.glo = (uint32_t)G; ky.ghi = (uint32_t)(G >> 32); }\n"
        "  uint32_t verdict = 1u;\n";
   g.decls();
   g.body(true);
@@ -537,7 +953,7 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  verdict = active ? verdict : 0u;\n"
        "  { const unsigned long long m = __ballot(verdict != 0u);\n"
        "    if (m) {\n"
-       "      const uint64_t first = start + base + (uint64_t)(__ffsll((long long)m) - 1);\n"
+       "      const uint64_t first = gbase + (uint64_t)(__ffsll((long long)m) - 1);\n"
        "      wave_hits += (uint64_t)__popcll(m);\n"
        "      if (first < wave_best) {\n"
        "        wave_best = first;\n"

@@ -161,7 +161,7 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
     uint32_t row = 0;
     for (uint64_t c = 0; c < n_coords; c++) {
       if (coords[c].width == 0 || coords[c].width > MG_MAX_WIDTH) fail(MG_E_UNSUPPORTED, "coordinate width");
-      if (coords[c].kind > MG_COORD_UF_SITE) fail(MG_E_INVALID, "coordinate kind");
+      if (coords[c].kind > MG_COORD_AUX) fail(MG_E_INVALID, "coordinate kind");
       if (coords[c].node >= n_nodes) fail(MG_E_INVALID, "coordinate node");
       out.coord_width[c] = coords[c].width;
       out.coord_kind[c] = coords[c].kind;
@@ -270,7 +270,8 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
           break;
         }
         case MG_OP_VAR: {
-          if (n.p0 >= n_coords || coords[n.p0].kind != MG_COORD_SCALAR || coords[n.p0].width != W)
+          if (n.p0 >= n_coords || (coords[n.p0].kind != MG_COORD_SCALAR && coords[n.p0].kind != MG_COORD_AUX) ||
+              coords[n.p0].width != W)
             fail(MG_E_INVALID, "VAR coordinate");
           vid[i] = new_vid(W);
           emit(K_COORD, W, vid[i], NONE, NONE, NONE, n.p0, out.coord_row[n.p0]);
@@ -416,8 +417,15 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
             if (n.p0 >= n_coords || coords[n.p0].kind != MG_COORD_ARRAY_SITE || coords[n.p0].table != A.table ||
                 coords[n.p0].width != W)
               fail(MG_E_INVALID, "select site coordinate");
-            uint32_t dflt = new_vid(W);
-            emit(K_COORD, W, dflt, NONE, NONE, NONE, n.p0, out.coord_row[n.p0]);
+            uint32_t dflt;
+            if (n.p1 != NONE) {  // lazy default: a program node (e.g. a byte of an AUX calldata word)
+              if (n.p1 >= i || is_arr[n.p1] || wid(n.p1) != W) fail(MG_E_INVALID, "select lazy default");
+              dflt = val(n.p1, i);
+              out.coord_lazy[n.p0] = n.p1;
+            } else {
+              dflt = new_vid(W);
+              emit(K_COORD, W, dflt, NONE, NONE, NONE, n.p0, out.coord_row[n.p0]);
+            }
             cur = new_vid(W);
             size_t at = emit(K_LOOKUP, W, cur, key, wid(n.b), 0, dflt, 0);
             auto& prior = table_sites[A.table];
@@ -431,7 +439,7 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
             prior.emplace_back(key, cur);
             site_base_vid[n.p0] = cur;
           } else {
-            if (n.p0 != NONE) fail(MG_E_INVALID, "select over K() has no site");
+            if (n.p0 != NONE || n.p1 != NONE) fail(MG_E_INVALID, "select over K() has no site");
             cur = val(A.default_node, i);
           }
           for (auto& st : A.stores) {
@@ -672,10 +680,29 @@ int parse_gen(const Lowered& prog, const uint32_t* blob, size_t n_words, std::ve
         if (s.p[1] == 0 && (s.kind & 0xFFu) == MG_GEN_DICT) { err = "empty dictionary"; return MG_E_INVALID; }
         if (s.p[1] > 65535) { err = "dictionary larger than 65535 entries"; return MG_E_INVALID; }
         if (!in_range(s.p[0], (uint64_t)s.p[1] * L)) { err = "dictionary out of range"; return MG_E_INVALID; }
-        if ((s.kind & 0xFFu) == MG_GEN_MIXED && s.p[3] != MG_NONE &&
-            (s.p[3] >= nc || prog.coord_width[s.p[3]] != prog.coord_width[c])) {
-          err = "copy source must be a coordinate of the same width";
-          return MG_E_INVALID;
+        if ((s.kind & 0xFFu) == MG_GEN_MIXED) {
+          if (s.p[3] != MG_NONE &&
+              (s.p[3] >= c || prog.coord_width[s.p[3]] != prog.coord_width[c] ||
+               (specs[s.p[3]].kind & 0xFFu) == MG_GEN_LAZY)) {
+            err = "copy source must be an earlier, generated coordinate of the same width";
+            return MG_E_INVALID;
+          }
+          if (s.p[6]) {  // clamp record {lo limbs[L], span}: lo + span <= 2^w
+            if (!in_range(s.p[6] - 1, (uint64_t)L + 1)) { err = "clamp record out of range"; return MG_E_INVALID; }
+            const uint32_t* lo = consts.data() + (s.p[6] - 1);
+            const uint64_t span = lo[L] ? lo[L] : (1ull << 32);
+            // (lo + span - 1) must fit in w bits
+            uint64_t carry = span - 1;
+            std::vector<uint32_t> top(L);
+            for (uint32_t j = 0; j < L; j++) {
+              const uint64_t t = (uint64_t)lo[j] + (carry & 0xFFFFFFFFull);
+              top[j] = (uint32_t)t;
+              carry = (carry >> 32) + (t >> 32);
+            }
+            const uint32_t w = prog.coord_width[c];
+            const bool over = carry != 0 || ((w & 31u) && (top[L - 1] >> (w & 31u)) != 0);
+            if (over) { err = "clamp range exceeds the coordinate width"; return MG_E_INVALID; }
+          }
         }
         break;
       case MG_GEN_LAZY:
@@ -683,6 +710,16 @@ int parse_gen(const Lowered& prog, const uint32_t* blob, size_t n_words, std::ve
       default:
         err = "unknown generator kind";
         return MG_E_INVALID;
+    }
+  }
+  // longest static COPY chain (the interpreter walks it per candidate)
+  std::vector<uint32_t> depth(nc, 0);
+  for (uint32_t c = 0; c < nc; c++) {
+    const GenSpec& s = specs[c];
+    if ((s.kind & 0xFFu) == MG_GEN_MIXED && s.p[3] != MG_NONE) depth[c] = depth[s.p[3]] + 1;
+    if (depth[c] > MG_GEN_MAX_COPY_DEPTH) {
+      err = "copy chain longer than MG_GEN_MAX_COPY_DEPTH";
+      return MG_E_UNSUPPORTED;
     }
   }
   return MG_OK;

@@ -124,13 +124,19 @@ class Propagator:
         # term id -> coordinate index, for terms that ARE a coordinate's value
         self.coord_of: Dict[int, int] = {}
         self.base_read_of: Dict[int, int] = {}
+        # term id -> (AUX coordinate, bit offset): a calldata byte that is a slice of an AUX word
+        self.slice_of: Dict[int, Tuple[int, int]] = {}
         self.hints: List[T.Term] = []  # terms a symbolic comparison wants small
         for c in P.coords:
             t = c.term
             if c.kind == ssa.COORD_SCALAR:
                 self.coord_of[t.id] = c.index
+            elif c.kind == ssa.COORD_AUX:
+                continue
             elif c.kind == ssa.COORD_ARRAY_SITE:
-                if t.args[0].op == "array_var":  # a store chain would override the value
+                if c.index in P.aux_slice:  # the site's value is bits of an AUX word (ssa.calldata_window)
+                    self.slice_of[t.id] = P.aux_slice[c.index]
+                elif t.args[0].op == "array_var":  # a store chain would override the value
                     self.coord_of[t.id] = c.index
                 else:  # the base read a store-chain select falls through to when no index matches
                     self.base_read_of[t.id] = c.index
@@ -157,6 +163,9 @@ class Propagator:
                 return False
             n = w - lo
         value &= _mask(n)
+        sl = self.slice_of.get(t.id)
+        if sl is not None:
+            return self.d(sl[0]).fix_bits(sl[1] + lo, n, value)
         c = self.coord_of.get(t.id)
         if c is None:
             c = self.base_read_of.get(t.id)

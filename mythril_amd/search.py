@@ -28,7 +28,7 @@ import numpy as np
 from . import ssa
 from .smt import terms as T
 
-GEN_MAGIC = 0x314E4547
+GEN_MAGIC = 0x324E4547  # "GEN2" (include/mythgpu.h)
 GEN_UNIFORM, GEN_RANGE, GEN_DICT, GEN_MIXED, GEN_ALIGNED, GEN_FIXED, GEN_LAZY = range(7)
 NONE = ssa.MG_NONE
 
@@ -41,7 +41,13 @@ ACTORS = [
 P16 = 65536
 
 # prefix-incremental flattening shared by every search (LASER's sibling queries share prefixes)
-FLATTEN_CACHE = ssa.FlattenCache()
+FLATTEN_CACHE = ssa.FlattenCache(aux_words=True)
+
+# A generator bound, not a fact of the query: LASER's ``<tx>_calldatasize``
+# (calldata.py:215-216) is a 256-bit symbol, but a transaction's calldata is paid
+# per byte and bounded by the block gas limit, so no realisable model has 2^32 bytes
+# of it.  Sizes are drawn inside [0, 2^32) (then the query's own bounds).
+CALLDATASIZE_MAX = (1 << 32) - 1
 
 
 class GenBuilder:
@@ -82,14 +88,26 @@ class GenBuilder:
         self.specs[c] = [GEN_LAZY, 0, 0, 0, 0, 0, 0, 0]
 
     def mixed(self, c: int, values: Sequence[int], p_dict: float, copy_from: Optional[int] = None,
-              p_copy: float = 0.0, p_delta: float = 0.0, small_bits: int = 0, p_small: float = 0.0):
+              p_copy: float = 0.0, p_delta: float = 0.0, small_bits: int = 0, p_small: float = 0.0,
+              clamp: Optional[tuple] = None):
+        """MIXED (GEN2): one alternative per aligned group of 64 candidates — COPY of an
+        earlier coordinate's final value, DICT, SMALL or UNIFORM — plus a per-lane +/-1/2
+        delta on COPY/DICT, then an optional clamp into ``[lo, lo + span)``."""
         w = self.P.coords[c].width
         values = list(values)
         off = self._push(values, w) if values else 0
+        pc = int(p_copy * P16) if copy_from is not None else 0
+        pd = int(p_dict * P16) if values else 0
+        rec = 0
+        if clamp is not None:
+            lo, span = clamp
+            rec = len(self.consts) + 1
+            self.consts.extend(ssa.int_to_limbs(lo % (1 << w), w))
+            self.consts.append(span & 0xFFFFFFFF)
         self.specs[c] = [
-            GEN_MIXED, off, len(values), int(p_dict * P16) if values else 0,
-            NONE if copy_from is None else copy_from, int(p_copy * P16), int(p_delta * P16),
-            ((small_bits & 0xFFFF) << 16) | (int(p_small * P16) & 0xFFFF),
+            GEN_MIXED, off, len(values), (pc & 0xFFFF) | ((pd & 0xFFFF) << 16),
+            NONE if copy_from is None else copy_from,
+            (int(p_small * P16) & 0xFFFF) | ((small_bits & 0xFFFF) << 16), int(p_delta * P16) & 0xFFFF, rec,
         ]
 
     def fix(self, c: int, mask: int, value: int):
@@ -147,10 +165,17 @@ def default_generator(P: ssa.Program, extra_dict: Sequence[int] = (), roots: Opt
     for c in P.coords:
         w = c.width
         mask = (1 << w) - 1
-        if c.kind == ssa.COORD_UF_SITE and P.nodes[c.node][7] != NONE:
-            g.lazy(c.index)
+        if (c.kind == ssa.COORD_UF_SITE and P.nodes[c.node][7] != NONE) or \
+                (c.kind == ssa.COORD_ARRAY_SITE and P.nodes[c.node][6] != NONE):
+            g.lazy(c.index)  # the program supplies the default (inverse UF argument, AUX word byte)
             continue
         dom = doms.get(c.index)
+        if c.kind == ssa.COORD_SCALAR and c.name.endswith("_calldatasize") and w > 32:
+            from .propagate import Domain
+
+            dom = dom or Domain(w)
+            if not dom.restrict([(0, CALLDATASIZE_MAX)]):
+                dom = None
         if dom is not None and _apply_domain(g, P, c.index, dom):
             last_of_width[w] = c.index
             continue
@@ -168,16 +193,19 @@ def default_generator(P: ssa.Program, extra_dict: Sequence[int] = (), roots: Opt
         for a in list(ACTORS) + list(extra_dict):
             vals.add(a & mask)
         small_bits, p_small = min(w, 8), 0.20
+        clamp = None
         if dom is not None:
-            # a huge interval is only a hint: keep the broad draw, steer the dictionary
             if dom.intervals:
                 for a_, b_ in dom.intervals[:4]:
                     vals |= {a_, (a_ + 1) & mask, b_, (b_ - 1) & mask}
+                a_, b_ = dom.intervals[0][0], dom.intervals[-1][1]
+                if len(dom.intervals) == 1 and b_ - a_ < (1 << 32):
+                    clamp = (a_, (b_ - a_ + 1) & 0xFFFFFFFF)  # span 2^32 is encoded as 0
             vals = {v for v in vals if dom.admissible(v)} or vals
         vals = sorted(vals)[:4096]
         copy = last_of_width.get(w) if w >= 32 else None
         g.mixed(c.index, vals, p_dict=0.45, copy_from=copy, p_copy=0.10 if copy is not None else 0.0,
-                p_delta=0.25 if w > 8 else 0.0, small_bits=small_bits, p_small=p_small)
+                p_delta=0.25 if w > 8 else 0.0, small_bits=small_bits, p_small=p_small, clamp=clamp)
         if dom is not None and dom.fmask:
             g.fix(c.index, dom.fmask, dom.fval)
         last_of_width[w] = c.index
@@ -212,7 +240,7 @@ def _apply_domain(g: GenBuilder, P: ssa.Program, c: int, dom) -> bool:
                     g.fix(c, rest, dom.fval)
                 return True
         span = sum(y - x + 1 for x, y in dom.intervals)
-        if span < (1 << 32) and len(dom.intervals) == 1:
+        if span <= (1 << 16) and len(dom.intervals) == 1:
             g.range(c, a, span)
             if dom.fmask:
                 g.fix(c, dom.fmask, dom.fval)
@@ -278,6 +306,14 @@ def materialize(engine, P: ssa.Program, gen_blob: np.ndarray, seed: int, index: 
     return int(ver[0]), scalars, arrays, funcs
 
 
+def prepare(roots: Sequence[T.Term], gen: Optional[GenBuilder] = None):
+    """The program and generator blob a search runs: prefix-incremental flattening with
+    AUX calldata words (``FLATTEN_CACHE``) and the propagation-shaped generator."""
+    P = FLATTEN_CACHE.flatten(roots)
+    g = gen or default_generator(P, roots=roots)
+    return P, g.blob()
+
+
 def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int = 1 << 22,
            max_candidates: int = 1 << 26, timeout_s: float = 10.0, gen: Optional[GenBuilder] = None,
            want_model: bool = True, jit: str = "auto", jit_cost_s: float = 0.5) -> SearchResult:
@@ -290,9 +326,7 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
     hipRTC, ~10x the interpreter's candidates/s) and continues the SAME index
     stream on it.  Both kernels compute identical verdicts for every index
     (``tests/test_gpu_jit.py``), so the first hit does not depend on the mode."""
-    P = FLATTEN_CACHE.flatten(roots)
-    g = gen or default_generator(P, roots=roots)
-    blob = g.blob()
+    P, blob = prepare(roots, gen)
     prog = engine.load(P.to_bytes())
     t0 = time.perf_counter()
     scanned = 0

@@ -34,7 +34,7 @@ from typing import Dict, Iterable, List, Optional, Sequence
 from .smt import terms as T
 
 MG_MAGIC = 0x3150474D
-MG_VERSION = 1
+MG_VERSION = 2
 MG_NONE = 0xFFFFFFFF
 MG_MAX_WIDTH = 32768
 
@@ -46,7 +46,7 @@ OPS = {
     "EQ": 23, "ULT": 24, "ULE": 25, "SLT": 26, "SLE": 27, "UMUL_NOOVF": 28, "ARR_VAR": 29,
     "ARR_K": 30, "ARR_STORE": 31, "SELECT": 32, "UFAPP": 33, "KECCAK": 34, "EXP": 35,
 }
-COORD_SCALAR, COORD_ARRAY_SITE, COORD_UF_SITE = 0, 1, 2
+COORD_SCALAR, COORD_ARRAY_SITE, COORD_UF_SITE, COORD_AUX = 0, 1, 2, 3
 TABLE_ARRAY, TABLE_UF = 0, 1
 
 _BIN = {
@@ -114,6 +114,7 @@ class Program:
         self.site_key_node: Dict[int, int] = {}  # coord index -> node of the key
         self.site_val_node: Dict[int, int] = {}  # coord index -> node of the site value
         self.const_values: List[tuple] = []      # (value, width) of every literal, for dictionaries
+        self.aux_slice: Dict[int, tuple] = {}     # site coord -> (AUX coord, bit offset) of its lazy default
         self._blob: Optional[bytes] = None
 
     # -- properties --------------------------------------------------
@@ -172,6 +173,22 @@ def _base_of(arr: T.Term) -> T.Term:
     while arr.op == "store":
         arr = arr.args[0]
     return arr
+
+
+def calldata_window(name: str, dom: int, rng: int, index: int):
+    """The AUX word a calldata byte belongs to (``aux_words`` flattening), or None.
+
+    LASER's calldata is the array ``<tx>_calldata`` (256 -> 8, ``calldata.py:215-216``)
+    and ABI data is a 4-byte selector followed by 32-byte words read with
+    CALLDATALOAD (``instructions.py:775-789``, ``calldata.py:47-54``): byte k belongs
+    to the selector window [0, 4) or to the word [4 + 32m, 36 + 32m).  Returns
+    ``(start, length)``.  The window depends on the index alone, so prefix-incremental
+    flattening stays byte-identical."""
+    if not name.endswith("_calldata") or dom != 256 or rng != 8 or index >= 1 << 32:
+        return None
+    if index < 4:
+        return 0, 4
+    return 4 + 32 * ((index - 4) // 32), 32
 
 
 def _extend(st: "_FlatState", terms: Sequence[T.Term], lazy_inverse: bool) -> None:
@@ -274,13 +291,33 @@ def _extend(st: "_FlatState", terms: Sequence[T.Term], lazy_inverse: bool) -> No
             base = _base_of(t.args[0])
             if base.op == "array_var":
                 tab = P.nodes[nid(base)][5]
-                n = new_node("SELECT", t.width, nid(t.args[0]), nid(t.args[1]), p0=len(P.coords), term=t)
+                lazy = MG_NONE
+                idx = t.args[1]
+                win = None
+                if st.aux_words and base is t.args[0] and idx.op == "bvconst":
+                    win = calldata_window(base.params[0], base.sort[1], base.sort[2], idx.params[0])
+                if win is not None:
+                    # the byte is a slice of a generator-only AUX word (one 256-bit draw per
+                    # ABI word instead of 32 byte draws); the site's table entry is still
+                    # read back as the model
+                    key = (base.params[0], win[0])
+                    if key not in st.aux_of:
+                        wbits = 8 * win[1]
+                        an = new_node("VAR", wbits, p0=len(P.coords))
+                        ac = new_coord(wbits, COORD_AUX, an, None, f"{base.params[0]}@{win[0]}", None)
+                        st.aux_of[key] = (ac.index, an)
+                    ac_i, an = st.aux_of[key]
+                    b = 8 * (win[0] + win[1] - 1 - idx.params[0])
+                    lazy = new_node("EXTRACT", 8, an, p0=b)
+                    P.aux_slice[len(P.coords)] = (ac_i, b)
+                n = new_node("SELECT", t.width, nid(t.args[0]), nid(t.args[1]), p0=len(P.coords), p1=lazy,
+                             term=t)
                 c = new_coord(t.width, COORD_ARRAY_SITE, n, tab, base.params[0], t)
                 P.sites.append(c)
                 P.site_key_node[c.index] = nid(t.args[1])
                 P.site_val_node[c.index] = n
             elif base.op == "const_array":
-                n = new_node("SELECT", t.width, nid(t.args[0]), nid(t.args[1]), p0=MG_NONE, term=t)
+                n = new_node("SELECT", t.width, nid(t.args[0]), nid(t.args[1]), p0=MG_NONE, p1=MG_NONE, term=t)
             else:
                 raise Unsupported(f"select over {base.op}")
         elif op == "app":
@@ -310,14 +347,19 @@ def _extend(st: "_FlatState", terms: Sequence[T.Term], lazy_inverse: bool) -> No
     P._blob = None
 
 
-def flatten(roots: Sequence[T.Term], lazy_inverse: bool = True, extra: Sequence[T.Term] = ()) -> Program:
+def flatten(roots: Sequence[T.Term], lazy_inverse: bool = True, extra: Sequence[T.Term] = (),
+            aux_words: bool = False) -> Program:
     """Flatten Bool roots (terms) into a :class:`Program`.  ``extra`` terms are
-    flattened too (so they can be watched) without becoming constraints."""
+    flattened too (so they can be watched) without becoming constraints.
+
+    ``aux_words`` (search mode): literal-index calldata bytes take their default from
+    a generator-only AUX word (:func:`calldata_window`) instead of a coordinate of
+    their own, so explicit-coordinate evaluation (``mg_eval``) leaves it off."""
     roots = list(roots)
     for r in roots:
         if not r.is_bool:
             raise TypeError("constraint roots must be Bool terms")
-    st = _FlatState()
+    st = _FlatState(aux_words)
     _extend(st, list(roots) + list(extra), lazy_inverse)
     st.P.roots = [st.P.term_node[r.id] for r in roots]
     return st.P
@@ -326,14 +368,16 @@ def flatten(roots: Sequence[T.Term], lazy_inverse: bool = True, extra: Sequence[
 class _FlatState:
     """A Program under construction plus the flattener's lookup tables."""
 
-    def __init__(self):
+    def __init__(self, aux_words: bool = False):
         self.P = Program()
         self.scalar_coord: Dict[str, int] = {}
         self.table_of: Dict[tuple, int] = {}
         self.fwd_arg: Dict[int, int] = {}   # term id of f(x) app -> term id of x
+        self.aux_words = aux_words
+        self.aux_of: Dict[tuple, tuple] = {}  # (calldata array, window start) -> (AUX coord, VAR node)
 
     def copy(self) -> "_FlatState":
-        c = _FlatState()
+        c = _FlatState(self.aux_words)
         P, Q = self.P, c.P
         Q.nodes = [list(n) for n in P.nodes]
         Q.node_width = list(P.node_width)
@@ -347,6 +391,8 @@ class _FlatState:
         Q.site_key_node = dict(P.site_key_node)
         Q.site_val_node = dict(P.site_val_node)
         Q.const_values = list(P.const_values)
+        Q.aux_slice = dict(P.aux_slice)
+        c.aux_of = dict(self.aux_of)
         c.scalar_coord = dict(self.scalar_coord)
         c.table_of = dict(self.table_of)
         c.fwd_arg = dict(self.fwd_arg)
@@ -365,10 +411,10 @@ class FlattenCache:
     this way is byte-identical to :func:`flatten` of the whole tuple
     (``tests/test_host_boundary.py``)."""
 
-    def __init__(self, capacity: int = 4096, lazy_inverse: bool = True):
+    def __init__(self, capacity: int = 4096, lazy_inverse: bool = True, aux_words: bool = False):
         from collections import OrderedDict
 
-        self.capacity, self.lazy_inverse = capacity, lazy_inverse
+        self.capacity, self.lazy_inverse, self.aux_words = capacity, lazy_inverse, aux_words
         self._lru: "OrderedDict[tuple, _FlatState]" = OrderedDict()
         self.hits = self.misses = 0
 
@@ -387,7 +433,7 @@ class FlattenCache:
             st = self._lru[ids[:k]].copy()
         else:
             self.misses += 1
-            st = _FlatState()
+            st = _FlatState(self.aux_words)
         if k == len(ids):
             return st.P
         _extend(st, roots[k:], self.lazy_inverse)

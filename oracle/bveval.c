@@ -239,170 +239,169 @@ static uint64_t vsmall(const val_t* b, uint32_t cap) {
   return b->w[0] < cap ? b->w[0] : cap;
 }
 
-/* ---- generator restatement (include/mythgpu.h MG_GEN_*) ---- */
-static uint32_t mix32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x7FEB352Du;
-  x ^= x >> 15;
-  x *= 0x846CA68Bu;
-  x ^= x >> 16;
+/* ---- generator restatement (include/mythgpu.h, format GEN2) ---- */
+static uint64_t fmix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xFF51AFD7ED558CCDull;
+  x ^= x >> 33;
+  x *= 0xC4CEB9FE1A85EC53ull;
+  x ^= x >> 33;
   return x;
 }
-static uint32_t cand_key(uint64_t idx, uint64_t seed) {
-  return mix32((uint32_t)idx ^ mix32((uint32_t)(idx >> 32) ^ (uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + 0x632BE5ABu)));
+
+typedef struct {
+  uint32_t klo, khi, glo, ghi;
+} keys_t;
+
+static void make_keys(uint64_t idx, uint64_t seed, keys_t* k) {
+  const uint64_t K = fmix64(idx ^ fmix64(seed ^ 0x6A09E667F3BCC908ull));
+  const uint64_t G = fmix64((idx >> 6) ^ fmix64(seed ^ 0xBB67AE8584CAA73Bull));
+  k->klo = (uint32_t)K;
+  k->khi = (uint32_t)(K >> 32);
+  k->glo = (uint32_t)G;
+  k->ghi = (uint32_t)(G >> 32);
 }
-static uint32_t rnd(uint32_t key, uint32_t c, uint32_t j) {
-  /* one-multiply finaliser of the (well mixed) candidate key; see MG_GEN_* in mythgpu.h */
-  uint32_t x = key ^ (c * 0x9E3779B9u + j * 0x85EBCA6Bu + 0x27D4EB2Fu);
+
+static uint32_t salt(uint32_t c, uint32_t j) { return c * 0x9E3779B9u + j * 0x85EBCA6Bu + 0x27D4EB2Fu; }
+
+static uint32_t fin(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7FEB352Du;
   x ^= x >> 15;
   return x;
 }
 
+static uint32_t rnd(const keys_t* k, uint32_t c, uint32_t j) { return fin(k->klo ^ salt(c, j)) + k->khi; }
+static uint32_t wsel(const keys_t* k, uint32_t c) { return fin(k->glo ^ salt(c, 0xFFFEu)) + k->ghi; }
+
 static void set_limb32(val_t* v, uint32_t j, uint32_t x) {
   v->w[j / 2] |= (uint64_t)x << (32 * (j % 2));
 }
+
+static uint32_t get_limb32(const val_t* v, uint32_t j) { return (uint32_t)(v->w[j / 2] >> (32 * (j % 2))); }
 
 static void from_limbs32(val_t* v, const uint32_t* src, uint32_t L) {
   vzero(v);
   for (uint32_t j = 0; j < L; j++) set_limb32(v, j, src[j]);
 }
 
-static void gen_coord(const prog_t* P, uint32_t c, uint32_t key, val_t* out) {
+static void mask_limbs(uint32_t* limb, uint32_t L, uint32_t width) {
+  if (width & 31u) limb[L - 1] &= (1u << (width & 31u)) - 1u;
+}
+
+/* lo + off over L limbs (carry out dropped) */
+static void add_small(uint32_t* out, const uint32_t* lo, uint64_t off, uint32_t L) {
+  uint64_t carry = off;
+  for (uint32_t j = 0; j < L; j++) {
+    uint64_t t = (uint64_t)lo[j] + (carry & 0xFFFFFFFFull);
+    carry = (carry >> 32) + (t >> 32);
+    out[j] = (uint32_t)t;
+  }
+}
+
+struct ctx;
+static void coord_value(struct ctx* X, uint32_t c, val_t* out);
+
+/* generated value of coordinate c (GEN2 semantics in include/mythgpu.h) into L limbs */
+static void gen_value(struct ctx* X, const prog_t* P, const keys_t* k, uint32_t c, uint32_t* limb) {
   const uint32_t width = P->coords[4 * c];
   const uint32_t L = (width + 31) / 32;
-  uint32_t cc = c;
-  uint32_t s[8];
-  memcpy(s, P->specs + 8 * c, 32);
-  const uint32_t fix_dst = s[0] >> 8; /* 1 + const offset of a (mask, value) fix */
-  uint32_t fix_src = 0;
-  s[0] &= 0xFFu;
-  uint32_t Lg = L;
-  int allow_copy = 1, from_mixed = 0, done = 0;
-  vzero(out);
-  for (int level = 0; level < 2; level++) {
-    if (s[0] != 3) break;
-    uint32_t h = rnd(key, cc, 0xFFFFu), sel = h & 0xFFFFu;
-    /* narrow coordinates (<= 16 bits, MG_GEN_NARROW_BITS): uniform / small value = h >> 16 */
-    int narrow = P->coords[4 * cc] <= 16;
-    uint32_t pc = (allow_copy && s[4] != NONE) ? s[5] : 0;
-    uint32_t pd = s[2] ? s[3] : 0;
-    uint32_t ps = s[7] & 0xFFFFu;
-    if (sel < pc) {
-      cc = s[4];
-      memcpy(s, P->specs + 8 * cc, 32);
-      fix_src = s[0] >> 8;
-      s[0] &= 0xFFu;
-      uint32_t Ls = (P->coords[4 * cc] + 31) / 32;
-      Lg = Ls < L ? Ls : L;
-      allow_copy = 0;
-      continue;
-    }
-    if (sel < pc + pd) {
-      s[0] = 2;
-      from_mixed = 1;
-    } else if (sel < pc + pd + ps) {
-      uint32_t bits = (s[7] >> 16) < width ? (s[7] >> 16) : width;
-      if (P->coords[4 * cc] < bits) bits = P->coords[4 * cc]; /* a copy keeps the source width */
-      for (uint32_t j = 0; j < L; j++) {
-        uint32_t v = narrow ? (j == 0 ? h >> 16 : 0u) : rnd(key, cc, j), lo = j * 32;
-        v = lo >= bits ? 0u : (bits - lo >= 32 ? v : (v & ((1u << (bits - lo)) - 1u)));
-        set_limb32(out, j, v);
-      }
-      vmask(out, width);
-      done = 1;
-    } else if (narrow) {
-      s[0] = 0xFFu; /* value complete: h >> 16 */
-    } else {
-      s[0] = 0;
-    }
-    break;
-  }
-  const uint32_t Lsrc = (P->coords[4 * cc] + 31) / 32;
-  uint32_t limb[64];
-  if (done) goto fixes;
-  memset(limb, 0, sizeof(limb));
-  switch (s[0]) {
-    case 0xFFu: /* narrow MIXED draw */
-      limb[0] = rnd(key, cc, 0xFFFFu) >> 16;
-      break;
-    case 2: { /* DICT */
-      uint32_t n = s[2];
-      uint32_t e = (((rnd(key, cc, 0xFFFFu) >> 16) * n) >> 16);
-      const uint32_t* src = P->gconsts + s[1] + e * Lsrc;
-      for (uint32_t j = 0; j < Lg; j++) limb[j] = src[j];
-      if (from_mixed && s[6]) {
-        uint32_t r = rnd(key, cc, 0u);
-        if ((r & 0xFFFFu) < s[6]) {
-          uint32_t mag = ((r >> 16) & 1u) + 1u;
-          int sub = (r >> 17) & 1u;
-          uint64_t carry = mag;
-          for (uint32_t j = 0; j < Lg; j++) {
-            uint64_t t = sub ? ((uint64_t)limb[j] - carry) : ((uint64_t)limb[j] + carry);
-            limb[j] = (uint32_t)t;
-            carry = sub ? ((t >> 32) & 1u) : (t >> 32);
-          }
-        }
-      }
-      break;
-    }
+  const uint32_t* s = P->specs + 8 * c;
+  const uint32_t kind = s[0] & 0xFFu, fix = s[0] >> 8;
+  memset(limb, 0, 4 * L);
+  switch (kind) {
     case 1: { /* RANGE */
-      uint32_t span = s[2], r = rnd(key, cc, 0);
-      uint32_t off = span ? (uint32_t)(((uint64_t)r * span) >> 32) : r;
-      uint64_t carry = off;
-      for (uint32_t j = 0; j < Lg; j++) {
-        uint64_t t = (uint64_t)P->gconsts[s[1] + j] + carry;
-        limb[j] = (uint32_t)t;
-        carry = t >> 32;
-      }
+      const uint32_t span = s[2], r = rnd(k, c, 0);
+      add_small(limb, P->gconsts + s[1], span ? (((uint64_t)r * span) >> 32) : r, L);
+      break;
+    }
+    case 2: { /* DICT */
+      const uint32_t e = ((rnd(k, c, 0xFFFFu) >> 16) * s[2]) >> 16;
+      memcpy(limb, P->gconsts + s[1] + e * L, 4 * L);
       break;
     }
     case 4: { /* ALIGNED */
-      uint32_t cnt = s[3], r = rnd(key, cc, 0);
-      uint64_t m = cnt ? (((uint64_t)r * cnt) >> 32) : r;
-      uint32_t sh = s[2];
+      const uint32_t cnt = s[3], r = rnd(k, c, 0);
+      const uint64_t m = cnt ? (((uint64_t)r * cnt) >> 32) : r;
+      const uint32_t sh = s[2];
       uint64_t carry = 0;
-      for (uint32_t j = 0; j < Lg; j++) {
-        int32_t bit0 = (int32_t)(j * 32) - (int32_t)sh;
+      for (uint32_t j = 0; j < L; j++) {
+        const int32_t bit0 = (int32_t)(j * 32) - (int32_t)sh;
         uint32_t mw;
         if (bit0 <= -32 || bit0 >= 64) mw = 0;
         else if (bit0 < 0) mw = (uint32_t)(m << (-bit0));
         else mw = (uint32_t)(m >> bit0);
-        uint64_t t = (uint64_t)P->gconsts[s[1] + j] + mw + carry;
+        const uint64_t t = (uint64_t)P->gconsts[s[1] + j] + mw + carry;
         limb[j] = (uint32_t)t;
         carry = t >> 32;
       }
       break;
     }
     case 5: /* FIXED */
-      for (uint32_t j = 0; j < Lg; j++) limb[j] = P->gconsts[s[1] + j];
+      memcpy(limb, P->gconsts + s[1], 4 * L);
       break;
+    case 3: { /* MIXED: one alternative per aligned group of 64 indices */
+      const uint32_t ws = wsel(k, c), sel = ws & 0xFFFFu;
+      const uint32_t pc = s[4] != NONE ? (s[3] & 0xFFFFu) : 0u;
+      const uint32_t pd = s[2] ? (s[3] >> 16) : 0u;
+      const uint32_t ps = s[5] & 0xFFFFu;
+      const uint32_t h = rnd(k, c, 0xFFFFu);
+      const int narrow = width <= 16;
+      int with_delta = 0;
+      if (sel < pc) { /* COPY: the source's final value */
+        val_t src;
+        coord_value(X, s[4], &src);
+        for (uint32_t j = 0; j < L; j++) limb[j] = get_limb32(&src, j);
+        with_delta = 1;
+      } else if (sel < pc + pd) { /* DICT */
+        const uint32_t e = ((h >> 16) * s[2]) >> 16;
+        memcpy(limb, P->gconsts + s[1] + e * L, 4 * L);
+        with_delta = 1;
+      } else {
+        const uint32_t small = sel < pc + pd + ps;
+        uint32_t bits = small ? (s[5] >> 16) : width;
+        if (bits > width) bits = width;
+        for (uint32_t j = 0; j < L; j++) {
+          uint32_t v = narrow ? (j == 0 ? (h & 0xFFFFu) : 0u) : rnd(k, c, j);
+          const uint32_t lo = 32 * j;
+          limb[j] = lo >= bits ? 0u : (bits - lo >= 32 ? v : (v & ((1u << (bits - lo)) - 1u)));
+        }
+      }
+      if (with_delta && (ws >> 16) < s[6]) {
+        const uint32_t mag = 1u + (h & 1u);
+        const int sub = (h >> 1) & 1u;
+        uint64_t cy = mag;
+        for (uint32_t j = 0; j < L; j++) {
+          const uint64_t t = sub ? ((uint64_t)limb[j] - cy) : ((uint64_t)limb[j] + cy);
+          limb[j] = (uint32_t)t;
+          cy = sub ? ((t >> 32) & 1u) : (t >> 32);
+        }
+      }
+      mask_limbs(limb, L, width);
+      if (s[7]) { /* clamp into [lo, lo + span) */
+        const uint32_t* lo = P->gconsts + (s[7] - 1);
+        const uint32_t span = lo[L];
+        uint64_t br = 0;
+        uint32_t hi_or = 0, t0 = 0;
+        for (uint32_t j = 0; j < L; j++) {
+          const uint64_t t = (uint64_t)limb[j] - lo[j] - br;
+          br = (t >> 32) & 1u;
+          if (j == 0) t0 = (uint32_t)t;
+          else hi_or |= (uint32_t)t;
+        }
+        const int in = !br && !hi_or && (span == 0 || t0 < span);
+        if (!in) add_small(limb, lo, span ? (((uint64_t)limb[0] * span) >> 32) : limb[0], L);
+      }
+      break;
+    }
     default: /* UNIFORM / LAZY */
-      for (uint32_t j = 0; j < Lg; j++) limb[j] = rnd(key, cc, j);
+      for (uint32_t j = 0; j < L; j++) limb[j] = rnd(k, c, j);
       break;
   }
-  /* a copy is the source's value: masked to the source width, then truncated / zero-extended */
-  if (cc != c && Lg == Lsrc && (P->coords[4 * cc] & 31u)) limb[Lg - 1] &= (1u << (P->coords[4 * cc] & 31u)) - 1u;
-  from_limbs32(out, limb, Lg);
-  vmask(out, width);
-fixes:
-  /* fixed bits (v & ~mask) | value: the copied source's fix, then this coordinate's */
-  if (cc != c && fix_src) {
-    const uint32_t* f = P->gconsts + (fix_src - 1);
-    for (uint32_t j = 0; j < Lg; j++) {
-      uint32_t x = (uint32_t)(out->w[j / 2] >> (32 * (j % 2)));
-      x = (x & ~f[j]) | f[Lsrc + j];
-      out->w[j / 2] = (out->w[j / 2] & ~(0xFFFFFFFFull << (32 * (j % 2)))) | ((uint64_t)x << (32 * (j % 2)));
-    }
-  }
-  if (fix_dst) {
-    const uint32_t* f = P->gconsts + (fix_dst - 1);
-    for (uint32_t j = 0; j < L; j++) {
-      uint32_t x = (uint32_t)(out->w[j / 2] >> (32 * (j % 2)));
-      x = (x & ~f[j]) | f[L + j];
-      out->w[j / 2] = (out->w[j / 2] & ~(0xFFFFFFFFull << (32 * (j % 2)))) | ((uint64_t)x << (32 * (j % 2)));
-    }
+  mask_limbs(limb, L, width);
+  if (fix) { /* fixed bits: (v & ~mask) | value */
+    const uint32_t* f = P->gconsts + (fix - 1);
+    for (uint32_t j = 0; j < L; j++) limb[j] = (limb[j] & ~f[j]) | f[L + j];
   }
 }
 
@@ -412,12 +411,14 @@ typedef struct {
   val_t key, val;
 } entry_t;
 
-typedef struct {
+typedef struct ctx {
   const prog_t* P;
   val_t* vals;       /* per node */
   entry_t* entries;  /* per-candidate tables, in SSA order */
   int n_entries;
-  uint32_t key;
+  keys_t keys;
+  val_t* cvals;      /* per coordinate: generated value (search mode), memoised per candidate */
+  uint8_t* cdone;
   const uint32_t* soa; /* optional explicit coordinates (rows x n) */
   uint64_t soa_n, soa_i;
   const uint32_t* coord_row;
@@ -430,9 +431,15 @@ static void coord_value(ctx_t* X, uint32_t c, val_t* out) {
     vzero(out);
     for (uint32_t j = 0; j < L; j++) set_limb32(out, j, X->soa[(uint64_t)(X->coord_row[c] + j) * X->soa_n + X->soa_i]);
     vmask(out, width);
-  } else {
-    gen_coord(X->P, c, X->key, out);
+    return;
   }
+  if (!X->cdone[c]) {
+    uint32_t limb[MAXW * 2];
+    gen_value(X, X->P, &X->keys, c, limb);
+    from_limbs32(&X->cvals[c], limb, (width + 31) / 32);
+    X->cdone[c] = 1;
+  }
+  *out = X->cvals[c];
 }
 
 static void site_lookup(ctx_t* X, uint32_t table, const val_t* key, const val_t* dflt, val_t* out) {
@@ -452,6 +459,7 @@ static void site_lookup(ctx_t* X, uint32_t table, const val_t* key, const val_t*
 static int eval_candidate(ctx_t* X) {
   const prog_t* P = X->P;
   X->n_entries = 0;
+  if (X->cdone) memset(X->cdone, 0, P->n_coords);
   for (uint32_t i = 0; i < P->n_nodes; i++) {
     const node_t* n = &P->nodes[i];
     val_t* r = &X->vals[i];
@@ -556,7 +564,8 @@ static int eval_candidate(ctx_t* X) {
           base = X->vals[P->nodes[arr].a];
         } else {
           val_t dflt;
-          coord_value(X, n->p0, &dflt);
+          if (n->p1 != NONE) dflt = X->vals[n->p1]; /* lazy default (an AUX word's byte) */
+          else coord_value(X, n->p0, &dflt);
           site_lookup(X, P->nodes[arr].p0, B, &dflt, &base);
         }
         *r = base;
@@ -602,7 +611,7 @@ static int eval_candidate(ctx_t* X) {
 }
 
 static int parse(prog_t* P, const uint32_t* w, size_t n, const uint32_t* gen, size_t gen_n) {
-  if (n < 16 || w[0] != 0x3150474Du) return -1;
+  if (n < 16 || w[0] != 0x3150474Du || w[1] != 2u) return -1;
   P->n_nodes = w[2];
   P->n_roots = w[3];
   P->n_coords = w[4];
@@ -625,7 +634,7 @@ static int parse(prog_t* P, const uint32_t* w, size_t n, const uint32_t* gen, si
   for (uint32_t i = 0; i < P->n_nodes; i++)
     if (P->nodes[i].width > MAXW * 64) return -2;
   if (gen) {
-    if (gen_n < 4 || gen[0] != 0x314E4547u || gen[1] != P->n_coords) return -1;
+    if (gen_n < 4 || gen[0] != 0x324E4547u || gen[1] != P->n_coords) return -1;
     P->gen_n = gen[1];
     P->specs = gen + 4;
     P->gconsts = gen + 4 + 8ull * gen[1];
@@ -653,12 +662,14 @@ int bv_search(const uint32_t* prog, size_t prog_words, const uint32_t* gen, size
     X.P = &P;
     X.vals = (val_t*)malloc(sizeof(val_t) * (P.n_nodes + 1));
     X.entries = (entry_t*)malloc(sizeof(entry_t) * (P.n_nodes + 1));
+    X.cvals = (val_t*)malloc(sizeof(val_t) * (P.n_coords + 1));
+    X.cdone = (uint8_t*)malloc(P.n_coords + 1);
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic, 256)
 #endif
     for (int64_t i = 0; i < (int64_t)count; i++) {
       uint64_t idx = start + (uint64_t)i;
-      X.key = cand_key(idx, seed);
+      make_keys(idx, seed, &X.keys);
       int v = eval_candidate(&X);
       if (v < 0) {
         err |= 1;
@@ -672,6 +683,8 @@ int bv_search(const uint32_t* prog, size_t prog_words, const uint32_t* gen, size
     }
     free(X.vals);
     free(X.entries);
+    free(X.cvals);
+    free(X.cdone);
   }
   if (err) return -3;
   *first_hit = best;

@@ -265,9 +265,10 @@ WORKLOAD_NAMES = ["token_transfer_underflow", "etherstore_reentrancy", "bectoken
                   "walletlibrary_kill", "sha3_keyed_mapping"]
 
 
+@pytest.mark.parametrize("aux", [False, True])
 @pytest.mark.parametrize("shaped", [False, True])
 @pytest.mark.parametrize("name", WORKLOAD_NAMES)
-def test_workload_verdicts_match_c_restatement(engine, name, shaped):
+def test_workload_verdicts_match_c_restatement(engine, name, shaped, aux):
     """Every candidate verdict of the benchmark workloads (search-mode generator, broad
     or propagation-shaped; full evaluation) equals the C restatement's, and the search
     first hit/count agree."""
@@ -275,7 +276,7 @@ def test_workload_verdicts_match_c_restatement(engine, name, shaped):
     from oracle import cport
 
     roots = [c.raw for c in workloads.WORKLOADS[name]()]
-    P = ssa.flatten(roots)
+    P = ssa.flatten(roots, aux_words=aux)
     blob = search.default_generator(P, roots=roots if shaped else None).blob()
     n, start, seed = 1 << 14, 12345, 0x6D797468
     prog = engine.load(P.to_bytes())

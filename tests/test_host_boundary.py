@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol(lib):
     assert declared == set(native.EXPORTS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.mg_version() == 1
+    assert lib.mg_version() == 2
 
 
 def test_init_without_device_fails_loudly(lib):
