@@ -220,12 +220,18 @@ int mg_version(void);
 
 /* host-only checks (no GPU needed) */
 int mg_program_check(const uint8_t* ssa, size_t len, mg_program_info_t* info);
+/* ... and the program specialised for a generator blob (what mg_gen_info reports) */
+int mg_program_check_gen(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words,
+                         mg_program_info_t* info);
 
 int mg_program_load(const uint8_t* ssa, size_t len, uint64_t* prog_handle);
 int mg_program_info(uint64_t prog, mg_program_info_t* info);
 int mg_program_free(uint64_t prog);
 
+/* a generator also specialises the program for the candidates it draws (range-decided
+ * compares folded, dead code removed): mg_gen_info describes what searches run */
 int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* gen_handle);
+int mg_gen_info(uint64_t gen, mg_program_info_t* info);
 int mg_gen_free(uint64_t gen);
 
 /* soa_coords: coord_words rows of n uint32 (row r = limb of a coordinate, coords in order)

@@ -42,6 +42,16 @@ __device__ __constant__ static const uint32_t kEmptyKeccak[8] = {
 
 enum Mode : int { MODE_EVAL = 0, MODE_GEN = 1, MODE_SEARCH = 2 };
 
+// Program data (instructions, literals, generator specs) is read-only for a kernel's
+// lifetime.  Reading it through the constant address space lets the compiler use
+// scalar loads (and the scalar cache) for every wave-uniform read; through a generic
+// pointer it must assume the kernel's own stores may alias and fetches every
+// interpreted instruction with a vector load (measured: ~2,000 cycles per op).
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* cst(const T* p) {
+  return (const __attribute__((address_space(4))) T*)p;
+}
+
 struct KArgs {
   const Instr* code;
   const uint32_t* consts;
@@ -59,6 +69,27 @@ struct KArgs {
   uint64_t sk, sg;           // GEN2 seed keys (seed_lane_key / seed_group_key of seed)
   uint32_t n_instr, value_words, flags, pad;
 };
+
+// uniform struct reads through the constant address space (scalar loads)
+__device__ __forceinline__ GenSpec ld_spec(const KArgs& k, uint32_t c) {
+  const auto* p = cst((const uint32_t*)k.specs) + 8u * c;
+  GenSpec s;
+  s.kind = p[0];
+#pragma unroll
+  for (int q = 0; q < 7; q++) s.p[q] = p[1 + q];
+  return s;
+}
+
+__device__ __forceinline__ Instr ld_instr(const KArgs& k, uint32_t pc) {
+  const auto* p = cst((const uint32_t*)k.code) + 8u * pc;
+  // wave-uniform by construction: keep every field in SGPRs (a scalar opcode switch)
+  Instr in;
+  uint32_t* f = &in.op;
+#pragma unroll
+  for (int q = 0; q < 8; q++) f[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)p[q]);
+  return in;
+}
+
 
 // ---------------------------------------------------------------------------
 // value file policies
@@ -94,7 +125,7 @@ __device__ __forceinline__ uint32_t mixed_alt(const GenSpec& s, uint32_t ws) {
 
 // value of coordinate c before its finish (MIXED: the chosen non-COPY alternative)
 template <class VF>
-__device__ void gen_base(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c, uint32_t width, const GKeys& ky,
+__device__ __forceinline__ void gen_base(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c, uint32_t width, const GKeys& ky,
                          const GenSpec& s, uint32_t alt) {
   const uint32_t L = (width + 31) >> 5;
   switch (MG_GEN_KIND(s.kind)) {
@@ -102,13 +133,13 @@ __device__ void gen_base(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c,
       const uint32_t span = s.p[1], r = grnd(ky, c, 0);
       uint32_t off = span ? (uint32_t)(((uint64_t)r * span) >> 32) : r, cy = 0;
       for (uint32_t j = 0; j < L; j++) {
-        vf.at(dst + j) = __builtin_addc(k.gconsts[s.p[0] + j], j ? 0u : off, cy, &cy);
+        vf.at(dst + j) = __builtin_addc(cst(k.gconsts)[s.p[0] + j], j ? 0u : off, cy, &cy);
       }
       break;
     }
     case MG_GEN_DICT: {
       const uint32_t e = ((grnd(ky, c, 0xFFFFu) >> 16) * s.p[1]) >> 16;
-      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = k.gconsts[s.p[0] + e * L + j];
+      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = cst(k.gconsts)[s.p[0] + e * L + j];
       break;
     }
     case MG_GEN_ALIGNED: {
@@ -122,18 +153,18 @@ __device__ void gen_base(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c,
         if (bit0 <= -32 || bit0 >= 64) mw = 0;
         else if (bit0 < 0) mw = (uint32_t)(m << (-bit0));
         else mw = (uint32_t)(m >> bit0);
-        vf.at(dst + j) = __builtin_addc(k.gconsts[s.p[0] + j], mw, cy, &cy);
+        vf.at(dst + j) = __builtin_addc(cst(k.gconsts)[s.p[0] + j], mw, cy, &cy);
       }
       break;
     }
     case MG_GEN_FIXED:
-      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = k.gconsts[s.p[0] + j];
+      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = cst(k.gconsts)[s.p[0] + j];
       break;
     case MG_GEN_MIXED: {
       const uint32_t h = grnd(ky, c, 0xFFFFu);
       if (alt == ALT_DICT) {
         const uint32_t e = ((h >> 16) * s.p[1]) >> 16;
-        for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = k.gconsts[s.p[0] + e * L + j];
+        for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = cst(k.gconsts)[s.p[0] + e * L + j];
       } else {  // SMALL / UNIFORM
         const bool narrow = width <= MG_GEN_NARROW_BITS;
         const uint32_t bits = alt == ALT_SMALL ? min(width, s.p[4] >> 16) : width;
@@ -153,7 +184,7 @@ __device__ void gen_base(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c,
 
 // MIXED: per-lane delta on COPY/DICT, width mask, clamp; every kind: width mask, fixed bits
 template <class VF>
-__device__ void gen_finish(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c, uint32_t width,
+__device__ __forceinline__ void gen_finish(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c, uint32_t width,
                            const GKeys& ky, const GenSpec& s, uint32_t alt, uint32_t ws) {
   const uint32_t L = (width + 31) >> 5;
   if (MG_GEN_KIND(s.kind) == MG_GEN_MIXED) {
@@ -167,7 +198,7 @@ __device__ void gen_finish(const KArgs& k, const VF& vf, uint32_t dst, uint32_t 
     }
     vf.at(dst + L - 1) &= top_mask(width);
     if (s.p[6]) {  // clamp into [lo, lo + span)
-      const uint32_t* lo = k.gconsts + (s.p[6] - 1);
+      const auto* lo = cst(k.gconsts) + (s.p[6] - 1);
       const uint32_t span = lo[L];
       uint32_t br = 0, hi_or = 0, t0 = 0;
       for (uint32_t j = 0; j < L; j++) {
@@ -185,7 +216,7 @@ __device__ void gen_finish(const KArgs& k, const VF& vf, uint32_t dst, uint32_t 
   }
   vf.at(dst + L - 1) &= top_mask(width);
   if (const uint32_t fix = s.kind >> 8) {
-    const uint32_t* f = k.gconsts + (fix - 1);
+    const auto* f = cst(k.gconsts) + (fix - 1);
     for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = (vf.at(dst + j) & ~f[j]) | f[L + j];
   }
 }
@@ -195,9 +226,9 @@ __device__ void gen_finish(const KArgs& k, const VF& vf, uint32_t dst, uint32_t 
 // smaller indices, so it ends; parse_gen bounds its static length).  The root is
 // generated, then every link's finish is applied from the root back to c.
 template <class VF>
-__device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c, uint32_t width, const GKeys& ky) {
+__device__ __forceinline__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c, uint32_t width, const GKeys& ky) {
   uint32_t m = 0, root = c;
-  GenSpec s = k.specs[c];
+  GenSpec s = ld_spec(k, c);
   uint32_t ws = 0, alt = ALT_NONE;
   for (;;) {
     alt = ALT_NONE;
@@ -206,15 +237,15 @@ __device__ void gen_coord(const KArgs& k, const VF& vf, uint32_t dst, uint32_t c
     alt = mixed_alt(s, ws);
     if (alt != ALT_COPY) break;
     root = s.p[3];
-    s = k.specs[root];
+    s = ld_spec(k, root);
     m++;
   }
   gen_base(k, vf, dst, root, width, ky, s, alt);
   gen_finish(k, vf, dst, root, width, ky, s, alt, ws);
   while (m-- > 0) {  // link m: m steps from c
     uint32_t l = c;
-    for (uint32_t t = 0; t < m; t++) l = k.specs[l].p[3];
-    const GenSpec sl = k.specs[l];
+    for (uint32_t t = 0; t < m; t++) l = ld_spec(k, l).p[3];
+    const GenSpec sl = ld_spec(k, l);
     gen_finish(k, vf, dst, l, width, ky, sl, ALT_COPY, gwsel(ky, l));
   }
 }
@@ -261,7 +292,7 @@ __device__ __forceinline__ uint32_t keccak_byte(const VF& vf, uint32_t off, uint
 }
 
 template <class VF>
-__device__ void do_keccak(const VF& vf, const Instr& in) {
+__device__ __forceinline__ void do_keccak(const VF& vf, const Instr& in) {
   uint64_t st[25];
 #pragma unroll
   for (int i = 0; i < 25; i++) st[i] = 0;
@@ -298,78 +329,92 @@ __device__ void do_keccak(const VF& vf, const Instr& in) {
 // ---------------------------------------------------------------------------
 // interpreter
 // ---------------------------------------------------------------------------
-template <class VF, int MODE>
+// Per-limb loops run fully unrolled for the two widths that dominate LASER queries
+// (L = 8: 256-bit words; L = 1: Bools, bytes, <= 32-bit values): the value-file
+// offsets then fold into the ds_read/ds_write immediates and the limb control leaves
+// the scalar unit (a rolled loop costs ~6 SALU + a branch per limb).
+#define MG_LIMBS(L, BODY)                        \
+  do {                                           \
+    if ((L) == 8) {                              \
+      _Pragma("unroll") for (uint32_t j = 0; j < 8; j++) { BODY }  \
+    } else if ((L) == 1) {                       \
+      const uint32_t j = 0;                      \
+      { BODY }                                   \
+    } else {                                     \
+      for (uint32_t j = 0; j < (L); j++) { BODY } \
+    }                                            \
+  } while (0)
+
+// HEAVY = false: a program with no MUL/DIV/REM/shift/EXP/UMUL_NOOVF/KECCAK (most LASER
+// queries): those handlers hold ~200 VGPRs of 256-bit temporaries, so leaving them out
+// of the kernel lets several times more waves hide the LDS and scalar-load latency.
+template <class VF, int MODE, bool HEAVY>
 __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, uint64_t i, const GKeys& key,
                                                 bool early, bool active) {
   uint32_t verdict = 1;
-  const Instr* code = k.code;
   const uint32_t n_instr = k.n_instr;
   for (uint32_t pc = 0; pc < n_instr; pc++) {
-    const Instr in = code[pc];
+    const Instr in = ld_instr(k, pc);
     const uint32_t W = in.wd;
     const uint32_t L = (W + 31) >> 5;
     switch (in.op) {
       case K_CONST: {
-        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = k.consts[in.p0 + j];
+        const auto* c = cst(k.consts) + in.p0;
+        MG_LIMBS(L, vf.at(in.dst + j) = c[j];);
         break;
       }
       case K_COORD: {
         if (MODE == MODE_EVAL) {
-          for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = k.soa[(uint64_t)(in.p1 + j) * k.count + i];
+          MG_LIMBS(L, vf.at(in.dst + j) = k.soa[(uint64_t)(in.p1 + j) * k.count + i];);
         } else {
           gen_coord<VF>(k, vf, in.dst, in.p0, W, key);
         }
         break;
       }
       case K_COPY: {
-        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = vf.at(in.a + j);
+        MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j););
         break;
       }
-      case K_ADD:
+      case K_ADD: {
+        uint32_t c = 0;
+        MG_LIMBS(L, vf.at(in.dst + j) = __builtin_addc(vf.at(in.a + j), vf.at(in.b + j), c, &c););
+        write_masked(vf, in.dst, L, W);
+        break;
+      }
       case K_SUB: {
-        uint64_t c = 0;
-        const bool sub = in.op == K_SUB;
-        for (uint32_t j = 0; j < L; j++) {
-          const uint64_t x = vf.at(in.a + j), y = vf.at(in.b + j);
-          const uint64_t t = sub ? (x - y - c) : (x + y + c);
-          vf.at(in.dst + j) = (uint32_t)t;
-          c = sub ? ((t >> 32) & 1u) : (t >> 32);
-        }
+        uint32_t c = 0;
+        MG_LIMBS(L, vf.at(in.dst + j) = __builtin_subc(vf.at(in.a + j), vf.at(in.b + j), c, &c););
         write_masked(vf, in.dst, L, W);
         break;
       }
       case K_NEG: {
-        uint64_t c = 0;
-        for (uint32_t j = 0; j < L; j++) {
-          const uint64_t t = 0ull - (uint64_t)vf.at(in.a + j) - c;
-          vf.at(in.dst + j) = (uint32_t)t;
-          c = (t >> 32) & 1u;
-        }
+        uint32_t c = 0;
+        MG_LIMBS(L, vf.at(in.dst + j) = __builtin_subc(0u, vf.at(in.a + j), c, &c););
         write_masked(vf, in.dst, L, W);
         break;
       }
       case K_AND:
-        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = vf.at(in.a + j) & vf.at(in.b + j);
+        MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) & vf.at(in.b + j););
         break;
       case K_OR:
-        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = vf.at(in.a + j) | vf.at(in.b + j);
+        MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) | vf.at(in.b + j););
         break;
       case K_XOR:
-        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = vf.at(in.a + j) ^ vf.at(in.b + j);
+        MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) ^ vf.at(in.b + j););
         break;
       case K_NOT:
-        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = ~vf.at(in.a + j);
+        MG_LIMBS(L, vf.at(in.dst + j) = ~vf.at(in.a + j););
         write_masked(vf, in.dst, L, W);
         break;
       case K_ITE: {
         const bool c = vf.at(in.a) != 0;
-        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = c ? vf.at(in.b + j) : vf.at(in.c + j);
+        MG_LIMBS(L, vf.at(in.dst + j) = c ? vf.at(in.b + j) : vf.at(in.c + j););
         break;
       }
       case K_EQ: {
         const uint32_t La = (in.p1 + 31) >> 5;
         uint32_t d = 0;
-        for (uint32_t j = 0; j < La; j++) d |= vf.at(in.a + j) ^ vf.at(in.b + j);
+        MG_LIMBS(La, d |= vf.at(in.a + j) ^ vf.at(in.b + j););
         vf.at(in.dst) = d == 0;
         break;
       }
@@ -380,18 +425,11 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
         const uint32_t wa = in.p1, La = (wa + 31) >> 5;
         // a - b borrow chain; for signed compare flip the sign bits first
         const uint32_t sflip = (in.op == K_SLT || in.op == K_SLE) ? (1u << ((wa - 1) & 31)) : 0u;
-        uint64_t br = 0;
-        uint32_t nz = 0;
-        for (uint32_t j = 0; j < La; j++) {
-          uint32_t x = vf.at(in.a + j), y = vf.at(in.b + j);
-          if (j == La - 1) {
-            x ^= sflip;
-            y ^= sflip;
-          }
-          const uint64_t t = (uint64_t)x - y - br;
-          br = (t >> 32) & 1u;
-          nz |= (uint32_t)t;
-        }
+        uint32_t br = 0, nz = 0;
+        MG_LIMBS(La, {
+          const uint32_t f = j == La - 1 ? sflip : 0u;
+          nz |= __builtin_subc(vf.at(in.a + j) ^ f, vf.at(in.b + j) ^ f, br, &br);
+        });
         const bool lt = br != 0;
         const bool le = lt || nz == 0;
         vf.at(in.dst) = (in.op == K_ULT || in.op == K_SLT) ? (uint32_t)lt : (uint32_t)le;
@@ -412,7 +450,11 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
         break;
       }
       case K_EXTRACT: {
-        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = bits32(vf, in.a, in.p1, in.p0 + j * 32);
+        if (L == 1) {
+          vf.at(in.dst) = bits32(vf, in.a, in.p1, in.p0);
+        } else {
+          for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = bits32(vf, in.a, in.p1, in.p0 + j * 32);
+        }
         write_masked(vf, in.dst, L, W);
         break;
       }
@@ -421,75 +463,63 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
         const uint32_t wa = in.p1, La = (wa + 31) >> 5;
         uint32_t fill = 0;
         if (in.op == K_SEXT) fill = ((vf.at(in.a + La - 1) >> ((wa - 1) & 31)) & 1u) ? 0xFFFFFFFFu : 0u;
-        for (uint32_t j = 0; j < L; j++) {
-          uint32_t v;
+        const uint32_t tm = top_mask(wa);
+        MG_LIMBS(L, {
+          uint32_t v = fill;
           if (j < La) {
             v = vf.at(in.a + j);
-            if (j == La - 1) v = (v & top_mask(wa)) | (fill & ~top_mask(wa));
-          } else {
-            v = fill;
+            if (j == La - 1) v = (v & tm) | (fill & ~tm);
           }
           vf.at(in.dst + j) = v;
-        }
+        });
         write_masked(vf, in.dst, L, W);
         break;
       }
       case K_MUL: {
-        W8 r = mul8(ld8(vf, in.a, L), ld8(vf, in.b, L));
-        canon8(r, W);
-        st8(vf, in.dst, L, r);
+        if constexpr (HEAVY) {
+          W8 r = mul8(ld8(vf, in.a, L), ld8(vf, in.b, L));
+          canon8(r, W);
+          st8(vf, in.dst, L, r);
+        }
         break;
       }
       case K_UMUL_NOOVF: {
-        const uint32_t wa = in.p1, La = (wa + 31) >> 5;
-        const W8 x = ld8(vf, in.a, La), y = ld8(vf, in.b, La);
-        const W8 lo = mul8(x, y);
-        const W8 hi = mulhi8(x, y);
-        // no overflow <=> bits >= wa of the 512-bit product are all zero
-        uint32_t ov = 0;
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-          ov |= hi.w[q];
-          const uint32_t lw = lo.w[q];
-          const uint32_t bit0 = q * 32;
-          uint32_t m;
-          if (bit0 + 32 <= wa) m = 0u;
-          else if (bit0 >= wa) m = 0xFFFFFFFFu;
-          else m = ~((1u << (wa - bit0)) - 1u);
-          ov |= lw & m;
+        if constexpr (HEAVY) {
+          const uint32_t wa = in.p1, La = (wa + 31) >> 5;
+          vf.at(in.dst) = umul_noovf8(ld8(vf, in.a, La), ld8(vf, in.b, La), wa);
         }
-        vf.at(in.dst) = ov == 0;
         break;
       }
-      case K_UDIV: st8(vf, in.dst, L, bv_udiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
-      case K_UREM: st8(vf, in.dst, L, bv_urem(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
-      case K_SDIV: st8(vf, in.dst, L, bv_sdiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
-      case K_SREM: st8(vf, in.dst, L, bv_srem(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
-      case K_SMOD: st8(vf, in.dst, L, bv_smod(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
-      case K_SHL: st8(vf, in.dst, L, bv_shl(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
-      case K_LSHR: st8(vf, in.dst, L, bv_lshr(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
-      case K_ASHR: st8(vf, in.dst, L, bv_ashr(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
-      case K_EXP: st8(vf, in.dst, L, bv_exp(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); break;
+      case K_UDIV: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_udiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_UREM: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_urem(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_SDIV: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_sdiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_SREM: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_srem(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_SMOD: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_smod(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_SHL: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_shl(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_LSHR: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_lshr(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_ASHR: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_ashr(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_EXP: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_exp(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
       case K_LOOKUP: {
         const uint32_t Lk = (in.b + 31) >> 5;
         uint32_t src = in.p0;
         bool found = false;
         for (uint32_t p = 0; p < in.c; p++) {
-          const uint32_t ko = k.aux[in.p1 + 2 * p], vo = k.aux[in.p1 + 2 * p + 1];
+          const uint32_t ko = cst(k.aux)[in.p1 + 2 * p], vo = cst(k.aux)[in.p1 + 2 * p + 1];
           uint32_t d = 0;
-          for (uint32_t j = 0; j < Lk; j++) d |= vf.at(in.a + j) ^ vf.at(ko + j);
+          MG_LIMBS(Lk, d |= vf.at(in.a + j) ^ vf.at(ko + j););
           const bool hit = !found && d == 0;
           src = hit ? vo : src;
           found = found || hit;
         }
-        for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = vf.at(src + j);
+        // src differs per lane: gather the limbs from the selected slot
+        MG_LIMBS(L, vf.at(in.dst + j) = vf.at(src + j););
         break;
       }
       case K_KECCAK: {
         if (in.a == MG_NONE) {
           // keccak256("") — the constant of keccak_function_manager.py:75-81
           for (uint32_t j = 0; j < 8; j++) vf.at(in.dst + j) = kEmptyKeccak[j];
-        } else {
+        } else if constexpr (HEAVY) {
           do_keccak(vf, in);
         }
         break;
@@ -512,7 +542,7 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
   return verdict;
 }
 
-template <class VF, int MODE>
+template <class VF, int MODE, bool HEAVY>
 __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
   extern __shared__ uint32_t lds[];
   VF vf(lds, k);
@@ -540,7 +570,7 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
     }
     GKeys key{};
     if (MODE != MODE_EVAL) key = gen_keys(idx, k.sk, k.sg);
-    uint32_t v = run_program<VF, MODE>(k, vf, i, key, early, active);
+    uint32_t v = run_program<VF, MODE, HEAVY>(k, vf, i, key, early, active);
     v = active ? v : 0u;
     if (MODE == MODE_SEARCH) {
       const unsigned long long m = __ballot(v != 0);
@@ -602,6 +632,7 @@ thread_local std::string g_err;
 
 struct DevProgram {
   Lowered low;
+  bool heavy = true;  // has MUL/DIV/REM/shift/EXP/UMUL_NOOVF/KECCAK: the full interpreter
   Instr* d_code = nullptr;
   uint32_t* d_consts = nullptr;
   uint32_t* d_aux = nullptr;
@@ -615,6 +646,7 @@ struct DevGen {
   std::vector<uint32_t> consts;
   GenSpec* d_specs = nullptr;
   uint32_t* d_consts = nullptr;
+  DevProgram spec;                // the program specialised for this generator (what searches run)
 };
 
 struct DevJit {
@@ -671,6 +703,48 @@ static int upload(T** d, const T* h, size_t n) {
   return MG_OK;
 }
 
+static int upload_code(DevProgram& p) {
+  int rc;
+  p.lds = p.low.value_words <= kLdsWordsMax;
+  p.heavy = false;
+  for (const Instr& in : p.low.code) {
+    switch (in.op) {
+      case K_MUL: case K_UDIV: case K_UREM: case K_SDIV: case K_SREM: case K_SMOD: case K_SHL: case K_LSHR:
+      case K_ASHR: case K_EXP: case K_UMUL_NOOVF: p.heavy = true; break;
+      case K_KECCAK: if (in.a != MG_NONE) p.heavy = true; break;
+      default: break;
+    }
+  }
+  if ((rc = upload(&p.d_code, p.low.code.data(), p.low.code.size()))) return rc;
+  if ((rc = upload(&p.d_consts, p.low.consts.data(), p.low.consts.size()))) return rc;
+  if ((rc = upload(&p.d_aux, p.low.aux.data(), p.low.aux.size()))) return rc;
+  if ((rc = upload(&p.d_coord_width, p.low.coord_width.data(), p.low.coord_width.size()))) return rc;
+  return MG_OK;
+}
+
+static void free_code(DevProgram& p) {
+  (void)hipFree(p.d_code);
+  (void)hipFree(p.d_consts);
+  (void)hipFree(p.d_aux);
+  (void)hipFree(p.d_coord_width);
+  p.d_code = nullptr;
+  p.d_consts = p.d_aux = p.d_coord_width = nullptr;
+}
+
+static void fill_info(const DevProgram& p, mg_program_info_t* info) {
+  std::memset(info, 0, sizeof(*info));
+  info->n_nodes = p.low.n_nodes;
+  info->n_instrs = (uint32_t)p.low.code.size();
+  info->n_coords = p.low.n_coords;
+  info->n_roots = p.low.n_roots;
+  info->value_words = p.low.value_words;
+  info->uses_lds = p.lds;
+  info->n_watch = p.low.n_watch;
+  info->watch_words = p.low.watch_words;
+  info->coord_words = p.low.coord_words;
+  info->limb_ops = p.low.limb_ops;
+}
+
 static int ensure_scratch(Engine& e, size_t bytes) {
   if (bytes <= e.scratch_bytes) return MG_OK;
   if (e.d_scratch) (void)hipFree(e.d_scratch);
@@ -681,13 +755,15 @@ static int ensure_scratch(Engine& e, size_t bytes) {
   return MG_OK;
 }
 
-// grid: enough waves to fill 256 CUs several times over, never more than needed
-static uint32_t grid_for(const Engine& e, uint64_t count, bool lds, uint32_t value_words) {
+// grid: enough waves to fill 256 CUs several times over, never more than needed.
+// Resident waves per CU: the LDS value file (160 KiB per CU) and the VGPRs of the
+// kernel variant (heavy ~230: 2 waves/SIMD; light ~55: 8 waves/SIMD).
+static uint32_t grid_for(const Engine& e, uint64_t count, bool lds, uint32_t value_words, bool heavy) {
   uint64_t want = (count + kWave - 1) / kWave;
-  uint32_t waves_per_cu = 8;
+  uint32_t waves_per_cu = heavy ? 8 : 32;
   if (lds) {
     const uint32_t bytes = value_words * kWave * 4;
-    waves_per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (160u * 1024u) / std::max<uint32_t>(bytes, 1)));
+    waves_per_cu = std::max<uint32_t>(1, std::min<uint32_t>(waves_per_cu, (160u * 1024u) / std::max<uint32_t>(bytes, 1)));
   }
   uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * waves_per_cu * 4;
   return (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
@@ -698,7 +774,7 @@ static int launch(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   if (count == 0) return MG_OK;
   // GEN / SEARCH sweep whole aligned 64-index groups (k_run)
   const uint64_t lanes = MODE == MODE_EVAL ? count : (k.start + count) - (k.start & ~63ull);
-  const uint32_t grid = grid_for(e, lanes, p.lds, p.low.value_words);
+  const uint32_t grid = grid_for(e, lanes, p.lds, p.low.value_words, p.heavy);
   k.sk = seed_lane_key(k.seed);
   k.sg = seed_group_key(k.seed);
   k.code = p.d_code;
@@ -717,10 +793,14 @@ static int launch(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   }
   const size_t shmem = p.lds ? (size_t)p.low.value_words * kWave * 4 : 0;
   HIPCHK(hipEventRecord(e.ev0, e.stream));
-  if (p.lds)
-    hipLaunchKernelGGL((k_run<VFLds, MODE>), dim3(grid), dim3(kWave), shmem, e.stream, k);
+  if (p.lds && p.heavy)
+    hipLaunchKernelGGL((k_run<VFLds, MODE, true>), dim3(grid), dim3(kWave), shmem, e.stream, k);
+  else if (p.lds)
+    hipLaunchKernelGGL((k_run<VFLds, MODE, false>), dim3(grid), dim3(kWave), shmem, e.stream, k);
+  else if (p.heavy)
+    hipLaunchKernelGGL((k_run<VFGlobal, MODE, true>), dim3(grid), dim3(kWave), 0, e.stream, k);
   else
-    hipLaunchKernelGGL((k_run<VFGlobal, MODE>), dim3(grid), dim3(kWave), 0, e.stream, k);
+    hipLaunchKernelGGL((k_run<VFGlobal, MODE, false>), dim3(grid), dim3(kWave), 0, e.stream, k);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e.ev1, e.stream));
   HIPCHK(hipEventSynchronize(e.ev1));
@@ -780,16 +860,12 @@ void mg_shutdown(void) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
   if (!e.init) return;
-  for (auto& kv : e.progs) {
-    (void)hipFree(kv.second->d_code);
-    (void)hipFree(kv.second->d_consts);
-    (void)hipFree(kv.second->d_aux);
-    (void)hipFree(kv.second->d_coord_width);
-  }
+  for (auto& kv : e.progs) free_code(*kv.second);
   e.progs.clear();
   for (auto& kv : e.gens) {
     (void)hipFree(kv.second->d_specs);
     (void)hipFree(kv.second->d_consts);
+    free_code(kv.second->spec);
   }
   e.gens.clear();
   if (e.d_scratch) (void)hipFree(e.d_scratch);
@@ -823,6 +899,23 @@ int mg_program_check(const uint8_t* ssa, size_t len, mg_program_info_t* info) {
   return MG_OK;
 }
 
+int mg_program_check_gen(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words,
+                         mg_program_info_t* info) {
+  DevProgram base, sp;
+  std::string err;
+  int rc = lower_program(ssa, len, base.low, err);
+  if (rc) return set_err(rc, err);
+  std::vector<GenSpec> specs;
+  std::vector<uint32_t> consts;
+  rc = parse_gen(base.low, gen_blob, gen_words, specs, consts, err);
+  if (rc) return set_err(rc, err);
+  rc = specialize_program(base.low, &specs, &consts, sp.low, err);
+  if (rc) return set_err(rc, err);
+  sp.lds = sp.low.value_words <= kLdsWordsMax;
+  if (info) fill_info(sp, info);
+  return MG_OK;
+}
+
 int mg_program_load(const uint8_t* ssa, size_t len, uint64_t* handle) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
@@ -831,11 +924,7 @@ int mg_program_load(const uint8_t* ssa, size_t len, uint64_t* handle) {
   std::string err;
   int rc = lower_program(ssa, len, p->low, err);
   if (rc) return set_err(rc, err);
-  p->lds = p->low.value_words <= kLdsWordsMax;
-  if ((rc = upload(&p->d_code, p->low.code.data(), p->low.code.size()))) return rc;
-  if ((rc = upload(&p->d_consts, p->low.consts.data(), p->low.consts.size()))) return rc;
-  if ((rc = upload(&p->d_aux, p->low.aux.data(), p->low.aux.size()))) return rc;
-  if ((rc = upload(&p->d_coord_width, p->low.coord_width.data(), p->low.coord_width.size()))) return rc;
+  if ((rc = upload_code(*p))) return rc;
   const uint64_t h = e.next_handle++;
   e.progs[h] = std::move(p);
   e.stats.programs_loaded++;
@@ -853,17 +942,16 @@ int mg_program_info(uint64_t prog, mg_program_info_t* info) {
   std::lock_guard<std::mutex> g(e.mu);
   DevProgram* p = find_prog(e, prog);
   if (!p) return set_err(MG_E_INVALID, "bad program handle");
-  std::memset(info, 0, sizeof(*info));
-  info->n_nodes = p->low.n_nodes;
-  info->n_instrs = (uint32_t)p->low.code.size();
-  info->n_coords = p->low.n_coords;
-  info->n_roots = p->low.n_roots;
-  info->value_words = p->low.value_words;
-  info->uses_lds = p->lds;
-  info->n_watch = p->low.n_watch;
-  info->watch_words = p->low.watch_words;
-  info->coord_words = p->low.coord_words;
-  info->limb_ops = p->low.limb_ops;
+  fill_info(*p, info);
+  return MG_OK;
+}
+
+int mg_gen_info(uint64_t gen, mg_program_info_t* info) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  auto it = e.gens.find(gen);
+  if (it == e.gens.end()) return set_err(MG_E_INVALID, "bad generator handle");
+  fill_info(it->second->spec, info);
   return MG_OK;
 }
 
@@ -872,10 +960,7 @@ int mg_program_free(uint64_t prog) {
   std::lock_guard<std::mutex> g(e.mu);
   auto it = e.progs.find(prog);
   if (it == e.progs.end()) return set_err(MG_E_INVALID, "bad program handle");
-  (void)hipFree(it->second->d_code);
-  (void)hipFree(it->second->d_consts);
-  (void)hipFree(it->second->d_aux);
-  (void)hipFree(it->second->d_coord_width);
+  free_code(*it->second);
   e.progs.erase(it);
   return MG_OK;
 }
@@ -894,6 +979,9 @@ int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* g
   gg->prog = prog;
   gg->specs = specs;
   gg->consts = consts;
+  rc = specialize_program(p->low, &gg->specs, &gg->consts, gg->spec.low, err);
+  if (rc) return set_err(rc, err);
+  if ((rc = upload_code(gg->spec))) return rc;
   if ((rc = upload(&gg->d_specs, specs.data(), specs.size()))) return rc;
   if ((rc = upload(&gg->d_consts, consts.data(), consts.size()))) return rc;
   const uint64_t h = e.next_handle++;
@@ -909,6 +997,7 @@ int mg_gen_free(uint64_t gen) {
   if (it == e.gens.end()) return set_err(MG_E_INVALID, "bad generator handle");
   (void)hipFree(it->second->d_specs);
   (void)hipFree(it->second->d_consts);
+  free_code(it->second->spec);
   e.gens.erase(it);
   return MG_OK;
 }
@@ -976,7 +1065,7 @@ int mg_eval_generated(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start
   k.watch = d_watch;
   k.start = start;
   k.seed = seed;
-  int rc = launch<MODE_GEN>(e, *p, k, n);
+  int rc = launch<MODE_GEN>(e, it->second->spec, k, n);
   if (rc == MG_OK) {
     HIPCHK(hipMemcpy(verdict_out, d_ver, n, hipMemcpyDeviceToHost));
     if (d_watch) HIPCHK(hipMemcpy(watch_out, d_watch, watch_bytes, hipMemcpyDeviceToHost));
@@ -1004,7 +1093,7 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
   k.start = start;
   k.seed = seed;
   k.flags = flags;
-  int rc = launch<MODE_SEARCH>(e, *p, k, count);
+  int rc = launch<MODE_SEARCH>(e, it->second->spec, k, count);
   if (rc) return rc;
   unsigned long long res[2];
   HIPCHK(hipMemcpy(res, e.d_hit, sizeof(res), hipMemcpyDeviceToHost));
@@ -1097,10 +1186,12 @@ int mg_dev_download(void* dst, const void* dptr, size_t bytes) {
 // ---------------------------------------------------------------------------
 namespace mg {
 
-static int jit_launch(Engine& e, hipFunction_t f, int nb, uint64_t count, void** args) {
+// `nblk` is the kernel's grid-size argument (the JIT kernels read no dispatch packet)
+static int jit_launch(Engine& e, hipFunction_t f, int nb, uint64_t count, void** args, uint32_t& nblk) {
   const uint64_t want = (count + 255) / 256;
   const uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * std::max(nb, 1) * 2;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+  nblk = grid;
   HIPCHK(hipEventRecord(e.ev0, e.stream));
   HIPCHK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, e.stream, args, nullptr));
   HIPCHK(hipEventRecord(e.ev1, e.stream));
@@ -1131,8 +1222,11 @@ int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_bl
     rc = parse_gen(low, gen_blob, gen_words, specs, consts, err);
     if (rc) return set_err(rc, err);
   }
-  const std::string src = gen_blob ? jit_source(low, &specs, &consts, true, false)
-                                   : jit_source(low, nullptr, nullptr, false, true);
+  Lowered sp;
+  rc = specialize_program(low, gen_blob ? &specs : nullptr, gen_blob ? &consts : nullptr, sp, err);
+  if (rc) return set_err(rc, err);
+  const std::string src = gen_blob ? jit_source(sp, &specs, &consts, true, false)
+                                   : jit_source(sp, nullptr, nullptr, false, true);
   if (out_len) *out_len = src.size();
   if (buf && cap) {
     const size_t n = std::min(cap - 1, src.size());
@@ -1160,8 +1254,16 @@ int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle) {
     gp = it->second.get();
   }
   // with a generator: the search kernel specialised on it; without: the eval kernel
-  const std::string src =
-      gp ? jit_source(p->low, &gp->specs, &gp->consts, true, false) : jit_source(p->low, nullptr, nullptr, false, true);
+  std::string src;
+  if (gp) {
+    src = jit_source(gp->spec.low, &gp->specs, &gp->consts, true, false);
+  } else {
+    Lowered ev;
+    std::string err;
+    int rc = specialize_program(p->low, nullptr, nullptr, ev, err);
+    if (rc) return set_err(rc, err);
+    src = jit_source(ev, nullptr, nullptr, false, true);
+  }
   auto t0 = std::chrono::steady_clock::now();
   auto hit = e.code_cache.find(src);
   if (hit == e.code_cache.end()) {
@@ -1227,10 +1329,11 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
   const uint32_t* gconsts = git->second->d_consts;
   unsigned long long* hitp = e.d_hit;
   uint64_t sk = seed_lane_key(seed), sg = seed_group_key(seed);
-  void* args[] = {&gconsts, &start, &count, &sk, &sg, &hitp, &flags};
+  uint32_t nblk = 0;
+  void* args[] = {&gconsts, &start, &count, &sk, &sg, &hitp, &flags, &nblk};
   // one wave per aligned 64-index group
   const uint64_t lanes = (start + count) - (start & ~63ull);
-  int rc = jit_launch(e, j.fsearch, j.nb_search, lanes, args);
+  int rc = jit_launch(e, j.fsearch, j.nb_search, lanes, args, nblk);
   if (rc) return rc;
   unsigned long long res[2];
   HIPCHK(hipMemcpy(res, e.d_hit, sizeof(res), hipMemcpyDeviceToHost));
@@ -1247,8 +1350,9 @@ int mg_jit_eval_dev(uint64_t jit, const uint32_t* d_soa, uint64_t n, uint8_t* d_
   if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
   DevJit& j = *it->second;
   if (!j.feval) return set_err(MG_E_INVALID, "jit was not compiled for eval (compile with gen = 0)");
-  void* args[] = {&d_soa, &n, &d_verdict, &d_watch};
-  return jit_launch(e, j.feval, j.nb_eval, n, args);
+  uint32_t nblk = 0;
+  void* args[] = {&d_soa, &n, &d_verdict, &d_watch, &nblk};
+  return jit_launch(e, j.feval, j.nb_eval, n, args, nblk);
 }
 
 int mg_jit_eval(uint64_t jit, const uint32_t* soa, uint64_t n, uint8_t* verdict_out, uint32_t* watch_out) {

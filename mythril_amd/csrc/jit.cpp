@@ -35,392 +35,11 @@ struct Gen {
       if (P.vcode[k].dst != MG_NONE && P.vcode[k].dst < def.size() && def[P.vcode[k].dst] < 0)
         def[P.vcode[k].dst] = (int32_t)k;
   }
-  const Instr* def_of(uint32_t id) const {
-    id = res(id);
-    return def[id] >= 0 ? &P.vcode[def[id]] : nullptr;
-  }
+  const Instr* def_of(uint32_t id) const { return def[id] >= 0 ? &P.vcode[def[id]] : nullptr; }
   // literal limbs of a value defined by K_CONST (else nullptr)
   const uint32_t* lit(uint32_t id) const {
     const Instr* d = def_of(id);
     return (d && d->op == K_CONST) ? &P.consts[d->p0] : nullptr;
-  }
-
-  // ---- value ranges, folding and aliases (analyze) ---------------------------
-  // rng[id]: when known, the value lies in [lo, hi] (so it fits in 64 bits).  In the
-  // search kernel a coordinate's range comes from its generator spec, which bounds
-  // EVERY candidate the kernel evaluates (clamp records, dictionaries, fixed bits), so a
-  // comparison decided by the ranges is decided for every candidate: it folds to a
-  // literal, an ITE on it becomes an alias of the chosen arm, and bits() then looks
-  // through it (e.g. the calldata guard If(k < size, calldata[k], 0) with size drawn
-  // from [68, 2^32) collapses to the byte, and a CALLDATALOAD to its AUX word).
-  struct Rng {
-    bool k = false;
-    uint64_t lo = 0, hi = 0;
-  };
-  std::vector<Rng> rng;
-  std::vector<int8_t> fold;       // per id: -1, or the folded Bool value
-  std::vector<uint32_t> alias;    // per id: the id it equals (itself if none)
-  std::vector<char> skip;         // per instruction: defines an alias / a decided assert
-  std::vector<Rng> crng;          // per coordinate (search mode)
-
-  uint32_t res(uint32_t id) const {
-    if (alias.empty() || id >= alias.size()) return id;
-    while (alias[id] != id) id = alias[id];
-    return id;
-  }
-  static Rng full(uint32_t w) {
-    Rng r;
-    if (w <= 64) {
-      r.k = true;
-      r.hi = w == 64 ? ~0ull : ((1ull << w) - 1ull);
-    }
-    return r;
-  }
-  static Rng exact(uint64_t v) {
-    Rng r;
-    r.k = true;
-    r.lo = r.hi = v;
-    return r;
-  }
-  static Rng hull(const Rng& a, const Rng& b) {
-    Rng r;
-    if (!a.k || !b.k) return r;
-    r.k = true;
-    r.lo = std::min(a.lo, b.lo);
-    r.hi = std::max(a.hi, b.hi);
-    return r;
-  }
-  // limbs [0, L) as one u64 if every limb >= 2 is zero
-  static bool fits64(const uint32_t* x, uint32_t L, uint64_t* v) {
-    for (uint32_t j = 2; j < L; j++)
-      if (x[j]) return false;
-    *v = (uint64_t)x[0] | (L > 1 ? (uint64_t)x[1] << 32 : 0ull);
-    return true;
-  }
-
-  // range of a generated coordinate's final value (include/mythgpu.h GEN2)
-  Rng coord_range(uint32_t c) const {
-    const GenSpec& sp = (*specs)[c];
-    const uint32_t w = P.coord_width[c], L = Lw(w), kind = sp.kind & 0xFFu;
-    const auto& G = *gconsts;
-    const unsigned __int128 wlim = w >= 128 ? ~(unsigned __int128)0 : (((unsigned __int128)1 << w) - 1);
-    Rng r;
-    switch (kind) {
-      case MG_GEN_FIXED: {
-        uint64_t v;
-        if (fits64(&G[sp.p[0]], L, &v)) r = exact(v);
-        break;
-      }
-      case MG_GEN_DICT:
-      case MG_GEN_MIXED: {
-        Rng d;  // dictionary hull
-        bool ok = sp.p[1] > 0;
-        for (uint32_t e = 0; ok && e < sp.p[1]; e++) {
-          uint64_t v;
-          if (!fits64(&G[sp.p[0] + e * L], L, &v)) ok = false;
-          else d = d.k ? hull(d, exact(v)) : exact(v);
-        }
-        if (kind == MG_GEN_DICT) {
-          if (ok) r = d;
-          break;
-        }
-        if (sp.p[6]) {  // clamp record: the final value is inside [lo, lo + span)
-          uint64_t lo;
-          const uint32_t rec = sp.p[6] - 1;
-          if (fits64(&G[rec], L, &lo)) {
-            const uint64_t span = G[rec + L] ? G[rec + L] : (1ull << 32);
-            if ((unsigned __int128)lo + span - 1 <= (unsigned __int128)~0ull) {
-              r.k = true;
-              r.lo = lo;
-              r.hi = lo + span - 1;
-            }
-          }
-          break;
-        }
-        const uint32_t pc = sp.p[3] != MG_NONE ? (sp.p[2] & 0xFFFFu) : 0u;
-        const uint32_t pd = sp.p[1] ? (sp.p[2] >> 16) : 0u;
-        const uint32_t ps = sp.p[4] & 0xFFFFu;
-        Rng u;
-        bool have = false, unknown = false;
-        auto add = [&](const Rng& x) {
-          if (!x.k) unknown = true;
-          else u = have ? hull(u, x) : x;
-          have = true;
-        };
-        Rng cd;  // COPY / DICT part, before the delta
-        bool cd_have = false, cd_unknown = false;
-        if (pc) {
-          const Rng s = crng[sp.p[3]];
-          if (!s.k) cd_unknown = true;
-          else cd = s;
-          cd_have = true;
-        }
-        if (pd) {
-          if (!ok) cd_unknown = true;
-          else cd = cd_have && cd.k ? hull(cd, d) : d;
-          cd_have = true;
-        }
-        if (cd_have) {
-          if (cd_unknown) add(Rng{});
-          else if (sp.p[5]) {  // +/-2 at most, no wrap
-            if (cd.lo >= 2 && (unsigned __int128)cd.hi + 2 <= wlim && cd.hi + 2 > cd.hi) {
-              Rng x;
-              x.k = true;
-              x.lo = cd.lo - 2;
-              x.hi = cd.hi + 2;
-              add(x);
-            } else {
-              add(full(w));
-            }
-          } else {
-            add(cd);
-          }
-        }
-        const uint32_t sb = std::min(w, sp.p[4] >> 16);
-        if (ps) add(full(sb));
-        if (pc + pd + ps < 65536u) add(full(w));
-        if (have && !unknown) r = u;
-        break;
-      }
-      case MG_GEN_RANGE: {
-        uint64_t lo;
-        if (fits64(&G[sp.p[0]], L, &lo)) {
-          const uint64_t span = sp.p[1] ? sp.p[1] : (1ull << 32);
-          if ((unsigned __int128)lo + span - 1 <= wlim && (unsigned __int128)lo + span - 1 <= (unsigned __int128)~0ull) {
-            r.k = true;
-            r.lo = lo;
-            r.hi = lo + span - 1;
-          }
-        }
-        break;
-      }
-      case MG_GEN_ALIGNED: {
-        uint64_t lo;
-        if (fits64(&G[sp.p[0]], L, &lo) && sp.p[1] < 64) {
-          const unsigned __int128 cnt = sp.p[2] ? sp.p[2] : (1ull << 32);
-          const unsigned __int128 top = (unsigned __int128)lo + ((cnt - 1) << sp.p[1]);
-          if (top <= wlim && top <= (unsigned __int128)~0ull) {
-            r.k = true;
-            r.lo = lo;
-            r.hi = (uint64_t)top;
-          }
-        }
-        break;
-      }
-      default:  // UNIFORM / LAZY
-        r = full(w);
-        break;
-    }
-    if (!r.k) r = full(w);
-    if (const uint32_t fix = sp.kind >> 8) {  // (v & ~m) | val lies in [val, val | ~m]
-      const uint32_t f = fix - 1;
-      uint64_t m, val;
-      std::vector<uint32_t> nm(L);
-      for (uint32_t j = 0; j < L; j++) nm[j] = ~G[f + j];
-      if (w & 31) nm[L - 1] &= (1u << (w & 31)) - 1u;
-      if (fits64(&G[f + L], L, &val) && fits64(nm.data(), L, &m)) {
-        r.k = true;
-        r.lo = val;
-        r.hi = val | m;
-      } else {
-        r = Rng{};
-      }
-    }
-    return r;
-  }
-
-  // decide a comparison from operand ranges: -1 undecided, else 0 / 1
-  static int decide(uint32_t op, const Rng& a, const Rng& b, uint32_t wa) {
-    if (!a.k || !b.k) return -1;
-    if (op == K_SLT || op == K_SLE) {
-      const uint64_t sign = wa >= 65 ? 0ull : (1ull << (wa - 1));
-      if (sign && (a.hi >= sign || b.hi >= sign)) return -1;  // a negative value may be inside
-      op = op == K_SLT ? K_ULT : K_ULE;
-    }
-    switch (op) {
-      case K_ULT:
-        if (a.hi < b.lo) return 1;
-        if (a.lo >= b.hi) return 0;
-        return -1;
-      case K_ULE:
-        if (a.hi <= b.lo) return 1;
-        if (a.lo > b.hi) return 0;
-        return -1;
-      case K_EQ:
-        if (a.lo == a.hi && b.lo == b.hi && a.lo == b.lo) return 1;
-        if (a.hi < b.lo || b.hi < a.lo) return 0;
-        return -1;
-      default:
-        return -1;
-    }
-  }
-
-  void analyze(bool search) {
-    const size_t nv = P.vwidth.size();
-    rng.assign(nv, Rng{});
-    fold.assign(nv, -1);
-    alias.resize(nv);
-    for (size_t i = 0; i < nv; i++) alias[i] = (uint32_t)i;
-    skip.assign(P.vcode.size(), 0);
-    if (search && specs) {
-      crng.assign(P.n_coords, Rng{});
-      for (uint32_t c = 0; c < P.n_coords; c++) crng[c] = coord_range(c);
-    }
-    for (size_t k = 0; k < P.vcode.size(); k++) {
-      const Instr& in = P.vcode[k];
-      const uint32_t d = in.dst, W = in.wd;
-      auto R = [&](uint32_t id) { return rng[res(id)]; };
-      auto F = [&](uint32_t id) { return (int)fold[res(id)]; };
-      auto alias_to = [&](uint32_t src) {
-        alias[d] = res(src);
-        rng[d] = rng[res(src)];
-        fold[d] = fold[res(src)];
-        skip[k] = 1;
-      };
-      auto set_fold = [&](int v) {
-        fold[d] = (int8_t)v;
-        rng[d] = exact((uint64_t)v);
-      };
-      if (d == MG_NONE || d >= nv) {
-        if (in.op == K_ASSERT && F(in.a) == 1) skip[k] = 1;
-        continue;
-      }
-      Rng r = full(W);
-      switch (in.op) {
-        case K_CONST: {
-          uint64_t v;
-          if (fits64(&P.consts[in.p0], Lw(W), &v)) r = exact(v);
-          break;
-        }
-        case K_COORD:
-          if (search && specs) r = crng[in.p0];
-          break;
-        case K_COPY:
-          alias_to(in.a);
-          continue;
-        case K_ZEXT:
-          if (R(in.a).k) r = R(in.a);
-          break;
-        case K_EXTRACT: {
-          const Rng a = R(in.a);
-          if (a.k && in.p0 < 64 && (W >= 64 || (a.hi >> in.p0) < (1ull << W))) {
-            r.k = true;
-            r.lo = a.lo >> in.p0;
-            r.hi = a.hi >> in.p0;
-          } else if (a.k && in.p0 >= 64) {
-            r = exact(0);
-          }
-          break;
-        }
-        case K_CONCAT: {
-          const Rng a = R(in.a), b = R(in.b);
-          const uint32_t wb = in.p1;
-          if (a.k && b.k && wb < 64 && (a.hi >> (64 - wb)) == 0) {
-            r.k = true;
-            r.lo = (a.lo << wb) | b.lo;
-            r.hi = (a.hi << wb) | b.hi;
-          }
-          break;
-        }
-        case K_AND:
-        case K_OR:
-        case K_XOR: {
-          const int fa = F(in.a), fb = F(in.b);
-          if (W == 1) {
-            if (in.op == K_AND) {
-              if (fa == 0 || fb == 0) { set_fold(0); continue; }
-              if (fa == 1) { alias_to(in.b); continue; }
-              if (fb == 1) { alias_to(in.a); continue; }
-            } else if (in.op == K_OR) {
-              if (fa == 1 || fb == 1) { set_fold(1); continue; }
-              if (fa == 0) { alias_to(in.b); continue; }
-              if (fb == 0) { alias_to(in.a); continue; }
-            } else if (fa >= 0 && fb >= 0) {
-              set_fold(fa ^ fb);
-              continue;
-            }
-            break;
-          }
-          const Rng a = R(in.a), b = R(in.b);
-          if (in.op == K_AND) {
-            if (a.k || b.k) {
-              r.k = true;
-              r.lo = 0;
-              r.hi = std::min(a.k ? a.hi : ~0ull, b.k ? b.hi : ~0ull);
-            }
-          } else if (a.k && b.k) {
-            const uint64_t m = std::max(a.hi, b.hi);
-            r.k = true;
-            r.lo = 0;
-            r.hi = m ? (~0ull >> __builtin_clzll(m)) : 0ull;
-          }
-          break;
-        }
-        case K_NOT:
-          if (W == 1 && F(in.a) >= 0) {
-            set_fold(1 - F(in.a));
-            continue;
-          }
-          break;
-        case K_ITE: {
-          const int fc = F(in.a);
-          if (fc >= 0) {
-            alias_to(fc ? in.b : in.c);
-            continue;
-          }
-          const Rng h = hull(R(in.b), R(in.c));
-          if (h.k) r = h;
-          break;
-        }
-        case K_ADD: {
-          const Rng a = R(in.a), b = R(in.b);
-          if (a.k && b.k && (unsigned __int128)a.hi + b.hi <= (unsigned __int128)full(std::min(W, 64u)).hi) {
-            r.k = true;
-            r.lo = a.lo + b.lo;
-            r.hi = a.hi + b.hi;
-          }
-          break;
-        }
-        case K_SUB: {
-          const Rng a = R(in.a), b = R(in.b);
-          if (a.k && b.k && a.lo >= b.hi) {
-            r.k = true;
-            r.lo = a.lo - b.hi;
-            r.hi = a.hi - b.lo;
-          }
-          break;
-        }
-        case K_EQ:
-        case K_ULT:
-        case K_ULE:
-        case K_SLT:
-        case K_SLE: {
-          const int v = decide(in.op, R(in.a), R(in.b), in.p1);
-          if (v >= 0) {
-            set_fold(v);
-            continue;
-          }
-          break;
-        }
-        case K_LOOKUP: {
-          if (in.c == 0) {  // no earlier site can share the key: the default
-            alias_to(in.p0);
-            continue;
-          }
-          Rng h = R(in.p0);
-          for (uint32_t p = 0; p < in.c && h.k; p++) h = hull(h, R(P.vaux[in.p1 + 2 * p + 1]));
-          if (h.k) r = h;
-          break;
-        }
-        default:
-          break;
-      }
-      if (r.k && W < 64) {  // intersect with the width
-        const uint64_t m = (1ull << W) - 1ull;
-        if (r.hi > m) r = full(W);
-      }
-      rng[d] = r;
-    }
   }
 
   // A dictionary of n entries of a coordinate at most 32 bits wide whose n*width bits fit in 64 is
@@ -606,7 +225,6 @@ struct Gen {
   }
 
   std::string v(uint32_t id, uint32_t j) const {
-    id = res(id);
     if (j >= Lw(P.vwidth[id])) return "0u";
     return "v" + std::to_string(id) + "_" + std::to_string(j);
   }
@@ -893,17 +511,10 @@ struct Gen {
     if (n % 16) o << ";\n";
   }
 
+  // P is specialised (program.cpp specialize_program): decided compares are literals,
+  // aliases are renamed away and dead instructions are gone
   void body(bool search) {
-    analyze(search);
-    for (size_t k = 0; k < P.vcode.size(); k++) {
-      const Instr& in = P.vcode[k];
-      if (skip[k]) continue;  // an alias of an earlier value, or an assert decided true
-      if (in.dst != MG_NONE && in.dst < fold.size() && fold[in.dst] >= 0 && in.op != K_COORD && in.op != K_CONST) {
-        o << "  " << v(in.dst, 0) << " = " << (int)fold[in.dst] << "u;  // decided by value ranges\n";
-        continue;
-      }
-      emit(in, search, !search);
-    }
+    for (const Instr& in : P.vcode) emit(in, search, !search);
   }
 };
 
@@ -913,25 +524,31 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
                        bool want_search, bool want_eval) {
   Gen g(P, specs, gconsts);
   auto& o = g.o;
+  // hipRTC compiles this with -nogpuinc -nogpulib: its own runtime header still supplies
+  // __ballot/atomicMin/..., but no device library is linked (the kernels read work-item
+  // ids through the clang builtins, so nothing references one) and clang's HIP wrapper
+  // headers are skipped, which together take ~1/3 off hipRTC's fixed cost.
   o << "typedef unsigned int uint32_t;\ntypedef int int32_t;\ntypedef unsigned long long uint64_t;\n"
-    << "typedef unsigned char uint8_t;\n";
+       "typedef unsigned char uint8_t;\n";
   o << kPrelude << "\nusing namespace mg;\n";
-  // optional occupancy target (min waves per SIMD) for the search kernel
-  std::string lb = "256";
+  // 256-lane blocks; optional occupancy target (min waves per SIMD) for the search kernel
+  std::string lb = "__attribute__((amdgpu_flat_work_group_size(1, 256)))";
   if (const char* wv = getenv("MYTHGPU_JIT_WAVES"))
-    if (atoi(wv) > 0) lb += std::string(", ") + std::to_string(atoi(wv));
+    if (atoi(wv) > 0) lb += " __attribute__((amdgpu_waves_per_eu(" + std::to_string(atoi(wv)) + ")))";
   if (want_search) {
   // search kernel
-  o << "extern \"C\" __global__ void __launch_bounds__(" << lb << ") mgj_search(const uint32_t* __restrict__ gconsts, "
-       "uint64_t start, uint64_t count, uint64_t sk, uint64_t sg, unsigned long long* hit, uint32_t flags) {\n"
+  o << "extern \"C\" __global__ void " << lb << " mgj_search(const uint32_t* __restrict__ gconsts, "
+       "uint64_t start, uint64_t count, uint64_t sk, uint64_t sg, unsigned long long* hit, uint32_t flags, uint32_t nblk) {\n"
+       "  // work-item ids from the builtins (no device library: hipRTC links none, -nogpulib)\n"
+       "  const uint32_t tid = __builtin_amdgcn_workitem_id_x(), bid = __builtin_amdgcn_workgroup_id_x();\n"
        "  const bool early = (flags & 1u) != 0u;\n"
-       "  const uint32_t lane = threadIdx.x & 63u;\n"
+       "  const uint32_t lane = tid & 63u;\n"
        "  // one aligned group of 64 candidate indices per wave (GEN2 group key, mythgpu.h)\n"
        "  const uint64_t a0 = start & ~63ull, end = start + count;\n"
        "  const uint64_t ngroups = (end - a0 + 63ull) >> 6;\n"
-       "  const uint64_t gstride = (uint64_t)gridDim.x * (blockDim.x >> 6);\n"
+       "  const uint64_t gstride = (uint64_t)nblk * 4u;  // 4 waves per 256-lane block\n"
        "  uint64_t wave_best = ~0ull, wave_hits = 0;  // per-wave, wave-uniform\n"
-       "  for (uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); g < ngroups; g += gstride) {\n"
+       "  for (uint64_t g = (uint64_t)bid * 4u + (tid >> 6); g < ngroups; g += gstride) {\n"
        "  const uint64_t gb = a0 + (g << 6);\n"
        "  const uint64_t gbase = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32)) << 32) | "
        "__builtin_amdgcn_readfirstlane((uint32_t)gb);\n"
@@ -969,10 +586,10 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   }
   if (want_eval) {
   // eval kernel (explicit SoA coordinates, verdicts, optional watch rows)
-  o << "extern \"C\" __global__ void __launch_bounds__(256) mgj_eval(const uint32_t* __restrict__ soa, uint64_t n, "
-       "uint8_t* __restrict__ verdict_out, uint32_t* __restrict__ watch) {\n"
-       "  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;\n"
-       "  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {\n"
+  o << "extern \"C\" __global__ void " << lb << " mgj_eval(const uint32_t* __restrict__ soa, uint64_t n, "
+       "uint8_t* __restrict__ verdict_out, uint32_t* __restrict__ watch, uint32_t nblk) {\n"
+       "  const uint64_t stride = (uint64_t)nblk * 256u;\n"
+       "  for (uint64_t i = (uint64_t)__builtin_amdgcn_workgroup_id_x() * 256u + __builtin_amdgcn_workitem_id_x(); i < n; i += stride) {\n"
        "  uint32_t verdict = 1u;\n";
   g.decls();
   g.body(false);
@@ -1037,9 +654,23 @@ int jit_compile(const std::string& src, std::vector<char>& code, std::string& lo
     log = "hiprtcCreateProgram failed";
     return MG_E_HIP;
   }
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-variable",
-                        "-Wno-uninitialized", "-Wno-sometimes-uninitialized"};
-  int rc = r.compile(prog, (int)(sizeof(opts) / sizeof(opts[0])), opts);
+  // MYTHGPU_JIT_OPT: optimisation level (default -O3)
+  static std::string optlvl = std::string("-O") + (getenv("MYTHGPU_JIT_OPT") ? getenv("MYTHGPU_JIT_OPT") : "3");
+  std::vector<const char*> opts = {"--offload-arch=gfx950", optlvl.c_str(), "-std=c++17", "-nogpuinc", "-nogpulib",
+                                   "-Wno-unused-variable", "-Wno-uninitialized", "-Wno-sometimes-uninitialized"};
+  // MYTHGPU_JIT_EXTRA: extra space-separated hipRTC options (tuning experiments)
+  static std::vector<std::string> extra;
+  static bool extra_init = false;
+  if (!extra_init) {
+    extra_init = true;
+    if (const char* e = getenv("MYTHGPU_JIT_EXTRA")) {
+      std::istringstream is(e);
+      std::string t;
+      while (is >> t) extra.push_back(t);
+    }
+  }
+  for (const auto& t : extra) opts.push_back(t.c_str());
+  int rc = r.compile(prog, (int)opts.size(), opts.data());
   size_t ls = 0;
   r.log_size(prog, &ls);
   if (ls > 1) {

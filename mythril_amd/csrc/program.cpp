@@ -76,17 +76,30 @@ struct Fail {
 
 class Alloc {
  public:
+  // best fit (smallest free run that holds n words; lowest address on ties): wide values
+  // (512-bit keccak arguments next to 8-bit bytes) fragment a first-fit file badly
   uint32_t alloc(uint32_t n) {
-    for (auto it = free_.begin(); it != free_.end(); ++it) {
-      if (it->second >= n) {
-        uint32_t s = it->first;
-        if (it->second == n) {
-          free_.erase(it);
-        } else {
-          uint32_t ns = it->first + n, nl = it->second - n;
-          free_.erase(it);
-          free_.emplace(ns, nl);
-        }
+    auto best = free_.end();
+    for (auto it = free_.begin(); it != free_.end(); ++it)
+      if (it->second >= n && (best == free_.end() || it->second < best->second)) best = it;
+    if (best != free_.end()) {
+      const uint32_t s = best->first;
+      if (best->second == n) {
+        free_.erase(best);
+      } else {
+        const uint32_t ns = best->first + n, nl = best->second - n;
+        free_.erase(best);
+        free_.emplace(ns, nl);
+      }
+      return s;
+    }
+    // extend the file; a free run touching the top is grown instead of skipped
+    if (!free_.empty()) {
+      auto last = std::prev(free_.end());
+      if (last->first + last->second == top_) {
+        const uint32_t s = last->first;
+        free_.erase(last);
+        top_ = s + n;
         return s;
       }
     }
@@ -116,6 +129,110 @@ class Alloc {
   std::map<uint32_t, uint32_t> free_;
   uint32_t top_ = 0;
 };
+
+// liveness + first-fit slot allocation of an SSA instruction list: fills out.code/aux
+// (slot operands, what the interpreter runs), out.vcode/vaux (value ids, what the JIT
+// emits), out.value_words and out.limb_ops
+void allocate(const std::vector<VInstr>& code, const std::vector<uint32_t>& vwidth, Lowered& out) {
+  const uint32_t NONE = MG_NONE;
+  const size_t nv = vwidth.size();
+  out.vcode.clear();
+  out.vaux.clear();
+  std::vector<int64_t> last(nv, -1), def(nv, -1);
+  for (size_t k = 0; k < code.size(); k++) {
+    const VInstr& c = code[k];
+    auto use = [&](uint32_t v) {
+      if (v != NONE && v < nv) last[v] = (int64_t)k;
+    };
+    if (c.op == K_LOOKUP) {
+      use(c.a);
+      use(c.p0);
+      for (uint32_t v : c.prior) use(v);
+    } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT ||
+               c.op == K_KECCAK || c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
+      use(c.a);
+      use(c.b);
+    } else if (c.op != K_CONST && c.op != K_COORD) {
+      use(c.a);
+      use(c.b);
+      use(c.c);
+    }
+    if (c.dst != NONE && def[c.dst] < 0) def[c.dst] = (int64_t)k;
+  }
+  std::vector<uint32_t> slot(nv, NONE);
+  std::vector<std::vector<uint32_t>> dies(code.size());
+  for (size_t v = 0; v < nv; v++) {
+    if (def[v] < 0) continue;
+    int64_t d = std::max(last[v], def[v]);
+    dies[(size_t)d].push_back((uint32_t)v);
+  }
+  Alloc al;
+  uint32_t dbg_high = 0;
+  out.code.clear();
+  out.aux.clear();
+  for (size_t k = 0; k < code.size(); k++) {
+    VInstr c = code[k];
+    if (c.dst != NONE && slot[c.dst] == NONE) slot[c.dst] = al.alloc(L_of(vwidth[c.dst]));
+    auto S = [&](uint32_t v) -> uint32_t {
+      if (v == NONE) return NONE;
+      if (slot[v] == NONE) fail(MG_E_INVALID, "internal: use before definition");
+      return slot[v];
+    };
+    Instr in{c.op, c.wd, c.dst == NONE ? NONE : slot[c.dst], 0, 0, 0, c.p0, c.p1};
+    if (c.op == K_LOOKUP) {
+      in.a = S(c.a);
+      in.b = c.b;
+      in.c = c.c;
+      in.p0 = S(c.p0);
+      in.p1 = (uint32_t)out.aux.size();
+      for (uint32_t v : c.prior) out.aux.push_back(S(v));
+    } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT || c.op == K_KECCAK ||
+               c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
+      in.a = S(c.a);
+      in.b = S(c.b);
+      in.c = NONE;
+    } else if (c.op == K_CONST || c.op == K_COORD) {
+      in.a = in.b = in.c = NONE;
+    } else {
+      in.a = S(c.a);
+      in.b = S(c.b);
+      in.c = S(c.c);
+    }
+    out.code.push_back(in);
+    {
+      Instr vi{c.op, c.wd, c.dst, c.a, c.b, c.c, c.p0, c.p1};
+      if (c.op == K_LOOKUP) {
+        vi.p1 = (uint32_t)out.vaux.size();
+        for (uint32_t v : c.prior) out.vaux.push_back(v);
+      }
+      out.vcode.push_back(vi);
+    }
+    // cost
+    uint32_t wa = c.p1;
+    if (c.op == K_LOOKUP) {
+      out.limb_ops += 3ull * L_of(c.b) * c.c + L_of(c.wd);
+    } else if (c.op == K_KECCAK) {
+      out.limb_ops += 7500ull * (c.p0 / 136 + 1);
+    } else {
+      out.limb_ops += op_cost(c.op, c.wd, wa ? wa : c.wd);
+    }
+    for (uint32_t v : dies[k]) al.release(slot[v], L_of(vwidth[v]));
+    if (getenv("MYTHGPU_DEBUG_ALLOC") && al.high() > dbg_high) {
+      dbg_high = al.high();
+      size_t live = 0;
+      std::string s;
+      for (size_t v = 0; v < nv; v++)
+        if (def[v] >= 0 && def[v] <= (int64_t)k && std::max(last[v], def[v]) > (int64_t)k) {
+          live += L_of(vwidth[v]);
+          s += " " + std::to_string(v) + ":" + std::to_string(vwidth[v]) + "@" + std::to_string(code[def[v]].op) +
+               "-" + std::to_string(last[v]);
+        }
+      fprintf(stderr, "instr %zu high %u live %zu:%s\n", k, al.high(), live, s.c_str());
+    }
+  }
+  out.value_words = std::max<uint32_t>(al.high(), 1);
+  out.vwidth = vwidth;
+}
 
 }  // namespace
 
@@ -536,102 +653,7 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
     out.watch_words = wrow;
     out.max_width = max_w;
 
-    // ---- liveness + allocation ----------------------------------------
-    const size_t nv = vwidth.size();
-    std::vector<int64_t> last(nv, -1), def(nv, -1);
-    for (size_t k = 0; k < code.size(); k++) {
-      const VInstr& c = code[k];
-      auto use = [&](uint32_t v) {
-        if (v != NONE && v < nv) last[v] = (int64_t)k;
-      };
-      if (c.op == K_LOOKUP) {
-        use(c.a);
-        use(c.p0);
-        for (uint32_t v : c.prior) use(v);
-      } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT ||
-                 c.op == K_KECCAK || c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
-        use(c.a);
-        use(c.b);
-      } else if (c.op != K_CONST && c.op != K_COORD) {
-        use(c.a);
-        use(c.b);
-        use(c.c);
-      }
-      if (c.dst != NONE && def[c.dst] < 0) def[c.dst] = (int64_t)k;
-    }
-    std::vector<uint32_t> slot(nv, NONE);
-    std::vector<std::vector<uint32_t>> dies(code.size());
-    for (size_t v = 0; v < nv; v++) {
-      if (def[v] < 0) continue;
-      int64_t d = std::max(last[v], def[v]);
-      dies[(size_t)d].push_back((uint32_t)v);
-    }
-    Alloc al;
-    uint32_t dbg_high = 0;
-    out.code.clear();
-    out.aux.clear();
-    for (size_t k = 0; k < code.size(); k++) {
-      VInstr c = code[k];
-      if (c.dst != NONE && slot[c.dst] == NONE) slot[c.dst] = al.alloc(L_of(vwidth[c.dst]));
-      auto S = [&](uint32_t v) -> uint32_t {
-        if (v == NONE) return NONE;
-        if (slot[v] == NONE) fail(MG_E_INVALID, "internal: use before definition");
-        return slot[v];
-      };
-      Instr in{c.op, c.wd, c.dst == NONE ? NONE : slot[c.dst], 0, 0, 0, c.p0, c.p1};
-      if (c.op == K_LOOKUP) {
-        in.a = S(c.a);
-        in.b = c.b;
-        in.c = c.c;
-        in.p0 = S(c.p0);
-        in.p1 = (uint32_t)out.aux.size();
-        for (uint32_t v : c.prior) out.aux.push_back(S(v));
-      } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT || c.op == K_KECCAK ||
-                 c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
-        in.a = S(c.a);
-        in.b = S(c.b);
-        in.c = NONE;
-      } else if (c.op == K_CONST || c.op == K_COORD) {
-        in.a = in.b = in.c = NONE;
-      } else {
-        in.a = S(c.a);
-        in.b = S(c.b);
-        in.c = S(c.c);
-      }
-      out.code.push_back(in);
-      {
-        Instr vi{c.op, c.wd, c.dst, c.a, c.b, c.c, c.p0, c.p1};
-        if (c.op == K_LOOKUP) {
-          vi.p1 = (uint32_t)out.vaux.size();
-          for (uint32_t v : c.prior) out.vaux.push_back(v);
-        }
-        out.vcode.push_back(vi);
-      }
-      // cost
-      uint32_t wa = c.p1;
-      if (c.op == K_LOOKUP) {
-        out.limb_ops += 3ull * L_of(c.b) * c.c + L_of(c.wd);
-      } else if (c.op == K_KECCAK) {
-        out.limb_ops += 7500ull * (c.p0 / 136 + 1);
-      } else {
-        out.limb_ops += op_cost(c.op, c.wd, wa ? wa : c.wd);
-      }
-      for (uint32_t v : dies[k]) al.release(slot[v], L_of(vwidth[v]));
-      if (getenv("MYTHGPU_DEBUG_ALLOC") && al.high() > dbg_high) {
-        dbg_high = al.high();
-        size_t live = 0;
-        std::string s;
-        for (size_t v = 0; v < nv; v++)
-          if (def[v] >= 0 && def[v] <= (int64_t)k && std::max(last[v], def[v]) > (int64_t)k) {
-            live += L_of(vwidth[v]);
-            s += " " + std::to_string(v) + ":" + std::to_string(vwidth[v]) + "@" + std::to_string(code[def[v]].op) +
-                 "-" + std::to_string(last[v]);
-          }
-        fprintf(stderr, "instr %zu high %u live %zu:%s\n", k, al.high(), live, s.c_str());
-      }
-    }
-    out.value_words = std::max<uint32_t>(al.high(), 1);
-    out.vwidth = vwidth;
+    allocate(code, vwidth, out);
     return MG_OK;
   } catch (const Fail& f) {
     err = f.msg;
@@ -641,6 +663,428 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
     return MG_E_INVALID;
   }
 }
+
+// ---------------------------------------------------------------------------
+// specialisation: value ranges, folding, aliases, dead code (specialize_program)
+// ---------------------------------------------------------------------------
+namespace {
+
+inline uint32_t Lw(uint32_t w) { return (w + 31) / 32; }
+
+struct Analysis {
+  const Lowered& P;
+  const std::vector<GenSpec>* specs;
+  const std::vector<uint32_t>* gconsts;
+  Analysis(const Lowered& p, const std::vector<GenSpec>* s, const std::vector<uint32_t>* g) : P(p), specs(s), gconsts(g) {}
+  // rng[id]: when known, the value lies in [lo, hi] (so it fits in 64 bits).  In the
+  // search kernel a coordinate's range comes from its generator spec, which bounds
+  // EVERY candidate the kernel evaluates (clamp records, dictionaries, fixed bits), so a
+  // comparison decided by the ranges is decided for every candidate: it folds to a
+  // literal, an ITE on it becomes an alias of the chosen arm, and bits() then looks
+  // through it (e.g. the calldata guard If(k < size, calldata[k], 0) with size drawn
+  // from [68, 2^32) collapses to the byte, and a CALLDATALOAD to its AUX word).
+  struct Rng {
+    bool k = false;
+    uint64_t lo = 0, hi = 0;
+  };
+  std::vector<Rng> rng;
+  // psrc/plo: the value is bits [plo, plo + width) of value psrc (a chain of EXTRACTs, and
+  // CONCATs of adjacent slices of one value, e.g. a CALLDATALOAD of an AUX word's bytes)
+  std::vector<uint32_t> psrc, plo;
+  std::vector<int8_t> fold;       // per id: -1, or the folded Bool value
+  std::vector<uint32_t> alias;    // per id: the id it equals (itself if none)
+  std::vector<char> skip;         // per instruction: defines an alias / a decided assert
+  std::vector<Rng> crng;          // per coordinate (search mode)
+
+  uint32_t res(uint32_t id) const {
+    if (alias.empty() || id >= alias.size()) return id;
+    while (alias[id] != id) id = alias[id];
+    return id;
+  }
+  static Rng full(uint32_t w) {
+    Rng r;
+    if (w <= 64) {
+      r.k = true;
+      r.hi = w == 64 ? ~0ull : ((1ull << w) - 1ull);
+    }
+    return r;
+  }
+  static Rng exact(uint64_t v) {
+    Rng r;
+    r.k = true;
+    r.lo = r.hi = v;
+    return r;
+  }
+  static Rng hull(const Rng& a, const Rng& b) {
+    Rng r;
+    if (!a.k || !b.k) return r;
+    r.k = true;
+    r.lo = std::min(a.lo, b.lo);
+    r.hi = std::max(a.hi, b.hi);
+    return r;
+  }
+  // limbs [0, L) as one u64 if every limb >= 2 is zero
+  static bool fits64(const uint32_t* x, uint32_t L, uint64_t* v) {
+    for (uint32_t j = 2; j < L; j++)
+      if (x[j]) return false;
+    *v = (uint64_t)x[0] | (L > 1 ? (uint64_t)x[1] << 32 : 0ull);
+    return true;
+  }
+
+  // range of a generated coordinate's final value (include/mythgpu.h GEN2)
+  Rng coord_range(uint32_t c) const {
+    const GenSpec& sp = (*specs)[c];
+    const uint32_t w = P.coord_width[c], L = Lw(w), kind = sp.kind & 0xFFu;
+    const auto& G = *gconsts;
+    const unsigned __int128 wlim = w >= 128 ? ~(unsigned __int128)0 : (((unsigned __int128)1 << w) - 1);
+    Rng r;
+    switch (kind) {
+      case MG_GEN_FIXED: {
+        uint64_t v;
+        if (fits64(&G[sp.p[0]], L, &v)) r = exact(v);
+        break;
+      }
+      case MG_GEN_DICT:
+      case MG_GEN_MIXED: {
+        Rng d;  // dictionary hull
+        bool ok = sp.p[1] > 0;
+        for (uint32_t e = 0; ok && e < sp.p[1]; e++) {
+          uint64_t v;
+          if (!fits64(&G[sp.p[0] + e * L], L, &v)) ok = false;
+          else d = d.k ? hull(d, exact(v)) : exact(v);
+        }
+        if (kind == MG_GEN_DICT) {
+          if (ok) r = d;
+          break;
+        }
+        if (sp.p[6]) {  // clamp record: the final value is inside [lo, lo + span)
+          uint64_t lo;
+          const uint32_t rec = sp.p[6] - 1;
+          if (fits64(&G[rec], L, &lo)) {
+            const uint64_t span = G[rec + L] ? G[rec + L] : (1ull << 32);
+            if ((unsigned __int128)lo + span - 1 <= (unsigned __int128)~0ull) {
+              r.k = true;
+              r.lo = lo;
+              r.hi = lo + span - 1;
+            }
+          }
+          break;
+        }
+        const uint32_t pc = sp.p[3] != MG_NONE ? (sp.p[2] & 0xFFFFu) : 0u;
+        const uint32_t pd = sp.p[1] ? (sp.p[2] >> 16) : 0u;
+        const uint32_t ps = sp.p[4] & 0xFFFFu;
+        Rng u;
+        bool have = false, unknown = false;
+        auto add = [&](const Rng& x) {
+          if (!x.k) unknown = true;
+          else u = have ? hull(u, x) : x;
+          have = true;
+        };
+        Rng cd;  // COPY / DICT part, before the delta
+        bool cd_have = false, cd_unknown = false;
+        if (pc) {
+          const Rng s = crng[sp.p[3]];
+          if (!s.k) cd_unknown = true;
+          else cd = s;
+          cd_have = true;
+        }
+        if (pd) {
+          if (!ok) cd_unknown = true;
+          else cd = cd_have && cd.k ? hull(cd, d) : d;
+          cd_have = true;
+        }
+        if (cd_have) {
+          if (cd_unknown) add(Rng{});
+          else if (sp.p[5]) {  // +/-2 at most, no wrap
+            if (cd.lo >= 2 && (unsigned __int128)cd.hi + 2 <= wlim && cd.hi + 2 > cd.hi) {
+              Rng x;
+              x.k = true;
+              x.lo = cd.lo - 2;
+              x.hi = cd.hi + 2;
+              add(x);
+            } else {
+              add(full(w));
+            }
+          } else {
+            add(cd);
+          }
+        }
+        const uint32_t sb = std::min(w, sp.p[4] >> 16);
+        if (ps) add(full(sb));
+        if (pc + pd + ps < 65536u) add(full(w));
+        if (have && !unknown) r = u;
+        break;
+      }
+      case MG_GEN_RANGE: {
+        uint64_t lo;
+        if (fits64(&G[sp.p[0]], L, &lo)) {
+          const uint64_t span = sp.p[1] ? sp.p[1] : (1ull << 32);
+          if ((unsigned __int128)lo + span - 1 <= wlim && (unsigned __int128)lo + span - 1 <= (unsigned __int128)~0ull) {
+            r.k = true;
+            r.lo = lo;
+            r.hi = lo + span - 1;
+          }
+        }
+        break;
+      }
+      case MG_GEN_ALIGNED: {
+        uint64_t lo;
+        if (fits64(&G[sp.p[0]], L, &lo) && sp.p[1] < 64) {
+          const unsigned __int128 cnt = sp.p[2] ? sp.p[2] : (1ull << 32);
+          const unsigned __int128 top = (unsigned __int128)lo + ((cnt - 1) << sp.p[1]);
+          if (top <= wlim && top <= (unsigned __int128)~0ull) {
+            r.k = true;
+            r.lo = lo;
+            r.hi = (uint64_t)top;
+          }
+        }
+        break;
+      }
+      default:  // UNIFORM / LAZY
+        r = full(w);
+        break;
+    }
+    if (!r.k) r = full(w);
+    if (const uint32_t fix = sp.kind >> 8) {  // (v & ~m) | val lies in [val, val | ~m]
+      const uint32_t f = fix - 1;
+      uint64_t m, val;
+      std::vector<uint32_t> nm(L);
+      for (uint32_t j = 0; j < L; j++) nm[j] = ~G[f + j];
+      if (w & 31) nm[L - 1] &= (1u << (w & 31)) - 1u;
+      if (fits64(&G[f + L], L, &val) && fits64(nm.data(), L, &m)) {
+        r.k = true;
+        r.lo = val;
+        r.hi = val | m;
+      } else {
+        r = Rng{};
+      }
+    }
+    return r;
+  }
+
+  // decide a comparison from operand ranges: -1 undecided, else 0 / 1
+  static int decide(uint32_t op, const Rng& a, const Rng& b, uint32_t wa) {
+    if (!a.k || !b.k) return -1;
+    if (op == K_SLT || op == K_SLE) {
+      const uint64_t sign = wa >= 65 ? 0ull : (1ull << (wa - 1));
+      if (sign && (a.hi >= sign || b.hi >= sign)) return -1;  // a negative value may be inside
+      op = op == K_SLT ? K_ULT : K_ULE;
+    }
+    switch (op) {
+      case K_ULT:
+        if (a.hi < b.lo) return 1;
+        if (a.lo >= b.hi) return 0;
+        return -1;
+      case K_ULE:
+        if (a.hi <= b.lo) return 1;
+        if (a.lo > b.hi) return 0;
+        return -1;
+      case K_EQ:
+        if (a.lo == a.hi && b.lo == b.hi && a.lo == b.lo) return 1;
+        if (a.hi < b.lo || b.hi < a.lo) return 0;
+        return -1;
+      default:
+        return -1;
+    }
+  }
+
+  void analyze(bool search) {
+    const size_t nv = P.vwidth.size();
+    rng.assign(nv, Rng{});
+    psrc.assign(nv, MG_NONE);
+    plo.assign(nv, 0);
+    fold.assign(nv, -1);
+    alias.resize(nv);
+    for (size_t i = 0; i < nv; i++) alias[i] = (uint32_t)i;
+    skip.assign(P.vcode.size(), 0);
+    if (search && specs) {
+      crng.assign(P.n_coords, Rng{});
+      for (uint32_t c = 0; c < P.n_coords; c++) crng[c] = coord_range(c);
+    }
+    for (size_t k = 0; k < P.vcode.size(); k++) {
+      const Instr& in = P.vcode[k];
+      const uint32_t d = in.dst, W = in.wd;
+      auto R = [&](uint32_t id) { return rng[res(id)]; };
+      auto F = [&](uint32_t id) { return (int)fold[res(id)]; };
+      auto alias_to = [&](uint32_t src) {
+        alias[d] = res(src);
+        rng[d] = rng[res(src)];
+        fold[d] = fold[res(src)];
+        skip[k] = 1;
+      };
+      auto set_fold = [&](int v) {
+        fold[d] = (int8_t)v;
+        rng[d] = exact((uint64_t)v);
+      };
+      if (d == MG_NONE || d >= nv) {
+        if (in.op == K_ASSERT && F(in.a) == 1) skip[k] = 1;
+        continue;
+      }
+      Rng r = full(W);
+      switch (in.op) {
+        case K_CONST: {
+          uint64_t v;
+          if (fits64(&P.consts[in.p0], Lw(W), &v)) r = exact(v);
+          break;
+        }
+        case K_COORD:
+          if (search && specs) r = crng[in.p0];
+          break;
+        case K_COPY:
+          alias_to(in.a);
+          continue;
+        case K_ZEXT:
+          if (R(in.a).k) r = R(in.a);
+          break;
+        case K_EXTRACT: {
+          const Rng a = R(in.a);
+          if (a.k && in.p0 < 64 && (W >= 64 || (a.hi >> in.p0) < (1ull << W))) {
+            r.k = true;
+            r.lo = a.lo >> in.p0;
+            r.hi = a.hi >> in.p0;
+          } else if (a.k && in.p0 >= 64) {
+            r = exact(0);
+          }
+          const uint32_t ra = res(in.a);
+          const uint32_t src = psrc[ra] != MG_NONE ? psrc[ra] : ra;
+          const uint32_t lo = (psrc[ra] != MG_NONE ? plo[ra] : 0u) + in.p0;
+          if (lo == 0 && W == P.vwidth[src]) {
+            alias_to(src);
+            continue;
+          }
+          psrc[d] = src;
+          plo[d] = lo;
+          break;
+        }
+        case K_CONCAT: {
+          {  // adjacent slices of one value: the high part starts where the low part ends
+            const uint32_t ra = res(in.a), rb = res(in.b);
+            const uint32_t sa = psrc[ra] != MG_NONE ? psrc[ra] : ra, la = psrc[ra] != MG_NONE ? plo[ra] : 0u;
+            const uint32_t sb = psrc[rb] != MG_NONE ? psrc[rb] : rb, lb = psrc[rb] != MG_NONE ? plo[rb] : 0u;
+            if (sa == sb && la == lb + P.vwidth[rb]) {
+              if (lb == 0 && W == P.vwidth[sa]) {
+                alias_to(sa);
+                continue;
+              }
+              psrc[d] = sa;
+              plo[d] = lb;
+              r = full(W);
+              break;
+            }
+          }
+          const Rng a = R(in.a), b = R(in.b);
+          const uint32_t wb = in.p1;
+          if (a.k && b.k && wb < 64 && (a.hi >> (64 - wb)) == 0) {
+            r.k = true;
+            r.lo = (a.lo << wb) | b.lo;
+            r.hi = (a.hi << wb) | b.hi;
+          }
+          break;
+        }
+        case K_AND:
+        case K_OR:
+        case K_XOR: {
+          const int fa = F(in.a), fb = F(in.b);
+          if (W == 1) {
+            if (in.op == K_AND) {
+              if (fa == 0 || fb == 0) { set_fold(0); continue; }
+              if (fa == 1) { alias_to(in.b); continue; }
+              if (fb == 1) { alias_to(in.a); continue; }
+            } else if (in.op == K_OR) {
+              if (fa == 1 || fb == 1) { set_fold(1); continue; }
+              if (fa == 0) { alias_to(in.b); continue; }
+              if (fb == 0) { alias_to(in.a); continue; }
+            } else if (fa >= 0 && fb >= 0) {
+              set_fold(fa ^ fb);
+              continue;
+            }
+            break;
+          }
+          const Rng a = R(in.a), b = R(in.b);
+          if (in.op == K_AND) {
+            if (a.k || b.k) {
+              r.k = true;
+              r.lo = 0;
+              r.hi = std::min(a.k ? a.hi : ~0ull, b.k ? b.hi : ~0ull);
+            }
+          } else if (a.k && b.k) {
+            const uint64_t m = std::max(a.hi, b.hi);
+            r.k = true;
+            r.lo = 0;
+            r.hi = m ? (~0ull >> __builtin_clzll(m)) : 0ull;
+          }
+          break;
+        }
+        case K_NOT:
+          if (W == 1 && F(in.a) >= 0) {
+            set_fold(1 - F(in.a));
+            continue;
+          }
+          break;
+        case K_ITE: {
+          const int fc = F(in.a);
+          if (fc >= 0) {
+            alias_to(fc ? in.b : in.c);
+            continue;
+          }
+          const Rng h = hull(R(in.b), R(in.c));
+          if (h.k) r = h;
+          break;
+        }
+        case K_ADD: {
+          const Rng a = R(in.a), b = R(in.b);
+          if (a.k && b.k && (unsigned __int128)a.hi + b.hi <= (unsigned __int128)full(std::min(W, 64u)).hi) {
+            r.k = true;
+            r.lo = a.lo + b.lo;
+            r.hi = a.hi + b.hi;
+          }
+          break;
+        }
+        case K_SUB: {
+          const Rng a = R(in.a), b = R(in.b);
+          if (a.k && b.k && a.lo >= b.hi) {
+            r.k = true;
+            r.lo = a.lo - b.hi;
+            r.hi = a.hi - b.lo;
+          }
+          break;
+        }
+        case K_EQ:
+        case K_ULT:
+        case K_ULE:
+        case K_SLT:
+        case K_SLE: {
+          const int v = decide(in.op, R(in.a), R(in.b), in.p1);
+          if (v >= 0) {
+            set_fold(v);
+            continue;
+          }
+          break;
+        }
+        case K_LOOKUP: {
+          if (in.c == 0) {  // no earlier site can share the key: the default
+            alias_to(in.p0);
+            continue;
+          }
+          Rng h = R(in.p0);
+          for (uint32_t p = 0; p < in.c && h.k; p++) h = hull(h, R(P.vaux[in.p1 + 2 * p + 1]));
+          if (h.k) r = h;
+          break;
+        }
+        default:
+          break;
+      }
+      if (r.k && W < 64) {  // intersect with the width
+        const uint64_t m = (1ull << W) - 1ull;
+        if (r.hi > m) r = full(W);
+      }
+      rng[d] = r;
+    }
+  }
+
+};
+
+}  // namespace
 
 int parse_gen(const Lowered& prog, const uint32_t* blob, size_t n_words, std::vector<GenSpec>& specs,
               std::vector<uint32_t>& consts, std::string& err) {
@@ -723,6 +1167,107 @@ int parse_gen(const Lowered& prog, const uint32_t* blob, size_t n_words, std::ve
     }
   }
   return MG_OK;
+}
+
+}  // namespace mg
+
+namespace mg {
+
+// The program a search actually runs once its generator is known.  Every candidate a
+// search kernel evaluates is drawn by that generator, so ranges derived from the
+// generator specs (clamp records, dictionaries, fixed bits) hold for every lane:
+//  * a comparison the ranges decide becomes a literal; an ITE on a literal, a Bool
+//    AND/OR with a literal, a LOOKUP with no prior site and a COPY become aliases
+//    (their uses are renamed to the value they equal);
+//  * an assert decided true disappears; dead instructions are removed;
+//  * liveness and slot allocation run again on what is left.
+// With specs == nullptr (explicit-coordinate eval) only literal-derived facts are used.
+// Verdicts are unchanged for every generated candidate (tests compare the specialised
+// interpreter and JIT kernels with the C restatement, which runs the full program).
+int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
+                       Lowered& out, std::string& err) {
+  try {
+    const uint32_t NONE = MG_NONE;
+    Analysis A(in, specs, gconsts);
+    A.analyze(specs != nullptr);
+    const size_t nv = in.vwidth.size();
+    out = in;
+    out.code.clear();
+    out.aux.clear();
+    std::vector<uint32_t> vwidth = in.vwidth;
+    // rewritten SSA list (value ids are kept; aliases renamed to their representative)
+    std::vector<VInstr> code;
+    code.reserve(in.vcode.size());
+    for (size_t k = 0; k < in.vcode.size(); k++) {
+      const Instr& c = in.vcode[k];
+      if (A.skip[k]) continue;
+      auto R = [&](uint32_t v) { return v == NONE || v >= nv ? v : A.res(v); };
+      if (c.dst != NONE && c.dst < nv && A.fold[c.dst] >= 0 && c.op != K_CONST && c.op != K_COORD) {
+        const uint32_t off = (uint32_t)out.consts.size();
+        out.consts.push_back((uint32_t)A.fold[c.dst]);
+        code.push_back(VInstr{K_CONST, 1, c.dst, NONE, NONE, NONE, off, 0, {}});
+        continue;
+      }
+      if ((c.op == K_EXTRACT || c.op == K_CONCAT) && c.dst < nv && A.psrc[c.dst] != NONE) {
+        const uint32_t src = A.psrc[c.dst];
+        code.push_back(VInstr{K_EXTRACT, c.wd, c.dst, src, NONE, NONE, A.plo[c.dst], in.vwidth[src], {}});
+        continue;
+      }
+      VInstr v{c.op, c.wd, c.dst, R(c.a), R(c.b), R(c.c), c.p0, c.p1, {}};
+      if (c.op == K_LOOKUP) {
+        v.a = R(c.a);
+        v.b = c.b;  // key width
+        v.c = c.c;  // number of priors
+        v.p0 = R(c.p0);
+        for (uint32_t p = 0; p < c.c; p++) {
+          v.prior.push_back(R(in.vaux[c.p1 + 2 * p]));
+          v.prior.push_back(R(in.vaux[c.p1 + 2 * p + 1]));
+        }
+      } else if (c.op == K_CONST || c.op == K_COORD) {
+        v.a = v.b = v.c = NONE;
+      }
+      code.push_back(std::move(v));
+    }
+    // dead code: keep asserts, watches and whatever they transitively use
+    std::vector<char> live(nv, 0), keep(code.size(), 0);
+    for (size_t k = code.size(); k-- > 0;) {
+      const VInstr& c = code[k];
+      const bool side = c.op == K_ASSERT || c.op == K_WATCH;
+      if (!side && (c.dst == NONE || c.dst >= nv || !live[c.dst])) continue;
+      keep[k] = 1;
+      auto use = [&](uint32_t x) {
+        if (x != NONE && x < nv) live[x] = 1;
+      };
+      if (c.op == K_LOOKUP) {
+        use(c.a);
+        use(c.p0);
+        for (uint32_t x : c.prior) use(x);
+      } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT || c.op == K_KECCAK ||
+                 c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
+        use(c.a);
+        use(c.b);
+      } else if (c.op != K_CONST && c.op != K_COORD) {
+        use(c.a);
+        use(c.b);
+        use(c.c);
+      }
+    }
+    std::vector<VInstr> kept;
+    kept.reserve(code.size());
+    for (size_t k = 0; k < code.size(); k++)
+      if (keep[k]) kept.push_back(std::move(code[k]));
+    const uint64_t ops = in.limb_ops;  // algorithmic work is the query's, not what survives
+    out.limb_ops = 0;
+    allocate(kept, vwidth, out);
+    out.limb_ops = ops;
+    return MG_OK;
+  } catch (const Fail& f) {
+    err = f.msg;
+    return f.code;
+  } catch (const std::exception& e) {
+    err = e.what();
+    return MG_E_INVALID;
+  }
 }
 
 }  // namespace mg

@@ -41,6 +41,10 @@ struct Instr {
 };
 static_assert(sizeof(Instr) == 32, "Instr must be 8 words");
 
+struct GenSpec {
+  uint32_t kind, p[7];
+};
+
 struct Lowered {
   std::vector<Instr> code;
   std::vector<uint32_t> consts;
@@ -68,9 +72,12 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
 // Fixed algorithmic cost table (32-bit limb ops), SURVEY.md §8(d).
 uint64_t op_cost(uint32_t node_op, uint32_t width, uint32_t operand_width);
 
-struct GenSpec {
-  uint32_t kind, p[7];
-};
+
+// Specialise a lowered program for a generator (specs/gconsts) or, with specs == nullptr,
+// for explicit coordinates: range-decided compares folded, aliases renamed, dead code
+// removed, slots re-allocated.  Same verdicts for every candidate the generator draws.
+int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
+                       Lowered& out, std::string& err);
 
 // Validate a generator blob against a lowered program; fills specs/consts.
 int parse_gen(const Lowered& prog, const uint32_t* blob, size_t n_words, std::vector<GenSpec>& specs,

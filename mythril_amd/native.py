@@ -28,8 +28,9 @@ MG_SEARCH_EARLY_EXIT = 1
 NO_HIT = (1 << 64) - 1
 
 EXPORTS = [
-    "mg_init", "mg_shutdown", "mg_last_error", "mg_version", "mg_program_check", "mg_program_load",
-    "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_free", "mg_eval", "mg_eval_dev",
+    "mg_init", "mg_shutdown", "mg_last_error", "mg_version", "mg_program_check", "mg_program_check_gen",
+    "mg_program_load",
+    "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_info", "mg_gen_free", "mg_eval", "mg_eval_dev",
     "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
     "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_jit_compile", "mg_jit_info",
     "mg_jit_free", "mg_jit_search", "mg_jit_eval", "mg_jit_eval_dev",
@@ -85,10 +86,12 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_last_error": (C.c_char_p, []),
             "mg_version": (C.c_int, []),
             "mg_program_check": (C.c_int, [u8p, C.c_size_t, C.POINTER(ProgramInfo)]),
+            "mg_program_check_gen": (C.c_int, [u8p, C.c_size_t, u32p, C.c_size_t, C.POINTER(ProgramInfo)]),
             "mg_program_load": (C.c_int, [u8p, C.c_size_t, u64p]),
             "mg_program_info": (C.c_int, [C.c_uint64, C.POINTER(ProgramInfo)]),
             "mg_program_free": (C.c_int, [C.c_uint64]),
             "mg_gen_load": (C.c_int, [C.c_uint64, u32p, C.c_size_t, u64p]),
+            "mg_gen_info": (C.c_int, [C.c_uint64, C.POINTER(ProgramInfo)]),
             "mg_gen_free": (C.c_int, [C.c_uint64]),
             "mg_eval": (C.c_int, [C.c_uint64, u32p, C.c_uint64, u8p, u32p]),
             "mg_eval_dev": (C.c_int, [C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
@@ -141,6 +144,15 @@ def check_program(blob: bytes) -> ProgramInfo:
     lib = load_library()
     info = ProgramInfo()
     _check(lib.mg_program_check(_u8(blob), len(blob), C.byref(info)))
+    return info
+
+
+def check_program_gen(blob: bytes, gen_blob: np.ndarray) -> ProgramInfo:
+    """Host-only: the program specialised for a generator (what a search runs)."""
+    lib = load_library()
+    g = np.ascontiguousarray(gen_blob, dtype=np.uint32)
+    info = ProgramInfo()
+    _check(lib.mg_program_check_gen(_u8(blob), len(blob), _ptr(g, C.c_uint32), g.size, C.byref(info)))
     return info
 
 
@@ -198,6 +210,12 @@ class Engine:
         h = C.c_uint64()
         _check(self.lib.mg_gen_load(prog, _ptr(blob, C.c_uint32), blob.size, C.byref(h)))
         return h.value
+
+    def gen_info(self, gen: int) -> ProgramInfo:
+        """The generator-specialised program the searches run."""
+        info = ProgramInfo()
+        _check(self.lib.mg_gen_info(gen, C.byref(info)))
+        return info
 
     def free_gen(self, gen: int):
         _check(self.lib.mg_gen_free(gen))

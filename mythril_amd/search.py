@@ -39,6 +39,7 @@ ACTORS = [
 ]
 
 P16 = 65536
+MAX_COPY_DEPTH = 16  # <= MG_GEN_MAX_COPY_DEPTH (include/mythgpu.h)
 
 # prefix-incremental flattening shared by every search (LASER's sibling queries share prefixes)
 FLATTEN_CACHE = ssa.FlattenCache(aux_words=True)
@@ -162,6 +163,7 @@ def default_generator(P: ssa.Program, extra_dict: Sequence[int] = (), roots: Opt
         by_width.setdefault(w, set()).add(v)
     bounds = _interval_bounds(P)
     last_of_width: Dict[int, int] = {}
+    depth: Dict[int, int] = {}  # COPY chain length per coordinate (MG_GEN_MAX_COPY_DEPTH bounds it)
     for c in P.coords:
         w = c.width
         mask = (1 << w) - 1
@@ -204,6 +206,9 @@ def default_generator(P: ssa.Program, extra_dict: Sequence[int] = (), roots: Opt
             vals = {v for v in vals if dom.admissible(v)} or vals
         vals = sorted(vals)[:4096]
         copy = last_of_width.get(w) if w >= 32 else None
+        if copy is not None and depth.get(copy, 0) >= MAX_COPY_DEPTH:
+            copy = None  # start a new chain (the interpreter walks chains per candidate)
+        depth[c.index] = depth.get(copy, 0) + 1 if copy is not None else 0
         g.mixed(c.index, vals, p_dict=0.45, copy_from=copy, p_copy=0.10 if copy is not None else 0.0,
                 p_delta=0.25 if w > 8 else 0.0, small_bits=small_bits, p_small=p_small, clamp=clamp)
         if dom is not None and dom.fmask:

@@ -7,7 +7,7 @@ import sys
 from collections import defaultdict
 
 d, workload = sys.argv[1], sys.argv[2]
-KERNEL = "mgj_search"
+KERNEL = sys.argv[3] if len(sys.argv) > 3 else "mgj_search"
 counters = defaultdict(list)
 for f in glob.glob(f"{d}/pmc*/**/*counter_collection.csv", recursive=True):
     per_dispatch = defaultdict(lambda: defaultdict(float))
