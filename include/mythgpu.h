@@ -242,9 +242,11 @@ int mg_eval_dev(uint64_t prog, const uint32_t* d_soa_coords, uint64_t n, uint8_t
 int mg_eval_generated(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64_t n,
                       uint8_t* verdict_out, uint32_t* watch_out);
 
-/* first_hit: lowest satisfying candidate index in [start, start+count), UINT64_MAX if none */
+/* first_hit: lowest satisfying candidate index in [start, start+count), UINT64_MAX if none.
+ * assign_out (nullable): on a hit, the winning candidate's watch rows (program watch list,
+ * watch_words uint32: the model read-back of Solver.model(), laser/smt/solver/solver.py:59-64) */
 int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags,
-              uint64_t* first_hit, uint64_t* n_hits);
+              uint64_t* first_hit, uint64_t* n_hits, uint32_t* assign_out);
 
 /* ---- JIT specialisation (hipRTC) ------------------------------------
  * mg_jit_compile turns a loaded program into straight-line gfx950 code: with a
@@ -258,7 +260,7 @@ int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle);
 int mg_jit_info(uint64_t jit, double* compile_ms, int* blocks_per_cu);
 int mg_jit_free(uint64_t jit);
 int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags, uint64_t* first_hit,
-                  uint64_t* n_hits);
+                  uint64_t* n_hits, uint32_t* assign_out);
 int mg_jit_eval(uint64_t jit, const uint32_t* soa_coords, uint64_t n, uint8_t* verdict_out, uint32_t* watch_out);
 int mg_jit_eval_dev(uint64_t jit, const uint32_t* d_soa_coords, uint64_t n, uint8_t* d_verdict_out,
                     uint32_t* d_watch_out);

@@ -22,6 +22,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <map>
 #include <unordered_map>
 #include <vector>
 
@@ -633,6 +634,9 @@ thread_local std::string g_err;
 struct DevProgram {
   Lowered low;
   bool heavy = true;  // has MUL/DIV/REM/shift/EXP/UMUL_NOOVF/KECCAK: the full interpreter
+  bool uploaded = false;
+  void* buf = nullptr;  // pooled device buffer holding the four arrays below
+  size_t cap = 0;
   Instr* d_code = nullptr;
   uint32_t* d_consts = nullptr;
   uint32_t* d_aux = nullptr;
@@ -647,6 +651,9 @@ struct DevGen {
   GenSpec* d_specs = nullptr;
   uint32_t* d_consts = nullptr;
   DevProgram spec;                // the program specialised for this generator (what searches run)
+  DevProgram spec_watch;          // the same with the watch list (model read-back, mg_eval_generated)
+  void* gbuf = nullptr;           // pooled buffer behind d_specs / d_consts
+  size_t gcap = 0;
 };
 
 struct DevJit {
@@ -672,6 +679,12 @@ struct Engine {
   unsigned long long* d_hit = nullptr;  // [0] first hit, [1] hit count
   uint32_t* d_scratch = nullptr;
   size_t scratch_bytes = 0;
+  // device buffers of freed programs/generators, by capacity: a query's uploads reuse them
+  // instead of paying hipMalloc (tens to hundreds of microseconds each) per query
+  std::multimap<size_t, void*> pool;
+  uint32_t* d_watch1 = nullptr;  // one candidate's watch rows (model read-back)
+  size_t watch1_words = 0;
+  uint8_t* d_ver1 = nullptr;
   mg_stats_t stats{};
 };
 
@@ -703,8 +716,26 @@ static int upload(T** d, const T* h, size_t n) {
   return MG_OK;
 }
 
-static int upload_code(DevProgram& p) {
-  int rc;
+static int pool_get(Engine& e, size_t bytes, void** ptr, size_t* cap) {
+  size_t c = 4096;
+  while (c < bytes) c <<= 1;
+  auto it = e.pool.find(c);
+  if (it != e.pool.end()) {
+    *ptr = it->second;
+    e.pool.erase(it);
+  } else {
+    HIPCHK(hipMalloc(ptr, c));
+  }
+  *cap = c;
+  return MG_OK;
+}
+
+static void pool_put(Engine& e, void* ptr, size_t cap) {
+  if (ptr) e.pool.emplace(cap, ptr);
+}
+
+// instructions, literals, lookup lists and coordinate widths in ONE pooled buffer, one copy
+static int upload_code(Engine& e, DevProgram& p) {
   p.lds = p.low.value_words <= kLdsWordsMax;
   p.heavy = false;
   for (const Instr& in : p.low.code) {
@@ -715,20 +746,34 @@ static int upload_code(DevProgram& p) {
       default: break;
     }
   }
-  if ((rc = upload(&p.d_code, p.low.code.data(), p.low.code.size()))) return rc;
-  if ((rc = upload(&p.d_consts, p.low.consts.data(), p.low.consts.size()))) return rc;
-  if ((rc = upload(&p.d_aux, p.low.aux.data(), p.low.aux.size()))) return rc;
-  if ((rc = upload(&p.d_coord_width, p.low.coord_width.data(), p.low.coord_width.size()))) return rc;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t b_code = al(p.low.code.size() * sizeof(Instr)), b_consts = al(p.low.consts.size() * 4),
+               b_aux = al(p.low.aux.size() * 4), b_cw = al(p.low.coord_width.size() * 4);
+  const size_t total = std::max<size_t>(b_code + b_consts + b_aux + b_cw, 256);
+  int rc = pool_get(e, total, &p.buf, &p.cap);
+  if (rc) return rc;
+  std::vector<uint8_t> h(total, 0);
+  std::memcpy(h.data(), p.low.code.data(), p.low.code.size() * sizeof(Instr));
+  std::memcpy(h.data() + b_code, p.low.consts.data(), p.low.consts.size() * 4);
+  std::memcpy(h.data() + b_code + b_consts, p.low.aux.data(), p.low.aux.size() * 4);
+  std::memcpy(h.data() + b_code + b_consts + b_aux, p.low.coord_width.data(), p.low.coord_width.size() * 4);
+  HIPCHK(hipMemcpy(p.buf, h.data(), total, hipMemcpyHostToDevice));
+  uint8_t* b = (uint8_t*)p.buf;
+  p.d_code = (Instr*)b;
+  p.d_consts = (uint32_t*)(b + b_code);
+  p.d_aux = (uint32_t*)(b + b_code + b_consts);
+  p.d_coord_width = (uint32_t*)(b + b_code + b_consts + b_aux);
+  p.uploaded = true;
   return MG_OK;
 }
 
-static void free_code(DevProgram& p) {
-  (void)hipFree(p.d_code);
-  (void)hipFree(p.d_consts);
-  (void)hipFree(p.d_aux);
-  (void)hipFree(p.d_coord_width);
+static void free_code(Engine& e, DevProgram& p) {
+  pool_put(e, p.buf, p.cap);
+  p.buf = nullptr;
+  p.cap = 0;
   p.d_code = nullptr;
   p.d_consts = p.d_aux = p.d_coord_width = nullptr;
+  p.uploaded = false;
 }
 
 static void fill_info(const DevProgram& p, mg_program_info_t* info) {
@@ -860,14 +905,21 @@ void mg_shutdown(void) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
   if (!e.init) return;
-  for (auto& kv : e.progs) free_code(*kv.second);
+  for (auto& kv : e.progs) free_code(e, *kv.second);
   e.progs.clear();
   for (auto& kv : e.gens) {
-    (void)hipFree(kv.second->d_specs);
-    (void)hipFree(kv.second->d_consts);
-    free_code(kv.second->spec);
+    pool_put(e, kv.second->gbuf, kv.second->gcap);
+    free_code(e, kv.second->spec);
+    free_code(e, kv.second->spec_watch);
   }
   e.gens.clear();
+  for (auto& kv : e.pool) (void)hipFree(kv.second);
+  e.pool.clear();
+  if (e.d_watch1) (void)hipFree(e.d_watch1);
+  if (e.d_ver1) (void)hipFree(e.d_ver1);
+  e.d_watch1 = nullptr;
+  e.d_ver1 = nullptr;
+  e.watch1_words = 0;
   if (e.d_scratch) (void)hipFree(e.d_scratch);
   e.d_scratch = nullptr;
   e.scratch_bytes = 0;
@@ -924,7 +976,8 @@ int mg_program_load(const uint8_t* ssa, size_t len, uint64_t* handle) {
   std::string err;
   int rc = lower_program(ssa, len, p->low, err);
   if (rc) return set_err(rc, err);
-  if ((rc = upload_code(*p))) return rc;
+  // uploaded on first use: searches run the generator-specialised copies (mg_gen_load),
+  // only explicit-coordinate evaluation runs this one
   const uint64_t h = e.next_handle++;
   e.progs[h] = std::move(p);
   e.stats.programs_loaded++;
@@ -960,7 +1013,7 @@ int mg_program_free(uint64_t prog) {
   std::lock_guard<std::mutex> g(e.mu);
   auto it = e.progs.find(prog);
   if (it == e.progs.end()) return set_err(MG_E_INVALID, "bad program handle");
-  free_code(*it->second);
+  free_code(e, *it->second);
   e.progs.erase(it);
   return MG_OK;
 }
@@ -979,11 +1032,23 @@ int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* g
   gg->prog = prog;
   gg->specs = specs;
   gg->consts = consts;
-  rc = specialize_program(p->low, &gg->specs, &gg->consts, gg->spec.low, err);
+  rc = specialize_program(p->low, &gg->specs, &gg->consts, gg->spec.low, err, /*keep_watch=*/false);
   if (rc) return set_err(rc, err);
-  if ((rc = upload_code(gg->spec))) return rc;
-  if ((rc = upload(&gg->d_specs, specs.data(), specs.size()))) return rc;
-  if ((rc = upload(&gg->d_consts, consts.data(), consts.size()))) return rc;
+  if ((rc = upload_code(e, gg->spec))) return rc;
+  rc = specialize_program(p->low, &gg->specs, &gg->consts, gg->spec_watch.low, err, /*keep_watch=*/true);
+  if (rc) return set_err(rc, err);
+  if ((rc = upload_code(e, gg->spec_watch))) return rc;
+  {  // specs | consts in one pooled buffer
+    const size_t b_specs = (specs.size() * sizeof(GenSpec) + 255) & ~(size_t)255;
+    const size_t total = std::max<size_t>(b_specs + consts.size() * 4, 256);
+    if ((rc = pool_get(e, total, &gg->gbuf, &gg->gcap))) return rc;
+    std::vector<uint8_t> h(total, 0);
+    std::memcpy(h.data(), specs.data(), specs.size() * sizeof(GenSpec));
+    std::memcpy(h.data() + b_specs, consts.data(), consts.size() * 4);
+    HIPCHK(hipMemcpy(gg->gbuf, h.data(), total, hipMemcpyHostToDevice));
+    gg->d_specs = (GenSpec*)gg->gbuf;
+    gg->d_consts = (uint32_t*)((uint8_t*)gg->gbuf + b_specs);
+  }
   const uint64_t h = e.next_handle++;
   e.gens[h] = std::move(gg);
   *gen_handle = h;
@@ -995,9 +1060,9 @@ int mg_gen_free(uint64_t gen) {
   std::lock_guard<std::mutex> g(e.mu);
   auto it = e.gens.find(gen);
   if (it == e.gens.end()) return set_err(MG_E_INVALID, "bad generator handle");
-  (void)hipFree(it->second->d_specs);
-  (void)hipFree(it->second->d_consts);
-  free_code(it->second->spec);
+  pool_put(e, it->second->gbuf, it->second->gcap);
+  free_code(e, it->second->spec);
+  free_code(e, it->second->spec_watch);
   e.gens.erase(it);
   return MG_OK;
 }
@@ -1007,6 +1072,10 @@ int mg_eval_dev(uint64_t prog, const uint32_t* d_soa, uint64_t n, uint8_t* d_ver
   std::lock_guard<std::mutex> g(e.mu);
   DevProgram* p = find_prog(e, prog);
   if (!p) return set_err(MG_E_INVALID, "bad program handle");
+  if (!p->uploaded) {
+    int rc = upload_code(e, *p);
+    if (rc) return rc;
+  }
   KArgs k{};
   k.soa = d_soa;
   k.verdict = d_verdict;
@@ -1065,7 +1134,7 @@ int mg_eval_generated(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start
   k.watch = d_watch;
   k.start = start;
   k.seed = seed;
-  int rc = launch<MODE_GEN>(e, it->second->spec, k, n);
+  int rc = launch<MODE_GEN>(e, it->second->spec_watch, k, n);
   if (rc == MG_OK) {
     HIPCHK(hipMemcpy(verdict_out, d_ver, n, hipMemcpyDeviceToHost));
     if (d_watch) HIPCHK(hipMemcpy(watch_out, d_watch, watch_bytes, hipMemcpyDeviceToHost));
@@ -1075,8 +1144,34 @@ int mg_eval_generated(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start
   return rc;
 }
 
+// the model of candidate `idx`: the watch rows of the generator's watch-list variant
+// (one interpreter lane; ~tens of microseconds) -> assign_out[watch_words]
+static int read_assignment(Engine& e, DevGen& g, uint64_t seed, uint64_t idx, uint32_t* assign_out) {
+  const uint32_t ww = g.spec_watch.low.watch_words;
+  if (ww == 0) return MG_OK;
+  if (ww > e.watch1_words) {
+    if (e.d_watch1) (void)hipFree(e.d_watch1);
+    e.d_watch1 = nullptr;
+    e.watch1_words = 0;
+    HIPCHK(hipMalloc((void**)&e.d_watch1, (size_t)ww * 4));
+    e.watch1_words = ww;
+  }
+  if (!e.d_ver1) HIPCHK(hipMalloc((void**)&e.d_ver1, 64));
+  KArgs k{};
+  k.specs = g.d_specs;
+  k.gconsts = g.d_consts;
+  k.verdict = e.d_ver1;
+  k.watch = e.d_watch1;
+  k.start = idx;
+  k.seed = seed;
+  int rc = launch<MODE_GEN>(e, g.spec_watch, k, 1);
+  if (rc) return rc;
+  HIPCHK(hipMemcpy(assign_out, e.d_watch1, (size_t)ww * 4, hipMemcpyDeviceToHost));
+  return MG_OK;
+}
+
 int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags,
-              uint64_t* first_hit, uint64_t* n_hits) {
+              uint64_t* first_hit, uint64_t* n_hits, uint32_t* assign_out) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
   DevProgram* p = find_prog(e, prog);
@@ -1100,6 +1195,7 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
   if (first_hit) *first_hit = res[0];
   if (n_hits) *n_hits = res[1];
   e.stats.hits += res[1];
+  if (assign_out && res[0] != ~0ull) return read_assignment(e, *it->second, seed, res[0], assign_out);
   return MG_OK;
 }
 
@@ -1315,7 +1411,7 @@ int mg_jit_free(uint64_t jit) {
 }
 
 int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags, uint64_t* first_hit,
-                  uint64_t* n_hits) {
+                  uint64_t* n_hits, uint32_t* assign_out) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
   auto it = e.jits.find(jit);
@@ -1340,6 +1436,7 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
   if (first_hit) *first_hit = res[0];
   if (n_hits) *n_hits = res[1];
   e.stats.hits += res[1];
+  if (assign_out && res[0] != ~0ull) return read_assignment(e, *git->second, seed, res[0], assign_out);
   return MG_OK;
 }
 

@@ -621,33 +621,47 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
         emit(K_ASSERT, 1, NONE, val(i, i + 1));
       }
     }
-    // watch list (after all nodes: watch entries refer to nodes or site bases)
+    // watch list (after all nodes: watch entries refer to nodes or site bases); every
+    // K_WATCH goes right after the instruction defining its value (one merge pass)
+    std::vector<int64_t> def_at(vwidth.size(), -1);
+    for (size_t k = 0; k < code.size(); k++)
+      if (code[k].dst != NONE && code[k].dst < def_at.size() && def_at[code[k].dst] < 0) def_at[code[k].dst] = (int64_t)k;
+    std::vector<std::vector<VInstr>> after(code.size() + 1);
     for (uint64_t j = 0; j < n_watch; j++) {
       uint32_t wv = watch[j];
       uint32_t v, width;
+      int64_t at;
       if (wv & 0x80000000u) {
         uint32_t c = wv & 0x7FFFFFFFu;
         if (c >= n_coords || site_base_vid[c] == NONE) fail(MG_E_INVALID, "watch site");
         v = site_base_vid[c];
         width = vwidth[v];
+        at = def_at[v];
       } else {
         if (wv >= n_nodes || is_arr[wv]) fail(MG_E_INVALID, "watch node");
+        width = nodes[wv].width;
         if (node_const[wv] != NONE) {
-          v = new_vid(nodes[wv].width);
-          emit(K_CONST, nodes[wv].width, v, NONE, NONE, NONE, node_const[wv]);
+          v = new_vid(width);
+          def_at.push_back(-1);
+          after[code.size()].push_back(VInstr{K_CONST, width, v, NONE, NONE, NONE, node_const[wv], 0, {}});
+          at = (int64_t)code.size();  // a rematerialised literal: appended at the end
         } else {
           v = vid[wv];
+          at = def_at[v];
         }
-        width = nodes[wv].width;
       }
       watch_row[j] = wrow;
-      // insert the K_WATCH right after the instruction defining v
-      VInstr wi{K_WATCH, width, NONE, v, NONE, NONE, wrow, 0, {}};
-      size_t def = 0;
-      for (size_t k = 0; k < code.size(); k++)
-        if (code[k].dst == v) { def = k; break; }
-      code.insert(code.begin() + def + 1, wi);
+      after[at < 0 ? code.size() : (size_t)at].push_back(VInstr{K_WATCH, width, NONE, v, NONE, NONE, wrow, 0, {}});
       wrow += L_of(width);
+    }
+    if (n_watch) {
+      std::vector<VInstr> merged;
+      merged.reserve(code.size() + 2 * n_watch);
+      for (size_t k = 0; k <= code.size(); k++) {
+        if (k < code.size()) merged.push_back(std::move(code[k]));
+        for (auto& w : after[k]) merged.push_back(std::move(w));
+      }
+      code.swap(merged);
     }
     out.watch_row = watch_row;
     out.watch_words = wrow;
@@ -1185,7 +1199,7 @@ namespace mg {
 // Verdicts are unchanged for every generated candidate (tests compare the specialised
 // interpreter and JIT kernels with the C restatement, which runs the full program).
 int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
-                       Lowered& out, std::string& err) {
+                       Lowered& out, std::string& err, bool keep_watch) {
   try {
     const uint32_t NONE = MG_NONE;
     Analysis A(in, specs, gconsts);
@@ -1232,7 +1246,7 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
     std::vector<char> live(nv, 0), keep(code.size(), 0);
     for (size_t k = code.size(); k-- > 0;) {
       const VInstr& c = code[k];
-      const bool side = c.op == K_ASSERT || c.op == K_WATCH;
+      const bool side = c.op == K_ASSERT || (c.op == K_WATCH && keep_watch);
       if (!side && (c.dst == NONE || c.dst >= nv || !live[c.dst])) continue;
       keep[k] = 1;
       auto use = [&](uint32_t x) {
@@ -1255,7 +1269,7 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
     std::vector<VInstr> kept;
     kept.reserve(code.size());
     for (size_t k = 0; k < code.size(); k++)
-      if (keep[k]) kept.push_back(std::move(code[k]));
+      if (keep[k] && (keep_watch || code[k].op != K_WATCH)) kept.push_back(std::move(code[k]));
     const uint64_t ops = in.limb_ops;  // algorithmic work is the query's, not what survives
     out.limb_ops = 0;
     allocate(kept, vwidth, out);

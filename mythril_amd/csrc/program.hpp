@@ -76,8 +76,10 @@ uint64_t op_cost(uint32_t node_op, uint32_t width, uint32_t operand_width);
 // Specialise a lowered program for a generator (specs/gconsts) or, with specs == nullptr,
 // for explicit coordinates: range-decided compares folded, aliases renamed, dead code
 // removed, slots re-allocated.  Same verdicts for every candidate the generator draws.
+// keep_watch = false drops the K_WATCH instructions (and what only they used): the
+// search variant; the model read-back (MODE_GEN) runs the keep_watch variant.
 int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
-                       Lowered& out, std::string& err);
+                       Lowered& out, std::string& err, bool keep_watch = true);
 
 // Validate a generator blob against a lowered program; fills specs/consts.
 int parse_gen(const Lowered& prog, const uint32_t* blob, size_t n_words, std::vector<GenSpec>& specs,

@@ -97,7 +97,7 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_eval_dev": (C.c_int, [C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
             "mg_eval_generated": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, u8p, u32p]),
             "mg_search": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32,
-                                    u64p, u64p]),
+                                    u64p, u64p, u32p]),
             "mg_keccak256": (C.c_int, [u8p, u32p, C.c_uint64, u8p]),
             "mg_stats": (C.c_int, [C.POINTER(Stats)]),
             "mg_stats_reset": (C.c_int, []),
@@ -110,7 +110,7 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_jit_compile": (C.c_int, [C.c_uint64, C.c_uint64, u64p]),
             "mg_jit_info": (C.c_int, [C.c_uint64, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
             "mg_jit_free": (C.c_int, [C.c_uint64]),
-            "mg_jit_search": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u64p, u64p]),
+            "mg_jit_search": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u64p, u64p, u32p]),
             "mg_jit_eval": (C.c_int, [C.c_uint64, u32p, C.c_uint64, u8p, u32p]),
             "mg_jit_eval_dev": (C.c_int, [C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
         }
@@ -237,10 +237,14 @@ class Engine:
                                           _ptr(watch, C.c_uint32) if watch is not None else None))
         return ver, watch
 
-    def search(self, prog: int, gen: int, seed: int, start: int, count: int, early_exit: bool = True):
+    def search(self, prog: int, gen: int, seed: int, start: int, count: int, early_exit: bool = True,
+               assign: Optional[np.ndarray] = None):
+        """(first hit or None, hit count); with ``assign`` (uint32[watch_words]) the winning
+        candidate's watch rows are written into it."""
         fh, nh = C.c_uint64(), C.c_uint64()
         flags = MG_SEARCH_EARLY_EXIT if early_exit else 0
-        _check(self.lib.mg_search(prog, gen, seed, start, count, flags, C.byref(fh), C.byref(nh)))
+        ap = _ptr(assign, C.c_uint32) if assign is not None else None
+        _check(self.lib.mg_search(prog, gen, seed, start, count, flags, C.byref(fh), C.byref(nh), ap))
         return (None if fh.value == NO_HIT else fh.value), nh.value
 
     # JIT-specialised kernels --------------------------------------
@@ -257,10 +261,12 @@ class Engine:
     def jit_free(self, jit: int):
         _check(self.lib.mg_jit_free(jit))
 
-    def jit_search(self, jit: int, seed: int, start: int, count: int, early_exit: bool = True):
+    def jit_search(self, jit: int, seed: int, start: int, count: int, early_exit: bool = True,
+                   assign: Optional[np.ndarray] = None):
         fh, nh = C.c_uint64(), C.c_uint64()
         flags = MG_SEARCH_EARLY_EXIT if early_exit else 0
-        _check(self.lib.mg_jit_search(jit, seed, start, count, flags, C.byref(fh), C.byref(nh)))
+        ap = _ptr(assign, C.c_uint32) if assign is not None else None
+        _check(self.lib.mg_jit_search(jit, seed, start, count, flags, C.byref(fh), C.byref(nh), ap))
         return (None if fh.value == NO_HIT else fh.value), nh.value
 
     def jit_eval(self, jit: int, soa: np.ndarray, n: int, watch_words: int = 0):

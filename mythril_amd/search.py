@@ -58,11 +58,19 @@ class GenBuilder:
         self.P = P
         self.specs: List[List[int]] = [[GEN_UNIFORM, 0, 0, 0, 0, 0, 0, 0] for _ in P.coords]
         self.consts: List[int] = []
+        self._pool: Dict[tuple, int] = {}  # (width, values) -> offset: coordinates share dictionaries
 
     def _push(self, values: Sequence[int], w: int) -> int:
+        key = (w, tuple(values))
+        off = self._pool.get(key)
+        if off is not None:
+            return off
         off = len(self.consts)
-        for v in values:
-            self.consts.extend(ssa.int_to_limbs(int(v) % (1 << w), w))
+        L = ssa.limbs(w)
+        m = (1 << w) - 1
+        raw = b"".join((int(v) & m).to_bytes(4 * L, "little") for v in values)
+        self.consts.extend(np.frombuffer(raw, dtype="<u4").tolist())
+        self._pool[key] = off
         return off
 
     def uniform(self, c: int):
@@ -123,11 +131,9 @@ class GenBuilder:
         self.specs[c][0] = (self.specs[c][0] & 0xFF) | ((off + 1) << 8)
 
     def blob(self) -> np.ndarray:
-        words = [GEN_MAGIC, len(self.specs), len(self.consts), 0]
-        for s in self.specs:
-            words.extend(int(x) & 0xFFFFFFFF for x in s)
-        words.extend(self.consts)
-        return np.array(words, dtype=np.uint32)
+        head = np.array([GEN_MAGIC, len(self.specs), len(self.consts), 0], dtype=np.uint32)
+        specs = np.array(self.specs, dtype=np.int64).astype(np.uint32).reshape(-1)
+        return np.concatenate([head, specs, np.array(self.consts, dtype=np.uint32)])
 
 
 def _interval_bounds(P: ssa.Program):
@@ -258,6 +264,7 @@ class SearchResult:
         self.index, self.hits, self.scanned, self.seconds, self.model = index, hits, scanned, seconds, model
         self.engine = "interp"
         self.buckets = 1
+        self.timing = {}
 
 
 def model_watch(P: ssa.Program):
@@ -313,13 +320,35 @@ def materialize(engine, P: ssa.Program, gen_blob: np.ndarray, seed: int, index: 
 
 def prepare(roots: Sequence[T.Term], gen: Optional[GenBuilder] = None):
     """The program and generator blob a search runs: prefix-incremental flattening with
-    AUX calldata words (``FLATTEN_CACHE``) and the propagation-shaped generator."""
+    AUX calldata words (``FLATTEN_CACHE``), the model watch list (``model_watch``: what
+    ``mg_search``'s ``assign_out`` returns for the winning candidate) and the
+    propagation-shaped generator."""
     P = FLATTEN_CACHE.flatten(roots)
+    P.set_watch(model_watch(P)[0])
     g = gen or default_generator(P, roots=roots)
     return P, g.blob()
 
 
-def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int = 1 << 22,
+def model_from_assignment(P: ssa.Program, assign: np.ndarray):
+    """(scalars, arrays, funcs) from the watch rows ``mg_search`` wrote for a hit."""
+    entries, widths = model_watch(P)
+    raw = np.ascontiguousarray(assign, dtype="<u4").tobytes()
+    vals_l, r = [], 0
+    for w in widths:
+        L = ssa.limbs(w)
+        vals_l.append(int.from_bytes(raw[4 * r:4 * (r + L)], "little"))
+        r += L
+    vals = iter(vals_l)
+    scal, keys, bases = {}, {}, {}
+    for c in P.scalar_coords():
+        scal[c.index] = next(vals)
+    for c in P.sites:
+        keys[c.index] = next(vals)
+        bases[c.index] = next(vals)
+    return ssa.model_from_sites(P, scal, keys, bases)
+
+
+def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int = 1 << 16,
            max_candidates: int = 1 << 26, timeout_s: float = 10.0, gen: Optional[GenBuilder] = None,
            want_model: bool = True, jit: str = "auto", jit_cost_s: float = 0.5) -> SearchResult:
     """Find the lowest-index satisfying candidate (or give up: None).
@@ -327,19 +356,24 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
     ``jit``: "never" keeps the generic interpreter (``k_run``, no compile
     latency); "always" compiles the query-specialised kernel first; "auto"
     starts on the interpreter, and when the first chunk has no hit and more than
-    ``jit_cost_s`` of the budget is left, compiles the JIT kernel (~0.35 s of
-    hipRTC, ~10x the interpreter's candidates/s) and continues the SAME index
-    stream on it.  Both kernels compute identical verdicts for every index
-    (``tests/test_gpu_jit.py``), so the first hit does not depend on the mode."""
+    ``jit_cost_s`` of the budget is left, compiles the JIT kernel and continues the
+    SAME index stream on it.  Both kernels compute identical verdicts for every index
+    (``tests/test_gpu_jit.py``), so the first hit does not depend on the mode.  The
+    model comes back with the hit (``mg_search``'s ``assign_out``)."""
+    tp = time.perf_counter()
     P, blob = prepare(roots, gen)
+    th = time.perf_counter()
     prog = engine.load(P.to_bytes())
     t0 = time.perf_counter()
+    timing = {"host_prepare_ms": (th - tp) * 1e3}
     scanned = 0
     hit = None
     hits = 0
     used = "interp"
+    assign = np.zeros(max(P.watch_words, 1), dtype=np.uint32) if want_model else None
     try:
         gh = engine.load_gen(prog, blob)
+        timing["load_ms"] = (time.perf_counter() - th) * 1e3
         jh = None
         try:
             start = 0
@@ -347,22 +381,26 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                 left = timeout_s - (time.perf_counter() - t0)
                 if jh is None and (jit == "always" or (jit == "auto" and scanned > 0 and left > jit_cost_s)):
                     try:
+                        tc = time.perf_counter()
                         jh = engine.jit_compile(prog, gh)
+                        timing["jit_compile_ms"] = (time.perf_counter() - tc) * 1e3
                         used = "jit"
                     except Exception:  # JIT unavailable for this program: stay on the interpreter
                         jit = "never"
                     continue
                 n = min(chunk, max_candidates - scanned)
                 if jh is not None:
-                    idx, nh = engine.jit_search(jh, seed, start, n, early_exit=True)
+                    idx, nh = engine.jit_search(jh, seed, start, n, early_exit=True, assign=assign)
                 else:
-                    idx, nh = engine.search(prog, gh, seed, start, n, early_exit=True)
+                    idx, nh = engine.search(prog, gh, seed, start, n, early_exit=True, assign=assign)
                 scanned += n
                 start += n
                 if idx is not None:
                     hit, hits = idx, nh
                     break
-                chunk = min(chunk * 2, 1 << 28 if jh is None else 1 << 30)
+                # a first launch of 1024 waves answers the easy queries in one program pass;
+                # then geometric growth amortises the launch + sync per chunk
+                chunk = min(chunk * 4, 1 << 26 if jh is None else 1 << 30)
         finally:
             if jh is not None:
                 engine.jit_free(jh)
@@ -373,7 +411,12 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
     res = SearchResult(hit, hits, scanned, dt)
     res.engine = used
     if hit is not None and want_model:
-        res.model = materialize(engine, P, blob, seed, hit) + (P,)
+        # the search only reports indices whose verdict is 1
+        tm = time.perf_counter()
+        res.model = (1,) + model_from_assignment(P, assign) + (P,)
+        timing["model_ms"] = (time.perf_counter() - tm) * 1e3
+    timing["search_ms"] = dt * 1e3
+    res.timing = timing
     return res
 
 

@@ -129,15 +129,19 @@ class Program:
             r += limbs(c.width)
         return out
 
+    def watch_width(self, entry: int) -> int:
+        """Width of a watch entry: a node, or 0x80000000 | coord for a site's base value."""
+        return self.coords[entry & 0x7FFFFFFF].width if entry & 0x80000000 else self.node_width[entry]
+
     @property
     def watch_words(self) -> int:
-        return sum(limbs(self.node_width[n]) for n in self.watch)
+        return sum(limbs(self.watch_width(n)) for n in self.watch)
 
     def watch_row_offsets(self) -> List[int]:
         out, r = [], 0
         for n in self.watch:
             out.append(r)
-            r += limbs(self.node_width[n])
+            r += limbs(self.watch_width(n))
         return out
 
     def scalar_coords(self):

@@ -5,6 +5,7 @@ tests/laser/keccak_tests.py.  Verdict mapping: where the reference expects
 ``unsat`` the engine must never return a model the oracle rejects (the engine
 answers ``unknown``, which get_model turns into UnsatError exactly like z3's
 unsat/unknown)."""
+import numpy as np
 import pytest
 
 from mythril_amd import solver
@@ -241,3 +242,31 @@ def test_partitioned_search_with_ground_bucket(engine):
     ground_false = (BVV(1, 256) == BVV(2, 256)).raw
     assert search.search_partitioned(engine, [cs[0], ground_false], timeout_s=0.2,
                                      max_candidates=1 << 22).index is None
+
+
+@pytest.mark.parametrize("name", ["suicide_kill", "token_transfer_underflow", "walletlibrary_kill", "sha3_keyed_mapping"])
+def test_assign_out_equals_materialized_model(engine, name):
+    """mg_search's assign_out (the winning candidate's watch rows, written with the hit)
+    equals the model read back by a separate generated evaluation of that index, for the
+    interpreter and the JIT search."""
+    from mythril_amd import search, workloads
+
+    roots = [c.raw for c in workloads.WORKLOADS[name]()]
+    P, blob = search.prepare(roots)
+    prog = engine.load(P.to_bytes())
+    gh = engine.load_gen(prog, blob)
+    jit = engine.jit_compile(prog, gh)
+    try:
+        a1 = np.zeros(P.watch_words, dtype=np.uint32)
+        a2 = np.zeros(P.watch_words, dtype=np.uint32)
+        i1, _ = engine.search(prog, gh, 5, 0, 1 << 22, early_exit=True, assign=a1)
+        i2, _ = engine.jit_search(jit, 5, 0, 1 << 22, early_exit=True, assign=a2)
+        assert i1 is not None and i1 == i2
+        assert (a1 == a2).all()
+        ver, watch = engine.eval_generated(prog, gh, 5, i1, 1, watch_words=P.watch_words)
+        assert ver[0] == 1
+        assert (watch[:, 0] == a1).all()
+    finally:
+        engine.jit_free(jit)
+        engine.free_gen(gh)
+        engine.free(prog)
