@@ -257,6 +257,10 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
 int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words, int compile,
                           char* buf, size_t cap, size_t* out_len);
 int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle);
+/* flags: MG_JIT_GEN_VERDICTS also builds mgj_gen (per-candidate verdicts, mg_jit_verdicts) */
+#define MG_JIT_GEN_VERDICTS 1u
+int mg_jit_compile_ex(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* jit_handle);
+int mg_jit_verdicts(uint64_t jit, uint64_t seed, uint64_t start, uint64_t n, uint8_t* verdict_out);
 int mg_jit_info(uint64_t jit, double* compile_ms, int* blocks_per_cu);
 int mg_jit_free(uint64_t jit);
 int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags, uint64_t* first_hit,

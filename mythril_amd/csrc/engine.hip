@@ -658,7 +658,7 @@ struct DevGen {
 
 struct DevJit {
   hipModule_t mod = nullptr;
-  hipFunction_t fsearch = nullptr, feval = nullptr;
+  hipFunction_t fsearch = nullptr, feval = nullptr, fgen = nullptr;
   uint64_t prog = 0, gen = 0;
   int nb_search = 1, nb_eval = 1;
   double compile_ms = 0;
@@ -1319,10 +1319,12 @@ int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_bl
     if (rc) return set_err(rc, err);
   }
   Lowered sp;
-  rc = specialize_program(low, gen_blob ? &specs : nullptr, gen_blob ? &consts : nullptr, sp, err);
+  // the same specialisation mg_gen_load / mg_jit_compile use (search: watch list dropped)
+  rc = specialize_program(low, gen_blob ? &specs : nullptr, gen_blob ? &consts : nullptr, sp, err,
+                          /*keep_watch=*/gen_blob == nullptr);
   if (rc) return set_err(rc, err);
-  const std::string src = gen_blob ? jit_source(sp, &specs, &consts, true, false)
-                                   : jit_source(sp, nullptr, nullptr, false, true);
+  const std::string src = gen_blob ? jit_source(sp, &specs, &consts, JIT_SEARCH)
+                                   : jit_source(sp, nullptr, nullptr, JIT_EVAL);
   if (out_len) *out_len = src.size();
   if (buf && cap) {
     const size_t n = std::min(cap - 1, src.size());
@@ -1338,7 +1340,9 @@ int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_bl
   return MG_OK;
 }
 
-int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle) {
+int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle) { return mg_jit_compile_ex(prog, gen, 0, jit_handle); }
+
+int mg_jit_compile_ex(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* jit_handle) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
   DevProgram* p = find_prog(e, prog);
@@ -1352,13 +1356,13 @@ int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle) {
   // with a generator: the search kernel specialised on it; without: the eval kernel
   std::string src;
   if (gp) {
-    src = jit_source(gp->spec.low, &gp->specs, &gp->consts, true, false);
+    src = jit_source(gp->spec.low, &gp->specs, &gp->consts, JIT_SEARCH | ((flags & MG_JIT_GEN_VERDICTS) ? JIT_GEN : 0u));
   } else {
     Lowered ev;
     std::string err;
     int rc = specialize_program(p->low, nullptr, nullptr, ev, err);
     if (rc) return set_err(rc, err);
-    src = jit_source(ev, nullptr, nullptr, false, true);
+    src = jit_source(ev, nullptr, nullptr, JIT_EVAL);
   }
   auto t0 = std::chrono::steady_clock::now();
   auto hit = e.code_cache.find(src);
@@ -1374,6 +1378,7 @@ int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle) {
   int nb = 0;
   if (gp) {
     HIPCHK(hipModuleGetFunction(&j->fsearch, j->mod, "mgj_search"));
+    if (flags & MG_JIT_GEN_VERDICTS) HIPCHK(hipModuleGetFunction(&j->fgen, j->mod, "mgj_gen"));
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, j->fsearch, 256, 0) == hipSuccess && nb > 0)
       j->nb_search = nb;
   } else {
@@ -1438,6 +1443,31 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
   e.stats.hits += res[1];
   if (assign_out && res[0] != ~0ull) return read_assignment(e, *git->second, seed, res[0], assign_out);
   return MG_OK;
+}
+
+int mg_jit_verdicts(uint64_t jit, uint64_t seed, uint64_t start, uint64_t n, uint8_t* verdict_out) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  auto it = e.jits.find(jit);
+  if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
+  DevJit& j = *it->second;
+  auto git = e.gens.find(j.gen);
+  if (git == e.gens.end() || !j.fgen) return set_err(MG_E_INVALID, "jit was not compiled with MG_JIT_GEN_VERDICTS");
+  if (n == 0) return MG_OK;
+  uint8_t* d_ver = nullptr;
+  HIPCHK(hipMalloc((void**)&d_ver, n));
+  const uint32_t* gconsts = git->second->d_consts;
+  uint64_t sk = seed_lane_key(seed), sg = seed_group_key(seed);
+  uint32_t nblk = 0;
+  void* args[] = {&gconsts, &start, &n, &sk, &sg, &d_ver, &nblk};
+  const uint64_t lanes = (start + n) - (start & ~63ull);
+  int rc = jit_launch(e, j.fgen, j.nb_search, lanes, args, nblk);
+  if (rc == MG_OK) {
+    hipError_t he = hipMemcpy(verdict_out, d_ver, n, hipMemcpyDeviceToHost);
+    if (he != hipSuccess) rc = set_err(MG_E_HIP, hipGetErrorString(he));
+  }
+  (void)hipFree(d_ver);
+  return rc;
 }
 
 int mg_jit_eval_dev(uint64_t jit, const uint32_t* d_soa, uint64_t n, uint8_t* d_verdict, uint32_t* d_watch) {

@@ -514,6 +514,7 @@ struct Gen {
   // P is specialised (program.cpp specialize_program): decided compares are literals,
   // aliases are renamed away and dead instructions are gone
   void body(bool search) {
+    coord_var.clear();  // generated-coordinate names are per kernel
     for (const Instr& in : P.vcode) emit(in, search, !search);
   }
 };
@@ -521,7 +522,8 @@ struct Gen {
 }  // namespace
 
 std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
-                       bool want_search, bool want_eval) {
+                       uint32_t kernels) {
+  const bool want_search = kernels & JIT_SEARCH, want_eval = kernels & JIT_EVAL, want_gen = kernels & JIT_GEN;
   Gen g(P, specs, gconsts);
   auto& o = g.o;
   // hipRTC compiles this with -nogpuinc -nogpulib: its own runtime header still supplies
@@ -582,6 +584,32 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  if (lane == 0u) {\n"
        "    if (wave_best != ~0ull) atomicMin(hit, (unsigned long long)wave_best);\n"
        "    if (wave_hits) atomicAdd(hit + 1, (unsigned long long)wave_hits);\n"
+       "  }\n}\n\n";
+  }
+  if (want_gen) {
+  // per-candidate verdicts of generated candidates [start, start + count) (parity tests)
+  o << "extern \"C\" __global__ void " << lb << " mgj_gen(const uint32_t* __restrict__ gconsts, "
+       "uint64_t start, uint64_t count, uint64_t sk, uint64_t sg, uint8_t* __restrict__ verdict_out, uint32_t nblk) {\n"
+       "  const uint32_t tid = __builtin_amdgcn_workitem_id_x(), bid = __builtin_amdgcn_workgroup_id_x();\n"
+       "  const bool early = false;\n"
+       "  const uint32_t lane = tid & 63u;\n"
+       "  const uint64_t a0 = start & ~63ull, end = start + count;\n"
+       "  const uint64_t ngroups = (end - a0 + 63ull) >> 6;\n"
+       "  const uint64_t gstride = (uint64_t)nblk * 4u;\n"
+       "  for (uint64_t g = (uint64_t)bid * 4u + (tid >> 6); g < ngroups; g += gstride) {\n"
+       "  const uint64_t gb = a0 + (g << 6);\n"
+       "  const uint64_t gbase = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32)) << 32) | "
+       "__builtin_amdgcn_readfirstlane((uint32_t)gb);\n"
+       "  const uint64_t idx = gbase + lane;\n"
+       "  const bool active = idx >= start && idx < end;\n"
+       "  GKeys ky;\n"
+       "  { const uint64_t K = fmix64(idx ^ sk), G = fmix64((gbase >> 6) ^ sg);\n"
+       "    ky.klo = (uint32_t)K; ky.khi = (uint32_t)(K >> 32); ky.glo = (uint32_t)G; ky.ghi = (uint32_t)(G >> 32); }\n"
+       "  uint32_t verdict = 1u;\n";
+  g.decls();
+  g.body(true);
+  o << "  mg_next:\n"
+       "  if (active) verdict_out[idx - start] = (uint8_t)verdict;\n"
        "  }\n}\n\n";
   }
   if (want_eval) {

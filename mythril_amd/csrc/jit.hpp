@@ -7,10 +7,12 @@
 
 namespace mg {
 
-// HIP source with two kernels: mgj_search (generator + first hit) and mgj_eval (SoA inputs).
+// HIP source of the requested kernels: mgj_search (generator + first hit), mgj_gen
+// (per-candidate verdicts of generated candidates) and mgj_eval (SoA inputs).
 // `specs`/`gconsts` (nullable) specialise the generator at codegen time.
+enum : uint32_t { JIT_SEARCH = 1, JIT_EVAL = 2, JIT_GEN = 4 };
 std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
-                       bool want_search, bool want_eval);
+                       uint32_t kernels);
 
 // hipRTC compile for gfx950 -> code object bytes. MG_OK or MG_E_*; `log` gets the compiler log.
 int jit_compile(const std::string& src, std::vector<char>& code, std::string& log);

@@ -32,7 +32,7 @@ EXPORTS = [
     "mg_program_load",
     "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_info", "mg_gen_free", "mg_eval", "mg_eval_dev",
     "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
-    "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_jit_compile", "mg_jit_info",
+    "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_jit_compile", "mg_jit_compile_ex", "mg_jit_verdicts", "mg_jit_info",
     "mg_jit_free", "mg_jit_search", "mg_jit_eval", "mg_jit_eval_dev",
 ]
 
@@ -108,6 +108,8 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_program_jit_source": (C.c_int, [u8p, C.c_size_t, u32p, C.c_size_t, C.c_int, C.c_char_p,
                                                 C.c_size_t, C.POINTER(C.c_size_t)]),
             "mg_jit_compile": (C.c_int, [C.c_uint64, C.c_uint64, u64p]),
+            "mg_jit_compile_ex": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, u64p]),
+            "mg_jit_verdicts": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, u8p]),
             "mg_jit_info": (C.c_int, [C.c_uint64, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
             "mg_jit_free": (C.c_int, [C.c_uint64]),
             "mg_jit_search": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u64p, u64p, u32p]),
@@ -248,10 +250,16 @@ class Engine:
         return (None if fh.value == NO_HIT else fh.value), nh.value
 
     # JIT-specialised kernels --------------------------------------
-    def jit_compile(self, prog: int, gen: int = 0) -> int:
+    def jit_compile(self, prog: int, gen: int = 0, gen_verdicts: bool = False) -> int:
         h = C.c_uint64()
-        _check(self.lib.mg_jit_compile(prog, gen, C.byref(h)))
+        _check(self.lib.mg_jit_compile_ex(prog, gen, 1 if gen_verdicts else 0, C.byref(h)))
         return h.value
+
+    def jit_verdicts(self, jit: int, seed: int, start: int, n: int) -> np.ndarray:
+        """Per-candidate verdicts of the JIT kernel (compiled with ``gen_verdicts``)."""
+        ver = np.zeros(n, dtype=np.uint8)
+        _check(self.lib.mg_jit_verdicts(jit, seed, start, n, _ptr(ver, C.c_uint8)))
+        return ver
 
     def jit_info(self, jit: int):
         ms, nb = C.c_double(), C.c_int()

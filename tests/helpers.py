@@ -143,9 +143,28 @@ def random_assignments(P: ssa.Program, n: int, seed: int):
     return [[edge_value(rng, c.width) for c in P.coords] for _ in range(n)]
 
 
-def gpu_eval_terms(engine, roots: Sequence[T.Term], watch_terms: Sequence[T.Term], assigns=None, n=64, seed=0):
-    """Evaluate on the GPU; returns (P, assigns, verdicts, per-candidate dict term-id -> value,
-    per-candidate oracle models)."""
+def lift_literals(terms: Sequence[T.Term], min_width: int = 8):
+    """Replace every bit-vector literal (width >= min_width) by a fresh variable ``lit<k>``.
+    Returns (new terms, {name: value}).  Evaluated with those values as runtime inputs, the
+    JIT cannot constant-fold the arithmetic (hipRTC folds literal operands at -O3)."""
+    memo: Dict[int, T.Term] = {}
+    vals: Dict[str, int] = {}
+    for t in T.postorder(list(terms)):
+        if t.op == "bvconst" and t.width >= min_width:
+            name = f"lit{len(vals)}_{t.width}"
+            vals[name] = t.params[0]
+            memo[t.id] = T.BitVecVar(name, t.width)
+            continue
+        args = tuple(memo[a.id] for a in t.args)
+        memo[t.id] = t if args == t.args else T.mk(t.op, t.sort, args, t.params)
+    return [memo[t.id] for t in terms], vals
+
+
+def gpu_eval_terms(engine, roots: Sequence[T.Term], watch_terms: Sequence[T.Term], assigns=None, n=64, seed=0,
+                   jit: bool = False):
+    """Evaluate on the GPU (the interpreter, or with ``jit`` the hipRTC-specialised eval kernel
+    on the same runtime SoA inputs); returns (P, assigns, verdicts, per-candidate dict
+    term-id -> value, per-candidate oracle models)."""
     P = ssa.flatten(list(roots), extra=list(watch_terms))
     # watch every requested term that the program contains, plus the model read-back entries
     from mythril_amd.search import model_watch
@@ -164,7 +183,14 @@ def gpu_eval_terms(engine, roots: Sequence[T.Term], watch_terms: Sequence[T.Term
     prog = engine.load(P.to_bytes())
     try:
         info = engine.info(prog)
-        ver, watch = engine.eval(prog, soa, len(assigns), watch_words=info.watch_words)
+        if jit:
+            jh = engine.jit_compile(prog, 0)
+            try:
+                ver, watch = engine.jit_eval(jh, soa, len(assigns), watch_words=info.watch_words)
+            finally:
+                engine.jit_free(jh)
+        else:
+            ver, watch = engine.eval(prog, soa, len(assigns), watch_words=info.watch_words)
     finally:
         engine.free(prog)
     from mythril_amd.search import read_rows

@@ -83,7 +83,7 @@ def test_jit_search_matches_interpreter_and_c(engine, name, shaped, aux):
     blob = search.default_generator(P, roots=roots if shaped else None).blob()
     prog = engine.load(P.to_bytes())
     gh = engine.load_gen(prog, blob)
-    jit = engine.jit_compile(prog, gh)
+    jit = engine.jit_compile(prog, gh, gen_verdicts=True)
     try:
         for start, n in ((0, 1 << 12), (987654321, 1 << 16)):
             a = engine.search(prog, gh, 77, start, n, early_exit=False)
@@ -96,6 +96,9 @@ def test_jit_search_matches_interpreter_and_c(engine, name, shaped, aux):
         cf, ch, cver = cport.search(P.to_bytes(), blob, 77, 4096 + 13, 3000, threads=8, verdicts=True)
         gver, _ = engine.eval_generated(prog, gh, 77, 4096 + 13, 3000)
         assert (gver == cver).all(), int((gver != cver).sum())
+        # the JIT kernel candidate by candidate (mgj_gen: the same specialised body as mgj_search)
+        jver = engine.jit_verdicts(jit, 77, 4096 + 13, 3000)
+        assert (jver == cver).all(), int((jver != cver).sum())
         assert (cf, ch) == engine.jit_search(jit, 77, 4096 + 13, 3000, early_exit=False)
         # early exit keeps the exact first hit
         full = engine.jit_search(jit, 77, 0, 1 << 20, early_exit=False)[0]
@@ -105,3 +108,93 @@ def test_jit_search_matches_interpreter_and_c(engine, name, shaped, aux):
         engine.jit_free(jit)
         engine.free_gen(gh)
         engine.free(prog)
+
+
+def test_jit_edge_arithmetic_runtime_operands(engine):
+    """Every binary op over the 256-bit edge set through the JIT eval kernel, operands as
+    runtime SoA inputs (nothing for hipRTC to fold), bit-exact against the oracle."""
+    from helpers import BIN_OPS, CMP_OPS, EDGE_256, gpu_eval_terms
+
+    a = T.BitVecVar("a", 256)
+    b = T.BitVecVar("b", 256)
+    terms = [T.bvbin(op, a, b) for op in BIN_OPS] + [T.bvcmp(op, a, b) for op in CMP_OPS] + \
+            [T.bvun("bvneg", a), T.bvun("bvnot", a), T.bvexp(a, b)]
+    vals = EDGE_256 + [(1 << 256) - 5, 3 << 254, 0x1234567890ABCDEF << 100, 7]
+    assigns = [[x, y] for x in vals for y in vals]
+    P, _, ver, got, models = gpu_eval_terms(engine, [T.BoolVal(True)], terms, assigns, jit=True)
+    for i, (x, y) in enumerate(assigns):
+        want = evaluate_many_terms(terms, {"a": x, "b": y})
+        for t, w in zip(terms, want):
+            assert got[i][t.id] == w, (t.op, hex(x), hex(y))
+
+
+def test_jit_narrow_widths_runtime_operands(engine):
+    from helpers import gpu_eval_terms
+
+    rng = random.Random(3)
+    for w in (1, 7, 8, 31, 32, 33, 63, 64, 65, 100, 160, 255):
+        a = T.BitVecVar("a", w)
+        b = T.BitVecVar("b", w)
+        terms = [T.bvbin(op, a, b) for op in ["bvadd", "bvsub", "bvmul", "bvudiv", "bvurem", "bvsdiv", "bvsrem",
+                                              "bvsmod", "bvshl", "bvlshr", "bvashr", "bvand", "bvor", "bvxor"]]
+        terms += [T.bvcmp(op, a, b) for op in ["bvult", "bvule", "bvslt", "bvsle", "bvumul_noovfl"]]
+        terms += [T.zero_extend(5, a), T.sign_extend(40, a), T.concat(a, b), T.extract(w - 1, w // 2, a)]
+        m = (1 << w) - 1
+        assigns = [[rng.choice([0, 1, m, m >> 1, (m >> 1) + 1, rng.getrandbits(w)]),
+                    rng.choice([0, 1, m, m >> 1, (m >> 1) + 1, rng.getrandbits(w), w, w - 1])] for _ in range(64)]
+        P, _, ver, got, models = gpu_eval_terms(engine, [T.BoolVal(True)], terms, assigns, jit=True)
+        for i, (x, y) in enumerate(assigns):
+            want = evaluate_many_terms(terms, {"a": x, "b": y})
+            for t, wv in zip(terms, want):
+                assert got[i][t.id] == wv, (w, t.op, x, y)
+
+
+def test_jit_vmtests_literals_as_runtime_inputs(engine):
+    """VMTests replay programs through the JIT eval kernel with every PUSH literal lifted
+    into a runtime coordinate (tests/laser/evm_testsuite/evm_test.py:109-188 post-states):
+    this checks the kernel's arithmetic, not hipRTC's constant folder."""
+    from helpers import lift_literals
+
+    cases = vmtest_cases()
+    checked = 0
+    for name, v, r in cases:
+        keys = [int(k, 16) for k in v["post_storage"]]
+        if not keys:
+            continue
+        words = [r.storage_word(k).raw for k in keys]
+        lifted, lits = lift_literals(words)
+        P = ssa.flatten([T.BoolVal(True)], extra=lifted)
+        P.set_watch([P.term_node[w.id] for w in lifted])
+        scal, arrs = replay_assignment(v)
+        scal = dict(scal, **lits)
+        m = OracleModel(scal, arrs)
+        assign = [0] * len(P.coords)
+        for c in P.coords:
+            if c.kind == ssa.COORD_SCALAR:
+                assign[c.index] = scal.get(c.name, 0)
+            else:
+                key = evaluate(P.node_term[P.site_key_node[c.index]], m)
+                assign[c.index] = arrs.get(c.name, ({}, 0))[0].get(key, 0)
+        soa = ssa.soa_from_assignments(P, [assign])
+        prog = engine.load(P.to_bytes())
+        try:
+            info = engine.info(prog)
+            jh = engine.jit_compile(prog, 0)
+            try:
+                _, w_j = engine.jit_eval(jh, soa, 1, watch_words=info.watch_words)
+            finally:
+                engine.jit_free(jh)
+        finally:
+            engine.free(prog)
+        row = 0
+        for k, x in v["post_storage"].items():
+            assert ssa.limbs_to_int(w_j[row:row + 8, 0]) == int(x, 16), (name, k)
+            row += 8
+            checked += 1
+    assert checked >= 390
+
+
+def evaluate_many_terms(terms, scalars):
+    from oracle.bv import evaluate_many
+
+    return evaluate_many(terms, OracleModel(scalars))
