@@ -215,12 +215,16 @@ def _extend(st: "_FlatState", terms: Sequence[T.Term], lazy_inverse: bool) -> No
         return new_node("CONST", w, p0=off, term=term)
 
     def table(kind, name, kw, vw):
-        key = (kind, name, kw, vw)
+        # keyed by name alone: the model (Model.arrays / funcs) is keyed by name, so one
+        # name at two sorts would silently merge two tables there
+        key = (kind, name)
         t = table_of.get(key)
         if t is None:
             t = len(P.tables)
             P.tables.append(Table(t, kind, name, kw, vw))
             table_of[key] = t
+        elif (P.tables[t].key_width, P.tables[t].val_width) != (kw, vw):
+            raise Unsupported(f"symbol {name} used with two sorts")
         return t
 
     def new_coord(width, kind, node, tab, name, term):
@@ -242,7 +246,9 @@ def _extend(st: "_FlatState", terms: Sequence[T.Term], lazy_inverse: bool) -> No
             n = const_node(T.const_value(t), t.width, term=t)
         elif op in ("bvvar", "boolvar"):
             name = t.params[0]
-            key = f"{name}:{t.width}:{t.sort[0]}"
+            # keyed by name alone (Model.scalars is): a second sort of the same name is
+            # a different z3 constant that this model layout cannot represent
+            key = name
             if key in scalar_coord:
                 raise Unsupported(f"symbol {name} used with two sorts")
             ci = len(P.coords)

@@ -155,3 +155,31 @@ def test_flatten_cache_survives_unsupported_extension():
     with pytest.raises(ssa.Unsupported):
         fc.flatten(roots[:-1] + [bad])
     assert fc.flatten(roots).to_bytes() == ssa.flatten(roots).to_bytes()
+
+
+def test_same_name_two_sorts_is_unsupported():
+    """BitVec('x', 8) and BitVec('x', 256) are different z3 constants, but Model.scalars is
+    keyed by name: the flattener must refuse the query (the caller falls back to z3)
+    rather than return a model where one value overwrote the other."""
+    x8 = T.BitVecVar("x", 8)
+    x256 = T.BitVecVar("x", 256)
+    roots = [T.eq(x8, T.BitVecVal(3, 8)), T.eq(x256, T.BitVecVal(1 << 200, 256))]
+    with pytest.raises(ssa.Unsupported, match="two sorts"):
+        ssa.flatten(roots)
+    # incremental: the second sort arrives in an extension of a cached prefix
+    fc = ssa.FlattenCache()
+    fc.flatten(roots[:1])
+    with pytest.raises(ssa.Unsupported, match="two sorts"):
+        fc.flatten(roots)
+    # arrays / UFs: same name at two sorts
+    a = T.ArrayVar("m", 256, 256)
+    b = T.ArrayVar("m", 256, 8)
+    with pytest.raises(ssa.Unsupported, match="two sorts"):
+        ssa.flatten([T.eq(T.select(a, x256), T.BitVecVal(1, 256)), T.eq(T.select(b, x256), T.BitVecVal(1, 8))])
+    f1 = Function("f", 256, 256)
+    f2 = Function("f", 256, 8)
+    y = symbol_factory.BitVecSym("y", 256)
+    with pytest.raises(ssa.Unsupported, match="two sorts"):
+        ssa.flatten([(f1(y) == 1).raw, (f2(y) == 1).raw])
+    # one name at one sort used many times is fine
+    assert len(ssa.flatten([roots[1], T.eq(x256, x256)]).scalar_coords()) == 1
