@@ -324,7 +324,7 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
       const uint32_t L = L_of(vwidth[x]);
       return std::memcmp(&consts[vconst[x]], &consts[vconst[y]], 4 * L) != 0;
     };
-    auto emit = [&](uint32_t op, uint32_t wd, uint32_t dst, uint32_t a = NONE, uint32_t b = NONE, uint32_t c = NONE,
+    auto emit = [&](uint32_t op, uint32_t wd, uint32_t dst, uint32_t a = MG_NONE, uint32_t b = MG_NONE, uint32_t c = MG_NONE,
                     uint32_t p0 = 0, uint32_t p1 = 0) {
       VInstr v{op, wd, dst, a, b, c, p0, p1, {}};
       code.push_back(v);
@@ -363,9 +363,14 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
       }
       return vid[i];
     };
-    auto wid = [&](uint32_t i) { return nodes[i].width; };
+    uint32_t cur_node = 0;  // operands must precede the node that reads them
+    auto wid = [&](uint32_t x) {
+      if (x >= cur_node) fail(MG_E_INVALID, "operand does not precede its use");
+      return nodes[x].width;
+    };
 
     for (uint32_t i = 0; i < n_nodes; i++) {
+      cur_node = i;
       const Node& n = nodes[i];
       const uint32_t W = n.width;
       if (n.op >= MG_OP_COUNT) fail(MG_E_UNSUPPORTED, "unknown operator");
