@@ -248,7 +248,7 @@ int mg_eval_generated(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start
 int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags,
               uint64_t* first_hit, uint64_t* n_hits, uint32_t* assign_out);
 
-/* ---- JIT specialisation (hipRTC) ------------------------------------
+/* ---- JIT specialisation (comgr; hipRTC fallback) -----------------------
  * mg_jit_compile turns a loaded program into straight-line gfx950 code: with a
  * generator handle, the search kernel (mg_jit_search) specialised on it; with
  * gen = 0, the eval kernel (mg_jit_eval*).  It emits straight-line code (values in VGPRs, literals as immediates,
@@ -261,6 +261,14 @@ int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle);
 #define MG_JIT_GEN_VERDICTS 1u
 int mg_jit_compile_ex(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* jit_handle);
 int mg_jit_verdicts(uint64_t jit, uint64_t seed, uint64_t start, uint64_t n, uint8_t* verdict_out);
+/* Asynchronous compile on the engine's compile thread (outside the engine lock: searches on
+ * the interpreter keep launching meanwhile).  mg_jit_poll: *jit_handle = 0 while pending
+ * (wait_ms: 0 = do not wait, < 0 = wait until done); the ticket is consumed once it reports
+ * a handle or an error.  mg_jit_cancel drops a ticket (a finished kernel is freed, a pending
+ * one is discarded when it completes).  mg_jit_compile_ex = submit + wait. */
+int mg_jit_compile_async(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* ticket);
+int mg_jit_poll(uint64_t ticket, int32_t wait_ms, uint64_t* jit_handle);
+int mg_jit_cancel(uint64_t ticket);
 int mg_jit_info(uint64_t jit, double* compile_ms, int* blocks_per_cu);
 int mg_jit_free(uint64_t jit);
 int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags, uint64_t* first_hit,

@@ -17,6 +17,10 @@
 #include <algorithm>
 #include <chrono>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <list>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -664,10 +668,71 @@ struct DevJit {
   double compile_ms = 0;
 };
 
+// compiled code objects by source text, least recently used first out (MYTHGPU_JIT_CACHE
+// entries, default 64): JIT sources embed the query, so this only serves repeats
+struct CodeCache {
+  struct Entry {
+    std::string src;
+    std::vector<char> code;
+  };
+  std::list<Entry> lru;  // front = most recent
+  std::unordered_multimap<size_t, std::list<Entry>::iterator> idx;
+  size_t cap = 64;
+  const std::vector<char>* find(const std::string& src) {
+    const size_t h = std::hash<std::string>()(src);
+    auto r = idx.equal_range(h);
+    for (auto it = r.first; it != r.second; ++it)
+      if (it->second->src == src) {
+        lru.splice(lru.begin(), lru, it->second);
+        return &it->second->code;
+      }
+    return nullptr;
+  }
+  const std::vector<char>* insert(const std::string& src, std::vector<char>&& code) {
+    if (const auto* c = find(src)) return c;
+    lru.push_front(Entry{src, std::move(code)});
+    idx.emplace(std::hash<std::string>()(src), lru.begin());
+    while (lru.size() > cap) {
+      auto last = std::prev(lru.end());
+      auto r = idx.equal_range(std::hash<std::string>()(last->src));
+      for (auto it = r.first; it != r.second; ++it)
+        if (it->second == last) {
+          idx.erase(it);
+          break;
+        }
+      lru.erase(last);
+    }
+    return &lru.front().code;
+  }
+};
+
+// one JIT compile request: the inputs are copied at submission, so the caller may free
+// the program / generator meanwhile (the result is then dropped)
+struct JitTicket {
+  enum State { PENDING, DONE, FAILED } state = PENDING;
+  uint64_t prog = 0, gen = 0;
+  uint32_t flags = 0;
+  Lowered low;
+  bool has_gen = false;
+  std::vector<GenSpec> specs;
+  std::vector<uint32_t> consts;
+  bool cancelled = false;
+  uint64_t jit = 0;
+  int rc = MG_OK;
+  std::string err;
+};
+
 struct Engine {
   std::mutex mu;
   std::unordered_map<uint64_t, std::unique_ptr<DevJit>> jits;
-  std::unordered_map<std::string, std::vector<char>> code_cache;  // JIT source -> code object
+  CodeCache code_cache;
+  // compile thread: hipRTC/comgr work runs off the caller's thread and outside `mu`, so
+  // searches keep launching while a query's kernel compiles (mg_jit_compile_async)
+  bool jit_worker_running = false;  // detached thread; never outlives the (leaked) Engine
+  bool jit_stop = false;
+  std::deque<std::shared_ptr<JitTicket>> jit_queue;
+  std::unordered_map<uint64_t, std::shared_ptr<JitTicket>> tickets;
+  std::condition_variable jit_cv, jit_done_cv;
   bool init = false;
   int device = -1;
   hipStream_t stream = nullptr;
@@ -689,8 +754,9 @@ struct Engine {
 };
 
 Engine& E() {
-  static Engine e;
-  return e;
+  // never destroyed: the detached JIT compile thread may still hold it at process exit
+  static Engine* e = new Engine;
+  return *e;
 }
 
 #define HIPCHK(x)                                                                  \
@@ -903,7 +969,18 @@ int mg_init(uint32_t device_mask) {
 
 void mg_shutdown(void) {
   Engine& e = E();
-  std::lock_guard<std::mutex> g(e.mu);
+  std::unique_lock<std::mutex> g(e.mu);
+  // stop the compile thread (a compile in flight finishes first; its result is dropped)
+  e.jit_stop = true;
+  for (auto& t : e.jit_queue) t->cancelled = true;
+  for (auto& kv : e.tickets) kv.second->cancelled = true;
+  e.jit_cv.notify_all();
+  e.jit_done_cv.wait(g, [&] { return !e.jit_worker_running; });
+  e.jit_stop = false;
+  e.jit_queue.clear();
+  e.tickets.clear();
+  for (auto& kv : e.jits) (void)hipModuleUnload(kv.second->mod);
+  e.jits.clear();
   if (!e.init) return;
   for (auto& kv : e.progs) free_code(e, *kv.second);
   e.progs.clear();
@@ -1342,43 +1419,18 @@ int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_bl
 
 int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle) { return mg_jit_compile_ex(prog, gen, 0, jit_handle); }
 
-int mg_jit_compile_ex(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* jit_handle) {
-  Engine& e = E();
-  std::lock_guard<std::mutex> g(e.mu);
-  DevProgram* p = find_prog(e, prog);
-  if (!p) return set_err(MG_E_INVALID, "bad program handle");
-  DevGen* gp = nullptr;
-  if (gen) {
-    auto it = e.gens.find(gen);
-    if (it == e.gens.end() || it->second->prog != prog) return set_err(MG_E_INVALID, "bad generator handle");
-    gp = it->second.get();
-  }
-  // with a generator: the search kernel specialised on it; without: the eval kernel
-  std::string src;
-  if (gp) {
-    src = jit_source(gp->spec.low, &gp->specs, &gp->consts, JIT_SEARCH | ((flags & MG_JIT_GEN_VERDICTS) ? JIT_GEN : 0u));
-  } else {
-    Lowered ev;
-    std::string err;
-    int rc = specialize_program(p->low, nullptr, nullptr, ev, err);
-    if (rc) return set_err(rc, err);
-    src = jit_source(ev, nullptr, nullptr, JIT_EVAL);
-  }
-  auto t0 = std::chrono::steady_clock::now();
-  auto hit = e.code_cache.find(src);
-  if (hit == e.code_cache.end()) {
-    std::vector<char> code;
-    std::string log;
-    int rc = jit_compile(src, code, log);
-    if (rc) return set_err(rc, "JIT compile failed: " + log.substr(0, 4000));
-    hit = e.code_cache.emplace(src, std::move(code)).first;
-  }
+}  // extern "C"
+
+namespace mg {
+
+// load a code object as a DevJit (caller holds e.mu); returns the jit handle
+static int load_jit(Engine& e, const std::vector<char>& code, const JitTicket& t, double compile_ms, uint64_t* out) {
   auto j = std::make_unique<DevJit>();
-  HIPCHK(hipModuleLoadData(&j->mod, hit->second.data()));
+  HIPCHK(hipModuleLoadData(&j->mod, code.data()));
   int nb = 0;
-  if (gp) {
+  if (t.has_gen) {
     HIPCHK(hipModuleGetFunction(&j->fsearch, j->mod, "mgj_search"));
-    if (flags & MG_JIT_GEN_VERDICTS) HIPCHK(hipModuleGetFunction(&j->fgen, j->mod, "mgj_gen"));
+    if (t.flags & MG_JIT_GEN_VERDICTS) HIPCHK(hipModuleGetFunction(&j->fgen, j->mod, "mgj_gen"));
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, j->fsearch, 256, 0) == hipSuccess && nb > 0)
       j->nb_search = nb;
   } else {
@@ -1386,12 +1438,168 @@ int mg_jit_compile_ex(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* jit
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, j->feval, 256, 0) == hipSuccess && nb > 0)
       j->nb_eval = nb;
   }
-  j->prog = prog;
-  j->gen = gen;
-  j->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  j->prog = t.prog;
+  j->gen = t.gen;
+  j->compile_ms = compile_ms;
   const uint64_t h = e.next_handle++;
   e.jits[h] = std::move(j);
-  *jit_handle = h;
+  *out = h;
+  return MG_OK;
+}
+
+static void jit_worker_main(Engine* ep) {
+  Engine& e = *ep;
+  bool dev_set = false;
+  std::unique_lock<std::mutex> lk(e.mu);
+  for (;;) {
+    e.jit_cv.wait(lk, [&] { return e.jit_stop || !e.jit_queue.empty(); });
+    if (e.jit_stop) {
+      e.jit_worker_running = false;
+      e.jit_done_cv.notify_all();
+      return;
+    }
+    std::shared_ptr<JitTicket> t = e.jit_queue.front();
+    e.jit_queue.pop_front();
+    if (t->cancelled) continue;
+    if (!dev_set && e.init) {
+      (void)hipSetDevice(e.device);
+      dev_set = true;
+    }
+    lk.unlock();
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t kernels = t->has_gen ? (JIT_SEARCH | ((t->flags & MG_JIT_GEN_VERDICTS) ? JIT_GEN : 0u)) : JIT_EVAL;
+    const std::string src = t->has_gen ? jit_source(t->low, &t->specs, &t->consts, kernels)
+                                       : jit_source(t->low, nullptr, nullptr, kernels);
+    lk.lock();
+    const std::vector<char>* code = e.code_cache.find(src);
+    int rc = MG_OK;
+    std::string log;
+    if (!code) {
+      lk.unlock();
+      std::vector<char> obj;
+      rc = jit_compile(src, obj, log);
+      lk.lock();
+      if (rc == MG_OK) code = e.code_cache.insert(src, std::move(obj));
+    }
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (rc != MG_OK) {
+      t->rc = rc;
+      t->err = "JIT compile failed: " + log.substr(0, 4000);
+      t->state = JitTicket::FAILED;
+    } else if (t->cancelled) {
+      t->state = JitTicket::FAILED;
+      t->rc = MG_E_INVALID;
+      t->err = "cancelled";
+    } else if (!e.progs.count(t->prog) || (t->has_gen && !e.gens.count(t->gen))) {
+      t->state = JitTicket::FAILED;
+      t->rc = MG_E_INVALID;
+      t->err = "program or generator freed before its JIT kernel was ready";
+    } else {
+      rc = load_jit(e, *code, *t, ms, &t->jit);
+      if (rc != MG_OK) {
+        t->rc = rc;
+        t->err = g_err;
+        t->state = JitTicket::FAILED;
+      } else {
+        t->state = JitTicket::DONE;
+      }
+    }
+    e.jit_done_cv.notify_all();
+  }
+}
+
+// caller holds e.mu
+static int submit_jit(Engine& e, uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* ticket) {
+  DevProgram* p = find_prog(e, prog);
+  if (!p) return set_err(MG_E_INVALID, "bad program handle");
+  auto t = std::make_shared<JitTicket>();
+  t->prog = prog;
+  t->gen = gen;
+  t->flags = flags;
+  if (gen) {
+    auto it = e.gens.find(gen);
+    if (it == e.gens.end() || it->second->prog != prog) return set_err(MG_E_INVALID, "bad generator handle");
+    // with a generator: the search kernel on its specialised program
+    t->low = it->second->spec.low;
+    t->specs = it->second->specs;
+    t->consts = it->second->consts;
+    t->has_gen = true;
+  } else {
+    // without: the eval kernel
+    std::string err;
+    int rc = specialize_program(p->low, nullptr, nullptr, t->low, err);
+    if (rc) return set_err(rc, err);
+  }
+  if (!e.jit_worker_running) {
+    if (const char* c = getenv("MYTHGPU_JIT_CACHE")) e.code_cache.cap = std::max(1, atoi(c));
+    std::thread(jit_worker_main, &e).detach();
+    e.jit_worker_running = true;
+  }
+  const uint64_t h = e.next_handle++;
+  e.tickets[h] = t;
+  e.jit_queue.push_back(t);
+  e.jit_cv.notify_one();
+  *ticket = h;
+  return MG_OK;
+}
+
+// caller holds lk on e.mu; wait_ms < 0: until done
+static int poll_jit(Engine& e, std::unique_lock<std::mutex>& lk, uint64_t ticket, int64_t wait_ms, uint64_t* jit) {
+  auto it = e.tickets.find(ticket);
+  if (it == e.tickets.end()) return set_err(MG_E_INVALID, "bad JIT ticket");
+  std::shared_ptr<JitTicket> t = it->second;
+  auto ready = [&] { return t->state != JitTicket::PENDING; };
+  if (wait_ms < 0) e.jit_done_cv.wait(lk, ready);
+  else if (wait_ms > 0) e.jit_done_cv.wait_for(lk, std::chrono::milliseconds(wait_ms), ready);
+  *jit = 0;
+  if (t->state == JitTicket::PENDING) return MG_OK;
+  e.tickets.erase(ticket);
+  if (t->state == JitTicket::FAILED) return set_err(t->rc ? t->rc : MG_E_HIP, t->err);
+  *jit = t->jit;
+  return MG_OK;
+}
+
+}  // namespace mg
+
+extern "C" {
+
+int mg_jit_compile_ex(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* jit_handle) {
+  Engine& e = E();
+  std::unique_lock<std::mutex> lk(e.mu);
+  uint64_t ticket = 0;
+  int rc = submit_jit(e, prog, gen, flags, &ticket);
+  if (rc) return rc;
+  return poll_jit(e, lk, ticket, -1, jit_handle);
+}
+
+int mg_jit_compile_async(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* ticket) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  return submit_jit(e, prog, gen, flags, ticket);
+}
+
+int mg_jit_poll(uint64_t ticket, int32_t wait_ms, uint64_t* jit_handle) {
+  Engine& e = E();
+  std::unique_lock<std::mutex> lk(e.mu);
+  return poll_jit(e, lk, ticket, wait_ms, jit_handle);
+}
+
+int mg_jit_cancel(uint64_t ticket) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  auto it = e.tickets.find(ticket);
+  if (it == e.tickets.end()) return set_err(MG_E_INVALID, "bad JIT ticket");
+  std::shared_ptr<JitTicket> t = it->second;
+  e.tickets.erase(it);
+  if (t->state == JitTicket::PENDING) {
+    t->cancelled = true;  // the worker drops it (before compiling if still queued)
+  } else if (t->state == JitTicket::DONE) {
+    auto j = e.jits.find(t->jit);
+    if (j != e.jits.end()) {
+      (void)hipModuleUnload(j->second->mod);
+      e.jits.erase(j);
+    }
+  }
   return MG_OK;
 }
 

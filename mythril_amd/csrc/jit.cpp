@@ -7,6 +7,11 @@
 
 #include <dlfcn.h>
 
+#include <amd_comgr/amd_comgr.h>
+
+#include <chrono>
+#include <mutex>
+
 #include <cstdio>
 #include <map>
 #include <cstdlib>
@@ -669,9 +674,182 @@ Rtc& rtc() {
   r.ok = r.create && r.compile && r.log_size && r.log && r.code_size && r.code && r.destroy;
   return r;
 }
-}  // namespace
 
-int jit_compile(const std::string& src, std::vector<char>& code, std::string& log) {
+// ---------------------------------------------------------------------------
+// comgr (the compiler library hipRTC itself drives), called directly: source -> LLVM
+// bitcode -> relocatable -> code object, with no hipRTC runtime header to parse and no
+// device libraries to link (the kernels call none).  About half of hipRTC's latency per
+// query kernel on this image; hipRTC stays as the fallback (MYTHGPU_JIT_COMPILER=hiprtc).
+// ---------------------------------------------------------------------------
+struct Comgr {
+  void* h = nullptr;
+  decltype(&amd_comgr_create_data) create_data = nullptr;
+  decltype(&amd_comgr_set_data) set_data = nullptr;
+  decltype(&amd_comgr_set_data_name) set_data_name = nullptr;
+  decltype(&amd_comgr_release_data) release_data = nullptr;
+  decltype(&amd_comgr_get_data) get_data = nullptr;
+  decltype(&amd_comgr_create_data_set) create_set = nullptr;
+  decltype(&amd_comgr_destroy_data_set) destroy_set = nullptr;
+  decltype(&amd_comgr_data_set_add) set_add = nullptr;
+  decltype(&amd_comgr_action_data_count) data_count = nullptr;
+  decltype(&amd_comgr_action_data_get_data) data_get = nullptr;
+  decltype(&amd_comgr_create_action_info) create_info = nullptr;
+  decltype(&amd_comgr_destroy_action_info) destroy_info = nullptr;
+  decltype(&amd_comgr_action_info_set_language) set_language = nullptr;
+  decltype(&amd_comgr_action_info_set_isa_name) set_isa = nullptr;
+  decltype(&amd_comgr_action_info_set_option_list) set_options = nullptr;
+  decltype(&amd_comgr_action_info_set_logging) set_logging = nullptr;
+  decltype(&amd_comgr_do_action) do_action = nullptr;
+  bool ok = false;
+};
+
+Comgr& comgr() {
+  static Comgr c;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    // fresh link namespace: torch bundles an older comgr under the same soname
+    c.h = dlmopen(LM_ID_NEWLM, "/opt/rocm/lib/libamd_comgr.so.3", RTLD_NOW | RTLD_LOCAL);
+    if (!c.h) c.h = dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_LOCAL);
+    if (!c.h) return;
+#define MG_SYM(field, name) c.field = (decltype(c.field))dlsym(c.h, #name)
+    MG_SYM(create_data, amd_comgr_create_data);
+    MG_SYM(set_data, amd_comgr_set_data);
+    MG_SYM(set_data_name, amd_comgr_set_data_name);
+    MG_SYM(release_data, amd_comgr_release_data);
+    MG_SYM(get_data, amd_comgr_get_data);
+    MG_SYM(create_set, amd_comgr_create_data_set);
+    MG_SYM(destroy_set, amd_comgr_destroy_data_set);
+    MG_SYM(set_add, amd_comgr_data_set_add);
+    MG_SYM(data_count, amd_comgr_action_data_count);
+    MG_SYM(data_get, amd_comgr_action_data_get_data);
+    MG_SYM(create_info, amd_comgr_create_action_info);
+    MG_SYM(destroy_info, amd_comgr_destroy_action_info);
+    MG_SYM(set_language, amd_comgr_action_info_set_language);
+    MG_SYM(set_isa, amd_comgr_action_info_set_isa_name);
+    MG_SYM(set_options, amd_comgr_action_info_set_option_list);
+    MG_SYM(set_logging, amd_comgr_action_info_set_logging);
+    MG_SYM(do_action, amd_comgr_do_action);
+#undef MG_SYM
+    c.ok = c.create_data && c.set_data && c.set_data_name && c.release_data && c.get_data && c.create_set &&
+           c.destroy_set && c.set_add && c.data_count && c.data_get && c.create_info && c.destroy_info &&
+           c.set_language && c.set_isa && c.set_options && c.set_logging && c.do_action;
+  });
+  return c;
+}
+
+// what hipRTC's runtime header would provide, reduced to what the JIT kernels use
+const char* kComgrShim = R"MGJ(
+#define __device__ __attribute__((device))
+#define __host__ __attribute__((host))
+#define __global__ __attribute__((global))
+#define __shared__ __attribute__((shared))
+#define __constant__ __attribute__((constant))
+#define __forceinline__ inline __attribute__((always_inline))
+__device__ inline unsigned long long __ballot(int p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ inline int __ffsll(unsigned long long x) { return x ? __builtin_ctzll(x) + 1 : 0; }
+__device__ inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
+__device__ inline unsigned long long atomicMin(unsigned long long* p, unsigned long long v) {
+  return __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+)MGJ";
+
+const std::vector<std::string>& extra_options() {
+  // MYTHGPU_JIT_EXTRA: extra space-separated compiler options (tuning experiments)
+  static std::vector<std::string> extra;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    if (const char* e = getenv("MYTHGPU_JIT_EXTRA")) {
+      std::istringstream is(e);
+      std::string t;
+      while (is >> t) extra.push_back(t);
+    }
+  });
+  return extra;
+}
+
+// MYTHGPU_JIT_OPT: optimisation level (default -O3)
+std::string opt_level() { return std::string("-O") + (getenv("MYTHGPU_JIT_OPT") ? getenv("MYTHGPU_JIT_OPT") : "3"); }
+
+int comgr_compile(const std::string& src, std::vector<char>& code, std::string& log) {
+  Comgr& c = comgr();
+  const std::string full = std::string(kComgrShim) + src;
+  const std::string optlvl = opt_level();
+  std::vector<const char*> opts = {optlvl.c_str(), "-std=c++17", "-nogpuinc", "-nogpulib", "-Wno-unused-variable",
+                                   "-Wno-uninitialized", "-Wno-sometimes-uninitialized"};
+  for (const auto& t : extra_options()) opts.push_back(t.c_str());
+  amd_comgr_data_t src_d{0};
+  amd_comgr_data_set_t in{0}, bc{0}, rel{0}, exe{0};
+  amd_comgr_action_info_t ai{0};
+  int rc = MG_E_HIP;
+  auto collect_log = [&](amd_comgr_data_set_t set) {
+    size_t n = 0;
+    if (c.data_count(set, AMD_COMGR_DATA_KIND_LOG, &n) != AMD_COMGR_STATUS_SUCCESS) return;
+    for (size_t i = 0; i < n; i++) {
+      amd_comgr_data_t d;
+      if (c.data_get(set, AMD_COMGR_DATA_KIND_LOG, i, &d) != AMD_COMGR_STATUS_SUCCESS) continue;
+      size_t sz = 0;
+      if (c.get_data(d, &sz, nullptr) == AMD_COMGR_STATUS_SUCCESS && sz > 1) {
+        std::string t(sz, '\0');
+        c.get_data(d, &sz, &t[0]);
+        log += t;
+      }
+      c.release_data(d);
+    }
+  };
+  do {
+    if (c.create_data(AMD_COMGR_DATA_KIND_SOURCE, &src_d) || c.set_data(src_d, full.size(), full.data()) ||
+        c.set_data_name(src_d, "mythgpu_jit.hip"))
+      break;
+    if (c.create_set(&in) || c.create_set(&bc) || c.create_set(&rel) || c.create_set(&exe) || c.set_add(in, src_d)) break;
+    if (c.create_info(&ai) || c.set_language(ai, AMD_COMGR_LANGUAGE_HIP) ||
+        c.set_isa(ai, "amdgcn-amd-amdhsa--gfx950") || c.set_options(ai, opts.data(), opts.size()) ||
+        c.set_logging(ai, true))
+      break;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (c.do_action(AMD_COMGR_ACTION_COMPILE_SOURCE_TO_BC, ai, in, bc)) {
+      collect_log(bc);
+      break;
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    if (c.do_action(AMD_COMGR_ACTION_CODEGEN_BC_TO_RELOCATABLE, ai, bc, rel)) {
+      collect_log(rel);
+      break;
+    }
+    const auto t2 = std::chrono::steady_clock::now();
+    if (c.do_action(AMD_COMGR_ACTION_LINK_RELOCATABLE_TO_EXECUTABLE, ai, rel, exe)) {
+      collect_log(exe);
+      break;
+    }
+    if (getenv("MYTHGPU_JIT_TIMING")) {
+      const auto t3 = std::chrono::steady_clock::now();
+      auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+      fprintf(stderr, "mythgpu jit: %zu bytes source, front+opt %.1f ms, codegen %.1f ms, link %.1f ms\n",
+              full.size(), ms(t0, t1), ms(t1, t2), ms(t2, t3));
+    }
+    size_t n = 0;
+    amd_comgr_data_t o;
+    if (c.data_count(exe, AMD_COMGR_DATA_KIND_EXECUTABLE, &n) || n != 1 ||
+        c.data_get(exe, AMD_COMGR_DATA_KIND_EXECUTABLE, 0, &o))
+      break;
+    size_t sz = 0;
+    if (c.get_data(o, &sz, nullptr) == AMD_COMGR_STATUS_SUCCESS && sz) {
+      code.resize(sz);
+      if (c.get_data(o, &sz, code.data()) == AMD_COMGR_STATUS_SUCCESS) rc = MG_OK;
+    }
+    c.release_data(o);
+  } while (false);
+  if (ai.handle) c.destroy_info(ai);
+  for (amd_comgr_data_set_t s : {in, bc, rel, exe})
+    if (s.handle) c.destroy_set(s);
+  if (src_d.handle) c.release_data(src_d);
+  if (rc != MG_OK && log.empty()) log = "comgr compile failed";
+  return rc;
+}
+
+int hiprtc_compile(const std::string& src, std::vector<char>& code, std::string& log) {
   Rtc& r = rtc();
   if (!r.ok) {
     log = "hipRTC not available";
@@ -682,22 +860,10 @@ int jit_compile(const std::string& src, std::vector<char>& code, std::string& lo
     log = "hiprtcCreateProgram failed";
     return MG_E_HIP;
   }
-  // MYTHGPU_JIT_OPT: optimisation level (default -O3)
-  static std::string optlvl = std::string("-O") + (getenv("MYTHGPU_JIT_OPT") ? getenv("MYTHGPU_JIT_OPT") : "3");
+  const std::string optlvl = opt_level();
   std::vector<const char*> opts = {"--offload-arch=gfx950", optlvl.c_str(), "-std=c++17", "-nogpuinc", "-nogpulib",
                                    "-Wno-unused-variable", "-Wno-uninitialized", "-Wno-sometimes-uninitialized"};
-  // MYTHGPU_JIT_EXTRA: extra space-separated hipRTC options (tuning experiments)
-  static std::vector<std::string> extra;
-  static bool extra_init = false;
-  if (!extra_init) {
-    extra_init = true;
-    if (const char* e = getenv("MYTHGPU_JIT_EXTRA")) {
-      std::istringstream is(e);
-      std::string t;
-      while (is >> t) extra.push_back(t);
-    }
-  }
-  for (const auto& t : extra) opts.push_back(t.c_str());
+  for (const auto& t : extra_options()) opts.push_back(t.c_str());
   int rc = r.compile(prog, (int)opts.size(), opts.data());
   size_t ls = 0;
   r.log_size(prog, &ls);
@@ -714,6 +880,20 @@ int jit_compile(const std::string& src, std::vector<char>& code, std::string& lo
   code.resize(cs);
   r.code(prog, code.data());
   r.destroy(&prog);
+  return MG_OK;
+}
+}  // namespace
+
+int jit_compile(const std::string& src, std::vector<char>& code, std::string& log) {
+  const char* which = getenv("MYTHGPU_JIT_COMPILER");
+  const bool use_rtc = which && std::strcmp(which, "hiprtc") == 0;
+  int rc;
+  if (!use_rtc && comgr().ok) {
+    rc = comgr_compile(src, code, log);
+  } else {
+    rc = hiprtc_compile(src, code, log);
+  }
+  if (rc != MG_OK) return rc;
   // MYTHGPU_JIT_DUMP=<prefix>: keep the source and code object for offline disassembly
   if (const char* dump = getenv("MYTHGPU_JIT_DUMP")) {
     const std::string base(dump);

@@ -121,7 +121,7 @@ class KeccakFunctionManager:
 
 
 def replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], model, km: KeccakFunctionManager,
-                            code=None, evaluate=None) -> None:
+                            code=None, evaluate=None, bvv=None) -> None:
     """``mythril/analysis/solver.py:119-152`` on the engine: every 64-hex-digit
     slice of a printed transaction input that is a stored interval hash (it
     contains ``hash_matcher``) is replaced by the real Keccak-256 of its
@@ -132,6 +132,7 @@ def replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], model, 
     batch and hashed in one ``mg_keccak256`` launch up front; a slice that only
     appears after an earlier replacement is evaluated and hashed on demand."""
     evaluate = evaluate or (lambda terms: model.eval_many(terms, model_completion=False))
+    bvv = bvv or symbol_factory.BitVecVal  # LASER's factory when driving LASER's manager
     concrete_hashes = km.get_concrete_hash_data(model, evaluate)
     bytecode = getattr(code, "bytecode", None)
 
@@ -144,11 +145,11 @@ def replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], model, 
             for size in concrete_hashes:
                 if w in concrete_hashes[size]:  # the reference keeps the LAST matching size
                     _, inverse = km.store_function[size]
-                    todo.append(inverse(symbol_factory.BitVecVal(w, 256)).raw)
+                    todo.append(inverse(bvv(w, 256)).raw)
                     keys.append((w, size))
         res: Dict[int, BitVec] = {}
         for (w, size), v in zip(keys, evaluate(todo) if todo else []):
-            res[w] = symbol_factory.BitVecVal(v.as_long(), size)
+            res[w] = bvv(v.as_long(), size)
         return res
 
     def scan(inp: str, s_index: int) -> List[int]:

@@ -33,6 +33,7 @@ EXPORTS = [
     "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_info", "mg_gen_free", "mg_eval", "mg_eval_dev",
     "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
     "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_jit_compile", "mg_jit_compile_ex", "mg_jit_verdicts", "mg_jit_info",
+    "mg_jit_compile_async", "mg_jit_poll", "mg_jit_cancel",
     "mg_jit_free", "mg_jit_search", "mg_jit_eval", "mg_jit_eval_dev",
 ]
 
@@ -111,6 +112,9 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_jit_compile_ex": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, u64p]),
             "mg_jit_verdicts": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, u8p]),
             "mg_jit_info": (C.c_int, [C.c_uint64, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+            "mg_jit_compile_async": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, u64p]),
+            "mg_jit_poll": (C.c_int, [C.c_uint64, C.c_int32, u64p]),
+            "mg_jit_cancel": (C.c_int, [C.c_uint64]),
             "mg_jit_free": (C.c_int, [C.c_uint64]),
             "mg_jit_search": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u64p, u64p, u32p]),
             "mg_jit_eval": (C.c_int, [C.c_uint64, u32p, C.c_uint64, u8p, u32p]),
@@ -254,6 +258,22 @@ class Engine:
         h = C.c_uint64()
         _check(self.lib.mg_jit_compile_ex(prog, gen, 1 if gen_verdicts else 0, C.byref(h)))
         return h.value
+
+    def jit_compile_async(self, prog: int, gen: int = 0, gen_verdicts: bool = False) -> int:
+        """Start compiling on the engine's compile thread; returns a ticket for :meth:`jit_poll`."""
+        t = C.c_uint64()
+        _check(self.lib.mg_jit_compile_async(prog, gen, 1 if gen_verdicts else 0, C.byref(t)))
+        return t.value
+
+    def jit_poll(self, ticket: int, wait_ms: int = 0) -> Optional[int]:
+        """The JIT handle once the compile is done (the ticket is then consumed), else None.
+        A failed compile raises (and consumes the ticket)."""
+        h = C.c_uint64()
+        _check(self.lib.mg_jit_poll(ticket, wait_ms, C.byref(h)))
+        return h.value or None
+
+    def jit_cancel(self, ticket: int) -> None:
+        _check(self.lib.mg_jit_cancel(ticket))
 
     def jit_verdicts(self, jit: int, seed: int, start: int, n: int) -> np.ndarray:
         """Per-candidate verdicts of the JIT kernel (compiled with ``gen_verdicts``)."""

@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import logging
 import os
+import time
 from functools import lru_cache
 
 log = logging.getLogger("mythgpu")
@@ -69,14 +70,45 @@ class HookStats:
         self.fallbacks = 0
         self.unsupported = 0
         self.errors = 0
+        self.rejected = 0      # GPU models z3 did not confirm (kept on z3)
+        self.candidates = 0    # candidate assignments the GPU evaluated
+        self.gpu_time = 0.0    # seconds inside the GPU attempt (hits and misses)
 
     def __repr__(self):
         return (f"mythgpu: {self.queries} queries, {self.gpu_models} GPU models, {self.fallbacks} to z3 "
-                f"({self.unsupported} unsupported, {self.errors} errors)")
+                f"({self.unsupported} unsupported, {self.errors} errors, {self.rejected} rejected), "
+                f"{self.candidates} candidates in {self.gpu_time:.3f} s")
 
 
 STATS = HookStats()
 _ORIGINAL = None
+_ORIGINAL_SHA = None
+
+
+def _solver_statistics():
+    """LASER's ``SolverStatistics`` singleton (``laser/smt/solver/solver_statistics.py:29-45``),
+    or None without Mythril."""
+    try:
+        from mythril.laser.smt.solver.solver_statistics import SolverStatistics  # type: ignore
+    except Exception:
+        return None
+    return SolverStatistics()
+
+
+def _record(dt: float, gpu_model: bool) -> None:
+    """Feed the hook's work into LASER's ``SolverStatistics`` (what ``--solver-log`` /
+    the statistics report print): a query the GPU answered never reaches the
+    ``stat_smt_query``-wrapped z3 check, so it is counted here, with its time; the GPU
+    counters ride along as extra attributes of the same singleton."""
+    st = _solver_statistics()
+    if st is None:
+        return
+    if gpu_model and getattr(st, "enabled", False):
+        st.query_count += 1
+        st.solver_time += dt
+    st.gpu_models = STATS.gpu_models
+    st.gpu_candidates = STATS.candidates
+    st.gpu_time = STATS.gpu_time
 
 
 def gpu_first(original):
@@ -88,6 +120,7 @@ def gpu_first(original):
         if minimize or maximize or os.environ.get("MYTHGPU_DISABLE") == "1":
             return original(constraints, minimize, maximize, enforce_execution_time)
         model = None
+        t0 = time.perf_counter()
         try:
             model = _try_gpu(constraints, enforce_execution_time)
         except Exception as e:  # never raise a new exception type into LASER
@@ -98,8 +131,12 @@ def gpu_first(original):
             else:
                 STATS.errors += 1
                 log.debug("mythgpu: engine error, falling back to z3: %s", e)
+        dt = time.perf_counter() - t0
+        STATS.gpu_time += dt
         if model is not None:
             STATS.gpu_models += 1
+        _record(dt, model is not None)
+        if model is not None:
             return model
         STATS.fallbacks += 1
         return original(constraints, minimize, maximize, enforce_execution_time)
@@ -109,6 +146,11 @@ def gpu_first(original):
 
 
 def _try_gpu(constraints, enforce_execution_time):
+    """One GPU attempt at ``get_model`` (``support/model.py:15-49``): the budget is the
+    smaller of the query's z3 budget (``args.solver_timeout``, minus the execution-time
+    reserve the reference keeps) and the hook's slice ``MYTHGPU_BUDGET_MS``; the search
+    escalates to the compiled kernel inside it (``search.search``, async compile).  A hit
+    is re-checked by z3 (``pin_model``) with what is left of the query's z3 budget."""
     from mythril.laser.ethereum.time_handler import time_handler  # type: ignore
     from mythril.laser.smt import Model  # type: ignore
     from mythril.support.support_args import args  # type: ignore
@@ -117,18 +159,21 @@ def _try_gpu(constraints, enforce_execution_time):
     from .native import Engine
     from .search import search_partitioned
 
+    t0 = time.perf_counter()
     if any(type(c) == bool and not c for c in constraints):
         return None  # the original raises UnsatError for this
     cs = [c for c in constraints if type(c) != bool]
     if not cs:
         return None
-    budget = min(args.solver_timeout, float(os.environ.get("MYTHGPU_BUDGET_MS", "200")))
+    total = float(args.solver_timeout)
     if enforce_execution_time:
-        budget = min(budget, time_handler.time_remaining() - 500)
+        total = min(total, time_handler.time_remaining() - 500)
+    budget = min(total, float(os.environ.get("MYTHGPU_BUDGET_MS", "200")))
     if budget <= 0:
         return None
     terms = z3bridge.to_terms(cs)
-    res = search_partitioned(Engine.get(), terms, timeout_s=budget / 1000.0, max_candidates=1 << 34)
+    res = search_partitioned(Engine.get(), terms, timeout_s=budget / 1000.0, max_candidates=1 << 40)
+    STATS.candidates += res.scanned
     if res.index is None:
         return None
     ver, scalars, arrays, funcs, _ = res.model
@@ -136,11 +181,47 @@ def _try_gpu(constraints, enforce_execution_time):
         return None
     from .solver import Model as GpuModel
 
-    z3m = z3bridge.pin_model(cs, GpuModel(scalars, arrays, funcs))
+    left_ms = total - (time.perf_counter() - t0) * 1e3
+    if left_ms <= 0:
+        return None
+    z3m = z3bridge.pin_model(cs, GpuModel(scalars, arrays, funcs), timeout_ms=left_ms)
     if z3m is None:
-        log.warning("mythgpu: z3 rejected a GPU model (kept on z3)")
+        STATS.rejected += 1
+        log.warning("mythgpu: z3 did not confirm a GPU model (kept on z3)")
         return None
     return Model([z3m])
+
+
+def batched_replace_with_actual_sha(concrete_transactions, model, code=None):
+    """Drop-in for ``mythril.analysis.solver._replace_with_actual_sha`` (``analysis/solver.py:119-152``):
+    the same scan and in-place replacements, with every preimage's Keccak-256 computed in one
+    ``mg_keccak256`` launch instead of one ``sha3`` call per slice (``keccak_model.replace_with_actual_sha``)."""
+    from mythril.laser.ethereum.keccak_function_manager import keccak_function_manager  # type: ignore
+    from mythril.laser.smt import symbol_factory  # type: ignore
+
+    from .keccak_model import replace_with_actual_sha
+    from .native import Engine
+
+    class _Manager:
+        """LASER's manager, with the hashing moved to the GPU."""
+
+        store_function = keccak_function_manager.store_function
+
+        @staticmethod
+        def get_concrete_hash_data(m, evaluate=None):
+            return keccak_function_manager.get_concrete_hash_data(m)
+
+        @staticmethod
+        def find_concrete_keccaks(datas):
+            digests = Engine.get().keccak256([d.value.to_bytes(d.size() // 8, "big") for d in datas])
+            return [symbol_factory.BitVecVal(int.from_bytes(h, "big"), 256) for h in digests]
+
+        @classmethod
+        def find_concrete_keccak(cls, data):
+            return cls.find_concrete_keccaks([data])[0]
+
+    replace_with_actual_sha(concrete_transactions, model, _Manager, code=code,
+                            evaluate=lambda terms: [model.eval(t) for t in terms], bvv=symbol_factory.BitVecVal)
 
 
 def install() -> bool:
@@ -152,6 +233,7 @@ def install() -> bool:
     import mythril.laser.ethereum.state.constraints as constraints_mod  # type: ignore
     import mythril.support.model as model_mod  # type: ignore
 
+    global _ORIGINAL_SHA
     if _ORIGINAL is not None:
         return True
     _ORIGINAL = model_mod.get_model
@@ -159,11 +241,15 @@ def install() -> bool:
     model_mod.get_model = hooked
     constraints_mod.get_model = hooked
     an_solver.get_model = hooked
+    # the transaction printer's Keccak fix-up (analysis/solver.py:88-92 calls it by module name)
+    _ORIGINAL_SHA = getattr(an_solver, "_replace_with_actual_sha", None)
+    if _ORIGINAL_SHA is not None:
+        an_solver._replace_with_actual_sha = batched_replace_with_actual_sha
     return True
 
 
 def uninstall() -> None:
-    global _ORIGINAL
+    global _ORIGINAL, _ORIGINAL_SHA
     if _ORIGINAL is None or not HAVE_MYTHRIL:
         return
     import mythril.analysis.solver as an_solver  # type: ignore
@@ -171,7 +257,9 @@ def uninstall() -> None:
     import mythril.support.model as model_mod  # type: ignore
 
     model_mod.get_model = constraints_mod.get_model = an_solver.get_model = _ORIGINAL
-    _ORIGINAL = None
+    if _ORIGINAL_SHA is not None:
+        an_solver._replace_with_actual_sha = _ORIGINAL_SHA
+    _ORIGINAL = _ORIGINAL_SHA = None
 
 
 class MythgpuPlugin(LaserPlugin):

@@ -348,18 +348,34 @@ def model_from_assignment(P: ssa.Program, assign: np.ndarray):
     return ssa.model_from_sites(P, scal, keys, bases)
 
 
+# expected latency of one query-kernel compile (submit -> loadable module), seconds: an
+# exponential average of the compiles this process measured (cold value from the bench:
+# ~0.2 s on the MI355X box's host through hipRTC, less through comgr)
+JIT_COMPILE_S = [0.15]
+# while a compile is pending, interpreter launches are cut to about this long so the search
+# switches to the compiled kernel soon after it is ready
+JIT_POLL_S = 0.010
+# kernel that produced the last search's result ("interp" / "jit"), for stream statistics
+LAST_ENGINE = None
+
+
 def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int = 1 << 16,
            max_candidates: int = 1 << 26, timeout_s: float = 10.0, gen: Optional[GenBuilder] = None,
-           want_model: bool = True, jit: str = "auto", jit_cost_s: float = 0.5) -> SearchResult:
+           want_model: bool = True, jit: str = "auto", jit_cost_s: Optional[float] = None) -> SearchResult:
     """Find the lowest-index satisfying candidate (or give up: None).
 
-    ``jit``: "never" keeps the generic interpreter (``k_run``, no compile
-    latency); "always" compiles the query-specialised kernel first; "auto"
-    starts on the interpreter, and when the first chunk has no hit and more than
-    ``jit_cost_s`` of the budget is left, compiles the JIT kernel and continues the
-    SAME index stream on it.  Both kernels compute identical verdicts for every index
-    (``tests/test_gpu_jit.py``), so the first hit does not depend on the mode.  The
-    model comes back with the hit (``mg_search``'s ``assign_out``)."""
+    ``jit``: "never" keeps the generic interpreter (``k_run``, no compile latency);
+    "always" compiles the query-specialised kernel first; "auto" starts on the
+    interpreter and, when the first launch has no hit and the budget left exceeds the
+    expected compile latency (``jit_cost_s``, default: the measured average
+    ``JIT_COMPILE_S``), compiles the JIT kernel on the engine's compile thread
+    (``mg_jit_compile_async``) while the interpreter keeps scanning, then continues the
+    SAME index stream on the compiled kernel.  Both kernels compute identical verdicts for
+    every index (``tests/test_gpu_jit.py``), so the first hit does not depend on the mode.
+
+    Launch sizes grow geometrically from ``chunk`` (easy queries answer in the first
+    launch) and are capped by the measured rate so that a launch ends inside the budget.
+    The model comes back with the hit (``mg_search``'s ``assign_out``)."""
     tp = time.perf_counter()
     P, blob = prepare(roots, gen)
     th = time.perf_counter()
@@ -370,29 +386,52 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
     hit = None
     hits = 0
     used = "interp"
+    expected_compile = JIT_COMPILE_S[0] if jit_cost_s is None else jit_cost_s
     assign = np.zeros(max(P.watch_words, 1), dtype=np.uint32) if want_model else None
     try:
         gh = engine.load_gen(prog, blob)
         timing["load_ms"] = (time.perf_counter() - th) * 1e3
         jh = None
+        ticket = None
+        rate = None  # candidates/s of the kernel in use (last launch)
         try:
+            if jit == "always":
+                tc = time.perf_counter()
+                jh = engine.jit_compile(prog, gh)
+                timing["jit_compile_ms"] = (time.perf_counter() - tc) * 1e3
+                used = "jit"
             start = 0
-            while scanned < max_candidates and time.perf_counter() - t0 < timeout_s:
-                left = timeout_s - (time.perf_counter() - t0)
-                if jh is None and (jit == "always" or (jit == "auto" and scanned > 0 and left > jit_cost_s)):
+            while scanned < max_candidates:
+                now = time.perf_counter()
+                left = timeout_s - (now - t0)
+                if left <= 0:
+                    break
+                if ticket is not None:
                     try:
-                        tc = time.perf_counter()
-                        jh = engine.jit_compile(prog, gh)
-                        timing["jit_compile_ms"] = (time.perf_counter() - tc) * 1e3
-                        used = "jit"
+                        h = engine.jit_poll(ticket)
                     except Exception:  # JIT unavailable for this program: stay on the interpreter
-                        jit = "never"
-                    continue
+                        ticket, jit = None, "never"
+                        h = None
+                    if h is not None:
+                        ticket, jh, used, rate = None, h, "jit", None
+                        took = now - tc
+                        timing["jit_compile_ms"] = took * 1e3
+                        JIT_COMPILE_S[0] = 0.5 * JIT_COMPILE_S[0] + 0.5 * took
+                        chunk = max(chunk, 1 << 22)
+                if jh is None and ticket is None and jit == "auto" and scanned > 0 and left > 1.2 * expected_compile:
+                    tc = time.perf_counter()
+                    ticket = engine.jit_compile_async(prog, gh)
                 n = min(chunk, max_candidates - scanned)
+                if rate:
+                    cap_s = min(left, JIT_POLL_S) if ticket is not None else left
+                    n = max(1, min(n, int(rate * cap_s)))
+                tl = time.perf_counter()
                 if jh is not None:
                     idx, nh = engine.jit_search(jh, seed, start, n, early_exit=True, assign=assign)
                 else:
                     idx, nh = engine.search(prog, gh, seed, start, n, early_exit=True, assign=assign)
+                dt = time.perf_counter() - tl
+                rate = n / dt if dt > 0 else None
                 scanned += n
                 start += n
                 if idx is not None:
@@ -402,6 +441,8 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                 # then geometric growth amortises the launch + sync per chunk
                 chunk = min(chunk * 4, 1 << 26 if jh is None else 1 << 30)
         finally:
+            if ticket is not None:
+                engine.jit_cancel(ticket)
             if jh is not None:
                 engine.jit_free(jh)
             engine.free_gen(gh)
@@ -410,6 +451,8 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
     dt = time.perf_counter() - t0
     res = SearchResult(hit, hits, scanned, dt)
     res.engine = used
+    global LAST_ENGINE
+    LAST_ENGINE = used
     if hit is not None and want_model:
         # the search only reports indices whose verdict is 1
         tm = time.perf_counter()

@@ -160,12 +160,21 @@ def _convert(e, a: List[T.Term]) -> T.Term:
     raise Unsupported(f"z3 operator {decl.name()} (kind {decl.kind()})")
 
 
-def pin_model(constraints, model) -> "z3.ModelRef":
+def pin_model(constraints, model, timeout_ms=None):
     """Re-check a GPU model with z3 and return a real ``z3.ModelRef``: the original
     constraints plus equalities pinning every symbol the GPU assigned (scalars,
-    array table entries, function table entries).  Runs in a fresh solver."""
-    s = z3.Solver()
-    raws = [getattr(c, "raw", c) for c in constraints]
+    array table entries, function table entries).
+
+    Runs in a fresh ``z3.Context`` (the constraints are translated into it), so LASER's
+    main context and its solvers see no new assertions or declarations; the model is
+    translated back to the main context for ``Model.eval``.  ``timeout_ms`` bounds the
+    check (the caller passes what is left of the query's budget); ``unknown`` -> None,
+    and the caller falls back to the original z3 path."""
+    ctx = z3.Context()
+    s = z3.Solver(ctx=ctx)
+    if timeout_ms is not None:
+        s.set("timeout", max(1, int(timeout_ms)))
+    raws = [getattr(c, "raw", c).translate(ctx) for c in constraints]
     s.add(*raws)
     syms = {}
     for r in raws:
@@ -176,7 +185,7 @@ def pin_model(constraints, model) -> "z3.ModelRef":
         if d is None:
             continue
         rng = d.range()
-        s.add(d() == (z3.BoolVal(bool(v)) if rng.kind() == z3.Z3_BOOL_SORT else z3.BitVecVal(v, rng.size())))
+        s.add(d() == (z3.BoolVal(bool(v), ctx) if rng.kind() == z3.Z3_BOOL_SORT else z3.BitVecVal(v, rng.size(), ctx)))
     for name, (table, _) in model.arrays.items():
         d = syms.get(name)
         if d is None:
@@ -184,16 +193,16 @@ def pin_model(constraints, model) -> "z3.ModelRef":
         arr = d()
         dom, rng = arr.sort().domain().size(), arr.sort().range().size()
         for k, v in table.items():
-            s.add(z3.Select(arr, z3.BitVecVal(k, dom)) == z3.BitVecVal(v, rng))
+            s.add(z3.Select(arr, z3.BitVecVal(k, dom, ctx)) == z3.BitVecVal(v, rng, ctx))
     for name, (table, _) in model.funcs.items():
         d = syms.get(name)
         if d is None:
             continue
         for k, v in table.items():
-            s.add(d(z3.BitVecVal(k, d.domain(0).size())) == z3.BitVecVal(v, d.range().size()))
+            s.add(d(z3.BitVecVal(k, d.domain(0).size(), ctx)) == z3.BitVecVal(v, d.range().size(), ctx))
     if s.check() != z3.sat:
         return None
-    return s.model()
+    return s.model().translate(z3.main_ctx())
 
 
 def _declarations(e):

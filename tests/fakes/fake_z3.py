@@ -1,0 +1,579 @@
+"""Test double of the z3py surface the drop-in touches — z3 is not installed in this image.
+
+Covers what ``mythril_amd/z3bridge.py`` (to_terms, pin_model) and ``plugin._try_gpu``
+call: ``Z3_OP_*`` operator codes, sort kinds, ``decl()/kind()/params()/name()/arity()/
+domain()/range()``, ``arg()/num_args()/get_id()/sort()/size()/as_long()``,
+``is_bv_value/is_app``, ``Context/main_ctx`` and ``translate``, and ``Solver``
+(``add/set/check/model``) with ``ModelRef.eval/translate``.  Expressions are built with
+the z3py constructors LASER uses (``BitVec``, ``BitVecVal``, ``Array``, ``Function``,
+``If``, ``Concat``, ``Extract``, ``ULT`` …, operators on ``ExprRef``).
+
+The solver is a checker, not a decision procedure: ``check()`` reads the pins
+``pin_model`` adds (``const == value``, ``Select(arr, k) == v``, ``f(k) == v``), evaluates
+every assertion under them with its own evaluator (independent of the engine's oracle)
+and answers sat / unsat; ``Solver.FORCE`` makes it answer ``unknown`` (a z3 timeout).
+Every Solver records itself in ``Solver.instances`` (context, parameters) for the tests.
+"""
+from __future__ import annotations
+
+import itertools
+
+_ids = itertools.count(1)
+
+Z3_BOOL_SORT, Z3_BV_SORT, Z3_ARRAY_SORT = 1, 4, 5
+_OP_NAMES = ["TRUE", "FALSE", "EQ", "DISTINCT", "ITE", "AND", "OR", "IFF", "XOR", "NOT", "IMPLIES", "BNUM", "BNEG",
+             "BADD", "BSUB", "BMUL", "BSDIV", "BUDIV", "BSREM", "BUREM", "BSMOD", "ULEQ", "SLEQ", "UGEQ", "SGEQ", "ULT",
+             "SLT", "UGT", "SGT", "BAND", "BOR", "BNOT", "BXOR", "CONCAT", "SIGN_EXT", "ZERO_EXT", "EXTRACT", "BSHL",
+             "BLSHR", "BASHR", "BUMUL_NO_OVFL", "SELECT", "STORE", "CONST_ARRAY", "UNINTERPRETED", "BSDIV_I",
+             "BUDIV_I", "BSREM_I", "BUREM_I", "BSMOD_I", "ROTATE_LEFT"]
+for _i, _n in enumerate(_OP_NAMES):
+    globals()["Z3_OP_" + _n] = 0x100 + _i
+
+
+class Context:
+    def __init__(self):
+        self.id = next(_ids)
+
+
+_MAIN = Context()
+
+
+def main_ctx():
+    return _MAIN
+
+
+def _ctx(c):
+    return c if c is not None else _MAIN
+
+
+class SortRef:
+    def __init__(self, kind, size=None, dom=None, rng=None, ctx=None):
+        self._kind, self._size, self._dom, self._rng, self.ctx = kind, size, dom, rng, _ctx(ctx)
+
+    def kind(self):
+        return self._kind
+
+    def size(self):
+        return self._size
+
+    def domain(self):
+        return self._dom
+
+    def range(self):
+        return self._rng
+
+    def key(self):
+        return (self._kind, self._size, self._dom.key() if self._dom else None, self._rng.key() if self._rng else None)
+
+    def translate(self, ctx):
+        return SortRef(self._kind, self._size, self._dom and self._dom.translate(ctx),
+                       self._rng and self._rng.translate(ctx), ctx)
+
+
+def BitVecSort(n, ctx=None):
+    return SortRef(Z3_BV_SORT, n, ctx=ctx)
+
+
+def BoolSort(ctx=None):
+    return SortRef(Z3_BOOL_SORT, ctx=ctx)
+
+
+def ArraySort(d, r):
+    return SortRef(Z3_ARRAY_SORT, dom=d, rng=r, ctx=d.ctx)
+
+
+def RealSort(ctx=None):
+    return SortRef(99, ctx=ctx)
+
+
+class FuncDeclRef:
+    def __init__(self, name, kind, dom, rng, params=(), ctx=None):
+        self._name, self._kind, self._dom, self._rng, self._params = name, kind, list(dom), rng, list(params)
+        self.ctx = _ctx(ctx)
+
+    def name(self):
+        return self._name
+
+    def kind(self):
+        return self._kind
+
+    def params(self):
+        return list(self._params)
+
+    def arity(self):
+        return len(self._dom)
+
+    def domain(self, i):
+        return self._dom[i]
+
+    def range(self):
+        return self._rng
+
+    def __call__(self, *args):
+        return ExprRef(self, [_coerce(a, s) for a, s in zip(args, self._dom)], self.ctx)
+
+    def translate(self, ctx):
+        return FuncDeclRef(self._name, self._kind, [d.translate(ctx) for d in self._dom], self._rng.translate(ctx),
+                           self._params, ctx)
+
+
+def _coerce(a, sort):
+    if isinstance(a, ExprRef):
+        return a
+    if isinstance(a, bool):
+        return BoolVal(a, sort.ctx)
+    return BitVecVal(a, sort.size(), sort.ctx)
+
+
+def _op(kind, args, rng, params=(), name=None):
+    ctx = args[0].ctx if args else _MAIN
+    d = FuncDeclRef(name or str(kind), kind, [a.sort() for a in args], rng, params, ctx)
+    return ExprRef(d, list(args), ctx)
+
+
+class ExprRef:
+    def __init__(self, decl, args, ctx):
+        self._decl, self._args, self.ctx = decl, list(args), ctx
+        self._id = next(_ids)
+
+    # --- the z3py AST surface ---------------------------------------------------
+    def decl(self):
+        return self._decl
+
+    def num_args(self):
+        return len(self._args)
+
+    def arg(self, i):
+        return self._args[i]
+
+    def get_id(self):
+        return self._id
+
+    def sort(self):
+        return self._decl.range()
+
+    def size(self):
+        return self.sort().size()
+
+    def as_long(self):
+        if self._decl.kind() != Z3_OP_BNUM:
+            raise AttributeError("not a numeral")
+        return self._decl.params()[0]
+
+    def translate(self, ctx):
+        memo = {}
+
+        def tr(e):
+            if e._id not in memo:
+                memo[e._id] = ExprRef(e._decl.translate(ctx), [tr(a) for a in e._args], ctx)
+            return memo[e._id]
+
+        return tr(self)
+
+    def __hash__(self):
+        return self._id
+
+    def __repr__(self):
+        return f"{self._decl.name()}({', '.join(map(repr, self._args))})" if self._args else self._decl.name()
+
+    # --- operators LASER's wrappers use ------------------------------------------
+    def _bin(self, kind, other, name):
+        o = _coerce(other, self.sort())
+        return _op(kind, [self, o], self.sort(), name=name)
+
+    def __add__(self, o):
+        return self._bin(Z3_OP_BADD, o, "bvadd")
+
+    def __sub__(self, o):
+        return self._bin(Z3_OP_BSUB, o, "bvsub")
+
+    def __mul__(self, o):
+        return self._bin(Z3_OP_BMUL, o, "bvmul")
+
+    def __truediv__(self, o):
+        return self._bin(Z3_OP_BSDIV, o, "bvsdiv")
+
+    def __mod__(self, o):
+        return self._bin(Z3_OP_BSMOD, o, "bvsmod")
+
+    def __and__(self, o):
+        return self._bin(Z3_OP_BAND, o, "bvand")
+
+    def __or__(self, o):
+        return self._bin(Z3_OP_BOR, o, "bvor")
+
+    def __xor__(self, o):
+        return self._bin(Z3_OP_BXOR, o, "bvxor")
+
+    def __lshift__(self, o):
+        return self._bin(Z3_OP_BSHL, o, "bvshl")
+
+    def __rshift__(self, o):
+        return self._bin(Z3_OP_BASHR, o, "bvashr")
+
+    def __invert__(self):
+        return _op(Z3_OP_BNOT, [self], self.sort(), name="bvnot")
+
+    def __neg__(self):
+        return _op(Z3_OP_BNEG, [self], self.sort(), name="bvneg")
+
+    def __lt__(self, o):
+        return _cmp(Z3_OP_SLT, self, o)
+
+    def __le__(self, o):
+        return _cmp(Z3_OP_SLEQ, self, o)
+
+    def __gt__(self, o):
+        return _cmp(Z3_OP_SGT, self, o)
+
+    def __ge__(self, o):
+        return _cmp(Z3_OP_SGEQ, self, o)
+
+    def __eq__(self, o):
+        return _cmp(Z3_OP_EQ, self, o, "=")
+
+    def __ne__(self, o):
+        return _cmp(Z3_OP_DISTINCT, self, o, "distinct")
+
+
+def _cmp(kind, a, b, name=None):
+    b = _coerce(b, a.sort())
+    return _op(kind, [a, b], BoolSort(a.ctx), name=name)
+
+
+class CheckSatResult:
+    def __init__(self, name):
+        self.name = name
+
+    def __repr__(self):
+        return self.name
+
+
+sat, unsat, unknown = CheckSatResult("sat"), CheckSatResult("unsat"), CheckSatResult("unknown")
+
+
+# --- constructors ------------------------------------------------------------------
+def BitVec(name, size, ctx=None):
+    return ExprRef(FuncDeclRef(name, Z3_OP_UNINTERPRETED, [], BitVecSort(size, ctx), ctx=ctx), [], _ctx(ctx))
+
+
+def BitVecVal(v, size, ctx=None):
+    v = int(v) % (1 << size)
+    return ExprRef(FuncDeclRef(str(v), Z3_OP_BNUM, [], BitVecSort(size, ctx), [v], ctx), [], _ctx(ctx))
+
+
+def Bool(name, ctx=None):
+    return ExprRef(FuncDeclRef(name, Z3_OP_UNINTERPRETED, [], BoolSort(ctx), ctx=ctx), [], _ctx(ctx))
+
+
+def BoolVal(b, ctx=None):
+    k = Z3_OP_TRUE if b else Z3_OP_FALSE
+    return ExprRef(FuncDeclRef("true" if b else "false", k, [], BoolSort(ctx), ctx=ctx), [], _ctx(ctx))
+
+
+def Real(name, ctx=None):
+    return ExprRef(FuncDeclRef(name, Z3_OP_UNINTERPRETED, [], RealSort(ctx), ctx=ctx), [], _ctx(ctx))
+
+
+def Array(name, dom, rng):
+    return ExprRef(FuncDeclRef(name, Z3_OP_UNINTERPRETED, [], ArraySort(dom, rng), ctx=dom.ctx), [], dom.ctx)
+
+
+def Function(name, *sorts):
+    return FuncDeclRef(name, Z3_OP_UNINTERPRETED, sorts[:-1], sorts[-1], ctx=sorts[-1].ctx)
+
+
+def K(dom, v):
+    v = _coerce(v, BitVecSort(256)) if not isinstance(v, ExprRef) else v
+    return _op(Z3_OP_CONST_ARRAY, [v], ArraySort(dom, v.sort()), name="K")
+
+
+def Select(a, i):
+    i = _coerce(i, a.sort().domain())
+    return _op(Z3_OP_SELECT, [a, i], a.sort().range(), name="select")
+
+
+def Store(a, i, v):
+    i, v = _coerce(i, a.sort().domain()), _coerce(v, a.sort().range())
+    return _op(Z3_OP_STORE, [a, i, v], a.sort(), name="store")
+
+
+def If(c, a, b):
+    b = _coerce(b, a.sort()) if isinstance(a, ExprRef) else b
+    a = _coerce(a, b.sort())
+    return _op(Z3_OP_ITE, [c, a, b], a.sort(), name="if")
+
+
+def And(*a):
+    return _op(Z3_OP_AND, list(a), BoolSort(a[0].ctx), name="and")
+
+
+def Or(*a):
+    return _op(Z3_OP_OR, list(a), BoolSort(a[0].ctx), name="or")
+
+
+def Not(a):
+    return _op(Z3_OP_NOT, [a], BoolSort(a.ctx), name="not")
+
+
+def Xor(a, b):
+    return _op(Z3_OP_XOR, [a, b], BoolSort(a.ctx), name="xor")
+
+
+def Implies(a, b):
+    return _op(Z3_OP_IMPLIES, [a, b], BoolSort(a.ctx), name="=>")
+
+
+def Iff(a, b):
+    return _op(Z3_OP_IFF, [a, b], BoolSort(a.ctx), name="iff")
+
+
+def Distinct(*a):
+    return _op(Z3_OP_DISTINCT, list(a), BoolSort(a[0].ctx), name="distinct")
+
+
+def Concat(*a):
+    return _op(Z3_OP_CONCAT, list(a), BitVecSort(sum(x.size() for x in a), a[0].ctx), name="concat")
+
+
+def Extract(hi, lo, a):
+    return _op(Z3_OP_EXTRACT, [a], BitVecSort(hi - lo + 1, a.ctx), [hi, lo], name="extract")
+
+
+def ZeroExt(n, a):
+    return _op(Z3_OP_ZERO_EXT, [a], BitVecSort(a.size() + n, a.ctx), [n], name="zero_extend")
+
+
+def SignExt(n, a):
+    return _op(Z3_OP_SIGN_EXT, [a], BitVecSort(a.size() + n, a.ctx), [n], name="sign_extend")
+
+
+def RotateLeft(a, n):
+    return _op(Z3_OP_ROTATE_LEFT, [a], a.sort(), [n], name="rotate_left")
+
+
+def ULT(a, b):
+    return _cmp(Z3_OP_ULT, a, b, "bvult")
+
+
+def ULE(a, b):
+    return _cmp(Z3_OP_ULEQ, a, b, "bvule")
+
+
+def UGT(a, b):
+    return _cmp(Z3_OP_UGT, a, b, "bvugt")
+
+
+def UGE(a, b):
+    return _cmp(Z3_OP_UGEQ, a, b, "bvuge")
+
+
+def UDiv(a, b):
+    return a._bin(Z3_OP_BUDIV, b, "bvudiv")
+
+
+def URem(a, b):
+    return a._bin(Z3_OP_BUREM, b, "bvurem")
+
+
+def SRem(a, b):
+    return a._bin(Z3_OP_BSREM, b, "bvsrem")
+
+
+def LShR(a, b):
+    return a._bin(Z3_OP_BLSHR, b, "bvlshr")
+
+
+def BVMulNoOverflow(a, b, signed):
+    assert not signed
+    return _cmp(Z3_OP_BUMUL_NO_OVFL, a, b, "bvumul_noovfl")
+
+
+def simplify(e):
+    return e
+
+
+def is_bv_value(e):
+    return isinstance(e, ExprRef) and e.decl().kind() == Z3_OP_BNUM
+
+
+def is_app(e):
+    return isinstance(e, ExprRef)
+
+
+# --- evaluation (the double's own semantics: SMT-LIB QF_BV / QF_ABV) ---------------------
+def _s(v, w):
+    return v - (1 << w) if v >> (w - 1) else v
+
+
+def evaluate(e, env):
+    """Value of ``e`` under env = (scalars, arrays, funcs): ints (Bools as 0/1), arrays as
+    (dict, default).  Unassigned symbols read 0."""
+    scal, arrs, funcs = env
+    memo = {}
+
+    def ev(x):
+        if x._id in memo:
+            return memo[x._id]
+        d, k = x.decl(), x.decl().kind()
+        a = [ev(c) for c in x._args]
+        srt = x.sort()
+        w = srt.size() if srt.kind() == Z3_BV_SORT else 1
+        m = (1 << w) - 1
+        if k == Z3_OP_BNUM:
+            r = d.params()[0]
+        elif k in (Z3_OP_TRUE, Z3_OP_FALSE):
+            r = int(k == Z3_OP_TRUE)
+        elif k == Z3_OP_UNINTERPRETED:
+            if not x._args:
+                r = arrs.get(d.name(), ({}, 0)) if srt.kind() == Z3_ARRAY_SORT else scal.get(d.name(), 0)
+            else:
+                r = funcs.get(d.name(), ({}, 0))[0].get(a[0], 0)
+        elif k == Z3_OP_BADD:
+            r = sum(a) & m
+        elif k == Z3_OP_BSUB:
+            r = (a[0] - a[1]) & m
+        elif k == Z3_OP_BMUL:
+            r = (a[0] * a[1]) & m
+        elif k == Z3_OP_BUDIV:
+            r = m if a[1] == 0 else a[0] // a[1]
+        elif k == Z3_OP_BUREM:
+            r = a[0] if a[1] == 0 else a[0] % a[1]
+        elif k in (Z3_OP_BSDIV, Z3_OP_BSREM, Z3_OP_BSMOD):
+            x0, y0 = _s(a[0], w), _s(a[1], w)
+            if k == Z3_OP_BSDIV:
+                r = (-1 if x0 >= 0 else 1) & m if y0 == 0 else (abs(x0) // abs(y0) * (1 if (x0 < 0) == (y0 < 0) else -1)) & m
+            elif k == Z3_OP_BSREM:
+                r = a[0] if y0 == 0 else ((abs(x0) % abs(y0)) * (1 if x0 >= 0 else -1)) & m
+            else:
+                r = a[0] if y0 == 0 else (x0 - y0 * (x0 // y0)) & m
+        elif k == Z3_OP_BAND:
+            r = a[0] & a[1]
+        elif k == Z3_OP_BOR:
+            r = a[0] | a[1]
+        elif k == Z3_OP_BXOR:
+            r = a[0] ^ a[1]
+        elif k == Z3_OP_BNOT:
+            r = ~a[0] & m
+        elif k == Z3_OP_BNEG:
+            r = -a[0] & m
+        elif k == Z3_OP_BSHL:
+            r = (a[0] << a[1]) & m if a[1] < w else 0
+        elif k == Z3_OP_BLSHR:
+            r = a[0] >> a[1] if a[1] < w else 0
+        elif k == Z3_OP_BASHR:
+            r = (_s(a[0], w) >> min(a[1], w)) & m
+        elif k == Z3_OP_ROTATE_LEFT:
+            n = d.params()[0] % w
+            r = ((a[0] << n) | (a[0] >> (w - n))) & m
+        elif k in (Z3_OP_ULT, Z3_OP_ULEQ, Z3_OP_UGT, Z3_OP_UGEQ):
+            r = int({Z3_OP_ULT: a[0] < a[1], Z3_OP_ULEQ: a[0] <= a[1], Z3_OP_UGT: a[0] > a[1],
+                     Z3_OP_UGEQ: a[0] >= a[1]}[k])
+        elif k in (Z3_OP_SLT, Z3_OP_SLEQ, Z3_OP_SGT, Z3_OP_SGEQ):
+            wa = x._args[0].size()
+            p, q = _s(a[0], wa), _s(a[1], wa)
+            r = int({Z3_OP_SLT: p < q, Z3_OP_SLEQ: p <= q, Z3_OP_SGT: p > q, Z3_OP_SGEQ: p >= q}[k])
+        elif k == Z3_OP_BUMUL_NO_OVFL:
+            r = int(a[0] * a[1] < (1 << x._args[0].size()))
+        elif k == Z3_OP_CONCAT:
+            r = 0
+            for c, v in zip(x._args, a):
+                r = (r << c.size()) | v
+        elif k == Z3_OP_EXTRACT:
+            hi, lo = d.params()
+            r = (a[0] >> lo) & ((1 << (hi - lo + 1)) - 1)
+        elif k == Z3_OP_ZERO_EXT:
+            r = a[0]
+        elif k == Z3_OP_SIGN_EXT:
+            r = _s(a[0], x._args[0].size()) & m
+        elif k == Z3_OP_ITE:
+            r = a[1] if a[0] else a[2]
+        elif k in (Z3_OP_EQ, Z3_OP_IFF):
+            r = int(a[0] == a[1])
+        elif k == Z3_OP_DISTINCT:
+            r = int(len(set(map(repr, a))) == len(a))
+        elif k == Z3_OP_AND:
+            r = int(all(a))
+        elif k == Z3_OP_OR:
+            r = int(any(a))
+        elif k == Z3_OP_NOT:
+            r = int(not a[0])
+        elif k == Z3_OP_XOR:
+            r = int(bool(a[0]) != bool(a[1]))
+        elif k == Z3_OP_IMPLIES:
+            r = int((not a[0]) or bool(a[1]))
+        elif k == Z3_OP_SELECT:
+            r = a[0][0].get(a[1], a[0][1])
+        elif k == Z3_OP_STORE:
+            t = dict(a[0][0])
+            t[a[1]] = a[2]
+            r = (t, a[0][1])
+        elif k == Z3_OP_CONST_ARRAY:
+            r = ({}, a[0])
+        else:
+            raise NotImplementedError(d.name())
+        memo[x._id] = r
+        return r
+
+    return ev(e)
+
+
+class ModelRef:
+    def __init__(self, env, ctx):
+        self.env, self.ctx = env, ctx
+
+    def eval(self, e, model_completion=False):
+        v = evaluate(e, self.env)
+        if e.sort().kind() == Z3_BOOL_SORT:
+            return BoolVal(bool(v), self.ctx)
+        return BitVecVal(v, e.size(), self.ctx)
+
+    def translate(self, ctx):
+        return ModelRef(self.env, ctx)
+
+
+class Solver:
+    instances = []
+    FORCE = None  # set to `unknown` to model a z3 timeout
+
+    def __init__(self, ctx=None):
+        self.ctx = _ctx(ctx)
+        self.assertions = []
+        self.params = {}
+        self._model = None
+        Solver.instances.append(self)
+
+    def set(self, key, value):
+        self.params[key] = value
+
+    def add(self, *es):
+        for e in es:
+            assert e.ctx is self.ctx, "assertion from another context"
+            self.assertions.append(e)
+
+    def check(self):
+        if Solver.FORCE is not None:
+            return Solver.FORCE
+        scal, arrs, funcs = {}, {}, {}
+        for e in self.assertions:
+            if e.decl().kind() != Z3_OP_EQ:
+                continue
+            lhs, rhs = e.arg(0), e.arg(1)
+            if rhs.decl().kind() not in (Z3_OP_BNUM, Z3_OP_TRUE, Z3_OP_FALSE):
+                continue
+            val = rhs.as_long() if rhs.decl().kind() == Z3_OP_BNUM else int(rhs.decl().kind() == Z3_OP_TRUE)
+            lk = lhs.decl().kind()
+            if lk == Z3_OP_UNINTERPRETED and lhs.num_args() == 0:
+                scal[lhs.decl().name()] = val
+            elif lk == Z3_OP_SELECT and lhs.arg(1).decl().kind() == Z3_OP_BNUM:
+                arrs.setdefault(lhs.arg(0).decl().name(), ({}, 0))[0][lhs.arg(1).as_long()] = val
+            elif lk == Z3_OP_UNINTERPRETED and lhs.num_args() == 1 and lhs.arg(0).decl().kind() == Z3_OP_BNUM:
+                funcs.setdefault(lhs.decl().name(), ({}, 0))[0][lhs.arg(0).as_long()] = val
+        env = (scal, arrs, funcs)
+        if all(evaluate(e, env) for e in self.assertions):
+            self._model = ModelRef(env, self.ctx)
+            return sat
+        return unsat
+
+    def model(self):
+        return self._model
