@@ -40,7 +40,7 @@ def fuzz_bin(tmp_path_factory):
     build.write_prelude()
     out = tmp_path_factory.mktemp("fuzz") / "fuzz_host"
     cmd = [cxx, "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
-           "-fno-omit-frame-pointer", f"-I{ROOT}", str(ROOT / "tests/fuzz/fuzz_host.cpp"),
+           "-fno-omit-frame-pointer", f"-I{ROOT}", "-I/opt/rocm/include", str(ROOT / "tests/fuzz/fuzz_host.cpp"),
            str(ROOT / "mythril_amd/csrc/program.cpp"), str(ROOT / "mythril_amd/csrc/jit.cpp"), "-ldl", "-o", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
