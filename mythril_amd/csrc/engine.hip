@@ -717,7 +717,7 @@ struct JitTicket {
   std::vector<GenSpec> specs;
   std::vector<uint32_t> consts;
   bool cancelled = false;
-  uint64_t jit = 0;
+  std::unique_ptr<DevJit> ready;  // loaded module, handed to Engine::jits by the poll
   int rc = MG_OK;
   std::string err;
 };
@@ -726,8 +726,11 @@ struct Engine {
   std::mutex mu;
   std::unordered_map<uint64_t, std::unique_ptr<DevJit>> jits;
   CodeCache code_cache;
-  // compile thread: hipRTC/comgr work runs off the caller's thread and outside `mu`, so
-  // searches keep launching while a query's kernel compiles (mg_jit_compile_async)
+  // compile thread: source emission, comgr and the module load run off the caller's thread
+  // and never take `mu` (a search holds `mu` for its whole launch + sync, back to back), so
+  // searches keep launching while a query's kernel compiles (mg_jit_compile_async).  `jit_mu`
+  // guards the members below; lock order: mu before jit_mu.
+  std::mutex jit_mu;
   bool jit_worker_running = false;  // detached thread; never outlives the (leaked) Engine
   bool jit_stop = false;
   std::deque<std::shared_ptr<JitTicket>> jit_queue;
@@ -969,16 +972,21 @@ int mg_init(uint32_t device_mask) {
 
 void mg_shutdown(void) {
   Engine& e = E();
-  std::unique_lock<std::mutex> g(e.mu);
-  // stop the compile thread (a compile in flight finishes first; its result is dropped)
-  e.jit_stop = true;
-  for (auto& t : e.jit_queue) t->cancelled = true;
-  for (auto& kv : e.tickets) kv.second->cancelled = true;
-  e.jit_cv.notify_all();
-  e.jit_done_cv.wait(g, [&] { return !e.jit_worker_running; });
-  e.jit_stop = false;
-  e.jit_queue.clear();
-  e.tickets.clear();
+  std::lock_guard<std::mutex> g(e.mu);
+  {
+    // stop the compile thread (a compile in flight finishes first; its result is dropped)
+    std::unique_lock<std::mutex> jl(e.jit_mu);
+    e.jit_stop = true;
+    for (auto& t : e.jit_queue) t->cancelled = true;
+    for (auto& kv : e.tickets) kv.second->cancelled = true;
+    e.jit_cv.notify_all();
+    e.jit_done_cv.wait(jl, [&] { return !e.jit_worker_running; });
+    e.jit_stop = false;
+    e.jit_queue.clear();
+    for (auto& kv : e.tickets)
+      if (kv.second->ready) (void)hipModuleUnload(kv.second->ready->mod);
+    e.tickets.clear();
+  }
   for (auto& kv : e.jits) (void)hipModuleUnload(kv.second->mod);
   e.jits.clear();
   if (!e.init) return;
@@ -1423,34 +1431,40 @@ int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle) { return m
 
 namespace mg {
 
-// load a code object as a DevJit (caller holds e.mu); returns the jit handle
-static int load_jit(Engine& e, const std::vector<char>& code, const JitTicket& t, double compile_ms, uint64_t* out) {
+// load a code object as a DevJit (any thread: HIP module calls are thread-safe)
+static int load_jit(const std::vector<char>& code, const JitTicket& t, double compile_ms, std::unique_ptr<DevJit>& out) {
   auto j = std::make_unique<DevJit>();
   HIPCHK(hipModuleLoadData(&j->mod, code.data()));
   int nb = 0;
+  auto fn = [&](hipFunction_t* f, const char* name) -> int {
+    if (hipModuleGetFunction(f, j->mod, name) != hipSuccess) {
+      (void)hipModuleUnload(j->mod);
+      return set_err(MG_E_HIP, std::string("JIT module has no ") + name);
+    }
+    return MG_OK;
+  };
   if (t.has_gen) {
-    HIPCHK(hipModuleGetFunction(&j->fsearch, j->mod, "mgj_search"));
-    if (t.flags & MG_JIT_GEN_VERDICTS) HIPCHK(hipModuleGetFunction(&j->fgen, j->mod, "mgj_gen"));
+    if (int rc = fn(&j->fsearch, "mgj_search")) return rc;
+    if (t.flags & MG_JIT_GEN_VERDICTS)
+      if (int rc = fn(&j->fgen, "mgj_gen")) return rc;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, j->fsearch, 256, 0) == hipSuccess && nb > 0)
       j->nb_search = nb;
   } else {
-    HIPCHK(hipModuleGetFunction(&j->feval, j->mod, "mgj_eval"));
+    if (int rc = fn(&j->feval, "mgj_eval")) return rc;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, j->feval, 256, 0) == hipSuccess && nb > 0)
       j->nb_eval = nb;
   }
   j->prog = t.prog;
   j->gen = t.gen;
   j->compile_ms = compile_ms;
-  const uint64_t h = e.next_handle++;
-  e.jits[h] = std::move(j);
-  *out = h;
+  out = std::move(j);
   return MG_OK;
 }
 
-static void jit_worker_main(Engine* ep) {
+static void jit_worker_main(Engine* ep, int device) {
   Engine& e = *ep;
-  bool dev_set = false;
-  std::unique_lock<std::mutex> lk(e.mu);
+  (void)hipSetDevice(device);
+  std::unique_lock<std::mutex> lk(e.jit_mu);
   for (;;) {
     e.jit_cv.wait(lk, [&] { return e.jit_stop || !e.jit_queue.empty(); });
     if (e.jit_stop) {
@@ -1461,51 +1475,62 @@ static void jit_worker_main(Engine* ep) {
     std::shared_ptr<JitTicket> t = e.jit_queue.front();
     e.jit_queue.pop_front();
     if (t->cancelled) continue;
-    if (!dev_set && e.init) {
-      (void)hipSetDevice(e.device);
-      dev_set = true;
-    }
     lk.unlock();
     const auto t0 = std::chrono::steady_clock::now();
     const uint32_t kernels = t->has_gen ? (JIT_SEARCH | ((t->flags & MG_JIT_GEN_VERDICTS) ? JIT_GEN : 0u)) : JIT_EVAL;
     const std::string src = t->has_gen ? jit_source(t->low, &t->specs, &t->consts, kernels)
                                        : jit_source(t->low, nullptr, nullptr, kernels);
     lk.lock();
-    const std::vector<char>* code = e.code_cache.find(src);
+    const std::vector<char>* cached = e.code_cache.find(src);
+    std::vector<char> code = cached ? *cached : std::vector<char>();
+    lk.unlock();
     int rc = MG_OK;
     std::string log;
-    if (!code) {
-      lk.unlock();
-      std::vector<char> obj;
-      rc = jit_compile(src, obj, log);
-      lk.lock();
-      if (rc == MG_OK) code = e.code_cache.insert(src, std::move(obj));
+    if (code.empty()) {
+      rc = jit_compile(src, code, log);
+      if (rc == MG_OK) {
+        lk.lock();
+        e.code_cache.insert(src, std::vector<char>(code));
+        lk.unlock();
+      }
     }
-    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    std::unique_ptr<DevJit> j;
+    std::string err;
+    if (rc != MG_OK) {
+      err = "JIT compile failed: " + log.substr(0, 4000);
+    } else {
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      rc = load_jit(code, *t, ms, j);
+      if (rc != MG_OK) err = g_err;
+    }
+    lk.lock();
     if (rc != MG_OK) {
       t->rc = rc;
-      t->err = "JIT compile failed: " + log.substr(0, 4000);
+      t->err = err;
       t->state = JitTicket::FAILED;
     } else if (t->cancelled) {
+      (void)hipModuleUnload(j->mod);
       t->state = JitTicket::FAILED;
       t->rc = MG_E_INVALID;
       t->err = "cancelled";
-    } else if (!e.progs.count(t->prog) || (t->has_gen && !e.gens.count(t->gen))) {
-      t->state = JitTicket::FAILED;
-      t->rc = MG_E_INVALID;
-      t->err = "program or generator freed before its JIT kernel was ready";
     } else {
-      rc = load_jit(e, *code, *t, ms, &t->jit);
-      if (rc != MG_OK) {
-        t->rc = rc;
-        t->err = g_err;
-        t->state = JitTicket::FAILED;
-      } else {
-        t->state = JitTicket::DONE;
-      }
+      t->ready = std::move(j);
+      t->state = JitTicket::DONE;
     }
     e.jit_done_cv.notify_all();
   }
+}
+
+// process exit with a compile in flight: stop the compile thread before the compiler
+// library's static destructors run (registered after them, so it runs first)
+static void jit_atexit() {
+  Engine& e = E();
+  std::unique_lock<std::mutex> jl(e.jit_mu);
+  e.jit_stop = true;
+  for (auto& t : e.jit_queue) t->cancelled = true;
+  for (auto& kv : e.tickets) kv.second->cancelled = true;
+  e.jit_cv.notify_all();
+  e.jit_done_cv.wait_for(jl, std::chrono::seconds(10), [&] { return !e.jit_worker_running; });
 }
 
 // caller holds e.mu
@@ -1530,12 +1555,18 @@ static int submit_jit(Engine& e, uint64_t prog, uint64_t gen, uint32_t flags, ui
     int rc = specialize_program(p->low, nullptr, nullptr, t->low, err);
     if (rc) return set_err(rc, err);
   }
+  const uint64_t h = e.next_handle++;
+  std::lock_guard<std::mutex> jl(e.jit_mu);
   if (!e.jit_worker_running) {
+    static std::once_flag once;
+    std::call_once(once, [] {
+      jit_compiler_preload();
+      std::atexit(jit_atexit);
+    });
     if (const char* c = getenv("MYTHGPU_JIT_CACHE")) e.code_cache.cap = std::max(1, atoi(c));
-    std::thread(jit_worker_main, &e).detach();
+    std::thread(jit_worker_main, &e, e.device).detach();
     e.jit_worker_running = true;
   }
-  const uint64_t h = e.next_handle++;
   e.tickets[h] = t;
   e.jit_queue.push_back(t);
   e.jit_cv.notify_one();
@@ -1543,19 +1574,29 @@ static int submit_jit(Engine& e, uint64_t prog, uint64_t gen, uint32_t flags, ui
   return MG_OK;
 }
 
-// caller holds lk on e.mu; wait_ms < 0: until done
-static int poll_jit(Engine& e, std::unique_lock<std::mutex>& lk, uint64_t ticket, int64_t wait_ms, uint64_t* jit) {
-  auto it = e.tickets.find(ticket);
-  if (it == e.tickets.end()) return set_err(MG_E_INVALID, "bad JIT ticket");
-  std::shared_ptr<JitTicket> t = it->second;
-  auto ready = [&] { return t->state != JitTicket::PENDING; };
-  if (wait_ms < 0) e.jit_done_cv.wait(lk, ready);
-  else if (wait_ms > 0) e.jit_done_cv.wait_for(lk, std::chrono::milliseconds(wait_ms), ready);
+// caller holds e.mu; wait_ms < 0: until done.  A finished kernel moves into e.jits here.
+static int poll_jit(Engine& e, uint64_t ticket, int64_t wait_ms, uint64_t* jit) {
   *jit = 0;
-  if (t->state == JitTicket::PENDING) return MG_OK;
-  e.tickets.erase(ticket);
+  std::shared_ptr<JitTicket> t;
+  {
+    std::unique_lock<std::mutex> jl(e.jit_mu);
+    auto it = e.tickets.find(ticket);
+    if (it == e.tickets.end()) return set_err(MG_E_INVALID, "bad JIT ticket");
+    t = it->second;
+    auto ready = [&] { return t->state != JitTicket::PENDING; };
+    if (wait_ms < 0) e.jit_done_cv.wait(jl, ready);
+    else if (wait_ms > 0) e.jit_done_cv.wait_for(jl, std::chrono::milliseconds(wait_ms), ready);
+    if (t->state == JitTicket::PENDING) return MG_OK;
+    e.tickets.erase(ticket);
+  }
   if (t->state == JitTicket::FAILED) return set_err(t->rc ? t->rc : MG_E_HIP, t->err);
-  *jit = t->jit;
+  if (!e.progs.count(t->prog) || (t->has_gen && !e.gens.count(t->gen))) {
+    (void)hipModuleUnload(t->ready->mod);
+    return set_err(MG_E_INVALID, "program or generator freed before its JIT kernel was ready");
+  }
+  const uint64_t h = e.next_handle++;
+  e.jits[h] = std::move(t->ready);
+  *jit = h;
   return MG_OK;
 }
 
@@ -1565,11 +1606,11 @@ extern "C" {
 
 int mg_jit_compile_ex(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* jit_handle) {
   Engine& e = E();
-  std::unique_lock<std::mutex> lk(e.mu);
+  std::lock_guard<std::mutex> g(e.mu);
   uint64_t ticket = 0;
   int rc = submit_jit(e, prog, gen, flags, &ticket);
   if (rc) return rc;
-  return poll_jit(e, lk, ticket, -1, jit_handle);
+  return poll_jit(e, ticket, -1, jit_handle);
 }
 
 int mg_jit_compile_async(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* ticket) {
@@ -1580,25 +1621,22 @@ int mg_jit_compile_async(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* 
 
 int mg_jit_poll(uint64_t ticket, int32_t wait_ms, uint64_t* jit_handle) {
   Engine& e = E();
-  std::unique_lock<std::mutex> lk(e.mu);
-  return poll_jit(e, lk, ticket, wait_ms, jit_handle);
+  std::lock_guard<std::mutex> g(e.mu);
+  return poll_jit(e, ticket, wait_ms, jit_handle);
 }
 
 int mg_jit_cancel(uint64_t ticket) {
   Engine& e = E();
-  std::lock_guard<std::mutex> g(e.mu);
+  std::lock_guard<std::mutex> jl(e.jit_mu);
   auto it = e.tickets.find(ticket);
   if (it == e.tickets.end()) return set_err(MG_E_INVALID, "bad JIT ticket");
   std::shared_ptr<JitTicket> t = it->second;
   e.tickets.erase(it);
   if (t->state == JitTicket::PENDING) {
     t->cancelled = true;  // the worker drops it (before compiling if still queued)
-  } else if (t->state == JitTicket::DONE) {
-    auto j = e.jits.find(t->jit);
-    if (j != e.jits.end()) {
-      (void)hipModuleUnload(j->second->mod);
-      e.jits.erase(j);
-    }
+  } else if (t->state == JitTicket::DONE && t->ready) {
+    (void)hipModuleUnload(t->ready->mod);
+    t->ready.reset();
   }
   return MG_OK;
 }

@@ -652,12 +652,8 @@ struct Rtc {
 Rtc& rtc() {
   static Rtc r;
   if (r.h) return r;
-  // the image's ROCm hipRTC first: a process that imported torch already has torch's bundled (older)
-  // libhiprtc loaded under the same soname, and its code for these kernels is measurably slower
-  // hipRTC dlopens its compiler (libamd_comgr.so.3) by soname, which would bind to torch's copy;
-  // a fresh link namespace makes it resolve the image's own comgr next to it.
-  const char* env = getenv("MYTHGPU_HIPRTC");
-  if (!env || std::strcmp(env, "shared") != 0) r.h = dlmopen(LM_ID_NEWLM, "/opt/rocm/lib/libhiprtc.so.7", RTLD_NOW | RTLD_LOCAL);
+  // fallback compiler (MYTHGPU_JIT_COMPILER=hiprtc or no comgr): the image's hipRTC by absolute
+  // path; no dlmopen namespace (see comgr()).
   const char* names[] = {"/opt/rocm/lib/libhiprtc.so.7", "libhiprtc.so.7", "libhiprtc.so"};
   for (const char* n : names) {
     if (r.h) break;
@@ -707,8 +703,11 @@ Comgr& comgr() {
   static Comgr c;
   static std::once_flag once;
   std::call_once(once, [] {
-    // fresh link namespace: torch bundles an older comgr under the same soname
-    c.h = dlmopen(LM_ID_NEWLM, "/opt/rocm/lib/libamd_comgr.so.3", RTLD_NOW | RTLD_LOCAL);
+    // by absolute path: the image's comgr, not torch's bundled copy of the same soname.  Not in
+    // a fresh link namespace (dlmopen): that loads a second libc whose malloc also moves the
+    // program break, and heap corruption follows once the compile thread runs beside the
+    // caller's allocations.
+    c.h = dlopen("/opt/rocm/lib/libamd_comgr.so.3", RTLD_NOW | RTLD_LOCAL);
     if (!c.h) c.h = dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_LOCAL);
     if (!c.h) return;
 #define MG_SYM(field, name) c.field = (decltype(c.field))dlsym(c.h, #name)
@@ -883,6 +882,12 @@ int hiprtc_compile(const std::string& src, std::vector<char>& code, std::string&
   return MG_OK;
 }
 }  // namespace
+
+void jit_compiler_preload() {
+  const char* which = getenv("MYTHGPU_JIT_COMPILER");
+  if (!(which && std::strcmp(which, "hiprtc") == 0) && comgr().ok) return;
+  (void)rtc();
+}
 
 int jit_compile(const std::string& src, std::vector<char>& code, std::string& log) {
   const char* which = getenv("MYTHGPU_JIT_COMPILER");

@@ -14,6 +14,10 @@ enum : uint32_t { JIT_SEARCH = 1, JIT_EVAL = 2, JIT_GEN = 4 };
 std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
                        uint32_t kernels);
 
+// Load the JIT compiler library now (on the calling thread): its static destructors then
+// register before anything the caller registers with atexit afterwards.
+void jit_compiler_preload();
+
 // hipRTC compile for gfx950 -> code object bytes. MG_OK or MG_E_*; `log` gets the compiler log.
 int jit_compile(const std::string& src, std::vector<char>& code, std::string& log);
 

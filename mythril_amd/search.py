@@ -355,8 +355,10 @@ JIT_COMPILE_S = [0.15]
 # while a compile is pending, interpreter launches are cut to about this long so the search
 # switches to the compiled kernel soon after it is ready
 JIT_POLL_S = 0.010
-# kernel that produced the last search's result ("interp" / "jit"), for stream statistics
+# kernel that produced the last search's result ("interp" / "jit") and that result, for
+# stream statistics (tools/stream_bench.py)
 LAST_ENGINE = None
+LAST_RESULT = None
 
 
 def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int = 1 << 16,
@@ -451,8 +453,8 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
     dt = time.perf_counter() - t0
     res = SearchResult(hit, hits, scanned, dt)
     res.engine = used
-    global LAST_ENGINE
-    LAST_ENGINE = used
+    global LAST_ENGINE, LAST_RESULT
+    LAST_ENGINE, LAST_RESULT = used, res
     if hit is not None and want_model:
         # the search only reports indices whose verdict is 1
         tm = time.perf_counter()

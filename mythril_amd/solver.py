@@ -261,7 +261,7 @@ def _solve(constraints: Sequence[T.Term], timeout_ms: float) -> Optional[Model]:
     st = SolverStatistics()
     eng = Engine.get()
     res = search.search_partitioned(eng, list(constraints), timeout_s=max(timeout_ms, 1.0) / 1000.0,
-                                    max_candidates=1 << 34)
+                                    max_candidates=1 << 40)
     st.candidates += res.scanned
     if res.index is None:
         st.gpu_unknown += 1

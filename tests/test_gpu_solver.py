@@ -224,7 +224,10 @@ def test_jit_escalation_same_first_hit(engine):
     r_i = search.search(engine, cs, timeout_s=30, jit="never", chunk=1 << 12)
     r_j = search.search(engine, cs, timeout_s=30, jit="always", chunk=1 << 12)
     r_a = search.search(engine, cs, timeout_s=30, jit="auto", chunk=1 << 12, jit_cost_s=0.0)
-    assert r_i.engine == "interp" and r_j.engine == "jit" and r_a.engine == "jit"
+    # auto: the interpreter keeps scanning while the kernel compiles (async), so a 2^-16
+    # needle may be found before the switch; the first hit is the same either way
+    # (tests/test_gpu_stream.py covers the switch itself with a 2^-32 needle)
+    assert r_i.engine == "interp" and r_j.engine == "jit" and r_a.engine in ("interp", "jit")
     assert r_i.index is not None and r_i.index == r_j.index == r_a.index
     assert r_i.model[1:4] == r_j.model[1:4]
 

@@ -49,7 +49,7 @@ def stream_queries(name):
     return out
 
 
-def run(names, budget_ms):
+def run(names, budget_ms, verbose=False):
     solver.args.solver_timeout = budget_ms
     st = solver.SolverStatistics()
     rows = []
@@ -78,6 +78,11 @@ def run(names, budget_ms):
             eng = getattr(search, "LAST_ENGINE", None)
             if eng:
                 engines[eng] = engines.get(eng, 0) + 1
+            if verbose:
+                r = search.LAST_RESULT
+                print(json.dumps({"q": label, "ms": round(dt * 1e3, 2), "candidates": int(dc), "engine": eng,
+                                  "timing": {k: round(v, 2) for k, v in (r.timing if r else {}).items()}}),
+                      flush=True)
         total = time.perf_counter() - t_all
         row = {"workload": name, "queries": len(qs), "sat": n_sat, "budget_ms": budget_ms,
                "stream_s": round(total, 4), "candidates": int(cand_all),
@@ -100,8 +105,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--budget-ms", type=float, default=200.0)
     ap.add_argument("--workloads", default=",".join(SHAPES))
+    ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args()
-    run([w for w in a.workloads.split(",") if w], a.budget_ms)
+    run([w for w in a.workloads.split(",") if w], a.budget_ms, a.verbose)
 
 
 if __name__ == "__main__":
