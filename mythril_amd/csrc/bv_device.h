@@ -136,31 +136,95 @@ __device__ __forceinline__ bool uge8(const W8& a, const W8& b) {
   return br == 0;
 }
 
-// Restoring division, 256 steps over the 512-bit pair (rem:quo); uniform trip
-// count (no lane divergence).  Invariant rem < b, so 2*rem+bit needs 257 bits:
-// the bit shifted out of rem is kept in `c`.
-__device__ __forceinline__ void udivrem8(const W8& a, const W8& b, W8& q, W8& r) {
-  W8 rem, quo = a;
+__device__ __forceinline__ W8 shl8(const W8& x, u32 s);
+
+// count of leading zero bits of a 256-bit value (256 for zero)
+__device__ __forceinline__ u32 clz8(const W8& a) {
+  u32 n = 256;
 #pragma unroll
-  for (int i = 0; i < 8; i++) rem.w[i] = 0;
+  for (int i = 0; i < 8; i++) n = a.w[i] ? (u32)(32 * (7 - i)) + (u32)__builtin_clz(a.w[i]) : n;
+  return n;
+}
+
+__device__ __forceinline__ W8 shr8(const W8& x, u32 s, u32 fill);
+
+// Restoring division over the quotient bits only.  With la, lb the bit lengths of a and
+// b, the quotient has n = la - lb + 1 bits (none if la < lb): the remainder starts as the
+// top la - n = lb - 1 bits of a (below b, so the first lb - 1 steps of the textbook loop
+// never subtract) and the low n bits of a come in at the top of `quo`, one per step.  The
+// remainder keeps NB limbs — every active lane's divisor fits NB limbs and rem < b is the
+// loop invariant, so 2*rem+bit needs NB limbs plus the carry bit `c`.  The trip count is
+// per lane (the wave runs its longest): a few steps for like-sized operands.
+template <int NB>
+__device__ __forceinline__ void udivrem_nb(const W8& rem0, const W8& quo0, u32 n, const W8& b, W8& q, W8& r) {
+  u32 rem[NB];
+#pragma unroll
+  for (int i = 0; i < NB; i++) rem[i] = rem0.w[i];
+  W8 quo = quo0;
 #pragma unroll 1
-  for (int it = 0; it < 256; it++) {
-    const u32 c = rem.w[7] >> 31;
+  for (u32 it = 0; it < n; it++) {
+    const u32 c = rem[NB - 1] >> 31;
 #pragma unroll
-    for (int i = 7; i > 0; i--) rem.w[i] = (rem.w[i] << 1) | (rem.w[i - 1] >> 31);
-    rem.w[0] = (rem.w[0] << 1) | (quo.w[7] >> 31);
+    for (int i = NB - 1; i > 0; i--) rem[i] = __builtin_amdgcn_alignbit(rem[i], rem[i - 1], 31);
+    rem[0] = __builtin_amdgcn_alignbit(rem[0], quo.w[7], 31);
 #pragma unroll
-    for (int i = 7; i > 0; i--) quo.w[i] = (quo.w[i] << 1) | (quo.w[i - 1] >> 31);
+    for (int i = 7; i > 0; i--) quo.w[i] = __builtin_amdgcn_alignbit(quo.w[i], quo.w[i - 1], 31);
     quo.w[0] <<= 1;
-    u32 br;
-    W8 d = sub8(rem, b, &br);
+    u32 br = 0, d[NB];
+#pragma unroll
+    for (int i = 0; i < NB; i++) d[i] = __builtin_subc(rem[i], b.w[i], br, &br);
     const bool ge = (c != 0) | (br == 0);
 #pragma unroll
-    for (int i = 0; i < 8; i++) rem.w[i] = ge ? d.w[i] : rem.w[i];
+    for (int i = 0; i < NB; i++) rem[i] = ge ? d[i] : rem[i];
     quo.w[0] |= ge ? 1u : 0u;
   }
   q = quo;
-  r = rem;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.w[i] = i < NB ? rem[i] : 0u;
+}
+
+// q, r of a / b for b != 0 (b == 0: the callers substitute the SMT-LIB results).
+// Wave-uniform limb count of the divisor (ballot) picks the path: a one-limb divisor
+// runs limb-serial long division (8 dependent 64/32 divides), wider ones the bit-serial
+// loop above with an NB-limb remainder.
+__device__ __forceinline__ void udivrem8(const W8& a, const W8& b, W8& q, W8& r) {
+  if (!__builtin_amdgcn_ballot_w64((b.w[1] | b.w[2] | b.w[3] | b.w[4] | b.w[5] | b.w[6] | b.w[7]) != 0u)) {
+    const u32 d = b.w[0] ? b.w[0] : 1u;
+    u32 rr = 0;
+#pragma unroll
+    for (int i = 7; i >= 0; i--) {
+      const u64 cur = ((u64)rr << 32) | a.w[i];
+      const u32 qi = (u32)(cur / d);
+      q.w[i] = qi;
+      rr = (u32)(cur - (u64)qi * d);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.w[i] = i ? 0u : rr;
+    return;
+  }
+  const u32 la = 256u - clz8(a), lb = 256u - clz8(b);
+  const u32 n = la >= lb ? la - lb + 1u : 0u;  // quotient bits (<= 256)
+  W8 rem0, quo0;
+  if (n == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) rem0.w[i] = quo0.w[i] = 0;
+  } else {
+    if (n >= 256u) {  // b == 1 beside wider divisors in the wave
+#pragma unroll
+      for (int i = 0; i < 8; i++) rem0.w[i] = 0;
+    } else {
+      rem0 = shr8(a, n, 0u);
+    }
+    quo0 = shl8(a, 256u - n);
+  }
+  if (__builtin_amdgcn_ballot_w64((b.w[4] | b.w[5] | b.w[6] | b.w[7]) != 0u)) {
+    udivrem_nb<8>(rem0, quo0, n, b, q, r);
+  } else if (__builtin_amdgcn_ballot_w64((b.w[2] | b.w[3]) != 0u)) {
+    udivrem_nb<4>(rem0, quo0, n, b, q, r);
+  } else {
+    udivrem_nb<2>(rem0, quo0, n, b, q, r);
+  }
+  if (n == 0) r = a;  // a < b: q = 0, r = a
 }
 
 // SMT-LIB bvudiv / bvurem with the total-division convention
@@ -395,10 +459,21 @@ __device__ __forceinline__ W8 bv_exp(const W8& base, const W8& e, u32 width) {
 #pragma unroll
     for (int i = 7; i >= 0; i--) ex.w[i] = i >= 1 ? ex.w[i - 1] : 0u;
   }
+  // the wave's longest exponent inside the top live limb (binary search over ballots), so
+  // leading zero digits are skipped too: an 8-bit exponent takes 4 steps, not 16
+  u32 m = 0;
+  if (live) {
+#pragma unroll
+    for (u32 step = 16; step >= 1; step >>= 1)
+      if (__builtin_amdgcn_ballot_w64((ex.w[7] >> (m + step - 1u)) != 0u)) m += step;
+  }
+  const u32 skip = (32u - m) & ~1u;  // even: digits stay aligned to the exponent's bit 0
+  if (live && skip) ex = shl8(ex, skip);
+  const u32 steps = live * 16u - (live ? skip / 2u : 0u);
   const W8 b2 = sqr8(base);
   const W8 b3 = mul8(b2, base);
 #pragma unroll 1
-  for (u32 it = 0; it < live * 16u; it++) {
+  for (u32 it = 0; it < steps; it++) {
     const u32 dg = ex.w[7] >> 30;
 #pragma unroll
     for (int i = 7; i > 0; i--) ex.w[i] = (ex.w[i] << 2) | (ex.w[i - 1] >> 30);

@@ -336,3 +336,34 @@ def test_power_of_two_strength_reduction(engine):
     finally:
         engine.free(prog)
     assert (wi == wj).all()
+
+
+@pytest.mark.parametrize("jit", [False, True])
+def test_division_operand_sizes(engine, jit):
+    """udivrem8's paths (one-limb long division, quotient-bit loop with 2/4/8-limb
+    remainders) under every mix of operand sizes within a wave: per-lane bit lengths of
+    dividend and divisor from 0 to 256, a < b, a = b, b = 1, b = 0, signed edge values."""
+    from helpers import gpu_eval_terms
+
+    rng = random.Random(11)
+    a = T.BitVecVar("a", 256)
+    b = T.BitVecVar("b", 256)
+    terms = [T.bvbin(op, a, b) for op in ["bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod"]]
+
+    def val(bits):
+        return rng.getrandbits(bits) | (1 << (bits - 1)) if bits else 0
+
+    assigns = []
+    for _ in range(6 * 64):
+        la, lb = rng.choice([0, 1, 2, 31, 32, 33, 64, 65, 96, 128, 129, 200, 255, 256]), \
+            rng.choice([0, 1, 2, 3, 31, 32, 33, 63, 64, 65, 127, 128, 160, 255, 256])
+        assigns.append([val(la), val(lb)])
+    # waves with one-limb divisors only, and the edge pairs
+    assigns += [[rng.getrandbits(256), rng.choice([1, 2, 3, 7, 10, 0xFFFFFFFF, 0])] for _ in range(128)]
+    edges = [0, 1, 2, 3, (1 << 255), (1 << 255) - 1, (1 << 256) - 1, (1 << 256) - 2, 1 << 128, (1 << 32) - 1, 1 << 32]
+    assigns += [[x, y] for x in edges for y in edges]
+    P, _, ver, got, models = gpu_eval_terms(engine, [T.BoolVal(True)], terms, assigns, jit=jit)
+    for i, (x, y) in enumerate(assigns):
+        want = evaluate_many(terms, OracleModel({"a": x, "b": y}))
+        for t, w in zip(terms, want):
+            assert got[i][t.id] == w, (t.op, hex(x), hex(y))

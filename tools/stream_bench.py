@@ -49,7 +49,7 @@ def stream_queries(name):
     return out
 
 
-def run(names, budget_ms, verbose=False):
+def run(names, budget_ms, verbose=False, quiet=False):
     solver.args.solver_timeout = budget_ms
     st = solver.SolverStatistics()
     rows = []
@@ -90,14 +90,16 @@ def run(names, budget_ms, verbose=False):
                "budget_bound_queries_s": round(bound_t, 4),
                "budget_bound_rate": bound_c / bound_t if bound_t else None, "engines": engines}
         rows.append(row)
-        print(json.dumps(row), flush=True)
+        if not quiet:
+            print(json.dumps(row), flush=True)
     bt = sum(r["budget_bound_queries_s"] for r in rows)
     bc = sum((r["budget_bound_rate"] or 0) * r["budget_bound_queries_s"] for r in rows)
     summary = {"summary": True, "budget_ms": budget_ms, "workloads": len(rows),
                "budget_bound_rate": bc / bt if bt else None,
                "stream_rate": sum(r["candidates"] for r in rows) / sum(r["stream_s"] for r in rows),
                "jit_compile_s_avg": search.JIT_COMPILE_S[0]}
-    print(json.dumps(summary), flush=True)
+    if not quiet:
+        print(json.dumps(summary), flush=True)
     return rows, summary
 
 
