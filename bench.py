@@ -175,6 +175,8 @@ def main():
         from mythril_amd import ssa as _ssa
 
         search.FLATTEN_CACHE = _ssa.FlattenCache(aux_words=True)
+        search._GEN_CACHE.clear()
+        eng.cache_clear()
         t1 = time.perf_counter()
         search.search(eng, roots, seed=args.seed, max_candidates=1 << 30, timeout_s=30)
         ttfm_cold_ms = (time.perf_counter() - t1) * 1e3

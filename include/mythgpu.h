@@ -269,6 +269,9 @@ int mg_jit_verdicts(uint64_t jit, uint64_t seed, uint64_t start, uint64_t n, uin
 int mg_jit_compile_async(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* ticket);
 int mg_jit_poll(uint64_t ticket, int32_t wait_ms, uint64_t* jit_handle);
 int mg_jit_cancel(uint64_t ticket);
+/* Drop the engine's host-side caches (lowered programs, generator specialisations, JIT code
+ * objects by source): the next query pays every pass again (cold-start measurement). */
+int mg_cache_clear(void);
 int mg_jit_info(uint64_t jit, double* compile_ms, int* blocks_per_cu);
 int mg_jit_free(uint64_t jit);
 int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags, uint64_t* first_hit,

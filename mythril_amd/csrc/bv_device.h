@@ -185,21 +185,37 @@ __device__ __forceinline__ void udivrem_nb(const W8& rem0, const W8& quo0, u32 n
 
 // q, r of a / b for b != 0 (b == 0: the callers substitute the SMT-LIB results).
 // Wave-uniform limb count of the divisor (ballot) picks the path: a one-limb divisor
-// runs limb-serial long division (8 dependent 64/32 divides), wider ones the bit-serial
-// loop above with an NB-limb remainder.
+// runs limb-serial long division by reciprocal, wider ones the bit-serial loop above
+// with an NB-limb remainder.
 __device__ __forceinline__ void udivrem8(const W8& a, const W8& b, W8& q, W8& r) {
   if (!__builtin_amdgcn_ballot_w64((b.w[1] | b.w[2] | b.w[3] | b.w[4] | b.w[5] | b.w[6] | b.w[7]) != 0u)) {
-    const u32 d = b.w[0] ? b.w[0] : 1u;
-    u32 rr = 0;
+    // one-limb divisor: normalised long division, one 2/1 step per limb with the divisor's
+    // reciprocal computed once (Moller & Granlund, "Improved division by invariant
+    // integers", IEEE TC 2011, Alg. 4): a multiply, a 64-bit add and two corrections per limb
+    const u32 d0 = b.w[0] ? b.w[0] : 1u;
+    const u32 sh = (u32)__builtin_clz(d0);
+    const u32 dn = d0 << sh;  // 2^31 <= dn < 2^32
+    const u32 v = (u32)(0xFFFFFFFFFFFFFFFFull / dn - 0x100000000ull);
+    u32 rr = sh ? (a.w[7] >> (32u - sh)) : 0u;  // top of the shifted dividend, < 2^sh <= dn
 #pragma unroll
     for (int i = 7; i >= 0; i--) {
-      const u64 cur = ((u64)rr << 32) | a.w[i];
-      const u32 qi = (u32)(cur / d);
-      q.w[i] = qi;
-      rr = (u32)(cur - (u64)qi * d);
+      const u32 lo = i ? a.w[i - 1] : 0u;
+      const u32 ui = sh ? ((a.w[i] << sh) | (lo >> (32u - sh))) : a.w[i];
+      const u64 qq = (u64)v * rr + (((u64)rr + 1u) << 32) + ui;  // mod 2^64
+      u32 q1 = (u32)(qq >> 32);
+      const u32 q0 = (u32)qq;
+      u32 r1 = ui - q1 * dn;
+      const bool over = r1 > q0;
+      q1 = over ? q1 - 1u : q1;
+      r1 = over ? r1 + dn : r1;
+      const bool ge = r1 >= dn;
+      q1 = ge ? q1 + 1u : q1;
+      r1 = ge ? r1 - dn : r1;
+      q.w[i] = q1;
+      rr = r1;
     }
 #pragma unroll
-    for (int i = 0; i < 8; i++) r.w[i] = i ? 0u : rr;
+    for (int i = 0; i < 8; i++) r.w[i] = i ? 0u : (rr >> sh);
     return;
   }
   const u32 la = 256u - clz8(a), lb = 256u - clz8(b);

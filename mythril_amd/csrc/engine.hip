@@ -637,6 +637,7 @@ thread_local std::string g_err;
 
 struct DevProgram {
   Lowered low;
+  std::string src;  // the program bytes (key of the specialisation cache)
   bool heavy = true;  // has MUL/DIV/REM/shift/EXP/UMUL_NOOVF/KECCAK: the full interpreter
   bool uploaded = false;
   void* buf = nullptr;  // pooled device buffer holding the four arrays below
@@ -726,6 +727,16 @@ struct Engine {
   std::mutex mu;
   std::unordered_map<uint64_t, std::unique_ptr<DevJit>> jits;
   CodeCache code_cache;
+  // host-side results of the per-query passes, by input bytes (FIFO, `cache_cap` entries):
+  // LASER re-asks the same constraint sets, and a repeat then skips lowering and the two
+  // generator specialisations (mg_program_load / mg_gen_load)
+  struct SpecPair {
+    Lowered search, watch;
+  };
+  std::unordered_map<std::string, std::shared_ptr<Lowered>> lower_cache;
+  std::unordered_map<std::string, std::shared_ptr<SpecPair>> spec_cache;
+  std::deque<std::string> lower_order, spec_order;
+  size_t cache_cap = 64;
   // compile thread: source emission, comgr and the module load run off the caller's thread
   // and never take `mu` (a search holds `mu` for its whole launch + sync, back to back), so
   // searches keep launching while a query's kernel compiles (mg_jit_compile_async).  `jit_mu`
@@ -1058,9 +1069,21 @@ int mg_program_load(const uint8_t* ssa, size_t len, uint64_t* handle) {
   std::lock_guard<std::mutex> g(e.mu);
   if (!e.init) return set_err(MG_E_NOTINIT, "mg_init not called");
   auto p = std::make_unique<DevProgram>();
-  std::string err;
-  int rc = lower_program(ssa, len, p->low, err);
-  if (rc) return set_err(rc, err);
+  p->src.assign((const char*)ssa, len);
+  auto hit = e.lower_cache.find(p->src);
+  if (hit != e.lower_cache.end()) {
+    p->low = *hit->second;
+  } else {
+    std::string err;
+    int rc = lower_program(ssa, len, p->low, err);
+    if (rc) return set_err(rc, err);
+    e.lower_cache[p->src] = std::make_shared<Lowered>(p->low);
+    e.lower_order.push_back(p->src);
+    if (e.lower_order.size() > e.cache_cap) {
+      e.lower_cache.erase(e.lower_order.front());
+      e.lower_order.pop_front();
+    }
+  }
   // uploaded on first use: searches run the generator-specialised copies (mg_gen_load),
   // only explicit-coordinate evaluation runs this one
   const uint64_t h = e.next_handle++;
@@ -1117,11 +1140,27 @@ int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* g
   gg->prog = prog;
   gg->specs = specs;
   gg->consts = consts;
-  rc = specialize_program(p->low, &gg->specs, &gg->consts, gg->spec.low, err, /*keep_watch=*/false);
-  if (rc) return set_err(rc, err);
+  const std::string key = p->src + std::string((const char*)blob, n_words * 4);
+  auto hit = e.spec_cache.find(key);
+  if (hit != e.spec_cache.end()) {
+    gg->spec.low = hit->second->search;
+    gg->spec_watch.low = hit->second->watch;
+  } else {
+    rc = specialize_program(p->low, &gg->specs, &gg->consts, gg->spec.low, err, /*keep_watch=*/false);
+    if (rc) return set_err(rc, err);
+    rc = specialize_program(p->low, &gg->specs, &gg->consts, gg->spec_watch.low, err, /*keep_watch=*/true);
+    if (rc) return set_err(rc, err);
+    auto sp = std::make_shared<Engine::SpecPair>();
+    sp->search = gg->spec.low;
+    sp->watch = gg->spec_watch.low;
+    e.spec_cache[key] = sp;
+    e.spec_order.push_back(key);
+    if (e.spec_order.size() > e.cache_cap) {
+      e.spec_cache.erase(e.spec_order.front());
+      e.spec_order.pop_front();
+    }
+  }
   if ((rc = upload_code(e, gg->spec))) return rc;
-  rc = specialize_program(p->low, &gg->specs, &gg->consts, gg->spec_watch.low, err, /*keep_watch=*/true);
-  if (rc) return set_err(rc, err);
   if ((rc = upload_code(e, gg->spec_watch))) return rc;
   {  // specs | consts in one pooled buffer
     const size_t b_specs = (specs.size() * sizeof(GenSpec) + 255) & ~(size_t)255;
@@ -1370,7 +1409,12 @@ namespace mg {
 // `nblk` is the kernel's grid-size argument (the JIT kernels read no dispatch packet)
 static int jit_launch(Engine& e, hipFunction_t f, int nb, uint64_t count, void** args, uint32_t& nblk) {
   const uint64_t want = (count + 255) / 256;
-  const uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * std::max(nb, 1) * 2;
+  // resident blocks x MYTHGPU_JIT_GRID (default 2): waves loop over aligned index groups
+  static const uint64_t mult = [] {
+    const char* g = getenv("MYTHGPU_JIT_GRID");
+    return (uint64_t)std::max(1, g ? atoi(g) : 2);
+  }();
+  const uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * std::max(nb, 1) * mult;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
   nblk = grid;
   HIPCHK(hipEventRecord(e.ev0, e.stream));
@@ -1426,6 +1470,19 @@ int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_bl
 }
 
 int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle) { return mg_jit_compile_ex(prog, gen, 0, jit_handle); }
+
+int mg_cache_clear(void) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  e.lower_cache.clear();
+  e.lower_order.clear();
+  e.spec_cache.clear();
+  e.spec_order.clear();
+  std::lock_guard<std::mutex> jl(e.jit_mu);
+  e.code_cache.lru.clear();
+  e.code_cache.idx.clear();
+  return MG_OK;
+}
 
 }  // extern "C"
 

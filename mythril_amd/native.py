@@ -33,7 +33,7 @@ EXPORTS = [
     "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_info", "mg_gen_free", "mg_eval", "mg_eval_dev",
     "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
     "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_jit_compile", "mg_jit_compile_ex", "mg_jit_verdicts", "mg_jit_info",
-    "mg_jit_compile_async", "mg_jit_poll", "mg_jit_cancel",
+    "mg_jit_compile_async", "mg_jit_poll", "mg_jit_cancel", "mg_cache_clear",
     "mg_jit_free", "mg_jit_search", "mg_jit_eval", "mg_jit_eval_dev",
 ]
 
@@ -115,6 +115,7 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_jit_compile_async": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, u64p]),
             "mg_jit_poll": (C.c_int, [C.c_uint64, C.c_int32, u64p]),
             "mg_jit_cancel": (C.c_int, [C.c_uint64]),
+            "mg_cache_clear": (C.c_int, []),
             "mg_jit_free": (C.c_int, [C.c_uint64]),
             "mg_jit_search": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u64p, u64p, u32p]),
             "mg_jit_eval": (C.c_int, [C.c_uint64, u32p, C.c_uint64, u8p, u32p]),
@@ -274,6 +275,10 @@ class Engine:
 
     def jit_cancel(self, ticket: int) -> None:
         _check(self.lib.mg_jit_cancel(ticket))
+
+    def cache_clear(self) -> None:
+        """Drop the engine's host-side caches (cold-start measurements)."""
+        _check(self.lib.mg_cache_clear())
 
     def jit_verdicts(self, jit: int, seed: int, start: int, n: int) -> np.ndarray:
         """Per-candidate verdicts of the JIT kernel (compiled with ``gen_verdicts``)."""

@@ -325,8 +325,24 @@ def prepare(roots: Sequence[T.Term], gen: Optional[GenBuilder] = None):
     propagation-shaped generator."""
     P = FLATTEN_CACHE.flatten(roots)
     P.set_watch(model_watch(P)[0])
-    g = gen or default_generator(P, roots=roots)
-    return P, g.blob()
+    if gen is not None:
+        return P, gen.blob()
+    # the propagation + generator pass is a pure function of the (hash-consed) roots:
+    # LASER re-asks the same constraint set (is_possible, then the detection modules)
+    key = tuple(t.id for t in roots)
+    blob = _GEN_CACHE.get(key)
+    if blob is None:
+        blob = default_generator(P, roots=roots).blob()
+        _GEN_CACHE[key] = blob
+        if len(_GEN_CACHE) > _GEN_CACHE_MAX:
+            _GEN_CACHE.pop(next(iter(_GEN_CACHE)))
+    else:
+        _GEN_CACHE[key] = _GEN_CACHE.pop(key)  # most recent last
+    return P, blob
+
+
+_GEN_CACHE: "dict" = {}
+_GEN_CACHE_MAX = 512
 
 
 def model_from_assignment(P: ssa.Program, assign: np.ndarray):
