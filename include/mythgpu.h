@@ -210,10 +210,18 @@ typedef struct mg_stats {
   uint32_t device;
   uint32_t cu_count;
   uint32_t clock_mhz;
-  uint32_t reserved;
+  uint32_t n_devices;  /* logical devices mg_init opened (the mask's GPUs) */
 } mg_stats_t;
 
+/* device_mask: every set bit d opens GPU d (0 = GPU 0).  With several, mg_search and
+ * mg_jit_search split each call's index range over them (mg_split_range: contiguous,
+ * group-aligned slices in index order), run the slices concurrently, one stream per
+ * device, and reduce on the host (first hit = min, hits = sum); every other call runs on
+ * the first device.  Programs, generators and JIT kernels are mirrored under the same
+ * handles and uploaded to a device on first use there. */
 int mg_init(uint32_t device_mask);
+/* host-only: the slice of [start, start+count) device d of n_dev sweeps */
+int mg_split_range(uint64_t start, uint64_t count, uint32_t n_dev, uint64_t* starts, uint64_t* counts);
 void mg_shutdown(void);
 const char* mg_last_error(void);
 int mg_version(void);

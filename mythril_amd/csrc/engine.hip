@@ -662,6 +662,7 @@ struct DevGen {
 };
 
 struct DevJit {
+  std::vector<char> code;  // the code object (loaded again on the node's other devices)
   hipModule_t mod = nullptr;
   hipFunction_t fsearch = nullptr, feval = nullptr, fgen = nullptr;
   uint64_t prog = 0, gen = 0;
@@ -894,9 +895,10 @@ static uint32_t grid_for(const Engine& e, uint64_t count, bool lds, uint32_t val
   return (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
 }
 
+// enqueue one interpreter launch on e's stream (e's device must be current); bracketed by
+// e.ev0 / e.ev1 so launch_wait can time it
 template <int MODE>
-static int launch(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
-  if (count == 0) return MG_OK;
+static int launch_async(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   // GEN / SEARCH sweep whole aligned 64-index groups (k_run)
   const uint64_t lanes = MODE == MODE_EVAL ? count : (k.start + count) - (k.start & ~63ull);
   const uint32_t grid = grid_for(e, lanes, p.lds, p.low.value_words, p.heavy);
@@ -928,15 +930,28 @@ static int launch(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
     hipLaunchKernelGGL((k_run<VFGlobal, MODE, false>), dim3(grid), dim3(kWave), 0, e.stream, k);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e.ev1, e.stream));
+  return MG_OK;
+}
+
+// wait for e's last launch; its time and `count` candidates go to `st`
+static int launch_wait(Engine& e, mg_stats_t& st, uint64_t count) {
   HIPCHK(hipEventSynchronize(e.ev1));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, e.ev0, e.ev1));
-  e.stats.launches++;
-  e.stats.last_kernel_ms = ms;
-  e.stats.kernel_ms_total += ms;
-  e.stats.candidates += count;
-  e.stats.last_candidates = count;
+  st.launches++;
+  st.last_kernel_ms = ms;
+  st.kernel_ms_total += ms;
+  st.candidates += count;
+  st.last_candidates = count;
   return MG_OK;
+}
+
+template <int MODE>
+static int launch(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
+  if (count == 0) return MG_OK;
+  int rc = launch_async<MODE>(e, p, k, count);
+  if (rc) return rc;
+  return launch_wait(e, e.stats, count);
 }
 
 }  // namespace mg
@@ -949,19 +964,16 @@ int mg_version(void) { return 2; }
 
 const char* mg_last_error(void) { return g_err.c_str(); }
 
-int mg_init(uint32_t device_mask) {
-  Engine& e = E();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (e.init) return MG_OK;
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return set_err(MG_E_NODEVICE, "no HIP device");
-  int dev = -1;
-  for (int d = 0; d < n && d < 32; d++)
-    if (device_mask & (1u << d)) {
-      dev = d;
-      break;
-    }
-  if (dev < 0) dev = 0;
+}  // extern "C"
+
+namespace mg {
+
+// every logical device of the node (mg_init's mask): [0] is E(), the primary, which owns
+// the handle tables; the others mirror its programs / generators / JIT kernels under the
+// same handles and upload to their device on first use.  Guarded by E().mu.
+static std::vector<Engine*> g_devs;
+
+static int init_dev(Engine& e, int dev) {
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, dev));
   if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
@@ -978,6 +990,60 @@ int mg_init(uint32_t device_mask) {
   e.stats.cu_count = e.cu_count;
   e.stats.clock_mhz = e.clock_mhz;
   e.init = true;
+  return MG_OK;
+}
+
+static void free_dev_buffers(Engine& e);
+
+}  // namespace mg
+
+extern "C" {
+
+int mg_init(uint32_t device_mask) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (e.init) return MG_OK;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return set_err(MG_E_NODEVICE, "no HIP device");
+  std::vector<int> devs;
+  for (int d = 0; d < n && d < 32; d++)
+    if (device_mask & (1u << d)) devs.push_back(d);
+  if (devs.empty()) devs.push_back(0);
+  // MYTHGPU_VIRTUAL_DEVICES=k: k logical devices on the first physical one (own streams and
+  // buffers) — exercises the multi-device split and reduction on a one-GPU machine
+  if (const char* v = getenv("MYTHGPU_VIRTUAL_DEVICES")) {
+    const int k = std::max(1, std::min(16, atoi(v)));
+    devs.assign((size_t)k, devs[0]);
+  }
+  int rc = init_dev(e, devs[0]);
+  if (rc) return rc;
+  g_devs.assign(1, &e);
+  for (size_t i = 1; i < devs.size(); i++) {
+    Engine* s2 = new Engine;  // leaked with the process, like E()
+    rc = init_dev(*s2, devs[i]);
+    if (rc) {
+      (void)hipSetDevice(e.device);
+      return rc;
+    }
+    g_devs.push_back(s2);
+  }
+  HIPCHK(hipSetDevice(e.device));
+  e.stats.n_devices = (uint32_t)g_devs.size();
+  return MG_OK;
+}
+
+int mg_split_range(uint64_t start, uint64_t count, uint32_t n_dev, uint64_t* starts, uint64_t* counts) {
+  if (n_dev == 0 || !starts || !counts) return set_err(MG_E_INVALID, "mg_split_range: bad arguments");
+  // whole aligned 64-index groups per device (one group = one wave, GEN2 group key), in
+  // index order: device d scans the d-th contiguous slice
+  const uint64_t end = start + count, a0 = start & ~63ull;
+  const uint64_t ngroups = count ? (end - a0 + 63ull) >> 6 : 0;
+  for (uint32_t d = 0; d < n_dev; d++) {
+    const uint64_t g0 = ngroups * d / n_dev, g1 = ngroups * (d + 1) / n_dev;
+    const uint64_t lo = std::max<uint64_t>(start, a0 + 64ull * g0), hi = std::min<uint64_t>(end, a0 + 64ull * g1);
+    starts[d] = lo;
+    counts[d] = hi > lo ? hi - lo : 0;
+  }
   return MG_OK;
 }
 
@@ -998,9 +1064,28 @@ void mg_shutdown(void) {
       if (kv.second->ready) (void)hipModuleUnload(kv.second->ready->mod);
     e.tickets.clear();
   }
+  if (!e.init) {
+    for (auto& kv : e.jits) (void)hipModuleUnload(kv.second->mod);
+    e.jits.clear();
+    return;
+  }
+  for (size_t i = g_devs.size(); i-- > 0;) {
+    Engine* d = g_devs[i];
+    (void)hipSetDevice(d->device);
+    free_dev_buffers(*d);
+    if (d != &e) delete d;
+  }
+  g_devs.clear();
+}
+
+}  // extern "C"
+
+namespace mg {
+
+// every device buffer, module and stream of one logical device (its device current)
+static void free_dev_buffers(Engine& e) {
   for (auto& kv : e.jits) (void)hipModuleUnload(kv.second->mod);
   e.jits.clear();
-  if (!e.init) return;
   for (auto& kv : e.progs) free_code(e, *kv.second);
   e.progs.clear();
   for (auto& kv : e.gens) {
@@ -1025,6 +1110,10 @@ void mg_shutdown(void) {
   (void)hipStreamDestroy(e.stream);
   e.init = false;
 }
+
+}  // namespace mg
+
+extern "C" {
 
 int mg_program_check(const uint8_t* ssa, size_t len, mg_program_info_t* info) {
   Lowered low;
@@ -1087,6 +1176,11 @@ int mg_program_load(const uint8_t* ssa, size_t len, uint64_t* handle) {
   // uploaded on first use: searches run the generator-specialised copies (mg_gen_load),
   // only explicit-coordinate evaluation runs this one
   const uint64_t h = e.next_handle++;
+  for (size_t i = 1; i < g_devs.size(); i++) {  // the other devices: same handle, uploaded on use
+    auto q = std::make_unique<DevProgram>();
+    q->low = p->low;
+    g_devs[i]->progs[h] = std::move(q);
+  }
   e.progs[h] = std::move(p);
   e.stats.programs_loaded++;
   *handle = h;
@@ -1123,8 +1217,46 @@ int mg_program_free(uint64_t prog) {
   if (it == e.progs.end()) return set_err(MG_E_INVALID, "bad program handle");
   free_code(e, *it->second);
   e.progs.erase(it);
+  for (size_t i = 1; i < g_devs.size(); i++) {
+    Engine& d = *g_devs[i];
+    auto q = d.progs.find(prog);
+    if (q == d.progs.end()) continue;
+    free_code(d, *q->second);  // pooled on that device (no device call)
+    d.progs.erase(q);
+  }
   return MG_OK;
 }
+
+}  // extern "C"
+
+namespace mg {
+
+// specs | consts in one pooled buffer on e's device (current)
+static int upload_gen_consts(Engine& e, DevGen& gg) {
+  const size_t b_specs = (gg.specs.size() * sizeof(GenSpec) + 255) & ~(size_t)255;
+  const size_t total = std::max<size_t>(b_specs + gg.consts.size() * 4, 256);
+  int rc = pool_get(e, total, &gg.gbuf, &gg.gcap);
+  if (rc) return rc;
+  std::vector<uint8_t> h(total, 0);
+  std::memcpy(h.data(), gg.specs.data(), gg.specs.size() * sizeof(GenSpec));
+  std::memcpy(h.data() + b_specs, gg.consts.data(), gg.consts.size() * 4);
+  HIPCHK(hipMemcpy(gg.gbuf, h.data(), total, hipMemcpyHostToDevice));
+  gg.d_specs = (GenSpec*)gg.gbuf;
+  gg.d_consts = (uint32_t*)((uint8_t*)gg.gbuf + b_specs);
+  return MG_OK;
+}
+
+// a mirrored generator's search program + constants on device d (d's device current)
+static int ensure_gen_on(Engine& d, DevGen& gg) {
+  int rc;
+  if (!gg.spec.uploaded && (rc = upload_code(d, gg.spec))) return rc;
+  if (!gg.gbuf && (rc = upload_gen_consts(d, gg))) return rc;
+  return MG_OK;
+}
+
+}  // namespace mg
+
+extern "C" {
 
 int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* gen_handle) {
   Engine& e = E();
@@ -1162,18 +1294,17 @@ int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* g
   }
   if ((rc = upload_code(e, gg->spec))) return rc;
   if ((rc = upload_code(e, gg->spec_watch))) return rc;
-  {  // specs | consts in one pooled buffer
-    const size_t b_specs = (specs.size() * sizeof(GenSpec) + 255) & ~(size_t)255;
-    const size_t total = std::max<size_t>(b_specs + consts.size() * 4, 256);
-    if ((rc = pool_get(e, total, &gg->gbuf, &gg->gcap))) return rc;
-    std::vector<uint8_t> h(total, 0);
-    std::memcpy(h.data(), specs.data(), specs.size() * sizeof(GenSpec));
-    std::memcpy(h.data() + b_specs, consts.data(), consts.size() * 4);
-    HIPCHK(hipMemcpy(gg->gbuf, h.data(), total, hipMemcpyHostToDevice));
-    gg->d_specs = (GenSpec*)gg->gbuf;
-    gg->d_consts = (uint32_t*)((uint8_t*)gg->gbuf + b_specs);
-  }
+  if ((rc = upload_gen_consts(e, *gg))) return rc;
   const uint64_t h = e.next_handle++;
+  for (size_t i = 1; i < g_devs.size(); i++) {  // mirrored, uploaded on first use there
+    auto q = std::make_unique<DevGen>();
+    q->prog = prog;
+    q->specs = gg->specs;
+    q->consts = gg->consts;
+    q->spec.low = gg->spec.low;
+    q->spec_watch.low = gg->spec_watch.low;
+    g_devs[i]->gens[h] = std::move(q);
+  }
   e.gens[h] = std::move(gg);
   *gen_handle = h;
   return MG_OK;
@@ -1184,10 +1315,21 @@ int mg_gen_free(uint64_t gen) {
   std::lock_guard<std::mutex> g(e.mu);
   auto it = e.gens.find(gen);
   if (it == e.gens.end()) return set_err(MG_E_INVALID, "bad generator handle");
-  pool_put(e, it->second->gbuf, it->second->gcap);
-  free_code(e, it->second->spec);
-  free_code(e, it->second->spec_watch);
-  e.gens.erase(it);
+  for (size_t i = 0; i < g_devs.size(); i++) {
+    Engine& d = *g_devs[i];
+    auto q = d.gens.find(gen);
+    if (q == d.gens.end()) continue;
+    pool_put(d, q->second->gbuf, q->second->gcap);
+    free_code(d, q->second->spec);
+    free_code(d, q->second->spec_watch);
+    d.gens.erase(q);
+  }
+  if (g_devs.empty()) {
+    pool_put(e, it->second->gbuf, it->second->gcap);
+    free_code(e, it->second->spec);
+    free_code(e, it->second->spec_watch);
+    e.gens.erase(it);
+  }
   return MG_OK;
 }
 
@@ -1302,20 +1444,61 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
   if (!p) return set_err(MG_E_INVALID, "bad program handle");
   auto it = e.gens.find(gen);
   if (it == e.gens.end() || it->second->prog != prog) return set_err(MG_E_INVALID, "bad generator handle");
-  unsigned long long init[2] = {~0ull, 0ull};
-  HIPCHK(hipMemcpyAsync(e.d_hit, init, sizeof(init), hipMemcpyHostToDevice, e.stream));
-  KArgs k{};
-  k.specs = it->second->d_specs;
-  k.gconsts = it->second->d_consts;
-  k.first_hit = e.d_hit;
-  k.hits = e.d_hit + 1;
-  k.start = start;
-  k.seed = seed;
-  k.flags = flags;
-  int rc = launch<MODE_SEARCH>(e, it->second->spec, k, count);
-  if (rc) return rc;
-  unsigned long long res[2];
-  HIPCHK(hipMemcpy(res, e.d_hit, sizeof(res), hipMemcpyDeviceToHost));
+  unsigned long long res[2] = {~0ull, 0ull};
+  if (g_devs.size() > 1) {
+    // the node's devices each sweep one contiguous, group-aligned slice (mg_split_range) on
+    // their own stream; first hit = min, hits = sum over the slices (a host reduction: one
+    // 16-byte read per device, no collective needed inside one process)
+    const uint32_t nd = (uint32_t)g_devs.size();
+    std::vector<uint64_t> st(nd), ct(nd);
+    mg_split_range(start, count, nd, st.data(), ct.data());
+    int rc = MG_OK;
+    for (uint32_t d = 0; d < nd && rc == MG_OK; d++) {
+      if (!ct[d]) continue;
+      Engine& de = *g_devs[d];
+      HIPCHK(hipSetDevice(de.device));
+      DevGen& dg = *de.gens.at(gen);
+      if ((rc = ensure_gen_on(de, dg))) break;
+      unsigned long long init[2] = {~0ull, 0ull};
+      HIPCHK(hipMemcpyAsync(de.d_hit, init, sizeof(init), hipMemcpyHostToDevice, de.stream));
+      KArgs k{};
+      k.specs = dg.d_specs;
+      k.gconsts = dg.d_consts;
+      k.first_hit = de.d_hit;
+      k.hits = de.d_hit + 1;
+      k.start = st[d];
+      k.seed = seed;
+      k.flags = flags;
+      rc = launch_async<MODE_SEARCH>(de, dg.spec, k, ct[d]);
+    }
+    for (uint32_t d = 0; d < nd; d++) {
+      if (!ct[d]) continue;
+      Engine& de = *g_devs[d];
+      (void)hipSetDevice(de.device);
+      if (rc == MG_OK) rc = launch_wait(de, e.stats, ct[d]);
+      unsigned long long r[2];
+      if (rc == MG_OK && hipMemcpy(r, de.d_hit, sizeof(r), hipMemcpyDeviceToHost) == hipSuccess) {
+        res[0] = std::min(res[0], r[0]);
+        res[1] += r[1];
+      }
+    }
+    HIPCHK(hipSetDevice(e.device));
+    if (rc) return rc;
+  } else {
+    unsigned long long init[2] = {~0ull, 0ull};
+    HIPCHK(hipMemcpyAsync(e.d_hit, init, sizeof(init), hipMemcpyHostToDevice, e.stream));
+    KArgs k{};
+    k.specs = it->second->d_specs;
+    k.gconsts = it->second->d_consts;
+    k.first_hit = e.d_hit;
+    k.hits = e.d_hit + 1;
+    k.start = start;
+    k.seed = seed;
+    k.flags = flags;
+    int rc = launch<MODE_SEARCH>(e, it->second->spec, k, count);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(res, e.d_hit, sizeof(res), hipMemcpyDeviceToHost));
+  }
   if (first_hit) *first_hit = res[0];
   if (n_hits) *n_hits = res[1];
   e.stats.hits += res[1];
@@ -1379,6 +1562,7 @@ int mg_stats_reset(void) {
   e.stats.device = keep.device;
   e.stats.cu_count = keep.cu_count;
   e.stats.clock_mhz = keep.clock_mhz;
+  e.stats.n_devices = keep.n_devices;
   return MG_OK;
 }
 
@@ -1407,7 +1591,7 @@ int mg_dev_download(void* dst, const void* dptr, size_t bytes) {
 namespace mg {
 
 // `nblk` is the kernel's grid-size argument (the JIT kernels read no dispatch packet)
-static int jit_launch(Engine& e, hipFunction_t f, int nb, uint64_t count, void** args, uint32_t& nblk) {
+static int jit_launch_async(Engine& e, hipFunction_t f, int nb, uint64_t count, void** args, uint32_t& nblk) {
   const uint64_t want = (count + 255) / 256;
   // resident blocks x MYTHGPU_JIT_GRID (default 2): waves loop over aligned index groups
   static const uint64_t mult = [] {
@@ -1420,14 +1604,30 @@ static int jit_launch(Engine& e, hipFunction_t f, int nb, uint64_t count, void**
   HIPCHK(hipEventRecord(e.ev0, e.stream));
   HIPCHK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, e.stream, args, nullptr));
   HIPCHK(hipEventRecord(e.ev1, e.stream));
-  HIPCHK(hipEventSynchronize(e.ev1));
-  float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, e.ev0, e.ev1));
-  e.stats.launches++;
-  e.stats.last_kernel_ms = ms;
-  e.stats.kernel_ms_total += ms;
-  e.stats.candidates += count;
-  e.stats.last_candidates = count;
+  return MG_OK;
+}
+
+static int jit_launch(Engine& e, hipFunction_t f, int nb, uint64_t count, void** args, uint32_t& nblk) {
+  int rc = jit_launch_async(e, f, nb, count, args, nblk);
+  if (rc) return rc;
+  return launch_wait(e, e.stats, count);
+}
+
+// the JIT kernel `h` on device d: the primary's code object loaded there on first use
+static int jit_on(Engine& d, const DevJit& pj, uint64_t h, DevJit** out) {
+  auto it = d.jits.find(h);
+  if (it != d.jits.end()) {
+    *out = it->second.get();
+    return MG_OK;
+  }
+  auto j = std::make_unique<DevJit>();
+  HIPCHK(hipModuleLoadData(&j->mod, pj.code.data()));
+  if (pj.fsearch) HIPCHK(hipModuleGetFunction(&j->fsearch, j->mod, "mgj_search"));
+  j->nb_search = pj.nb_search;
+  j->prog = pj.prog;
+  j->gen = pj.gen;
+  *out = j.get();
+  d.jits[h] = std::move(j);
   return MG_OK;
 }
 
@@ -1491,6 +1691,7 @@ namespace mg {
 // load a code object as a DevJit (any thread: HIP module calls are thread-safe)
 static int load_jit(const std::vector<char>& code, const JitTicket& t, double compile_ms, std::unique_ptr<DevJit>& out) {
   auto j = std::make_unique<DevJit>();
+  j->code = code;
   HIPCHK(hipModuleLoadData(&j->mod, code.data()));
   int nb = 0;
   auto fn = [&](hipFunction_t* f, const char* name) -> int {
@@ -1715,6 +1916,14 @@ int mg_jit_free(uint64_t jit) {
   if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
   (void)hipModuleUnload(it->second->mod);
   e.jits.erase(it);
+  for (size_t i = 1; i < g_devs.size(); i++) {
+    auto q = g_devs[i]->jits.find(jit);
+    if (q == g_devs[i]->jits.end()) continue;
+    (void)hipSetDevice(g_devs[i]->device);
+    (void)hipModuleUnload(q->second->mod);
+    g_devs[i]->jits.erase(q);
+  }
+  if (g_devs.size() > 1) (void)hipSetDevice(e.device);
   return MG_OK;
 }
 
@@ -1728,19 +1937,63 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
   DevProgram* p = find_prog(e, j.prog);
   auto git = e.gens.find(j.gen);
   if (!p || git == e.gens.end() || !j.fsearch) return set_err(MG_E_INVALID, "jit was not compiled for search");
-  unsigned long long init[2] = {~0ull, 0ull};
-  HIPCHK(hipMemcpyAsync(e.d_hit, init, sizeof(init), hipMemcpyHostToDevice, e.stream));
-  const uint32_t* gconsts = git->second->d_consts;
-  unsigned long long* hitp = e.d_hit;
   uint64_t sk = seed_lane_key(seed), sg = seed_group_key(seed);
-  uint32_t nblk = 0;
-  void* args[] = {&gconsts, &start, &count, &sk, &sg, &hitp, &flags, &nblk};
-  // one wave per aligned 64-index group
-  const uint64_t lanes = (start + count) - (start & ~63ull);
-  int rc = jit_launch(e, j.fsearch, j.nb_search, lanes, args, nblk);
-  if (rc) return rc;
-  unsigned long long res[2];
-  HIPCHK(hipMemcpy(res, e.d_hit, sizeof(res), hipMemcpyDeviceToHost));
+  unsigned long long res[2] = {~0ull, 0ull};
+  if (g_devs.size() > 1) {  // as mg_search: one group-aligned slice per device, host min/sum
+    const uint32_t nd = (uint32_t)g_devs.size();
+    std::vector<uint64_t> st(nd), ct(nd);
+    mg_split_range(start, count, nd, st.data(), ct.data());
+    // kernel arguments must outlive the asynchronous launches
+    struct A {
+      const uint32_t* gconsts;
+      uint64_t start, count, sk, sg;
+      unsigned long long* hit;
+      uint32_t flags, nblk;
+    };
+    std::vector<A> a(nd);
+    int rc = MG_OK;
+    for (uint32_t d = 0; d < nd && rc == MG_OK; d++) {
+      if (!ct[d]) continue;
+      Engine& de = *g_devs[d];
+      HIPCHK(hipSetDevice(de.device));
+      DevGen& dg = *de.gens.at(j.gen);
+      if ((rc = ensure_gen_on(de, dg))) break;
+      DevJit* dj = &j;
+      if (d > 0 && (rc = jit_on(de, j, jit, &dj))) break;
+      unsigned long long init[2] = {~0ull, 0ull};
+      HIPCHK(hipMemcpyAsync(de.d_hit, init, sizeof(init), hipMemcpyHostToDevice, de.stream));
+      a[d] = A{dg.d_consts, st[d], ct[d], sk, sg, de.d_hit, flags, 0};
+      void* args[] = {&a[d].gconsts, &a[d].start, &a[d].count, &a[d].sk, &a[d].sg, &a[d].hit, &a[d].flags, &a[d].nblk};
+      const uint64_t lanes = (st[d] + ct[d]) - (st[d] & ~63ull);
+      // hipModuleLaunchKernel copies the argument values at the call (nblk is set before it)
+      rc = jit_launch_async(de, dj->fsearch, dj->nb_search, lanes, args, a[d].nblk);
+    }
+    for (uint32_t d = 0; d < nd; d++) {
+      if (!ct[d]) continue;
+      Engine& de = *g_devs[d];
+      (void)hipSetDevice(de.device);
+      if (rc == MG_OK) rc = launch_wait(de, e.stats, ct[d]);
+      unsigned long long r[2];
+      if (rc == MG_OK && hipMemcpy(r, de.d_hit, sizeof(r), hipMemcpyDeviceToHost) == hipSuccess) {
+        res[0] = std::min(res[0], r[0]);
+        res[1] += r[1];
+      }
+    }
+    HIPCHK(hipSetDevice(e.device));
+    if (rc) return rc;
+  } else {
+    unsigned long long init[2] = {~0ull, 0ull};
+    HIPCHK(hipMemcpyAsync(e.d_hit, init, sizeof(init), hipMemcpyHostToDevice, e.stream));
+    const uint32_t* gconsts = git->second->d_consts;
+    unsigned long long* hitp = e.d_hit;
+    uint32_t nblk = 0;
+    void* args[] = {&gconsts, &start, &count, &sk, &sg, &hitp, &flags, &nblk};
+    // one wave per aligned 64-index group
+    const uint64_t lanes = (start + count) - (start & ~63ull);
+    int rc = jit_launch(e, j.fsearch, j.nb_search, lanes, args, nblk);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(res, e.d_hit, sizeof(res), hipMemcpyDeviceToHost));
+  }
   if (first_hit) *first_hit = res[0];
   if (n_hits) *n_hits = res[1];
   e.stats.hits += res[1];

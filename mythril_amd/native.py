@@ -33,7 +33,7 @@ EXPORTS = [
     "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_info", "mg_gen_free", "mg_eval", "mg_eval_dev",
     "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
     "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_jit_compile", "mg_jit_compile_ex", "mg_jit_verdicts", "mg_jit_info",
-    "mg_jit_compile_async", "mg_jit_poll", "mg_jit_cancel", "mg_cache_clear",
+    "mg_jit_compile_async", "mg_jit_poll", "mg_jit_cancel", "mg_cache_clear", "mg_split_range",
     "mg_jit_free", "mg_jit_search", "mg_jit_eval", "mg_jit_eval_dev",
 ]
 
@@ -62,7 +62,7 @@ class Stats(C.Structure):
         ("programs_loaded", C.c_uint64), ("launches", C.c_uint64), ("candidates", C.c_uint64),
         ("hits", C.c_uint64), ("kernel_ms_total", C.c_double), ("last_kernel_ms", C.c_double),
         ("last_candidates", C.c_uint64), ("device", C.c_uint32), ("cu_count", C.c_uint32),
-        ("clock_mhz", C.c_uint32), ("reserved", C.c_uint32),
+        ("clock_mhz", C.c_uint32), ("n_devices", C.c_uint32),
     ]
 
 
@@ -116,6 +116,7 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_jit_poll": (C.c_int, [C.c_uint64, C.c_int32, u64p]),
             "mg_jit_cancel": (C.c_int, [C.c_uint64]),
             "mg_cache_clear": (C.c_int, []),
+            "mg_split_range": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, u64p, u64p]),
             "mg_jit_free": (C.c_int, [C.c_uint64]),
             "mg_jit_search": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u64p, u64p, u32p]),
             "mg_jit_eval": (C.c_int, [C.c_uint64, u32p, C.c_uint64, u8p, u32p]),
@@ -178,8 +179,31 @@ def jit_source(blob: bytes, gen_blob: Optional[np.ndarray] = None, compile: bool
     return buf.value.decode()
 
 
+def split_range(start: int, count: int, n_dev: int):
+    """Host-only ``mg_split_range``: the [start, start+count) slice each of ``n_dev`` devices
+    sweeps in a multi-device ``mg_search`` — [(start_d, count_d)] in device order."""
+    lib = load_library()
+    st = (C.c_uint64 * max(n_dev, 1))()
+    ct = (C.c_uint64 * max(n_dev, 1))()
+    _check(lib.mg_split_range(start, count, n_dev, st, ct))
+    return [(st[i], ct[i]) for i in range(n_dev)]
+
+
+def device_mask_from_env() -> int:
+    """``MYTHGPU_DEVICES``: "all" or a comma list of GPU indices opens several GPUs in this
+    process (the shim splits every search over them); otherwise one GPU,
+    ``MYTHGPU_DEVICE`` / ``LOCAL_RANK`` (one process per GPU, the torch.distributed layout)."""
+    spec = os.environ.get("MYTHGPU_DEVICES")
+    if spec:
+        if spec.strip() == "all":
+            return 0xFFFFFFFF
+        return sum(1 << int(x) for x in spec.split(",") if x.strip())
+    return 1 << int(os.environ.get("MYTHGPU_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
 class Engine:
-    """Process-wide handle on one GPU (one process per GPU)."""
+    """Process-wide handle on the engine: one GPU (one process per GPU), or every GPU of
+    ``MYTHGPU_DEVICES`` with searches split across them inside the shim."""
 
     _instance = None
     _ilock = threading.Lock()
@@ -191,12 +215,23 @@ class Engine:
                 cls._instance = Engine()
             return cls._instance
 
-    def __init__(self, device: Optional[int] = None):
+    def __init__(self, device: Optional[int] = None, mask: Optional[int] = None):
         self.lib = load_library()
-        if device is None:
-            device = int(os.environ.get("MYTHGPU_DEVICE", os.environ.get("LOCAL_RANK", "0")))
-        _check(self.lib.mg_init(1 << device))
-        self.device = device
+        if mask is None:
+            mask = (1 << device) if device is not None else device_mask_from_env()
+        _check(self.lib.mg_init(mask))
+        self.mask = mask
+        self.device = (mask & -mask).bit_length() - 1 if mask else 0
+
+    def reinit(self, mask: int) -> None:
+        """Shut the engine down (every handle becomes invalid) and open ``mask`` instead."""
+        self.lib.mg_shutdown()
+        _check(self.lib.mg_init(mask))
+        self.mask = mask
+
+    @property
+    def n_devices(self) -> int:
+        return self.stats().n_devices
 
     # programs -------------------------------------------------------
     def load(self, blob: bytes) -> int:

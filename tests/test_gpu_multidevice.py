@@ -1,0 +1,67 @@
+"""Multi-device search inside the shim (no torch.distributed): mg_init with several devices
+splits every mg_search / mg_jit_search over them (mg_split_range) and reduces on the host.
+The box has one MI355X, so MYTHGPU_VIRTUAL_DEVICES=k opens k logical devices on it (own
+streams, buffers, mirrored handles, per-device JIT module loads) — the same split,
+mirroring and reduction code as k physical GPUs.  The first hit and hit count must equal
+the single-device engine's on every workload, interpreter and JIT."""
+import os
+
+import pytest
+
+from mythril_amd import search, workloads
+
+pytestmark = pytest.mark.gpu
+
+NAMES = ["token_transfer_underflow", "bectoken_batch_overflow", "walletlibrary_kill", "sha3_keyed_mapping"]
+
+
+def _run(engine, P, blob, windows, jit):
+    prog = engine.load(P.to_bytes())
+    gh = engine.load_gen(prog, blob)
+    out = []
+    try:
+        jh = engine.jit_compile(prog, gh) if jit else None
+        for (s, n, early) in windows:
+            if jh is not None:
+                out.append(engine.jit_search(jh, 7, s, n, early_exit=early))
+            else:
+                out.append(engine.search(prog, gh, 7, s, n, early_exit=early))
+        if jh is not None:
+            engine.jit_free(jh)
+    finally:
+        engine.free_gen(gh)
+        engine.free(prog)
+    return out
+
+
+def test_full_mask_and_virtual_devices_same_hits(engine):
+    windows = [(0, 1 << 22, True), (0, 1 << 22, False), (12345, (1 << 21) + 77, False), (1 << 33, 1 << 20, True),
+               (5, 3, False)]
+    cases = []
+    for name in NAMES:
+        roots = [c.raw for c in workloads.WORKLOADS[name]()]
+        P, blob = search.prepare(roots)
+        cases.append((name, P, blob))
+    single = {(name, jit): _run(engine, P, blob, windows, jit) for name, P, blob in cases for jit in (False, True)}
+    old_mask = engine.mask
+    try:
+        # every device of the box (one MI355X here): the multi-device code path with one slice
+        engine.reinit(0xFFFFFFFF)
+        for name, P, blob in cases:
+            for jit in (False, True):
+                assert _run(engine, P, blob, windows, jit) == single[(name, jit)], (name, jit, "full mask")
+        # four logical devices on it: four slices per call, host min / sum
+        os.environ["MYTHGPU_VIRTUAL_DEVICES"] = "4"
+        engine.reinit(1 << engine.device)
+        assert engine.n_devices == 4
+        for name, P, blob in cases:
+            for jit in (False, True):
+                assert _run(engine, P, blob, windows, jit) == single[(name, jit)], (name, jit, "4 devices")
+        # the search loop and the model read-back on top of it
+        roots = [c.raw for c in workloads.WORKLOADS["token_transfer_underflow"]()]
+        r = search.search(engine, roots, timeout_s=10, jit="never")
+        assert r.index is not None and r.model[0] == 1
+    finally:
+        os.environ.pop("MYTHGPU_VIRTUAL_DEVICES", None)
+        engine.reinit(old_mask)
+    assert engine.n_devices == 1

@@ -183,3 +183,30 @@ def test_same_name_two_sorts_is_unsupported():
         ssa.flatten([(f1(y) == 1).raw, (f2(y) == 1).raw])
     # one name at one sort used many times is fine
     assert len(ssa.flatten([roots[1], T.eq(x256, x256)]).scalar_coords()) == 1
+
+
+@pytest.mark.parametrize("start,count,n", [(0, 1 << 20, 4), (13, 100_000, 3), (64, 64, 8), (5, 3, 4), (0, 0, 2),
+                                           (1 << 40, (1 << 26) + 7, 8), (63, 2, 2), (100, 1, 1)])
+def test_split_range_chunk_to_device(lib, start, count, n):
+    """mg_split_range (the multi-device mg_search / mg_jit_search split): contiguous slices
+    in device order that tile [start, start+count) exactly, boundaries on aligned 64-index
+    groups (one wave's group key: a group is never shared by two devices), balanced to
+    within one group."""
+    sl = native.split_range(start, count, n)
+    assert len(sl) == n
+    pos = start
+    sizes = []
+    for s0, c in sl:
+        if c == 0:
+            continue
+        assert s0 == pos  # contiguous, in order
+        if s0 != start:
+            assert s0 % 64 == 0
+        pos = s0 + c
+        groups = ((s0 + c - 1) >> 6) - (s0 >> 6) + 1
+        sizes.append(groups)
+    assert pos == start + count
+    if sizes:
+        assert max(sizes) - min(sizes) <= 2
+    with pytest.raises(native.EngineError):
+        native.split_range(0, 10, 0)
