@@ -23,9 +23,11 @@ def _run(engine, P, blob, windows, jit):
         jh = engine.jit_compile(prog, gh) if jit else None
         for (s, n, early) in windows:
             if jh is not None:
-                out.append(engine.jit_search(jh, 7, s, n, early_exit=early))
+                r = engine.jit_search(jh, 7, s, n, early_exit=early)
             else:
-                out.append(engine.search(prog, gh, 7, s, n, early_exit=early))
+                r = engine.search(prog, gh, 7, s, n, early_exit=early)
+            # with early exit the hit count depends on when waves see the first hit
+            out.append(r[0] if early else r)
         if jh is not None:
             engine.jit_free(jh)
     finally:
