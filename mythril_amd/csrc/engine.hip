@@ -358,8 +358,13 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
                                                 bool early, bool active) {
   uint32_t verdict = 1;
   const uint32_t n_instr = k.n_instr;
+  // the next instruction's scalar load is issued before this one executes, so its latency
+  // overlaps this instruction's LDS traffic instead of adding to it (the code buffer has
+  // one padding record after the last instruction)
+  Instr nx = ld_instr(k, 0);
   for (uint32_t pc = 0; pc < n_instr; pc++) {
-    const Instr in = ld_instr(k, pc);
+    const Instr in = nx;
+    nx = ld_instr(k, pc + 1);
     const uint32_t W = in.wd;
     const uint32_t L = (W + 31) >> 5;
     switch (in.op) {
@@ -751,12 +756,17 @@ struct Engine {
   bool init = false;
   int device = -1;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   int cu_count = 0, clock_mhz = 0;
   uint64_t next_handle = 1;
   std::unordered_map<uint64_t, std::unique_ptr<DevProgram>> progs;
   std::unordered_map<uint64_t, std::unique_ptr<DevGen>> gens;
   unsigned long long* d_hit = nullptr;  // [0] first hit, [1] hit count
+  // pinned host staging: [0..1] the reset values, [2..3] the result (async copies on `stream`,
+  // one event wait per call instead of two blocking hipMemcpy round trips)
+  unsigned long long* h_hit = nullptr;
+  uint32_t* h_watch1 = nullptr;  // pinned copy of d_watch1
+  size_t h_watch1_words = 0;
   uint32_t* d_scratch = nullptr;
   size_t scratch_bytes = 0;
   // device buffers of freed programs/generators, by capacity: a query's uploads reuse them
@@ -828,7 +838,8 @@ static int upload_code(Engine& e, DevProgram& p) {
     }
   }
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const size_t b_code = al(p.low.code.size() * sizeof(Instr)), b_consts = al(p.low.consts.size() * 4),
+  // one zeroed Instr past the end: the interpreter prefetches instruction pc + 1
+  const size_t b_code = al((p.low.code.size() + 1) * sizeof(Instr)), b_consts = al(p.low.consts.size() * 4),
                b_aux = al(p.low.aux.size() * 4), b_cw = al(p.low.coord_width.size() * 4);
   const size_t total = std::max<size_t>(b_code + b_consts + b_aux + b_cw, 256);
   int rc = pool_get(e, total, &p.buf, &p.cap);
@@ -946,6 +957,36 @@ static int launch_wait(Engine& e, mg_stats_t& st, uint64_t count) {
   return MG_OK;
 }
 
+// reset e's hit buffer before a search launch (async, from pinned memory)
+static int arm_hits(Engine& e) {
+  e.h_hit[0] = ~0ull;
+  e.h_hit[1] = 0ull;
+  HIPCHK(hipMemcpyAsync(e.d_hit, e.h_hit, 2 * sizeof(unsigned long long), hipMemcpyHostToDevice, e.stream));
+  return MG_OK;
+}
+
+// queue the hit buffer's read-back behind e's last launch (async); collect_hits waits for it
+static int fetch_hits(Engine& e) {
+  HIPCHK(hipMemcpyAsync(e.h_hit + 2, e.d_hit, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e.stream));
+  HIPCHK(hipEventRecord(e.ev2, e.stream));
+  return MG_OK;
+}
+
+// one wait for launch + read-back; the kernel's time (ev0 -> ev1) and `count` go to `st`
+static int collect_hits(Engine& e, mg_stats_t& st, uint64_t count, unsigned long long res[2]) {
+  HIPCHK(hipEventSynchronize(e.ev2));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e.ev0, e.ev1));
+  st.launches++;
+  st.last_kernel_ms = ms;
+  st.kernel_ms_total += ms;
+  st.candidates += count;
+  st.last_candidates = count;
+  res[0] = e.h_hit[2];
+  res[1] = e.h_hit[3];
+  return MG_OK;
+}
+
 template <int MODE>
 static int launch(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   if (count == 0) return MG_OK;
@@ -979,10 +1020,15 @@ static int init_dev(Engine& e, int dev) {
   if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
     return set_err(MG_E_NODEVICE, std::string("device is ") + prop.gcnArchName + ", engine is built for gfx950");
   HIPCHK(hipSetDevice(dev));
+  // the host waits on every search result: spin instead of sleeping on an interrupt (a
+  // no-op when the device's context already exists, e.g. torch created it first)
+  (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
   HIPCHK(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreate(&e.ev0));
   HIPCHK(hipEventCreate(&e.ev1));
+  HIPCHK(hipEventCreateWithFlags(&e.ev2, hipEventDisableTiming));
   HIPCHK(hipMalloc((void**)&e.d_hit, 2 * sizeof(unsigned long long)));
+  HIPCHK(hipHostMalloc((void**)&e.h_hit, 4 * sizeof(unsigned long long), hipHostMallocDefault));
   e.device = dev;
   e.cu_count = prop.multiProcessorCount;
   e.clock_mhz = prop.clockRate / 1000;
@@ -1105,8 +1151,14 @@ static void free_dev_buffers(Engine& e) {
   e.d_scratch = nullptr;
   e.scratch_bytes = 0;
   (void)hipFree(e.d_hit);
+  if (e.h_hit) (void)hipHostFree(e.h_hit);
+  if (e.h_watch1) (void)hipHostFree(e.h_watch1);
+  e.h_hit = nullptr;
+  e.h_watch1 = nullptr;
+  e.h_watch1_words = 0;
   (void)hipEventDestroy(e.ev0);
   (void)hipEventDestroy(e.ev1);
+  (void)hipEventDestroy(e.ev2);
   (void)hipStreamDestroy(e.stream);
   e.init = false;
 }
@@ -1430,9 +1482,19 @@ static int read_assignment(Engine& e, DevGen& g, uint64_t seed, uint64_t idx, ui
   k.watch = e.d_watch1;
   k.start = idx;
   k.seed = seed;
-  int rc = launch<MODE_GEN>(e, g.spec_watch, k, 1);
+  if (ww > e.h_watch1_words) {
+    if (e.h_watch1) (void)hipHostFree(e.h_watch1);
+    e.h_watch1 = nullptr;
+    e.h_watch1_words = 0;
+    HIPCHK(hipHostMalloc((void**)&e.h_watch1, (size_t)ww * 4, hipHostMallocDefault));
+    e.h_watch1_words = ww;
+  }
+  int rc = launch_async<MODE_GEN>(e, g.spec_watch, k, 1);
   if (rc) return rc;
-  HIPCHK(hipMemcpy(assign_out, e.d_watch1, (size_t)ww * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpyAsync(e.h_watch1, e.d_watch1, (size_t)ww * 4, hipMemcpyDeviceToHost, e.stream));
+  HIPCHK(hipEventRecord(e.ev2, e.stream));
+  HIPCHK(hipEventSynchronize(e.ev2));
+  std::memcpy(assign_out, e.h_watch1, (size_t)ww * 4);
   return MG_OK;
 }
 
@@ -1459,8 +1521,7 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
       HIPCHK(hipSetDevice(de.device));
       DevGen& dg = *de.gens.at(gen);
       if ((rc = ensure_gen_on(de, dg))) break;
-      unsigned long long init[2] = {~0ull, 0ull};
-      HIPCHK(hipMemcpyAsync(de.d_hit, init, sizeof(init), hipMemcpyHostToDevice, de.stream));
+      if ((rc = arm_hits(de))) break;
       KArgs k{};
       k.specs = dg.d_specs;
       k.gconsts = dg.d_consts;
@@ -1470,14 +1531,15 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
       k.seed = seed;
       k.flags = flags;
       rc = launch_async<MODE_SEARCH>(de, dg.spec, k, ct[d]);
+      if (rc == MG_OK) rc = fetch_hits(de);
     }
     for (uint32_t d = 0; d < nd; d++) {
       if (!ct[d]) continue;
       Engine& de = *g_devs[d];
       (void)hipSetDevice(de.device);
-      if (rc == MG_OK) rc = launch_wait(de, e.stats, ct[d]);
       unsigned long long r[2];
-      if (rc == MG_OK && hipMemcpy(r, de.d_hit, sizeof(r), hipMemcpyDeviceToHost) == hipSuccess) {
+      if (rc == MG_OK) rc = collect_hits(de, e.stats, ct[d], r);
+      if (rc == MG_OK) {
         res[0] = std::min(res[0], r[0]);
         res[1] += r[1];
       }
@@ -1485,8 +1547,6 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
     HIPCHK(hipSetDevice(e.device));
     if (rc) return rc;
   } else {
-    unsigned long long init[2] = {~0ull, 0ull};
-    HIPCHK(hipMemcpyAsync(e.d_hit, init, sizeof(init), hipMemcpyHostToDevice, e.stream));
     KArgs k{};
     k.specs = it->second->d_specs;
     k.gconsts = it->second->d_consts;
@@ -1495,9 +1555,14 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
     k.start = start;
     k.seed = seed;
     k.flags = flags;
-    int rc = launch<MODE_SEARCH>(e, it->second->spec, k, count);
-    if (rc) return rc;
-    HIPCHK(hipMemcpy(res, e.d_hit, sizeof(res), hipMemcpyDeviceToHost));
+    if (count) {
+      int rc = arm_hits(e);
+      if (!rc) rc = launch_async<MODE_SEARCH>(e, it->second->spec, k, count);
+      if (!rc) rc = fetch_hits(e);
+      if (!rc) rc = collect_hits(e, e.stats, count, res);
+      if (rc) return rc;
+    }
+
   }
   if (first_hit) *first_hit = res[0];
   if (n_hits) *n_hits = res[1];
@@ -1960,21 +2025,21 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
       if ((rc = ensure_gen_on(de, dg))) break;
       DevJit* dj = &j;
       if (d > 0 && (rc = jit_on(de, j, jit, &dj))) break;
-      unsigned long long init[2] = {~0ull, 0ull};
-      HIPCHK(hipMemcpyAsync(de.d_hit, init, sizeof(init), hipMemcpyHostToDevice, de.stream));
+      if ((rc = arm_hits(de))) break;
       a[d] = A{dg.d_consts, st[d], ct[d], sk, sg, de.d_hit, flags, 0};
       void* args[] = {&a[d].gconsts, &a[d].start, &a[d].count, &a[d].sk, &a[d].sg, &a[d].hit, &a[d].flags, &a[d].nblk};
       const uint64_t lanes = (st[d] + ct[d]) - (st[d] & ~63ull);
       // hipModuleLaunchKernel copies the argument values at the call (nblk is set before it)
       rc = jit_launch_async(de, dj->fsearch, dj->nb_search, lanes, args, a[d].nblk);
+      if (rc == MG_OK) rc = fetch_hits(de);
     }
     for (uint32_t d = 0; d < nd; d++) {
       if (!ct[d]) continue;
       Engine& de = *g_devs[d];
       (void)hipSetDevice(de.device);
-      if (rc == MG_OK) rc = launch_wait(de, e.stats, ct[d]);
       unsigned long long r[2];
-      if (rc == MG_OK && hipMemcpy(r, de.d_hit, sizeof(r), hipMemcpyDeviceToHost) == hipSuccess) {
+      if (rc == MG_OK) rc = collect_hits(de, e.stats, ct[d], r);
+      if (rc == MG_OK) {
         res[0] = std::min(res[0], r[0]);
         res[1] += r[1];
       }
@@ -1982,17 +2047,17 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
     HIPCHK(hipSetDevice(e.device));
     if (rc) return rc;
   } else {
-    unsigned long long init[2] = {~0ull, 0ull};
-    HIPCHK(hipMemcpyAsync(e.d_hit, init, sizeof(init), hipMemcpyHostToDevice, e.stream));
     const uint32_t* gconsts = git->second->d_consts;
     unsigned long long* hitp = e.d_hit;
     uint32_t nblk = 0;
     void* args[] = {&gconsts, &start, &count, &sk, &sg, &hitp, &flags, &nblk};
     // one wave per aligned 64-index group
     const uint64_t lanes = (start + count) - (start & ~63ull);
-    int rc = jit_launch(e, j.fsearch, j.nb_search, lanes, args, nblk);
+    int rc = arm_hits(e);
+    if (!rc) rc = jit_launch_async(e, j.fsearch, j.nb_search, lanes, args, nblk);
+    if (!rc) rc = fetch_hits(e);
+    if (!rc) rc = collect_hits(e, e.stats, lanes, res);
     if (rc) return rc;
-    HIPCHK(hipMemcpy(res, e.d_hit, sizeof(res), hipMemcpyDeviceToHost));
   }
   if (first_hit) *first_hit = res[0];
   if (n_hits) *n_hits = res[1];

@@ -151,7 +151,7 @@ struct Gen {
             << " const uint32_t mag = 1u + (h & 1u); const bool sb = (h >> 1) & 1u;"
             << " const uint32_t a0 = sb ? 0u - mag : mag, ah = sb ? 0xFFFFFFFFu : 0u; uint32_t cy = 0u;";
           for (uint32_t j = 0; j < L; j++)
-            o << " " << lim(j) << " = __builtin_addc(" << lim(j) << ", " << (j ? "ah" : "a0") << ", cy, &cy);";
+            o << " " << lim(j) << " = mg_addc(" << lim(j) << ", " << (j ? "ah" : "a0") << ", cy, &cy);";
           o << " (void)cy; (void)ah; }\n";
         }
         if (width & 31) o << "  " << lim(L - 1) << " &= " << hex(topmask(width)) << ";\n";
@@ -160,14 +160,14 @@ struct Gen {
           const uint32_t span = G[r + L];
           o << "  { uint32_t br = 0u, hz = 0u, t0;";
           for (uint32_t j = 0; j < L; j++) {
-            if (j == 0) o << " t0 = __builtin_subc(" << lim(0) << ", " << hex(G[r]) << ", br, &br);";
-            else o << " hz |= __builtin_subc(" << lim(j) << ", " << hex(G[r + j]) << ", br, &br);";
+            if (j == 0) o << " t0 = mg_subc(" << lim(0) << ", " << hex(G[r]) << ", br, &br);";
+            else o << " hz |= mg_subc(" << lim(j) << ", " << hex(G[r + j]) << ", br, &br);";
           }
           o << " if (br | hz" << (span ? " | (uint32_t)(t0 >= " + hex(span) + ")" : std::string("")) << ") {"
             << " const uint32_t off = " << (span ? "(uint32_t)(((uint64_t)" + lim(0) + " * " + std::to_string(span) + "ull) >> 32)" : lim(0))
             << "; uint32_t cy = 0u;";
           for (uint32_t j = 0; j < L; j++)
-            o << " " << lim(j) << " = __builtin_addc(" << hex(G[r + j]) << ", " << (j ? "0u" : "off") << ", cy, &cy);";
+            o << " " << lim(j) << " = mg_addc(" << hex(G[r + j]) << ", " << (j ? "0u" : "off") << ", cy, &cy);";
           o << " (void)cy; } }\n";
         }
         break;
@@ -187,7 +187,7 @@ struct Gen {
           << (sp.p[1] ? ("(uint32_t)(((uint64_t)r * " + std::to_string(sp.p[1]) + "ull) >> 32)") : std::string("r"))
           << "; uint32_t cy = 0u;\n";
         for (uint32_t j = 0; j < L; j++)
-          o << "  " << lim(j) << " = __builtin_addc(" << hex(G[sp.p[0] + j]) << ", " << (j ? "0u" : "off")
+          o << "  " << lim(j) << " = mg_addc(" << hex(G[sp.p[0] + j]) << ", " << (j ? "0u" : "off")
             << ", cy, &cy);\n";
         o << "  (void)cy;\n";
         break;
@@ -203,7 +203,7 @@ struct Gen {
           if (bit0 <= -32 || bit0 >= 64) mw = "0u";
           else if (bit0 < 0) mw = "(uint32_t)(m << " + std::to_string(-bit0) + ")";
           else mw = "(uint32_t)(m >> " + std::to_string(bit0) + ")";
-          o << "  " << lim(j) << " = __builtin_addc(" << hex(G[sp.p[0] + j]) << ", " << mw << ", cy, &cy);\n";
+          o << "  " << lim(j) << " = mg_addc(" << hex(G[sp.p[0] + j]) << ", " << mw << ", cy, &cy);\n";
         }
         o << "  (void)cy;\n";
         break;
@@ -240,39 +240,74 @@ struct Gen {
   }
   static uint32_t topmask(uint32_t w) { return (w & 31) ? ((1u << (w & 31)) - 1u) : 0xFFFFFFFFu; }
 
-  // 32 bits of value id starting at bit p (zero above width w)
-  // Expression for bits [p, p+need) of value `id` (width w) in its low bits.
-  // Bits of the expression at k >= need are either the value's bit p+k or 0, and
-  // are 0 above the value's width; need = 32 therefore gives an exact limb.
-  // Looks through CONCAT / ZEXT / EXTRACT definitions down to their operands, so
-  // a left-folded Concat of 32 calldata bytes costs O(32) shifts, not O(32^2).
-  std::string bits(uint32_t id, uint32_t w, uint32_t p, int need = 32, int depth = 0) const {
-    if (p >= w || need <= 0) return "0u";
+  // Bits [p, p+need) of value `id` (width w) as an expression in the low bits, zero above
+  // `need` (bits at or above a value's width are zero by invariant).  Looks through CONCAT /
+  // ZEXT / EXTRACT definitions down to their operands and literals, collecting pieces
+  // (source value, source bit, length, destination bit); pieces that continue each other in
+  // the same source merge, so a calldata word re-assembled from 32 byte-Extracts of one
+  // 256-bit AUX word is one funnel shift per limb (v_alignbit_b32), and literal pieces fold
+  // into one immediate.
+  struct Piece {
+    uint32_t id, w, p, n, sh;  // id == MG_NONE: literal bits `p` (already shifted to 0)
+  };
+  void collect(uint32_t id, uint32_t w, uint32_t p, uint32_t need, uint32_t sh, int depth,
+               std::vector<Piece>& out) const {
+    if (p >= w || need == 0) return;
+    need = std::min(need, w - p);
     const Instr* d = def_of(id);
     if (d && depth < 96) {
       if (d->op == K_CONCAT) {
         const uint32_t wb = d->p1, wa = w - wb;
-        if (p >= wb) return bits(d->a, wa, p - wb, need, depth + 1);
-        if (p + (uint32_t)need <= wb) return bits(d->b, wb, p, need, depth + 1);
-        const uint32_t sft = wb - p;
-        const std::string lo = bits(d->b, wb, p, (int)sft, depth + 1);
-        const std::string hi = bits(d->a, wa, 0, need - (int)sft, depth + 1);
-        if (hi == "0u") return lo;
-        return "(" + lo + " | (" + hi + " << " + std::to_string(sft) + "))";
+        if (p >= wb) return collect(d->a, wa, p - wb, need, sh, depth + 1, out);
+        const uint32_t nlo = std::min(need, wb - p);
+        collect(d->b, wb, p, nlo, sh, depth + 1, out);
+        if (need > nlo) collect(d->a, wa, 0, need - nlo, sh + nlo, depth + 1, out);
+        return;
       }
-      if (d->op == K_ZEXT) return bits(d->a, d->p1, p, need, depth + 1);
-      if (d->op == K_EXTRACT) {
-        std::string e = bits(d->a, d->p1, d->p0 + p, need, depth + 1);
-        if (p + 32 > w && e != "0u") e = "(" + e + " & " + hex(topmask(w - p)) + ")";
-        return e;
+      if (d->op == K_ZEXT) return collect(d->a, d->p1, p, need, sh, depth + 1, out);
+      if (d->op == K_EXTRACT) return collect(d->a, d->p1, d->p0 + p, need, sh, depth + 1, out);
+      if (const uint32_t* c = lit(id)) {
+        const uint32_t q = p >> 5, r = p & 31, L = Lw(w);
+        uint32_t x = c[q] >> r;
+        if (r && q + 1 < L) x |= c[q + 1] << (32 - r);
+        if (need < 32) x &= (1u << need) - 1u;
+        out.push_back({MG_NONE, 0, x, need, sh});
+        return;
       }
     }
-    const uint32_t q = p >> 5, r = p & 31;
-    const uint32_t L = Lw(w);
-    if (r == 0) return v(id, q);
-    std::string lo = "(" + v(id, q) + " >> " + std::to_string(r) + ")";
-    if (q + 1 < L && need > (int)(32 - r)) lo = "(" + lo + " | (" + v(id, q + 1) + " << " + std::to_string(32 - r) + "))";
-    return lo;
+    out.push_back({id, w, p, need, sh});
+  }
+
+  std::string bits(uint32_t id, uint32_t w, uint32_t p, int need = 32) const {
+    std::vector<Piece> ps;
+    collect(id, w, p, (uint32_t)std::max(need, 0), 0, 0, ps);
+    std::vector<Piece> m;
+    uint32_t litv = 0;
+    for (const Piece& q : ps) {
+      if (q.id == MG_NONE) {
+        litv |= q.sh < 32 ? q.p << q.sh : 0u;
+        continue;
+      }
+      if (!m.empty() && m.back().id == q.id && m.back().p + m.back().n == q.p && m.back().sh + m.back().n == q.sh) {
+        m.back().n += q.n;
+        continue;
+      }
+      m.push_back(q);
+    }
+    std::string e;
+    for (const Piece& q : m) {
+      const uint32_t qq = q.p >> 5, r = q.p & 31, L = Lw(q.w);
+      std::string x;
+      if (r == 0) x = v(q.id, qq);
+      else if (qq + 1 < L && q.n > 32 - r)
+        x = "__builtin_amdgcn_alignbit(" + v(q.id, qq + 1) + ", " + v(q.id, qq) + ", " + std::to_string(r) + ")";
+      else x = "(" + v(q.id, qq) + " >> " + std::to_string(r) + ")";
+      if (q.n < 32 && q.p + q.n < q.w) x = "(" + x + " & " + hex((1u << q.n) - 1u) + ")";
+      if (q.sh) x = "(" + x + " << " + std::to_string(q.sh) + ")";
+      e = e.empty() ? x : "(" + e + " | " + x + ")";
+    }
+    if (litv) e = e.empty() ? hex(litv) : "(" + e + " | " + hex(litv) + ")";
+    return e.empty() ? "0u" : e;
   }
 
   // x <op> c / c <op> x with a literal c that fits in limb 0 (and, for signed
@@ -340,7 +375,7 @@ struct Gen {
         // carry / borrow chain: one v_add_co / v_addc_co (v_sub_co / v_subb_co) per limb
         o << "  { uint32_t c = 0u;";
         for (uint32_t j = 0; j < L; j++)
-          o << " " << v(d, j) << " = " << (sub ? "__builtin_subc(" : "__builtin_addc(") << v(in.a, j) << ", "
+          o << " " << v(d, j) << " = " << (sub ? "mg_subc(" : "mg_addc(") << v(in.a, j) << ", "
             << v(in.b, j) << ", c, &c);";
         o << " (void)c; }\n";
         mask_top(d);
@@ -348,7 +383,7 @@ struct Gen {
       }
       case K_NEG: {
         o << "  { uint32_t c = 0u;";
-        for (uint32_t j = 0; j < L; j++) o << " " << v(d, j) << " = __builtin_subc(0u, " << v(in.a, j) << ", c, &c);";
+        for (uint32_t j = 0; j < L; j++) o << " " << v(d, j) << " = mg_subc(0u, " << v(in.a, j) << ", c, &c);";
         o << " (void)c; }\n";
         mask_top(d);
         break;
@@ -385,7 +420,7 @@ struct Gen {
             x = "(" + x + " ^ " + flip + ")";
             y = "(" + y + " ^ " + flip + ")";
           }
-          o << " nz |= __builtin_subc(" << x << ", " << y << ", br, &br);";
+          o << " nz |= mg_subc(" << x << ", " << y << ", br, &br);";
         }
         if (in.op == K_ULT || in.op == K_SLT)
           o << " " << v(d, 0) << " = (uint32_t)br; (void)nz; }\n";
@@ -393,23 +428,10 @@ struct Gen {
           o << " " << v(d, 0) << " = (uint32_t)(br != 0 || nz == 0); }\n";
         break;
       }
-      case K_CONCAT: {
-        const uint32_t wb = in.p1, wa = W - wb;
-        for (uint32_t j = 0; j < L; j++) {
-          const uint32_t p = 32 * j;
-          std::string e = bits(in.b, wb, p);
-          if (p + 32 > wb) {
-            std::string hi = p >= wb ? bits(in.a, wa, p - wb) : "(" + bits(in.a, wa, 0) + " << " + std::to_string(wb - p) + ")";
-            e = "(" + e + " | " + hi + ")";
-          }
-          o << "  " << v(d, j) << " = " << e << ";\n";
-        }
-        mask_top(d);
-        break;
-      }
+      case K_CONCAT:
       case K_EXTRACT:
-        for (uint32_t j = 0; j < L; j++) o << "  " << v(d, j) << " = " << bits(in.a, in.p1, in.p0 + 32 * j) << ";\n";
-        mask_top(d);
+        // through the value's own definition: bits() merges the pieces across both operands
+        for (uint32_t j = 0; j < L; j++) o << "  " << v(d, j) << " = " << bits(d, W, 32 * j) << ";\n";
         break;
       case K_ZEXT: {
         const uint32_t La = Lw(in.p1);
@@ -460,9 +482,25 @@ struct Gen {
       case K_LOOKUP: {
         const uint32_t Lk = Lw(in.b), n = in.c;
         for (uint32_t j = 0; j < L; j++) o << "  " << v(d, j) << " = " << v(in.p0, j) << ";\n";
-        // first match wins: apply the priors from last to first
+        // first match wins: apply the priors from last to first.  MYTHGPU_JIT_LOOKUP_GATE=1:
+        // limb 0 decides for the whole wave first (one compare and a ballot) and the full
+        // compare + select runs only when some lane's limb 0 matches — measured no faster on
+        // C1-C4 (their keys coincide in some lane of most waves), so off by default.
+        static const bool gate = [] {
+          const char* g = getenv("MYTHGPU_JIT_LOOKUP_GATE");
+          return g && g[0] == '1';
+        }();
         for (int32_t p = (int32_t)n - 1; p >= 0; p--) {
           const uint32_t kv = P.vaux[in.p1 + 2 * p], vv = P.vaux[in.p1 + 2 * p + 1];
+          if (gate && Lk > 1) {
+            o << "  { const bool h0 = " << v(in.a, 0) << " == " << v(kv, 0) << ";";
+            o << " if (__builtin_amdgcn_ballot_w64(h0)) { const bool h = h0 && (0u";
+            for (uint32_t j = 1; j < Lk; j++) o << " | (" << v(in.a, j) << " ^ " << v(kv, j) << ")";
+            o << ") == 0u;";
+            for (uint32_t j = 0; j < L; j++) o << " " << v(d, j) << " = h ? " << v(vv, j) << " : " << v(d, j) << ";";
+            o << " } }\n";
+            continue;
+          }
           o << "  { const bool h = (0u";
           for (uint32_t j = 0; j < Lk; j++) o << " | (" << v(in.a, j) << " ^ " << v(kv, j) << ")";
           o << ") == 0u;";

@@ -9,6 +9,31 @@
 
 namespace mg {
 
+// add / subtract with carry for the emitted carry chains.  Default: the hardware carry
+// (v_add_co / v_addc_co through VCC).  MG_VGPR_CARRY: the carry as a 0/1 VGPR value —
+// s = a + b + c (v_add3_u32), carry-out = bit 31 of (a & b) | ((a | b) & ~s) (one v_bitop3_b32,
+// table 0xD4) — which has no VALU-writes-SGPR -> VALU-reads hazard between links.
+__device__ __forceinline__ uint32_t mg_addc(uint32_t a, uint32_t b, uint32_t ci, uint32_t* co) {
+#ifdef MG_VGPR_CARRY
+  const uint32_t s = a + b + ci;
+  *co = __builtin_amdgcn_bitop3_b32(a, b, s, 0xD4) >> 31;
+  return s;
+#else
+  return __builtin_addc(a, b, ci, co);
+#endif
+}
+
+// borrow-out = bit 31 of (~a & b) | (~(a ^ b) & d) (table 0x8E)
+__device__ __forceinline__ uint32_t mg_subc(uint32_t a, uint32_t b, uint32_t bi, uint32_t* bo) {
+#ifdef MG_VGPR_CARRY
+  const uint32_t d = a - b - bi;
+  *bo = __builtin_amdgcn_bitop3_b32(a, b, d, 0x8E) >> 31;
+  return d;
+#else
+  return __builtin_subc(a, b, bi, bo);
+#endif
+}
+
 // Keccak-256 of the LEN big-endian bytes of an L-limb value (LEN >= 1)
 template <int L, int LEN>
 __device__ __forceinline__ void keccak_value(const uint32_t (&in)[L], uint32_t (&out)[8]) {

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Throughput of one workload's JIT kernel under compiler / launch variants (GPU box).
-#   tools/jit_sweep.sh <workload> -> gpurun_out/sweep_<workload>.jsonl
-W=${1:-token_transfer_underflow}
+#   tools/jit_sweep.sh <workload> [label=ENV=value ...] -> gpurun_out/sweep_<workload>.jsonl
+W=${1:-token_transfer_underflow}; shift
 O=gpurun_out/sweep_$W.jsonl
 mkdir -p gpurun_out; : > $O
 run() {  # label, env...
@@ -9,10 +9,13 @@ run() {  # label, env...
   env "$@" AMD_COMGR_CACHE=0 timeout -k 10 120 python bench.py --workload $W --no-cpu-baseline --no-ttfm --no-stream --steps 20 > /tmp/sw.json 2>/tmp/sw.err || { echo "{\"label\": \"$label\", \"error\": true}" >> $O; return 0; }
   python3 -c "import json,sys; d=json.load(open('/tmp/sw.json')); print(json.dumps({'label': sys.argv[1], 'value': d['value'], 'kernel_ms': d['roofline']['kernel_ms'], 'compile_ms': d['config']['jit_compile_ms_cold']}))" "$label" >> $O
 }
-run base
-run grid1 MYTHGPU_JIT_GRID=1
-run grid4 MYTHGPU_JIT_GRID=4
-run maxilp "MYTHGPU_JIT_EXTRA=-mllvm --amdgpu-sched-strategy=max-ilp"
-run O2 MYTHGPU_JIT_OPT=2
-run wpe4 "MYTHGPU_JIT_EXTRA=-mllvm -amdgpu-waves-per-eu=4"
+if [ $# -eq 0 ]; then
+  run base
+  run grid1 MYTHGPU_JIT_GRID=1
+  run maxilp "MYTHGPU_JIT_EXTRA=-mllvm --amdgpu-sched-strategy=max-ilp"
+  run O2 MYTHGPU_JIT_OPT=2
+else
+  run base
+  for v in "$@"; do run "${v%%=*}" "${v#*=}"; done
+fi
 cat $O
