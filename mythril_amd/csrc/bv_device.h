@@ -184,11 +184,13 @@ __device__ __forceinline__ void udivrem_nb(const W8& rem0, const W8& quo0, u32 n
 }
 
 // q, r of a / b for b != 0 (b == 0: the callers substitute the SMT-LIB results).
-// Wave-uniform limb count of the divisor (ballot) picks the path: a one-limb divisor
-// runs limb-serial long division by reciprocal, wider ones the bit-serial loop above
-// with an NB-limb remainder.
+// Per lane: a one-limb divisor takes limb-serial long division by reciprocal; a wider one the
+// bit-serial loop above, with the remainder width chosen by a ballot over just those lanes.
+// The branch is divergent on purpose: in a wave that mixes small and wide divisors each path
+// runs for its own lanes only, so a small divisor (hundreds of quotient bits) never drags the
+// wide-divisor lanes' loop count up, and vice versa.
 __device__ __forceinline__ void udivrem8(const W8& a, const W8& b, W8& q, W8& r) {
-  if (!__builtin_amdgcn_ballot_w64((b.w[1] | b.w[2] | b.w[3] | b.w[4] | b.w[5] | b.w[6] | b.w[7]) != 0u)) {
+  if ((b.w[1] | b.w[2] | b.w[3] | b.w[4] | b.w[5] | b.w[6] | b.w[7]) == 0u) {
     // one-limb divisor: normalised long division, one 2/1 step per limb with the divisor's
     // reciprocal computed once (Moller & Granlund, "Improved division by invariant
     // integers", IEEE TC 2011, Alg. 4): a multiply, a 64-bit add and two corrections per limb
@@ -216,31 +218,26 @@ __device__ __forceinline__ void udivrem8(const W8& a, const W8& b, W8& q, W8& r)
     }
 #pragma unroll
     for (int i = 0; i < 8; i++) r.w[i] = i ? 0u : (rr >> sh);
-    return;
-  }
-  const u32 la = 256u - clz8(a), lb = 256u - clz8(b);
-  const u32 n = la >= lb ? la - lb + 1u : 0u;  // quotient bits (<= 256)
-  W8 rem0, quo0;
-  if (n == 0) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) rem0.w[i] = quo0.w[i] = 0;
   } else {
-    if (n >= 256u) {  // b == 1 beside wider divisors in the wave
+    const u32 la = 256u - clz8(a), lb = 256u - clz8(b);
+    const u32 n = la >= lb ? la - lb + 1u : 0u;  // quotient bits (<= 255 here: lb > 32)
+    W8 rem0, quo0;
+    if (n == 0) {
 #pragma unroll
-      for (int i = 0; i < 8; i++) rem0.w[i] = 0;
+      for (int i = 0; i < 8; i++) rem0.w[i] = quo0.w[i] = 0;
     } else {
       rem0 = shr8(a, n, 0u);
+      quo0 = shl8(a, 256u - n);
     }
-    quo0 = shl8(a, 256u - n);
+    if (__builtin_amdgcn_ballot_w64((b.w[4] | b.w[5] | b.w[6] | b.w[7]) != 0u)) {
+      udivrem_nb<8>(rem0, quo0, n, b, q, r);
+    } else if (__builtin_amdgcn_ballot_w64((b.w[2] | b.w[3]) != 0u)) {
+      udivrem_nb<4>(rem0, quo0, n, b, q, r);
+    } else {
+      udivrem_nb<2>(rem0, quo0, n, b, q, r);
+    }
+    if (n == 0) r = a;  // a < b: q = 0, r = a
   }
-  if (__builtin_amdgcn_ballot_w64((b.w[4] | b.w[5] | b.w[6] | b.w[7]) != 0u)) {
-    udivrem_nb<8>(rem0, quo0, n, b, q, r);
-  } else if (__builtin_amdgcn_ballot_w64((b.w[2] | b.w[3]) != 0u)) {
-    udivrem_nb<4>(rem0, quo0, n, b, q, r);
-  } else {
-    udivrem_nb<2>(rem0, quo0, n, b, q, r);
-  }
-  if (n == 0) r = a;  // a < b: q = 0, r = a
 }
 
 // SMT-LIB bvudiv / bvurem with the total-division convention

@@ -35,6 +35,10 @@ __device__ __forceinline__ uint32_t xor3_32(uint32_t a, uint32_t b, uint32_t c) 
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+__device__ __forceinline__ uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+  return mk64(xor3_32(lo32(a), lo32(b), lo32(c)), xor3_32(hi32(a), hi32(b), hi32(c)));
+}
+
 __device__ __forceinline__ uint64_t xor5(uint64_t a, uint64_t b, uint64_t c, uint64_t d, uint64_t e) {
   return mk64(xor3_32(xor3_32(lo32(a), lo32(b), lo32(c)), lo32(d), lo32(e)),
               xor3_32(xor3_32(hi32(a), hi32(b), hi32(c)), hi32(d), hi32(e)));
@@ -54,11 +58,15 @@ __device__ __forceinline__ void keccak_f1600(uint64_t (&a)[25]) {
     const uint64_t c2 = xor5(a[2], a[7], a[12], a[17], a[22]);
     const uint64_t c3 = xor5(a[3], a[8], a[13], a[18], a[23]);
     const uint64_t c4 = xor5(a[4], a[9], a[14], a[19], a[24]);
-    const uint64_t d0 = c4 ^ rol64(c1, 1), d1 = c0 ^ rol64(c2, 1), d2 = c1 ^ rol64(c3, 1),
-                   d3 = c2 ^ rol64(c4, 1), d4 = c3 ^ rol64(c0, 1);
+    // a[x] ^= C[x-1] ^ rot(C[x+1], 1): one 3-input XOR per half instead of forming D first
+    const uint64_t r0 = rol64(c0, 1), r1 = rol64(c1, 1), r2 = rol64(c2, 1), r3 = rol64(c3, 1), r4 = rol64(c4, 1);
 #pragma unroll
     for (int y = 0; y < 25; y += 5) {
-      a[y + 0] ^= d0; a[y + 1] ^= d1; a[y + 2] ^= d2; a[y + 3] ^= d3; a[y + 4] ^= d4;
+      a[y + 0] = xor3_64(a[y + 0], c4, r1);
+      a[y + 1] = xor3_64(a[y + 1], c0, r2);
+      a[y + 2] = xor3_64(a[y + 2], c1, r3);
+      a[y + 3] = xor3_64(a[y + 3], c2, r4);
+      a[y + 4] = xor3_64(a[y + 4], c3, r0);
     }
     // rho + pi: b[y, 2x+3y] = rot(a[x, y], r[x, y]) — unrolled along the pi cycle
     uint64_t t = a[1], u;
