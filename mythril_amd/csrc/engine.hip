@@ -654,8 +654,16 @@ struct DevProgram {
   bool lds = false;
 };
 
+// host-side specialisations of one (program, generator) pair, shared through the cache
+struct SpecSet {
+  Lowered search, watch;
+  std::shared_ptr<Lowered> model;  // watch list only, asserts dropped: built on the first hit
+};
+
 struct DevGen {
   uint64_t prog = 0;
+  std::shared_ptr<SpecSet> set;   // (primary) where the model-only variant is cached
+  DevProgram spec_model;          // that variant, uploaded on the first model read-back
   std::vector<GenSpec> specs;     // host copies: the JIT specialises on them
   std::vector<uint32_t> consts;
   GenSpec* d_specs = nullptr;
@@ -736,11 +744,8 @@ struct Engine {
   // host-side results of the per-query passes, by input bytes (FIFO, `cache_cap` entries):
   // LASER re-asks the same constraint sets, and a repeat then skips lowering and the two
   // generator specialisations (mg_program_load / mg_gen_load)
-  struct SpecPair {
-    Lowered search, watch;
-  };
   std::unordered_map<std::string, std::shared_ptr<Lowered>> lower_cache;
-  std::unordered_map<std::string, std::shared_ptr<SpecPair>> spec_cache;
+  std::unordered_map<std::string, std::shared_ptr<SpecSet>> spec_cache;
   std::deque<std::string> lower_order, spec_order;
   size_t cache_cap = 64;
   // compile thread: source emission, comgr and the module load run off the caller's thread
@@ -1138,6 +1143,7 @@ static void free_dev_buffers(Engine& e) {
     pool_put(e, kv.second->gbuf, kv.second->gcap);
     free_code(e, kv.second->spec);
     free_code(e, kv.second->spec_watch);
+    free_code(e, kv.second->spec_model);
   }
   e.gens.clear();
   for (auto& kv : e.pool) (void)hipFree(kv.second);
@@ -1329,14 +1335,16 @@ int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* g
   if (hit != e.spec_cache.end()) {
     gg->spec.low = hit->second->search;
     gg->spec_watch.low = hit->second->watch;
+    gg->set = hit->second;
   } else {
     rc = specialize_program(p->low, &gg->specs, &gg->consts, gg->spec.low, err, /*keep_watch=*/false);
     if (rc) return set_err(rc, err);
     rc = specialize_program(p->low, &gg->specs, &gg->consts, gg->spec_watch.low, err, /*keep_watch=*/true);
     if (rc) return set_err(rc, err);
-    auto sp = std::make_shared<Engine::SpecPair>();
+    auto sp = std::make_shared<SpecSet>();
     sp->search = gg->spec.low;
     sp->watch = gg->spec_watch.low;
+    gg->set = sp;
     e.spec_cache[key] = sp;
     e.spec_order.push_back(key);
     if (e.spec_order.size() > e.cache_cap) {
@@ -1374,12 +1382,14 @@ int mg_gen_free(uint64_t gen) {
     pool_put(d, q->second->gbuf, q->second->gcap);
     free_code(d, q->second->spec);
     free_code(d, q->second->spec_watch);
+    free_code(d, q->second->spec_model);
     d.gens.erase(q);
   }
   if (g_devs.empty()) {
     pool_put(e, it->second->gbuf, it->second->gcap);
     free_code(e, it->second->spec);
     free_code(e, it->second->spec_watch);
+    free_code(e, it->second->spec_model);
     e.gens.erase(it);
   }
   return MG_OK;
@@ -1467,6 +1477,24 @@ int mg_eval_generated(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start
 static int read_assignment(Engine& e, DevGen& g, uint64_t seed, uint64_t idx, uint32_t* assign_out) {
   const uint32_t ww = g.spec_watch.low.watch_words;
   if (ww == 0) return MG_OK;
+  // the model of a known hit: the watch list's slice of the program only (no asserts), a
+  // shorter single-candidate pass than the full keep_watch program
+  if (!g.spec_model.uploaded) {
+    if (!g.set || !g.set->model) {
+      DevProgram* p = find_prog(e, g.prog);
+      if (!p) return set_err(MG_E_INVALID, "bad program handle");
+      auto m = std::make_shared<Lowered>();
+      std::string err;
+      int rc = specialize_program(p->low, &g.specs, &g.consts, *m, err, /*keep_watch=*/true, /*keep_asserts=*/false);
+      if (rc) return set_err(rc, err);
+      if (!g.set) g.set = std::make_shared<SpecSet>();
+      g.set->model = m;
+    }
+    g.spec_model.low = *g.set->model;
+    int rc = upload_code(e, g.spec_model);
+    if (rc) return rc;
+  }
+  if (g.spec_model.low.watch_words != ww) return set_err(MG_E_INVALID, "internal: model read-back layout");
   if (ww > e.watch1_words) {
     if (e.d_watch1) (void)hipFree(e.d_watch1);
     e.d_watch1 = nullptr;
@@ -1489,7 +1517,7 @@ static int read_assignment(Engine& e, DevGen& g, uint64_t seed, uint64_t idx, ui
     HIPCHK(hipHostMalloc((void**)&e.h_watch1, (size_t)ww * 4, hipHostMallocDefault));
     e.h_watch1_words = ww;
   }
-  int rc = launch_async<MODE_GEN>(e, g.spec_watch, k, 1);
+  int rc = launch_async<MODE_GEN>(e, g.spec_model, k, 1);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(e.h_watch1, e.d_watch1, (size_t)ww * 4, hipMemcpyDeviceToHost, e.stream));
   HIPCHK(hipEventRecord(e.ev2, e.stream));

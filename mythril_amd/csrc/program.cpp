@@ -1204,7 +1204,7 @@ namespace mg {
 // Verdicts are unchanged for every generated candidate (tests compare the specialised
 // interpreter and JIT kernels with the C restatement, which runs the full program).
 int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
-                       Lowered& out, std::string& err, bool keep_watch) {
+                       Lowered& out, std::string& err, bool keep_watch, bool keep_asserts) {
   try {
     const uint32_t NONE = MG_NONE;
     Analysis A(in, specs, gconsts);
@@ -1247,11 +1247,12 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
       }
       code.push_back(std::move(v));
     }
-    // dead code: keep asserts, watches and whatever they transitively use
+    // dead code: keep asserts (unless dropped: the model read-back of a known hit), watches
+    // and whatever they transitively use
     std::vector<char> live(nv, 0), keep(code.size(), 0);
     for (size_t k = code.size(); k-- > 0;) {
       const VInstr& c = code[k];
-      const bool side = c.op == K_ASSERT || (c.op == K_WATCH && keep_watch);
+      const bool side = (c.op == K_ASSERT && keep_asserts) || (c.op == K_WATCH && keep_watch);
       if (!side && (c.dst == NONE || c.dst >= nv || !live[c.dst])) continue;
       keep[k] = 1;
       auto use = [&](uint32_t x) {

@@ -77,9 +77,11 @@ uint64_t op_cost(uint32_t node_op, uint32_t width, uint32_t operand_width);
 // for explicit coordinates: range-decided compares folded, aliases renamed, dead code
 // removed, slots re-allocated.  Same verdicts for every candidate the generator draws.
 // keep_watch = false drops the K_WATCH instructions (and what only they used): the
-// search variant; the model read-back (MODE_GEN) runs the keep_watch variant.
+// search variant; per-candidate verdicts with the model (mg_eval_generated) run the
+// keep_watch variant.  keep_asserts = false also drops the asserts: the model read-back of a
+// candidate already known to satisfy them evaluates only what the watch list needs.
 int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
-                       Lowered& out, std::string& err, bool keep_watch = true);
+                       Lowered& out, std::string& err, bool keep_watch = true, bool keep_asserts = true);
 
 // Validate a generator blob against a lowered program; fills specs/consts.
 int parse_gen(const Lowered& prog, const uint32_t* blob, size_t n_words, std::vector<GenSpec>& specs,
