@@ -53,8 +53,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="token_transfer_underflow")
-    ap.add_argument("--candidates", type=int, default=1 << 26,
-                    help="candidates per GPU per step (~5 ms on C2, so the per-step RCCL exchange is amortised)")
+    ap.add_argument("--candidates", type=int, default=1 << 28,
+                    help="candidates per GPU per step (~3 ms on C2, so the per-step host sync and RCCL "
+                         "exchange cost ~1-2 %% of a step)")
     ap.add_argument("--seed", type=int, default=0x6D797468)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -558,6 +558,22 @@ struct Gen {
   // aliases are renamed away and dead instructions are gone
   void body(bool search) {
     coord_var.clear();  // generated-coordinate names are per kernel
+    // MYTHGPU_JIT_GEN_ONLY=1 (diagnostic, search kernels): only the candidate generator, its
+    // limbs folded into the verdict so none is dead — the generator's share of the kernel time
+    static const bool gen_only = [] {
+      const char* g = getenv("MYTHGPU_JIT_GEN_ONLY");
+      return g && g[0] == '1';
+    }();
+    if (search && gen_only) {
+      o << "  { uint32_t fold_ = 0u;\n";
+      for (const Instr& in : P.vcode) {
+        if (in.op != K_COORD) continue;
+        emit(in, true, false);
+        for (uint32_t j = 0; j < Lw(in.wd); j++) o << "  fold_ ^= " << v(in.dst, j) << ";\n";
+      }
+      o << "  verdict &= (uint32_t)(fold_ == 0x9E3779B9u); }\n";
+      return;
+    }
     for (const Instr& in : P.vcode) emit(in, search, !search);
   }
 };

@@ -8,7 +8,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 W=${1:-token_transfer_underflow}
 E=${2:-jit}
-N=${3:-67108864}
+N=${3:-268435456}
 if [ "$E" = "jit" ]; then D=gpurun_out/prof_$W; K=mgj_search; else D=gpurun_out/prof_${W}_$E; K=k_run; fi
 rm -rf $D && mkdir -p $D
 B="python3 bench.py --workload $W --engine $E --candidates $N --no-cpu-baseline --no-ttfm --no-stream"
