@@ -122,7 +122,7 @@ enum mg_op {
 enum mg_coord_kind { MG_COORD_SCALAR = 0, MG_COORD_ARRAY_SITE = 1, MG_COORD_UF_SITE = 2, MG_COORD_AUX = 3 };
 enum mg_table_kind { MG_TABLE_ARRAY = 0, MG_TABLE_UF = 1 };
 
-/* ---- candidate generator (search mode), format GEN2 -------------------- *
+/* ---- candidate generator (search mode), format GEN3 -------------------- *
  * blob: header[4] {MG_GEN_MAGIC, n_coords, n_const_words, 0}
  *       specs: n_coords x 8 words {kind, p0, p1, p2, p3, p4, p5, p6}
  *       consts: n_const_words
@@ -130,20 +130,24 @@ enum mg_table_kind { MG_TABLE_ARRAY = 0, MG_TABLE_UF = 1 };
  * Coordinate c of candidate i is a pure function of (seed, i, c).  Two keys:
  *   fmix64(x)   = x ^= x>>33; x *= 0xFF51AFD7ED558CCD; x ^= x>>33;
  *                 x *= 0xC4CEB9FE1A85EC53; x ^= x>>33        (a bijection of u64)
- *   lane key    K = fmix64(i ^ fmix64(seed ^ 0x6A09E667F3BCC908))        (K_lo, K_hi)
  *   group key   G = fmix64((i >> 6) ^ fmix64(seed ^ 0xBB67AE8584CAA73B)) (G_lo, G_hi)
- * K is distinct for every index, so no two indices of one seed draw the same
- * candidate (all 2^64 indices are usable).  G is shared by the 64 consecutive
- * indices of one aligned group — exactly one wave of the search kernels — so a
- * choice made from G is wave-uniform (a scalar branch, not a per-lane select).
+ *   lane key    K = G ^ fmix64((i & 63) ^ fmix64(seed ^ 0x6A09E667F3BCC908))  (K_lo, K_hi)
+ * G is a bijection of the group number and K of the lane within a group, so the
+ * pair (G, K) is distinct for every index (all 2^64 indices are usable).  G is
+ * shared by the 64 consecutive indices of one aligned group — exactly one wave of
+ * the search kernels — so a choice made from G is wave-uniform (a scalar branch,
+ * not a per-lane select); the lane half of K is a per-thread constant.
  *   salt(c, j)  = c*0x9E3779B9 + j*0x85EBCA6B + 0x27D4EB2F           (mod 2^32)
- *   fin(x)      = x ^= x>>16; x *= 0x7FEB352D; x ^= x>>15
+ *   fin(x)      = x ^= x>>16; x = (x & 0xFFFFFF) * 0x9E3779; x ^= x>>15  (mod 2^32)
  *   rnd(c, j)   = fin(K_lo ^ salt(c, j)) + K_hi      per-lane 32 random bits
  *   h(c)        = rnd(c, 0xFFFF)                     per-lane index / delta bits
  *   wsel(c)     = fin(G_lo ^ salt(c, 0xFFFE)) + G_hi per-group choice bits
+ *   raw uniform limbs u_0 = rnd(c, 0), u_1 = rnd(c, 1),
+ *               u_j = lo32((u_{j-1} : u_{j-2}) >> s_j) + u_{j-2}  (mod 2^32, j >= 2),
+ *               s_j = (7j + 3) mod 31 + 1
  *
  * Kinds (L = ceil(w/32) limbs; every value is masked to its width w):
- *   UNIFORM  limb j = rnd(c, j)
+ *   UNIFORM  limb j = u_j
  *   RANGE    lo + (((u64)rnd(c,0) * span) >> 32) (span 0: + rnd(c,0)), carried over L limbs
  *   DICT     entry ((h(c) >> 16) * n) >> 16 of the n-entry table
  *   ALIGNED  lo + (m << p1), m = ((u64)rnd(c,0) * count) >> 32 (count 0: m = rnd(c,0))
@@ -153,7 +157,7 @@ enum mg_table_kind { MG_TABLE_ARRAY = 0, MG_TABLE_UF = 1 };
  *              pc = P(copy) if p3 != MG_NONE else 0, pd = P(dict) if n else 0, ps = P(small)
  *              s < pc            COPY     the FINAL value of coordinate p3 (p3 < c, same width)
  *              s < pc+pd         DICT     entry ((h(c) >> 16) * n) >> 16
- *              s < pc+pd+ps      SMALL    UNIFORM masked to min(w, small_bits) bits
+ *              s < pc+pd+ps      SMALL    UNIFORM (u_j) masked to min(w, small_bits) bits
  *              otherwise         UNIFORM
  *            narrow coordinates (w <= MG_GEN_NARROW_BITS) take UNIFORM / SMALL from
  *            h(c) & 0xFFFF (one hash each);
@@ -165,7 +169,7 @@ enum mg_table_kind { MG_TABLE_ARRAY = 0, MG_TABLE_UF = 1 };
  * Finally every kind applies its fixed-bit record (kind bits 8..31).
  * Probabilities are 16-bit fixed point (/65536).
  */
-#define MG_GEN_MAGIC 0x324E4547u /* "GEN2" */
+#define MG_GEN_MAGIC 0x334E4547u /* "GEN3" */
 #define MG_GEN_NARROW_BITS 16u
 #define MG_GEN_MAX_COPY_DEPTH 64u  /* longest static COPY chain a generator may hold */
 enum mg_gen_kind {

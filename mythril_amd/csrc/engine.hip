@@ -71,7 +71,7 @@ struct KArgs {
   unsigned long long* first_hit;
   unsigned long long* hits;
   uint64_t start, count, seed, stride;
-  uint64_t sk, sg;           // GEN2 seed keys (seed_lane_key / seed_group_key of seed)
+  uint64_t sk, sg;           // GEN3 seed keys (seed_lane_key / seed_group_key of seed)
   uint32_t n_instr, value_words, flags, pad;
 };
 
@@ -114,7 +114,7 @@ struct VFGlobal {
 };
 
 // ---------------------------------------------------------------------------
-// candidate generator, GEN2 (include/mythgpu.h): a pure function of (seed, index,
+// candidate generator, GEN3 (include/mythgpu.h): a pure function of (seed, index,
 // coordinate); the same function as oracle/bveval.c gen_value and the JIT's
 // straight-line gen_value (jit.cpp), checked candidate by candidate by the tests
 // ---------------------------------------------------------------------------
@@ -173,17 +173,30 @@ __device__ __forceinline__ void gen_base(const KArgs& k, const VF& vf, uint32_t 
       } else {  // SMALL / UNIFORM
         const bool narrow = width <= MG_GEN_NARROW_BITS;
         const uint32_t bits = alt == ALT_SMALL ? min(width, s.p[4] >> 16) : width;
+        uint32_t u1 = 0, u2 = 0;  // raw limbs j-1, j-2 (GEN3 gext chain)
         for (uint32_t j = 0; j < L; j++) {
-          const uint32_t v = narrow ? (j == 0 ? (h & 0xFFFFu) : 0u) : grnd(ky, c, j);
           const uint32_t lo = j * 32;
+          uint32_t v = 0;
+          if (lo < bits) {  // limbs past `bits` are zero, and no later limb needs their raw value
+            v = narrow ? (j == 0 ? (h & 0xFFFFu) : 0u) : j < 2 ? grnd(ky, c, j) : gext(u1, u2, j);
+            u2 = u1;
+            u1 = v;
+          }
           vf.at(dst + j) = lo >= bits ? 0u : (bits - lo >= 32 ? v : (v & ((1u << (bits - lo)) - 1u)));
         }
       }
       break;
     }
-    default:  // UNIFORM (and LAZY coordinates, which the program never reads)
-      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = grnd(ky, c, j);
+    default: {  // UNIFORM (and LAZY coordinates, which the program never reads)
+      uint32_t u1 = 0, u2 = 0;
+      for (uint32_t j = 0; j < L; j++) {
+        const uint32_t v = j < 2 ? grnd(ky, c, j) : gext(u1, u2, j);
+        vf.at(dst + j) = v;
+        u2 = u1;
+        u1 = v;
+      }
       break;
+    }
   }
 }
 
@@ -557,13 +570,16 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
   extern __shared__ uint32_t lds[];
   VF vf(lds, k);
   // EVAL sweeps rows [0, count); GEN / SEARCH sweep the aligned 64-index groups that
-  // cover [start, start + count), one group per wave (the GEN2 group key is per wave)
+  // cover [start, start + count), one group per wave (the GEN3 group key is per wave)
   const uint64_t a0 = (MODE == MODE_EVAL) ? 0ull : (k.start & ~63ull);
   const uint64_t end = k.start + k.count;
   const uint64_t total = (MODE == MODE_EVAL) ? k.count : (end - a0);
   const uint64_t step = (uint64_t)gridDim.x * kWave;
   const bool early = (MODE == MODE_SEARCH) && (k.flags & MG_SEARCH_EARLY_EXIT);
   uint64_t wave_best = ~0ull, wave_hits = 0;  // wave-uniform; published once per wave
+  // idx & 63 == threadIdx.x & 63 below (a0 and base are multiples of 64): the lane half of
+  // the GEN3 lane key is fixed per thread
+  const uint64_t lk = (MODE == MODE_EVAL) ? 0ull : gen_lane_key(threadIdx.x & 63u, k.sk);
   for (uint64_t base = (uint64_t)blockIdx.x * kWave; base < total; base += step) {
     const uint64_t off = base + threadIdx.x;
     const uint64_t idx = a0 + off;  // candidate index (GEN / SEARCH)
@@ -579,7 +595,7 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
       if (a0 + base >= cur_u) break;
     }
     GKeys key{};
-    if (MODE != MODE_EVAL) key = gen_keys(idx, k.sk, k.sg);
+    if (MODE != MODE_EVAL) key = gen_keys_lk(idx, lk, k.sg);
     uint32_t v = run_program<VF, MODE, HEAVY>(k, vf, i, key, early, active);
     v = active ? v : 0u;
     if (MODE == MODE_SEARCH) {
@@ -1085,7 +1101,7 @@ int mg_init(uint32_t device_mask) {
 
 int mg_split_range(uint64_t start, uint64_t count, uint32_t n_dev, uint64_t* starts, uint64_t* counts) {
   if (n_dev == 0 || !starts || !counts) return set_err(MG_E_INVALID, "mg_split_range: bad arguments");
-  // whole aligned 64-index groups per device (one group = one wave, GEN2 group key), in
+  // whole aligned 64-index groups per device (one group = one wave, GEN3 group key), in
   // index order: device d scans the d-th contiguous slice
   const uint64_t end = start + count, a0 = start & ~63ull;
   const uint64_t ngroups = count ? (end - a0 + 63ull) >> 6 : 0;

@@ -1,11 +1,13 @@
-// GEN2 candidate-generator primitives (format in include/mythgpu.h), shared by the
+// GEN3 candidate-generator primitives (format in include/mythgpu.h), shared by the
 // interpreter kernels (engine.hip), the JIT prelude (jit.cpp -> hipRTC) and the host
 // (seed keys are folded once per launch on the CPU and passed as kernel arguments).
 //
 // Two keys per candidate index i:
-//   K = fmix64(i ^ SK)        per lane: limb / index / delta bits
-//   G = fmix64((i >> 6) ^ SG) per aligned group of 64 indices = one wave: the MIXED
-//                             alternative, so the choice is a scalar (SGPR) branch
+//   G = fmix64((i >> 6) ^ SG)      per aligned group of 64 indices = one wave: the MIXED
+//                                  alternative, so the choice is a scalar (SGPR) branch
+//   K = G ^ fmix64((i & 63) ^ SK)  per lane: limb / index / delta bits.  The lane half
+//                                  depends on the lane only, so a kernel computes it once
+//                                  and pays one 64-bit XOR per group (GEN2 hashed i itself)
 #pragma once
 
 namespace mg {
@@ -26,26 +28,44 @@ __host__ __device__ __forceinline__ uint32_t gsalt(uint32_t c, uint32_t j) {
   return c * 0x9E3779B9u + j * 0x85EBCA6Bu + 0x27D4EB2Fu;
 }
 
+// xorshift-multiply-xorshift; the multiply takes 24 bits (v_mul_u32_u24, a full-rate VALU
+// op; the 32-bit v_mul_lo_u32 issues at a quarter of the rate).  Every input bit still
+// reaches the product: bits 24..31 come in through x ^ (x >> 16).
 __host__ __device__ __forceinline__ uint32_t gfin(uint32_t x) {
   x ^= x >> 16;
-  x *= 0x7FEB352Du;
+  x = (x & 0xFFFFFFu) * 0x9E3779u;
   x ^= x >> 15;
   return x;
+}
+
+// raw limb j >= 2 of a UNIFORM value from its raw limbs j-1 (a) and j-2 (b): a funnel
+// shift of a:b (v_alignbit_b32) plus b — two VALU instructions where a hashed limb takes
+// five; limbs 0 and 1 are hashed (grnd)
+__host__ __device__ __forceinline__ uint32_t gext(uint32_t a, uint32_t b, uint32_t j) {
+  const uint32_t s = (7u * j + 3u) % 31u + 1u;  // 1..31
+  return (uint32_t)(((((uint64_t)a) << 32) | b) >> s) + b;
 }
 
 struct GKeys {
   uint32_t klo, khi, glo, ghi;
 };
 
-__device__ __forceinline__ GKeys gen_keys(uint64_t idx, uint64_t sk, uint64_t sg) {
-  const uint64_t K = fmix64(idx ^ sk);
+// lk = gen_lane_key(idx & 63, sk), computed once per lane by kernels whose lanes keep their slot
+__device__ __forceinline__ uint64_t gen_lane_key(uint64_t lane, uint64_t sk) { return fmix64(lane ^ sk); }
+
+__device__ __forceinline__ GKeys gen_keys_lk(uint64_t idx, uint64_t lk, uint64_t sg) {
   const uint64_t G = fmix64((idx >> 6) ^ sg);
+  const uint64_t K = G ^ lk;
   GKeys k;
   k.klo = (uint32_t)K;
   k.khi = (uint32_t)(K >> 32);
   k.glo = (uint32_t)G;
   k.ghi = (uint32_t)(G >> 32);
   return k;
+}
+
+__device__ __forceinline__ GKeys gen_keys(uint64_t idx, uint64_t sk, uint64_t sg) {
+  return gen_keys_lk(idx, gen_lane_key(idx & 63u, sk), sg);
 }
 
 // per-lane random limb j of coordinate c; h(c) = grnd(k, c, 0xFFFF)

@@ -62,7 +62,7 @@ struct Gen {
     return t.str();
   }
 
-  // Spec-specialised GEN2 generator for coordinate c (the same function of (seed, index, c)
+  // Spec-specialised GEN3 generator for coordinate c (the same function of (seed, index, c)
   // as gen_coord in engine.hip and gen_value in oracle/bveval.c).  Writes L limbs into
   // `out`_j.  A MIXED coordinate's alternative comes from the group key (SGPRs), so the
   // alternatives are scalar branches: a lane computes only the one its wave chose.
@@ -80,6 +80,28 @@ struct Gen {
     o << ";\n";
     gen_value(c, pre);
     return pre;
+  }
+
+  // UNIFORM raw limbs (mythgpu.h GEN3): u0, u1 hashed, u_j = gext(u_{j-1}, u_{j-2}, j); limb j of
+  // the value is u_j masked to the low `bits` bits of the value
+  template <class Lim>
+  void uniform_limbs(const std::string& C, uint32_t L, uint32_t bits, const Lim& lim, const char* ind) {
+    const uint32_t need = std::min(L, (bits + 31) / 32);  // raw limbs that reach the value
+    const std::string u = "u" + std::to_string(tmp_id++) + "_";
+    for (uint32_t j = 0; j < need; j++) {
+      o << ind << "const uint32_t " << u << j << " = "
+        << (j < 2 ? "grnd(ky, " + C + ", " + std::to_string(j) + "u)"
+                  : "gext(" + u + std::to_string(j - 1) + ", " + u + std::to_string(j - 2) + ", " + std::to_string(j) + "u)")
+        << ";\n";
+    }
+    for (uint32_t j = 0; j < L; j++) {
+      const uint32_t lo = 32 * j;
+      const uint32_t m = lo >= bits ? 0u : (bits - lo >= 32 ? 0xFFFFFFFFu : ((1u << (bits - lo)) - 1u));
+      std::string e = u + std::to_string(j);
+      if (m == 0) e = "0u";
+      else if (m != 0xFFFFFFFFu) e = "(" + e + " & " + hex(m) + ")";
+      o << ind << lim(j) << " = " << e << ";\n";
+    }
   }
 
   void gen_value(uint32_t c, const std::string& out) {
@@ -102,17 +124,16 @@ struct Gen {
         const bool narrow = width <= MG_GEN_NARROW_BITS;
         o << "  const uint32_t ws = gwsel(ky, " << C << "), sel = ws & 0xFFFFu;\n";
         o << "  const uint32_t h = grnd(ky, " << C << ", 0xFFFFu);\n";
-        // uniform / small limbs (one draw per limb; narrow: from h)
+        // uniform / small limbs (narrow: from h)
         auto uni = [&](uint32_t bits) {
-          for (uint32_t j = 0; j < L; j++) {
-            const uint32_t lo = 32 * j;
-            const uint32_t m = lo >= bits ? 0u : (bits - lo >= 32 ? 0xFFFFFFFFu : ((1u << (bits - lo)) - 1u));
-            std::string e = narrow ? (j ? std::string("0u") : std::string("(h & 0xFFFFu)"))
-                                   : "grnd(ky, " + C + ", " + std::to_string(j) + "u)";
-            if (m == 0) e = "0u";
-            else if (m != 0xFFFFFFFFu) e = "(" + e + " & " + hex(m) + ")";
-            o << "    " << lim(j) << " = " << e << ";\n";
+          if (narrow) {
+            for (uint32_t j = 0; j < L; j++) {
+              const uint32_t m = j ? 0u : (bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u));
+              o << "    " << lim(j) << " = " << (m ? "(h & " + hex(m & 0xFFFFu) + ")" : std::string("0u")) << ";\n";
+            }
+            return;
           }
+          uniform_limbs(C, L, bits, lim, "    ");
         };
         bool first = true;
         auto branch = [&](const std::string& cond) {
@@ -212,7 +233,7 @@ struct Gen {
         for (uint32_t j = 0; j < L; j++) o << "  " << lim(j) << " = " << hex(G[sp.p[0] + j]) << ";\n";
         break;
       default:  // UNIFORM / LAZY
-        for (uint32_t j = 0; j < L; j++) o << "  " << lim(j) << " = grnd(ky, " << C << ", " << j << "u);\n";
+        uniform_limbs(C, L, 32 * L, lim, "  ");
         break;
     }
     if (width & 31) o << "  " << lim(L - 1) << " &= " << hex(topmask(width)) << ";\n";
@@ -567,7 +588,7 @@ struct Gen {
     if (search && gen_only) {
       o << "  { uint32_t fold_ = 0u;\n";
       for (const Instr& in : P.vcode) {
-        if (in.op != K_COORD) continue;
+        if (in.op != K_COORD || ((*specs)[in.p0].kind & 0xFFu) == MG_GEN_LAZY) continue;
         emit(in, true, false);
         for (uint32_t j = 0; j < Lw(in.wd); j++) o << "  fold_ ^= " << v(in.dst, j) << ";\n";
       }
@@ -604,7 +625,8 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  const uint32_t tid = __builtin_amdgcn_workitem_id_x(), bid = __builtin_amdgcn_workgroup_id_x();\n"
        "  const bool early = (flags & 1u) != 0u;\n"
        "  const uint32_t lane = tid & 63u;\n"
-       "  // one aligned group of 64 candidate indices per wave (GEN2 group key, mythgpu.h)\n"
+       "  const uint64_t LK = fmix64((uint64_t)lane ^ sk);  // lane half of the lane key (GEN3)\n"
+       "  // one aligned group of 64 candidate indices per wave (GEN3 group key, mythgpu.h)\n"
        "  const uint64_t a0 = start & ~63ull, end = start + count;\n"
        "  const uint64_t ngroups = (end - a0 + 63ull) >> 6;\n"
        "  const uint64_t gstride = (uint64_t)nblk * 4u;  // 4 waves per 256-lane block\n"
@@ -622,7 +644,7 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  const uint64_t idx = gbase + lane;\n"
        "  const bool active = idx >= start && idx < end;\n"
        "  GKeys ky;\n"
-       "  { const uint64_t K = fmix64(idx ^ sk), G = fmix64((gbase >> 6) ^ sg);\n"
+       "  { const uint64_t G = fmix64((gbase >> 6) ^ sg), K = G ^ LK;\n"
        "    ky.klo = (uint32_t)K; ky.khi = (uint32_t)(K >> 32); ky.glo = (uint32_t)G; ky.ghi = (uint32_t)(G >> 32); }\n"
        "  uint32_t verdict = 1u;\n";
   g.decls();
@@ -652,6 +674,7 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  const uint32_t tid = __builtin_amdgcn_workitem_id_x(), bid = __builtin_amdgcn_workgroup_id_x();\n"
        "  const bool early = false;\n"
        "  const uint32_t lane = tid & 63u;\n"
+       "  const uint64_t LK = fmix64((uint64_t)lane ^ sk);  // lane half of the lane key (GEN3)\n"
        "  const uint64_t a0 = start & ~63ull, end = start + count;\n"
        "  const uint64_t ngroups = (end - a0 + 63ull) >> 6;\n"
        "  const uint64_t gstride = (uint64_t)nblk * 4u;\n"
@@ -662,7 +685,7 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  const uint64_t idx = gbase + lane;\n"
        "  const bool active = idx >= start && idx < end;\n"
        "  GKeys ky;\n"
-       "  { const uint64_t K = fmix64(idx ^ sk), G = fmix64((gbase >> 6) ^ sg);\n"
+       "  { const uint64_t G = fmix64((gbase >> 6) ^ sg), K = G ^ LK;\n"
        "    ky.klo = (uint32_t)K; ky.khi = (uint32_t)(K >> 32); ky.glo = (uint32_t)G; ky.ghi = (uint32_t)(G >> 32); }\n"
        "  uint32_t verdict = 1u;\n";
   g.decls();

@@ -750,7 +750,7 @@ struct Analysis {
     return true;
   }
 
-  // range of a generated coordinate's final value (include/mythgpu.h GEN2)
+  // range of a generated coordinate's final value (include/mythgpu.h GEN3)
   Rng coord_range(uint32_t c) const {
     const GenSpec& sp = (*specs)[c];
     const uint32_t w = P.coord_width[c], L = Lw(w), kind = sp.kind & 0xFFu;

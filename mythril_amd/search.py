@@ -28,7 +28,7 @@ import numpy as np
 from . import ssa
 from .smt import terms as T
 
-GEN_MAGIC = 0x324E4547  # "GEN2" (include/mythgpu.h)
+GEN_MAGIC = 0x334E4547  # "GEN3" (include/mythgpu.h)
 GEN_UNIFORM, GEN_RANGE, GEN_DICT, GEN_MIXED, GEN_ALIGNED, GEN_FIXED, GEN_LAZY = range(7)
 NONE = ssa.MG_NONE
 
@@ -99,7 +99,7 @@ class GenBuilder:
     def mixed(self, c: int, values: Sequence[int], p_dict: float, copy_from: Optional[int] = None,
               p_copy: float = 0.0, p_delta: float = 0.0, small_bits: int = 0, p_small: float = 0.0,
               clamp: Optional[tuple] = None):
-        """MIXED (GEN2): one alternative per aligned group of 64 candidates — COPY of an
+        """MIXED (GEN3): one alternative per aligned group of 64 candidates — COPY of an
         earlier coordinate's final value, DICT, SMALL or UNIFORM — plus a per-lane +/-1/2
         delta on COPY/DICT, then an optional clamp into ``[lo, lo + span)``."""
         w = self.P.coords[c].width

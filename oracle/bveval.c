@@ -239,7 +239,7 @@ static uint64_t vsmall(const val_t* b, uint32_t cap) {
   return b->w[0] < cap ? b->w[0] : cap;
 }
 
-/* ---- generator restatement (include/mythgpu.h, format GEN2) ---- */
+/* ---- generator restatement (include/mythgpu.h, format GEN3) ---- */
 static uint64_t fmix64(uint64_t x) {
   x ^= x >> 33;
   x *= 0xFF51AFD7ED558CCDull;
@@ -254,8 +254,8 @@ typedef struct {
 } keys_t;
 
 static void make_keys(uint64_t idx, uint64_t seed, keys_t* k) {
-  const uint64_t K = fmix64(idx ^ fmix64(seed ^ 0x6A09E667F3BCC908ull));
   const uint64_t G = fmix64((idx >> 6) ^ fmix64(seed ^ 0xBB67AE8584CAA73Bull));
+  const uint64_t K = G ^ fmix64((idx & 63u) ^ fmix64(seed ^ 0x6A09E667F3BCC908ull));
   k->klo = (uint32_t)K;
   k->khi = (uint32_t)(K >> 32);
   k->glo = (uint32_t)G;
@@ -266,13 +266,27 @@ static uint32_t salt(uint32_t c, uint32_t j) { return c * 0x9E3779B9u + j * 0x85
 
 static uint32_t fin(uint32_t x) {
   x ^= x >> 16;
-  x *= 0x7FEB352Du;
+  x = (x & 0xFFFFFFu) * 0x9E3779u; /* 24 x 24 -> low 32 bits */
   x ^= x >> 15;
   return x;
 }
 
 static uint32_t rnd(const keys_t* k, uint32_t c, uint32_t j) { return fin(k->klo ^ salt(c, j)) + k->khi; }
 static uint32_t wsel(const keys_t* k, uint32_t c) { return fin(k->glo ^ salt(c, 0xFFFEu)) + k->ghi; }
+
+/* the raw limbs of a UNIFORM draw: u0 = rnd(c, 0), u1 = rnd(c, 1), then
+   u_j = low 32 bits of ((u_{j-1} : u_{j-2}) >> s_j) + u_{j-2}  (mod 2^32),
+   s_j = (7j + 3) mod 31 + 1 */
+static void uniform_raw(const keys_t* k, uint32_t c, uint32_t L, uint32_t* u) {
+  for (uint32_t j = 0; j < L; j++) {
+    if (j < 2) {
+      u[j] = rnd(k, c, j);
+    } else {
+      const uint64_t pair = ((uint64_t)u[j - 1] << 32) | u[j - 2];
+      u[j] = (uint32_t)(pair >> ((7u * j + 3u) % 31u + 1u)) + u[j - 2];
+    }
+  }
+}
 
 static void set_limb32(val_t* v, uint32_t j, uint32_t x) {
   v->w[j / 2] |= (uint64_t)x << (32 * (j % 2));
@@ -302,7 +316,7 @@ static void add_small(uint32_t* out, const uint32_t* lo, uint64_t off, uint32_t 
 struct ctx;
 static void coord_value(struct ctx* X, uint32_t c, val_t* out);
 
-/* generated value of coordinate c (GEN2 semantics in include/mythgpu.h) into L limbs */
+/* generated value of coordinate c (GEN3 semantics in include/mythgpu.h) into L limbs */
 static void gen_value(struct ctx* X, const prog_t* P, const keys_t* k, uint32_t c, uint32_t* limb) {
   const uint32_t width = P->coords[4 * c];
   const uint32_t L = (width + 31) / 32;
@@ -361,10 +375,14 @@ static void gen_value(struct ctx* X, const prog_t* P, const keys_t* k, uint32_t 
         const uint32_t small = sel < pc + pd + ps;
         uint32_t bits = small ? (s[5] >> 16) : width;
         if (bits > width) bits = width;
+        if (narrow) {
+          limb[0] = h & 0xFFFFu;
+        } else {
+          uniform_raw(k, c, L, limb);
+        }
         for (uint32_t j = 0; j < L; j++) {
-          uint32_t v = narrow ? (j == 0 ? (h & 0xFFFFu) : 0u) : rnd(k, c, j);
           const uint32_t lo = 32 * j;
-          limb[j] = lo >= bits ? 0u : (bits - lo >= 32 ? v : (v & ((1u << (bits - lo)) - 1u)));
+          limb[j] = lo >= bits ? 0u : (bits - lo >= 32 ? limb[j] : (limb[j] & ((1u << (bits - lo)) - 1u)));
         }
       }
       if (with_delta && (ws >> 16) < s[6]) {
@@ -395,7 +413,7 @@ static void gen_value(struct ctx* X, const prog_t* P, const keys_t* k, uint32_t 
       break;
     }
     default: /* UNIFORM / LAZY */
-      for (uint32_t j = 0; j < L; j++) limb[j] = rnd(k, c, j);
+      uniform_raw(k, c, L, limb);
       break;
   }
   mask_limbs(limb, L, width);
@@ -634,7 +652,7 @@ static int parse(prog_t* P, const uint32_t* w, size_t n, const uint32_t* gen, si
   for (uint32_t i = 0; i < P->n_nodes; i++)
     if (P->nodes[i].width > MAXW * 64) return -2;
   if (gen) {
-    if (gen_n < 4 || gen[0] != 0x324E4547u || gen[1] != P->n_coords) return -1;
+    if (gen_n < 4 || gen[0] != 0x334E4547u || gen[1] != P->n_coords) return -1;
     P->gen_n = gen[1];
     P->specs = gen + 4;
     P->gconsts = gen + 4 + 8ull * gen[1];

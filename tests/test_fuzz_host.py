@@ -2,7 +2,7 @@
 
 tests/fuzz/fuzz_host.cpp links program.cpp (lower_program, parse_gen,
 specialize_program) and jit.cpp (jit_source) with g++ -fsanitize=address,undefined
--fno-sanitize-recover=all.  Hypothesis mutates valid program and GEN2 generator blobs
+-fno-sanitize-recover=all.  Hypothesis mutates valid program and GEN3 generator blobs
 (the workloads' and random DAGs'; word-level: bit flips, boundary values, truncation,
 extension, splices) and every mutant goes through the same calls mg_program_check_gen
 and mg_jit_compile_ex make before any device work.  Pass = the process exits 0 with no
