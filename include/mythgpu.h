@@ -141,7 +141,7 @@ enum mg_table_kind { MG_TABLE_ARRAY = 0, MG_TABLE_UF = 1 };
  *   fin(x)      = x ^= x>>16; x = (x & 0xFFFFFF) * 0x9E3779; x ^= x>>15  (mod 2^32)
  *   rnd(c, j)   = fin(K_lo ^ salt(c, j)) + K_hi      per-lane 32 random bits
  *   h(c)        = rnd(c, 0xFFFF)                     per-lane index / delta bits
- *   wsel(c)     = fin(G_lo ^ salt(c, 0xFFFE)) + G_hi per-group choice bits
+ *   wsel(c)     = (G_lo ^ salt(c, 0xFFFE)) * 0x9E3779B1 + G_hi   per-group choice bits
  *   raw uniform limbs u_0 = rnd(c, 0), u_1 = rnd(c, 1),
  *               u_j = lo32((u_{j-1} : u_{j-2}) >> s_j) + u_{j-2}  (mod 2^32, j >= 2),
  *               s_j = (7j + 3) mod 31 + 1
@@ -153,7 +153,7 @@ enum mg_table_kind { MG_TABLE_ARRAY = 0, MG_TABLE_UF = 1 };
  *   ALIGNED  lo + (m << p1), m = ((u64)rnd(c,0) * count) >> 32 (count 0: m = rnd(c,0))
  *   FIXED    the value
  *   LAZY     never generated (a site whose default is a program node)
- *   MIXED    one alternative per aligned group, chosen by s = wsel(c) & 0xFFFF:
+ *   MIXED    one alternative per aligned group, chosen by s = wsel(c) >> 16:
  *              pc = P(copy) if p3 != MG_NONE else 0, pd = P(dict) if n else 0, ps = P(small)
  *              s < pc            COPY     the FINAL value of coordinate p3 (p3 < c, same width)
  *              s < pc+pd         DICT     entry ((h(c) >> 16) * n) >> 16
@@ -161,7 +161,7 @@ enum mg_table_kind { MG_TABLE_ARRAY = 0, MG_TABLE_UF = 1 };
  *              otherwise         UNIFORM
  *            narrow coordinates (w <= MG_GEN_NARROW_BITS) take UNIFORM / SMALL from
  *            h(c) & 0xFFFF (one hash each);
- *            COPY and DICT add a per-lane delta when (wsel(c) >> 16) < P(delta):
+ *            COPY and DICT add a per-lane delta when (wsel(c) & 0xFFFF) < P(delta):
  *              +/-(1 + (h & 1)), minus when (h >> 1) & 1, modulo 2^(32 L);
  *            then mask to w, then the clamp record (if any): v stays if
  *              lo <= v < lo + span, else v = lo + (((u64)limb0(v) * span) >> 32)

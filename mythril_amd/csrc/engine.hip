@@ -121,7 +121,7 @@ struct VFGlobal {
 enum : uint32_t { ALT_NONE = 0, ALT_COPY = 1, ALT_DICT = 2, ALT_SMALL = 3, ALT_UNIFORM = 4 };
 
 __device__ __forceinline__ uint32_t mixed_alt(const GenSpec& s, uint32_t ws) {
-  const uint32_t sel = ws & 0xFFFFu;
+  const uint32_t sel = ws >> 16;
   const uint32_t pc = s.p[3] != MG_NONE ? (s.p[2] & 0xFFFFu) : 0u;
   const uint32_t pd = s.p[1] ? (s.p[2] >> 16) : 0u;
   const uint32_t ps = s.p[4] & 0xFFFFu;
@@ -206,7 +206,7 @@ __device__ __forceinline__ void gen_finish(const KArgs& k, const VF& vf, uint32_
                            const GKeys& ky, const GenSpec& s, uint32_t alt, uint32_t ws) {
   const uint32_t L = (width + 31) >> 5;
   if (MG_GEN_KIND(s.kind) == MG_GEN_MIXED) {
-    if ((alt == ALT_COPY || alt == ALT_DICT) && (ws >> 16) < s.p[5]) {
+    if ((alt == ALT_COPY || alt == ALT_DICT) && (ws & 0xFFFFu) < s.p[5]) {
       const uint32_t h = grnd(ky, c, 0xFFFFu);
       const uint32_t mag = 1u + (h & 1u);
       const bool sub = (h >> 1) & 1u;

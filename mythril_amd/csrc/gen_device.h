@@ -73,7 +73,12 @@ __device__ __forceinline__ uint32_t grnd(const GKeys& k, uint32_t c, uint32_t j)
   return gfin(k.klo ^ gsalt(c, j)) + k.khi;
 }
 
-// per-group choice bits of coordinate c (low 16: alternative, high 16: delta)
-__device__ __forceinline__ uint32_t gwsel(const GKeys& k, uint32_t c) { return gfin(k.glo ^ gsalt(c, 0xFFFEu)) + k.ghi; }
+// per-group choice bits of coordinate c (high 16: alternative, low 16: delta).  Wave-uniform,
+// so it runs on the scalar unit, which every SIMD of the CU shares: a multiply-add (3 SALU)
+// instead of the lane finaliser (9 SALU), and the alternative comes from the better-mixed
+// high half of the product
+__device__ __forceinline__ uint32_t gwsel(const GKeys& k, uint32_t c) {
+  return (k.glo ^ gsalt(c, 0xFFFEu)) * 0x9E3779B1u + k.ghi;
+}
 
 }  // namespace mg

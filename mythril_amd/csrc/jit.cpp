@@ -122,11 +122,17 @@ struct Gen {
         const uint32_t ps = sp.p[4] & 0xFFFFu;
         const uint32_t small_bits = std::min(width, sp.p[4] >> 16);
         const bool narrow = width <= MG_GEN_NARROW_BITS;
-        o << "  const uint32_t ws = gwsel(ky, " << C << "), sel = ws & 0xFFFFu;\n";
-        o << "  const uint32_t h = grnd(ky, " << C << ", 0xFFFFu);\n";
+        // the alternative is s = ws >> 16 (wave-uniform, SGPRs): s < T  <=>  ws < T << 16, so each
+        // test is one scalar compare; h is hashed only in the branches that read it
+        o << "  const uint32_t ws = gwsel(ky, " << C << ");\n";
+        const std::string hdecl = "const uint32_t h = grnd(ky, " + C + ", 0xFFFFu);";
+        auto below = [&](uint32_t T) {
+          return T >= 65536u ? std::string("true") : "ws < " + hex(T << 16);
+        };
         // uniform / small limbs (narrow: from h)
         auto uni = [&](uint32_t bits) {
           if (narrow) {
+            o << "    " << hdecl << "\n";
             for (uint32_t j = 0; j < L; j++) {
               const uint32_t m = j ? 0u : (bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u));
               o << "    " << lim(j) << " = " << (m ? "(h & " + hex(m & 0xFFFFu) + ")" : std::string("0u")) << ";\n";
@@ -135,18 +141,31 @@ struct Gen {
           }
           uniform_limbs(C, L, bits, lim, "    ");
         };
+        // +/-(1 + (h & 1)) on COPY / DICT as ONE carry chain over the sign-extended step, when the
+        // low half of ws is below P(delta); emitted inside the COPY and DICT branches
+        auto delta = [&](bool h_known) {
+          if (!sp.p[5]) return;
+          o << "    if ((ws & 0xFFFFu) < " << sp.p[5] << "u) {" << (h_known ? "" : " " + hdecl)
+            << " const uint32_t mag = 1u + (h & 1u); const bool sb = (h >> 1) & 1u;"
+            << " const uint32_t a0 = sb ? 0u - mag : mag, ah = sb ? 0xFFFFFFFFu : 0u; uint32_t cy = 0u;";
+          for (uint32_t j = 0; j < L; j++)
+            o << " " << lim(j) << " = mg_addc(" << lim(j) << ", " << (j ? "ah" : "a0") << ", cy, &cy);";
+          o << " (void)cy; (void)ah; }\n";
+        };
         bool first = true;
         auto branch = [&](const std::string& cond) {
           o << (first ? "  if (" : "  } else if (") << cond << ") {\n";
           first = false;
         };
         if (pc) {
-          branch("sel < " + std::to_string(pc) + "u");
+          branch(below(pc));
           const std::string src = coord_var.at(sp.p[3]);
           for (uint32_t j = 0; j < L; j++) o << "    " << lim(j) << " = " << src << "_" << j << ";\n";
+          delta(false);
         }
         if (pd) {
-          branch("sel < " + std::to_string(pc + pd) + "u");
+          branch(below(pc + pd));
+          o << "    " << hdecl << "\n";
           o << "    const uint32_t e = ((h >> 16) * " << sp.p[1] << "u) >> 16;\n";
           const std::string packed = packed_dict(sp.p[0], sp.p[1], width, "e");
           for (uint32_t j = 0; j < L; j++)
@@ -154,9 +173,10 @@ struct Gen {
               << (!packed.empty() ? (j ? std::string("0u") : packed)
                                   : "gconsts[" + std::to_string(sp.p[0] + j) + "u + e * " + std::to_string(L) + "u]")
               << ";\n";
+          delta(true);
         }
         if (ps) {
-          branch("sel < " + std::to_string(pc + pd + ps) + "u");
+          branch(below(pc + pd + ps));
           uni(small_bits);
         }
         if (first) {
@@ -165,15 +185,6 @@ struct Gen {
           o << "  } else {\n";
           uni(width);
           o << "  }\n";
-        }
-        if (sp.p[5] && (pc || pd)) {
-          // +/-(1 + (h & 1)) on COPY / DICT as ONE carry chain over the sign-extended step
-          o << "  if ((ws >> 16) < " << sp.p[5] << "u && sel < " << (pc + pd) << "u) {"
-            << " const uint32_t mag = 1u + (h & 1u); const bool sb = (h >> 1) & 1u;"
-            << " const uint32_t a0 = sb ? 0u - mag : mag, ah = sb ? 0xFFFFFFFFu : 0u; uint32_t cy = 0u;";
-          for (uint32_t j = 0; j < L; j++)
-            o << " " << lim(j) << " = mg_addc(" << lim(j) << ", " << (j ? "ah" : "a0") << ", cy, &cy);";
-          o << " (void)cy; (void)ah; }\n";
         }
         if (width & 31) o << "  " << lim(L - 1) << " &= " << hex(topmask(width)) << ";\n";
         if (sp.p[6]) {

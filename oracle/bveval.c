@@ -272,7 +272,7 @@ static uint32_t fin(uint32_t x) {
 }
 
 static uint32_t rnd(const keys_t* k, uint32_t c, uint32_t j) { return fin(k->klo ^ salt(c, j)) + k->khi; }
-static uint32_t wsel(const keys_t* k, uint32_t c) { return fin(k->glo ^ salt(c, 0xFFFEu)) + k->ghi; }
+static uint32_t wsel(const keys_t* k, uint32_t c) { return (k->glo ^ salt(c, 0xFFFEu)) * 0x9E3779B1u + k->ghi; }
 
 /* the raw limbs of a UNIFORM draw: u0 = rnd(c, 0), u1 = rnd(c, 1), then
    u_j = low 32 bits of ((u_{j-1} : u_{j-2}) >> s_j) + u_{j-2}  (mod 2^32),
@@ -355,7 +355,7 @@ static void gen_value(struct ctx* X, const prog_t* P, const keys_t* k, uint32_t 
       memcpy(limb, P->gconsts + s[1], 4 * L);
       break;
     case 3: { /* MIXED: one alternative per aligned group of 64 indices */
-      const uint32_t ws = wsel(k, c), sel = ws & 0xFFFFu;
+      const uint32_t ws = wsel(k, c), sel = ws >> 16;
       const uint32_t pc = s[4] != NONE ? (s[3] & 0xFFFFu) : 0u;
       const uint32_t pd = s[2] ? (s[3] >> 16) : 0u;
       const uint32_t ps = s[5] & 0xFFFFu;
@@ -385,7 +385,7 @@ static void gen_value(struct ctx* X, const prog_t* P, const keys_t* k, uint32_t 
           limb[j] = lo >= bits ? 0u : (bits - lo >= 32 ? limb[j] : (limb[j] & ((1u << (bits - lo)) - 1u)));
         }
       }
-      if (with_delta && (ws >> 16) < s[6]) {
+      if (with_delta && (ws & 0xFFFFu) < s[6]) {
         const uint32_t mag = 1u + (h & 1u);
         const int sub = (h >> 1) & 1u;
         uint64_t cy = mag;
