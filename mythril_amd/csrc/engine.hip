@@ -40,9 +40,6 @@
 namespace mg {
 
 constexpr int kWave = 64;
-// device hit buffer words: first hit, hit count, and the JIT search kernel's 8 group-claim
-// counters (jit.cpp: one per eighth of a launch's groups), all re-armed before every launch
-constexpr int kHitWords = 10;
 constexpr uint32_t kLdsWordsMax = 160;  // value file in LDS up to 160 words (40 KiB per wave)
 
 __device__ __constant__ static const uint32_t kEmptyKeccak[8] = {
@@ -785,7 +782,7 @@ struct Engine {
   uint64_t next_handle = 1;
   std::unordered_map<uint64_t, std::unique_ptr<DevProgram>> progs;
   std::unordered_map<uint64_t, std::unique_ptr<DevGen>> gens;
-  unsigned long long* d_hit = nullptr;  // [0] first hit, [1] hit count, [2..9] JIT claim counters
+  unsigned long long* d_hit = nullptr;  // [0] first hit, [1] hit count
   // pinned host staging: [0..1] the reset values, [2..3] the result (async copies on `stream`,
   // one event wait per call instead of two blocking hipMemcpy round trips)
   unsigned long long* h_hit = nullptr;
@@ -984,14 +981,14 @@ static int launch_wait(Engine& e, mg_stats_t& st, uint64_t count) {
 // reset e's hit buffer before a search launch (async, from pinned memory)
 static int arm_hits(Engine& e) {
   e.h_hit[0] = ~0ull;
-  for (int w = 1; w < kHitWords; w++) e.h_hit[w] = 0ull;  // hit count, JIT claim counters
-  HIPCHK(hipMemcpyAsync(e.d_hit, e.h_hit, kHitWords * sizeof(unsigned long long), hipMemcpyHostToDevice, e.stream));
+  e.h_hit[1] = 0ull;
+  HIPCHK(hipMemcpyAsync(e.d_hit, e.h_hit, 2 * sizeof(unsigned long long), hipMemcpyHostToDevice, e.stream));
   return MG_OK;
 }
 
 // queue the hit buffer's read-back behind e's last launch (async); collect_hits waits for it
 static int fetch_hits(Engine& e) {
-  HIPCHK(hipMemcpyAsync(e.h_hit + kHitWords, e.d_hit, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e.stream));
+  HIPCHK(hipMemcpyAsync(e.h_hit + 2, e.d_hit, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e.stream));
   HIPCHK(hipEventRecord(e.ev2, e.stream));
   return MG_OK;
 }
@@ -1006,8 +1003,8 @@ static int collect_hits(Engine& e, mg_stats_t& st, uint64_t count, unsigned long
   st.kernel_ms_total += ms;
   st.candidates += count;
   st.last_candidates = count;
-  res[0] = e.h_hit[kHitWords];
-  res[1] = e.h_hit[kHitWords + 1];
+  res[0] = e.h_hit[2];
+  res[1] = e.h_hit[3];
   return MG_OK;
 }
 
@@ -1051,8 +1048,8 @@ static int init_dev(Engine& e, int dev) {
   HIPCHK(hipEventCreate(&e.ev0));
   HIPCHK(hipEventCreate(&e.ev1));
   HIPCHK(hipEventCreateWithFlags(&e.ev2, hipEventDisableTiming));
-  HIPCHK(hipMalloc((void**)&e.d_hit, kHitWords * sizeof(unsigned long long)));
-  HIPCHK(hipHostMalloc((void**)&e.h_hit, (kHitWords + 2) * sizeof(unsigned long long), hipHostMallocDefault));
+  HIPCHK(hipMalloc((void**)&e.d_hit, 2 * sizeof(unsigned long long)));
+  HIPCHK(hipHostMalloc((void**)&e.h_hit, 4 * sizeof(unsigned long long), hipHostMallocDefault));
   e.device = dev;
   e.cu_count = prop.multiProcessorCount;
   e.clock_mhz = prop.clockRate / 1000;

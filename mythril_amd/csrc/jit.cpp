@@ -624,11 +624,6 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   o << "typedef unsigned int uint32_t;\ntypedef int int32_t;\ntypedef unsigned long long uint64_t;\n"
        "typedef unsigned char uint8_t;\n";
   o << kPrelude << "\nusing namespace mg;\n";
-  // groups per claim of the search kernel's dynamic distribution (MYTHGPU_JIT_CHUNK, default 4)
-  {
-    const char* ch = getenv("MYTHGPU_JIT_CHUNK");
-    o << "#define MG_CHUNK " << std::max(1, ch ? atoi(ch) : 4) << "ull\n";
-  }
   // 256-lane blocks; optional occupancy target (min waves per SIMD) for the search kernel
   std::string lb = "__attribute__((amdgpu_flat_work_group_size(1, 256)))";
   if (const char* wv = getenv("MYTHGPU_JIT_WAVES"))
@@ -645,40 +640,9 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  // one aligned group of 64 candidate indices per wave (GEN3 group key, mythgpu.h)\n"
        "  const uint64_t a0 = start & ~63ull, end = start + count;\n"
        "  const uint64_t ngroups = (end - a0 + 63ull) >> 6;\n"
+       "  const uint64_t gstride = (uint64_t)nblk * 4u;  // 4 waves per 256-lane block\n"
        "  uint64_t wave_best = ~0ull, wave_hits = 0;  // per-wave, wave-uniform\n"
-       "  // Dynamic work distribution, so every wave of the launch finishes at about the same time\n"
-       "  // (with a static grid-stride split the oldest waves of a SIMD win the issue arbitration\n"
-       "  // and finish first, and the launch ends on a few young waves).  The groups are cut into\n"
-       "  // 8 contiguous ranges with one claim counter each (hit[2 + r], zeroed by the host before\n"
-       "  // every launch; 8 counters keep same-address atomics off the critical path).  A wave\n"
-       "  // claims MG_CHUNK groups at a time, starting in range bid & 7 and moving to the next range\n"
-       "  // when its range is exhausted; the next claim is issued before the current chunk runs.\n"
-       "  // Claims within a range are monotonic, so an early-exit wave that reaches a group at or\n"
-       "  // above the current first hit abandons only the rest of that range (all above it) and\n"
-       "  // moves on: every group below the final first hit is evaluated by some wave.\n"
-       "  const uint64_t per = (ngroups + 7ull) >> 3;\n"
-       "  uint32_t rng = bid & 7u, tried = 0u;\n"
-       "  unsigned long long claim = 0ull;\n"
-       "  if (lane == 0u) claim = atomicAdd(hit + 2 + rng, (unsigned long long)MG_CHUNK);\n"
-       "  uint64_t c0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(claim >> 32)) << 32) | "
-       "__builtin_amdgcn_readfirstlane((uint32_t)claim);\n"
-       "  while (tried < 8u) {\n"
-       "  const uint64_t rlo = (uint64_t)rng * per, rhi = rlo + per < ngroups ? rlo + per : ngroups;\n"
-       "  if (rlo + c0 >= rhi) {  // range exhausted: the next one (a plain load first: at the end of a\n"
-       "    // launch every wave walks the ranges, and a read does not serialise like an atomic)\n"
-       "    tried++; rng = (rng + 1u) & 7u;\n"
-       "    if (lane == 0u) {\n"
-       "      claim = __hip_atomic_load(hit + 2 + rng, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
-       "      if (claim < per) claim = atomicAdd(hit + 2 + rng, (unsigned long long)MG_CHUNK);\n"
-       "    }\n"
-       "    c0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(claim >> 32)) << 32) | "
-       "__builtin_amdgcn_readfirstlane((uint32_t)claim);\n"
-       "    continue;\n"
-       "  }\n"
-       "  if (lane == 0u) claim = atomicAdd(hit + 2 + rng, (unsigned long long)MG_CHUNK);  // the next chunk\n"
-       "  const uint64_t g0 = rlo + c0, g1 = g0 + MG_CHUNK < rhi ? g0 + MG_CHUNK : rhi;\n"
-       "  bool above = false;\n"
-       "  for (uint64_t g = g0; g < g1; g++) {\n"
+       "  for (uint64_t g = (uint64_t)bid * 4u + (tid >> 6); g < ngroups; g += gstride) {\n"
        "  const uint64_t gb = a0 + (g << 6);\n"
        "  const uint64_t gbase = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32)) << 32) | "
        "__builtin_amdgcn_readfirstlane((uint32_t)gb);\n"
@@ -686,7 +650,7 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "    const unsigned long long cur = __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
        "    const uint64_t cu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) | "
        "__builtin_amdgcn_readfirstlane((uint32_t)cur);\n"
-       "    if (gbase >= cu) { above = true; break; }\n"
+       "    if (gbase >= cu) break;\n"
        "  }\n"
        "  const uint64_t idx = gbase + lane;\n"
        "  const bool active = idx >= start && idx < end;\n"
@@ -708,13 +672,6 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "        if (early && lane == 0u) atomicMin(hit, (unsigned long long)first);\n"
        "      }\n"
        "    } }\n"
-       "  }\n"
-       "  if (above) {  // the rest of this range is above the current first hit\n"
-       "    tried++; rng = (rng + 1u) & 7u;\n"
-       "    if (lane == 0u) claim = atomicAdd(hit + 2 + rng, (unsigned long long)MG_CHUNK);\n"
-       "  }\n"
-       "  c0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(claim >> 32)) << 32) | "
-       "__builtin_amdgcn_readfirstlane((uint32_t)claim);\n"
        "  }\n"
        "  if (lane == 0u) {\n"
        "    if (wave_best != ~0ull) atomicMin(hit, (unsigned long long)wave_best);\n"
