@@ -1702,12 +1702,18 @@ namespace mg {
 // `nblk` is the kernel's grid-size argument (the JIT kernels read no dispatch packet)
 static int jit_launch_async(Engine& e, hipFunction_t f, int nb, uint64_t count, void** args, uint32_t& nblk) {
   const uint64_t want = (count + 255) / 256;
-  // resident blocks x MYTHGPU_JIT_GRID (default 2): waves loop over aligned index groups
-  static const uint64_t mult = [] {
-    const char* g = getenv("MYTHGPU_JIT_GRID");
-    return (uint64_t)std::max(1, g ? atoi(g) : 2);
+  // MYTHGPU_JIT_BPC (default 32) 256-lane blocks per CU, i.e. 32 waves per SIMD over the
+  // launch, whatever the occupancy (`nb`, unused here: the API answers 4 blocks/CU for a
+  // 52-VGPR kernel the hardware runs 8 deep); the waves loop over aligned index groups.
+  // Measured (tools/grid_sweep.sh, 2^28 candidates): 16/CU leaves a tail where the oldest waves
+  // of each SIMD have finished (C4 -8 %, C5 -3 %, C2 -2 %), 64/CU and more pays per-wave start-up
+  // and end-of-wave atomics (C3 +50 %, C2 +40 % at 128/CU).
+  static const uint64_t bpc = [] {
+    const char* g = getenv("MYTHGPU_JIT_BPC");
+    return (uint64_t)std::max(1, g ? atoi(g) : 32);
   }();
-  const uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * std::max(nb, 1) * mult;
+  (void)nb;
+  const uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * bpc;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
   nblk = grid;
   HIPCHK(hipEventRecord(e.ev0, e.stream));

@@ -11,7 +11,7 @@ run() {  # label, env...
 }
 if [ $# -eq 0 ]; then
   run base
-  run grid1 MYTHGPU_JIT_GRID=1
+  run bpc16 MYTHGPU_JIT_BPC=16
   run maxilp "MYTHGPU_JIT_EXTRA=-mllvm --amdgpu-sched-strategy=max-ilp"
   run O2 MYTHGPU_JIT_OPT=2
 else
