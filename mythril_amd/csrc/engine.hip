@@ -381,14 +381,13 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
   const uint32_t n_instr = k.n_instr;
   // code blocks (see code_block): the current one in a VGPR, the next one in flight (the code
   // buffer is padded with 16 zero records, so the block after the last is in bounds)
-  // The block loop is explicit so that the instruction loop leaves both registers alone (a
-  // rotate inside it made the compiler copy `nxt`, and wait for its load, every instruction).
-  uint32_t nxt = code_block(k, 0u);
-  for (uint32_t blk = 0, pc = 0; pc < n_instr; blk++) {
-    const uint32_t cur = nxt;
-    nxt = code_block(k, blk + 1u);
-    const uint32_t jn = n_instr - pc < 8u ? n_instr - pc : 8u;
-  for (uint32_t j = 0; j < jn; j++, pc++) {
+  uint32_t cur = code_block(k, 0u), nxt = code_block(k, 1u);
+  for (uint32_t pc = 0; pc < n_instr; pc++) {
+    const uint32_t j = pc & 7u;
+    if (j == 0u && pc != 0u) {
+      cur = nxt;
+      nxt = code_block(k, (pc >> 3) + 1u);
+    }
     const Instr in = instr_from_block(cur, j);
     const uint32_t W = in.wd;
     const uint32_t L = (W + 31) >> 5;
@@ -573,7 +572,6 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
       default:
         break;
     }
-  }
   }
   return verdict;
 }
