@@ -59,7 +59,6 @@ __device__ __forceinline__ const __attribute__((address_space(4))) T* cst(const 
 
 struct KArgs {
   const Instr* code;
-  const uint32_t* code_words;  // the same buffer, read with vector loads (code_block)
   const uint32_t* consts;
   const uint32_t* aux;
   const GenSpec* specs;
@@ -86,20 +85,13 @@ __device__ __forceinline__ GenSpec ld_spec(const KArgs& k, uint32_t c) {
   return s;
 }
 
-// The instruction stream reaches the wave as one coalesced 256-B vector load per block of 8
-// instructions (lane l holds word l & 7 of instruction l >> 3 of the block), issued one block
-// ahead; each instruction's fields then move to SGPRs with v_readlane (a scalar opcode switch).
-// A scalar load per instruction (the round-1/2 scheme) missed the scalar cache on most lines
-// of a long program, and its L2 latency was exposed on every one of them.
-__device__ __forceinline__ uint32_t code_block(const KArgs& k, uint32_t blk) {
-  return k.code_words[(uint64_t)blk * 64u + (threadIdx.x & 63u)];
-}
-
-__device__ __forceinline__ Instr instr_from_block(uint32_t blockw, uint32_t j) {
+__device__ __forceinline__ Instr ld_instr(const KArgs& k, uint32_t pc) {
+  const auto* p = cst((const uint32_t*)k.code) + 8u * pc;
+  // wave-uniform by construction: keep every field in SGPRs (a scalar opcode switch)
   Instr in;
   uint32_t* f = &in.op;
 #pragma unroll
-  for (int q = 0; q < 8; q++) f[q] = (uint32_t)__builtin_amdgcn_readlane((int)blockw, (int)(8u * j + (uint32_t)q));
+  for (int q = 0; q < 8; q++) f[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)p[q]);
   return in;
 }
 
@@ -379,16 +371,13 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
                                                 bool early, bool active) {
   uint32_t verdict = 1;
   const uint32_t n_instr = k.n_instr;
-  // code blocks (see code_block): the current one in a VGPR, the next one in flight (the code
-  // buffer is padded with 16 zero records, so the block after the last is in bounds)
-  uint32_t cur = code_block(k, 0u), nxt = code_block(k, 1u);
+  // the next instruction's scalar load is issued before this one executes, so its latency
+  // overlaps this instruction's LDS traffic instead of adding to it (the code buffer has
+  // one padding record after the last instruction)
+  Instr nx = ld_instr(k, 0);
   for (uint32_t pc = 0; pc < n_instr; pc++) {
-    const uint32_t j = pc & 7u;
-    if (j == 0u && pc != 0u) {
-      cur = nxt;
-      nxt = code_block(k, (pc >> 3) + 1u);
-    }
-    const Instr in = instr_from_block(cur, j);
+    const Instr in = nx;
+    nx = ld_instr(k, pc + 1);
     const uint32_t W = in.wd;
     const uint32_t L = (W + 31) >> 5;
     switch (in.op) {
@@ -870,8 +859,8 @@ static int upload_code(Engine& e, DevProgram& p) {
     }
   }
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  // 16 zeroed Instrs past the end: the interpreter loads the block of 8 after the current one
-  const size_t b_code = al((p.low.code.size() + 16) * sizeof(Instr)), b_consts = al(p.low.consts.size() * 4),
+  // one zeroed Instr past the end: the interpreter prefetches instruction pc + 1
+  const size_t b_code = al((p.low.code.size() + 1) * sizeof(Instr)), b_consts = al(p.low.consts.size() * 4),
                b_aux = al(p.low.aux.size() * 4), b_cw = al(p.low.coord_width.size() * 4);
   const size_t total = std::max<size_t>(b_code + b_consts + b_aux + b_cw, 256);
   int rc = pool_get(e, total, &p.buf, &p.cap);
@@ -948,7 +937,6 @@ static int launch_async(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   k.sk = seed_lane_key(k.seed);
   k.sg = seed_group_key(k.seed);
   k.code = p.d_code;
-  k.code_words = (const uint32_t*)p.d_code;
   k.consts = p.d_consts;
   k.aux = p.d_aux;
   k.coord_width = p.d_coord_width;
