@@ -35,6 +35,18 @@ t("load_gen_us", lambda: eng.free_gen(eng.load_gen(prog, blob)))
 assign = np.zeros(max(P.watch_words, 1), dtype=np.uint32)
 for n in (64, 1 << 12, 1 << 16, 1 << 20):
     t(f"search_{n}_us", lambda n=n: eng.search(prog, gh, 7, 1 << 40, n, early_exit=True))
+for n in (64, 1 << 16):
+    eng.search(prog, gh, 7, 1 << 40, n, early_exit=True)
+    out[f"search_{n}_kernel_us"] = round(1e3 * eng.stats().last_kernel_ms, 1)
+# a one-constraint program: the fixed cost of a search call (launch, hit-buffer copies, sync)
+from mythril_amd.smt import symbol_factory as _sf  # noqa: E402
+_x = _sf.BitVecSym("probe_x", 8)
+P1, blob1 = search.prepare([(_x == _sf.BitVecVal(5, 8)).raw])
+prog1 = eng.load(P1.to_bytes())
+gh1 = eng.load_gen(prog1, blob1)
+t("trivial_search_64_us", lambda: eng.search(prog1, gh1, 7, 1 << 40, 64, early_exit=True))
+eng.search(prog1, gh1, 7, 1 << 40, 64, early_exit=True)
+out["trivial_search_64_kernel_us"] = round(1e3 * eng.stats().last_kernel_ms, 1)
 t("search_hit_with_assign_us", lambda: eng.search(prog, gh, 7, 0, 1 << 16, early_exit=True, assign=assign))
 t("keccak_1_us", lambda: eng.keccak256([b"abc"]))
 t("search_py_total_us", lambda: search.search(eng, roots, timeout_s=10, jit="never"))
