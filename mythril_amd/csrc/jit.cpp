@@ -62,6 +62,77 @@ struct Gen {
     return t.str();
   }
 
+  // Dictionary tables of the generator, staged in LDS by the search/gen kernels' prologue: a
+  // per-lane gather of a 256-bit entry from global memory moves 32 B per lane through the
+  // vector L1 (measured on C2: two 3-entry DICT coordinates cost a quarter of the kernel time),
+  // LDS serves it at twice the bandwidth and nothing else in the kernel uses LDS.  Limbs that
+  // are the same in every entry are literals and are not read at all.
+  std::map<uint32_t, uint32_t> dict_lds;  // gconsts offset of a table -> LDS word offset
+  uint32_t lds_words = 0;
+  static constexpr uint32_t kDictLdsWords = 4096;  // 16 KiB per 256-lane block
+
+  void plan_dict_lds() {
+    dict_lds.clear();
+    lds_words = 0;
+    if (!specs) return;
+    for (uint32_t c = 0; c < specs->size(); c++) {
+      const GenSpec& sp = (*specs)[c];
+      const uint32_t kind = sp.kind & 0xFFu;
+      const uint32_t n = sp.p[1], off = sp.p[0];
+      const bool dict = kind == MG_GEN_DICT || (kind == MG_GEN_MIXED && n && (sp.p[2] >> 16));
+      if (!dict || n == 0 || c >= P.coord_width.size()) continue;
+      const uint32_t w = P.coord_width[c], L = Lw(w);
+      if (!packed_dict(off, n, w, "e").empty() || dict_lds.count(off)) continue;
+      const uint32_t need = (n * L + 3u) & ~3u;  // 16-B aligned tables (ds_read_b128)
+      if (lds_words + need > kDictLdsWords) continue;
+      dict_lds[off] = lds_words;
+      lds_words += need;
+    }
+  }
+
+  // kernel prologue: copy the planned tables into LDS (all 256 lanes), then a block barrier
+  void emit_dict_prologue() {
+    if (!lds_words) return;
+    o << "  __shared__ uint32_t mg_dict[" << lds_words << "];\n";
+    std::map<uint32_t, uint32_t> len;  // table -> words (n * L)
+    for (uint32_t c = 0; c < specs->size(); c++) {
+      const GenSpec& sp = (*specs)[c];
+      auto it = dict_lds.find(sp.p[0]);
+      const uint32_t kind = sp.kind & 0xFFu;
+      if (it == dict_lds.end() || c >= P.coord_width.size()) continue;
+      if (!(kind == MG_GEN_DICT || kind == MG_GEN_MIXED)) continue;
+      len[sp.p[0]] = std::max(len[sp.p[0]], sp.p[1] * Lw(P.coord_width[c]));
+    }
+    for (const auto& kv : len)
+      o << "  for (uint32_t i = tid; i < " << kv.second << "u; i += 256u) mg_dict[" << dict_lds.at(kv.first)
+        << "u + i] = gconsts[" << kv.first << "u + i];\n";
+    o << "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"workgroup\");\n"
+         "  __builtin_amdgcn_s_barrier();\n"
+         "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"workgroup\");\n";
+  }
+
+  // limbs of entry `idx` of the n-entry table at gconsts offset `off` (coordinate width w)
+  template <class Lim>
+  void dict_limbs(uint32_t off, uint32_t n, uint32_t w, const std::string& idx, const Lim& lim, const char* ind) {
+    const uint32_t L = Lw(w);
+    const std::string packed = packed_dict(off, n, w, idx);
+    if (!packed.empty()) {
+      for (uint32_t j = 0; j < L; j++) o << ind << lim(j) << " = " << (j ? std::string("0u") : packed) << ";\n";
+      return;
+    }
+    const auto& G = *gconsts;
+    auto lds = dict_lds.find(off);
+    for (uint32_t j = 0; j < L; j++) {
+      bool same = true;
+      for (uint32_t e = 1; e < n && same; e++) same = G[off + e * L + j] == G[off + j];
+      std::string v;
+      if (same) v = hex(G[off + j]);
+      else if (lds != dict_lds.end()) v = "mg_dict[" + std::to_string(lds->second + j) + "u + " + idx + " * " + std::to_string(L) + "u]";
+      else v = "gconsts[" + std::to_string(off + j) + "u + " + idx + " * " + std::to_string(L) + "u]";
+      o << ind << lim(j) << " = " << v << ";\n";
+    }
+  }
+
   // Spec-specialised GEN3 generator for coordinate c (the same function of (seed, index, c)
   // as gen_coord in engine.hip and gen_value in oracle/bveval.c).  Writes L limbs into
   // `out`_j.  A MIXED coordinate's alternative comes from the group key (SGPRs), so the
@@ -167,12 +238,7 @@ struct Gen {
           branch(below(pc + pd));
           o << "    " << hdecl << "\n";
           o << "    const uint32_t e = ((h >> 16) * " << sp.p[1] << "u) >> 16;\n";
-          const std::string packed = packed_dict(sp.p[0], sp.p[1], width, "e");
-          for (uint32_t j = 0; j < L; j++)
-            o << "    " << lim(j) << " = "
-              << (!packed.empty() ? (j ? std::string("0u") : packed)
-                                  : "gconsts[" + std::to_string(sp.p[0] + j) + "u + e * " + std::to_string(L) + "u]")
-              << ";\n";
+          dict_limbs(sp.p[0], sp.p[1], width, "e", lim, "    ");
           delta(true);
         }
         if (ps) {
@@ -206,12 +272,7 @@ struct Gen {
       }
       case MG_GEN_DICT: {
         o << "  const uint32_t e = ((grnd(ky, " << C << ", 0xFFFFu) >> 16) * " << sp.p[1] << "u) >> 16;\n";
-        const std::string packed = packed_dict(sp.p[0], sp.p[1], width, "e");
-        for (uint32_t j = 0; j < L; j++)
-          o << "  " << lim(j) << " = "
-            << (!packed.empty() ? (j ? std::string("0u") : packed)
-                                : "gconsts[" + std::to_string(sp.p[0] + j) + "u + e * " + std::to_string(L) + "u]")
-            << ";\n";
+        dict_limbs(sp.p[0], sp.p[1], width, "e", lim, "  ");
         break;
       }
       case MG_GEN_RANGE: {
@@ -600,6 +661,9 @@ struct Gen {
       o << "  { uint32_t fold_ = 0u;\n";
       for (const Instr& in : P.vcode) {
         if (in.op != K_COORD || ((*specs)[in.p0].kind & 0xFFu) == MG_GEN_LAZY) continue;
+        // MYTHGPU_JIT_GEN_KIND=<k>: only the coordinates of generator kind k (mythgpu.h mg_gen_kind)
+        if (const char* gk = getenv("MYTHGPU_JIT_GEN_KIND"))
+          if (((*specs)[in.p0].kind & 0xFFu) != (uint32_t)atoi(gk)) continue;
         emit(in, true, false);
         for (uint32_t j = 0; j < Lw(in.wd); j++) o << "  fold_ ^= " << v(in.dst, j) << ";\n";
       }
@@ -616,6 +680,7 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
                        uint32_t kernels) {
   const bool want_search = kernels & JIT_SEARCH, want_eval = kernels & JIT_EVAL, want_gen = kernels & JIT_GEN;
   Gen g(P, specs, gconsts);
+  g.plan_dict_lds();
   auto& o = g.o;
   // hipRTC compiles this with -nogpuinc -nogpulib: its own runtime header still supplies
   // __ballot/atomicMin/..., but no device library is linked (the kernels read work-item
@@ -637,7 +702,9 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  const bool early = (flags & 1u) != 0u;\n"
        "  const uint32_t lane = tid & 63u;\n"
        "  const uint64_t LK = fmix64((uint64_t)lane ^ sk);  // lane half of the lane key (GEN3)\n"
-       "  // one aligned group of 64 candidate indices per wave (GEN3 group key, mythgpu.h)\n"
+       ;
+  g.emit_dict_prologue();
+  o << "  // one aligned group of 64 candidate indices per wave (GEN3 group key, mythgpu.h)\n"
        "  const uint64_t a0 = start & ~63ull, end = start + count;\n"
        "  const uint64_t ngroups = (end - a0 + 63ull) >> 6;\n"
        "  const uint64_t gstride = (uint64_t)nblk * 4u;  // 4 waves per 256-lane block\n"
@@ -685,8 +752,9 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  const uint32_t tid = __builtin_amdgcn_workitem_id_x(), bid = __builtin_amdgcn_workgroup_id_x();\n"
        "  const bool early = false;\n"
        "  const uint32_t lane = tid & 63u;\n"
-       "  const uint64_t LK = fmix64((uint64_t)lane ^ sk);  // lane half of the lane key (GEN3)\n"
-       "  const uint64_t a0 = start & ~63ull, end = start + count;\n"
+       "  const uint64_t LK = fmix64((uint64_t)lane ^ sk);  // lane half of the lane key (GEN3)\n";
+  g.emit_dict_prologue();
+  o << "  const uint64_t a0 = start & ~63ull, end = start + count;\n"
        "  const uint64_t ngroups = (end - a0 + 63ull) >> 6;\n"
        "  const uint64_t gstride = (uint64_t)nblk * 4u;\n"
        "  for (uint64_t g = (uint64_t)bid * 4u + (tid >> 6); g < ngroups; g += gstride) {\n"
