@@ -74,7 +74,11 @@ struct Gen {
   void plan_dict_lds() {
     dict_lds.clear();
     lds_words = 0;
-    if (!specs) return;
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_DICT_LDS");
+      return g && g[0] == '1';
+    }();
+    if (!specs || !on) return;
     for (uint32_t c = 0; c < specs->size(); c++) {
       const GenSpec& sp = (*specs)[c];
       const uint32_t kind = sp.kind & 0xFFu;
