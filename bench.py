@@ -84,6 +84,12 @@ def load_pmc(pmc_dir: str, workload: str, sha: str, candidates: int):
 
 def main():
     args = parse()
+    # stdout carries exactly the one JSON line: native libraries print to fd 1 on their own
+    # (RCCL's version banner at communicator set-up), so fd 1 goes to stderr for the run and the
+    # line is written to the saved stdout
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -287,7 +293,7 @@ def main():
             "hits_in_timed_region": int(total_hits),
             "dropin_stream": stream,
         }
-        print(json.dumps(out), flush=True)
+        os.write(out_fd, (json.dumps(out) + "\n").encode())
     if jit is not None:
         eng.jit_free(jit)
     eng.free_gen(gh)
