@@ -58,7 +58,11 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     write_prelude()
     if not force and not stale():
         return LIB
+    # -structurizecfg-skip-uniform-regions: the interpreter's opcode switch is wave-uniform (an
+    # SGPR opcode), so its regions need no exec-mask structurisation; without the option every
+    # dispatch walks flow blocks of s_mov/s_andn2/s_cbranch_vccnz (1,879 -> 1,507 SALU in k_run)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-mllvm", "-structurizecfg-skip-uniform-regions",
            "-Wno-unused-result", "-o", str(LIB), "-ldl"] + [str(s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

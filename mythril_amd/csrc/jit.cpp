@@ -925,6 +925,13 @@ const std::vector<std::string>& extra_options() {
       std::string t;
       while (is >> t) extra.push_back(t);
     }
+    // MYTHGPU_JIT_SKIP_UNIFORM=1: no exec-mask structurisation of wave-uniform regions (the MIXED
+    // alternatives and the early-exit jumps are SGPR branches), as the engine itself is built
+    if (const char* u = getenv("MYTHGPU_JIT_SKIP_UNIFORM"))
+      if (u[0] == '1') {
+        extra.push_back("-mllvm");
+        extra.push_back("-structurizecfg-skip-uniform-regions");
+      }
   });
   return extra;
 }
