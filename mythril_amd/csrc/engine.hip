@@ -72,7 +72,8 @@ struct KArgs {
   unsigned long long* hits;
   uint64_t start, count, seed, stride;
   uint64_t sk, sg;           // GEN3 seed keys (seed_lane_key / seed_group_key of seed)
-  uint32_t n_instr, value_words, flags, pad;
+  uint32_t n_instr, value_words, flags;
+  uint32_t watch_words;      // SEARCH with `watch`: rows per block of the capture buffer (see K_WATCH)
 };
 
 // uniform struct reads through the constant address space (scalar loads)
@@ -555,6 +556,11 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
       case K_WATCH: {
         if (MODE != MODE_SEARCH && k.watch && active) {
           for (uint32_t j = 0; j < L; j++) k.watch[(uint64_t)(in.p0 + j) * k.count + i] = vf.at(in.a + j);
+        } else if (MODE == MODE_SEARCH && k.watch) {
+          // capture launch (one group per block): every lane's watch rows, [block][row][lane],
+          // so the first hit's model is read back without a second program pass
+          uint32_t* w = k.watch + ((uint64_t)blockIdx.x * k.watch_words + in.p0) * kWave + threadIdx.x;
+          for (uint32_t j = 0; j < L; j++) w[(uint64_t)j * kWave] = vf.at(in.a + j);
         }
         break;
       }
@@ -783,6 +789,8 @@ struct Engine {
   std::unordered_map<uint64_t, std::unique_ptr<DevProgram>> progs;
   std::unordered_map<uint64_t, std::unique_ptr<DevGen>> gens;
   unsigned long long* d_hit = nullptr;  // [0] first hit, [1] hit count
+  uint32_t* d_capture = nullptr;         // watch-row capture of a one-group-per-block search
+  size_t capture_bytes = 0;
   // pinned host staging: [0..1] the reset values, [2..3] the result (async copies on `stream`,
   // one event wait per call instead of two blocking hipMemcpy round trips)
   unsigned long long* h_hit = nullptr;
@@ -905,6 +913,9 @@ static void fill_info(const DevProgram& p, mg_program_info_t* info) {
 
 static int ensure_scratch(Engine& e, size_t bytes) {
   if (bytes <= e.scratch_bytes) return MG_OK;
+  if (e.d_capture) (void)hipFree(e.d_capture);
+  e.d_capture = nullptr;
+  e.capture_bytes = 0;
   if (e.d_scratch) (void)hipFree(e.d_scratch);
   e.d_scratch = nullptr;
   e.scratch_bytes = 0;
@@ -1169,6 +1180,9 @@ static void free_dev_buffers(Engine& e) {
   e.d_watch1 = nullptr;
   e.d_ver1 = nullptr;
   e.watch1_words = 0;
+  if (e.d_capture) (void)hipFree(e.d_capture);
+  e.d_capture = nullptr;
+  e.capture_bytes = 0;
   if (e.d_scratch) (void)hipFree(e.d_scratch);
   e.d_scratch = nullptr;
   e.scratch_bytes = 0;
@@ -1600,11 +1614,48 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
     k.seed = seed;
     k.flags = flags;
     if (count) {
-      int rc = arm_hits(e);
-      if (!rc) rc = launch_async<MODE_SEARCH>(e, it->second->spec, k, count);
+      DevGen& dg = *it->second;
+      const uint32_t ww = dg.spec_watch.low.watch_words;
+      const uint64_t lanes = (start + count) - (start & ~63ull);
+      // a latency-bound launch (every block sweeps one 64-index group, e.g. the first launch of
+      // a get_model query) runs the program with its watch list and captures every lane's
+      // watch rows, so a hit's model needs no second pass (read_assignment); the capture buffer
+      // is blocks x watch_words x 64 words
+      const DevProgram& pw = dg.spec_watch;
+      const uint32_t grid_w = grid_for(e, lanes, pw.lds, pw.low.value_words, pw.heavy);
+      const bool capture = assign_out && ww && pw.uploaded && lanes <= (uint64_t)grid_w * kWave &&
+                           (uint64_t)grid_w * ww * kWave * 4u <= (64ull << 20);
+      int rc = MG_OK;
+      if (capture) {
+        const size_t need = (size_t)grid_w * ww * kWave * 4u;
+        if (need > e.capture_bytes) {
+          if (e.d_capture) (void)hipFree(e.d_capture);
+          e.d_capture = nullptr;
+          e.capture_bytes = 0;
+          HIPCHK(hipMalloc((void**)&e.d_capture, need));
+          e.capture_bytes = need;
+        }
+        k.watch = e.d_capture;
+        k.watch_words = ww;
+      }
+      rc = arm_hits(e);
+      if (!rc) rc = launch_async<MODE_SEARCH>(e, capture ? dg.spec_watch : dg.spec, k, count);
       if (!rc) rc = fetch_hits(e);
       if (!rc) rc = collect_hits(e, e.stats, count, res);
       if (rc) return rc;
+      if (capture) {
+        if (first_hit) *first_hit = res[0];
+        if (n_hits) *n_hits = res[1];
+        e.stats.hits += res[1];
+        if (res[0] == ~0ull) return MG_OK;
+        // the hit's block (one group per block, in order) and lane
+        const uint64_t off = res[0] - (start & ~63ull);
+        const uint64_t b = off / kWave, lane = off % kWave;
+        const uint32_t* src = e.d_capture + (b * ww) * kWave + lane;
+        HIPCHK(hipMemcpy2DAsync(assign_out, 4, src, kWave * 4, 4, ww, hipMemcpyDeviceToHost, e.stream));
+        HIPCHK(hipStreamSynchronize(e.stream));
+        return MG_OK;
+      }
     }
 
   }
