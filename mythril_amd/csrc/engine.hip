@@ -913,9 +913,6 @@ static void fill_info(const DevProgram& p, mg_program_info_t* info) {
 
 static int ensure_scratch(Engine& e, size_t bytes) {
   if (bytes <= e.scratch_bytes) return MG_OK;
-  if (e.d_capture) (void)hipFree(e.d_capture);
-  e.d_capture = nullptr;
-  e.capture_bytes = 0;
   if (e.d_scratch) (void)hipFree(e.d_scratch);
   e.d_scratch = nullptr;
   e.scratch_bytes = 0;
