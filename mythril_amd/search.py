@@ -377,7 +377,7 @@ LAST_ENGINE = None
 LAST_RESULT = None
 
 
-def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int = 1 << 16,
+def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int = 1 << 12,
            max_candidates: int = 1 << 26, timeout_s: float = 10.0, gen: Optional[GenBuilder] = None,
            want_model: bool = True, jit: str = "auto", jit_cost_s: Optional[float] = None) -> SearchResult:
     """Find the lowest-index satisfying candidate (or give up: None).
@@ -455,8 +455,9 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                 if idx is not None:
                     hit, hits = idx, nh
                     break
-                # a first launch of 1024 waves answers the easy queries in one program pass;
-                # then geometric growth amortises the launch + sync per chunk
+                # a first launch of 64 waves answers the easy queries in one program pass, and
+                # with one group per block the engine captures the hit's model in the same pass
+                # (mg_search); then geometric growth amortises the launch + sync per chunk
                 chunk = min(chunk * 4, 1 << 26 if jh is None else 1 << 30)
         finally:
             if ticket is not None:
