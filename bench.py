@@ -187,11 +187,19 @@ def main():
         t1 = time.perf_counter()
         search.search(eng, roots, seed=args.seed, max_candidates=1 << 30, timeout_s=30)
         ttfm_cold_ms = (time.perf_counter() - t1) * 1e3
-        t1 = time.perf_counter()
-        res = search.search(eng, roots, seed=args.seed, max_candidates=1 << 30, timeout_s=30)
-        ttfm_ms = (time.perf_counter() - t1) * 1e3 if res.index is not None else None
+        # warm: the median of 7 repeats (one query is ~1 ms of host + GPU work, so a single
+        # sample is at the mercy of host scheduling); the breakdown is the median run's
+        runs = []
+        for _ in range(7):
+            t1 = time.perf_counter()
+            res = search.search(eng, roots, seed=args.seed, max_candidates=1 << 30, timeout_s=30)
+            runs.append(((time.perf_counter() - t1) * 1e3, res))
+        runs.sort(key=lambda r: r[0])
+        ms, res = runs[len(runs) // 2]
+        ttfm_ms = ms if res.index is not None else None
         ttfm_breakdown = {k: round(v, 3) for k, v in res.timing.items()}
         ttfm_breakdown["engine"] = res.engine
+        ttfm_breakdown["warm_runs"] = len(runs)
 
     # time to first model on ALL ranks: the compiled kernel sweeps epochs of `chunk` candidates per
     # rank from index 0, one all-reduce(MIN) per epoch (distributed.sharded_first_hit); the index found
