@@ -177,6 +177,7 @@ def main():
     ttfm_ms = None
     ttfm_breakdown = None
     ttfm_cold_ms = None
+    ttfm_cold_breakdown = None
     if rank == 0 and not args.no_ttfm:
         # cold: a fresh flatten cache (the query is new to the process), nothing pooled for it yet
         from mythril_amd import ssa as _ssa
@@ -185,8 +186,9 @@ def main():
         search._GEN_CACHE.clear()
         eng.cache_clear()
         t1 = time.perf_counter()
-        search.search(eng, roots, seed=args.seed, max_candidates=1 << 30, timeout_s=30)
+        res_cold = search.search(eng, roots, seed=args.seed, max_candidates=1 << 30, timeout_s=30)
         ttfm_cold_ms = (time.perf_counter() - t1) * 1e3
+        ttfm_cold_breakdown = {k: round(v, 3) for k, v in res_cold.timing.items()}
         # warm: the median of 7 repeats (one query is ~1 ms of host + GPU work, so a single
         # sample is at the mercy of host scheduling); the breakdown is the median run's
         runs = []
@@ -295,6 +297,7 @@ def main():
             "cpu_baseline": cpu,
             "time_to_first_model_ms": ttfm_ms,
             "time_to_first_model_cold_ms": ttfm_cold_ms,
+            "time_to_first_model_cold_breakdown": ttfm_cold_breakdown,
             "time_to_first_model_breakdown": ttfm_breakdown,
             "time_to_first_model_sharded_ms": ttfm_sharded_ms,
             "first_model_index": ttfm_index,

@@ -40,6 +40,7 @@
 namespace mg {
 
 constexpr int kWave = 64;
+constexpr size_t kCaptureBytes = 64ull << 20;  // watch-row capture buffer (mg_search), per device
 constexpr uint32_t kLdsWordsMax = 160;  // value file in LDS up to 160 words (40 KiB per wave)
 
 __device__ __constant__ static const uint32_t kEmptyKeccak[8] = {
@@ -1058,6 +1059,10 @@ static int init_dev(Engine& e, int dev) {
   HIPCHK(hipEventCreateWithFlags(&e.ev2, hipEventDisableTiming));
   HIPCHK(hipMalloc((void**)&e.d_hit, 2 * sizeof(unsigned long long)));
   HIPCHK(hipHostMalloc((void**)&e.h_hit, 4 * sizeof(unsigned long long), hipHostMallocDefault));
+  // the model-capture buffer of latency-bound searches (mg_search), allocated up front so that no
+  // query's time to first model includes the allocation
+  HIPCHK(hipMalloc((void**)&e.d_capture, kCaptureBytes));
+  e.capture_bytes = kCaptureBytes;
   e.device = dev;
   e.cu_count = prop.multiProcessorCount;
   e.clock_mhz = prop.clockRate / 1000;
@@ -1621,16 +1626,21 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
       const DevProgram& pw = dg.spec_watch;
       const uint32_t grid_w = grid_for(e, lanes, pw.lds, pw.low.value_words, pw.heavy);
       const bool capture = assign_out && ww && pw.uploaded && lanes <= (uint64_t)grid_w * kWave &&
-                           (uint64_t)grid_w * ww * kWave * 4u <= (64ull << 20);
+                           (uint64_t)grid_w * ww * kWave * 4u <= kCaptureBytes;
       int rc = MG_OK;
       if (capture) {
-        const size_t need = (size_t)grid_w * ww * kWave * 4u;
-        if (need > e.capture_bytes) {
-          if (e.d_capture) (void)hipFree(e.d_capture);
-          e.d_capture = nullptr;
-          e.capture_bytes = 0;
-          HIPCHK(hipMalloc((void**)&e.d_capture, need));
-          e.capture_bytes = need;
+        // allocated once per device (64 MiB) and the staging rows pinned, so a query's first
+        // search pays neither an allocation nor a pageable copy
+        if (!e.d_capture) {
+          HIPCHK(hipMalloc((void**)&e.d_capture, kCaptureBytes));
+          e.capture_bytes = kCaptureBytes;
+        }
+        if (ww > e.h_watch1_words) {
+          if (e.h_watch1) (void)hipHostFree(e.h_watch1);
+          e.h_watch1 = nullptr;
+          e.h_watch1_words = 0;
+          HIPCHK(hipHostMalloc((void**)&e.h_watch1, (size_t)ww * 4, hipHostMallocDefault));
+          e.h_watch1_words = ww;
         }
         k.watch = e.d_capture;
         k.watch_words = ww;
@@ -1649,8 +1659,9 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
         const uint64_t off = res[0] - (start & ~63ull);
         const uint64_t b = off / kWave, lane = off % kWave;
         const uint32_t* src = e.d_capture + (b * ww) * kWave + lane;
-        HIPCHK(hipMemcpy2DAsync(assign_out, 4, src, kWave * 4, 4, ww, hipMemcpyDeviceToHost, e.stream));
+        HIPCHK(hipMemcpy2DAsync(e.h_watch1, 4, src, kWave * 4, 4, ww, hipMemcpyDeviceToHost, e.stream));
         HIPCHK(hipStreamSynchronize(e.stream));
+        std::memcpy(assign_out, e.h_watch1, (size_t)ww * 4);
         return MG_OK;
       }
     }

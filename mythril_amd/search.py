@@ -458,7 +458,8 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                 # a first launch of 64 waves answers the easy queries in one program pass, and
                 # with one group per block the engine captures the hit's model in the same pass
                 # (mg_search); then geometric growth amortises the launch + sync per chunk
-                chunk = min(chunk * 4, 1 << 26 if jh is None else 1 << 30)
+                # (x16 after the 2^12 capture launch: a query that misses there is not an easy one)
+                chunk = min(chunk * (16 if chunk < (1 << 16) else 4), 1 << 26 if jh is None else 1 << 30)
         finally:
             if ticket is not None:
                 engine.jit_cancel(ticket)
