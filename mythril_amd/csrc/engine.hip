@@ -572,6 +572,13 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
   return verdict;
 }
 
+// one lane's column of a capture block: dst[r] = src[r * 64] (mg_search model read-back)
+__global__ void __launch_bounds__(256) k_gather_rows(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                      uint32_t rows) {
+  const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+  if (r < rows) dst[r] = src[(uint64_t)r * kWave];
+}
+
 template <class VF, int MODE, bool HEAVY>
 __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
   extern __shared__ uint32_t lds[];
@@ -1658,8 +1665,19 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
         // the hit's block (one group per block, in order) and lane
         const uint64_t off = res[0] - (start & ~63ull);
         const uint64_t b = off / kWave, lane = off % kWave;
+        // gather the lane's column on the device (a 2-D copy would load HIP's blit kernel on
+        // first use, milliseconds inside a cold query), then one contiguous read-back
+        if (ww > e.watch1_words) {
+          if (e.d_watch1) (void)hipFree(e.d_watch1);
+          e.d_watch1 = nullptr;
+          e.watch1_words = 0;
+          HIPCHK(hipMalloc((void**)&e.d_watch1, (size_t)ww * 4));
+          e.watch1_words = ww;
+        }
         const uint32_t* src = e.d_capture + (b * ww) * kWave + lane;
-        HIPCHK(hipMemcpy2DAsync(e.h_watch1, 4, src, kWave * 4, 4, ww, hipMemcpyDeviceToHost, e.stream));
+        hipLaunchKernelGGL(k_gather_rows, dim3((ww + 255) / 256), dim3(256), 0, e.stream, src, e.d_watch1, ww);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(e.h_watch1, e.d_watch1, (size_t)ww * 4, hipMemcpyDeviceToHost, e.stream));
         HIPCHK(hipStreamSynchronize(e.stream));
         std::memcpy(assign_out, e.h_watch1, (size_t)ww * 4);
         return MG_OK;
