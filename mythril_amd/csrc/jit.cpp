@@ -925,11 +925,14 @@ const std::vector<std::string>& extra_options() {
       std::string t;
       while (is >> t) extra.push_back(t);
     }
-    // no exec-mask structurisation of wave-uniform regions (the MIXED alternatives and the
-    // early-exit jumps are SGPR branches), as the engine itself is built.  Measured on the
-    // search kernel: C1 -4 %, C2 -3 %, C3 -5 %, C4 -4 %, C5 +3 % time.  MYTHGPU_JIT_SKIP_UNIFORM=0: off
+    // MYTHGPU_JIT_SKIP_UNIFORM=1: no exec-mask structurisation of wave-uniform regions (the MIXED
+    // alternatives and the early-exit jumps are SGPR branches), as the engine itself is built.
+    // Measured on the search kernel: C1 -4 %, C2 -3 %, C3 -5 %, C4 -4 %, C5 +3 % time.  Off by
+    // default: -mllvm options go through comgr's process-global LLVM option state, and a stream
+    // run with it on ended in an LLVM fatal error at process exit (a compile in flight), which
+    // the drop-in cannot risk inside a Mythril process
     const char* u = getenv("MYTHGPU_JIT_SKIP_UNIFORM");
-    if (!u || u[0] != '0') {
+    if (u && u[0] == '1') {
       extra.push_back("-mllvm");
       extra.push_back("-structurizecfg-skip-uniform-regions");
     }
