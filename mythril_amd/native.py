@@ -7,6 +7,7 @@ fallback: if the library or a gfx950 device is missing, the calls raise
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
 import threading
@@ -70,6 +71,15 @@ _lib = None
 _lib_lock = threading.Lock()
 
 
+def _shutdown_at_exit():
+    lib = _lib
+    if lib is not None:
+        try:
+            lib.mg_shutdown()
+        except Exception:  # exiting anyway
+            pass
+
+
 def load_library(path: Optional[Path] = None) -> C.CDLL:
     """Load (and type) the shared library.  Loading needs no GPU."""
     global _lib
@@ -127,6 +137,11 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             fn.restype = res
             fn.argtypes = args
         _lib = lib
+        # stop the engine (its compile thread finishes any compile in flight, modules and
+        # device buffers are released) while Python is still finalising, i.e. before the
+        # C-level exit handlers and library destructors run: a compile thread still inside the
+        # compiler, or HIP work, racing the runtime's teardown can crash the process at exit
+        atexit.register(_shutdown_at_exit)
         return lib
 
 
