@@ -925,14 +925,14 @@ const std::vector<std::string>& extra_options() {
       std::string t;
       while (is >> t) extra.push_back(t);
     }
-    // MYTHGPU_JIT_SKIP_UNIFORM=1: no exec-mask structurisation of wave-uniform regions (the MIXED
-    // alternatives and the early-exit jumps are SGPR branches), as the engine itself is built.
-    // Measured on the search kernel: C1 -4 %, C2 -3 %, C3 -5 %, C4 -4 %, C5 +3 % time.  Off by
-    // default: -mllvm options go through comgr's process-global LLVM option state, and a stream
-    // run with it on ended in an LLVM fatal error at process exit (a compile in flight), which
-    // the drop-in cannot risk inside a Mythril process
+    // no exec-mask structurisation of wave-uniform regions (the MIXED alternatives and the
+    // early-exit jumps are SGPR branches), as the engine itself is built.  Measured on the
+    // search kernel: C1 -4 %, C2 -3 %, C3 -5 %, C4 -4 %, C5 +3 % time; every distinct kernel of
+    // the C1-C4 stream (123) compiles with it.  An LLVM fatal error
+    // seen once at process exit was the compile thread racing the runtime's teardown, fixed by
+    // stopping the engine from Python's atexit (native.py).  MYTHGPU_JIT_SKIP_UNIFORM=0: off
     const char* u = getenv("MYTHGPU_JIT_SKIP_UNIFORM");
-    if (u && u[0] == '1') {
+    if (!u || u[0] != '0') {
       extra.push_back("-mllvm");
       extra.push_back("-structurizecfg-skip-uniform-regions");
     }
