@@ -604,8 +604,10 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
       // every candidate below the current first hit is still evaluated, so the
       // final minimum is exact; waves entirely above it stop
       const unsigned long long cur = __hip_atomic_load(k.first_hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t cur_u = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) |
-                             __builtin_amdgcn_readfirstlane((uint32_t)cur);
+      // readfirstlane returns int: widen through uint32_t, or a low word with bit 31 set would
+      // sign-extend over the high word
+      const uint64_t cur_u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cur);
       if (a0 + base >= cur_u) break;
     }
     GKeys key{};

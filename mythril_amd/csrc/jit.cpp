@@ -715,12 +715,12 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  uint64_t wave_best = ~0ull, wave_hits = 0;  // per-wave, wave-uniform\n"
        "  for (uint64_t g = (uint64_t)bid * 4u + (tid >> 6); g < ngroups; g += gstride) {\n"
        "  const uint64_t gb = a0 + (g << 6);\n"
-       "  const uint64_t gbase = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32)) << 32) | "
-       "__builtin_amdgcn_readfirstlane((uint32_t)gb);\n"
+       "  const uint64_t gbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32)) << 32) | "
+       "(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)gb);\n"
        "  if (early) {\n"
        "    const unsigned long long cur = __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
-       "    const uint64_t cu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) | "
-       "__builtin_amdgcn_readfirstlane((uint32_t)cur);\n"
+       "    const uint64_t cu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) | "
+       "(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cur);\n"
        "    if (gbase >= cu) break;\n"
        "  }\n"
        "  const uint64_t idx = gbase + lane;\n"
@@ -763,8 +763,8 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  const uint64_t gstride = (uint64_t)nblk * 4u;\n"
        "  for (uint64_t g = (uint64_t)bid * 4u + (tid >> 6); g < ngroups; g += gstride) {\n"
        "  const uint64_t gb = a0 + (g << 6);\n"
-       "  const uint64_t gbase = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32)) << 32) | "
-       "__builtin_amdgcn_readfirstlane((uint32_t)gb);\n"
+       "  const uint64_t gbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32)) << 32) | "
+       "(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)gb);\n"
        "  const uint64_t idx = gbase + lane;\n"
        "  const bool active = idx >= start && idx < end;\n"
        "  GKeys ky;\n"

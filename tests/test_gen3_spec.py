@@ -81,7 +81,10 @@ def hits(prog, gen, seed, idx):
 
 SEED = 0x6D797468
 rng = random.Random(3)
-INDICES = [0, 1, 63, 64, 65, 1 << 20, (1 << 40) + 17, (1 << 63) + 5] + [rng.getrandbits(64) for _ in range(6)]
+# indices whose low 32-bit word has bit 31 set pin the kernels' 64-bit index handling (a
+# sign-extended readfirstlane once corrupted the high word of such group bases in the JIT)
+INDICES = [0, 1, 63, 64, 65, (1 << 31) + 7, (1 << 40) | 0x80000041, 1 << 20, (1 << 40) + 17, (1 << 63) + 5,
+           (1 << 63) | 0xFFFFFFC3] + [rng.getrandbits(64) for _ in range(6)]
 
 
 @pytest.mark.parametrize("w", [256, 160, 64, 33, 32, 20])
@@ -123,7 +126,7 @@ def test_gpu_kernels_follow_documented_formula():
     eng = native.Engine.get()
     w = 256
     _, _, c = one_query(w, 0, lambda gb, c: gb.uniform(c))
-    for idx in INDICES[:8]:
+    for idx in INDICES[:11]:
         want = value(uniform_raw(keys(idx, SEED), c, 8), w)
         prog_b, gen_b, _ = one_query(w, want, lambda gb, c: gb.uniform(c))
         prog = eng.load(prog_b)

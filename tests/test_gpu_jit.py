@@ -198,3 +198,27 @@ def evaluate_many_terms(terms, scalars):
     from oracle.bv import evaluate_many
 
     return evaluate_many(terms, OracleModel(scalars))
+
+
+@pytest.mark.gpu
+def test_jit_verdicts_at_high_indices():
+    """Per-candidate JIT verdicts against the C port on windows whose group bases have bit 31 of
+    the low word set, and near 2^63 (64-bit index handling in the kernel prologue)."""
+    from mythril_amd import native, search, workloads
+    from oracle import cport
+
+    eng = native.Engine.get()
+    for name in ("token_transfer_underflow", "etherstore_reentrancy", "bectoken_batch_overflow"):
+        P, blob = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
+        prog = eng.load(P.to_bytes())
+        gh = eng.load_gen(prog, blob)
+        jh = eng.jit_compile(prog, gh, gen_verdicts=True)
+        try:
+            for start in ((1 << 31) - 100, (1 << 40) | 0x80000013, (1 << 63) | 0xFFFFF000, (1 << 62) + 0x9ABCDEF1):
+                _, _, want = cport.search(P.to_bytes(), blob, 0x5EED, start, 1500, threads=8, verdicts=True)
+                got = eng.jit_verdicts(jh, 0x5EED, start, 1500)
+                assert np.array_equal(got, want), (name, hex(start))
+        finally:
+            eng.jit_free(jh)
+            eng.free_gen(gh)
+            eng.free(prog)
