@@ -27,7 +27,10 @@ from __future__ import annotations
 
 import logging
 import os
+import threading
 import time
+from collections import OrderedDict
+from concurrent.futures import FIRST_COMPLETED, ThreadPoolExecutor, wait
 from functools import lru_cache
 
 log = logging.getLogger("mythgpu")
@@ -73,11 +76,18 @@ class HookStats:
         self.rejected = 0      # GPU models z3 did not confirm (kept on z3)
         self.candidates = 0    # candidate assignments the GPU evaluated
         self.gpu_time = 0.0    # seconds inside the GPU attempt (hits and misses)
+        self.races = 0         # queries raced against z3
+        self.z3_answers = 0    # raced queries z3 answered (GPU miss or slower)
+        self.race_z3_time = 0.0   # z3 check seconds of those
+        self.race_overhead = 0.0  # hook wall time beyond z3's own, summed over them
+        self.negative_hits = 0    # repeats of a GPU-missed unsat/unknown tuple sent straight to z3
 
     def __repr__(self):
         return (f"mythgpu: {self.queries} queries, {self.gpu_models} GPU models, {self.fallbacks} to z3 "
                 f"({self.unsupported} unsupported, {self.errors} errors, {self.rejected} rejected), "
-                f"{self.candidates} candidates in {self.gpu_time:.3f} s")
+                f"{self.candidates} candidates in {self.gpu_time:.3f} s; {self.races} raced, "
+                f"{self.z3_answers} by z3 (+{self.race_overhead * 1e3:.1f} ms over z3), "
+                f"{self.negative_hits} negative-cache repeats")
 
 
 STATS = HookStats()
@@ -95,7 +105,7 @@ def _solver_statistics():
     return SolverStatistics()
 
 
-def _record(dt: float, gpu_model: bool) -> None:
+def _record(dt: float, answered: bool) -> None:
     """Feed the hook's work into LASER's ``SolverStatistics`` (what ``--solver-log`` /
     the statistics report print): a query the GPU answered never reaches the
     ``stat_smt_query``-wrapped z3 check, so it is counted here, with its time; the GPU
@@ -103,7 +113,7 @@ def _record(dt: float, gpu_model: bool) -> None:
     st = _solver_statistics()
     if st is None:
         return
-    if gpu_model and getattr(st, "enabled", False):
+    if answered and getattr(st, "enabled", False):
         st.query_count += 1
         st.solver_time += dt
     st.gpu_models = STATS.gpu_models
@@ -111,26 +121,118 @@ def _record(dt: float, gpu_model: bool) -> None:
     st.gpu_time = STATS.gpu_time
 
 
+class NegativeCache:
+    """Bounded LRU set of constraint tuples that the GPU missed AND z3 answered unsat/unknown.
+    Keys are the tuples ``get_model`` receives, hashed and compared exactly as its
+    ``lru_cache`` does (``Bool.__hash__``/``__eq__``, ``laser/smt/bool.py:50-84``).  A repeat
+    goes straight to the reference's z3 path: the ``lru_cache`` does not cache ``UnsatError``,
+    and LASER re-asks (``Constraints.is_possible`` per successor, ``svm.py:252-257``; the
+    modules at the end of a transaction)."""
+
+    def __init__(self, size: int = 4096):
+        self.size = size
+        self._d = OrderedDict()
+
+    def __contains__(self, key) -> bool:
+        try:
+            if key in self._d:
+                self._d.move_to_end(key)
+                return True
+        except Exception:  # an unhashable/uncomparable key is simply not cached
+            pass
+        return False
+
+    def add(self, key) -> None:
+        try:
+            self._d[key] = True
+            self._d.move_to_end(key)
+        except Exception:
+            return
+        while len(self._d) > self.size:
+            self._d.popitem(last=False)
+
+    def clear(self) -> None:
+        self._d.clear()
+
+    def __len__(self) -> int:
+        return len(self._d)
+
+
+NEGATIVE = NegativeCache()
+# z3 runs on its own worker threads, the GPU search on one more: ctypes releases the GIL inside
+# ``Z3_optimize_check`` and inside every engine call, so both make progress while the calling
+# thread waits for the first answer.  Two z3 workers: an interrupted check that is slow to
+# notice ``Z3_interrupt`` does not hold up the next query's.
+_Z3_POOL = ThreadPoolExecutor(max_workers=2, thread_name_prefix="mythgpu-z3")
+_GPU_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="mythgpu-gpu")
+# longest single launch while racing: after z3 answers, the engine is free within this
+RACE_LAUNCH_S = 0.002
+
+
+class Z3Race:
+    """The reference's own check of the query (``support/model.py:25-49``: ``Optimize``, the
+    same timeout, no objectives), run in a fresh ``z3.Context`` on a worker thread.  The
+    constraints are translated on the calling thread (LASER's main context is not
+    thread-safe); the worker touches only the fresh context.  ``interrupt`` is
+    ``Z3_interrupt`` on that context, which z3 allows from any thread."""
+
+    def __init__(self, z3, constraints, timeout_ms: int):
+        self.z3 = z3
+        self.ctx = z3.Context()
+        self.raws = [getattr(c, "raw", c).translate(self.ctx) for c in constraints]
+        self.timeout_ms = max(1, int(timeout_ms))
+        self.result = None
+        self.model = None
+        self.seconds = 0.0
+
+    def run(self):
+        z3 = self.z3
+        t0 = time.perf_counter()
+        s = z3.Optimize(ctx=self.ctx)
+        s.set("timeout", self.timeout_ms)
+        s.add(*self.raws)
+        self.result = s.check()
+        if self.result == z3.sat:
+            self.model = s.model()
+        self.seconds = time.perf_counter() - t0
+        return self
+
+    def interrupt(self) -> None:
+        try:
+            self.ctx.interrupt()
+        except Exception:  # pragma: no cover - the check already ended
+            pass
+
+
+def _unsat_error():
+    from mythril.exceptions import UnsatError  # type: ignore
+
+    return UnsatError
+
+
 def gpu_first(original):
-    """Build the cached hook around the reference's ``get_model``."""
+    """Build the cached hook around the reference's ``get_model``.
+
+    With ``MYTHGPU_RACE`` unset or ``1`` (the default) the GPU search and the reference's z3
+    check race (``_race``): a GPU miss then costs only the hand-off, not the GPU slice.  With
+    ``MYTHGPU_RACE=0`` the GPU searches first and z3 runs after a miss (``_try_gpu``)."""
 
     @lru_cache(maxsize=2 ** 23)
     def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True):
         STATS.queries += 1
         if minimize or maximize or os.environ.get("MYTHGPU_DISABLE") == "1":
             return original(constraints, minimize, maximize, enforce_execution_time)
+        if constraints in NEGATIVE:
+            STATS.negative_hits += 1
+            return original(constraints, minimize, maximize, enforce_execution_time)
+        if os.environ.get("MYTHGPU_RACE", "1") != "0":
+            return _race(original, constraints, enforce_execution_time)
         model = None
         t0 = time.perf_counter()
         try:
             model = _try_gpu(constraints, enforce_execution_time)
         except Exception as e:  # never raise a new exception type into LASER
-            from .ssa import Unsupported
-
-            if isinstance(e, Unsupported):
-                STATS.unsupported += 1
-            else:
-                STATS.errors += 1
-                log.debug("mythgpu: engine error, falling back to z3: %s", e)
+            _count_error(e)
         dt = time.perf_counter() - t0
         STATS.gpu_time += dt
         if model is not None:
@@ -142,54 +244,170 @@ def gpu_first(original):
         return original(constraints, minimize, maximize, enforce_execution_time)
 
     get_model.__wrapped_original__ = original
+    get_model.negative_cache = NEGATIVE
     return get_model
 
 
+def _count_error(e) -> None:
+    from .ssa import Unsupported
+
+    if isinstance(e, Unsupported):
+        STATS.unsupported += 1
+    else:
+        STATS.errors += 1
+        log.debug("mythgpu: engine error, falling back to z3: %s", e)
+
+
+def _budgets(constraints, enforce_execution_time):
+    """The reference's budget arithmetic (``support/model.py:26-31``): ``(cs, z3 budget ms,
+    GPU slice ms)``, or None where the reference raises before solving (no time left, a
+    literal ``False``) or where there is nothing to search (only literal ``True``)."""
+    from mythril.laser.ethereum.time_handler import time_handler  # type: ignore
+    from mythril.support.support_args import args  # type: ignore
+
+    total = float(args.solver_timeout)
+    if enforce_execution_time:
+        total = min(total, time_handler.time_remaining() - 500)
+    if total <= 0 or any(type(c) == bool and not c for c in constraints):
+        return None
+    cs = [c for c in constraints if type(c) != bool]
+    if not cs:
+        return None
+    return cs, total, min(total, float(os.environ.get("MYTHGPU_BUDGET_MS", "200")))
+
+
+def _race(original, constraints, enforce_execution_time):
+    """z3 and the GPU on the same query, first answer wins (``get_model``'s contract,
+    ``support/model.py:15-49``):
+
+    * z3 answers first: the GPU search is cancelled (it stops at its next launch boundary,
+      launches are at most ``RACE_LAUNCH_S`` long) and z3's answer is returned — ``sat`` as the
+      reference's ``Model([z3.ModelRef])`` (translated back to the main context), ``unsat`` /
+      ``unknown`` as ``UnsatError``, exactly as the reference raises;
+    * the GPU hits first: the hit is re-checked by z3 (``pin_model``) and returned, and the z3
+      worker is interrupted; a model z3 does not confirm is dropped and z3's answer awaited;
+    * the GPU misses: z3's answer is awaited; a z3 ``unsat``/``unknown`` puts the tuple in the
+      negative cache, so a repeat does not search again.
+
+    Whatever the GPU side does — unsupported operator, engine error — only z3's answer can
+    then come back, so the hook never changes a verdict and never raises a new exception
+    type.  The hook's own z3 check is counted in LASER's ``SolverStatistics`` here, as
+    ``stat_smt_query`` (``solver_statistics.py:8-25``) counts the reference's."""
+    from . import z3bridge
+
+    t0 = time.perf_counter()
+    try:
+        from mythril.laser.smt import Model  # type: ignore
+
+        b = _budgets(constraints, enforce_execution_time)
+    except Exception as e:  # no Mythril around the hook: nothing to race
+        _count_error(e)
+        b = None
+    if b is None:
+        return original(constraints, (), (), enforce_execution_time)
+    cs, total, gpu_ms = b
+    terms = None
+    try:
+        terms = z3bridge.to_terms(cs)
+    except Exception as e:
+        _count_error(e)
+    if terms is None:  # nothing to race: the reference's path, unchanged
+        STATS.fallbacks += 1
+        return original(constraints, (), (), enforce_execution_time)
+    z3 = z3bridge.z3
+    try:
+        race = Z3Race(z3, cs, total)
+    except Exception as e:  # translation refused: the reference's path, unchanged
+        log.debug("mythgpu: cannot race z3 on this query: %s", e)
+        STATS.fallbacks += 1
+        return original(constraints, (), (), enforce_execution_time)
+    cancel = threading.Event()
+    f_z3 = _Z3_POOL.submit(race.run)
+    f_gpu = _GPU_POOL.submit(_gpu_search, terms, gpu_ms / 1000.0, cancel)
+    STATS.races += 1
+    try:
+        done, _ = wait([f_z3, f_gpu], return_when=FIRST_COMPLETED)
+        if f_z3 not in done:
+            res = None
+            try:
+                res = f_gpu.result()
+            except Exception as e:
+                _count_error(e)
+            model = _confirm(cs, res, total - (time.perf_counter() - t0) * 1e3)
+            if model is not None:
+                race.interrupt()
+                STATS.gpu_models += 1
+                _record(time.perf_counter() - t0, True)
+                return Model([model])
+        r = f_z3.result()  # z3's own answer (an exception in z3 propagates, as in the reference)
+    finally:
+        cancel.set()
+    STATS.z3_answers += 1
+    dt = time.perf_counter() - t0
+    STATS.race_z3_time += r.seconds
+    STATS.race_overhead += max(0.0, dt - r.seconds)
+    _record(dt, True)
+    if r.result == z3.sat:
+        return Model([r.model.translate(z3.main_ctx())])
+    NEGATIVE.add(constraints)
+    if r.result == z3.unknown:
+        log.debug("Timeout encountered while solving expression using z3")
+    raise _unsat_error()
+
+
+def _gpu_search(terms, budget_s, cancel):
+    from .native import Engine
+    from .search import search_partitioned
+
+    t0 = time.perf_counter()
+    try:
+        res = search_partitioned(Engine.get(), terms, timeout_s=budget_s, max_candidates=1 << 40,
+                                 cancel=cancel, max_launch_s=RACE_LAUNCH_S)
+    finally:
+        STATS.gpu_time += time.perf_counter() - t0
+    STATS.candidates += res.scanned
+    return res
+
+
+def _confirm(cs, res, left_ms):
+    """A GPU hit re-checked by z3 in a fresh context (``z3bridge.pin_model``), or None."""
+    from . import z3bridge
+    from .solver import Model as GpuModel
+
+    if res is None or res.index is None or left_ms <= 0:
+        return None
+    ver, scalars, arrays, funcs, _ = res.model
+    if not ver:
+        return None
+    z3m = z3bridge.pin_model(cs, GpuModel(scalars, arrays, funcs), timeout_ms=left_ms)
+    if z3m is None:
+        STATS.rejected += 1
+        log.warning("mythgpu: z3 did not confirm a GPU model (kept on z3)")
+    return z3m
+
+
 def _try_gpu(constraints, enforce_execution_time):
-    """One GPU attempt at ``get_model`` (``support/model.py:15-49``): the budget is the
+    """One GPU attempt at ``get_model`` before z3 (``MYTHGPU_RACE=0``): the budget is the
     smaller of the query's z3 budget (``args.solver_timeout``, minus the execution-time
     reserve the reference keeps) and the hook's slice ``MYTHGPU_BUDGET_MS``; the search
     escalates to the compiled kernel inside it (``search.search``, async compile).  A hit
     is re-checked by z3 (``pin_model``) with what is left of the query's z3 budget."""
-    from mythril.laser.ethereum.time_handler import time_handler  # type: ignore
     from mythril.laser.smt import Model  # type: ignore
-    from mythril.support.support_args import args  # type: ignore
 
     from . import z3bridge
     from .native import Engine
     from .search import search_partitioned
 
     t0 = time.perf_counter()
-    if any(type(c) == bool and not c for c in constraints):
-        return None  # the original raises UnsatError for this
-    cs = [c for c in constraints if type(c) != bool]
-    if not cs:
+    b = _budgets(constraints, enforce_execution_time)
+    if b is None:
         return None
-    total = float(args.solver_timeout)
-    if enforce_execution_time:
-        total = min(total, time_handler.time_remaining() - 500)
-    budget = min(total, float(os.environ.get("MYTHGPU_BUDGET_MS", "200")))
-    if budget <= 0:
-        return None
+    cs, total, budget = b
     terms = z3bridge.to_terms(cs)
     res = search_partitioned(Engine.get(), terms, timeout_s=budget / 1000.0, max_candidates=1 << 40)
     STATS.candidates += res.scanned
-    if res.index is None:
-        return None
-    ver, scalars, arrays, funcs, _ = res.model
-    if not ver:
-        return None
-    from .solver import Model as GpuModel
-
-    left_ms = total - (time.perf_counter() - t0) * 1e3
-    if left_ms <= 0:
-        return None
-    z3m = z3bridge.pin_model(cs, GpuModel(scalars, arrays, funcs), timeout_ms=left_ms)
-    if z3m is None:
-        STATS.rejected += 1
-        log.warning("mythgpu: z3 did not confirm a GPU model (kept on z3)")
-        return None
-    return Model([z3m])
+    z3m = _confirm(cs, res, total - (time.perf_counter() - t0) * 1e3)
+    return None if z3m is None else Model([z3m])
 
 
 def batched_replace_with_actual_sha(concrete_transactions, model, code=None):

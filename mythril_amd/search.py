@@ -379,7 +379,8 @@ LAST_RESULT = None
 
 def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int = 1 << 12,
            max_candidates: int = 1 << 26, timeout_s: float = 10.0, gen: Optional[GenBuilder] = None,
-           want_model: bool = True, jit: str = "auto", jit_cost_s: Optional[float] = None) -> SearchResult:
+           want_model: bool = True, jit: str = "auto", jit_cost_s: Optional[float] = None,
+           cancel=None, max_launch_s: Optional[float] = None) -> SearchResult:
     """Find the lowest-index satisfying candidate (or give up: None).
 
     ``jit``: "never" keeps the generic interpreter (``k_run``, no compile latency);
@@ -392,7 +393,9 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
     every index (``tests/test_gpu_jit.py``), so the first hit does not depend on the mode.
 
     Launch sizes grow geometrically from ``chunk`` (easy queries answer in the first
-    launch) and are capped by the measured rate so that a launch ends inside the budget.
+    launch) and are capped by the measured rate so that a launch ends inside the budget
+    (and inside ``max_launch_s``).  ``cancel`` (a ``threading.Event``) is checked before
+    every launch: the hook sets it when z3 answered first (``plugin._race``).
     The model comes back with the hit (``mg_search``'s ``assign_out``)."""
     tp = time.perf_counter()
     P, blob = prepare(roots, gen)
@@ -415,14 +418,17 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
         try:
             if jit == "always":
                 tc = time.perf_counter()
-                jh = engine.jit_compile(prog, gh)
-                timing["jit_compile_ms"] = (time.perf_counter() - tc) * 1e3
-                used = "jit"
+                try:
+                    jh = engine.jit_compile(prog, gh)
+                    timing["jit_compile_ms"] = (time.perf_counter() - tc) * 1e3
+                    used = "jit"
+                except Exception:  # the JIT rejected this program: scan on the interpreter
+                    jit = "never"
             start = 0
             while scanned < max_candidates:
                 now = time.perf_counter()
                 left = timeout_s - (now - t0)
-                if left <= 0:
+                if left <= 0 or (cancel is not None and cancel.is_set()):
                     break
                 if ticket is not None:
                     try:
@@ -442,6 +448,8 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                 n = min(chunk, max_candidates - scanned)
                 if rate:
                     cap_s = min(left, JIT_POLL_S) if ticket is not None else left
+                    if max_launch_s is not None:
+                        cap_s = min(cap_s, max_launch_s)
                     n = max(1, min(n, int(rate * cap_s)))
                 tl = time.perf_counter()
                 if jh is not None:
@@ -499,7 +507,11 @@ def search_partitioned(engine, roots: Sequence[T.Term], timeout_s: float = 10.0,
     engines = set()
     for b in buckets:
         left = timeout_s - (time.perf_counter() - t0)
-        r = search(engine, b, timeout_s=max(left, 1e-3), **kw)
+        if left <= 0 or (kw.get("cancel") is not None and kw["cancel"].is_set()):
+            res = SearchResult(None, 0, scanned, time.perf_counter() - t0)
+            res.buckets = len(buckets)
+            return res
+        r = search(engine, b, timeout_s=left, **kw)
         scanned += r.scanned
         engines.add(getattr(r, "engine", "interp"))
         if r.index is None:

@@ -284,3 +284,18 @@ WORKLOADS = {
     "walletlibrary_kill": walletlibrary_kill,
     "sha3_keyed_mapping": sha3_keyed_mapping,
 }
+
+# the BASELINE.json config each workload stands for (``configs[i]`` -> "C{i+1}")
+CONFIG = {
+    "suicide_kill": "C1",
+    "token_transfer_underflow": "C2",
+    "etherstore_reentrancy": "C2",
+    "bectoken_batch_overflow": "C3",
+    "walletlibrary_kill": "C4",
+    "sha3_keyed_mapping": "C5",
+}
+
+
+def test_id(name: str) -> str:
+    """``C2-token_transfer_underflow``: the config label tests carry in their ids."""
+    return f"{CONFIG[name]}-{name}"

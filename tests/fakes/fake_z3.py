@@ -13,10 +13,17 @@ The solver is a checker, not a decision procedure: ``check()`` reads the pins
 every assertion under them with its own evaluator (independent of the engine's oracle)
 and answers sat / unsat; ``Solver.FORCE`` makes it answer ``unknown`` (a z3 timeout).
 Every Solver records itself in ``Solver.instances`` (context, parameters) for the tests.
+
+``Optimize`` stands in for the reference's own check (``support/model.py:25-49``) that the hook
+races: ``Optimize.DELAY`` seconds of "solving" (interruptible through ``Context.interrupt``, then
+``unknown``), after which it answers ``Optimize.ANSWER`` (``sat`` with an all-zero model, or
+``unsat``/``unknown``); ``Optimize.calls`` records (thread name, timeout, seconds, result).
 """
 from __future__ import annotations
 
 import itertools
+import threading
+import time
 
 _ids = itertools.count(1)
 
@@ -33,6 +40,11 @@ for _i, _n in enumerate(_OP_NAMES):
 class Context:
     def __init__(self):
         self.id = next(_ids)
+        self.interrupted = threading.Event()
+
+    def interrupt(self):
+        """``Z3_interrupt``: callable from any thread; a running check returns ``unknown``."""
+        self.interrupted.set()
 
 
 _MAIN = Context()
@@ -577,3 +589,24 @@ class Solver:
 
     def model(self):
         return self._model
+
+
+class Optimize(Solver):
+    DELAY = 0.0
+    ANSWER = None  # None: check the assertions like Solver (all symbols 0 unless pinned)
+    calls = []
+
+    def check(self, *args):
+        t0 = time.perf_counter()
+        interrupted = self.ctx.interrupted.wait(Optimize.DELAY) if Optimize.DELAY > 0 else False
+        if interrupted:
+            r = unknown
+        elif Optimize.ANSWER is not None:
+            r = Optimize.ANSWER
+            if r is sat:
+                self._model = ModelRef(({}, {}, {}), self.ctx)
+        else:
+            r = Solver.check(self)
+        Optimize.calls.append((threading.current_thread().name, self.params.get("timeout"),
+                               time.perf_counter() - t0, r))
+        return r

@@ -23,7 +23,7 @@ def test_cport_eval_matches_python_oracle(seed):
         assert ver[i] == want, (seed, i)
 
 
-@pytest.mark.parametrize("name", sorted(workloads.WORKLOADS))
+@pytest.mark.parametrize("name", sorted(workloads.WORKLOADS), ids=workloads.test_id)
 def test_cport_generator_matches_python_oracle_on_workloads(name):
     """Search-mode candidates (generator restated in C) evaluated by the C port agree
     with the Python oracle evaluating the same coordinates."""

@@ -11,7 +11,7 @@ SEED = 0x6D797468
 
 
 @pytest.mark.parametrize("name", ["suicide_kill", "token_transfer_underflow", "etherstore_reentrancy",
-                                  "bectoken_batch_overflow", "walletlibrary_kill"])
+                                  "bectoken_batch_overflow", "walletlibrary_kill"], ids=workloads.test_id)
 def test_capture_matches_readback(name):
     eng = native.Engine.get()
     roots = [c.raw for c in workloads.WORKLOADS[name]()]

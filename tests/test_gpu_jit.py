@@ -74,7 +74,7 @@ def test_jit_eval_vmtests_sample(engine):
 
 @pytest.mark.parametrize("aux", [False, True])
 @pytest.mark.parametrize("shaped", [False, True])
-@pytest.mark.parametrize("name", sorted(workloads.WORKLOADS))
+@pytest.mark.parametrize("name", sorted(workloads.WORKLOADS), ids=workloads.test_id)
 def test_jit_search_matches_interpreter_and_c(engine, name, shaped, aux):
     from oracle import cport
 

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from helpers import RandomProgram, gpu_eval_terms, load_json, random_assignments, vmtest_cases
-from mythril_amd import search, ssa
+from mythril_amd import search, ssa, workloads
 from mythril_amd.replay import replay_assignment
 from mythril_amd.smt import (And, Array, BVMulNoOverflow, Concat, Function, LShR, Not, UGE, UGT, ULT,
                              symbol_factory)
@@ -267,7 +267,7 @@ WORKLOAD_NAMES = ["token_transfer_underflow", "etherstore_reentrancy", "bectoken
 
 @pytest.mark.parametrize("aux", [False, True])
 @pytest.mark.parametrize("shaped", [False, True])
-@pytest.mark.parametrize("name", WORKLOAD_NAMES)
+@pytest.mark.parametrize("name", WORKLOAD_NAMES, ids=workloads.test_id)
 def test_workload_verdicts_match_c_restatement(engine, name, shaped, aux):
     """Every candidate verdict of the benchmark workloads (search-mode generator, broad
     or propagation-shaped; full evaluation) equals the C restatement's, and the search
@@ -292,7 +292,7 @@ def test_workload_verdicts_match_c_restatement(engine, name, shaped, aux):
     assert (gfirst, ghits) == (cfirst, chits)
 
 
-@pytest.mark.parametrize("name", WORKLOAD_NAMES)
+@pytest.mark.parametrize("name", WORKLOAD_NAMES, ids=workloads.test_id)
 def test_workload_models_verified(engine, name):
     """The GPU finds a model of each workload query and the oracle accepts it."""
     from mythril_amd import workloads

@@ -8,7 +8,7 @@ unsat/unknown)."""
 import numpy as np
 import pytest
 
-from mythril_amd import solver
+from mythril_amd import solver, workloads
 from mythril_amd.keccak_model import KeccakFunctionManager
 from mythril_amd.smt import And, Array, If, symbol_factory
 from mythril_amd.solver import Solver, sat, unknown
@@ -247,7 +247,7 @@ def test_partitioned_search_with_ground_bucket(engine):
                                      max_candidates=1 << 22).index is None
 
 
-@pytest.mark.parametrize("name", ["suicide_kill", "token_transfer_underflow", "walletlibrary_kill", "sha3_keyed_mapping"])
+@pytest.mark.parametrize("name", ["suicide_kill", "token_transfer_underflow", "walletlibrary_kill", "sha3_keyed_mapping"], ids=workloads.test_id)
 def test_assign_out_equals_materialized_model(engine, name):
     """mg_search's assign_out (the winning candidate's watch rows, written with the hit)
     equals the model read back by a separate generated evaluation of that index, for the

@@ -36,8 +36,11 @@ def fz3(monkeypatch):
     monkeypatch.setattr(z3bridge, "_OPS", None)
     z3.Solver.instances.clear()
     z3.Solver.FORCE = None
+    z3.Optimize.DELAY, z3.Optimize.ANSWER = 0.0, None
+    z3.Optimize.calls.clear()
     yield z3
     z3.Solver.FORCE = None
+    z3.Optimize.DELAY, z3.Optimize.ANSWER = 0.0, None
 
 
 # ---------------------------------------------------------------------------------------
@@ -201,6 +204,10 @@ class _Stats:
         return cls._inst
 
 
+class _UnsatError(Exception):
+    """``mythril.exceptions.UnsatError`` (``exceptions.py:16-20``)."""
+
+
 class _LaserModel:
     def __init__(self, models):
         self.raw = models
@@ -240,6 +247,7 @@ def mythril_standin(monkeypatch, fz3):
     mod("mythril.support.model", get_model=original)
     mod("mythril.laser.ethereum.state.constraints", get_model=original)
     mod("mythril.analysis.solver", get_model=original, _replace_with_actual_sha=original_sha)
+    mod("mythril.exceptions", UnsatError=_UnsatError)
     monkeypatch.setattr(plugin, "HAVE_MYTHRIL", True)
     monkeypatch.setattr(plugin, "_ORIGINAL", None)
     monkeypatch.setattr(plugin, "_ORIGINAL_SHA", None)
@@ -248,13 +256,20 @@ def mythril_standin(monkeypatch, fz3):
 
     from mythril_amd import native, search
 
-    state = types.SimpleNamespace(result=None, delay=0.0, raise_=None, budgets=[])
+    state = types.SimpleNamespace(result=None, delay=0.0, raise_=None, budgets=[], cancelled=[])
 
-    def fake_search(engine, terms, timeout_s, **kw):
+    def fake_search(engine, terms, timeout_s, cancel=None, **kw):
+        """The GPU search: ``delay`` seconds of launches, stopping at a launch boundary
+        (every 1 ms) once ``cancel`` is set, as search.search does."""
         state.budgets.append(timeout_s)
         if state.raise_ is not None:
             raise state.raise_
-        time.sleep(state.delay)
+        t_end = time.perf_counter() + state.delay
+        while time.perf_counter() < t_end:
+            if cancel is not None and cancel.is_set():
+                state.cancelled.append(True)
+                return SearchResult(None, 0, 1 << 20, 0.0)
+            time.sleep(0.001)
         return state.result
 
     monkeypatch.setattr(search, "search_partitioned", fake_search)
@@ -305,7 +320,9 @@ def test_try_gpu_every_branch(mythril_standin):
     assert 0 < z3.Solver.instances[-1].params["timeout"] <= 10_000
 
 
-def test_gpu_first_counts_and_falls_back(mythril_standin):
+def test_gpu_first_counts_and_falls_back(mythril_standin, monkeypatch):
+    """The sequential mode (``MYTHGPU_RACE=0``): GPU slice first, then the reference's z3."""
+    monkeypatch.setenv("MYTHGPU_RACE", "0")
     S = mythril_standin
     cs = tuple(_query())
     hooked = plugin.gpu_first(S.original)
