@@ -2,7 +2,10 @@
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1
 it is launched by torch.distributed.run, one rank per GPU.  Rank 0 prints ONE
-JSON line.
+JSON line.  ``--gpus N`` without a launcher (no ``WORLD_SIZE``) runs the product's own
+multi-GPU path instead: one process opens N devices (``mg_init`` mask) and the shim splits
+every search over them (``parallelism: inprocN``); it exits 2 if fewer than N GPUs are
+visible.
 
 A *step* is one full sweep of the hot path over one batch of candidates: every
 rank evaluates C candidates of the workload's constraint program (no early exit:
@@ -99,6 +102,16 @@ def main():
 
     # launched by torch.distributed.run (even at one rank): use the RCCL exchange path
     distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    # --gpus N without a launcher: the product's own multi-GPU path — one process opens N devices
+    # (mg_init mask) and every search call is split over them inside the shim, host min/sum
+    inproc = 1
+    if not distributed and args.gpus > 1:
+        visible = torch.cuda.device_count()
+        if visible < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible", file=sys.stderr)
+            sys.exit(2)
+        inproc = args.gpus
+        os.environ["MYTHGPU_DEVICES"] = ",".join(str(d) for d in range(inproc))
     torch.cuda.set_device(local_rank)
     if distributed:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -111,6 +124,9 @@ def main():
         dist.barrier()
     os.environ["MYTHGPU_DEVICE"] = str(local_rank)
     eng = native.Engine.get()
+    if eng.n_devices != inproc:
+        print(f"bench.py: engine opened {eng.n_devices} device(s), wanted {inproc}", file=sys.stderr)
+        sys.exit(2)
 
     cs = workloads.WORKLOADS[args.workload]()
     roots = [c.raw for c in cs]
@@ -138,12 +154,15 @@ def main():
 
     from mythril_amd.distributed import chunk_start, first_hit_allreduce
 
+    # in-process multi-GPU: one call sweeps inproc x C candidates, split over the devices in the shim
+    CC = C * inproc
+
     def step(s):
-        start = chunk_start(s, rank, world, C)
+        start = chunk_start(s, rank, world, CC)
         if jit is not None:
-            idx, nh = eng.jit_search(jit, args.seed, start, C, early_exit=False)
+            idx, nh = eng.jit_search(jit, args.seed, start, CC, early_exit=False)
         else:
-            idx, nh = eng.search(prog, gh, args.seed, start, C, early_exit=False)
+            idx, nh = eng.search(prog, gh, args.seed, start, CC, early_exit=False)
         if distributed:  # the path's one exchange step: all-reduce(MIN) of the first hit over RCCL
             idx = first_hit_allreduce(idx, device="cuda")
         return idx, nh
@@ -224,7 +243,7 @@ def main():
     else:
         ttfm_index = None
         for e in range(1024):
-            ttfm_index = first_hit(e << 20, 1 << 20)
+            ttfm_index = first_hit(e * inproc << 20, inproc << 20)
             if ttfm_index is not None:
                 break
     ttfm_sharded_ms = (time.perf_counter() - t1) * 1e3 if ttfm_index is not None else None
@@ -232,7 +251,7 @@ def main():
     # the drop-in under a LASER-shaped stream of this workload's queries through solver.get_model,
     # 200 ms budget each (tools/stream_bench.py; async JIT compile inside the budget), rank 0
     stream = None
-    if rank == 0 and world == 1 and not args.no_stream:
+    if rank == 0 and world == 1 and inproc == 1 and not args.no_stream:
         sys.path.insert(0, str(Path(__file__).resolve().parent / "tools"))
         import stream_bench
 
@@ -243,14 +262,19 @@ def main():
                   "engines": r0["engines"], "jit_compile_s_avg": summ["jit_compile_s_avg"],
                   "note": "candidates/s through solver.get_model incl. flatten, async compile, model read-back; "
                           "waves rejected by an early constraint stop there (early exit)"}
+        # the same stream through the hook's race core against a z3 stand-in answering unsat after 50 ms:
+        # what a GPU miss adds to z3's own time (plugin.race; no z3 on the box)
+        rr = stream_bench.run_race([args.workload], 200.0, 50.0, quiet=True)[0]
+        stream["race"] = {k: rr[k] for k in ("race_z3_standin_ms", "gpu_won", "z3_won", "added_ms_per_miss_median",
+                                             "added_ms_per_miss_max", "gpu_won_wall_ms_median")}
 
     # CPU baseline: the C restatement over a bounded sample of the same candidates
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and inproc == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(P, blob, args, eng, prog, gh, jit)
 
     if rank == 0:
-        total = world * C * args.steps
+        total = world * inproc * C * args.steps
         value = total / dt
         kernel_s = kernel_ms * 1e-3
         pmc = load_pmc(args.pmc_dir, args.workload, sha, C) if sha else None
@@ -273,7 +297,7 @@ def main():
             "metric": METRIC,
             "value": value,
             "unit": "candidate assignments/s",
-            "n_gpus": world,
+            "n_gpus": world * inproc,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
@@ -290,7 +314,7 @@ def main():
                 "engine": args.engine,
                 "jit_source_sha16": sha,
                 "jit_compile_ms_cold": compile_ms,
-                "parallelism": f"shard{world}",
+                "parallelism": f"inproc{inproc}" if inproc > 1 else f"shard{world}",
             },
             "roofline": roofline,
             "algorithmic": algorithmic,

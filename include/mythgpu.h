@@ -35,8 +35,11 @@
  * failure (no C++ exception crosses the ABI). Host buffers are caller-owned.
  * Functions with the `_dev` suffix take device pointers already resident in HBM
  * (used by the benchmark so that the timed region excludes PCIe).
- * One process drives one GPU (one process per GPU; multi-GPU sharding and the
- * first-hit all-reduce are done by the caller over RCCL).
+ * Multi-GPU: mg_init's mask opens several GPUs in one process, and mg_search /
+ * mg_jit_search split a large call over them inside the shim (host min/sum of 16 bytes
+ * per device, no collective).  One process per GPU also works (mask = one bit): the
+ * caller then shards the index space and reduces the first hit itself (bench.py under
+ * torch.distributed.run: one all-reduce(MIN) over RCCL per epoch).
  */
 #ifndef MYTHGPU_H
 #define MYTHGPU_H
@@ -217,11 +220,12 @@ typedef struct mg_stats {
   uint32_t n_devices;  /* logical devices mg_init opened (the mask's GPUs) */
 } mg_stats_t;
 
-/* device_mask: every set bit d opens GPU d (0 = GPU 0).  With several, mg_search and
- * mg_jit_search split each call's index range over them (mg_split_range: contiguous,
- * group-aligned slices in index order), run the slices concurrently, one stream per
- * device, and reduce on the host (first hit = min, hits = sum); every other call runs on
- * the first device.  Programs, generators and JIT kernels are mirrored under the same
+/* device_mask: every set bit d opens GPU d (0 = GPU 0); all or nothing (a device that fails
+ * to open closes the others and mg_init returns the error).  With several, mg_search and
+ * mg_jit_search split a call of at least 2^20 candidates per device (MYTHGPU_SPLIT_MIN) over
+ * them (mg_split_range: contiguous, group-aligned slices in index order), run the slices
+ * concurrently, one stream per device, and reduce on the host (first hit = min, hits = sum);
+ * smaller, latency-bound calls and every other call run on the first device.  Programs, generators and JIT kernels are mirrored under the same
  * handles and uploaded to a device on first use there. */
 int mg_init(uint32_t device_mask);
 /* host-only: the slice of [start, start+count) device d of n_dev sweeps */
@@ -261,6 +265,12 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
               uint64_t* first_hit, uint64_t* n_hits, uint32_t* assign_out);
 
 /* ---- JIT specialisation (comgr; hipRTC fallback) -----------------------
+ * The compiler runs in a helper process (mythgpu_jitd, next to the library; started on the
+ * first compile, MYTHGPU_JIT_ISOLATE=0 compiles in-process): a compiler abort fails that
+ * compile with MG_E_UNSUPPORTED and turns the JIT off for the process; searches go on on
+ * the interpreter.  mg_jit_helper_pid: its pid, -1 before the first compile, -2 after it died. */
+int mg_jit_helper_pid(void);
+/*
  * mg_jit_compile turns a loaded program into straight-line gfx950 code: with a
  * generator handle, the search kernel (mg_jit_search) specialised on it; with
  * gen = 0, the eval kernel (mg_jit_eval*).  It emits straight-line code (values in VGPRs, literals as immediates,

@@ -15,6 +15,8 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 INCLUDE = PKG.parent / "include"
 LIB = PKG / "libmythgpu.so"
+JITD = PKG / "mythgpu_jitd"  # the JIT compiler process (csrc/jitd.cpp), next to the library
+JITD_SOURCES = [CSRC / "jitd.cpp", CSRC / "jit.cpp", CSRC / "program.cpp"]
 
 SOURCES = [CSRC / "engine.hip", CSRC / "program.cpp", CSRC / "jit.cpp"]
 HEADERS = [CSRC / "bv_device.h", CSRC / "keccak_device.h", CSRC / "gen_device.h", CSRC / "jit_device.h", CSRC / "program.hpp",
@@ -47,16 +49,38 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build libmythgpu.so)")
 
 
-def stale() -> bool:
-    if not LIB.exists():
+def _stale(out: Path, sources) -> bool:
+    if not out.exists():
         return True
-    t = LIB.stat().st_mtime
-    return any(p.stat().st_mtime > t for p in SOURCES + HEADERS + [PRELUDE_INC])
+    t = out.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in list(sources) + HEADERS + [PRELUDE_INC])
+
+
+def stale() -> bool:
+    return _stale(LIB, SOURCES) or _stale(JITD, JITD_SOURCES)
+
+
+def build_jitd(verbose: bool = False) -> Path:
+    """The compiler helper: host code only (comgr is dlopen'ed at run time), so plain g++."""
+    cxx = shutil.which("g++") or shutil.which("c++")
+    if cxx is None:
+        raise RuntimeError("g++ not found (needed for mythgpu_jitd)")
+    tmp = JITD.with_suffix(".tmp")
+    cmd = [cxx, "-O2", "-std=c++17", "-I/opt/rocm/include", "-o", str(tmp)] + [str(s) for s in JITD_SOURCES] + ["-ldl"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"g++ failed ({r.returncode}):\n{r.stderr[-4000:]}")
+    os.replace(tmp, JITD)
+    return JITD
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
     write_prelude()
-    if not force and not stale():
+    if force or _stale(JITD, JITD_SOURCES):
+        build_jitd(verbose)
+    if not force and not _stale(LIB, SOURCES):
         return LIB
     # -structurizecfg-skip-uniform-regions: the interpreter's opcode switch is wave-uniform (an
     # SGPR opcode), so its regions need no exec-mask structurisation; without the option every

@@ -1053,6 +1053,18 @@ namespace mg {
 // same handles and upload to their device on first use.  Guarded by E().mu.
 static std::vector<Engine*> g_devs;
 
+// a search is split over the devices only when every device gets at least this many candidates
+// (MYTHGPU_SPLIT_MIN overrides): below it the launch is latency-bound — one launch + one sync on
+// device 0, with the model capture, beats N launches + N syncs of a few groups each
+static uint64_t split_min_per_device() {
+  const char* s = getenv("MYTHGPU_SPLIT_MIN");
+  return s ? std::max<uint64_t>(64, strtoull(s, nullptr, 0)) : (uint64_t)1 << 20;
+}
+
+static bool split_over_devices(uint64_t count) {
+  return g_devs.size() > 1 && count / g_devs.size() >= split_min_per_device();
+}
+
 static int init_dev(Engine& e, int dev) {
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, dev));
@@ -1108,11 +1120,21 @@ int mg_init(uint32_t device_mask) {
   if (rc) return rc;
   g_devs.assign(1, &e);
   for (size_t i = 1; i < devs.size(); i++) {
-    Engine* s2 = new Engine;  // leaked with the process, like E()
+    Engine* s2 = new Engine;  // freed by mg_shutdown
     rc = init_dev(*s2, devs[i]);
     if (rc) {
-      (void)hipSetDevice(e.device);
-      return rc;
+      // all or nothing: a retry must not run on fewer devices than the mask asked for
+      const std::string why = g_err;
+      if (s2->init) free_dev_buffers(*s2);
+      delete s2;
+      for (size_t k = g_devs.size(); k-- > 0;) {
+        (void)hipSetDevice(g_devs[k]->device);
+        free_dev_buffers(*g_devs[k]);
+        if (g_devs[k] != &e) delete g_devs[k];
+      }
+      g_devs.clear();
+      e.init = false;
+      return set_err(rc, "mg_init: device " + std::to_string(devs[i]) + ": " + why);
     }
     g_devs.push_back(s2);
   }
@@ -1153,6 +1175,7 @@ void mg_shutdown(void) {
       if (kv.second->ready) (void)hipModuleUnload(kv.second->ready->mod);
     e.tickets.clear();
   }
+  jit_helper_stop();  // the compiler process ends on end of input (started again on demand)
   if (!e.init) {
     for (auto& kv : e.jits) (void)hipModuleUnload(kv.second->mod);
     e.jits.clear();
@@ -1576,7 +1599,7 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
   auto it = e.gens.find(gen);
   if (it == e.gens.end() || it->second->prog != prog) return set_err(MG_E_INVALID, "bad generator handle");
   unsigned long long res[2] = {~0ull, 0ull};
-  if (g_devs.size() > 1) {
+  if (split_over_devices(count)) {
     // the node's devices each sweep one contiguous, group-aligned slice (mg_split_range) on
     // their own stream; first hit = min, hits = sum over the slices (a host reduction: one
     // 16-byte read per device, no collective needed inside one process)
@@ -1865,6 +1888,8 @@ int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_bl
 
 int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle) { return mg_jit_compile_ex(prog, gen, 0, jit_handle); }
 
+int mg_jit_helper_pid(void) { return jit_helper_pid(); }
+
 int mg_cache_clear(void) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
@@ -2133,7 +2158,7 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
   if (!p || git == e.gens.end() || !j.fsearch) return set_err(MG_E_INVALID, "jit was not compiled for search");
   uint64_t sk = seed_lane_key(seed), sg = seed_group_key(seed);
   unsigned long long res[2] = {~0ull, 0ull};
-  if (g_devs.size() > 1) {  // as mg_search: one group-aligned slice per device, host min/sum
+  if (split_over_devices(count)) {  // as mg_search: one group-aligned slice per device, host min/sum
     const uint32_t nd = (uint32_t)g_devs.size();
     std::vector<uint64_t> st(nd), ct(nd);
     mg_split_range(start, count, nd, st.data(), ct.data());
@@ -2185,7 +2210,7 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
     int rc = arm_hits(e);
     if (!rc) rc = jit_launch_async(e, j.fsearch, j.nb_search, lanes, args, nblk);
     if (!rc) rc = fetch_hits(e);
-    if (!rc) rc = collect_hits(e, e.stats, lanes, res);
+    if (!rc) rc = collect_hits(e, e.stats, count, res);
     if (rc) return rc;
   }
   if (first_hit) *first_hit = res[0];

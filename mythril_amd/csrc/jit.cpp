@@ -6,12 +6,18 @@
 #include "jit.hpp"
 
 #include <dlfcn.h>
+#include <signal.h>
+#include <spawn.h>
+#include <sys/socket.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include <amd_comgr/amd_comgr.h>
 
 #include <chrono>
 #include <mutex>
 
+#include <cerrno>
 #include <cstdio>
 #include <map>
 #include <cstdlib>
@@ -925,14 +931,12 @@ const std::vector<std::string>& extra_options() {
       std::string t;
       while (is >> t) extra.push_back(t);
     }
-    // no exec-mask structurisation of wave-uniform regions (the MIXED alternatives and the
-    // early-exit jumps are SGPR branches), as the engine itself is built.  Measured on the
-    // search kernel: C1 -4 %, C2 -3 %, C3 -5 %, C4 -4 %, C5 +3 % time; every distinct kernel of
-    // the C1-C4 stream (123) compiles with it.  An LLVM fatal error
-    // seen once at process exit was the compile thread racing the runtime's teardown, fixed by
-    // stopping the engine from Python's atexit (native.py).  MYTHGPU_JIT_SKIP_UNIFORM=0: off
+    // MYTHGPU_JIT_SKIP_UNIFORM=1: no exec-mask structurisation of wave-uniform regions (the
+    // MIXED alternatives and the early-exit jumps are SGPR branches), as the engine itself is
+    // built.  A non-default LLVM option, so opt-in: round 2 measured C1 -4 %, C2 -3 %, C3 -5 %,
+    // C4 -4 %, C5 +3 % kernel time with it (profiles/r02_skip_uniform_sweep.jsonl).
     const char* u = getenv("MYTHGPU_JIT_SKIP_UNIFORM");
-    if (!u || u[0] != '0') {
+    if (u && u[0] == '1') {
       extra.push_back("-mllvm");
       extra.push_back("-structurizecfg-skip-uniform-regions");
     }
@@ -1054,13 +1058,208 @@ int hiprtc_compile(const std::string& src, std::vector<char>& code, std::string&
 }
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// The compiler in its own process (mythgpu_jitd, jitd.cpp).  comgr is LLVM: an internal error
+// is report_fatal_error -> abort(), which inside the caller would end the Mythril analysis with
+// no z3 fallback.  So by default the engine never loads comgr itself: every compile is one
+// request over a socketpair to a helper started with posix_spawn on first use.  If the helper
+// dies (LLVM abort, a signal), the compile that was in flight fails, the engine marks the JIT
+// unavailable and every later compile fails at once — searches stay on the interpreter (k_run)
+// for the rest of the process; there is no restart.  MYTHGPU_JIT_ISOLATE=0 compiles in-process.
+//
+// Protocol (host byte order, both directions on one SOCK_STREAM socket):
+//   request:  u64 env_len, env ("NAME=VALUE\0" for every AMD_COMGR_* / MYTHGPU_JIT* variable of
+//             the caller at this moment), u64 src_len, src
+//   response: i32 rc, u64 code_len, code, u64 log_len, log
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Helper {
+  std::mutex mu;
+  pid_t pid = -1;
+  int fd = -1;
+  bool dead = false;
+  std::string why;
+};
+
+Helper& helper() {
+  static Helper* h = new Helper;  // leaked: usable from exit handlers
+  return *h;
+}
+
+bool send_all(int fd, const void* p, size_t n) {
+  const char* c = (const char*)p;
+  while (n) {
+    ssize_t k = send(fd, c, n, MSG_NOSIGNAL);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return false;
+    c += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+bool recv_all(int fd, void* p, size_t n) {
+  char* c = (char*)p;
+  while (n) {
+    ssize_t k = recv(fd, c, n, 0);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return false;
+    c += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+std::string helper_path() {
+  if (const char* p = getenv("MYTHGPU_JITD")) return p;
+  Dl_info info;
+  if (dladdr((void*)&helper, &info) && info.dli_fname) {
+    std::string lib(info.dli_fname);
+    const size_t slash = lib.rfind('/');
+    return (slash == std::string::npos ? std::string(".") : lib.substr(0, slash)) + "/mythgpu_jitd";
+  }
+  return "mythgpu_jitd";
+}
+
+extern "C" char** environ;
+
+// caller holds h.mu
+bool helper_start(Helper& h) {
+  int sv[2];
+  if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0) {
+    h.why = "socketpair failed";
+    return false;
+  }
+  posix_spawn_file_actions_t fa;
+  posix_spawn_file_actions_init(&fa);
+  posix_spawn_file_actions_adddup2(&fa, sv[1], 0);  // dup2 clears CLOEXEC on the child's copy
+  posix_spawn_file_actions_adddup2(&fa, sv[1], 1);
+  const std::string path = helper_path();
+  char* argv[] = {(char*)path.c_str(), nullptr};
+  pid_t pid = -1;
+  const int rc = posix_spawn(&pid, path.c_str(), &fa, nullptr, argv, environ);
+  posix_spawn_file_actions_destroy(&fa);
+  close(sv[1]);
+  if (rc != 0) {
+    close(sv[0]);
+    h.why = "cannot start " + path + ": " + strerror(rc);
+    return false;
+  }
+  h.pid = pid;
+  h.fd = sv[0];
+  return true;
+}
+
+// caller holds h.mu: the helper is gone; record how, reap it, never start another
+void helper_lost(Helper& h) {
+  int status = 0;
+  std::string how = "JIT compiler process " + std::to_string(h.pid);
+  if (h.fd >= 0) close(h.fd);
+  h.fd = -1;
+  if (h.pid > 0 && waitpid(h.pid, &status, 0) == h.pid) {
+    if (WIFSIGNALED(status)) how += " killed by signal " + std::to_string(WTERMSIG(status));
+    else if (WIFEXITED(status)) how += " exited with status " + std::to_string(WEXITSTATUS(status));
+  } else {
+    how += " lost";
+  }
+  h.pid = -1;
+  h.dead = true;
+  h.why = how + "; the JIT is off for the rest of this process (searches stay on the interpreter)";
+  fprintf(stderr, "mythgpu: %s\n", h.why.c_str());
+}
+
+std::string env_snapshot() {
+  std::string env;
+  for (char** e = environ; e && *e; e++)
+    if (!std::strncmp(*e, "AMD_COMGR_", 10) || !std::strncmp(*e, "MYTHGPU_JIT", 11)) {
+      env += *e;
+      env.push_back('\0');
+    }
+  return env;
+}
+
+int helper_compile(const std::string& src, std::vector<char>& code, std::string& log, bool& available) {
+  Helper& h = helper();
+  std::lock_guard<std::mutex> g(h.mu);
+  available = true;
+  if (h.dead) {
+    log = h.why;
+    return MG_E_UNSUPPORTED;
+  }
+  if (h.fd < 0 && !helper_start(h)) {
+    available = false;  // no helper binary: the caller may compile in-process
+    return MG_E_UNSUPPORTED;
+  }
+  const std::string env = env_snapshot();
+  const uint64_t el = env.size(), sl = src.size();
+  int32_t rc = MG_E_HIP;
+  uint64_t cl = 0, ll = 0;
+  bool ok = send_all(h.fd, &el, 8) && send_all(h.fd, env.data(), el) && send_all(h.fd, &sl, 8) &&
+            send_all(h.fd, src.data(), sl) && recv_all(h.fd, &rc, 4) && recv_all(h.fd, &cl, 8);
+  if (ok) {
+    code.resize(cl);
+    ok = recv_all(h.fd, code.data(), cl) && recv_all(h.fd, &ll, 8);
+  }
+  if (ok) {
+    log.resize(ll);
+    ok = recv_all(h.fd, &log[0], ll);
+  }
+  if (!ok) {
+    helper_lost(h);
+    code.clear();
+    log = h.why;
+    return MG_E_UNSUPPORTED;
+  }
+  return rc;
+}
+
+}  // namespace
+
+void jit_helper_stop() {
+  Helper& h = helper();
+  std::lock_guard<std::mutex> g(h.mu);
+  if (h.fd >= 0) {
+    close(h.fd);  // the helper exits on end of input
+    h.fd = -1;
+  }
+  if (h.pid > 0) {
+    int status;
+    (void)waitpid(h.pid, &status, 0);
+    h.pid = -1;
+  }
+}
+
+int jit_helper_pid() {
+  Helper& h = helper();
+  std::lock_guard<std::mutex> g(h.mu);
+  return h.dead ? -2 : (int)h.pid;
+}
+
+static bool isolated() {
+  const char* v = getenv("MYTHGPU_JIT_ISOLATE");
+  return !(v && v[0] == '0');
+}
+
 void jit_compiler_preload() {
+  if (isolated()) return;  // the compiler lives in the helper process
   const char* which = getenv("MYTHGPU_JIT_COMPILER");
   if (!(which && std::strcmp(which, "hiprtc") == 0) && comgr().ok) return;
   (void)rtc();
 }
 
 int jit_compile(const std::string& src, std::vector<char>& code, std::string& log) {
+  if (isolated()) {
+    bool available = true;
+    const int rc = helper_compile(src, code, log, available);
+    if (available) return rc;
+    static std::once_flag warn;
+    std::call_once(warn, [&] { fprintf(stderr, "mythgpu: %s; compiling in-process\n", helper().why.c_str()); });
+  }
+  return jit_compile_local(src, code, log);
+}
+
+int jit_compile_local(const std::string& src, std::vector<char>& code, std::string& log) {
   const char* which = getenv("MYTHGPU_JIT_COMPILER");
   const bool use_rtc = which && std::strcmp(which, "hiprtc") == 0;
   int rc;

@@ -18,7 +18,14 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
 // register before anything the caller registers with atexit afterwards.
 void jit_compiler_preload();
 
-// hipRTC compile for gfx950 -> code object bytes. MG_OK or MG_E_*; `log` gets the compiler log.
+// compile for gfx950 -> code object bytes. MG_OK or MG_E_*; `log` gets the compiler log.  By
+// default through the compiler helper process (mythgpu_jitd): a compiler abort there fails the
+// compile, not the caller.  jit_compile_local: comgr (or hipRTC) in this process.
 int jit_compile(const std::string& src, std::vector<char>& code, std::string& log);
+int jit_compile_local(const std::string& src, std::vector<char>& code, std::string& log);
+
+// the helper process: stop it (end of input; it exits), and its pid (-1 none yet, -2 died)
+void jit_helper_stop();
+int jit_helper_pid();
 
 }  // namespace mg

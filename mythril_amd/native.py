@@ -34,7 +34,7 @@ EXPORTS = [
     "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_info", "mg_gen_free", "mg_eval", "mg_eval_dev",
     "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
     "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_jit_compile", "mg_jit_compile_ex", "mg_jit_verdicts", "mg_jit_info",
-    "mg_jit_compile_async", "mg_jit_poll", "mg_jit_cancel", "mg_cache_clear", "mg_split_range",
+    "mg_jit_compile_async", "mg_jit_poll", "mg_jit_cancel", "mg_jit_helper_pid", "mg_cache_clear", "mg_split_range",
     "mg_jit_free", "mg_jit_search", "mg_jit_eval", "mg_jit_eval_dev",
 ]
 
@@ -125,6 +125,7 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_jit_compile_async": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, u64p]),
             "mg_jit_poll": (C.c_int, [C.c_uint64, C.c_int32, u64p]),
             "mg_jit_cancel": (C.c_int, [C.c_uint64]),
+            "mg_jit_helper_pid": (C.c_int, []),
             "mg_cache_clear": (C.c_int, []),
             "mg_split_range": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, u64p, u64p]),
             "mg_jit_free": (C.c_int, [C.c_uint64]),
@@ -143,6 +144,11 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
         # compiler, or HIP work, racing the runtime's teardown can crash the process at exit
         atexit.register(_shutdown_at_exit)
         return lib
+
+
+def jit_helper_pid() -> int:
+    """pid of the compiler helper process (-1: not started yet, -2: it died; JIT off)."""
+    return int(load_library().mg_jit_helper_pid())
 
 
 def _check(rc: int):

@@ -204,6 +204,32 @@ class Z3Race:
             pass
 
 
+def race(gpu_job, z3_job, confirm):
+    """First answer of two workers: ``gpu_job(cancel)`` on the GPU thread and ``z3_job.run()``
+    on a z3 thread.  A GPU result that ``confirm`` turns into a model wins (``z3_job`` is then
+    interrupted): ``("gpu", model)``.  Otherwise z3's answer is awaited: ``("z3", z3_job.run()'s
+    value)``; a z3 exception propagates.  ``cancel`` is set on every exit, so a GPU search still
+    running stops at its next launch boundary.  GPU-side exceptions are counted, never raised."""
+    cancel = threading.Event()
+    f_z3 = _Z3_POOL.submit(z3_job.run)
+    f_gpu = _GPU_POOL.submit(gpu_job, cancel)
+    try:
+        done, _ = wait([f_z3, f_gpu], return_when=FIRST_COMPLETED)
+        if f_z3 not in done:
+            res = None
+            try:
+                res = f_gpu.result()
+            except Exception as e:
+                _count_error(e)
+            model = confirm(res)
+            if model is not None:
+                z3_job.interrupt()
+                return "gpu", model
+        return "z3", f_z3.result()
+    finally:
+        cancel.set()
+
+
 def _unsat_error():
     from mythril.exceptions import UnsatError  # type: ignore
 
@@ -316,32 +342,19 @@ def _race(original, constraints, enforce_execution_time):
         return original(constraints, (), (), enforce_execution_time)
     z3 = z3bridge.z3
     try:
-        race = Z3Race(z3, cs, total)
+        zr = Z3Race(z3, cs, total)
     except Exception as e:  # translation refused: the reference's path, unchanged
         log.debug("mythgpu: cannot race z3 on this query: %s", e)
         STATS.fallbacks += 1
         return original(constraints, (), (), enforce_execution_time)
-    cancel = threading.Event()
-    f_z3 = _Z3_POOL.submit(race.run)
-    f_gpu = _GPU_POOL.submit(_gpu_search, terms, gpu_ms / 1000.0, cancel)
     STATS.races += 1
-    try:
-        done, _ = wait([f_z3, f_gpu], return_when=FIRST_COMPLETED)
-        if f_z3 not in done:
-            res = None
-            try:
-                res = f_gpu.result()
-            except Exception as e:
-                _count_error(e)
-            model = _confirm(cs, res, total - (time.perf_counter() - t0) * 1e3)
-            if model is not None:
-                race.interrupt()
-                STATS.gpu_models += 1
-                _record(time.perf_counter() - t0, True)
-                return Model([model])
-        r = f_z3.result()  # z3's own answer (an exception in z3 propagates, as in the reference)
-    finally:
-        cancel.set()
+    winner, out = race(lambda cancel: _gpu_search(terms, gpu_ms / 1000.0, cancel), zr,
+                       lambda res: _confirm(cs, res, total - (time.perf_counter() - t0) * 1e3))
+    if winner == "gpu":
+        STATS.gpu_models += 1
+        _record(time.perf_counter() - t0, True)
+        return Model([out])
+    r = out
     STATS.z3_answers += 1
     dt = time.perf_counter() - t0
     STATS.race_z3_time += r.seconds

@@ -52,18 +52,58 @@ def test_full_mask_and_virtual_devices_same_hits(engine):
         for name, P, blob in cases:
             for jit in (False, True):
                 assert _run(engine, P, blob, windows, jit) == single[(name, jit)], (name, jit, "full mask")
-        # four logical devices on it: four slices per call, host min / sum
+        # four logical devices on it: four slices per call, host min / sum — with the default
+        # split threshold (only launches of >= 2^20 candidates per device are split) and with
+        # every launch split (MYTHGPU_SPLIT_MIN=64)
         os.environ["MYTHGPU_VIRTUAL_DEVICES"] = "4"
         engine.reinit(1 << engine.device)
         assert engine.n_devices == 4
-        for name, P, blob in cases:
-            for jit in (False, True):
-                assert _run(engine, P, blob, windows, jit) == single[(name, jit)], (name, jit, "4 devices")
+        for split_min in (None, "64"):
+            if split_min:
+                os.environ["MYTHGPU_SPLIT_MIN"] = split_min
+            for name, P, blob in cases:
+                for jit in (False, True):
+                    assert _run(engine, P, blob, windows, jit) == single[(name, jit)], (name, jit, "4 devices",
+                                                                                          split_min)
+            os.environ.pop("MYTHGPU_SPLIT_MIN", None)
         # the search loop and the model read-back on top of it
         roots = [c.raw for c in workloads.WORKLOADS["token_transfer_underflow"]()]
         r = search.search(engine, roots, timeout_s=10, jit="never")
         assert r.index is not None and r.model[0] == 1
     finally:
         os.environ.pop("MYTHGPU_VIRTUAL_DEVICES", None)
+        os.environ.pop("MYTHGPU_SPLIT_MIN", None)
         engine.reinit(old_mask)
     assert engine.n_devices == 1
+
+
+def _ttfm(engine, roots, reps=9):
+    import statistics
+    import time
+
+    search.search(engine, roots, timeout_s=10)  # warm: caches, capture buffers, code
+    out, idx = [], set()
+    for _ in range(reps):
+        t = time.perf_counter()
+        r = search.search(engine, roots, timeout_s=10)
+        out.append(time.perf_counter() - t)
+        idx.add(r.index)
+    return statistics.median(out), idx
+
+
+def test_time_to_first_model_at_four_devices(engine):
+    """An easy query's first launch (2^12 candidates) stays on device 0 with the model capture at
+    N > 1, so time to first model does not regress with the device count (C2 within 10 %, same hit)."""
+    roots = [c.raw for c in workloads.WORKLOADS["token_transfer_underflow"]()]
+    t1, i1 = _ttfm(engine, roots)
+    old_mask = engine.mask
+    try:
+        os.environ["MYTHGPU_VIRTUAL_DEVICES"] = "4"
+        engine.reinit(1 << engine.device)
+        assert engine.n_devices == 4
+        t4, i4 = _ttfm(engine, roots)
+    finally:
+        os.environ.pop("MYTHGPU_VIRTUAL_DEVICES", None)
+        engine.reinit(old_mask)
+    assert i1 == i4 and len(i1) == 1
+    assert t4 <= 1.10 * t1 + 50e-6, (t1, t4)

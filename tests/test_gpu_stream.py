@@ -67,3 +67,19 @@ def test_laser_stream_reaches_jit_within_budget(engine):
         assert r["engines"].get("jit", 0) >= 1, r
         assert r["budget_bound_rate"] >= 1e9, r
     assert summary["budget_bound_rate"] >= 1e9
+
+
+def test_race_miss_adds_little_over_z3(engine):
+    """The hook's race core (``plugin.race``) with the real GPU search against a z3 stand-in that
+    answers unsat after 40 ms: a GPU miss costs the hand-off and the cancel latency (one launch of
+    at most ``RACE_LAUNCH_S``), not the 200 ms slice; satisfiable queries are won by the GPU."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "tools"))
+    import stream_bench
+
+    rows = stream_bench.run_race(["token_transfer_underflow", "walletlibrary_kill"], 200.0, 40.0)
+    for r in rows:
+        assert r["z3_won"] >= 1 and r["gpu_won"] >= 1, r  # the hard sibling misses; the path itself hits
+        assert r["added_ms_per_miss_median"] <= 5.0, r

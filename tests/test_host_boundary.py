@@ -210,3 +210,20 @@ def test_split_range_chunk_to_device(lib, start, count, n):
         assert max(sizes) - min(sizes) <= 2
     with pytest.raises(native.EngineError):
         native.split_range(0, 10, 0)
+
+
+def test_bench_gpus_without_launcher_needs_the_devices():
+    """``bench.py --gpus N`` with no torch.distributed launcher opens N devices in one process
+    (the product's in-shim split); with fewer GPUs visible it exits 2 before touching a GPU."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    env = {k: v for k, v in __import__("os").environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "--gpus 2 but only 0 GPU(s) visible" in r.stderr
+    assert r.stdout == ""

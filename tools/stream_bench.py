@@ -15,11 +15,20 @@ JIT compile and the model read-back are all inside the measured time.
 Prints one JSON line per workload and a summary:
   budget_bound_rate   candidates / second over the queries that ran out of budget
   stream_rate         candidates / second over the whole stream
-usage: python tools/stream_bench.py [--budget-ms 200] [--workloads a,b]
+
+``--race-z3-ms D`` instead runs every query through the hook's race core (``plugin.race``, the
+same code ``get_model`` runs inside Mythril) against a z3 stand-in that "solves" for D ms on its
+worker thread and then answers unsat (there is no z3 on the box).  The GPU side is the real
+search (``search_partitioned`` with the race's cancel event and launch cap).  Reported: for the
+queries the stand-in answered (GPU misses), the hook's wall time beyond z3's own — the latency a
+miss adds — and for the queries the GPU won, their wall time.
+usage: python tools/stream_bench.py [--budget-ms 200] [--workloads a,b] [--race-z3-ms 50]
 """
 import argparse
 import json
+import statistics
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -47,6 +56,57 @@ def stream_queries(name):
     needle = Extract(63, 0, BitVec(v) * k) == symbol_factory.BitVecVal(0x0123456789ABCDEF, 64)
     out.append(("hard", tuple(cs) + (needle,)))
     return out
+
+
+class StandInZ3:
+    """The z3 side of the race on a box without z3: D ms of interruptible "solving", then unsat."""
+
+    def __init__(self, delay_s: float):
+        self.delay_s = delay_s
+        self.stop = threading.Event()
+        self.result = None
+        self.seconds = 0.0
+
+    def run(self):
+        t0 = time.perf_counter()
+        self.result = "unknown" if self.stop.wait(self.delay_s) else "unsat"
+        self.seconds = time.perf_counter() - t0
+        return self
+
+    def interrupt(self):
+        self.stop.set()
+
+
+def run_race(names, budget_ms, z3_ms, quiet=False):
+    """Every stream query through ``plugin.race`` (GPU search vs the z3 stand-in)."""
+    from mythril_amd import native, plugin
+
+    eng = native.Engine.get()
+    rows = []
+    for name in names:
+        added, gpu_wall = [], []
+        for label, q in stream_queries(name):
+            roots = [c.raw for c in q]
+            z3j = StandInZ3(z3_ms / 1e3)
+            t = time.perf_counter()
+            winner, out = plugin.race(
+                lambda cancel: search.search_partitioned(eng, roots, timeout_s=budget_ms / 1e3,
+                                                         max_candidates=1 << 40, cancel=cancel,
+                                                         max_launch_s=plugin.RACE_LAUNCH_S),
+                z3j, lambda res: res if res is not None and res.index is not None else None)
+            dt = time.perf_counter() - t
+            if winner == "gpu":
+                gpu_wall.append(dt * 1e3)
+            else:
+                added.append((dt - out.seconds) * 1e3)
+        row = {"workload": name, "race_z3_standin_ms": z3_ms, "gpu_won": len(gpu_wall), "z3_won": len(added),
+               "added_ms_per_miss_median": round(statistics.median(added), 3) if added else None,
+               "added_ms_per_miss_max": round(max(added), 3) if added else None,
+               "gpu_won_wall_ms_median": round(statistics.median(gpu_wall), 3) if gpu_wall else None}
+        rows.append(row)
+        if not quiet:
+            print(json.dumps(row), flush=True)
+    return rows
 
 
 def run(names, budget_ms, verbose=False, quiet=False):
@@ -108,8 +168,13 @@ def main():
     ap.add_argument("--budget-ms", type=float, default=200.0)
     ap.add_argument("--workloads", default=",".join(SHAPES))
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--race-z3-ms", type=float, default=None)
     a = ap.parse_args()
-    run([w for w in a.workloads.split(",") if w], a.budget_ms, a.verbose)
+    names = [w for w in a.workloads.split(",") if w]
+    if a.race_z3_ms is not None:
+        run_race(names, a.budget_ms, a.race_z3_ms)
+    else:
+        run(names, a.budget_ms, a.verbose)
 
 
 if __name__ == "__main__":
