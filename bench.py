@@ -34,10 +34,13 @@ import sys
 import time
 from pathlib import Path
 
+import numpy as np
+
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.6 T int32 lane-ops/s
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 METRIC = "candidate assignments evaluated/sec (node) + time-to-first-model vs z3"
 # workload -> the BASELINE.json config it stands for
 CONFIG_OF = {
@@ -65,6 +68,11 @@ def parse():
     ap.add_argument("--no-stream", action="store_true", help="skip the LASER-shaped get_model stream")
     ap.add_argument("--no-ttfm", action="store_true",
                     help="skip the time-to-first-model searches (profiling passes: full launches only)")
+    ap.add_argument("--no-eval", action="store_true", help="skip the eval-kernel roofline (roofline_eval)")
+    ap.add_argument("--eval-candidates", type=int, default=1 << 22,
+                    help="candidates per eval launch (HBM-resident SoA; C2: 1,241 B each)")
+    ap.add_argument("--eval-only", action="store_true",
+                    help="profiling pass: only the eval-kernel launches (tools/profile.sh eval)")
     ap.add_argument("--engine", choices=["jit", "interp"], default="jit",
                     help="jit: hipRTC-specialised search kernel; interp: the generic interpreter kernel")
     ap.add_argument("--pmc-dir", default=str(ROOT / "profiles"),
@@ -222,6 +230,28 @@ def main():
         ttfm_breakdown["engine"] = res.engine
         ttfm_breakdown["warm_runs"] = len(runs)
 
+    # time to first model of a query that needs a search: the workload plus a ~2^-24 needle on one of
+    # its own 256-bit symbols (Extract(23, 0, v * K) == C), through the product path search.search
+    # (interpreter first, async JIT compile, compiled kernel); "cold" compiles the kernel inside the
+    # timing, "warm" finds it in the code cache (the same query asked again)
+    hard = None
+    if rank == 0 and not args.no_ttfm:
+        hroots = hard_query(cs)
+        search.FLATTEN_CACHE = ssa.FlattenCache(aux_words=True)
+        search._GEN_CACHE.clear()
+        eng.cache_clear()
+        hard = {}
+        for label in ("cold", "warm"):
+            t1 = time.perf_counter()
+            rh = search.search(eng, hroots, seed=args.seed, max_candidates=1 << 40, timeout_s=60)
+            hard[f"{label}_ms"] = (time.perf_counter() - t1) * 1e3
+            hard[f"{label}_engine"] = rh.engine
+            hard["index"] = rh.index
+            hard["candidates"] = rh.scanned
+            if label == "cold":
+                hard["jit_compile_ms"] = rh.timing.get("jit_compile_ms")
+        hard["needle"] = "Extract(23, 0, v * K) == C on the workload's first 256-bit symbol (~2^-24 per candidate)"
+
     # time to first model on ALL ranks: the compiled kernel sweeps epochs of `chunk` candidates per
     # rank from index 0, one all-reduce(MIN) per epoch (distributed.sharded_first_hit); the index found
     # is the global lowest, identical at every GPU count
@@ -267,6 +297,11 @@ def main():
         rr = stream_bench.run_race([args.workload], 200.0, 50.0, quiet=True)[0]
         stream["race"] = {k: rr[k] for k in ("race_z3_standin_ms", "gpu_won", "z3_won", "added_ms_per_miss_median",
                                              "added_ms_per_miss_max", "gpu_won_wall_ms_median")}
+
+    # the eval kernel's own roofline (unspecialised C2 and C4 programs on HBM-resident SoA inputs)
+    evals = None
+    if rank == 0 and world == 1 and inproc == 1 and not args.no_eval:
+        evals = [eval_roofline(eng, torch, w, args.eval_candidates, args.pmc_dir) for w in EVAL_WORKLOADS]
 
     # CPU baseline: the C restatement over a bounded sample of the same candidates
     cpu = None
@@ -317,6 +352,7 @@ def main():
                 "parallelism": f"inproc{inproc}" if inproc > 1 else f"shard{world}",
             },
             "roofline": roofline,
+            "roofline_eval": evals,
             "algorithmic": algorithmic,
             "cpu_baseline": cpu,
             "time_to_first_model_ms": ttfm_ms,
@@ -325,7 +361,10 @@ def main():
             "time_to_first_model_breakdown": ttfm_breakdown,
             "time_to_first_model_sharded_ms": ttfm_sharded_ms,
             "first_model_index": ttfm_index,
+            "time_to_first_model_hard_ms": None if hard is None else hard["cold_ms"],
+            "time_to_first_model_hard": hard,
             "hits_in_timed_region": int(total_hits),
+            "hit_rate_in_timed_region": total_hits / total,
             "dropin_stream": stream,
         }
         os.write(out_fd, (json.dumps(out) + "\n").encode())
@@ -335,6 +374,79 @@ def main():
     eng.free(prog)
     if distributed:
         dist.destroy_process_group()
+
+
+EVAL_WORKLOADS = ("token_transfer_underflow", "walletlibrary_kill")
+
+
+def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5):
+    """``Model.eval`` batched (``laser/smt/model.py:45-59``): the compiled eval kernel
+    (``mg_jit_eval_dev``) of the UNSPECIALISED program — no generator, no value ranges, every
+    instruction evaluated — over n candidates whose coordinates are already in HBM as a
+    ``[coord limb row][candidate]`` uint32 SoA (uniform random, masked to each coordinate's
+    width), one verdict byte out per candidate.  Algorithmic bytes per candidate:
+    4 x coord_words in + 1 out."""
+    from mythril_amd import native, search, ssa, workloads
+
+    cs = workloads.WORKLOADS[workload]()
+    P, _ = search.prepare([c.raw for c in cs])
+    blob = P.to_bytes()
+    prog = eng.load(blob)
+    info = eng.info(prog)
+    jh = eng.jit_compile(prog, 0)
+    try:
+        cw = int(info.coord_words)
+        mask = np.zeros(cw, dtype=np.int64)
+        offs = P.coord_row_offsets()
+        for c in P.coords:
+            for j in range(ssa.limbs(c.width)):
+                bits = min(32, c.width - 32 * j)
+                mask[offs[c.index] + j] = (1 << bits) - 1
+        soa = torch.randint(-(1 << 31), (1 << 31) - 1, (cw, n), dtype=torch.int32, device="cuda")
+        soa &= torch.from_numpy(mask.astype(np.uint32).view(np.int32)).to("cuda")[:, None]
+        ver = torch.empty(n, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        eng.jit_eval_dev(jh, soa.data_ptr(), n, ver.data_ptr())  # warm-up (module load, caches)
+        eng.reset_stats()
+        for _ in range(reps):
+            eng.jit_eval_dev(jh, soa.data_ptr(), n, ver.data_ptr())
+        st = eng.stats()
+        kernel_ms = st.kernel_ms_total / max(st.launches, 1)
+        sat = int(ver.sum().item())
+        sha = hashlib.sha256(native.jit_source(blob).encode()).hexdigest()[:16]
+    finally:
+        eng.jit_free(jh)
+        eng.free(prog)
+    del soa, ver
+    bpc = 4 * cw + 1
+    gbs = n * bpc / (kernel_ms * 1e-3) / 1e9
+    out = {"workload": CONFIG_OF[workload], "kernel": "mgj_eval (unspecialised program)", "candidates_per_launch": n,
+           "program_instrs": int(info.n_instrs), "coord_words": cw, "bytes_per_candidate": bpc,
+           "kernel_ms": kernel_ms, "candidates_per_s": n / (kernel_ms * 1e-3),
+           "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS},
+           "valu": None, "traffic": None, "sat_fraction": sat / n, "jit_source_sha16": sha}
+    pmc = load_pmc(pmc_dir, "eval_" + workload, sha, n)
+    if pmc is not None:
+        n_instr = pmc["derived"]["valu_wave_instructions_per_candidate"]
+        achieved = n_instr * n / (kernel_ms * 1e-3) / 1e12
+        out["valu"] = {"achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "TOP/s (int32 lane-ops)",
+                       "frac": achieved / VALU_PEAK_TOPS, "valu_instructions_per_candidate": n_instr,
+                       "basis": pmc["_file"]}
+        out["traffic"] = pmc["derived"].get("hbm_bytes_per_launch")
+    out["bound"] = "hbm" if out["valu"] is None or out["hbm"]["frac"] >= out["valu"]["frac"] else "valu"
+    return out
+
+
+def hard_query(cs):
+    """The workload's constraints plus a ~2^-24 needle on its first 256-bit symbol."""
+    from mythril_amd.smt import BitVec, Extract, symbol_factory
+    from mythril_amd.smt import terms as T
+
+    roots = [c.raw for c in cs]
+    v = next(t for t in T.postorder(roots) if t.op == "bvvar" and t.width == 256)
+    k = symbol_factory.BitVecVal(0x9E3779B97F4A7C15F39CC0605CEDC835, 256)
+    needle = Extract(23, 0, BitVec(v) * k) == symbol_factory.BitVecVal(0xA5C3E1, 24)
+    return roots + [needle.raw]
 
 
 def cpu_baseline(P, blob, args, eng, prog, gh, jit=None):

@@ -403,3 +403,7 @@ class Engine:
 
     def eval_dev(self, prog: int, d_soa: int, n: int, d_ver: int, d_watch: int = 0):
         _check(self.lib.mg_eval_dev(prog, d_soa, n, d_ver, d_watch or None))
+
+    def jit_eval_dev(self, jit: int, d_soa: int, n: int, d_ver: int, d_watch: int = 0):
+        """The compiled eval kernel on HBM-resident SoA inputs (device pointers)."""
+        _check(self.lib.mg_jit_eval_dev(jit, d_soa, n, d_ver, d_watch or None))

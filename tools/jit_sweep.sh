@@ -6,7 +6,7 @@ O=gpurun_out/sweep_$W.jsonl
 mkdir -p gpurun_out; : > $O
 run() {  # label, env...
   local label=$1; shift
-  env "$@" AMD_COMGR_CACHE=0 timeout -k 10 120 python bench.py --workload $W --no-cpu-baseline --no-ttfm --no-stream --steps 20 > /tmp/sw.json 2>/tmp/sw.err || { echo "{\"label\": \"$label\", \"error\": true}" >> $O; return 0; }
+  env "$@" AMD_COMGR_CACHE=0 timeout -k 10 120 python bench.py --workload $W --no-cpu-baseline --no-ttfm --no-stream --no-eval --steps 20 > /tmp/sw.json 2>/tmp/sw.err || { echo "{\"label\": \"$label\", \"error\": true}" >> $O; return 0; }
   python3 -c "import json,sys; d=json.load(open('/tmp/sw.json')); print(json.dumps({'label': sys.argv[1], 'value': d['value'], 'kernel_ms': d['roofline']['kernel_ms'], 'compile_ms': d['config']['jit_compile_ms_cold']}))" "$label" >> $O
 }
 if [ $# -eq 0 ]; then
