@@ -931,12 +931,17 @@ const std::vector<std::string>& extra_options() {
       std::string t;
       while (is >> t) extra.push_back(t);
     }
-    // MYTHGPU_JIT_SKIP_UNIFORM=1: no exec-mask structurisation of wave-uniform regions (the
-    // MIXED alternatives and the early-exit jumps are SGPR branches), as the engine itself is
-    // built.  A non-default LLVM option, so opt-in: round 2 measured C1 -4 %, C2 -3 %, C3 -5 %,
-    // C4 -4 %, C5 +3 % kernel time with it (profiles/r02_skip_uniform_sweep.jsonl).
+    // -structurizecfg-skip-uniform-regions: no exec-mask structurisation of wave-uniform
+    // regions (the MIXED alternatives and the early-exit jumps are SGPR branches), as the
+    // engine itself is built.  A non-default LLVM option: on by default only while the
+    // compiler runs in its own process (a compiler abort then costs one kernel, not the
+    // caller; a wrong kernel is caught by z3's re-check of every GPU model).  Kernel time
+    // with it, this round (profiles/r03_skip_uniform_sweep.jsonl): C1 -1.2 %, C2 -3.1 %,
+    // C3 -4.7 %, C4 -5.4 %, C5 -1.2 %.  MYTHGPU_JIT_SKIP_UNIFORM=0 / =1 forces it off / on.
     const char* u = getenv("MYTHGPU_JIT_SKIP_UNIFORM");
-    if (u && u[0] == '1') {
+    const char* iso = getenv("MYTHGPU_JIT_ISOLATE");
+    const bool isolated = !(iso && iso[0] == '0');
+    if (u ? u[0] == '1' : isolated) {
       extra.push_back("-mllvm");
       extra.push_back("-structurizecfg-skip-uniform-regions");
     }

@@ -295,6 +295,7 @@ def read_rows(watch: np.ndarray, widths: Sequence[int], col: int) -> List[int]:
 def materialize(engine, P: ssa.Program, gen_blob: np.ndarray, seed: int, index: int):
     """Re-run candidate ``index`` with the model watch list; returns (verdict, scalars, arrays, funcs)."""
     entries, widths = model_watch(P)
+    prev = P.watch
     P.set_watch(entries)
     prog = engine.load(P.to_bytes())
     try:
@@ -305,7 +306,7 @@ def materialize(engine, P: ssa.Program, gen_blob: np.ndarray, seed: int, index: 
             engine.free_gen(gen)
     finally:
         engine.free(prog)
-        P.set_watch([])
+        P.set_watch(prev)
     vals = read_rows(watch, widths, 0) if watch is not None else []
     scal, keys, bases = {}, {}, {}
     it = iter(vals)
@@ -322,22 +323,27 @@ def prepare(roots: Sequence[T.Term], gen: Optional[GenBuilder] = None):
     """The program and generator blob a search runs: prefix-incremental flattening with
     AUX calldata words (``FLATTEN_CACHE``), the model watch list (``model_watch``: what
     ``mg_search``'s ``assign_out`` returns for the winning candidate) and the
-    propagation-shaped generator."""
+    propagation-shaped generator.
+
+    The whole result is a pure function of the (hash-consed) roots, and LASER re-asks the
+    same constraint set (``is_possible``, then the detection modules): a repeat returns the
+    SAME Program object (its serialised bytes and model read-back plan already built), so
+    callers must not mutate it."""
+    if gen is not None:
+        P = FLATTEN_CACHE.flatten(roots)
+        P.set_watch(model_watch(P)[0])
+        return P, gen.blob()
+    key = tuple(t.id for t in roots)
+    hit = _GEN_CACHE.get(key)
+    if hit is not None:
+        _GEN_CACHE[key] = _GEN_CACHE.pop(key)  # most recent last
+        return hit
     P = FLATTEN_CACHE.flatten(roots)
     P.set_watch(model_watch(P)[0])
-    if gen is not None:
-        return P, gen.blob()
-    # the propagation + generator pass is a pure function of the (hash-consed) roots:
-    # LASER re-asks the same constraint set (is_possible, then the detection modules)
-    key = tuple(t.id for t in roots)
-    blob = _GEN_CACHE.get(key)
-    if blob is None:
-        blob = default_generator(P, roots=roots).blob()
-        _GEN_CACHE[key] = blob
-        if len(_GEN_CACHE) > _GEN_CACHE_MAX:
-            _GEN_CACHE.pop(next(iter(_GEN_CACHE)))
-    else:
-        _GEN_CACHE[key] = _GEN_CACHE.pop(key)  # most recent last
+    blob = default_generator(P, roots=roots).blob()
+    _GEN_CACHE[key] = (P, blob)
+    if len(_GEN_CACHE) > _GEN_CACHE_MAX:
+        _GEN_CACHE.pop(next(iter(_GEN_CACHE)))
     return P, blob
 
 
@@ -345,23 +351,41 @@ _GEN_CACHE: "dict" = {}
 _GEN_CACHE_MAX = 512
 
 
+def _model_plan(P: ssa.Program):
+    """How ``model_from_assignment`` decodes P's model watch rows (built once per Program):
+    byte slices of the rows, scalar coordinate names and the site coordinates."""
+    plan = getattr(P, "_model_plan", None)
+    if plan is None:
+        _, widths = model_watch(P)
+        slices, r = [], 0
+        for w in widths:
+            L = ssa.limbs(w)
+            slices.append((4 * r, 4 * (r + L)))
+            r += L
+        scal = [(c.index, c.name) for c in P.scalar_coords()]
+        sites = [(c.index, c.name, c.kind == ssa.COORD_ARRAY_SITE) for c in P.sites]
+        plan = (slices, scal, sites)
+        P._model_plan = plan
+    return plan
+
+
 def model_from_assignment(P: ssa.Program, assign: np.ndarray):
-    """(scalars, arrays, funcs) from the watch rows ``mg_search`` wrote for a hit."""
-    entries, widths = model_watch(P)
+    """(scalars, arrays, funcs) from the watch rows ``mg_search`` wrote for a hit — the same
+    finite model ``ssa.model_from_sites`` builds (first site wins per key)."""
+    slices, scal, sites = _model_plan(P)
     raw = np.ascontiguousarray(assign, dtype="<u4").tobytes()
-    vals_l, r = [], 0
-    for w in widths:
-        L = ssa.limbs(w)
-        vals_l.append(int.from_bytes(raw[4 * r:4 * (r + L)], "little"))
-        r += L
-    vals = iter(vals_l)
-    scal, keys, bases = {}, {}, {}
-    for c in P.scalar_coords():
-        scal[c.index] = next(vals)
-    for c in P.sites:
-        keys[c.index] = next(vals)
-        bases[c.index] = next(vals)
-    return ssa.model_from_sites(P, scal, keys, bases)
+    fb = int.from_bytes
+    vals = [fb(raw[a:b], "little") for a, b in slices]
+    ns = len(scal)
+    scalars = {name: vals[i] for i, (_, name) in enumerate(scal)}
+    arrays: dict = {}
+    funcs: dict = {}
+    for j, (_, name, is_array) in enumerate(sites):
+        table = (arrays if is_array else funcs).setdefault(name, ({}, 0))[0]
+        k = vals[ns + 2 * j]
+        if k not in table:
+            table[k] = vals[ns + 2 * j + 1]
+    return scalars, arrays, funcs
 
 
 # expected latency of one query-kernel compile (submit -> loadable module), seconds: an

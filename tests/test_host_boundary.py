@@ -227,3 +227,29 @@ def test_bench_gpus_without_launcher_needs_the_devices():
     assert r.returncode == 2, r.stderr[-2000:]
     assert "--gpus 2 but only 0 GPU(s) visible" in r.stderr
     assert r.stdout == ""
+
+
+def test_model_from_assignment_matches_model_from_sites():
+    """The planned decode of mg_search's assign_out rows equals the generic path
+    (model_watch -> read_rows -> ssa.model_from_sites), duplicate site keys included."""
+    import numpy as np
+
+    from mythril_amd import search, workloads
+
+    rng = np.random.default_rng(5)
+    for name, fn in workloads.WORKLOADS.items():
+        P, _ = search.prepare([c.raw for c in fn()])
+        assert search.prepare([c.raw for c in fn()])[0] is P  # the prepared query is cached whole
+        for trial in range(3):
+            a = rng.integers(0, 2 ** 32, size=max(P.watch_words, 1), dtype=np.uint64).astype(np.uint32)
+            if trial == 2:
+                a[:] = rng.integers(0, 3, size=a.size)  # few distinct values: colliding site keys
+            _, widths = search.model_watch(P)
+            vals = iter(search.read_rows(a.reshape(-1, 1), widths, 0))
+            scal, keys, bases = {}, {}, {}
+            for c in P.scalar_coords():
+                scal[c.index] = next(vals)
+            for c in P.sites:
+                keys[c.index] = next(vals)
+                bases[c.index] = next(vals)
+            assert search.model_from_assignment(P, a) == ssa.model_from_sites(P, scal, keys, bases), name
