@@ -267,20 +267,79 @@ class SearchResult:
         self.timing = {}
 
 
-def model_watch(P: ssa.Program):
-    """Watch entries that read a whole model back: scalar VAR nodes, site keys and
-    site base values (0x80000000 | coord).  Returns (entries, widths)."""
+def _const_node_value(P: ssa.Program, node: int) -> Optional[int]:
+    """The value of a literal node (host-known), else None."""
+    t = P.node_term[node] if node < len(P.node_term) else None
+    return t.params[0] if t is not None and t.op == "bvconst" else None
+
+
+def _model_layout(P: ssa.Program):
+    """The model read-back layout (built once per Program, ``P._model_layout``).
+
+    A model is the scalar coordinates plus one (key, value) table entry per array/UF site
+    (``ssa.model_from_sites``).  What the host already knows is not read back from the GPU:
+    a site key that is a literal (``Select(<tx>_calldata, k)`` at a literal index, a literal
+    storage slot), and the value of a calldata site whose default is a byte of an AUX word
+    (``ssa.calldata_window``: read the word once, slice the bytes on the host).  So the watch
+    list is: scalar VAR nodes, AUX word VAR nodes, then per site its key node (unless literal)
+    and its base value (``0x80000000 | coord``, unless AUX-sliced).
+
+    Returns (entries, widths, plan); plan = (scalars [(entry position, name)], aux {coord:
+    position}, sites [(name, is_array, key position or None, literal key, base position or
+    None, (aux coord, bit offset, width) or None)])."""
+    lay = getattr(P, "_model_layout", None)
+    if lay is not None:
+        return lay
     entries, widths = [], []
-    for c in P.scalar_coords():
-        entries.append(c.node)
-        widths.append(c.width)
+
+    def add(e, w):
+        entries.append(e)
+        widths.append(w)
+        return len(entries) - 1
+
+    scal = [(add(c.node, c.width), c.name) for c in P.scalar_coords()]
+    aux_used = {a for a, _ in P.aux_slice.values()}
+    aux = {c.index: add(c.node, c.width) for c in P.coords if c.kind == ssa.COORD_AUX and c.index in aux_used}
+    sites = []
     for c in P.sites:
         k = P.site_key_node[c.index]
-        entries.append(k)
-        widths.append(P.node_width[k])
-        entries.append(0x80000000 | c.index)
-        widths.append(c.width)
+        lit = _const_node_value(P, k)
+        kpos = None if lit is not None else add(k, P.node_width[k])
+        sl = P.aux_slice.get(c.index)
+        if sl is not None:
+            bpos, slc = None, (sl[0], sl[1], c.width)
+        else:
+            bpos, slc = add(0x80000000 | c.index, c.width), None
+        sites.append((c.name, c.kind == ssa.COORD_ARRAY_SITE, kpos, lit, bpos, slc))
+    lay = (entries, widths, (scal, aux, sites))
+    P._model_layout = lay
+    return lay
+
+
+def model_watch(P: ssa.Program):
+    """Watch entries that read a whole model back (``_model_layout``): (entries, widths)."""
+    entries, widths, _ = _model_layout(P)
     return entries, widths
+
+
+def decode_model(P: ssa.Program, vals: Sequence[int]):
+    """(scalars, arrays, funcs) from the values of P's model watch entries, in order: the
+    finite z3 model of one candidate (first site wins per key, as ``ssa.model_from_sites``)."""
+    _, _, (scal, aux, sites) = _model_layout(P)
+    scalars = {name: vals[i] for i, name in scal}
+    arrays: dict = {}
+    funcs: dict = {}
+    for name, is_array, kpos, lit, bpos, slc in sites:
+        table = (arrays if is_array else funcs).setdefault(name, ({}, 0))[0]
+        k = lit if kpos is None else vals[kpos]
+        if k in table:
+            continue
+        if bpos is not None:
+            table[k] = vals[bpos]
+        else:
+            a, off, w = slc
+            table[k] = (vals[aux[a]] >> off) & ((1 << w) - 1)
+    return scalars, arrays, funcs
 
 
 def read_rows(watch: np.ndarray, widths: Sequence[int], col: int) -> List[int]:
@@ -308,14 +367,7 @@ def materialize(engine, P: ssa.Program, gen_blob: np.ndarray, seed: int, index: 
         engine.free(prog)
         P.set_watch(prev)
     vals = read_rows(watch, widths, 0) if watch is not None else []
-    scal, keys, bases = {}, {}, {}
-    it = iter(vals)
-    for c in P.scalar_coords():
-        scal[c.index] = next(it)
-    for c in P.sites:
-        keys[c.index] = next(it)
-        bases[c.index] = next(it)
-    scalars, arrays, funcs = ssa.model_from_sites(P, scal, keys, bases)
+    scalars, arrays, funcs = decode_model(P, vals)
     return int(ver[0]), scalars, arrays, funcs
 
 
@@ -352,40 +404,24 @@ _GEN_CACHE_MAX = 512
 
 
 def _model_plan(P: ssa.Program):
-    """How ``model_from_assignment`` decodes P's model watch rows (built once per Program):
-    byte slices of the rows, scalar coordinate names and the site coordinates."""
+    """Byte slices of P's model watch rows in an ``assign_out`` buffer (built once)."""
     plan = getattr(P, "_model_plan", None)
     if plan is None:
         _, widths = model_watch(P)
-        slices, r = [], 0
+        plan, r = [], 0
         for w in widths:
             L = ssa.limbs(w)
-            slices.append((4 * r, 4 * (r + L)))
+            plan.append((4 * r, 4 * (r + L)))
             r += L
-        scal = [(c.index, c.name) for c in P.scalar_coords()]
-        sites = [(c.index, c.name, c.kind == ssa.COORD_ARRAY_SITE) for c in P.sites]
-        plan = (slices, scal, sites)
         P._model_plan = plan
     return plan
 
 
 def model_from_assignment(P: ssa.Program, assign: np.ndarray):
-    """(scalars, arrays, funcs) from the watch rows ``mg_search`` wrote for a hit — the same
-    finite model ``ssa.model_from_sites`` builds (first site wins per key)."""
-    slices, scal, sites = _model_plan(P)
+    """(scalars, arrays, funcs) from the watch rows ``mg_search`` wrote for a hit."""
     raw = np.ascontiguousarray(assign, dtype="<u4").tobytes()
     fb = int.from_bytes
-    vals = [fb(raw[a:b], "little") for a, b in slices]
-    ns = len(scal)
-    scalars = {name: vals[i] for i, (_, name) in enumerate(scal)}
-    arrays: dict = {}
-    funcs: dict = {}
-    for j, (_, name, is_array) in enumerate(sites):
-        table = (arrays if is_array else funcs).setdefault(name, ({}, 0))[0]
-        k = vals[ns + 2 * j]
-        if k not in table:
-            table[k] = vals[ns + 2 * j + 1]
-    return scalars, arrays, funcs
+    return decode_model(P, [fb(raw[a:b], "little") for a, b in _model_plan(P)])
 
 
 # expected latency of one query-kernel compile (submit -> loadable module), seconds: an
@@ -563,6 +599,7 @@ def eval_with_models(engine, P: ssa.Program, assigns: Sequence[Sequence[int]]):
     """Batched eval of explicit assignments; also reads every candidate back as a
     finite model ``(scalars, arrays, funcs)`` (site canonicalisation applied)."""
     entries, widths = model_watch(P)
+    prev = P.watch
     P.set_watch(entries)
     soa = ssa.soa_from_assignments(P, assigns)
     prog = engine.load(P.to_bytes())
@@ -571,15 +608,6 @@ def eval_with_models(engine, P: ssa.Program, assigns: Sequence[Sequence[int]]):
         ver, watch = engine.eval(prog, soa, len(assigns), watch_words=ww)
     finally:
         engine.free(prog)
-        P.set_watch([])
-    models = []
-    for i in range(len(assigns)):
-        vals = iter(read_rows(watch, widths, i)) if watch is not None else iter(())
-        scal, keys, bases = {}, {}, {}
-        for c in P.scalar_coords():
-            scal[c.index] = next(vals)
-        for c in P.sites:
-            keys[c.index] = next(vals)
-            bases[c.index] = next(vals)
-        models.append(ssa.model_from_sites(P, scal, keys, bases))
+        P.set_watch(prev)
+    models = [decode_model(P, read_rows(watch, widths, i) if watch is not None else []) for i in range(len(assigns))]
     return ver, models

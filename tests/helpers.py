@@ -193,20 +193,13 @@ def gpu_eval_terms(engine, roots: Sequence[T.Term], watch_terms: Sequence[T.Term
             ver, watch = engine.eval(prog, soa, len(assigns), watch_words=info.watch_words)
     finally:
         engine.free(prog)
-    from mythril_amd.search import read_rows
+    from mythril_amd.search import decode_model, read_rows
 
     results, models = [], []
     for i in range(len(assigns)):
         vals = read_rows(watch, widths, i)
         tv = {t.id: vals[j] for j, t in enumerate(watch_terms)}
-        rest = iter(vals[len(watch_terms):])
-        scal, keys, bases = {}, {}, {}
-        for c in P.scalar_coords():
-            scal[c.index] = next(rest)
-        for c in P.sites:
-            keys[c.index] = next(rest)
-            bases[c.index] = next(rest)
-        s, a, f = ssa.model_from_sites(P, scal, keys, bases)
+        s, a, f = decode_model(P, vals[len(watch_terms):])
         results.append(tv)
         models.append(OracleModel(s, a, f))
     return P, assigns, ver, results, models

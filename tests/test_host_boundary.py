@@ -230,26 +230,55 @@ def test_bench_gpus_without_launcher_needs_the_devices():
 
 
 def test_model_from_assignment_matches_model_from_sites():
-    """The planned decode of mg_search's assign_out rows equals the generic path
-    (model_watch -> read_rows -> ssa.model_from_sites), duplicate site keys included."""
+    """The model read back from mg_search's assign_out rows (literal site keys and AUX-sliced
+    calldata bytes filled in on the host, ``search._model_layout``) equals the generic
+    ``ssa.model_from_sites`` of the full per-site key / base values, duplicate keys included
+    (random coordinate and key values; the watch rows are what the kernel writes for them)."""
+    import random
+
     import numpy as np
 
     from mythril_amd import search, workloads
 
-    rng = np.random.default_rng(5)
+    rng = random.Random(5)
     for name, fn in workloads.WORKLOADS.items():
-        P, _ = search.prepare([c.raw for c in fn()])
-        assert search.prepare([c.raw for c in fn()])[0] is P  # the prepared query is cached whole
+        roots = [c.raw for c in fn()]
+        P, _ = search.prepare(roots)
+        assert search.prepare(roots)[0] is P  # the prepared query is cached whole
+        entries, widths = search.model_watch(P)
+        n_sites_lit = sum(1 for c in P.sites if search._const_node_value(P, P.site_key_node[c.index]) is not None)
+        assert len(entries) == len(P.scalar_coords()) + len({a for a, _ in P.aux_slice.values()}) + \
+            2 * len(P.sites) - n_sites_lit - len(P.aux_slice), name
+        node_of = {c.node: c for c in P.coords if c.kind in (ssa.COORD_SCALAR, ssa.COORD_AUX)}
         for trial in range(3):
-            a = rng.integers(0, 2 ** 32, size=max(P.watch_words, 1), dtype=np.uint64).astype(np.uint32)
-            if trial == 2:
-                a[:] = rng.integers(0, 3, size=a.size)  # few distinct values: colliding site keys
-            _, widths = search.model_watch(P)
-            vals = iter(search.read_rows(a.reshape(-1, 1), widths, 0))
-            scal, keys, bases = {}, {}, {}
-            for c in P.scalar_coords():
-                scal[c.index] = next(vals)
+            draw = (lambda w: rng.randrange(3)) if trial == 2 else rng.getrandbits  # trial 2: colliding keys
+            vals_c = {c.index: draw(c.width) for c in P.coords}
+            # a key node's value (what the kernel computes for it): literal, or any value
+            key_val = {}
             for c in P.sites:
-                keys[c.index] = next(vals)
-                bases[c.index] = next(vals)
-            assert search.model_from_assignment(P, a) == ssa.model_from_sites(P, scal, keys, bases), name
+                k = P.site_key_node[c.index]
+                lit = search._const_node_value(P, k)
+                if k in node_of:
+                    key_val[k] = vals_c[node_of[k].index]
+                elif k not in key_val:
+                    key_val[k] = lit if lit is not None else draw(P.node_width[k])
+            keys = {c.index: key_val[P.site_key_node[c.index]] for c in P.sites}
+            bases = {}
+            for c in P.sites:
+                sl = P.aux_slice.get(c.index)
+                bases[c.index] = (vals_c[sl[0]] >> sl[1]) & 0xFF if sl else vals_c[c.index]
+            want = ssa.model_from_sites(P, {c.index: vals_c[c.index] for c in P.scalar_coords()}, keys, bases)
+            # the watch rows the kernel writes: one value per entry
+            row_vals = []
+            for e in entries:
+                if e & 0x80000000:
+                    row_vals.append(bases[e & 0x7FFFFFFF])
+                elif e in node_of:
+                    row_vals.append(vals_c[node_of[e].index])
+                else:
+                    row_vals.append(key_val[e])
+            assign = []
+            for v, w in zip(row_vals, widths):
+                assign += [(v >> (32 * j)) & 0xFFFFFFFF for j in range(ssa.limbs(w))]
+            got = search.model_from_assignment(P, np.array(assign or [0], dtype=np.uint32))
+            assert got == want, name
