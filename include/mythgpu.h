@@ -240,6 +240,18 @@ int mg_program_check(const uint8_t* ssa, size_t len, mg_program_info_t* info);
 int mg_program_check_gen(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words,
                          mg_program_info_t* info);
 
+/* host-only: the lowered program a search (gen_blob) or an eval (gen_blob = NULL) actually
+ * runs after specialisation, in SSA form, for inspection and for the oracle-side check that
+ * specialisation keeps every verdict (tests/test_specialize_cpu.py).  Layout (uint32 words):
+ * {MG_SPEC_MAGIC, n_instr, n_consts, n_aux, n_values, n_coords}, n_instr x 8-word
+ * instructions {op, width, dst, a, b, c, p0, p1} (operands are value ids; op codes are the
+ * device ops of mythril_amd/csrc/program.hpp), consts, aux (LOOKUP prior pairs), value
+ * widths.  buf = NULL: only *out_words. */
+#define MG_SPEC_MAGIC 0x43455053u /* "SPEC" */
+#define MG_SPEC_KEEP_WATCH 1u
+int mg_program_specialized(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words,
+                           uint32_t flags, uint32_t* buf, size_t cap_words, size_t* out_words);
+
 int mg_program_load(const uint8_t* ssa, size_t len, uint64_t* prog_handle);
 int mg_program_info(uint64_t prog, mg_program_info_t* info);
 int mg_program_free(uint64_t prog);

@@ -1275,6 +1275,33 @@ int mg_program_check_gen(const uint8_t* ssa, size_t len, const uint32_t* gen_blo
   return MG_OK;
 }
 
+int mg_program_specialized(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words,
+                           uint32_t flags, uint32_t* buf, size_t cap_words, size_t* out_words) {
+  Lowered base, sp;
+  std::string err;
+  int rc = lower_program(ssa, len, base, err);
+  if (rc) return set_err(rc, err);
+  std::vector<GenSpec> specs;
+  std::vector<uint32_t> consts;
+  if (gen_blob) {
+    rc = parse_gen(base, gen_blob, gen_words, specs, consts, err);
+    if (rc) return set_err(rc, err);
+  }
+  rc = specialize_program(base, gen_blob ? &specs : nullptr, gen_blob ? &consts : nullptr, sp, err,
+                          (flags & MG_SPEC_KEEP_WATCH) != 0);
+  if (rc) return set_err(rc, err);
+  std::vector<uint32_t> w = {MG_SPEC_MAGIC, (uint32_t)sp.vcode.size(), (uint32_t)sp.consts.size(),
+                             (uint32_t)sp.vaux.size(), (uint32_t)sp.vwidth.size(), sp.n_coords};
+  for (const Instr& in : sp.vcode) w.insert(w.end(), &in.op, &in.op + 8);
+  w.insert(w.end(), sp.consts.begin(), sp.consts.end());
+  w.insert(w.end(), sp.vaux.begin(), sp.vaux.end());
+  w.insert(w.end(), sp.vwidth.begin(), sp.vwidth.end());
+  if (out_words) *out_words = w.size();
+  if (buf == nullptr || cap_words < w.size()) return buf == nullptr ? MG_OK : set_err(MG_E_INVALID, "buffer too small");
+  std::memcpy(buf, w.data(), 4 * w.size());
+  return MG_OK;
+}
+
 int mg_program_load(const uint8_t* ssa, size_t len, uint64_t* handle) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);

@@ -194,7 +194,6 @@ struct Gen {
     const std::string C = std::to_string(c) + "u";
     auto lim = [&](uint32_t j) { return out + "_" + std::to_string(j); };
     const auto& G = *gconsts;
-    if (kind == MG_GEN_MIXED && sp.p[3] != MG_NONE && (sp.p[2] & 0xFFFFu)) gen_coord_value(sp.p[3]);
     o << "  {\n";
     switch (kind) {
       case MG_GEN_MIXED: {
@@ -233,40 +232,16 @@ struct Gen {
             o << " " << lim(j) << " = mg_addc(" << lim(j) << ", " << (j ? "ah" : "a0") << ", cy, &cy);";
           o << " (void)cy; (void)ah; }\n";
         };
-        bool first = true;
-        auto branch = [&](const std::string& cond) {
-          o << (first ? "  if (" : "  } else if (") << cond << ") {\n";
-          first = false;
-        };
-        if (pc) {
-          branch(below(pc));
-          const std::string src = coord_var.at(sp.p[3]);
-          for (uint32_t j = 0; j < L; j++) o << "    " << lim(j) << " = " << src << "_" << j << ";\n";
-          delta(false);
-        }
-        if (pd) {
-          branch(below(pc + pd));
-          o << "    " << hdecl << "\n";
-          o << "    const uint32_t e = ((h >> 16) * " << sp.p[1] << "u) >> 16;\n";
-          dict_limbs(sp.p[0], sp.p[1], width, "e", lim, "    ");
-          delta(true);
-        }
-        if (ps) {
-          branch(below(pc + pd + ps));
-          uni(small_bits);
-        }
-        if (first) {
-          uni(width);
-        } else {
-          o << "  } else {\n";
-          uni(width);
-          o << "  }\n";
-        }
-        if (width & 31) o << "  " << lim(L - 1) << " &= " << hex(topmask(width)) << ";\n";
-        if (sp.p[6]) {
+        // mask + clamp, emitted at the end of EACH branch: what a branch knows about its limbs
+        // (SMALL: the high limbs are zero; DICT: limbs equal in every entry are literals) folds
+        // the clamp test there
+        auto finish = [&]() {
+          if (width & 31) o << "    " << lim(L - 1) << " &= " << hex(topmask(width)) << ";\n";
+          if (!sp.p[6]) return;
           const uint32_t r = sp.p[6] - 1;
           const uint32_t span = G[r + L];
-          o << "  { uint32_t br = 0u, hz = 0u, t0;";
+          const uint32_t k = reach_limbs(&G[r], L, span ? span - 1u : 0xFFFFFFFFull, 0);
+          o << "    { uint32_t br = 0u, hz = 0u, t0;";
           for (uint32_t j = 0; j < L; j++) {
             if (j == 0) o << " t0 = mg_subc(" << lim(0) << ", " << hex(G[r]) << ", br, &br);";
             else o << " hz |= mg_subc(" << lim(j) << ", " << hex(G[r + j]) << ", br, &br);";
@@ -274,9 +249,55 @@ struct Gen {
           o << " if (br | hz" << (span ? " | (uint32_t)(t0 >= " + hex(span) + ")" : std::string("")) << ") {"
             << " const uint32_t off = " << (span ? "(uint32_t)(((uint64_t)" + lim(0) + " * " + std::to_string(span) + "ull) >> 32)" : lim(0))
             << "; uint32_t cy = 0u;";
-          for (uint32_t j = 0; j < L; j++)
-            o << " " << lim(j) << " = mg_addc(" << hex(G[r + j]) << ", " << (j ? "0u" : "off") << ", cy, &cy);";
+          for (uint32_t j = 0; j < L; j++) {
+            if (j < k) o << " " << lim(j) << " = mg_addc(" << hex(G[r + j]) << ", " << (j ? "0u" : "off") << ", cy, &cy);";
+            else o << " " << lim(j) << " = " << hex(G[r + j]) << ";";
+          }
           o << " (void)cy; } }\n";
+        };
+        bool first = true;
+        auto branch = [&](const std::string& cond) {
+          o << (first ? "  if (" : "  } else if (") << cond << ") {\n";
+          first = false;
+        };
+        if (pc) {
+          branch(below(pc));
+          std::string src;
+          auto cv = coord_var.find(sp.p[3]);
+          if (cv != coord_var.end()) {
+            src = cv->second;
+          } else {
+            // a copy source the program does not read before this point: generated only by the
+            // waves that take this branch, into temporaries scoped to it
+            const auto saved = coord_var;
+            src = gen_coord_value(sp.p[3]);
+            coord_var = saved;
+          }
+          for (uint32_t j = 0; j < L; j++) o << "    " << lim(j) << " = " << src << "_" << j << ";\n";
+          delta(false);
+          finish();
+        }
+        if (pd) {
+          branch(below(pc + pd));
+          o << "    " << hdecl << "\n";
+          o << "    const uint32_t e = ((h >> 16) * " << sp.p[1] << "u) >> 16;\n";
+          dict_limbs(sp.p[0], sp.p[1], width, "e", lim, "    ");
+          delta(true);
+          finish();
+        }
+        if (ps) {
+          branch(below(pc + pd + ps));
+          uni(small_bits);
+          finish();
+        }
+        if (first) {
+          uni(width);
+          finish();
+        } else {
+          o << "  } else {\n";
+          uni(width);
+          finish();
+          o << "  }\n";
         }
         break;
       }
@@ -289,9 +310,13 @@ struct Gen {
         o << "  const uint32_t r = grnd(ky, " << C << ", 0u); const uint32_t off = "
           << (sp.p[1] ? ("(uint32_t)(((uint64_t)r * " + std::to_string(sp.p[1]) + "ull) >> 32)") : std::string("r"))
           << "; uint32_t cy = 0u;\n";
-        for (uint32_t j = 0; j < L; j++)
-          o << "  " << lim(j) << " = mg_addc(" << hex(G[sp.p[0] + j]) << ", " << (j ? "0u" : "off")
-            << ", cy, &cy);\n";
+        const uint32_t k = reach_limbs(&G[sp.p[0]], L, sp.p[1] ? sp.p[1] - 1u : 0xFFFFFFFFull, 0);
+        for (uint32_t j = 0; j < L; j++) {
+          if (j < k)
+            o << "  " << lim(j) << " = mg_addc(" << hex(G[sp.p[0] + j]) << ", " << (j ? "0u" : "off") << ", cy, &cy);\n";
+          else
+            o << "  " << lim(j) << " = " << hex(G[sp.p[0] + j]) << ";\n";
+        }
         o << "  (void)cy;\n";
         break;
       }
@@ -300,13 +325,15 @@ struct Gen {
           << (sp.p[2] ? ("(((uint64_t)r * " + std::to_string(sp.p[2]) + "ull) >> 32)") : std::string("(uint64_t)r"))
           << "; uint32_t cy = 0u;\n";
         const int32_t sh = (int32_t)sp.p[1];
+        const uint32_t k = reach_limbs(&G[sp.p[0]], L, sp.p[2] ? sp.p[2] - 1u : 0xFFFFFFFFull, (uint32_t)sh);
         for (uint32_t j = 0; j < L; j++) {
           const int32_t bit0 = (int32_t)(j * 32) - sh;
           std::string mw;
           if (bit0 <= -32 || bit0 >= 64) mw = "0u";
           else if (bit0 < 0) mw = "(uint32_t)(m << " + std::to_string(-bit0) + ")";
           else mw = "(uint32_t)(m >> " + std::to_string(bit0) + ")";
-          o << "  " << lim(j) << " = mg_addc(" << hex(G[sp.p[0] + j]) << ", " << mw << ", cy, &cy);\n";
+          if (j < k) o << "  " << lim(j) << " = mg_addc(" << hex(G[sp.p[0] + j]) << ", " << mw << ", cy, &cy);\n";
+          else o << "  " << lim(j) << " = " << hex(G[sp.p[0] + j]) << ";\n";
         }
         o << "  (void)cy;\n";
         break;
@@ -342,6 +369,26 @@ struct Gen {
     return b;
   }
   static uint32_t topmask(uint32_t w) { return (w & 31) ? ((1u << (w & 31)) - 1u) : 0xFFFFFFFFu; }
+  // lo + x for every 0 <= x <= (maxadd << sh), over L limbs: the number k of low limbs that can
+  // differ from lo's.  lo <= lo + x <= lo + max and, when that does not wrap, lo and lo + max agree
+  // on every limb >= k, so lo + x does too: those limbs are literals and the carry chain stops at
+  // limb k - 1.  L when the sum can wrap.
+  static uint32_t reach_limbs(const uint32_t* lo, uint32_t L, uint64_t maxadd, uint32_t sh) {
+    std::vector<uint32_t> add(L + 3, 0u);
+    const uint32_t q = sh / 32, r = sh % 32;
+    const unsigned __int128 x = (unsigned __int128)maxadd << r;
+    for (uint32_t t = 0; t < 3 && q + t < L + 3; t++) add[q + t] = (uint32_t)(x >> (32 * t));
+    for (uint32_t j = L; j < L + 3; j++)
+      if (add[j]) return L;  // the addend alone reaches past the value
+    uint64_t cy = 0;
+    uint32_t k = 0;
+    for (uint32_t j = 0; j < L; j++) {
+      const uint64_t t = (uint64_t)lo[j] + add[j] + cy;
+      if ((uint32_t)t != lo[j]) k = j + 1;
+      cy = t >> 32;
+    }
+    return cy ? L : k;
+  }
 
   // Bits [p, p+need) of value `id` (width w) as an expression in the low bits, zero above
   // `need` (bits at or above a value's width are zero by invariant).  Looks through CONCAT /

@@ -690,101 +690,327 @@ namespace {
 
 inline uint32_t Lw(uint32_t w) { return (w + 31) / 32; }
 
+// 256-bit unsigned words for the analysis (values of width <= 256; wider values are unknown)
+struct U256 {
+  uint64_t w[4] = {0, 0, 0, 0};
+  static U256 of(uint64_t v) {
+    U256 r;
+    r.w[0] = v;
+    return r;
+  }
+  // limbs [0, L) of 32 bits; false if a limb at or above 256 bits is nonzero
+  static bool from_limbs(const uint32_t* x, uint32_t L, U256* out) {
+    U256 r;
+    for (uint32_t j = 0; j < L; j++) {
+      if (j >= 8) {
+        if (x[j]) return false;
+        continue;
+      }
+      r.w[j / 2] |= (uint64_t)x[j] << (32 * (j % 2));
+    }
+    *out = r;
+    return true;
+  }
+  static U256 ones(uint32_t w) {  // 2^w - 1, w <= 256
+    U256 r;
+    for (int i = 0; i < 4; i++) {
+      const int b = (int)w - 64 * i;
+      r.w[i] = b >= 64 ? ~0ull : b <= 0 ? 0ull : ((1ull << b) - 1ull);
+    }
+    return r;
+  }
+  bool zero() const { return !(w[0] | w[1] | w[2] | w[3]); }
+  bool operator==(const U256& o) const { return !std::memcmp(w, o.w, sizeof(w)); }
+  bool operator!=(const U256& o) const { return !(*this == o); }
+  bool operator<(const U256& o) const {
+    for (int i = 3; i >= 0; i--)
+      if (w[i] != o.w[i]) return w[i] < o.w[i];
+    return false;
+  }
+  bool operator<=(const U256& o) const { return !(o < *this); }
+  U256 operator&(const U256& o) const { U256 r; for (int i = 0; i < 4; i++) r.w[i] = w[i] & o.w[i]; return r; }
+  U256 operator|(const U256& o) const { U256 r; for (int i = 0; i < 4; i++) r.w[i] = w[i] | o.w[i]; return r; }
+  U256 operator^(const U256& o) const { U256 r; for (int i = 0; i < 4; i++) r.w[i] = w[i] ^ o.w[i]; return r; }
+  U256 operator~() const { U256 r; for (int i = 0; i < 4; i++) r.w[i] = ~w[i]; return r; }
+  // sum; *carry = carry out of bit 255
+  static U256 add(const U256& a, const U256& b, bool* carry) {
+    U256 r;
+    unsigned __int128 c = 0;
+    for (int i = 0; i < 4; i++) {
+      c += (unsigned __int128)a.w[i] + b.w[i];
+      r.w[i] = (uint64_t)c;
+      c >>= 64;
+    }
+    if (carry) *carry = c != 0;
+    return r;
+  }
+  static U256 sub(const U256& a, const U256& b) {  // mod 2^256
+    U256 r;
+    uint64_t br = 0;
+    for (int i = 0; i < 4; i++) {
+      const unsigned __int128 t = (unsigned __int128)a.w[i] - b.w[i] - br;
+      r.w[i] = (uint64_t)t;
+      br = (uint64_t)(t >> 64) & 1u;
+    }
+    return r;
+  }
+  U256 shr(uint32_t n) const {
+    if (n >= 256) return U256{};
+    U256 r;
+    const uint32_t q = n / 64, s = n % 64;
+    for (uint32_t i = 0; i + q < 4; i++) {
+      uint64_t v = w[i + q] >> s;
+      if (s && i + q + 1 < 4) v |= w[i + q + 1] << (64 - s);
+      r.w[i] = v;
+    }
+    return r;
+  }
+  U256 shl(uint32_t n) const {  // bits beyond 255 dropped
+    if (n >= 256) return U256{};
+    U256 r;
+    const uint32_t q = n / 64, s = n % 64;
+    for (uint32_t i = q; i < 4; i++) {
+      uint64_t v = w[i - q] << s;
+      if (s && i - q >= 1) v |= w[i - q - 1] >> (64 - s);
+      r.w[i] = v;
+    }
+    return r;
+  }
+  int top_bit() const {  // index of the highest set bit, -1 if zero
+    for (int i = 3; i >= 0; i--)
+      if (w[i]) return 64 * i + 63 - __builtin_clzll(w[i]);
+    return -1;
+  }
+  int trailing_ones() const {
+    for (int i = 0; i < 4; i++)
+      if (~w[i]) return 64 * i + __builtin_ctzll(~w[i]);
+    return 256;
+  }
+};
+
+constexpr size_t kMaxSet = 16;  // value sets (DICT coordinates, constants) up to this many entries
+
 struct Analysis {
   const Lowered& P;
   const std::vector<GenSpec>* specs;
   const std::vector<uint32_t>* gconsts;
   Analysis(const Lowered& p, const std::vector<GenSpec>* s, const std::vector<uint32_t>* g) : P(p), specs(s), gconsts(g) {}
-  // rng[id]: when known, the value lies in [lo, hi] (so it fits in 64 bits).  In the
-  // search kernel a coordinate's range comes from its generator spec, which bounds
-  // EVERY candidate the kernel evaluates (clamp records, dictionaries, fixed bits), so a
-  // comparison decided by the ranges is decided for every candidate: it folds to a
-  // literal, an ITE on it becomes an alias of the chosen arm, and bits() then looks
-  // through it (e.g. the calldata guard If(k < size, calldata[k], 0) with size drawn
-  // from [68, 2^32) collapses to the byte, and a CALLDATALOAD to its AUX word).
+  // Abstract value of an SSA id (widths <= 256; anything wider is unknown), three facts that
+  // hold for EVERY candidate the kernel evaluates.  In the search kernel a coordinate's facts
+  // come from its generator spec, which bounds every candidate it draws (clamp records,
+  // dictionaries, alignment, fixed bits):
+  //  * rng: the value lies in [lo, hi];
+  //  * known bits: bits in z are 0, bits in o are 1 (bits at or above the width are in z);
+  //  * set (has_set): the value is one of at most kMaxSet values (a DICT coordinate, e.g. the
+  //    caller drawn from LASER's actors, and what selects or slices of it give).
+  // A comparison they decide folds to a literal, an ITE on it becomes an alias of the chosen
+  // arm, and bits() then looks through it (e.g. the calldata guard If(k < size, calldata[k], 0)
+  // with size drawn from [68, 2^32) collapses to the byte, and a CALLDATALOAD to its AUX word).
   struct Rng {
     bool k = false;
-    uint64_t lo = 0, hi = 0;
+    U256 lo, hi;
   };
-  std::vector<Rng> rng;
+  struct KB {
+    bool k = false;
+    U256 z, o;
+  };
+  struct Val {
+    Rng r;
+    KB kb;
+    bool has_set = false;
+    std::vector<U256> set;  // sorted, unique
+  };
+  // A Bool that equals (src in S), or its negation: the disjunction Or(x == c1, x == c2, ...)
+  // LASER builds for the caller of every transaction is one; when src's own set lies inside S
+  // (or outside it) the predicate is decided.
+  struct Mem {
+    bool k = false, neg = false;
+    uint32_t src = 0;
+    std::vector<U256> S;
+  };
+  std::vector<Val> val;
+  std::vector<Mem> mem;
   // psrc/plo: the value is bits [plo, plo + width) of value psrc (a chain of EXTRACTs, and
   // CONCATs of adjacent slices of one value, e.g. a CALLDATALOAD of an AUX word's bytes)
   std::vector<uint32_t> psrc, plo;
   std::vector<int8_t> fold;       // per id: -1, or the folded Bool value
   std::vector<uint32_t> alias;    // per id: the id it equals (itself if none)
   std::vector<char> skip;         // per instruction: defines an alias / a decided assert
-  std::vector<Rng> crng;          // per coordinate (search mode)
+  std::vector<Val> cval;          // per coordinate (search mode)
 
   uint32_t res(uint32_t id) const {
     if (alias.empty() || id >= alias.size()) return id;
     while (alias[id] != id) id = alias[id];
     return id;
   }
-  static Rng full(uint32_t w) {
+
+  // ---- lattice helpers ----
+  static Rng rfull(uint32_t w) {
     Rng r;
-    if (w <= 64) {
+    if (w <= 256) {
       r.k = true;
-      r.hi = w == 64 ? ~0ull : ((1ull << w) - 1ull);
+      r.hi = U256::ones(w);
     }
     return r;
   }
-  static Rng exact(uint64_t v) {
+  static Rng rexact(const U256& v) {
     Rng r;
     r.k = true;
     r.lo = r.hi = v;
     return r;
   }
-  static Rng hull(const Rng& a, const Rng& b) {
+  static Rng rhull(const Rng& a, const Rng& b) {
     Rng r;
     if (!a.k || !b.k) return r;
     r.k = true;
-    r.lo = std::min(a.lo, b.lo);
-    r.hi = std::max(a.hi, b.hi);
+    r.lo = a.lo < b.lo ? a.lo : b.lo;
+    r.hi = a.hi < b.hi ? b.hi : a.hi;
     return r;
   }
-  // limbs [0, L) as one u64 if every limb >= 2 is zero
-  static bool fits64(const uint32_t* x, uint32_t L, uint64_t* v) {
-    for (uint32_t j = 2; j < L; j++)
-      if (x[j]) return false;
-    *v = (uint64_t)x[0] | (L > 1 ? (uint64_t)x[1] << 32 : 0ull);
-    return true;
+  static KB kfull(uint32_t w) {
+    KB k;
+    if (w <= 256) {
+      k.k = true;
+      k.z = ~U256::ones(w);
+    }
+    return k;
+  }
+  static KB kexact(const U256& v, uint32_t w) {
+    KB k;
+    k.k = true;
+    k.o = v;
+    k.z = ~v;
+    (void)w;
+    return k;
+  }
+  static KB kmeet(const KB& a, const KB& b) {
+    KB k;
+    if (!a.k || !b.k) return k;
+    k.k = true;
+    k.z = a.z & b.z;
+    k.o = a.o & b.o;
+    return k;
+  }
+  static Val vfull(uint32_t w) {
+    Val v;
+    v.r = rfull(w);
+    v.kb = kfull(w);
+    return v;
+  }
+  static Val vexact(const U256& x, uint32_t w) {
+    Val v;
+    v.r = rexact(x);
+    v.kb = kexact(x, w);
+    v.has_set = true;
+    v.set = {x};
+    return v;
+  }
+  static void set_norm(std::vector<U256>& s) {
+    std::sort(s.begin(), s.end());
+    s.erase(std::unique(s.begin(), s.end()), s.end());
+  }
+  static bool exact_of(const Val& v, U256* x) {
+    if (v.r.k && v.r.lo == v.r.hi) {
+      *x = v.r.lo;
+      return true;
+    }
+    return false;
+  }
+  // tighten: range from known bits and known bits from range; a set tightens both
+  static void tighten(Val& v, uint32_t w) {
+    if (w > 256) {
+      v = Val{};
+      return;
+    }
+    if (!v.r.k) v.r = rfull(w);
+    if (!v.kb.k) v.kb = kfull(w);
+    const U256 m = U256::ones(w);
+    v.kb.z = v.kb.z | ~m;
+    v.kb.o = v.kb.o & m;
+    if (v.has_set) {
+      if (v.set.empty() || v.set.size() > kMaxSet) {
+        v.has_set = false;
+        v.set.clear();
+      } else {
+        Rng h = rexact(v.set[0]);
+        KB kk = kexact(v.set[0], w);
+        for (const U256& x : v.set) {
+          h = rhull(h, rexact(x));
+          kk = kmeet(kk, kexact(x, w));
+        }
+        v.r = h;  // the set's hull is inside any other range fact we hold
+        v.kb.z = v.kb.z | kk.z;
+        v.kb.o = v.kb.o | kk.o;
+      }
+    }
+    // bits above the highest bit of hi are zero; the common prefix of lo and hi is known
+    const int d = (v.r.lo ^ v.r.hi).top_bit();
+    const U256 above = d >= 255 ? U256{} : ~U256::ones((uint32_t)(d + 1));
+    v.kb.z = v.kb.z | (above & ~v.r.lo);
+    v.kb.o = v.kb.o | (above & v.r.lo);
+    // range from known bits: lo >= ones, hi <= not-zeros
+    const U256 klo = v.kb.o, khi = ~v.kb.z & m;
+    if (v.r.lo < klo) v.r.lo = klo;
+    if (khi < v.r.hi) v.r.hi = khi;
+    if (v.r.hi < v.r.lo) {  // contradictory facts cannot happen for reachable values; stay safe
+      v.r = rfull(w);
+      v.kb = kfull(w);
+      v.has_set = false;
+      v.set.clear();
+    }
   }
 
-  // range of a generated coordinate's final value (include/mythgpu.h GEN3)
-  Rng coord_range(uint32_t c) const {
+  // value of a generated coordinate (include/mythgpu.h GEN3)
+  Val coord_val(uint32_t c) const {
     const GenSpec& sp = (*specs)[c];
     const uint32_t w = P.coord_width[c], L = Lw(w), kind = sp.kind & 0xFFu;
+    Val v;
+    if (w > 256) return v;
     const auto& G = *gconsts;
-    const unsigned __int128 wlim = w >= 128 ? ~(unsigned __int128)0 : (((unsigned __int128)1 << w) - 1);
-    Rng r;
+    const U256 wlim = U256::ones(w);
+    auto lim = [&](uint32_t off, U256* x) { return U256::from_limbs(&G[off], L, x); };
     switch (kind) {
       case MG_GEN_FIXED: {
-        uint64_t v;
-        if (fits64(&G[sp.p[0]], L, &v)) r = exact(v);
+        U256 x;
+        if (lim(sp.p[0], &x)) v = vexact(x, w);
         break;
       }
       case MG_GEN_DICT:
       case MG_GEN_MIXED: {
-        Rng d;  // dictionary hull
+        std::vector<U256> d;  // dictionary entries
         bool ok = sp.p[1] > 0;
         for (uint32_t e = 0; ok && e < sp.p[1]; e++) {
-          uint64_t v;
-          if (!fits64(&G[sp.p[0] + e * L], L, &v)) ok = false;
-          else d = d.k ? hull(d, exact(v)) : exact(v);
+          U256 x;
+          if (!lim(sp.p[0] + e * L, &x)) ok = false;
+          else d.push_back(x);
+        }
+        Rng dh;
+        if (ok) {
+          dh = rexact(d[0]);
+          for (const U256& x : d) dh = rhull(dh, rexact(x));
         }
         if (kind == MG_GEN_DICT) {
-          if (ok) r = d;
+          if (ok) {
+            v.r = dh;
+            if (d.size() <= kMaxSet) {
+              v.has_set = true;
+              v.set = d;
+              set_norm(v.set);
+            }
+          }
           break;
         }
         if (sp.p[6]) {  // clamp record: the final value is inside [lo, lo + span)
-          uint64_t lo;
+          U256 lo;
           const uint32_t rec = sp.p[6] - 1;
-          if (fits64(&G[rec], L, &lo)) {
+          if (lim(rec, &lo)) {
             const uint64_t span = G[rec + L] ? G[rec + L] : (1ull << 32);
-            if ((unsigned __int128)lo + span - 1 <= (unsigned __int128)~0ull) {
-              r.k = true;
-              r.lo = lo;
-              r.hi = lo + span - 1;
+            bool cy = false;
+            const U256 hi = U256::add(lo, U256::of(span - 1), &cy);
+            if (!cy && hi <= wlim) {
+              v.r.k = true;
+              v.r.lo = lo;
+              v.r.hi = hi;
             }
           }
           break;
@@ -796,120 +1022,164 @@ struct Analysis {
         bool have = false, unknown = false;
         auto add = [&](const Rng& x) {
           if (!x.k) unknown = true;
-          else u = have ? hull(u, x) : x;
+          else u = have ? rhull(u, x) : x;
           have = true;
         };
         Rng cd;  // COPY / DICT part, before the delta
         bool cd_have = false, cd_unknown = false;
         if (pc) {
-          const Rng s = crng[sp.p[3]];
+          const Rng s = cval[sp.p[3]].r;
           if (!s.k) cd_unknown = true;
           else cd = s;
           cd_have = true;
         }
         if (pd) {
           if (!ok) cd_unknown = true;
-          else cd = cd_have && cd.k ? hull(cd, d) : d;
+          else cd = cd_have && cd.k ? rhull(cd, dh) : dh;
           cd_have = true;
         }
         if (cd_have) {
-          if (cd_unknown) add(Rng{});
-          else if (sp.p[5]) {  // +/-2 at most, no wrap
-            if (cd.lo >= 2 && (unsigned __int128)cd.hi + 2 <= wlim && cd.hi + 2 > cd.hi) {
+          if (cd_unknown) {
+            add(Rng{});
+          } else if (sp.p[5]) {  // +/-2 at most, no wrap
+            bool cy = false;
+            const U256 hi2 = U256::add(cd.hi, U256::of(2), &cy);
+            if (U256::of(2) <= cd.lo && !cy && hi2 <= wlim) {
               Rng x;
               x.k = true;
-              x.lo = cd.lo - 2;
-              x.hi = cd.hi + 2;
+              x.lo = U256::sub(cd.lo, U256::of(2));
+              x.hi = hi2;
               add(x);
             } else {
-              add(full(w));
+              add(rfull(w));
             }
           } else {
             add(cd);
           }
         }
         const uint32_t sb = std::min(w, sp.p[4] >> 16);
-        if (ps) add(full(sb));
-        if (pc + pd + ps < 65536u) add(full(w));
-        if (have && !unknown) r = u;
+        if (ps) add(rfull(sb));
+        if (pc + pd + ps < 65536u) add(rfull(w));
+        if (have && !unknown) v.r = u;
         break;
       }
       case MG_GEN_RANGE: {
-        uint64_t lo;
-        if (fits64(&G[sp.p[0]], L, &lo)) {
+        U256 lo;
+        if (lim(sp.p[0], &lo)) {
           const uint64_t span = sp.p[1] ? sp.p[1] : (1ull << 32);
-          if ((unsigned __int128)lo + span - 1 <= wlim && (unsigned __int128)lo + span - 1 <= (unsigned __int128)~0ull) {
-            r.k = true;
-            r.lo = lo;
-            r.hi = lo + span - 1;
+          bool cy = false;
+          const U256 hi = U256::add(lo, U256::of(span - 1), &cy);
+          if (!cy && hi <= wlim) {
+            v.r.k = true;
+            v.r.lo = lo;
+            v.r.hi = hi;
           }
         }
         break;
       }
       case MG_GEN_ALIGNED: {
-        uint64_t lo;
-        if (fits64(&G[sp.p[0]], L, &lo) && sp.p[1] < 64) {
-          const unsigned __int128 cnt = sp.p[2] ? sp.p[2] : (1ull << 32);
-          const unsigned __int128 top = (unsigned __int128)lo + ((cnt - 1) << sp.p[1]);
-          if (top <= wlim && top <= (unsigned __int128)~0ull) {
-            r.k = true;
-            r.lo = lo;
-            r.hi = (uint64_t)top;
+        U256 lo;
+        if (lim(sp.p[0], &lo) && sp.p[1] < 256) {
+          const uint64_t cnt = sp.p[2] ? sp.p[2] : (1ull << 32);
+          const U256 step = U256::of(cnt - 1).shl(sp.p[1]);
+          bool cy = false;
+          const U256 top = U256::add(lo, step, &cy);
+          // (cnt - 1) << p1 must not lose bits either
+          if (!cy && top <= wlim && step.shr(sp.p[1]) == U256::of(cnt - 1)) {
+            v.r.k = true;
+            v.r.lo = lo;
+            v.r.hi = top;
           }
+          // lo + (m << p1): the low p1 bits are lo's, wrap or not
+          v.kb = kfull(w);
+          const U256 low = U256::ones(std::min(sp.p[1], w));
+          v.kb.z = v.kb.z | (low & ~lo);
+          v.kb.o = lo & low;
         }
         break;
       }
       default:  // UNIFORM / LAZY
-        r = full(w);
         break;
     }
-    if (!r.k) r = full(w);
-    if (const uint32_t fix = sp.kind >> 8) {  // (v & ~m) | val lies in [val, val | ~m]
-      const uint32_t f = fix - 1;
-      uint64_t m, val;
-      std::vector<uint32_t> nm(L);
-      for (uint32_t j = 0; j < L; j++) nm[j] = ~G[f + j];
-      if (w & 31) nm[L - 1] &= (1u << (w & 31)) - 1u;
-      if (fits64(&G[f + L], L, &val) && fits64(nm.data(), L, &m)) {
-        r.k = true;
-        r.lo = val;
-        r.hi = val | m;
+    tighten(v, w);
+    if (const uint32_t fix = sp.kind >> 8) {  // (v & ~m) | val
+      U256 m, fv;
+      if (U256::from_limbs(&G[fix - 1], L, &m) && U256::from_limbs(&G[fix - 1 + L], L, &fv)) {
+        m = m & wlim;
+        fv = fv & m;
+        Val f;
+        f.kb.k = true;
+        f.kb.z = (v.kb.z & ~m) | (m & ~fv);
+        f.kb.o = (v.kb.o & ~m) | fv;
+        if (v.has_set) {
+          f.has_set = true;
+          for (const U256& x : v.set) f.set.push_back((x & ~m) | fv);
+          set_norm(f.set);
+        }
+        v = f;
+        tighten(v, w);
       } else {
-        r = Rng{};
+        v = vfull(w);
       }
     }
-    return r;
+    return v;
   }
 
-  // decide a comparison from operand ranges: -1 undecided, else 0 / 1
-  static int decide(uint32_t op, const Rng& a, const Rng& b, uint32_t wa) {
-    if (!a.k || !b.k) return -1;
+  // decide a comparison from the operands' facts: -1 undecided, else 0 / 1
+  static int decide(uint32_t op, const Val& a, const Val& b, uint32_t wa) {
+    if (wa > 256 || !a.r.k || !b.r.k) return -1;
+    if (op == K_EQ) {
+      U256 x, y;
+      if (exact_of(a, &x) && exact_of(b, &y)) return x == y;
+      if (a.r.hi < b.r.lo || b.r.hi < a.r.lo) return 0;
+      if (a.kb.k && b.kb.k && !((a.kb.o & b.kb.z) | (a.kb.z & b.kb.o)).zero()) return 0;
+      if (a.has_set && b.has_set) {
+        bool any = false;
+        for (const U256& p : a.set)
+          if (std::binary_search(b.set.begin(), b.set.end(), p)) any = true;
+        if (!any) return 0;
+      }
+      return -1;
+    }
+    Rng ra = a.r, rb = b.r;
     if (op == K_SLT || op == K_SLE) {
-      const uint64_t sign = wa >= 65 ? 0ull : (1ull << (wa - 1));
-      if (sign && (a.hi >= sign || b.hi >= sign)) return -1;  // a negative value may be inside
+      // both non-negative (sign bit known zero): signed order is unsigned order
+      const U256 sign = U256::of(1).shl(wa - 1);
+      if (sign <= ra.hi || sign <= rb.hi) return -1;
       op = op == K_SLT ? K_ULT : K_ULE;
     }
     switch (op) {
       case K_ULT:
-        if (a.hi < b.lo) return 1;
-        if (a.lo >= b.hi) return 0;
+        if (ra.hi < rb.lo) return 1;
+        if (rb.hi <= ra.lo) return 0;
         return -1;
       case K_ULE:
-        if (a.hi <= b.lo) return 1;
-        if (a.lo > b.hi) return 0;
-        return -1;
-      case K_EQ:
-        if (a.lo == a.hi && b.lo == b.hi && a.lo == b.lo) return 1;
-        if (a.hi < b.lo || b.hi < a.lo) return 0;
+        if (ra.hi <= rb.lo) return 1;
+        if (rb.hi < ra.lo) return 0;
         return -1;
       default:
         return -1;
     }
   }
 
+  int decide_mem(const Mem& m) const {
+    if (!m.k) return -1;
+    const Val& s = val[res(m.src)];
+    if (!s.has_set) return -1;
+    size_t in = 0;
+    for (const U256& x : s.set)
+      if (std::binary_search(m.S.begin(), m.S.end(), x)) in++;
+    int v = -1;
+    if (in == s.set.size()) v = 1;
+    else if (in == 0) v = 0;
+    if (v >= 0 && m.neg) v = 1 - v;
+    return v;
+  }
+
   void analyze(bool search) {
     const size_t nv = P.vwidth.size();
-    rng.assign(nv, Rng{});
+    val.assign(nv, Val{});
+    mem.assign(nv, Mem{});
     psrc.assign(nv, MG_NONE);
     plo.assign(nv, 0);
     fold.assign(nv, -1);
@@ -917,52 +1187,89 @@ struct Analysis {
     for (size_t i = 0; i < nv; i++) alias[i] = (uint32_t)i;
     skip.assign(P.vcode.size(), 0);
     if (search && specs) {
-      crng.assign(P.n_coords, Rng{});
-      for (uint32_t c = 0; c < P.n_coords; c++) crng[c] = coord_range(c);
+      cval.assign(P.n_coords, Val{});
+      for (uint32_t c = 0; c < P.n_coords; c++) cval[c] = coord_val(c);
     }
     for (size_t k = 0; k < P.vcode.size(); k++) {
       const Instr& in = P.vcode[k];
       const uint32_t d = in.dst, W = in.wd;
-      auto R = [&](uint32_t id) { return rng[res(id)]; };
+      auto V = [&](uint32_t id) -> const Val& { return val[res(id)]; };
       auto F = [&](uint32_t id) { return (int)fold[res(id)]; };
       auto alias_to = [&](uint32_t src) {
         alias[d] = res(src);
-        rng[d] = rng[res(src)];
+        val[d] = val[res(src)];
+        mem[d] = mem[res(src)];
         fold[d] = fold[res(src)];
         skip[k] = 1;
       };
       auto set_fold = [&](int v) {
         fold[d] = (int8_t)v;
-        rng[d] = exact((uint64_t)v);
+        val[d] = vexact(U256::of((uint64_t)v), 1);
       };
       if (d == MG_NONE || d >= nv) {
         if (in.op == K_ASSERT && F(in.a) == 1) skip[k] = 1;
         continue;
       }
-      Rng r = full(W);
+      Val r = vfull(W);
       switch (in.op) {
         case K_CONST: {
-          uint64_t v;
-          if (fits64(&P.consts[in.p0], Lw(W), &v)) r = exact(v);
+          U256 x;
+          if (W <= 256 && U256::from_limbs(&P.consts[in.p0], Lw(W), &x)) r = vexact(x & U256::ones(W), W);
+          if (W == 1 && r.r.k) fold[d] = (int8_t)(r.r.lo.w[0] & 1u);  // a Bool literal (e.g. a folded root)
           break;
         }
         case K_COORD:
-          if (search && specs) r = crng[in.p0];
+          if (search && specs) r = cval[in.p0];
           break;
         case K_COPY:
           alias_to(in.a);
           continue;
-        case K_ZEXT:
-          if (R(in.a).k) r = R(in.a);
+        case K_ZEXT: {
+          const Val& a = V(in.a);
+          if (W <= 256 && in.p1 <= 256) {
+            r = a;
+            if (!r.r.k) r.r = rfull(in.p1);
+            if (!r.kb.k) r.kb = kfull(in.p1);
+          }
           break;
+        }
+        case K_SEXT: {
+          const Val& a = V(in.a);
+          const uint32_t wa = in.p1;
+          if (W <= 256 && wa <= 256 && a.kb.k) {
+            const U256 sign = U256::of(1).shl(wa - 1);
+            const U256 ext = U256::ones(W) & ~U256::ones(wa);
+            if (!(a.kb.z & sign).zero()) {  // non-negative: a zero extension
+              r = a;
+            } else if (!(a.kb.o & sign).zero()) {  // negative: high bits ones
+              r.kb.k = true;
+              r.kb.z = a.kb.z & U256::ones(wa);
+              r.kb.o = a.kb.o | ext;
+              r.r = rfull(W);
+            }
+          }
+          break;
+        }
         case K_EXTRACT: {
-          const Rng a = R(in.a);
-          if (a.k && in.p0 < 64 && (W >= 64 || (a.hi >> in.p0) < (1ull << W))) {
-            r.k = true;
-            r.lo = a.lo >> in.p0;
-            r.hi = a.hi >> in.p0;
-          } else if (a.k && in.p0 >= 64) {
-            r = exact(0);
+          const Val& a = V(in.a);
+          const uint32_t wa = in.p1;
+          if (W <= 256 && wa <= 256) {
+            const U256 m = U256::ones(W);
+            if (a.r.k && a.r.hi.shr(in.p0) <= m) {
+              r.r.k = true;
+              r.r.lo = a.r.lo.shr(in.p0);
+              r.r.hi = a.r.hi.shr(in.p0);
+            }
+            if (a.kb.k) {
+              r.kb.k = true;
+              r.kb.z = a.kb.z.shr(in.p0) | ~m;
+              r.kb.o = a.kb.o.shr(in.p0) & m;
+            }
+            if (a.has_set) {
+              r.has_set = true;
+              for (const U256& x : a.set) r.set.push_back(x.shr(in.p0) & m);
+              set_norm(r.set);
+            }
           }
           const uint32_t ra = res(in.a);
           const uint32_t src = psrc[ra] != MG_NONE ? psrc[ra] : ra;
@@ -987,16 +1294,27 @@ struct Analysis {
               }
               psrc[d] = sa;
               plo[d] = lb;
-              r = full(W);
+              r = vfull(W);
               break;
             }
           }
-          const Rng a = R(in.a), b = R(in.b);
+          const Val &a = V(in.a), &b = V(in.b);
           const uint32_t wb = in.p1;
-          if (a.k && b.k && wb < 64 && (a.hi >> (64 - wb)) == 0) {
-            r.k = true;
-            r.lo = (a.lo << wb) | b.lo;
-            r.hi = (a.hi << wb) | b.hi;
+          if (W <= 256 && a.r.k && b.r.k) {
+            r.r.k = true;  // a * 2^wb + b, b < 2^wb
+            r.r.lo = a.r.lo.shl(wb) | b.r.lo;
+            r.r.hi = a.r.hi.shl(wb) | b.r.hi;
+          }
+          if (W <= 256 && a.kb.k && b.kb.k) {
+            r.kb.k = true;
+            r.kb.z = a.kb.z.shl(wb) | (b.kb.z & U256::ones(wb)) | ~U256::ones(W);
+            r.kb.o = a.kb.o.shl(wb) | (b.kb.o & U256::ones(wb));
+          }
+          if (W <= 256 && a.has_set && b.has_set && a.set.size() * b.set.size() <= kMaxSet) {
+            r.has_set = true;
+            for (const U256& x : a.set)
+              for (const U256& y : b.set) r.set.push_back(x.shl(wb) | y);
+            set_norm(r.set);
           }
           break;
         }
@@ -1017,27 +1335,79 @@ struct Analysis {
               set_fold(fa ^ fb);
               continue;
             }
+            // membership predicates over one value: Or = union, And = intersection
+            const Mem &ma = mem[res(in.a)], &mb = mem[res(in.b)];
+            if (in.op != K_XOR && ma.k && mb.k && res(ma.src) == res(mb.src) && ma.neg == mb.neg) {
+              Mem m;
+              m.k = true;
+              m.src = res(ma.src);
+              m.neg = ma.neg;
+              // Or of positives = union; And of positives = intersection (negated: De Morgan)
+              const bool uni = (in.op == K_OR) != ma.neg;
+              if (uni) {
+                m.S = ma.S;
+                m.S.insert(m.S.end(), mb.S.begin(), mb.S.end());
+                set_norm(m.S);
+              } else {
+                for (const U256& x : ma.S)
+                  if (std::binary_search(mb.S.begin(), mb.S.end(), x)) m.S.push_back(x);
+              }
+              const int v = decide_mem(m);
+              if (v >= 0) { set_fold(v); continue; }
+              mem[d] = m;
+            }
             break;
           }
-          const Rng a = R(in.a), b = R(in.b);
-          if (in.op == K_AND) {
-            if (a.k || b.k) {
-              r.k = true;
-              r.lo = 0;
-              r.hi = std::min(a.k ? a.hi : ~0ull, b.k ? b.hi : ~0ull);
+          const Val &a = V(in.a), &b = V(in.b);
+          if (W <= 256 && a.kb.k && b.kb.k) {
+            r.kb.k = true;
+            if (in.op == K_AND) {
+              r.kb.z = a.kb.z | b.kb.z;
+              r.kb.o = a.kb.o & b.kb.o;
+            } else if (in.op == K_OR) {
+              r.kb.z = a.kb.z & b.kb.z;
+              r.kb.o = a.kb.o | b.kb.o;
+            } else {
+              const U256 kn = (a.kb.z | a.kb.o) & (b.kb.z | b.kb.o), x = a.kb.o ^ b.kb.o;
+              r.kb.z = kn & ~x;
+              r.kb.o = kn & x;
             }
-          } else if (a.k && b.k) {
-            const uint64_t m = std::max(a.hi, b.hi);
-            r.k = true;
-            r.lo = 0;
-            r.hi = m ? (~0ull >> __builtin_clzll(m)) : 0ull;
+            r.r = rfull(W);
+          }
+          if (W <= 256 && a.has_set && b.has_set && a.set.size() * b.set.size() <= kMaxSet) {
+            r.has_set = true;
+            for (const U256& x : a.set)
+              for (const U256& y : b.set) r.set.push_back(in.op == K_AND ? (x & y) : in.op == K_OR ? (x | y) : (x ^ y));
+            set_norm(r.set);
           }
           break;
         }
         case K_NOT:
-          if (W == 1 && F(in.a) >= 0) {
-            set_fold(1 - F(in.a));
-            continue;
+          if (W == 1) {
+            if (F(in.a) >= 0) {
+              set_fold(1 - F(in.a));
+              continue;
+            }
+            const Mem& ma = mem[res(in.a)];
+            if (ma.k) {
+              mem[d] = ma;
+              mem[d].neg = !ma.neg;
+            }
+            break;
+          }
+          if (W <= 256) {
+            const Val& a = V(in.a);
+            const U256 m = U256::ones(W);
+            if (a.kb.k) {
+              r.kb.k = true;
+              r.kb.z = a.kb.o | ~m;
+              r.kb.o = a.kb.z & m;
+            }
+            if (a.has_set) {
+              r.has_set = true;
+              for (const U256& x : a.set) r.set.push_back(~x & m);
+              set_norm(r.set);
+            }
           }
           break;
         case K_ITE: {
@@ -1046,25 +1416,70 @@ struct Analysis {
             alias_to(fc ? in.b : in.c);
             continue;
           }
-          const Rng h = hull(R(in.b), R(in.c));
-          if (h.k) r = h;
+          if (res(in.b) == res(in.c)) {
+            alias_to(in.b);
+            continue;
+          }
+          const Val &b = V(in.b), &c = V(in.c);
+          if (W <= 256) {
+            r.r = rhull(b.r, c.r);
+            r.kb = kmeet(b.kb, c.kb);
+            if (b.has_set && c.has_set) {
+              r.has_set = true;
+              r.set = b.set;
+              r.set.insert(r.set.end(), c.set.begin(), c.set.end());
+              set_norm(r.set);
+            }
+          }
           break;
         }
         case K_ADD: {
-          const Rng a = R(in.a), b = R(in.b);
-          if (a.k && b.k && (unsigned __int128)a.hi + b.hi <= (unsigned __int128)full(std::min(W, 64u)).hi) {
-            r.k = true;
-            r.lo = a.lo + b.lo;
-            r.hi = a.hi + b.hi;
+          const Val &a = V(in.a), &b = V(in.b);
+          if (W <= 256 && a.r.k && b.r.k) {
+            bool cy = false;
+            const U256 hi = U256::add(a.r.hi, b.r.hi, &cy);
+            if (!cy && hi <= U256::ones(W)) {
+              r.r.lo = U256::add(a.r.lo, b.r.lo, nullptr);
+              r.r.hi = hi;
+            }
+          }
+          if (W <= 256 && a.kb.k && b.kb.k) {  // low bits known in both operands: known sum
+            const int t = std::min((a.kb.z | a.kb.o).trailing_ones(), (b.kb.z | b.kb.o).trailing_ones());
+            if (t > 0) {
+              const U256 lm = U256::ones((uint32_t)std::min(t, (int)W));
+              const U256 s = U256::add(a.kb.o & lm, b.kb.o & lm, nullptr) & lm;
+              r.kb.z = r.kb.z | (lm & ~s);
+              r.kb.o = r.kb.o | s;
+            }
+          }
+          if (W <= 256 && a.has_set && b.has_set && a.set.size() * b.set.size() <= kMaxSet) {
+            r.has_set = true;
+            for (const U256& x : a.set)
+              for (const U256& y : b.set) r.set.push_back(U256::add(x, y, nullptr) & U256::ones(W));
+            set_norm(r.set);
           }
           break;
         }
         case K_SUB: {
-          const Rng a = R(in.a), b = R(in.b);
-          if (a.k && b.k && a.lo >= b.hi) {
-            r.k = true;
-            r.lo = a.lo - b.hi;
-            r.hi = a.hi - b.lo;
+          const Val &a = V(in.a), &b = V(in.b);
+          if (W <= 256 && a.r.k && b.r.k && b.r.hi <= a.r.lo) {
+            r.r.lo = U256::sub(a.r.lo, b.r.hi);
+            r.r.hi = U256::sub(a.r.hi, b.r.lo);
+          }
+          if (W <= 256 && a.kb.k && b.kb.k) {
+            const int t = std::min((a.kb.z | a.kb.o).trailing_ones(), (b.kb.z | b.kb.o).trailing_ones());
+            if (t > 0) {
+              const U256 lm = U256::ones((uint32_t)std::min(t, (int)W));
+              const U256 s = U256::sub(a.kb.o & lm, b.kb.o & lm) & lm;
+              r.kb.z = r.kb.z | (lm & ~s);
+              r.kb.o = r.kb.o | s;
+            }
+          }
+          if (W <= 256 && a.has_set && b.has_set && a.set.size() * b.set.size() <= kMaxSet) {
+            r.has_set = true;
+            for (const U256& x : a.set)
+              for (const U256& y : b.set) r.set.push_back(U256::sub(x, y) & U256::ones(W));
+            set_norm(r.set);
           }
           break;
         }
@@ -1073,11 +1488,29 @@ struct Analysis {
         case K_ULE:
         case K_SLT:
         case K_SLE: {
-          const int v = decide(in.op, R(in.a), R(in.b), in.p1);
+          const Val &a = V(in.a), &b = V(in.b);
+          int v = decide(in.op, a, b, in.p1);
+          if (v < 0 && res(in.a) == res(in.b)) v = (in.op == K_ULT || in.op == K_SLT) ? 0 : 1;  // x op x
           if (v >= 0) {
             set_fold(v);
             continue;
           }
+          if (in.op == K_EQ) {  // x == c: a membership predicate {c} over x
+            U256 c;
+            uint32_t x = MG_NONE;
+            if (exact_of(b, &c)) x = res(in.a);
+            else if (exact_of(a, &c)) x = res(in.b);
+            if (x != MG_NONE) {
+              Mem m;
+              m.k = true;
+              m.src = x;
+              m.S = {c};
+              const int dv = decide_mem(m);
+              if (dv >= 0) { set_fold(dv); continue; }
+              mem[d] = m;
+            }
+          }
+          r = vfull(1);
           break;
         }
         case K_LOOKUP: {
@@ -1085,22 +1518,36 @@ struct Analysis {
             alias_to(in.p0);
             continue;
           }
-          Rng h = R(in.p0);
-          for (uint32_t p = 0; p < in.c && h.k; p++) h = hull(h, R(P.vaux[in.p1 + 2 * p + 1]));
-          if (h.k) r = h;
+          Val h = V(in.p0);
+          bool all_same = true;
+          for (uint32_t p = 0; p < in.c; p++) {
+            const uint32_t vv = P.vaux[in.p1 + 2 * p + 1];
+            if (res(vv) != res(in.p0)) all_same = false;
+            const Val& x = V(vv);
+            h.r = rhull(h.r, x.r);
+            h.kb = kmeet(h.kb, x.kb);
+            if (h.has_set && x.has_set) {
+              h.set.insert(h.set.end(), x.set.begin(), x.set.end());
+              set_norm(h.set);
+            } else {
+              h.has_set = false;
+              h.set.clear();
+            }
+          }
+          if (all_same) {  // every source is the same value
+            alias_to(in.p0);
+            continue;
+          }
+          if (W <= 256) r = h;
           break;
         }
         default:
           break;
       }
-      if (r.k && W < 64) {  // intersect with the width
-        const uint64_t m = (1ull << W) - 1ull;
-        if (r.hi > m) r = full(W);
-      }
-      rng[d] = r;
+      tighten(r, W);
+      val[d] = std::move(r);
     }
   }
-
 };
 
 }  // namespace
@@ -1226,6 +1673,16 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
         out.consts.push_back((uint32_t)A.fold[c.dst]);
         code.push_back(VInstr{K_CONST, 1, c.dst, NONE, NONE, NONE, off, 0, {}});
         continue;
+      }
+      {  // a value every candidate gives the same (e.g. the low bits of an aligned site) is a literal
+        U256 x;
+        if (c.dst != NONE && c.dst < nv && c.wd <= 256 && c.op != K_CONST && c.op != K_COORD &&
+            c.op != K_ASSERT && c.op != K_WATCH && Analysis::exact_of(A.val[c.dst], &x)) {
+          const uint32_t off = (uint32_t)out.consts.size();
+          for (uint32_t j = 0; j < Lw(c.wd); j++) out.consts.push_back((uint32_t)(x.w[j / 2] >> (32 * (j % 2))));
+          code.push_back(VInstr{K_CONST, c.wd, c.dst, NONE, NONE, NONE, off, 0, {}});
+          continue;
+        }
       }
       if ((c.op == K_EXTRACT || c.op == K_CONCAT) && c.dst < nv && A.psrc[c.dst] != NONE) {
         const uint32_t src = A.psrc[c.dst];

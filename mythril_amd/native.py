@@ -30,7 +30,7 @@ NO_HIT = (1 << 64) - 1
 
 EXPORTS = [
     "mg_init", "mg_shutdown", "mg_last_error", "mg_version", "mg_program_check", "mg_program_check_gen",
-    "mg_program_load",
+    "mg_program_specialized", "mg_program_load",
     "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_info", "mg_gen_free", "mg_eval", "mg_eval_dev",
     "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
     "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_jit_compile", "mg_jit_compile_ex", "mg_jit_verdicts", "mg_jit_info",
@@ -98,6 +98,8 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_version": (C.c_int, []),
             "mg_program_check": (C.c_int, [u8p, C.c_size_t, C.POINTER(ProgramInfo)]),
             "mg_program_check_gen": (C.c_int, [u8p, C.c_size_t, u32p, C.c_size_t, C.POINTER(ProgramInfo)]),
+            "mg_program_specialized": (C.c_int, [u8p, C.c_size_t, u32p, C.c_size_t, C.c_uint32, u32p, C.c_size_t,
+                                                 C.POINTER(C.c_size_t)]),
             "mg_program_load": (C.c_int, [u8p, C.c_size_t, u64p]),
             "mg_program_info": (C.c_int, [C.c_uint64, C.POINTER(ProgramInfo)]),
             "mg_program_free": (C.c_int, [C.c_uint64]),
@@ -183,6 +185,37 @@ def check_program_gen(blob: bytes, gen_blob: np.ndarray) -> ProgramInfo:
     info = ProgramInfo()
     _check(lib.mg_program_check_gen(_u8(blob), len(blob), _ptr(g, C.c_uint32), g.size, C.byref(info)))
     return info
+
+
+MG_SPEC_MAGIC = 0x43455053
+MG_SPEC_KEEP_WATCH = 1
+
+
+def specialized_program(blob: bytes, gen_blob: Optional[np.ndarray] = None, keep_watch: bool = False) -> dict:
+    """Host-only ``mg_program_specialized``: the lowered, specialised program a search (with a
+    generator) or an eval (without) runs, in SSA form — ``code`` (n x 8 uint32:
+    op, width, dst, a, b, c, p0, p1), ``consts``, ``aux``, ``widths``, ``n_coords``."""
+    lib = load_library()
+    g = None if gen_blob is None else np.ascontiguousarray(gen_blob, dtype=np.uint32)
+    gp = _ptr(g, C.c_uint32) if g is not None else None
+    gn = 0 if g is None else g.size
+    flags = MG_SPEC_KEEP_WATCH if keep_watch else 0
+    n = C.c_size_t()
+    _check(lib.mg_program_specialized(_u8(blob), len(blob), gp, gn, flags, None, 0, C.byref(n)))
+    w = np.zeros(n.value, dtype=np.uint32)
+    _check(lib.mg_program_specialized(_u8(blob), len(blob), gp, gn, flags, _ptr(w, C.c_uint32), w.size,
+                                      C.byref(n)))
+    assert int(w[0]) == MG_SPEC_MAGIC
+    ni, nc, na, nv, ncoord = (int(x) for x in w[1:6])
+    pos = 6
+    code = w[pos:pos + 8 * ni].reshape(ni, 8)
+    pos += 8 * ni
+    consts = w[pos:pos + nc]
+    pos += nc
+    aux = w[pos:pos + na]
+    pos += na
+    widths = w[pos:pos + nv]
+    return {"code": code, "consts": consts, "aux": aux, "widths": widths, "n_coords": ncoord}
 
 
 def jit_source(blob: bytes, gen_blob: Optional[np.ndarray] = None, compile: bool = False) -> str:

@@ -742,3 +742,41 @@ int bv_eval(const uint32_t* prog, size_t prog_words, const uint32_t* soa, uint64
   free(rows);
   return bad ? -3 : 0;
 }
+
+/* The generated coordinates of candidates [start, start+n) as an SoA buffer ([row][n], the
+ * mg_eval layout; LAZY coordinates, whose values the program supplies, stay zero): lets a
+ * test run another evaluator (oracle/kops.py over the engine's specialised program) on
+ * exactly the candidates the generator draws. */
+int bv_gen_soa(const uint32_t* prog, size_t prog_words, const uint32_t* gen, size_t gen_words, uint64_t seed,
+               uint64_t start, uint64_t n, uint32_t* soa) {
+  prog_t P;
+  int rc = parse(&P, prog, prog_words, gen, gen_words);
+  if (rc) return rc;
+  uint32_t* rows = (uint32_t*)malloc(sizeof(uint32_t) * (P.n_coords + 1));
+  uint32_t acc = 0;
+  for (uint32_t c = 0; c < P.n_coords; c++) {
+    rows[c] = acc;
+    acc += (P.coords[4 * c] + 31) / 32;
+  }
+  ctx_t X;
+  memset(&X, 0, sizeof(X));
+  X.P = &P;
+  X.cvals = (val_t*)malloc(sizeof(val_t) * (P.n_coords + 1));
+  X.cdone = (uint8_t*)malloc(P.n_coords + 1);
+  memset(soa, 0, sizeof(uint32_t) * (size_t)acc * n);
+  for (uint64_t i = 0; i < n; i++) {
+    make_keys(start + i, seed, &X.keys);
+    memset(X.cdone, 0, P.n_coords);
+    for (uint32_t c = 0; c < P.n_coords; c++) {
+      if ((P.specs[8 * c] & 0xFFu) == 6u) continue; /* LAZY */
+      val_t v;
+      coord_value(&X, c, &v);
+      const uint32_t L = (P.coords[4 * c] + 31) / 32;
+      for (uint32_t j = 0; j < L; j++) soa[(uint64_t)(rows[c] + j) * n + i] = get_limb32(&v, j);
+    }
+  }
+  free(X.cvals);
+  free(X.cdone);
+  free(rows);
+  return 0;
+}

@@ -19,6 +19,8 @@ def lib():
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_void_p]
         _lib.bv_eval.restype = C.c_int
         _lib.bv_eval.argtypes = [u32p, C.c_size_t, u32p, C.c_uint64, C.c_void_p]
+        _lib.bv_gen_soa.restype = C.c_int
+        _lib.bv_gen_soa.argtypes = [u32p, C.c_size_t, u32p, C.c_size_t, C.c_uint64, C.c_uint64, C.c_uint64, u32p]
     return _lib
 
 
@@ -50,3 +52,16 @@ def eval_soa(prog_blob: bytes, soa: np.ndarray, n: int):
     if rc:
         raise RuntimeError(f"bv_eval failed: {rc}")
     return ver
+
+
+def gen_soa(prog_blob: bytes, gen_blob: np.ndarray, seed: int, start: int, n: int, coord_words: int) -> np.ndarray:
+    """The generated coordinates of candidates [start, start+n) as SoA rows (mg_eval layout)."""
+    p = _words(prog_blob)
+    g = np.ascontiguousarray(gen_blob, dtype=np.uint32)
+    soa = np.zeros((max(coord_words, 1), n), dtype=np.uint32)
+    u32p = C.POINTER(C.c_uint32)
+    rc = lib().bv_gen_soa(p.ctypes.data_as(u32p), p.size, g.ctypes.data_as(u32p), g.size, seed, start, n,
+                          soa.ctypes.data_as(u32p))
+    if rc:
+        raise RuntimeError(f"bv_gen_soa failed: {rc}")
+    return soa

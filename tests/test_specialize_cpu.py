@@ -1,0 +1,77 @@
+"""Specialisation keeps every verdict (CPU, no GPU).
+
+A search does not run the program it was given: ``program.cpp: specialize_program`` first
+folds every comparison the generator's value ranges, known bits and value sets decide, aliases
+ITEs/ORs/ANDs on decided conditions, drops decided asserts and dead code.  Both GPU kernels
+(the interpreter and the JIT) run that specialised program, so a wrong fold would change
+verdicts on the GPU without any kernel bug.  Here the specialised program
+(``mg_program_specialized``) is evaluated by the oracle's plain-Python evaluator of device ops
+(``oracle/kops.py``) on exactly the candidates the generator draws (``bv_gen_soa`` in
+``oracle/bveval.c``), and every verdict must equal the C port's on the *unspecialised* program.
+The eval-mode specialisation (literal facts only) is checked the same way on random
+assignments.
+
+Reference anchor: a candidate's verdict is ``Model.eval(And(constraints), model_completion=True)``
+(``mythril/laser/smt/model.py:45-59``); workloads follow SURVEY.md §8(d) C1-C5.
+"""
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+from mythril_amd import native, search, ssa, workloads
+from oracle import cport, kops
+from tests.helpers import random_assignments
+
+N = 384
+
+
+def _coord_words(P):
+    return sum(ssa.limbs(c.width) for c in P.coords)
+
+
+@pytest.mark.parametrize("keep_watch", [False, True], ids=["search", "watch"])
+@pytest.mark.parametrize("name", sorted(workloads.WORKLOADS), ids=workloads.test_id)
+def test_specialised_search_program_keeps_verdicts(name, keep_watch):
+    rng = random.Random(zlib.crc32(name.encode()) ^ 0x5BEC)
+    P, blob = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
+    pb = P.to_bytes()
+    spec = native.specialized_program(pb, blob, keep_watch=keep_watch)
+    widths = [c.width for c in P.coords]
+    n = N if name != "sha3_keyed_mapping" else 96
+    for start in (0, rng.getrandbits(63) | 1):
+        seed = rng.getrandbits(32)
+        soa = cport.gen_soa(pb, blob, seed, start, n, _coord_words(P))
+        want = cport.search(pb, blob, seed, start, n, threads=4, verdicts=True)[2]
+        got = kops.verdicts(spec, soa, widths, n)
+        bad = np.flatnonzero(got != want)
+        assert bad.size == 0, f"{name}: specialised verdict differs at index {start + int(bad[0])} (seed {seed})"
+
+
+@pytest.mark.parametrize("name", sorted(workloads.WORKLOADS), ids=workloads.test_id)
+def test_specialised_eval_program_keeps_verdicts(name):
+    P = ssa.flatten([c.raw for c in workloads.WORKLOADS[name]()])
+    pb = P.to_bytes()
+    spec = native.specialized_program(pb, None)
+    n = 128 if name != "sha3_keyed_mapping" else 48
+    soa = ssa.soa_from_assignments(P, random_assignments(P, n, seed=zlib.crc32(name.encode())))
+    want = cport.eval_soa(pb, soa, n)
+    got = kops.verdicts(spec, soa, [c.width for c in P.coords], n)
+    assert np.array_equal(got, want)
+
+
+def test_specialisation_folds_actor_membership():
+    """LASER pins every transaction's caller to the actors (``Or(caller == a, ...)``,
+    ``mythril/laser/ethereum/transaction/symbolic.py``); with the sender drawn from that same
+    set the disjunction is true for every candidate, so no instruction of it survives."""
+    P, blob = search.prepare([c.raw for c in workloads.WORKLOADS["token_transfer_underflow"]()])
+    senders = {c.index for c in P.coords if c.name.startswith("sender_")}
+    assert senders
+
+    def sender_eqs(spec):
+        vids = {int(r[2]) for r in spec["code"] if int(r[0]) == kops.K_COORD and int(r[6]) in senders}
+        return sum(1 for r in spec["code"] if int(r[0]) == kops.K_EQ and (int(r[3]) in vids or int(r[4]) in vids))
+
+    assert sender_eqs(native.specialized_program(P.to_bytes(), None)) >= 6  # 3 actors x 2 transactions
+    assert sender_eqs(native.specialized_program(P.to_bytes(), blob)) == 0
