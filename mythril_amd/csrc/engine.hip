@@ -377,7 +377,8 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
   // overlaps this instruction's LDS traffic instead of adding to it (the code buffer has
   // one padding record after the last instruction)
   Instr nx = ld_instr(k, 0);
-  for (uint32_t pc = 0; pc < n_instr; pc++) {
+  bool stop = false;
+  for (uint32_t pc = 0; pc < n_instr && !stop; pc++) {
     const Instr in = nx;
     nx = ld_instr(k, pc + 1);
     const uint32_t W = in.wd;
@@ -551,7 +552,10 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
       }
       case K_ASSERT: {
         verdict &= vf.at(in.a);
-        if (early && __ballot(verdict != 0) == 0ull) return 0u;
+        // every lane failed: stop (verdict is 0 everywhere).  A loop flag, not a return: a second
+        // loop exit made the compiler keep pc in a VGPR (vector address math + readfirstlane per
+        // fetch); readfirstlane makes the flag's uniformity explicit
+        if (early && __builtin_amdgcn_readfirstlane((uint32_t)(__ballot(verdict != 0) != 0ull)) == 0u) stop = true;
         break;
       }
       case K_WATCH: {
@@ -611,7 +615,10 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
       if (a0 + base >= cur_u) break;
     }
     GKeys key{};
-    if (MODE != MODE_EVAL) key = gen_keys_lk(idx, lk, k.sg);
+    // the group key from the wave's group base (a0 + base, a multiple of 64: idx >> 6 is the same for
+    // every lane), so the compiler sees G as wave-uniform: the MIXED alternatives are scalar branches
+    // and the generator specs scalar loads (from idx, G looked per-lane: divergent branches, vector loads)
+    if (MODE != MODE_EVAL) key = gen_keys_lk(a0 + base, lk, k.sg);
     uint32_t v = run_program<VF, MODE, HEAVY>(k, vf, i, key, early, active);
     v = active ? v : 0u;
     if (MODE == MODE_SEARCH) {

@@ -76,6 +76,14 @@ struct Gen {
   std::map<uint32_t, uint32_t> dict_lds;  // gconsts offset of a table -> LDS word offset
   uint32_t lds_words = 0;
   static constexpr uint32_t kDictLdsWords = 4096;  // 16 KiB per 256-lane block
+  // dictionaries up to this many entries are selects, not gathers (MYTHGPU_JIT_SELECT_DICT, default 4)
+  static uint32_t select_dict_max() {
+    static const uint32_t n = [] {
+      const char* g = getenv("MYTHGPU_JIT_SELECT_DICT");
+      return g ? (uint32_t)atoi(g) : 4u;
+    }();
+    return n;
+  }
 
   void plan_dict_lds() {
     dict_lds.clear();
@@ -136,8 +144,16 @@ struct Gen {
       bool same = true;
       for (uint32_t e = 1; e < n && same; e++) same = G[off + e * L + j] == G[off + j];
       std::string v;
-      if (same) v = hex(G[off + j]);
-      else if (lds != dict_lds.end()) v = "mg_dict[" + std::to_string(lds->second + j) + "u + " + idx + " * " + std::to_string(L) + "u]";
+      if (same) {
+        v = hex(G[off + j]);
+      } else if (n <= select_dict_max()) {
+        // a select over the entries' literals (v_cndmask): a per-lane gather is one VMEM
+        // instruction per limb, and the CU's one texture path serves its four SIMDs at a
+        // fraction of their VALU issue rate
+        v = hex(G[off + (n - 1) * L + j]);
+        for (int32_t e = (int32_t)n - 2; e >= 0; e--)
+          v = "(" + idx + " == " + std::to_string(e) + "u ? " + hex(G[off + e * L + j]) + " : " + v + ")";
+      } else if (lds != dict_lds.end()) v = "mg_dict[" + std::to_string(lds->second + j) + "u + " + idx + " * " + std::to_string(L) + "u]";
       else v = "gconsts[" + std::to_string(off + j) + "u + " + idx + " * " + std::to_string(L) + "u]";
       o << ind << lim(j) << " = " << v << ";\n";
     }

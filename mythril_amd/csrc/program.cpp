@@ -837,6 +837,8 @@ struct Analysis {
   std::vector<uint32_t> alias;    // per id: the id it equals (itself if none)
   std::vector<char> skip;         // per instruction: defines an alias / a decided assert
   std::vector<Val> cval;          // per coordinate (search mode)
+  std::vector<int32_t> defk;      // per id: index of its defining instruction (-1: none)
+  std::map<size_t, Instr> rewrite;  // instruction index -> the instruction emitted instead
 
   uint32_t res(uint32_t id) const {
     if (alias.empty() || id >= alias.size()) return id;
@@ -1186,6 +1188,10 @@ struct Analysis {
     alias.resize(nv);
     for (size_t i = 0; i < nv; i++) alias[i] = (uint32_t)i;
     skip.assign(P.vcode.size(), 0);
+    defk.assign(nv, -1);
+    rewrite.clear();
+    for (size_t k = 0; k < P.vcode.size(); k++)
+      if (P.vcode[k].dst < nv && defk[P.vcode[k].dst] < 0) defk[P.vcode[k].dst] = (int32_t)k;
     if (search && specs) {
       cval.assign(P.n_coords, Val{});
       for (uint32_t c = 0; c < P.n_coords; c++) cval[c] = coord_val(c);
@@ -1355,6 +1361,22 @@ struct Analysis {
               const int v = decide_mem(m);
               if (v >= 0) { set_fold(v); continue; }
               mem[d] = m;
+            }
+            // Or(a < b, a == b) is a <= b: LASER's ULE/UGE/SLE/SGE (mythril/laser/smt/bitvec_helper.py:53-80,
+            // Or(ULT(a, b), a == b)) as one borrow chain instead of a chain plus an equality
+            if (in.op == K_OR) {
+              auto def = [&](uint32_t id) -> const Instr* {
+                const int32_t x = defk[res(id)];
+                return x >= 0 && !skip[x] ? &P.vcode[x] : nullptr;
+              };
+              const Instr *x = def(in.a), *y = def(in.b);
+              if (x && y && x->op == K_EQ) std::swap(x, y);
+              if (x && y && y->op == K_EQ && (x->op == K_ULT || x->op == K_SLT) && x->p1 == y->p1) {
+                const uint32_t xa = res(x->a), xb = res(x->b), ya = res(y->a), yb = res(y->b);
+                if ((xa == ya && xb == yb) || (xa == yb && xb == ya)) {
+                  rewrite[k] = Instr{x->op == K_ULT ? (uint32_t)K_ULE : (uint32_t)K_SLE, 1, d, x->a, x->b, MG_NONE, 0, x->p1};
+                }
+              }
             }
             break;
           }
@@ -1687,6 +1709,12 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
       if ((c.op == K_EXTRACT || c.op == K_CONCAT) && c.dst < nv && A.psrc[c.dst] != NONE) {
         const uint32_t src = A.psrc[c.dst];
         code.push_back(VInstr{K_EXTRACT, c.wd, c.dst, src, NONE, NONE, A.plo[c.dst], in.vwidth[src], {}});
+        continue;
+      }
+      auto rw = A.rewrite.find(k);
+      if (rw != A.rewrite.end()) {
+        const Instr& x = rw->second;
+        code.push_back(VInstr{x.op, x.wd, x.dst, R(x.a), R(x.b), R(x.c), x.p0, x.p1, {}});
         continue;
       }
       VInstr v{c.op, c.wd, c.dst, R(c.a), R(c.b), R(c.c), c.p0, c.p1, {}};

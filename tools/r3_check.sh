@@ -14,3 +14,8 @@ for W in suicide_kill token_transfer_underflow etherstore_reentrancy bectoken_ba
 done
 timeout -k 10 400 python bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { tail -20 gpurun_out/${T}_bench.err; exit 1; }
 cat gpurun_out/${T}_bench.json
+# A/B: small dictionaries as gathers (the round-2 emission)
+for W in token_transfer_underflow suicide_kill; do
+  MYTHGPU_JIT_SELECT_DICT=0 timeout -k 10 300 python bench.py --workload $W --no-stream --no-eval --no-cpu-baseline --no-ttfm > gpurun_out/${T}_b_${W}_gather.json 2> gpurun_out/${T}_b_${W}_gather.err || { tail -20 gpurun_out/${T}_b_${W}_gather.err; exit 1; }
+  cat gpurun_out/${T}_b_${W}_gather.json >> gpurun_out/${T}_workloads.jsonl
+done
