@@ -839,6 +839,23 @@ struct Analysis {
   std::vector<Val> cval;          // per coordinate (search mode)
   std::vector<int32_t> defk;      // per id: index of its defining instruction (-1: none)
   std::map<size_t, Instr> rewrite;  // instruction index -> the instruction emitted instead
+  std::map<std::vector<uint32_t>, uint32_t> lit_id;  // literal (limbs, width) -> its first value id
+  // segs[id]: the value as slices of other values, low bits first (empty: see segs_of)
+  struct Seg {
+    uint32_t src, lo, w;
+  };
+  static constexpr size_t kMaxSegs = 4;
+  std::vector<std::vector<Seg>> segs;
+  std::vector<Seg> segs_of(uint32_t id) const {
+    id = res(id);
+    if (!segs[id].empty()) return segs[id];
+    if (psrc[id] != MG_NONE) return {Seg{psrc[id], plo[id], P.vwidth[id]}};
+    return {Seg{id, 0, P.vwidth[id]}};
+  }
+  static void seg_push(std::vector<Seg>& v, const Seg& x) {
+    if (!v.empty() && v.back().src == x.src && v.back().lo + v.back().w == x.lo) v.back().w += x.w;
+    else v.push_back(x);
+  }
 
   uint32_t res(uint32_t id) const {
     if (alias.empty() || id >= alias.size()) return id;
@@ -1190,6 +1207,8 @@ struct Analysis {
     skip.assign(P.vcode.size(), 0);
     defk.assign(nv, -1);
     rewrite.clear();
+    lit_id.clear();
+    segs.assign(nv, {});
     for (size_t k = 0; k < P.vcode.size(); k++)
       if (P.vcode[k].dst < nv && defk[P.vcode[k].dst] < 0) defk[P.vcode[k].dst] = (int32_t)k;
     if (search && specs) {
@@ -1219,6 +1238,17 @@ struct Analysis {
       Val r = vfull(W);
       switch (in.op) {
         case K_CONST: {
+          {  // one value per literal: later copies alias the first (no reload in the interpreter, and
+             // rewrites that match operands by id see equal literals as equal)
+            std::vector<uint32_t> key(P.consts.begin() + in.p0, P.consts.begin() + in.p0 + Lw(W));
+            key.push_back(W);
+            auto it = lit_id.find(key);
+            if (it != lit_id.end()) {
+              alias_to(it->second);
+              continue;
+            }
+            lit_id.emplace(std::move(key), d);
+          }
           U256 x;
           if (W <= 256 && U256::from_limbs(&P.consts[in.p0], Lw(W), &x)) r = vexact(x & U256::ones(W), W);
           if (W == 1 && r.r.k) fold[d] = (int8_t)(r.r.lo.w[0] & 1u);  // a Bool literal (e.g. a folded root)
@@ -1278,14 +1308,27 @@ struct Analysis {
             }
           }
           const uint32_t ra = res(in.a);
-          const uint32_t src = psrc[ra] != MG_NONE ? psrc[ra] : ra;
-          const uint32_t lo = (psrc[ra] != MG_NONE ? plo[ra] : 0u) + in.p0;
-          if (lo == 0 && W == P.vwidth[src]) {
-            alias_to(src);
-            continue;
+          std::vector<Seg> sl;  // the slice [p0, p0 + W) of a's segments
+          {
+            uint32_t pos = 0;
+            for (const Seg& sg : segs_of(ra)) {
+              const uint32_t lo = std::max(pos, in.p0), hi = std::min(pos + sg.w, in.p0 + W);
+              if (lo < hi) seg_push(sl, Seg{sg.src, sg.lo + (lo - pos), hi - lo});
+              pos += sg.w;
+            }
           }
-          psrc[d] = src;
-          plo[d] = lo;
+          if (sl.size() == 1) {  // bits of one value (through EXTRACTs and CONCATs of its slices)
+            if (sl[0].lo == 0 && W == P.vwidth[sl[0].src]) {
+              alias_to(sl[0].src);
+              continue;
+            }
+            psrc[d] = sl[0].src;
+            plo[d] = sl[0].lo;
+          } else {
+            psrc[d] = ra;
+            plo[d] = in.p0;
+            if (sl.size() <= kMaxSegs) segs[d] = std::move(sl);
+          }
           break;
         }
         case K_CONCAT: {
@@ -1303,6 +1346,26 @@ struct Analysis {
               r = vfull(W);
               break;
             }
+          }
+          {  // a chain of concatenated slices (e.g. a word rebuilt byte by byte from another word,
+             // Concat(x, Extract(255, 248, y), ..., Extract(7, 0, y))): merged segments; when they are
+             // two whole values the chain is one CONCAT of them
+            std::vector<Seg> sg = segs_of(in.b);
+            for (const Seg& x : segs_of(in.a)) seg_push(sg, x);
+            auto whole = [&](const Seg& x) { return x.lo == 0 && x.w == P.vwidth[x.src]; };
+            if (sg.size() == 1) {
+              if (whole(sg[0])) {
+                alias_to(sg[0].src);
+                continue;
+              }
+              psrc[d] = sg[0].src;
+              plo[d] = sg[0].lo;
+              r = vfull(W);
+              break;
+            }
+            if (sg.size() == 2 && whole(sg[0]) && whole(sg[1]) && (sg[0].src != res(in.b) || sg[1].src != res(in.a)))
+              rewrite[k] = Instr{K_CONCAT, W, d, sg[1].src, sg[0].src, MG_NONE, 0, sg[0].w};
+            if (sg.size() <= kMaxSegs) segs[d] = std::move(sg);
           }
           const Val &a = V(in.a), &b = V(in.b);
           const uint32_t wb = in.p1;
@@ -1327,6 +1390,10 @@ struct Analysis {
         case K_AND:
         case K_OR:
         case K_XOR: {
+          if (in.op != K_XOR && res(in.a) == res(in.b)) {  // x & x = x | x = x
+            alias_to(in.a);
+            continue;
+          }
           const int fa = F(in.a), fb = F(in.b);
           if (W == 1) {
             if (in.op == K_AND) {
