@@ -782,18 +782,21 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  const uint64_t ngroups = (end - a0 + 63ull) >> 6;\n"
        "  const uint64_t gstride = (uint64_t)nblk * 4u;  // 4 waves per 256-lane block\n"
        "  uint64_t wave_best = ~0ull, wave_hits = 0;  // per-wave, wave-uniform\n"
-       "  for (uint64_t g = (uint64_t)bid * 4u + (tid >> 6); g < ngroups; g += gstride) {\n"
-       "  const uint64_t gb = a0 + (g << 6);\n"
-       "  const uint64_t gbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32)) << 32) | "
-       "(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)gb);\n"
+       "  // the wave's index in its block through readfirstlane: the group loop, its bookkeeping and\n"
+       "  // wave_best / wave_hits are then scalar (from tid >> 6 they looked per-lane: a divergent loop\n"
+       "  // with 64-bit VALU counters and exec-mask exits)\n"
+       "  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);\n"
+       "  for (uint64_t g = (uint64_t)bid * 4u + wv; g < ngroups; g += gstride) {\n"
+       "  const uint64_t gbase = a0 + (g << 6);\n"
        "  if (early) {\n"
        "    const unsigned long long cur = __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
        "    const uint64_t cu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) | "
        "(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cur);\n"
        "    if (gbase >= cu) break;\n"
        "  }\n"
-       "  const uint64_t idx = gbase + lane;\n"
-       "  const bool active = idx >= start && idx < end;\n"
+       "  // a group wholly inside [start, end) (every group of a call but its first and last) needs no\n"
+       "  // per-lane bounds\n"
+       "  const bool full = gbase >= start && end > gbase && end - gbase >= 64u;\n"
        "  GKeys ky;\n"
        "  { const uint64_t G = fmix64((gbase >> 6) ^ sg), K = G ^ LK;\n"
        "    ky.klo = (uint32_t)K; ky.khi = (uint32_t)(K >> 32); ky.glo = (uint32_t)G; ky.ghi = (uint32_t)(G >> 32); }\n"
@@ -801,8 +804,8 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   g.decls();
   g.body(true);
   o << "  mg_next:\n"
-       "  verdict = active ? verdict : 0u;\n"
-       "  { const unsigned long long m = __ballot(verdict != 0u);\n"
+       "  { unsigned long long m = __ballot(verdict != 0u);\n"
+       "    if (!full) { const uint64_t idx = gbase + lane; m &= __ballot(idx >= start && idx < end); }\n"
        "    if (m) {\n"
        "      const uint64_t first = gbase + (uint64_t)(__ffsll((long long)m) - 1);\n"
        "      wave_hits += (uint64_t)__popcll(m);\n"
@@ -830,10 +833,9 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   o << "  const uint64_t a0 = start & ~63ull, end = start + count;\n"
        "  const uint64_t ngroups = (end - a0 + 63ull) >> 6;\n"
        "  const uint64_t gstride = (uint64_t)nblk * 4u;\n"
-       "  for (uint64_t g = (uint64_t)bid * 4u + (tid >> 6); g < ngroups; g += gstride) {\n"
-       "  const uint64_t gb = a0 + (g << 6);\n"
-       "  const uint64_t gbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(gb >> 32)) << 32) | "
-       "(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)gb);\n"
+       "  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);\n"
+       "  for (uint64_t g = (uint64_t)bid * 4u + wv; g < ngroups; g += gstride) {\n"
+       "  const uint64_t gbase = a0 + (g << 6);\n"
        "  const uint64_t idx = gbase + lane;\n"
        "  const bool active = idx >= start && idx < end;\n"
        "  GKeys ky;\n"
