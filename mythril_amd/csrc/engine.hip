@@ -2190,6 +2190,8 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
   DevProgram* p = find_prog(e, j.prog);
   auto git = e.gens.find(j.gen);
   if (!p || git == e.gens.end() || !j.fsearch) return set_err(MG_E_INVALID, "jit was not compiled for search");
+  // the search kernel counts each wave's groups in 32 bits (jit.cpp): at most 2^52 candidates per call
+  if (count > (1ull << 52)) return set_err(MG_E_INVALID, "mg_jit_search: more than 2^52 candidates in one call");
   uint64_t sk = seed_lane_key(seed), sg = seed_group_key(seed);
   unsigned long long res[2] = {~0ull, 0ull};
   if (split_over_devices(count)) {  // as mg_search: one group-aligned slice per device, host min/sum

@@ -163,6 +163,69 @@ struct Gen {
   // as gen_coord in engine.hip and gen_value in oracle/bveval.c).  Writes L limbs into
   // `out`_j.  A MIXED coordinate's alternative comes from the group key (SGPRs), so the
   // alternatives are scalar branches: a lane computes only the one its wave chose.
+  // Lane-parallel group keys (MYTHGPU_JIT_LANE_KEYS, default on).  Per group of 64 candidates the
+  // scalar unit would hash the group key G (fmix64: ~20 SALU) and every MIXED coordinate's choice
+  // word ws (3 SALU each); with four SIMDs sharing the CU's scalar unit, small query kernels (C1,
+  // C3) are scalar-bound.  Instead lane l of a wave hashes G of the wave's (k + l)-th group once
+  // per 64 groups (VALU), and per group lane j computes ws of the j-th MIXED coordinate (3 VALU for
+  // all of them); G and each ws are then one v_readlane each.  Same values as gen_keys / gwsel.
+  std::map<uint32_t, uint32_t> ws_slot;  // MIXED coordinate -> lane of wsv holding its ws
+  static bool lane_keys() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_LANE_KEYS");
+      return !(g && g[0] == '0');
+    }();
+    return on;
+  }
+  void plan_ws_slots() {
+    ws_slot.clear();
+    if (!specs || !lane_keys()) return;
+    for (uint32_t c = 0; c < specs->size() && ws_slot.size() < 64; c++)
+      if (((*specs)[c].kind & 0xFFu) == MG_GEN_MIXED && !coord_dead(c)) ws_slot[c] = (uint32_t)ws_slot.size();
+  }
+  // a coordinate no search can read: LAZY, or neither read by the program nor a COPY source of one
+  std::vector<char> reach;
+  bool coord_dead(uint32_t c) {
+    if (reach.empty()) {
+      reach.assign(specs->size(), 0);
+      std::vector<uint32_t> st;
+      for (const Instr& in : P.vcode)
+        if (in.op == K_COORD && in.p0 < reach.size() && !reach[in.p0]) { reach[in.p0] = 1; st.push_back(in.p0); }
+      while (!st.empty()) {
+        const uint32_t x = st.back();
+        st.pop_back();
+        const GenSpec& sp = (*specs)[x];
+        if ((sp.kind & 0xFFu) == MG_GEN_MIXED && sp.p[3] != MG_NONE && (sp.p[2] & 0xFFFFu) && !reach[sp.p[3]]) {
+          reach[sp.p[3]] = 1;
+          st.push_back(sp.p[3]);
+        }
+      }
+    }
+    return !reach[c];
+  }
+  // kernel prologue: the per-lane salt of the choice word (lane j: coordinate of slot j)
+  void emit_ws_salt() {
+    if (ws_slot.empty()) return;
+    std::vector<uint32_t> salt(ws_slot.size());
+    for (const auto& kv : ws_slot) salt[kv.second] = kv.first * 0x9E3779B9u + 0xFFFEu * 0x85EBCA6Bu + 0x27D4EB2Fu;
+    std::string e = hex(salt.back());
+    for (int32_t j = (int32_t)salt.size() - 2; j >= 0; j--) e = "(lane == " + std::to_string(j) + "u ? " + hex(salt[j]) + " : " + e + ")";
+    o << "  const uint32_t wsalt = " << e << ";\n"
+         "  uint32_t gkv_lo = 0u, gkv_hi = 0u;  // lane l: the group key of the wave's group kk + l\n";
+  }
+  // group prologue: G for this group (from the lanes' cache, refilled every 64 groups) and wsv
+  void emit_group_keys(const char* kk, const char* g, const char* gstride) {
+    if (!lane_keys()) {
+      o << "  const uint64_t G = fmix64((gbase >> 6) ^ sg);\n";
+      return;
+    }
+    o << "  if ((" << kk << " & 63u) == 0u) { const uint64_t Gx = fmix64(((a0 >> 6) + " << g << " + (uint64_t)lane * "
+      << gstride << ") ^ sg); gkv_lo = (uint32_t)Gx; gkv_hi = (uint32_t)(Gx >> 32); }\n"
+         "  const uint64_t G = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)gkv_hi, (int)(" << kk << " & 63u)) << 32) | "
+         "(uint32_t)__builtin_amdgcn_readlane((int)gkv_lo, (int)(" << kk << " & 63u));\n";
+    if (!ws_slot.empty())
+      o << "  const uint32_t wsv = (((uint32_t)G ^ wsalt) * 0x9E3779B1u) + (uint32_t)(G >> 32);\n";
+  }
   std::map<uint32_t, std::string> coord_var;  // coordinate -> prefix of its generated (final) limbs
   int tmp_id = 0;
 
@@ -220,7 +283,13 @@ struct Gen {
         const bool narrow = width <= MG_GEN_NARROW_BITS;
         // the alternative is s = ws >> 16 (wave-uniform, SGPRs): s < T  <=>  ws < T << 16, so each
         // test is one scalar compare; h is hashed only in the branches that read it
-        o << "  const uint32_t ws = gwsel(ky, " << C << ");\n";
+        {
+          auto sl = ws_slot.find(c);
+          if (sl != ws_slot.end())  // the choice word computed lane-parallel for the group (lane_keys)
+            o << "  const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane((int)wsv, " << sl->second << ");\n";
+          else
+            o << "  const uint32_t ws = gwsel(ky, " << C << ");\n";
+        }
         const std::string hdecl = "const uint32_t h = grnd(ky, " + C + ", 0xFFFFu);";
         auto below = [&](uint32_t T) {
           return T >= 65536u ? std::string("true") : "ws < " + hex(T << 16);
@@ -754,6 +823,7 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   const bool want_search = kernels & JIT_SEARCH, want_eval = kernels & JIT_EVAL, want_gen = kernels & JIT_GEN;
   Gen g(P, specs, gconsts);
   g.plan_dict_lds();
+  g.plan_ws_slots();
   auto& o = g.o;
   // hipRTC compiles this with -nogpuinc -nogpulib: its own runtime header still supplies
   // __ballot/atomicMin/..., but no device library is linked (the kernels read work-item
@@ -785,9 +855,16 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  // the wave's index in its block through readfirstlane: the group loop, its bookkeeping and\n"
        "  // wave_best / wave_hits are then scalar (from tid >> 6 they looked per-lane: a divergent loop\n"
        "  // with 64-bit VALU counters and exec-mask exits)\n"
-       "  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);\n"
-       "  for (uint64_t g = (uint64_t)bid * 4u + wv; g < ngroups; g += gstride) {\n"
-       "  const uint64_t gbase = a0 + (g << 6);\n"
+       "  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);\n";
+  g.emit_ws_salt();
+  o << "  // this wave sweeps groups g0, g0 + gstride, ...: nk of them, counted in 32 bits (the engine\n"
+       "  // launches at most 2^52 candidates); the call's partial first / last group, as iteration numbers\n"
+       "  const uint64_t g0 = (uint64_t)bid * 4u + wv;\n"
+       "  const uint32_t nk = g0 < ngroups ? (uint32_t)((ngroups - 1u - g0) / gstride + 1u) : 0u;\n"
+       "  const uint32_t kpf = (g0 == 0u && (start & 63u)) ? 0u : 0xFFFFFFFFu;\n"
+       "  const uint32_t kpl = ((end & 63u) && nk && g0 + (uint64_t)(nk - 1u) * gstride == ngroups - 1u) ? nk - 1u : 0xFFFFFFFFu;\n"
+       "  uint64_t gbase = a0 + (g0 << 6);\n"
+       "  for (uint32_t kk = 0u; kk < nk; kk++, gbase += gstride << 6) {\n"
        "  if (early) {\n"
        "    const unsigned long long cur = __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
        "    const uint64_t cu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) | "
@@ -796,9 +873,10 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  }\n"
        "  // a group wholly inside [start, end) (every group of a call but its first and last) needs no\n"
        "  // per-lane bounds\n"
-       "  const bool full = gbase >= start && end > gbase && end - gbase >= 64u;\n"
-       "  GKeys ky;\n"
-       "  { const uint64_t G = fmix64((gbase >> 6) ^ sg), K = G ^ LK;\n"
+       "  const bool full = kk != kpf && kk != kpl;\n";
+  g.emit_group_keys("kk", "g0 + (uint64_t)kk * gstride", "gstride");
+  o << "  GKeys ky;\n"
+       "  { const uint64_t K = G ^ LK;\n"
        "    ky.klo = (uint32_t)K; ky.khi = (uint32_t)(K >> 32); ky.glo = (uint32_t)G; ky.ghi = (uint32_t)(G >> 32); }\n"
        "  uint32_t verdict = 1u;\n";
   g.decls();
@@ -833,13 +911,16 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   o << "  const uint64_t a0 = start & ~63ull, end = start + count;\n"
        "  const uint64_t ngroups = (end - a0 + 63ull) >> 6;\n"
        "  const uint64_t gstride = (uint64_t)nblk * 4u;\n"
-       "  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);\n"
-       "  for (uint64_t g = (uint64_t)bid * 4u + wv; g < ngroups; g += gstride) {\n"
+       "  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);\n";
+  g.emit_ws_salt();
+  o << "  uint32_t kk = 0u;\n"
+       "  for (uint64_t g = (uint64_t)bid * 4u + wv; g < ngroups; g += gstride, kk++) {\n"
        "  const uint64_t gbase = a0 + (g << 6);\n"
        "  const uint64_t idx = gbase + lane;\n"
-       "  const bool active = idx >= start && idx < end;\n"
-       "  GKeys ky;\n"
-       "  { const uint64_t G = fmix64((gbase >> 6) ^ sg), K = G ^ LK;\n"
+       "  const bool active = idx >= start && idx < end;\n";
+  g.emit_group_keys("kk", "g", "gstride");
+  o << "  GKeys ky;\n"
+       "  { const uint64_t K = G ^ LK;\n"
        "    ky.klo = (uint32_t)K; ky.khi = (uint32_t)(K >> 32); ky.glo = (uint32_t)G; ky.ghi = (uint32_t)(G >> 32); }\n"
        "  uint32_t verdict = 1u;\n";
   g.decls();
