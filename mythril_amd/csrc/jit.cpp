@@ -205,13 +205,14 @@ struct Gen {
   }
   // kernel prologue: the per-lane salt of the choice word (lane j: coordinate of slot j)
   void emit_ws_salt() {
+    if (!lane_keys()) return;
+    o << "  uint32_t gkv_lo = 0u, gkv_hi = 0u;  // lane l: the group key of the wave's group kk + l\n";
     if (ws_slot.empty()) return;
     std::vector<uint32_t> salt(ws_slot.size());
     for (const auto& kv : ws_slot) salt[kv.second] = kv.first * 0x9E3779B9u + 0xFFFEu * 0x85EBCA6Bu + 0x27D4EB2Fu;
     std::string e = hex(salt.back());
     for (int32_t j = (int32_t)salt.size() - 2; j >= 0; j--) e = "(lane == " + std::to_string(j) + "u ? " + hex(salt[j]) + " : " + e + ")";
-    o << "  const uint32_t wsalt = " << e << ";\n"
-         "  uint32_t gkv_lo = 0u, gkv_hi = 0u;  // lane l: the group key of the wave's group kk + l\n";
+    o << "  const uint32_t wsalt = " << e << ";\n";
   }
   // group prologue: G for this group (from the lanes' cache, refilled every 64 groups) and wsv
   void emit_group_keys(const char* kk, const char* g, const char* gstride) {

@@ -75,3 +75,25 @@ def test_specialisation_folds_actor_membership():
 
     assert sender_eqs(native.specialized_program(P.to_bytes(), None)) >= 6  # 3 actors x 2 transactions
     assert sender_eqs(native.specialized_program(P.to_bytes(), blob)) == 0
+
+
+def _tiny_queries():
+    from mythril_amd.smt import ULT, symbol_factory
+
+    x = symbol_factory.BitVecSym("tiny_x", 8)
+    y = symbol_factory.BitVecSym("tiny_y", 256)
+    return {
+        "one_narrow_constraint": [(x == symbol_factory.BitVecVal(5, 8)).raw],
+        "one_wide_compare": [ULT(y, symbol_factory.BitVecVal(1000, 256)).raw],
+    }
+
+
+@pytest.mark.parametrize("name", sorted(workloads.WORKLOADS) + sorted(_tiny_queries()))
+def test_jit_kernels_compile_on_host(name):
+    """Every kernel the JIT emits for a query compiles for gfx950 on the host (comgr in the
+    helper process, no GPU): the search kernel of each workload, and of queries with no MIXED
+    coordinate (no choice words), whose emission paths differ."""
+    roots = _tiny_queries()[name] if name in _tiny_queries() else [c.raw for c in workloads.WORKLOADS[name]()]
+    P, blob = search.prepare(roots)
+    src = native.jit_source(P.to_bytes(), blob, compile=True)
+    assert "mgj_search" in src
