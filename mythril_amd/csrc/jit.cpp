@@ -163,7 +163,8 @@ struct Gen {
   // as gen_coord in engine.hip and gen_value in oracle/bveval.c).  Writes L limbs into
   // `out`_j.  A MIXED coordinate's alternative comes from the group key (SGPRs), so the
   // alternatives are scalar branches: a lane computes only the one its wave chose.
-  // Lane-parallel group keys (MYTHGPU_JIT_LANE_KEYS, default on).  Per group of 64 candidates the
+  // Lane-parallel group keys (MYTHGPU_JIT_LANE_KEYS=1; off by default: measured C1 -1 %, C2 -6 %,
+  // C3 +1.7 %, C4 +0.6 %, profiles/r03_ab_lanekeys.jsonl — the scalar unit was not what bounds C1/C3).  Per group of 64 candidates the
   // scalar unit would hash the group key G (fmix64: ~20 SALU) and every MIXED coordinate's choice
   // word ws (3 SALU each); with four SIMDs sharing the CU's scalar unit, small query kernels (C1,
   // C3) are scalar-bound.  Instead lane l of a wave hashes G of the wave's (k + l)-th group once
@@ -173,7 +174,7 @@ struct Gen {
   static bool lane_keys() {
     static const bool on = [] {
       const char* g = getenv("MYTHGPU_JIT_LANE_KEYS");
-      return !(g && g[0] == '0');
+      return g && g[0] == '1';
     }();
     return on;
   }
