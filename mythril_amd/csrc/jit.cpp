@@ -74,6 +74,7 @@ struct Gen {
   // LDS serves it at twice the bandwidth and nothing else in the kernel uses LDS.  Limbs that
   // are the same in every entry are literals and are not read at all.
   std::map<uint32_t, uint32_t> dict_lds;  // gconsts offset of a table -> LDS word offset
+  std::map<uint32_t, uint32_t> dict_n;    // gconsts offset of a table -> entries
   uint32_t lds_words = 0;
   static constexpr uint32_t kDictLdsWords = 4096;  // 16 KiB per 256-lane block
   // dictionaries up to this many entries are selects, not gathers (MYTHGPU_JIT_SELECT_DICT, default 4)
@@ -87,6 +88,7 @@ struct Gen {
 
   void plan_dict_lds() {
     dict_lds.clear();
+    dict_n.clear();
     lds_words = 0;
     static const bool on = [] {
       const char* g = getenv("MYTHGPU_JIT_DICT_LDS");
@@ -100,10 +102,11 @@ struct Gen {
       const bool dict = kind == MG_GEN_DICT || (kind == MG_GEN_MIXED && n && (sp.p[2] >> 16));
       if (!dict || n == 0 || c >= P.coord_width.size()) continue;
       const uint32_t w = P.coord_width[c], L = Lw(w);
-      if (!packed_dict(off, n, w, "e").empty() || dict_lds.count(off)) continue;
+      if (!packed_dict(off, n, w, "e").empty() || dict_lds.count(off) || n <= select_dict_max()) continue;
       const uint32_t need = (n * L + 3u) & ~3u;  // 16-B aligned tables (ds_read_b128)
       if (lds_words + need > kDictLdsWords) continue;
       dict_lds[off] = lds_words;
+      dict_n[off] = n;
       lds_words += need;
     }
   }
@@ -121,9 +124,13 @@ struct Gen {
       if (!(kind == MG_GEN_DICT || kind == MG_GEN_MIXED)) continue;
       len[sp.p[0]] = std::max(len[sp.p[0]], sp.p[1] * Lw(P.coord_width[c]));
     }
-    for (const auto& kv : len)
+    // limb-major ([limb][entry]): lanes that drew different entries read different banks (entry-major,
+    // a 256-bit table put every lane's limb j in one of 4 banks: 16-way conflicts)
+    for (const auto& kv : len) {
+      const uint32_t n = dict_n.at(kv.first), L = kv.second / std::max(n, 1u);
       o << "  for (uint32_t i = tid; i < " << kv.second << "u; i += 256u) mg_dict[" << dict_lds.at(kv.first)
-        << "u + i] = gconsts[" << kv.first << "u + i];\n";
+        << "u + (i % " << L << "u) * " << n << "u + i / " << L << "u] = gconsts[" << kv.first << "u + i];\n";
+    }
     o << "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"workgroup\");\n"
          "  __builtin_amdgcn_s_barrier();\n"
          "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"workgroup\");\n";
@@ -153,7 +160,7 @@ struct Gen {
         v = hex(G[off + (n - 1) * L + j]);
         for (int32_t e = (int32_t)n - 2; e >= 0; e--)
           v = "(" + idx + " == " + std::to_string(e) + "u ? " + hex(G[off + e * L + j]) + " : " + v + ")";
-      } else if (lds != dict_lds.end()) v = "mg_dict[" + std::to_string(lds->second + j) + "u + " + idx + " * " + std::to_string(L) + "u]";
+      } else if (lds != dict_lds.end()) v = "mg_dict[" + std::to_string(lds->second + j * n) + "u + " + idx + "]";
       else v = "gconsts[" + std::to_string(off + j) + "u + " + idx + " * " + std::to_string(L) + "u]";
       o << ind << lim(j) << " = " << v << ";\n";
     }
@@ -779,9 +786,28 @@ struct Gen {
   }
 
   void decls() {
-    // declare every limb of every value up front (gotos may jump over the body)
+    // declare every limb of every value the code defines or reads, up front (gotos may jump over
+    // the body).  Only those: the value ids are the unspecialised program's, and declaring all of
+    // them (C2: 4,385 limbs for 287 used) was a large share of the compiler's front-end time.
+    std::vector<char> used(P.vwidth.size(), 0);
+    auto mark = [&](uint32_t id) {
+      if (id != MG_NONE && id < used.size()) used[id] = 1;
+    };
+    for (const Instr& in : P.vcode) {
+      mark(in.dst);
+      if (in.op == K_CONST || in.op == K_COORD) continue;
+      mark(in.a);
+      if (in.op == K_LOOKUP) {
+        mark(in.p0);
+        for (uint32_t q = 0; q < 2 * in.c; q++) mark(P.vaux[in.p1 + q]);
+        continue;
+      }
+      mark(in.b);
+      mark(in.c);
+    }
     size_t n = 0;
     for (uint32_t id = 0; id < P.vwidth.size(); id++) {
+      if (!used[id]) continue;
       for (uint32_t j = 0; j < Lw(P.vwidth[id]); j++) {
         o << (n % 16 == 0 ? "  uint32_t " : ", ") << v(id, j);
         if (n % 16 == 15) o << ";\n";

@@ -429,8 +429,11 @@ def model_from_assignment(P: ssa.Program, assign: np.ndarray):
 # ~0.2 s on the MI355X box's host through hipRTC, less through comgr)
 JIT_COMPILE_S = [0.15]
 # while a compile is pending, interpreter launches are cut to about this long so the search
-# switches to the compiled kernel soon after it is ready
+# switches to the compiled kernel soon after it is ready; in the first few ms after the submit they
+# are cut to JIT_FIRST_POLL_S, so a kernel the engine already holds (same source: LASER re-asks
+# constraint sets) is picked up at once instead of after a full 10 ms interpreter launch
 JIT_POLL_S = 0.010
+JIT_FIRST_POLL_S = 0.001
 # kernel that produced the last search's result ("interp" / "jit") and that result, for
 # stream statistics (tools/stream_bench.py)
 LAST_ENGINE = None
@@ -507,7 +510,9 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                     ticket = engine.jit_compile_async(prog, gh)
                 n = min(chunk, max_candidates - scanned)
                 if rate:
-                    cap_s = min(left, JIT_POLL_S) if ticket is not None else left
+                    cap_s = left
+                    if ticket is not None:
+                        cap_s = min(left, JIT_FIRST_POLL_S if now - tc < 5 * JIT_FIRST_POLL_S else JIT_POLL_S)
                     if max_launch_s is not None:
                         cap_s = min(cap_s, max_launch_s)
                     n = max(1, min(n, int(rate * cap_s)))
