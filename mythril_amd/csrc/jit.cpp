@@ -90,9 +90,11 @@ struct Gen {
     dict_lds.clear();
     dict_n.clear();
     lds_words = 0;
+    // on by default since the tables are limb-major (MYTHGPU_JIT_DICT_LDS=0: per-lane gathers from
+    // global memory): C1 +40 %, C2 +3.7 %, C4 +2.5 %, C3 -8 % (profiles/r03_ab_dict_lds.jsonl)
     static const bool on = [] {
       const char* g = getenv("MYTHGPU_JIT_DICT_LDS");
-      return g && g[0] == '1';
+      return !(g && g[0] == '0');
     }();
     if (!specs || !on) return;
     for (uint32_t c = 0; c < specs->size(); c++) {

@@ -839,6 +839,8 @@ struct Analysis {
   std::vector<Val> cval;          // per coordinate (search mode)
   std::vector<int32_t> defk;      // per id: index of its defining instruction (-1: none)
   std::map<size_t, Instr> rewrite;  // instruction index -> the instruction emitted instead
+  // LOOKUP instruction index -> (default, (key, value) pairs) after pruning
+  std::map<size_t, std::pair<uint32_t, std::vector<uint32_t>>> lookup_rw;
   std::map<std::vector<uint32_t>, uint32_t> lit_id;  // literal (limbs, width) -> its first value id
   // segs[id]: the value as slices of other values, low bits first (empty: see segs_of)
   struct Seg {
@@ -1181,6 +1183,28 @@ struct Analysis {
     }
   }
 
+  // x == y decided from the facts, looking through CONCATs of equal split (keys of 512 bits and
+  // more, e.g. Concat(address, slot) of a keccak site): -1 undecided, else 0 / 1
+  int decide_eq(uint32_t x, uint32_t y, uint32_t w, int depth = 0) const {
+    x = res(x);
+    y = res(y);
+    if (x == y) return 1;
+    if (w <= 256) {
+      const int v = decide(K_EQ, val[x], val[y], w);
+      if (v >= 0 || depth > 8) return v;
+    }
+    if (depth > 8) return -1;
+    const int32_t kx = defk[x], ky = defk[y];
+    if (kx < 0 || ky < 0) return -1;
+    const Instr &dx = P.vcode[kx], &dy = P.vcode[ky];
+    if (dx.op != K_CONCAT || dy.op != K_CONCAT || dx.p1 != dy.p1) return -1;
+    const int lo = decide_eq(dx.b, dy.b, dx.p1, depth + 1);
+    if (lo == 0) return 0;
+    const int hi = decide_eq(dx.a, dy.a, w - dx.p1, depth + 1);
+    if (hi == 0) return 0;
+    return lo == 1 && hi == 1 ? 1 : -1;
+  }
+
   int decide_mem(const Mem& m) const {
     if (!m.k) return -1;
     const Val& s = val[res(m.src)];
@@ -1207,6 +1231,7 @@ struct Analysis {
     skip.assign(P.vcode.size(), 0);
     defk.assign(nv, -1);
     rewrite.clear();
+    lookup_rw.clear();
     lit_id.clear();
     segs.assign(nv, {});
     for (size_t k = 0; k < P.vcode.size(); k++)
@@ -1578,7 +1603,7 @@ struct Analysis {
         case K_SLT:
         case K_SLE: {
           const Val &a = V(in.a), &b = V(in.b);
-          int v = decide(in.op, a, b, in.p1);
+          int v = in.op == K_EQ ? decide_eq(in.a, in.b, in.p1) : decide(in.op, a, b, in.p1);
           if (v < 0 && res(in.a) == res(in.b)) v = (in.op == K_ULT || in.op == K_SLT) ? 0 : 1;  // x op x
           if (v >= 0) {
             set_fold(v);
@@ -1607,11 +1632,31 @@ struct Analysis {
             alias_to(in.p0);
             continue;
           }
-          Val h = V(in.p0);
-          bool all_same = true;
+          // priors whose key can never equal this key are dropped; a prior whose key always
+          // equals it ends the list and becomes the default (first match wins)
+          std::vector<uint32_t> kept;  // (key, value) pairs
+          uint32_t dflt = in.p0;
           for (uint32_t p = 0; p < in.c; p++) {
-            const uint32_t vv = P.vaux[in.p1 + 2 * p + 1];
-            if (res(vv) != res(in.p0)) all_same = false;
+            const uint32_t kv = P.vaux[in.p1 + 2 * p], vv = P.vaux[in.p1 + 2 * p + 1];
+            const int e = decide_eq(in.a, kv, in.b);
+            if (e == 0) continue;
+            if (e == 1) {
+              dflt = vv;
+              break;
+            }
+            kept.push_back(kv);
+            kept.push_back(vv);
+          }
+          if (kept.empty()) {
+            alias_to(dflt);
+            continue;
+          }
+          if (kept.size() != 2u * in.c || dflt != in.p0) lookup_rw[k] = {dflt, kept};
+          Val h = V(dflt);
+          bool all_same = true;
+          for (size_t p = 0; p < kept.size(); p += 2) {
+            const uint32_t vv = kept[p + 1];
+            if (res(vv) != res(dflt)) all_same = false;
             const Val& x = V(vv);
             h.r = rhull(h.r, x.r);
             h.kb = kmeet(h.kb, x.kb);
@@ -1624,7 +1669,7 @@ struct Analysis {
             }
           }
           if (all_same) {  // every source is the same value
-            alias_to(in.p0);
+            alias_to(dflt);
             continue;
           }
           if (W <= 256) r = h;
@@ -1790,9 +1835,16 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
         v.b = c.b;  // key width
         v.c = c.c;  // number of priors
         v.p0 = R(c.p0);
-        for (uint32_t p = 0; p < c.c; p++) {
-          v.prior.push_back(R(in.vaux[c.p1 + 2 * p]));
-          v.prior.push_back(R(in.vaux[c.p1 + 2 * p + 1]));
+        auto lr = A.lookup_rw.find(k);
+        if (lr != A.lookup_rw.end()) {
+          v.p0 = R(lr->second.first);
+          v.c = (uint32_t)(lr->second.second.size() / 2);
+          for (uint32_t x : lr->second.second) v.prior.push_back(R(x));
+        } else {
+          for (uint32_t p = 0; p < c.c; p++) {
+            v.prior.push_back(R(in.vaux[c.p1 + 2 * p]));
+            v.prior.push_back(R(in.vaux[c.p1 + 2 * p + 1]));
+          }
         }
       } else if (c.op == K_CONST || c.op == K_COORD) {
         v.a = v.b = v.c = NONE;
