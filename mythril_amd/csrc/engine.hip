@@ -693,10 +693,23 @@ struct DevProgram {
   bool lds = false;
 };
 
-// host-side specialisations of one (program, generator) pair, shared through the cache
+struct Engine;
+static void pool_put(Engine& e, void* ptr, size_t cap);
+
+// specialisations of one (program, generator) pair, shared through the cache.  On the primary
+// device they stay uploaded with the cache entry (`dev`): LASER re-asks constraint sets, and a
+// repeat's mg_gen_load then makes no copy to the device (three synchronous copies, ~50 us, were
+// a quarter of a warm query's time to first model).  A generator loaded from the entry borrows
+// these buffers (DevGen::borrowed); they go back to the pool when the last holder lets go.
 struct SpecSet {
-  Lowered search, watch;
+  DevProgram search, watch;  // .low: the specialised programs
   std::shared_ptr<Lowered> model;  // watch list only, asserts dropped: built on the first hit
+  Engine* dev = nullptr;     // the device the buffers below live on (nullptr: not uploaded)
+  void* gbuf = nullptr;      // generator specs | constants
+  size_t gcap = 0;
+  GenSpec* d_specs = nullptr;
+  uint32_t* d_consts = nullptr;
+  ~SpecSet();
 };
 
 struct DevGen {
@@ -711,6 +724,7 @@ struct DevGen {
   DevProgram spec_watch;          // the same with the watch list (model read-back, mg_eval_generated)
   void* gbuf = nullptr;           // pooled buffer behind d_specs / d_consts
   size_t gcap = 0;
+  bool borrowed = false;          // spec / spec_watch / d_specs / d_consts are `set`'s (not freed here)
 };
 
 struct DevJit {
@@ -871,6 +885,25 @@ static void pool_put(Engine& e, void* ptr, size_t cap) {
   if (ptr) e.pool.emplace(cap, ptr);
 }
 
+SpecSet::~SpecSet() {
+  if (!dev) return;
+  pool_put(*dev, search.buf, search.cap);
+  pool_put(*dev, watch.buf, watch.cap);
+  pool_put(*dev, gbuf, gcap);
+}
+
+// a generator's own device buffers (a borrowed generator's belong to its cache entry)
+static void free_gen_buffers(Engine& e, DevGen& g) {
+  void free_code(Engine&, DevProgram&);
+  if (!g.borrowed) {
+    pool_put(e, g.gbuf, g.gcap);
+    free_code(e, g.spec);
+    free_code(e, g.spec_watch);
+  }
+  g.gbuf = nullptr;
+  free_code(e, g.spec_model);
+}
+
 // instructions, literals, lookup lists and coordinate widths in ONE pooled buffer, one copy
 static int upload_code(Engine& e, DevProgram& p) {
   p.lds = p.low.value_words <= kLdsWordsMax;
@@ -905,7 +938,7 @@ static int upload_code(Engine& e, DevProgram& p) {
   return MG_OK;
 }
 
-static void free_code(Engine& e, DevProgram& p) {
+void free_code(Engine& e, DevProgram& p) {
   pool_put(e, p.buf, p.cap);
   p.buf = nullptr;
   p.cap = 0;
@@ -1207,13 +1240,11 @@ static void free_dev_buffers(Engine& e) {
   e.jits.clear();
   for (auto& kv : e.progs) free_code(e, *kv.second);
   e.progs.clear();
-  for (auto& kv : e.gens) {
-    pool_put(e, kv.second->gbuf, kv.second->gcap);
-    free_code(e, kv.second->spec);
-    free_code(e, kv.second->spec_watch);
-    free_code(e, kv.second->spec_model);
-  }
+  for (auto& kv : e.gens) free_gen_buffers(e, *kv.second);
   e.gens.clear();
+  // the cache's resident specialisations return their buffers to the pool before it is freed
+  e.spec_cache.clear();
+  e.spec_order.clear();
   for (auto& kv : e.pool) (void)hipFree(kv.second);
   e.pool.clear();
   if (e.d_watch1) (void)hipFree(e.d_watch1);
@@ -1429,20 +1460,28 @@ int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* g
   gg->specs = specs;
   gg->consts = consts;
   const std::string key = p->src + std::string((const char*)blob, n_words * 4);
+  std::shared_ptr<SpecSet> sp;
   auto hit = e.spec_cache.find(key);
   if (hit != e.spec_cache.end()) {
-    gg->spec.low = hit->second->search;
-    gg->spec_watch.low = hit->second->watch;
-    gg->set = hit->second;
+    sp = hit->second;
   } else {
-    rc = specialize_program(p->low, &gg->specs, &gg->consts, gg->spec.low, err, /*keep_watch=*/false);
+    sp = std::make_shared<SpecSet>();
+    rc = specialize_program(p->low, &gg->specs, &gg->consts, sp->search.low, err, /*keep_watch=*/false);
     if (rc) return set_err(rc, err);
-    rc = specialize_program(p->low, &gg->specs, &gg->consts, gg->spec_watch.low, err, /*keep_watch=*/true);
+    rc = specialize_program(p->low, &gg->specs, &gg->consts, sp->watch.low, err, /*keep_watch=*/true);
     if (rc) return set_err(rc, err);
-    auto sp = std::make_shared<SpecSet>();
-    sp->search = gg->spec.low;
-    sp->watch = gg->spec_watch.low;
-    gg->set = sp;
+  }
+  if (!sp->dev) {  // upload once: code of both variants, then specs | constants
+    if ((rc = upload_code(e, sp->search))) return rc;
+    if ((rc = upload_code(e, sp->watch))) return rc;
+    if ((rc = upload_gen_consts(e, *gg))) return rc;
+    sp->gbuf = gg->gbuf;
+    sp->gcap = gg->gcap;
+    sp->d_specs = gg->d_specs;
+    sp->d_consts = gg->d_consts;
+    sp->dev = &e;
+  }
+  if (hit == e.spec_cache.end()) {
     e.spec_cache[key] = sp;
     e.spec_order.push_back(key);
     if (e.spec_order.size() > e.cache_cap) {
@@ -1450,9 +1489,14 @@ int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* g
       e.spec_order.pop_front();
     }
   }
-  if ((rc = upload_code(e, gg->spec))) return rc;
-  if ((rc = upload_code(e, gg->spec_watch))) return rc;
-  if ((rc = upload_gen_consts(e, *gg))) return rc;
+  gg->set = sp;
+  gg->spec = sp->search;
+  gg->spec_watch = sp->watch;
+  gg->gbuf = nullptr;
+  gg->gcap = 0;
+  gg->d_specs = sp->d_specs;
+  gg->d_consts = sp->d_consts;
+  gg->borrowed = true;
   const uint64_t h = e.next_handle++;
   for (size_t i = 1; i < g_devs.size(); i++) {  // mirrored, uploaded on first use there
     auto q = std::make_unique<DevGen>();
@@ -1477,17 +1521,11 @@ int mg_gen_free(uint64_t gen) {
     Engine& d = *g_devs[i];
     auto q = d.gens.find(gen);
     if (q == d.gens.end()) continue;
-    pool_put(d, q->second->gbuf, q->second->gcap);
-    free_code(d, q->second->spec);
-    free_code(d, q->second->spec_watch);
-    free_code(d, q->second->spec_model);
+    free_gen_buffers(d, *q->second);
     d.gens.erase(q);
   }
   if (g_devs.empty()) {
-    pool_put(e, it->second->gbuf, it->second->gcap);
-    free_code(e, it->second->spec);
-    free_code(e, it->second->spec_watch);
-    free_code(e, it->second->spec_model);
+    free_gen_buffers(e, *it->second);
     e.gens.erase(it);
   }
   return MG_OK;

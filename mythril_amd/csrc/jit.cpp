@@ -97,12 +97,24 @@ struct Gen {
       return !(g && g[0] == '0');
     }();
     if (!specs || !on) return;
+    // only when several coordinates gather from tables: with one or two (C3) the per-block staging
+    // and the LDS reads cost more than the gathers they replace (C3 -8 %, profiles/r03_ab_dict_lds.jsonl)
+    uint32_t gathering = 0;
+    for (uint32_t c = 0; c < specs->size(); c++) {
+      const GenSpec& sp = (*specs)[c];
+      const uint32_t kind = sp.kind & 0xFFu, n = sp.p[1];
+      const bool dict = kind == MG_GEN_DICT || (kind == MG_GEN_MIXED && n && (sp.p[2] >> 16));
+      if (dict && c < P.coord_width.size() && n > select_dict_max() && !coord_dead(c) &&
+          packed_dict(sp.p[0], n, P.coord_width[c], "e").empty())
+        gathering++;
+    }
+    if (gathering < 3) return;
     for (uint32_t c = 0; c < specs->size(); c++) {
       const GenSpec& sp = (*specs)[c];
       const uint32_t kind = sp.kind & 0xFFu;
       const uint32_t n = sp.p[1], off = sp.p[0];
       const bool dict = kind == MG_GEN_DICT || (kind == MG_GEN_MIXED && n && (sp.p[2] >> 16));
-      if (!dict || n == 0 || c >= P.coord_width.size()) continue;
+      if (!dict || n == 0 || c >= P.coord_width.size() || coord_dead(c)) continue;
       const uint32_t w = P.coord_width[c], L = Lw(w);
       if (!packed_dict(off, n, w, "e").empty() || dict_lds.count(off) || n <= select_dict_max()) continue;
       const uint32_t need = (n * L + 3u) & ~3u;  // 16-B aligned tables (ds_read_b128)
