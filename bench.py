@@ -251,6 +251,7 @@ def main():
             hard["candidates"] = rh.scanned
             if label == "cold":
                 hard["jit_compile_ms"] = rh.timing.get("jit_compile_ms")
+            hard[f"{label}_timing"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in rh.timing.items()}
         hard["needle"] = "Extract(23, 0, x * K) == C on a fresh 256-bit symbol x (~2^-24 per candidate)"
 
     # time to first model on ALL ranks: the compiled kernel sweeps epochs of `chunk` candidates per

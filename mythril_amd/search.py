@@ -503,6 +503,8 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                         ticket, jh, used, rate = None, h, "jit", None
                         took = now - tc
                         timing["jit_compile_ms"] = took * 1e3
+                        timing["jit_switch_ms"] = (now - t0) * 1e3  # when the search moved to the kernel
+                        timing["interp_candidates"] = scanned
                         JIT_COMPILE_S[0] = 0.5 * JIT_COMPILE_S[0] + 0.5 * took
                         chunk = max(chunk, 1 << 22)
                 if jh is None and ticket is None and jit == "auto" and scanned > 0 and left > 1.2 * expected_compile:
