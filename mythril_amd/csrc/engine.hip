@@ -75,7 +75,10 @@ struct KArgs {
   uint64_t sk, sg;           // GEN3 seed keys (seed_lane_key / seed_group_key of seed)
   uint32_t n_instr, value_words, flags;
   uint32_t watch_words;      // SEARCH with `watch`: rows per block of the capture buffer (see K_WATCH)
+  uint32_t n_specs;          // generator specs (coordinates): the prologue's scalar-cache warm-up
 };
+
+constexpr uint32_t kFlagPrefetch = 1u << 16;  // KArgs::flags: warm the scalar cache first (launch_async)
 
 // uniform struct reads through the constant address space (scalar loads)
 __device__ __forceinline__ GenSpec ld_spec(const KArgs& k, uint32_t c) {
@@ -598,6 +601,26 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
   // idx & 63 == threadIdx.x & 63 below (a0 and base are multiples of 64): the lane half of
   // the GEN3 lane key is fixed per thread
   const uint64_t lk = (MODE == MODE_EVAL) ? 0ull : gen_lane_key(threadIdx.x & 63u, k.sk);
+  // Warm the scalar cache with the program and the generator specs, 64-byte lines eight loads at a
+  // time: a wave reads them with dependent scalar loads, one instruction (32 B) or spec ahead, so a
+  // cold cache costs it an L2 round trip every other instruction — the floor of an easy query's time
+  // to first model, which one wave's pass over the program is.
+  if (k.flags & kFlagPrefetch) {
+    uint32_t acc = 0;
+    auto warm = [&acc](const uint32_t* base, uint32_t lines) {
+      const auto* b = cst(base);
+      for (uint32_t l = 0; l < lines; l += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) x[q] = (l + q < lines) ? b[16u * (l + q)] : 0u;
+#pragma unroll
+        for (int q = 0; q < 8; q++) acc ^= x[q];
+      }
+    };
+    warm((const uint32_t*)k.code, min((k.n_instr + 2u) / 2u, 512u));
+    if (MODE != MODE_EVAL && k.specs) warm((const uint32_t*)k.specs, min((k.n_specs + 1u) / 2u, 512u));
+    if (acc == 0x5EED1E55u && k.count == ~0ull) k.hits[0] = acc;  // never true: keeps the loads
+  }
   for (uint64_t base = (uint64_t)blockIdx.x * kWave; base < total; base += step) {
     const uint64_t off = base + threadIdx.x;
     const uint64_t idx = a0 + off;  // candidate index (GEN / SEARCH)
@@ -1001,6 +1024,13 @@ static int launch_async(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   k.count = count;
   k.n_instr = (uint32_t)p.low.code.size();
   k.value_words = p.low.value_words;
+  k.n_specs = p.low.n_coords;
+  // MYTHGPU_INTERP_PREFETCH=0: no scalar-cache warm-up in the prologue
+  static const bool prefetch = [] {
+    const char* g = getenv("MYTHGPU_INTERP_PREFETCH");
+    return !(g && g[0] == '0');
+  }();
+  if (prefetch) k.flags |= kFlagPrefetch;
   k.stride = (uint64_t)grid * kWave;
   if (!p.lds) {
     const size_t need = (size_t)p.low.value_words * k.stride * 4;

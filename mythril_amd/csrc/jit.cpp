@@ -889,6 +889,11 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  const uint64_t LK = fmix64((uint64_t)lane ^ sk);  // lane half of the lane key (GEN3)\n"
        ;
   g.emit_dict_prologue();
+  o << "  __shared__ unsigned long long mg_blk[2];  // the block's first hit and hit count\n"
+       "  if (tid == 0u) { mg_blk[0] = ~0ull; mg_blk[1] = 0ull; }\n"
+       "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"workgroup\");\n"
+       "  __builtin_amdgcn_s_barrier();\n"
+       "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"workgroup\");\n";
   o << "  // one aligned group of 64 candidate indices per wave (GEN3 group key, mythgpu.h)\n"
        "  const uint64_t a0 = start & ~63ull, end = start + count;\n"
        "  const uint64_t ngroups = (end - a0 + 63ull) >> 6;\n"
@@ -902,7 +907,10 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   o << "  // this wave sweeps groups g0, g0 + gstride, ...: nk of them, counted in 32 bits (the engine\n"
        "  // launches at most 2^52 candidates); the call's partial first / last group, as iteration numbers\n"
        "  const uint64_t g0 = (uint64_t)bid * 4u + wv;\n"
-       "  const uint32_t nk = g0 < ngroups ? (uint32_t)((ngroups - 1u - g0) / gstride + 1u) : 0u;\n"
+       "  // (32-bit division when the operands fit: a 64-bit one is a long call per wave)\n"
+       "  const uint64_t gleft = g0 < ngroups ? ngroups - 1u - g0 : 0u;\n"
+       "  const uint32_t nk = g0 >= ngroups ? 0u : ((gleft >> 32) == 0u && (gstride >> 32) == 0u)\n"
+       "      ? (uint32_t)gleft / (uint32_t)gstride + 1u : (uint32_t)(gleft / gstride + 1u);\n"
        "  const uint32_t kpf = (g0 == 0u && (start & 63u)) ? 0u : 0xFFFFFFFFu;\n"
        "  const uint32_t kpl = ((end & 63u) && nk && g0 + (uint64_t)(nk - 1u) * gstride == ngroups - 1u) ? nk - 1u : 0xFFFFFFFFu;\n"
        "  uint64_t gbase = a0 + (g0 << 6);\n"
@@ -936,9 +944,20 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "      }\n"
        "    } }\n"
        "  }\n"
+       "  // the block's four waves combine in LDS, then one thread publishes: the end-of-wave global\n"
+       "  // atomics on one address from every wave serialised in the launch's tail; a first hit that\n"
+       "  // cannot lower the current minimum is not published at all\n"
        "  if (lane == 0u) {\n"
-       "    if (wave_best != ~0ull) atomicMin(hit, (unsigned long long)wave_best);\n"
-       "    if (wave_hits) atomicAdd(hit + 1, (unsigned long long)wave_hits);\n"
+       "    if (wave_best != ~0ull) __hip_atomic_fetch_min(&mg_blk[0], (unsigned long long)wave_best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
+       "    if (wave_hits) __hip_atomic_fetch_add(&mg_blk[1], (unsigned long long)wave_hits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
+       "  }\n"
+       "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"workgroup\");\n"
+       "  __builtin_amdgcn_s_barrier();\n"
+       "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"workgroup\");\n"
+       "  if (tid == 0u) {\n"
+       "    const unsigned long long bb = mg_blk[0], bh = mg_blk[1];\n"
+       "    if (bb != ~0ull && bb < __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(hit, bb);\n"
+       "    if (bh) atomicAdd(hit + 1, bh);\n"
        "  }\n}\n\n";
   }
   if (want_gen) {
