@@ -750,14 +750,32 @@ struct DevGen {
   bool borrowed = false;          // spec / spec_watch / d_specs / d_consts are `set`'s (not freed here)
 };
 
+// a loaded JIT module shared by the code cache and the kernels handed out from it: unloaded
+// when the last holder lets go
+struct ModHold {
+  hipModule_t mod = nullptr;
+  explicit ModHold(hipModule_t m) : mod(m) {}
+  ~ModHold() {
+    if (mod) (void)hipModuleUnload(mod);
+  }
+};
+
 struct DevJit {
   std::vector<char> code;  // the code object (loaded again on the node's other devices)
   hipModule_t mod = nullptr;
+  std::shared_ptr<ModHold> hold;  // set: `mod` belongs to it (primary device, code cache)
   hipFunction_t fsearch = nullptr, feval = nullptr, fgen = nullptr;
   uint64_t prog = 0, gen = 0;
   int nb_search = 1, nb_eval = 1;
   double compile_ms = 0;
 };
+
+// unload (or let go of) a JIT kernel's module
+static void release_jit(DevJit& j) {
+  if (j.hold) j.hold.reset();
+  else if (j.mod) (void)hipModuleUnload(j.mod);
+  j.mod = nullptr;
+}
 
 // compiled code objects by source text, least recently used first out (MYTHGPU_JIT_CACHE
 // entries, default 64): JIT sources embed the query, so this only serves repeats
@@ -765,23 +783,32 @@ struct CodeCache {
   struct Entry {
     std::string src;
     std::vector<char> code;
+    // the module as loaded on the primary device, kept resident: a repeated query's kernel is
+    // ready without a module load (hipModuleLoadData per repeat was most of a warm switch)
+    std::shared_ptr<ModHold> hold;
+    hipFunction_t fsearch = nullptr, feval = nullptr, fgen = nullptr;
+    int nb_search = 1, nb_eval = 1;
   };
   std::list<Entry> lru;  // front = most recent
   std::unordered_multimap<size_t, std::list<Entry>::iterator> idx;
   size_t cap = 64;
-  const std::vector<char>* find(const std::string& src) {
+  Entry* find_entry(const std::string& src) {
     const size_t h = std::hash<std::string>()(src);
     auto r = idx.equal_range(h);
     for (auto it = r.first; it != r.second; ++it)
       if (it->second->src == src) {
         lru.splice(lru.begin(), lru, it->second);
-        return &it->second->code;
+        return &*it->second;
       }
     return nullptr;
   }
+  const std::vector<char>* find(const std::string& src) {
+    Entry* en = find_entry(src);
+    return en ? &en->code : nullptr;
+  }
   const std::vector<char>* insert(const std::string& src, std::vector<char>&& code) {
     if (const auto* c = find(src)) return c;
-    lru.push_front(Entry{src, std::move(code)});
+    lru.push_front(Entry{src, std::move(code), nullptr});
     idx.emplace(std::hash<std::string>()(src), lru.begin());
     while (lru.size() > cap) {
       auto last = std::prev(lru.end());
@@ -1242,13 +1269,15 @@ void mg_shutdown(void) {
     e.jit_stop = false;
     e.jit_queue.clear();
     for (auto& kv : e.tickets)
-      if (kv.second->ready) (void)hipModuleUnload(kv.second->ready->mod);
+      if (kv.second->ready) release_jit(*kv.second->ready);
     e.tickets.clear();
   }
   jit_helper_stop();  // the compiler process ends on end of input (started again on demand)
   if (!e.init) {
-    for (auto& kv : e.jits) (void)hipModuleUnload(kv.second->mod);
+    for (auto& kv : e.jits) release_jit(*kv.second);
     e.jits.clear();
+    e.code_cache.lru.clear();
+    e.code_cache.idx.clear();
     return;
   }
   for (size_t i = g_devs.size(); i-- > 0;) {
@@ -1266,8 +1295,10 @@ namespace mg {
 
 // every device buffer, module and stream of one logical device (its device current)
 static void free_dev_buffers(Engine& e) {
-  for (auto& kv : e.jits) (void)hipModuleUnload(kv.second->mod);
+  for (auto& kv : e.jits) release_jit(*kv.second);
   e.jits.clear();
+  e.code_cache.lru.clear();  // the resident modules
+  e.code_cache.idx.clear();
   for (auto& kv : e.progs) free_code(e, *kv.second);
   e.progs.clear();
   for (auto& kv : e.gens) free_gen_buffers(e, *kv.second);
@@ -2059,28 +2090,59 @@ static void jit_worker_main(Engine* ep, int device) {
     const uint32_t kernels = t->has_gen ? (JIT_SEARCH | ((t->flags & MG_JIT_GEN_VERDICTS) ? JIT_GEN : 0u)) : JIT_EVAL;
     const std::string src = t->has_gen ? jit_source(t->low, &t->specs, &t->consts, kernels)
                                        : jit_source(t->low, nullptr, nullptr, kernels);
+    std::unique_ptr<DevJit> j;
+    std::vector<char> code;
     lk.lock();
-    const std::vector<char>* cached = e.code_cache.find(src);
-    std::vector<char> code = cached ? *cached : std::vector<char>();
+    if (CodeCache::Entry* en = e.code_cache.find_entry(src)) {
+      code = en->code;
+      if (en->hold) {  // resident module: no load
+        j = std::make_unique<DevJit>();
+        j->code = en->code;
+        j->hold = en->hold;
+        j->mod = en->hold->mod;
+        j->fsearch = en->fsearch;
+        j->feval = en->feval;
+        j->fgen = en->fgen;
+        j->nb_search = en->nb_search;
+        j->nb_eval = en->nb_eval;
+        j->prog = t->prog;
+        j->gen = t->gen;
+        j->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      }
+    }
     lk.unlock();
     int rc = MG_OK;
     std::string log;
-    if (code.empty()) {
+    bool compiled = false;
+    if (!j && code.empty()) {
       rc = jit_compile(src, code, log);
-      if (rc == MG_OK) {
-        lk.lock();
-        e.code_cache.insert(src, std::vector<char>(code));
-        lk.unlock();
-      }
+      compiled = rc == MG_OK;
     }
-    std::unique_ptr<DevJit> j;
     std::string err;
     if (rc != MG_OK) {
       err = "JIT compile failed: " + log.substr(0, 4000);
-    } else {
+    } else if (!j) {
       const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       rc = load_jit(code, *t, ms, j);
-      if (rc != MG_OK) err = g_err;
+      if (rc != MG_OK) {
+        err = g_err;
+      } else {
+        // the cache keeps the module loaded for the next request of the same source
+        j->hold = std::make_shared<ModHold>(j->mod);
+        lk.lock();
+        if (compiled) e.code_cache.insert(src, std::vector<char>(code));
+        if (CodeCache::Entry* en = e.code_cache.find_entry(src)) {
+          if (!en->hold) {
+            en->hold = j->hold;
+            en->fsearch = j->fsearch;
+            en->feval = j->feval;
+            en->fgen = j->fgen;
+            en->nb_search = j->nb_search;
+            en->nb_eval = j->nb_eval;
+          }
+        }
+        lk.unlock();
+      }
     }
     lk.lock();
     if (rc != MG_OK) {
@@ -2088,7 +2150,7 @@ static void jit_worker_main(Engine* ep, int device) {
       t->err = err;
       t->state = JitTicket::FAILED;
     } else if (t->cancelled) {
-      (void)hipModuleUnload(j->mod);
+      release_jit(*j);
       t->state = JitTicket::FAILED;
       t->rc = MG_E_INVALID;
       t->err = "cancelled";
@@ -2170,7 +2232,7 @@ static int poll_jit(Engine& e, uint64_t ticket, int64_t wait_ms, uint64_t* jit) 
   }
   if (t->state == JitTicket::FAILED) return set_err(t->rc ? t->rc : MG_E_HIP, t->err);
   if (!e.progs.count(t->prog) || (t->has_gen && !e.gens.count(t->gen))) {
-    (void)hipModuleUnload(t->ready->mod);
+    release_jit(*t->ready);
     return set_err(MG_E_INVALID, "program or generator freed before its JIT kernel was ready");
   }
   const uint64_t h = e.next_handle++;
@@ -2214,7 +2276,7 @@ int mg_jit_cancel(uint64_t ticket) {
   if (t->state == JitTicket::PENDING) {
     t->cancelled = true;  // the worker drops it (before compiling if still queued)
   } else if (t->state == JitTicket::DONE && t->ready) {
-    (void)hipModuleUnload(t->ready->mod);
+    release_jit(*t->ready);
     t->ready.reset();
   }
   return MG_OK;
@@ -2235,13 +2297,13 @@ int mg_jit_free(uint64_t jit) {
   std::lock_guard<std::mutex> g(e.mu);
   auto it = e.jits.find(jit);
   if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
-  (void)hipModuleUnload(it->second->mod);
+  release_jit(*it->second);
   e.jits.erase(it);
   for (size_t i = 1; i < g_devs.size(); i++) {
     auto q = g_devs[i]->jits.find(jit);
     if (q == g_devs[i]->jits.end()) continue;
     (void)hipSetDevice(g_devs[i]->device);
-    (void)hipModuleUnload(q->second->mod);
+    release_jit(*q->second);
     g_devs[i]->jits.erase(q);
   }
   if (g_devs.size() > 1) (void)hipSetDevice(e.device);

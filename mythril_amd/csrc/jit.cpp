@@ -125,6 +125,52 @@ struct Gen {
     }
   }
 
+  // Tables gathered from global memory are baked into the code object, entry-major with each
+  // entry on a 16-B boundary, so a lane reads a 256-bit entry with two 16-B loads instead of one
+  // 4-B load per limb: a per-lane gather is one texture-path request per lane and instruction,
+  // and eight of them per entry kept the path busy (C3: two 74-entry tables of 256-bit words,
+  // frac 0.31 with 2.8 gathers per wave and half the wave cycles waiting).
+  // MYTHGPU_JIT_DICT_VEC=0: per-limb gathers from the generator blob.
+  std::map<uint32_t, uint32_t> dict_gv;  // gconsts offset of a table -> word offset in mg_gd
+  std::map<uint32_t, uint32_t> dict_gv_stride;
+  std::vector<uint32_t> gd;              // the baked tables
+  void plan_dict_gv() {
+    dict_gv.clear();
+    dict_gv_stride.clear();
+    gd.clear();
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_DICT_VEC");
+      return !(g && g[0] == '0');
+    }();
+    if (!specs || !on) return;
+    const auto& G = *gconsts;
+    for (uint32_t c = 0; c < specs->size(); c++) {
+      const GenSpec& sp = (*specs)[c];
+      const uint32_t kind = sp.kind & 0xFFu;
+      const uint32_t n = sp.p[1], off = sp.p[0];
+      const bool dict = kind == MG_GEN_DICT || (kind == MG_GEN_MIXED && n && (sp.p[2] >> 16));
+      if (!dict || n == 0 || c >= P.coord_width.size() || coord_dead(c)) continue;
+      const uint32_t w = P.coord_width[c], L = Lw(w);
+      if (L < 2 || dict_gv.count(off) || dict_lds.count(off) || n <= select_dict_max()) continue;
+      if ((size_t)off + (size_t)n * L > G.size()) continue;
+      const uint32_t S = L == 2 ? 2u : (L + 3u) & ~3u;
+      if (gd.size() + (size_t)n * S > (1u << 16)) continue;
+      dict_gv[off] = (uint32_t)gd.size();
+      dict_gv_stride[off] = S;
+      for (uint32_t e = 0; e < n; e++)
+        for (uint32_t j = 0; j < S; j++) gd.push_back(j < L ? G[off + e * L + j] : 0u);
+    }
+  }
+
+  // the baked tables, at namespace scope before the kernels
+  void emit_dict_gv_table() {
+    if (gd.empty()) return;
+    o << "__device__ __attribute__((aligned(16))) const uint32_t mg_gd[" << gd.size() << "] = {";
+    for (size_t i = 0; i < gd.size(); i++) o << (i % 8 ? "" : "\n  ") << hex(gd[i]) << ",";
+    o << "\n};\n";
+  }
+  uint32_t gv_tmp = 0;
+
   // kernel prologue: copy the planned tables into LDS (all 256 lanes), then a block barrier
   void emit_dict_prologue() {
     if (!lds_words) return;
@@ -161,6 +207,22 @@ struct Gen {
     }
     const auto& G = *gconsts;
     auto lds = dict_lds.find(off);
+    auto gv = dict_gv.find(off);
+    std::vector<std::string> gvl(L);  // limb j of the entry read by vector loads from mg_gd
+    if (gv != dict_gv.end() && n > select_dict_max()) {
+      const uint32_t S = dict_gv_stride.at(off), q = S == 2 ? 2u : 4u;
+      for (uint32_t b = 0; b < L; b += q) {
+        bool need = false;
+        for (uint32_t j = b; j < std::min(L, b + q) && !need; j++)
+          for (uint32_t e = 1; e < n && !need; e++) need = G[off + e * L + j] != G[off + j];
+        if (!need) continue;
+        const std::string t = "mg_gq" + std::to_string(gv_tmp++);
+        o << ind << "const u32x" << q << " " << t << " = *(const u32x" << q << "*)(mg_gd + " << gv->second + b
+          << "u + " << idx << " * " << S << "u);\n";
+        static const char* comp = "xyzw";
+        for (uint32_t j = b; j < std::min(L, b + q); j++) gvl[j] = t + "." + comp[j - b];
+      }
+    }
     for (uint32_t j = 0; j < L; j++) {
       bool same = true;
       for (uint32_t e = 1; e < n && same; e++) same = G[off + e * L + j] == G[off + j];
@@ -174,7 +236,8 @@ struct Gen {
         v = hex(G[off + (n - 1) * L + j]);
         for (int32_t e = (int32_t)n - 2; e >= 0; e--)
           v = "(" + idx + " == " + std::to_string(e) + "u ? " + hex(G[off + e * L + j]) + " : " + v + ")";
-      } else if (lds != dict_lds.end()) v = "mg_dict[" + std::to_string(lds->second + j * n) + "u + " + idx + "]";
+      } else if (!gvl[j].empty()) v = gvl[j];
+      else if (lds != dict_lds.end()) v = "mg_dict[" + std::to_string(lds->second + j * n) + "u + " + idx + "]";
       else v = "gconsts[" + std::to_string(off + j) + "u + " + idx + " * " + std::to_string(L) + "u]";
       o << ind << lim(j) << " = " << v << ";\n";
     }
@@ -336,8 +399,18 @@ struct Gen {
           o << "    if ((ws & 0xFFFFu) < " << sp.p[5] << "u) {" << (h_known ? "" : " " + hdecl)
             << " const uint32_t mag = 1u + (h & 1u); const bool sb = (h >> 1) & 1u;"
             << " const uint32_t a0 = sb ? 0u - mag : mag, ah = sb ? 0xFFFFFFFFu : 0u; uint32_t cy = 0u;";
-          for (uint32_t j = 0; j < L; j++)
+          // the high limbs change only in a lane whose low-limb carry differs from the step's sign
+          // (x + 0 + 0 and x + ~0 + 1 are x): the rest of the chain runs only when some lane of the
+          // wave needs it (MYTHGPU_JIT_DELTA_SKIP=0: always)
+          static const bool skip = [] {
+            const char* g = getenv("MYTHGPU_JIT_DELTA_SKIP");
+            return !(g && g[0] == '0');
+          }();
+          for (uint32_t j = 0; j < L; j++) {
+            if (j == 1 && skip) o << " if (__ballot(cy != (uint32_t)sb)) {";
             o << " " << lim(j) << " = mg_addc(" << lim(j) << ", " << (j ? "ah" : "a0") << ", cy, &cy);";
+          }
+          if (L > 1 && skip) o << " }";
           o << " (void)cy; (void)ah; }\n";
         };
         // mask + clamp, emitted at the end of EACH branch: what a branch knows about its limbs
@@ -865,6 +938,7 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   const bool want_search = kernels & JIT_SEARCH, want_eval = kernels & JIT_EVAL, want_gen = kernels & JIT_GEN;
   Gen g(P, specs, gconsts);
   g.plan_dict_lds();
+  g.plan_dict_gv();
   g.plan_ws_slots();
   auto& o = g.o;
   // hipRTC compiles this with -nogpuinc -nogpulib: its own runtime header still supplies
@@ -874,6 +948,9 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   o << "typedef unsigned int uint32_t;\ntypedef int int32_t;\ntypedef unsigned long long uint64_t;\n"
        "typedef unsigned char uint8_t;\n";
   o << kPrelude << "\nusing namespace mg;\n";
+  o << "typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));\n"
+       "typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));\n";
+  g.emit_dict_gv_table();
   // 256-lane blocks; optional occupancy target (min waves per SIMD) for the search kernel
   std::string lb = "__attribute__((amdgpu_flat_work_group_size(1, 256)))";
   if (const char* wv = getenv("MYTHGPU_JIT_WAVES"))
