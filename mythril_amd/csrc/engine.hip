@@ -76,6 +76,7 @@ struct KArgs {
   uint32_t n_instr, value_words, flags;
   uint32_t watch_words;      // SEARCH with `watch`: rows per block of the capture buffer (see K_WATCH)
   uint32_t n_specs;          // generator specs (coordinates): the prologue's scalar-cache warm-up
+  uint32_t pc0;              // code[0, pc0): hoisted K_CONSTs, run once per thread (Lowered::n_hoisted)
 };
 
 constexpr uint32_t kFlagPrefetch = 1u << 16;  // KArgs::flags: warm the scalar cache first (launch_async)
@@ -368,6 +369,27 @@ __device__ __forceinline__ void do_keccak(const VF& vf, const Instr& in) {
     }                                            \
   } while (0)
 
+// EQ / ULT / ULE / SLT / SLE of the width-wa values in slots a and b (0 or 1)
+template <class VF>
+__device__ __forceinline__ uint32_t compare(const VF& vf, uint32_t op, uint32_t a, uint32_t b, uint32_t wa) {
+  const uint32_t La = (wa + 31) >> 5;
+  if (op == K_EQ) {
+    uint32_t d = 0;
+    MG_LIMBS(La, d |= vf.at(a + j) ^ vf.at(b + j););
+    return d == 0;
+  }
+  // a - b borrow chain; for signed compare flip the sign bits first
+  const uint32_t sflip = (op == K_SLT || op == K_SLE) ? (1u << ((wa - 1) & 31)) : 0u;
+  uint32_t br = 0, nz = 0;
+  MG_LIMBS(La, {
+    const uint32_t f = j == La - 1 ? sflip : 0u;
+    nz |= __builtin_subc(vf.at(a + j) ^ f, vf.at(b + j) ^ f, br, &br);
+  });
+  const bool lt = br != 0;
+  const bool le = lt || nz == 0;
+  return (op == K_ULT || op == K_SLT) ? (uint32_t)lt : (uint32_t)le;
+}
+
 // HEAVY = false: a program with no MUL/DIV/REM/shift/EXP/UMUL_NOOVF/KECCAK (most LASER
 // queries): those handlers hold ~200 VGPRs of 256-bit temporaries, so leaving them out
 // of the kernel lets several times more waves hide the LDS and scalar-load latency.
@@ -379,9 +401,9 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
   // the next instruction's scalar load is issued before this one executes, so its latency
   // overlaps this instruction's LDS traffic instead of adding to it (the code buffer has
   // one padding record after the last instruction)
-  Instr nx = ld_instr(k, 0);
+  Instr nx = ld_instr(k, k.pc0);
   bool stop = false;
-  for (uint32_t pc = 0; pc < n_instr && !stop; pc++) {
+  for (uint32_t pc = k.pc0; pc < n_instr && !stop; pc++) {
     const Instr in = nx;
     nx = ld_instr(k, pc + 1);
     const uint32_t W = in.wd;
@@ -450,18 +472,13 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
       case K_ULT:
       case K_ULE:
       case K_SLT:
-      case K_SLE: {
-        const uint32_t wa = in.p1, La = (wa + 31) >> 5;
-        // a - b borrow chain; for signed compare flip the sign bits first
-        const uint32_t sflip = (in.op == K_SLT || in.op == K_SLE) ? (1u << ((wa - 1) & 31)) : 0u;
-        uint32_t br = 0, nz = 0;
-        MG_LIMBS(La, {
-          const uint32_t f = j == La - 1 ? sflip : 0u;
-          nz |= __builtin_subc(vf.at(in.a + j) ^ f, vf.at(in.b + j) ^ f, br, &br);
-        });
-        const bool lt = br != 0;
-        const bool le = lt || nz == 0;
-        vf.at(in.dst) = (in.op == K_ULT || in.op == K_SLT) ? (uint32_t)lt : (uint32_t)le;
+      case K_SLE:
+        vf.at(in.dst) = compare(vf, in.op, in.a, in.b, in.p1);
+        break;
+      case K_ASSERT_CMP: {
+        // a compare whose one use was this assert (program.cpp: fuse_asserts)
+        verdict &= compare(vf, in.p0 & 0xFFu, in.a, in.b, in.p1) ^ (in.p0 >> 8);
+        if (early && __builtin_amdgcn_readfirstlane((uint32_t)(__ballot(verdict != 0) != 0ull)) == 0u) stop = true;
         break;
       }
       case K_CONCAT: {
@@ -620,6 +637,13 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
     warm((const uint32_t*)k.code, min((k.n_instr + 2u) / 2u, 512u));
     if (MODE != MODE_EVAL && k.specs) warm((const uint32_t*)k.specs, min((k.n_specs + 1u) / 2u, 512u));
     if (acc == 0x5EED1E55u && k.count == ~0ull) k.hits[0] = acc;  // never true: keeps the loads
+  }
+  // the hoisted literals: their slots are never reused, so once per thread is enough
+  for (uint32_t pc = 0; pc < k.pc0; pc++) {
+    const Instr in = ld_instr(k, pc);
+    const uint32_t L = (in.wd + 31) >> 5;
+    const auto* c = cst(k.consts) + in.p0;
+    MG_LIMBS(L, vf.at(in.dst + j) = c[j];);
   }
   for (uint64_t base = (uint64_t)blockIdx.x * kWave; base < total; base += step) {
     const uint64_t off = base + threadIdx.x;
@@ -1052,6 +1076,7 @@ static int launch_async(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   k.n_instr = (uint32_t)p.low.code.size();
   k.value_words = p.low.value_words;
   k.n_specs = p.low.n_coords;
+  k.pc0 = p.low.n_hoisted;
   // MYTHGPU_INTERP_PREFETCH=0: no scalar-cache warm-up in the prologue
   static const bool prefetch = [] {
     const char* g = getenv("MYTHGPU_INTERP_PREFETCH");

@@ -133,11 +133,106 @@ class Alloc {
 // liveness + first-fit slot allocation of an SSA instruction list: fills out.code/aux
 // (slot operands, what the interpreter runs), out.vcode/vaux (value ids, what the JIT
 // emits), out.value_words and out.limb_ops
-void allocate(const std::vector<VInstr>& code, const std::vector<uint32_t>& vwidth, Lowered& out) {
+// Interpreter superinstructions (slot code only; the JIT's vcode keeps every instruction): a
+// compare whose only use is an ASSERT, directly or through one NOT whose only use is the ASSERT,
+// becomes one K_ASSERT_CMP at the compare's place.  The verdict is the same AND of the same Bools;
+// only the point where the wave may stop early moves up.  MYTHGPU_INTERP_FUSE=0: off.
+std::vector<VInstr> fuse_asserts(const std::vector<VInstr>& code, size_t nv) {
+  static const bool on = [] {
+    const char* g = getenv("MYTHGPU_INTERP_FUSE");
+    return !(g && g[0] == '0');
+  }();
+  if (!on) return code;
+  const uint32_t NONE = MG_NONE;
+  std::vector<uint32_t> uses(nv, 0);
+  std::vector<int64_t> user(nv, -1);
+  auto use = [&](uint32_t v, size_t k) {
+    if (v != NONE && v < nv) {
+      uses[v]++;
+      user[v] = (int64_t)k;
+    }
+  };
+  for (size_t k = 0; k < code.size(); k++) {
+    const VInstr& c = code[k];
+    if (c.op == K_LOOKUP) {
+      use(c.a, k);
+      use(c.p0, k);
+      for (uint32_t v : c.prior) use(v, k);
+    } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT || c.op == K_KECCAK ||
+               c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
+      use(c.a, k);
+      use(c.b, k);
+    } else if (c.op != K_CONST && c.op != K_COORD) {
+      use(c.a, k);
+      use(c.b, k);
+      use(c.c, k);
+    }
+  }
+  std::vector<char> drop(code.size(), 0);
+  std::vector<VInstr> out;
+  out.reserve(code.size());
+  for (size_t k = 0; k < code.size(); k++) {
+    if (drop[k]) continue;
+    const VInstr& c = code[k];
+    const bool cmp = c.op == K_EQ || c.op == K_ULT || c.op == K_ULE || c.op == K_SLT || c.op == K_SLE;
+    if (cmp && c.dst != NONE && c.dst < nv && uses[c.dst] == 1) {
+      int64_t u = user[c.dst];
+      uint32_t neg = 0;
+      int64_t mid = -1;
+      if (code[u].op == K_NOT && code[u].wd == 1 && code[u].dst != NONE && code[u].dst < nv &&
+          uses[code[u].dst] == 1) {
+        mid = u;
+        neg = 1;
+        u = user[code[u].dst];
+      }
+      if (code[u].op == K_ASSERT) {
+        if (mid >= 0) drop[mid] = 1;
+        drop[u] = 1;
+        out.push_back(VInstr{K_ASSERT_CMP, 1, NONE, c.a, c.b, NONE, c.op | (neg << 8), c.p1, {}});
+        continue;
+      }
+    }
+    out.push_back(c);
+  }
+  return out;
+}
+
+void allocate(const std::vector<VInstr>& vlist, const std::vector<uint32_t>& vwidth, Lowered& out) {
   const uint32_t NONE = MG_NONE;
   const size_t nv = vwidth.size();
   out.vcode.clear();
   out.vaux.clear();
+  // the JIT's SSA list and the cost table: every instruction
+  for (const VInstr& c : vlist) {
+    Instr vi{c.op, c.wd, c.dst, c.a, c.b, c.c, c.p0, c.p1};
+    if (c.op == K_LOOKUP) {
+      vi.p1 = (uint32_t)out.vaux.size();
+      for (uint32_t v : c.prior) out.vaux.push_back(v);
+    }
+    out.vcode.push_back(vi);
+    uint32_t wa = c.p1;
+    if (c.op == K_LOOKUP) {
+      out.limb_ops += 3ull * L_of(c.b) * c.c + L_of(c.wd);
+    } else if (c.op == K_KECCAK) {
+      out.limb_ops += 7500ull * (c.p0 / 136 + 1);
+    } else {
+      out.limb_ops += op_cost(c.op, c.wd, wa ? wa : c.wd);
+    }
+  }
+  // the interpreter's slot code: superinstructions, then liveness and slots
+  std::vector<VInstr> code = fuse_asserts(vlist, nv);
+  // literals do not change from one candidate to the next: the K_CONSTs go first, keep their slots
+  // to the end, and the interpreter writes them once per thread instead of once per candidate
+  // (MYTHGPU_INTERP_HOIST=0: in place)
+  static const bool hoist = [] {
+    const char* g = getenv("MYTHGPU_INTERP_HOIST");
+    return !(g && g[0] == '0');
+  }();
+  out.n_hoisted = 0;
+  if (hoist) {
+    std::stable_partition(code.begin(), code.end(), [](const VInstr& c) { return c.op == K_CONST; });
+    while (out.n_hoisted < code.size() && code[out.n_hoisted].op == K_CONST) out.n_hoisted++;
+  }
   std::vector<int64_t> last(nv, -1), def(nv, -1);
   for (size_t k = 0; k < code.size(); k++) {
     const VInstr& c = code[k];
@@ -159,6 +254,8 @@ void allocate(const std::vector<VInstr>& code, const std::vector<uint32_t>& vwid
     }
     if (c.dst != NONE && def[c.dst] < 0) def[c.dst] = (int64_t)k;
   }
+  for (uint32_t k = 0; k < out.n_hoisted; k++)
+    if (code[k].dst != NONE && code[k].dst < nv) last[code[k].dst] = (int64_t)code.size() - 1;
   std::vector<uint32_t> slot(nv, NONE);
   std::vector<std::vector<uint32_t>> dies(code.size());
   for (size_t v = 0; v < nv; v++) {
@@ -199,23 +296,6 @@ void allocate(const std::vector<VInstr>& code, const std::vector<uint32_t>& vwid
       in.c = S(c.c);
     }
     out.code.push_back(in);
-    {
-      Instr vi{c.op, c.wd, c.dst, c.a, c.b, c.c, c.p0, c.p1};
-      if (c.op == K_LOOKUP) {
-        vi.p1 = (uint32_t)out.vaux.size();
-        for (uint32_t v : c.prior) out.vaux.push_back(v);
-      }
-      out.vcode.push_back(vi);
-    }
-    // cost
-    uint32_t wa = c.p1;
-    if (c.op == K_LOOKUP) {
-      out.limb_ops += 3ull * L_of(c.b) * c.c + L_of(c.wd);
-    } else if (c.op == K_KECCAK) {
-      out.limb_ops += 7500ull * (c.p0 / 136 + 1);
-    } else {
-      out.limb_ops += op_cost(c.op, c.wd, wa ? wa : c.wd);
-    }
     for (uint32_t v : dies[k]) al.release(slot[v], L_of(vwidth[v]));
     if (getenv("MYTHGPU_DEBUG_ALLOC") && al.high() > dbg_high) {
       dbg_high = al.high();

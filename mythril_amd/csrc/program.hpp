@@ -33,6 +33,10 @@ enum KOp : uint32_t {
   K_ASSERT,      // verdict &= a ; may early-exit the wave
   K_WATCH,       // watch rows [p0 .. p0+L) <- a  (eval only)
   K_COPY,        // dst <- a
+  // interpreter only (slot code, never in vcode): verdict &= (a <cmp> b) ^ neg, where
+  // p0 = cmp op (K_EQ/K_ULT/K_ULE/K_SLT/K_SLE) | neg << 8, p1 = operand width; the fusion of a
+  // compare whose one use is an ASSERT (through at most one NOT) — one dispatch instead of 2-3
+  K_ASSERT_CMP,
   K_COUNT
 };
 
@@ -50,6 +54,7 @@ struct Lowered {
   std::vector<uint32_t> consts;
   std::vector<uint32_t> aux;          // LOOKUP prior lists: pairs (key slot, value slot)
   uint32_t value_words = 0;
+  uint32_t n_hoisted = 0;             // code[0, n_hoisted): K_CONSTs the interpreter runs once per thread
   uint32_t n_nodes = 0, n_roots = 0, n_coords = 0, n_watch = 0;
   std::vector<uint32_t> coord_width;
   std::vector<uint32_t> coord_row;    // SoA row offset of each coordinate
