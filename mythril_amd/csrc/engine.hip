@@ -41,7 +41,16 @@ namespace mg {
 
 constexpr int kWave = 64;
 constexpr size_t kCaptureBytes = 64ull << 20;  // watch-row capture buffer (mg_search), per device
-constexpr uint32_t kLdsWordsMax = 160;  // value file in LDS up to 160 words (40 KiB per wave)
+// value file in LDS up to this many words per lane (160: 40 KiB per wave), else in global memory;
+// MYTHGPU_INTERP_LDS_MAX overrides (at most 255: 64 KiB per one-wave block)
+static uint32_t lds_words_max() {
+  static const uint32_t n = [] {
+    const char* g = getenv("MYTHGPU_INTERP_LDS_MAX");
+    const int v = g ? atoi(g) : 160;
+    return (uint32_t)std::max(1, std::min(v, 255));
+  }();
+  return n;
+}
 
 __device__ __constant__ static const uint32_t kEmptyKeccak[8] = {
     0x5d85a470u, 0x7bfad804u, 0xca82273bu, 0xe500b653u, 0xdcc703c0u, 0x927e7db2u, 0x86f7233cu, 0xc5d24601u};
@@ -980,7 +989,7 @@ static void free_gen_buffers(Engine& e, DevGen& g) {
 
 // instructions, literals, lookup lists and coordinate widths in ONE pooled buffer, one copy
 static int upload_code(Engine& e, DevProgram& p) {
-  p.lds = p.low.value_words <= kLdsWordsMax;
+  p.lds = p.low.value_words <= lds_words_max();
   p.heavy = false;
   for (const Instr& in : p.low.code) {
     switch (in.op) {
@@ -1373,7 +1382,7 @@ int mg_program_check(const uint8_t* ssa, size_t len, mg_program_info_t* info) {
     info->n_coords = low.n_coords;
     info->n_roots = low.n_roots;
     info->value_words = low.value_words;
-    info->uses_lds = low.value_words <= kLdsWordsMax;
+    info->uses_lds = low.value_words <= lds_words_max();
     info->n_watch = low.n_watch;
     info->watch_words = low.watch_words;
     info->coord_words = low.coord_words;
@@ -1394,7 +1403,7 @@ int mg_program_check_gen(const uint8_t* ssa, size_t len, const uint32_t* gen_blo
   if (rc) return set_err(rc, err);
   rc = specialize_program(base.low, &specs, &consts, sp.low, err);
   if (rc) return set_err(rc, err);
-  sp.lds = sp.low.value_words <= kLdsWordsMax;
+  sp.lds = sp.low.value_words <= lds_words_max();
   if (info) fill_info(sp, info);
   return MG_OK;
 }

@@ -197,7 +197,94 @@ std::vector<VInstr> fuse_asserts(const std::vector<VInstr>& code, size_t nv) {
   return out;
 }
 
-void allocate(const std::vector<VInstr>& vlist, const std::vector<uint32_t>& vwidth, Lowered& out) {
+// liveness and best-fit slots of the interpreter's slot code; returns the value file's words.
+// code[0, n_hoisted) are K_CONSTs whose slots stay reserved to the end.
+uint32_t assign_slots(const std::vector<VInstr>& code, uint32_t n_hoisted, const std::vector<uint32_t>& vwidth,
+                      std::vector<Instr>& ocode, std::vector<uint32_t>& oaux) {
+  const uint32_t NONE = MG_NONE;
+  const size_t nv = vwidth.size();
+  std::vector<int64_t> last(nv, -1), def(nv, -1);
+  for (size_t k = 0; k < code.size(); k++) {
+    const VInstr& c = code[k];
+    auto use = [&](uint32_t v) {
+      if (v != NONE && v < nv) last[v] = (int64_t)k;
+    };
+    if (c.op == K_LOOKUP) {
+      use(c.a);
+      use(c.p0);
+      for (uint32_t v : c.prior) use(v);
+    } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT ||
+               c.op == K_KECCAK || c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
+      use(c.a);
+      use(c.b);
+    } else if (c.op != K_CONST && c.op != K_COORD) {
+      use(c.a);
+      use(c.b);
+      use(c.c);
+    }
+    if (c.dst != NONE && def[c.dst] < 0) def[c.dst] = (int64_t)k;
+  }
+  for (uint32_t k = 0; k < n_hoisted; k++)
+    if (code[k].dst != NONE && code[k].dst < nv) last[code[k].dst] = (int64_t)code.size() - 1;
+  std::vector<uint32_t> slot(nv, NONE);
+  std::vector<std::vector<uint32_t>> dies(code.size());
+  for (size_t v = 0; v < nv; v++) {
+    if (def[v] < 0) continue;
+    int64_t d = std::max(last[v], def[v]);
+    dies[(size_t)d].push_back((uint32_t)v);
+  }
+  Alloc al;
+  uint32_t dbg_high = 0;
+  ocode.clear();
+  oaux.clear();
+  for (size_t k = 0; k < code.size(); k++) {
+    VInstr c = code[k];
+    if (c.dst != NONE && slot[c.dst] == NONE) slot[c.dst] = al.alloc(L_of(vwidth[c.dst]));
+    auto S = [&](uint32_t v) -> uint32_t {
+      if (v == NONE) return NONE;
+      if (slot[v] == NONE) fail(MG_E_INVALID, "internal: use before definition");
+      return slot[v];
+    };
+    Instr in{c.op, c.wd, c.dst == NONE ? NONE : slot[c.dst], 0, 0, 0, c.p0, c.p1};
+    if (c.op == K_LOOKUP) {
+      in.a = S(c.a);
+      in.b = c.b;
+      in.c = c.c;
+      in.p0 = S(c.p0);
+      in.p1 = (uint32_t)oaux.size();
+      for (uint32_t v : c.prior) oaux.push_back(S(v));
+    } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT || c.op == K_KECCAK ||
+               c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
+      in.a = S(c.a);
+      in.b = S(c.b);
+      in.c = NONE;
+    } else if (c.op == K_CONST || c.op == K_COORD) {
+      in.a = in.b = in.c = NONE;
+    } else {
+      in.a = S(c.a);
+      in.b = S(c.b);
+      in.c = S(c.c);
+    }
+    ocode.push_back(in);
+    for (uint32_t v : dies[k]) al.release(slot[v], L_of(vwidth[v]));
+    if (getenv("MYTHGPU_DEBUG_ALLOC") && al.high() > dbg_high) {
+      dbg_high = al.high();
+      size_t live = 0;
+      std::string s;
+      for (size_t v = 0; v < nv; v++)
+        if (def[v] >= 0 && def[v] <= (int64_t)k && std::max(last[v], def[v]) > (int64_t)k) {
+          live += L_of(vwidth[v]);
+          s += " " + std::to_string(v) + ":" + std::to_string(vwidth[v]) + "@" + std::to_string(code[def[v]].op) +
+               "-" + std::to_string(last[v]);
+        }
+      fprintf(stderr, "instr %zu high %u live %zu:%s\n", k, al.high(), live, s.c_str());
+    }
+  }
+  return std::max<uint32_t>(al.high(), 1);
+}
+
+void allocate(const std::vector<VInstr>& vlist, const std::vector<uint32_t>& vwidth, Lowered& out,
+              const std::vector<VInstr>* slot_list = nullptr) {
   const uint32_t NONE = MG_NONE;
   const size_t nv = vwidth.size();
   out.vcode.clear();
@@ -220,97 +307,35 @@ void allocate(const std::vector<VInstr>& vlist, const std::vector<uint32_t>& vwi
     }
   }
   // the interpreter's slot code: superinstructions, then liveness and slots
-  std::vector<VInstr> code = fuse_asserts(vlist, nv);
-  // literals do not change from one candidate to the next: the K_CONSTs go first, keep their slots
-  // to the end, and the interpreter writes them once per thread instead of once per candidate
-  // (MYTHGPU_INTERP_HOIST=0: in place)
+  // (slot_list: a different program with the same verdicts for the interpreter, e.g. narrowed)
+  const std::vector<VInstr> code = fuse_asserts(slot_list ? *slot_list : vlist, nv);
+  out.n_hoisted = 0;
+  out.value_words = assign_slots(code, 0, vwidth, out.code, out.aux);
+  // literals do not change from one candidate to the next: with the K_CONSTs first and their slots
+  // kept to the end, the interpreter writes them once per thread instead of once per candidate —
+  // unless that makes the value file larger (fewer waves per CU cost more than the CONSTs: C2 was
+  // 13 % slower with two pinned 256-bit literals).  MYTHGPU_INTERP_HOIST=0: never
   static const bool hoist = [] {
     const char* g = getenv("MYTHGPU_INTERP_HOIST");
     return !(g && g[0] == '0');
   }();
-  out.n_hoisted = 0;
   if (hoist) {
-    std::stable_partition(code.begin(), code.end(), [](const VInstr& c) { return c.op == K_CONST; });
-    while (out.n_hoisted < code.size() && code[out.n_hoisted].op == K_CONST) out.n_hoisted++;
-  }
-  std::vector<int64_t> last(nv, -1), def(nv, -1);
-  for (size_t k = 0; k < code.size(); k++) {
-    const VInstr& c = code[k];
-    auto use = [&](uint32_t v) {
-      if (v != NONE && v < nv) last[v] = (int64_t)k;
-    };
-    if (c.op == K_LOOKUP) {
-      use(c.a);
-      use(c.p0);
-      for (uint32_t v : c.prior) use(v);
-    } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT ||
-               c.op == K_KECCAK || c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
-      use(c.a);
-      use(c.b);
-    } else if (c.op != K_CONST && c.op != K_COORD) {
-      use(c.a);
-      use(c.b);
-      use(c.c);
-    }
-    if (c.dst != NONE && def[c.dst] < 0) def[c.dst] = (int64_t)k;
-  }
-  for (uint32_t k = 0; k < out.n_hoisted; k++)
-    if (code[k].dst != NONE && code[k].dst < nv) last[code[k].dst] = (int64_t)code.size() - 1;
-  std::vector<uint32_t> slot(nv, NONE);
-  std::vector<std::vector<uint32_t>> dies(code.size());
-  for (size_t v = 0; v < nv; v++) {
-    if (def[v] < 0) continue;
-    int64_t d = std::max(last[v], def[v]);
-    dies[(size_t)d].push_back((uint32_t)v);
-  }
-  Alloc al;
-  uint32_t dbg_high = 0;
-  out.code.clear();
-  out.aux.clear();
-  for (size_t k = 0; k < code.size(); k++) {
-    VInstr c = code[k];
-    if (c.dst != NONE && slot[c.dst] == NONE) slot[c.dst] = al.alloc(L_of(vwidth[c.dst]));
-    auto S = [&](uint32_t v) -> uint32_t {
-      if (v == NONE) return NONE;
-      if (slot[v] == NONE) fail(MG_E_INVALID, "internal: use before definition");
-      return slot[v];
-    };
-    Instr in{c.op, c.wd, c.dst == NONE ? NONE : slot[c.dst], 0, 0, 0, c.p0, c.p1};
-    if (c.op == K_LOOKUP) {
-      in.a = S(c.a);
-      in.b = c.b;
-      in.c = c.c;
-      in.p0 = S(c.p0);
-      in.p1 = (uint32_t)out.aux.size();
-      for (uint32_t v : c.prior) out.aux.push_back(S(v));
-    } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT || c.op == K_KECCAK ||
-               c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
-      in.a = S(c.a);
-      in.b = S(c.b);
-      in.c = NONE;
-    } else if (c.op == K_CONST || c.op == K_COORD) {
-      in.a = in.b = in.c = NONE;
-    } else {
-      in.a = S(c.a);
-      in.b = S(c.b);
-      in.c = S(c.c);
-    }
-    out.code.push_back(in);
-    for (uint32_t v : dies[k]) al.release(slot[v], L_of(vwidth[v]));
-    if (getenv("MYTHGPU_DEBUG_ALLOC") && al.high() > dbg_high) {
-      dbg_high = al.high();
-      size_t live = 0;
-      std::string s;
-      for (size_t v = 0; v < nv; v++)
-        if (def[v] >= 0 && def[v] <= (int64_t)k && std::max(last[v], def[v]) > (int64_t)k) {
-          live += L_of(vwidth[v]);
-          s += " " + std::to_string(v) + ":" + std::to_string(vwidth[v]) + "@" + std::to_string(code[def[v]].op) +
-               "-" + std::to_string(last[v]);
-        }
-      fprintf(stderr, "instr %zu high %u live %zu:%s\n", k, al.high(), live, s.c_str());
+    std::vector<VInstr> h = code;
+    std::stable_partition(h.begin(), h.end(), [](const VInstr& c) { return c.op == K_CONST; });
+    uint32_t nh = 0;
+    while (nh < h.size() && h[nh].op == K_CONST) nh++;
+    if (nh) {
+      std::vector<Instr> hc;
+      std::vector<uint32_t> ha;
+      const uint32_t words = assign_slots(h, nh, vwidth, hc, ha);
+      if (words <= out.value_words) {
+        out.code.swap(hc);
+        out.aux.swap(ha);
+        out.value_words = words;
+        out.n_hoisted = nh;
+      }
     }
   }
-  out.value_words = std::max<uint32_t>(al.high(), 1);
   out.vwidth = vwidth;
 }
 
@@ -1864,6 +1889,101 @@ namespace mg {
 // With specs == nullptr (explicit-coordinate eval) only literal-derived facts are used.
 // Verdicts are unchanged for every generated candidate (tests compare the specialised
 // interpreter and JIT kernels with the C restatement, which runs the full program).
+namespace {
+
+// Keys with a shared literal tail.  LASER addresses a mapping entry as keccak(Concat(key, slot))
+// with a literal slot, so the UF sites' preimages are 512-bit CONCATs whose low 256 bits are the
+// same literal everywhere: the site LOOKUPs compare them, the inverse LOOKUPs return them and
+// the injectivity asserts compare those with EQ.  Where every value in such a comparison is
+// CONCAT(h, T) with one literal T, the comparison is the same on the h parts: LOOKUP keys and EQ
+// operands are narrowed to h, a LOOKUP / ITE whose every candidate value is CONCAT(h, T) gets a
+// narrow twin returning h.  The wide CONCATs then die.  Same verdicts (x:T == y:T iff x == y);
+// the interpreter's value file loses half of every such key (C2: 112 -> 72 words per lane, i.e.
+// more waves per CU), the JIT half of the limbs it selects.  MYTHGPU_NARROW_TAILS=0: off.
+std::vector<uint32_t> narrow_literal_tails(std::vector<VInstr>& code, std::vector<uint32_t>& vwidth,
+                                           const std::vector<uint32_t>& consts) {
+  static const bool on = [] {
+    const char* g = getenv("MYTHGPU_NARROW_TAILS");
+    return !(g && g[0] == '0');
+  }();
+  std::vector<uint32_t> twinned;  // wide values that got a narrow twin
+  if (!on) return twinned;
+  const uint32_t NONE = MG_NONE;
+  std::map<uint32_t, std::string> lit;  // K_CONST value id -> its literal (width + words)
+  struct Split {
+    uint32_t h;
+    std::string t;
+  };
+  std::map<uint32_t, Split> split;  // value id -> (h, T) with value == h:T
+  auto same = [&](const Split& x, const Split& y) {
+    return x.t == y.t && vwidth[x.h] == vwidth[y.h];
+  };
+  std::vector<VInstr> add;  // narrow twins, inserted right after their wide instruction
+  std::vector<VInstr> outc;
+  outc.reserve(code.size() + 8);
+  for (VInstr& c : code) {
+    if (c.op == K_CONST && c.dst != NONE && c.dst < vwidth.size()) {
+      std::string t = std::to_string(c.wd) + ":";
+      for (uint32_t j = 0; j < Lw(c.wd); j++) t += std::to_string(consts.at(c.p0 + j)) + ",";
+      lit[c.dst] = t;
+    } else if (c.op == K_CONCAT && c.dst != NONE && lit.count(c.b) && c.a != NONE && c.a < vwidth.size()) {
+      split[c.dst] = Split{c.a, lit[c.b]};
+    } else if (c.op == K_EQ && split.count(c.a) && split.count(c.b) && same(split[c.a], split[c.b])) {
+      const uint32_t ha = split[c.a].h, hb = split[c.b].h;
+      c.a = ha;
+      c.b = hb;
+      c.p1 = vwidth[ha];
+    } else if (c.op == K_LOOKUP) {
+      // keys: the site key and every prior key
+      bool keys = split.count(c.a) > 0;
+      for (size_t q = 0; keys && q < c.prior.size(); q += 2)
+        keys = split.count(c.prior[q]) && same(split[c.prior[q]], split[c.a]);
+      if (keys) {
+        const Split ka = split[c.a];
+        for (size_t q = 0; q < c.prior.size(); q += 2) c.prior[q] = split[c.prior[q]].h;
+        c.a = ka.h;
+        c.b = vwidth[ka.h];
+      }
+      // values: the default and every prior value
+      bool vals = c.dst != NONE && split.count(c.p0);
+      for (size_t q = 1; vals && q < c.prior.size(); q += 2)
+        vals = split.count(c.prior[q]) && same(split[c.prior[q]], split[c.p0]);
+      if (vals) {
+        const Split d0 = split[c.p0];
+        VInstr n = c;
+        n.dst = (uint32_t)vwidth.size();
+        vwidth.push_back(vwidth[d0.h]);
+        n.wd = vwidth[d0.h];
+        n.p0 = d0.h;
+        for (size_t q = 1; q < n.prior.size(); q += 2) n.prior[q] = split[n.prior[q]].h;
+        split[c.dst] = Split{n.dst, d0.t};
+        twinned.push_back(c.dst);
+        outc.push_back(c);
+        outc.push_back(std::move(n));
+        continue;
+      }
+    } else if (c.op == K_ITE && c.dst != NONE && split.count(c.b) && split.count(c.c) &&
+               same(split[c.b], split[c.c])) {
+      VInstr n = c;
+      n.dst = (uint32_t)vwidth.size();
+      vwidth.push_back(vwidth[split[c.b].h]);
+      n.wd = vwidth[n.dst];
+      n.b = split[c.b].h;
+      n.c = split[c.c].h;
+      split[c.dst] = Split{n.dst, split[c.b].t};
+      twinned.push_back(c.dst);
+      outc.push_back(c);
+      outc.push_back(std::move(n));
+      continue;
+    }
+    outc.push_back(std::move(c));
+  }
+  code.swap(outc);
+  return twinned;
+}
+
+}  // namespace
+
 int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
                        Lowered& out, std::string& err, bool keep_watch, bool keep_asserts) {
   try {
@@ -1931,38 +2051,59 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
       }
       code.push_back(std::move(v));
     }
+    std::vector<VInstr> wide = code;
+    const std::vector<uint32_t> twinned = narrow_literal_tails(code, vwidth, out.consts);
+    const size_t nw = vwidth.size();  // with the narrow twins' values
     // dead code: keep asserts (unless dropped: the model read-back of a known hit), watches
     // and whatever they transitively use
-    std::vector<char> live(nv, 0), keep(code.size(), 0);
-    for (size_t k = code.size(); k-- > 0;) {
-      const VInstr& c = code[k];
-      const bool side = (c.op == K_ASSERT && keep_asserts) || (c.op == K_WATCH && keep_watch);
-      if (!side && (c.dst == NONE || c.dst >= nv || !live[c.dst])) continue;
-      keep[k] = 1;
-      auto use = [&](uint32_t x) {
-        if (x != NONE && x < nv) live[x] = 1;
-      };
-      if (c.op == K_LOOKUP) {
-        use(c.a);
-        use(c.p0);
-        for (uint32_t x : c.prior) use(x);
-      } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT || c.op == K_KECCAK ||
-                 c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
-        use(c.a);
-        use(c.b);
-      } else if (c.op != K_CONST && c.op != K_COORD) {
-        use(c.a);
-        use(c.b);
-        use(c.c);
+    auto dce = [&](std::vector<VInstr>& list) {
+      std::vector<char> live(nw, 0), keep(list.size(), 0);
+      for (size_t k = list.size(); k-- > 0;) {
+        const VInstr& c = list[k];
+        const bool side = (c.op == K_ASSERT && keep_asserts) || (c.op == K_WATCH && keep_watch);
+        if (!side && (c.dst == NONE || c.dst >= nw || !live[c.dst])) continue;
+        keep[k] = 1;
+        auto use = [&](uint32_t x) {
+          if (x != NONE && x < nw) live[x] = 1;
+        };
+        if (c.op == K_LOOKUP) {
+          use(c.a);
+          use(c.p0);
+          for (uint32_t x : c.prior) use(x);
+        } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT || c.op == K_KECCAK ||
+                   c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
+          use(c.a);
+          use(c.b);
+        } else if (c.op != K_CONST && c.op != K_COORD) {
+          use(c.a);
+          use(c.b);
+          use(c.c);
+        }
       }
+      std::vector<VInstr> kept;
+      kept.reserve(list.size());
+      for (size_t k = 0; k < list.size(); k++)
+        if (keep[k] && (keep_watch || list[k].op != K_WATCH)) kept.push_back(std::move(list[k]));
+      return kept;
+    };
+    std::vector<VInstr> kept = dce(code);
+    // the JIT folds literal limbs by itself, so it gains from the narrow form only where the wide
+    // values die; where a wide one stays live (a LOOKUP over keys with different literal tails
+    // still reads it: C4) its narrow twin is extra work there, and the JIT keeps the wide program
+    bool wide_live = false;
+    if (!twinned.empty()) {
+      std::vector<char> tw(nw, 0);
+      for (uint32_t v : twinned) tw[v] = 1;
+      for (const VInstr& c : kept) wide_live = wide_live || (c.dst != NONE && c.dst < nw && tw[c.dst]);
     }
-    std::vector<VInstr> kept;
-    kept.reserve(code.size());
-    for (size_t k = 0; k < code.size(); k++)
-      if (keep[k] && (keep_watch || code[k].op != K_WATCH)) kept.push_back(std::move(code[k]));
     const uint64_t ops = in.limb_ops;  // algorithmic work is the query's, not what survives
     out.limb_ops = 0;
-    allocate(kept, vwidth, out);
+    if (wide_live) {
+      std::vector<VInstr> kept_wide = dce(wide);
+      allocate(kept_wide, vwidth, out, &kept);
+    } else {
+      allocate(kept, vwidth, out);
+    }
     out.limb_ops = ops;
     return MG_OK;
   } catch (const Fail& f) {

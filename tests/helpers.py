@@ -203,3 +203,20 @@ def gpu_eval_terms(engine, roots: Sequence[T.Term], watch_terms: Sequence[T.Term
         results.append(tv)
         models.append(OracleModel(s, a, f))
     return P, assigns, ver, results, models
+
+
+def literal_tail_query():
+    """Mapping keys ``Concat(key, slot)`` with literal slots, as LASER addresses storage through
+    ``keccak(Concat(key, slot))``: an EQ of an ITE over such keys, two keccak sites with slot 5 and
+    one with slot 6 (different literal tails never compare equal)."""
+    from mythril_amd.smt import Array, Concat, Function, If, Not, ULT, symbol_factory
+
+    BVV, S = symbol_factory.BitVecVal, symbol_factory.BitVecSym
+    a, b, d, e = S("nk_a", 256), S("nk_b", 256), S("nk_d", 256), S("nk_e", 256)
+    slot, other = BVV(5, 256), BVV(6, 256)
+    k1, k2, k3 = Concat(a, slot), Concat(b, slot), Concat(d, slot)
+    h = Function("keccak256_512", 512, 256)
+    storage = Array("Storage", 256, 256)
+    return [If(ULT(a, b), k1, k2) == k3, Not(a == b),
+            ULT(storage[h(k1)], storage[h(k3)] + BVV(3, 256)),
+            Not(storage[h(Concat(e, other))] == BVV(0, 256))]

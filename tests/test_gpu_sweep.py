@@ -43,10 +43,22 @@ def _windows(rng):
 
 @pytest.mark.parametrize("name", sorted(workloads.WORKLOADS), ids=workloads.test_id)
 def test_sweep_random_windows(engine, name):
+    _sweep(engine, name, [c.raw for c in workloads.WORKLOADS[name]()])
+
+
+def test_sweep_literal_tail_keys(engine):
+    """Keys Concat(key, literal slot) compared through EQ, ITE and keccak sites: the interpreter
+    runs them narrowed to the key halves (program.cpp: narrow_literal_tails), mixed tails included."""
+    from tests.helpers import literal_tail_query
+
+    _sweep(engine, "literal_tail_keys", [c.raw for c in literal_tail_query()])
+
+
+def _sweep(engine, name, roots):
     from oracle import cport
 
     rng = random.Random(zlib.crc32(name.encode()) ^ 0x6D797468)
-    P, blob = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
+    P, blob = search.prepare(roots)
     pb = P.to_bytes()
     prog = engine.load(pb)
     gh = engine.load_gen(prog, blob)

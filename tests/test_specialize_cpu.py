@@ -97,3 +97,26 @@ def test_jit_kernels_compile_on_host(name):
     P, blob = search.prepare(roots)
     src = native.jit_source(P.to_bytes(), blob, compile=True)
     assert "mgj_search" in src
+
+
+def test_literal_tail_keys_are_narrowed():
+    """Mapping keys ``Concat(key, slot)`` with a literal slot (LASER's storage addressing through
+    ``keccak(Concat(key, slot))``): comparisons of such keys (EQ, ITE arms, LOOKUP sites) run on the
+    key halves (``program.cpp: narrow_literal_tails``), and the verdicts stay those of the C port on
+    the unspecialised program — also where the keys carry different literal tails (they never
+    compare equal, and the wide values stay)."""
+    from tests.helpers import literal_tail_query
+
+    cs = literal_tail_query()
+    P, blob = search.prepare([c.raw for c in cs])
+    pb = P.to_bytes()
+    spec = native.specialized_program(pb, blob)
+    eq512 = [r for r in spec["code"] if int(r[0]) == kops.K_EQ and int(r[7]) == 512]
+    assert not eq512, "a comparison of literal-tail keys was not narrowed"
+    rng = random.Random(0x7A11)
+    for start in (0, rng.getrandbits(63) | 1):
+        seed = rng.getrandbits(32)
+        soa = cport.gen_soa(pb, blob, seed, start, N, _coord_words(P))
+        want = cport.search(pb, blob, seed, start, N, threads=4, verdicts=True)[2]
+        got = kops.verdicts(spec, soa, [c.width for c in P.coords], N)
+        assert np.array_equal(got, want)
