@@ -137,6 +137,53 @@ class Alloc {
 // compare whose only use is an ASSERT, directly or through one NOT whose only use is the ASSERT,
 // becomes one K_ASSERT_CMP at the compare's place.  The verdict is the same AND of the same Bools;
 // only the point where the wave may stop early moves up.  MYTHGPU_INTERP_FUSE=0: off.
+// every value id an instruction reads
+template <class F>
+void for_each_use(const VInstr& c, F&& f) {
+  const uint32_t NONE = MG_NONE;
+  auto use = [&](uint32_t v) {
+    if (v != NONE) f(v);
+  };
+  if (c.op == K_LOOKUP) {
+    use(c.a);
+    use(c.p0);
+    for (uint32_t v : c.prior) use(v);
+  } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT || c.op == K_KECCAK ||
+             c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
+    use(c.a);
+    use(c.b);
+  } else if (c.op != K_CONST && c.op != K_COORD) {
+    use(c.a);
+    use(c.b);
+    use(c.c);
+  }
+}
+
+// K_COORD / K_CONST moved to just before their first use (order among them kept)
+std::vector<VInstr> sink_inputs(const std::vector<VInstr>& code, size_t nv) {
+  std::vector<int64_t> first(nv, -1);
+  for (size_t k = 0; k < code.size(); k++)
+    for_each_use(code[k], [&](uint32_t v) {
+      if (v < nv && first[v] < 0) first[v] = (int64_t)k;
+    });
+  std::vector<std::vector<size_t>> before(code.size());
+  std::vector<char> moved(code.size(), 0);
+  for (size_t k = 0; k < code.size(); k++) {
+    const VInstr& c = code[k];
+    if ((c.op == K_COORD || c.op == K_CONST) && c.dst < nv && first[c.dst] > (int64_t)k) {
+      before[(size_t)first[c.dst]].push_back(k);
+      moved[k] = 1;
+    }
+  }
+  std::vector<VInstr> out;
+  out.reserve(code.size());
+  for (size_t k = 0; k < code.size(); k++) {
+    for (size_t m : before[k]) out.push_back(code[m]);
+    if (!moved[k]) out.push_back(code[k]);
+  }
+  return out;
+}
+
 std::vector<VInstr> fuse_asserts(const std::vector<VInstr>& code, size_t nv) {
   static const bool on = [] {
     const char* g = getenv("MYTHGPU_INTERP_FUSE");
@@ -308,31 +355,46 @@ void allocate(const std::vector<VInstr>& vlist, const std::vector<uint32_t>& vwi
   }
   // the interpreter's slot code: superinstructions, then liveness and slots
   // (slot_list: a different program with the same verdicts for the interpreter, e.g. narrowed)
-  const std::vector<VInstr> code = fuse_asserts(slot_list ? *slot_list : vlist, nv);
-  out.n_hoisted = 0;
-  out.value_words = assign_slots(code, 0, vwidth, out.code, out.aux);
-  // literals do not change from one candidate to the next: with the K_CONSTs first and their slots
-  // kept to the end, the interpreter writes them once per thread instead of once per candidate —
-  // unless that makes the value file larger (fewer waves per CU cost more than the CONSTs: C2 was
-  // 13 % slower with two pinned 256-bit literals).  MYTHGPU_INTERP_HOIST=0: never
+  const std::vector<VInstr> fused = fuse_asserts(slot_list ? *slot_list : vlist, nv);
+  // coordinates (and literals) sunk to just before their first use: a COORD has no inputs (the
+  // generator regenerates a COPY's source itself), so its value need not sit in the value file
+  // from the top of the program — the file is what limits the interpreter's waves per CU — and a
+  // wave that stops at an earlier assert never generates it.  MYTHGPU_INTERP_SINK=0: in place
+  static const bool sink_on = [] {
+    const char* g = getenv("MYTHGPU_INTERP_SINK");
+    return !(g && g[0] == '0');
+  }();
+  // the smallest value file over {as is, sunk} x {literals in place, hoisted}; ties prefer sunk
+  // and hoisted.  Literals do not change from one candidate to the next: with the K_CONSTs first
+  // and their slots kept to the end, the interpreter writes them once per thread instead of once
+  // per candidate — unless that makes the value file larger (fewer waves per CU cost more than the
+  // CONSTs: C2 was 13 % slower with two pinned 256-bit literals).  MYTHGPU_INTERP_HOIST=0: never
   static const bool hoist = [] {
     const char* g = getenv("MYTHGPU_INTERP_HOIST");
     return !(g && g[0] == '0');
   }();
-  if (hoist) {
-    std::vector<VInstr> h = code;
-    std::stable_partition(h.begin(), h.end(), [](const VInstr& c) { return c.op == K_CONST; });
-    uint32_t nh = 0;
-    while (nh < h.size() && h[nh].op == K_CONST) nh++;
-    if (nh) {
+  std::vector<std::vector<VInstr>> orders;
+  if (sink_on) orders.push_back(sink_inputs(fused, nv));
+  orders.push_back(fused);
+  bool have = false;
+  for (const auto& code : orders) {
+    for (int hz = hoist ? 1 : 0; hz >= 0; hz--) {
+      std::vector<VInstr> h = code;
+      uint32_t nh = 0;
+      if (hz) {
+        std::stable_partition(h.begin(), h.end(), [](const VInstr& c) { return c.op == K_CONST; });
+        while (nh < h.size() && h[nh].op == K_CONST) nh++;
+        if (!nh) continue;
+      }
       std::vector<Instr> hc;
       std::vector<uint32_t> ha;
       const uint32_t words = assign_slots(h, nh, vwidth, hc, ha);
-      if (words <= out.value_words) {
+      if (!have || words < out.value_words) {
         out.code.swap(hc);
         out.aux.swap(ha);
         out.value_words = words;
         out.n_hoisted = nh;
+        have = true;
       }
     }
   }
