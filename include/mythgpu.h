@@ -249,6 +249,7 @@ int mg_program_check_gen(const uint8_t* ssa, size_t len, const uint32_t* gen_blo
  * widths.  buf = NULL: only *out_words. */
 #define MG_SPEC_MAGIC 0x43455053u /* "SPEC" */
 #define MG_SPEC_KEEP_WATCH 1u
+#define MG_SPEC_INTERP 2u     /* the interpreter's program (narrowed literal-tail keys), before slots */
 int mg_program_specialized(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words,
                            uint32_t flags, uint32_t* buf, size_t cap_words, size_t* out_words);
 

@@ -1423,11 +1423,15 @@ int mg_program_specialized(const uint8_t* ssa, size_t len, const uint32_t* gen_b
   rc = specialize_program(base, gen_blob ? &specs : nullptr, gen_blob ? &consts : nullptr, sp, err,
                           (flags & MG_SPEC_KEEP_WATCH) != 0);
   if (rc) return set_err(rc, err);
-  std::vector<uint32_t> w = {MG_SPEC_MAGIC, (uint32_t)sp.vcode.size(), (uint32_t)sp.consts.size(),
-                             (uint32_t)sp.vaux.size(), (uint32_t)sp.vwidth.size(), sp.n_coords};
-  for (const Instr& in : sp.vcode) w.insert(w.end(), &in.op, &in.op + 8);
+  // MG_SPEC_INTERP: the interpreter's program where it differs from the JIT's
+  const bool interp = (flags & MG_SPEC_INTERP) && !sp.ivcode.empty();
+  const std::vector<Instr>& code = interp ? sp.ivcode : sp.vcode;
+  const std::vector<uint32_t>& aux = interp ? sp.ivaux : sp.vaux;
+  std::vector<uint32_t> w = {MG_SPEC_MAGIC, (uint32_t)code.size(), (uint32_t)sp.consts.size(),
+                             (uint32_t)aux.size(), (uint32_t)sp.vwidth.size(), sp.n_coords};
+  for (const Instr& in : code) w.insert(w.end(), &in.op, &in.op + 8);
   w.insert(w.end(), sp.consts.begin(), sp.consts.end());
-  w.insert(w.end(), sp.vaux.begin(), sp.vaux.end());
+  w.insert(w.end(), aux.begin(), aux.end());
   w.insert(w.end(), sp.vwidth.begin(), sp.vwidth.end());
   if (out_words) *out_words = w.size();
   if (buf == nullptr || cap_words < w.size()) return buf == nullptr ? MG_OK : set_err(MG_E_INVALID, "buffer too small");

@@ -355,6 +355,17 @@ void allocate(const std::vector<VInstr>& vlist, const std::vector<uint32_t>& vwi
   }
   // the interpreter's slot code: superinstructions, then liveness and slots
   // (slot_list: a different program with the same verdicts for the interpreter, e.g. narrowed)
+  out.ivcode.clear();
+  out.ivaux.clear();
+  if (slot_list)
+    for (const VInstr& c : *slot_list) {
+      Instr vi{c.op, c.wd, c.dst, c.a, c.b, c.c, c.p0, c.p1};
+      if (c.op == K_LOOKUP) {
+        vi.p1 = (uint32_t)out.ivaux.size();
+        for (uint32_t v : c.prior) out.ivaux.push_back(v);
+      }
+      out.ivcode.push_back(vi);
+    }
   const std::vector<VInstr> fused = fuse_asserts(slot_list ? *slot_list : vlist, nv);
   // coordinates (and literals) sunk to just before their first use: a COORD has no inputs (the
   // generator regenerates a COPY's source itself), so its value need not sit in the value file
@@ -1953,17 +1964,23 @@ namespace mg {
 // interpreter and JIT kernels with the C restatement, which runs the full program).
 namespace {
 
-// Keys with a shared literal tail.  LASER addresses a mapping entry as keccak(Concat(key, slot))
-// with a literal slot, so the UF sites' preimages are 512-bit CONCATs whose low 256 bits are the
-// same literal everywhere: the site LOOKUPs compare them, the inverse LOOKUPs return them and
-// the injectivity asserts compare those with EQ.  Where every value in such a comparison is
-// CONCAT(h, T) with one literal T, the comparison is the same on the h parts: LOOKUP keys and EQ
-// operands are narrowed to h, a LOOKUP / ITE whose every candidate value is CONCAT(h, T) gets a
-// narrow twin returning h.  The wide CONCATs then die.  Same verdicts (x:T == y:T iff x == y);
-// the interpreter's value file loses half of every such key (C2: 112 -> 72 words per lane, i.e.
-// more waves per CU), the JIT half of the limbs it selects.  MYTHGPU_NARROW_TAILS=0: off.
+// Keys with literal tails.  LASER addresses a mapping entry as keccak(Concat(key, slot)) with a
+// literal slot, so the UF sites' preimages are 512-bit CONCATs whose low 256 bits are literals:
+// the site LOOKUPs compare them, the inverse LOOKUPs return them and the injectivity asserts
+// compare those with EQ.  A value that is CONCAT(h, T) with a literal T is carried as the pair
+// (h, tail id): the id is a small number per distinct literal tail, itself a literal or (through
+// a LOOKUP / ITE over values with different tails) a 32-bit value.  Then
+//   EQ(x, y)            -> EQ(h_x, h_y), AND EQ(id_x, id_y) unless both ids are literals (equal:
+//                          dropped; different: the EQ is the literal false);
+//   LOOKUP / ITE values -> narrow twins over the h parts (and over the ids if they differ);
+//   LOOKUP keys         -> the h parts, where every key has the same literal tail.
+// x:T == y:U iff x == y and T == U, so every verdict is unchanged; the wide CONCATs and LOOKUPs
+// die where nothing else reads them.  The interpreter's value file loses half of every such key
+// (C2: 112 -> 80 words per lane, so more waves per CU); the JIT half the limbs it selects.
+// MYTHGPU_NARROW_TAILS=0: off.  Returns the wide values that got a narrow twin.
 std::vector<uint32_t> narrow_literal_tails(std::vector<VInstr>& code, std::vector<uint32_t>& vwidth,
-                                           const std::vector<uint32_t>& consts) {
+                                           std::vector<uint32_t>& consts, bool& changed) {
+  changed = false;
   static const bool on = [] {
     const char* g = getenv("MYTHGPU_NARROW_TAILS");
     return !(g && g[0] == '0');
@@ -1971,36 +1988,75 @@ std::vector<uint32_t> narrow_literal_tails(std::vector<VInstr>& code, std::vecto
   std::vector<uint32_t> twinned;  // wide values that got a narrow twin
   if (!on) return twinned;
   const uint32_t NONE = MG_NONE;
-  std::map<uint32_t, std::string> lit;  // K_CONST value id -> its literal (width + words)
+  std::map<uint32_t, std::string> lit;    // K_CONST value id -> its literal (width + words)
+  std::map<std::string, uint32_t> tails;  // literal tail -> its id
+  std::map<uint32_t, uint32_t> tid_vid;   // tail id -> the value id of its 32-bit literal
   struct Split {
     uint32_t h;
-    std::string t;
+    uint32_t t;     // value id of the tail id (32 bits)
+    int64_t tlit;   // the tail id when it is a literal, else -1
   };
-  std::map<uint32_t, Split> split;  // value id -> (h, T) with value == h:T
-  auto same = [&](const Split& x, const Split& y) {
-    return x.t == y.t && vwidth[x.h] == vwidth[y.h];
-  };
-  std::vector<VInstr> add;  // narrow twins, inserted right after their wide instruction
+  std::map<uint32_t, Split> split;  // value id -> (h, tail id) with value == h:tail
   std::vector<VInstr> outc;
   outc.reserve(code.size() + 8);
+  auto fresh = [&](uint32_t w) {
+    vwidth.push_back(w);
+    return (uint32_t)(vwidth.size() - 1);
+  };
+  auto literal = [&](uint32_t w, uint32_t word) {  // a new K_CONST of width w <= 32
+    const uint32_t v = fresh(w), off = (uint32_t)consts.size();
+    consts.push_back(word);
+    outc.push_back(VInstr{K_CONST, w, v, NONE, NONE, NONE, off, 0, {}});
+    return v;
+  };
+  auto tid_of = [&](const std::string& t) {
+    auto it = tails.find(t);
+    const uint32_t id = it != tails.end() ? it->second : (uint32_t)tails.size();
+    if (it == tails.end()) tails[t] = id;
+    auto iv = tid_vid.find(id);
+    if (iv != tid_vid.end()) return Split{NONE, iv->second, (int64_t)id};
+    const uint32_t v = literal(32, id);
+    tid_vid[id] = v;
+    return Split{NONE, v, (int64_t)id};
+  };
+  auto hw = [&](uint32_t v) { return vwidth[split.at(v).h]; };
   for (VInstr& c : code) {
     if (c.op == K_CONST && c.dst != NONE && c.dst < vwidth.size()) {
       std::string t = std::to_string(c.wd) + ":";
       for (uint32_t j = 0; j < Lw(c.wd); j++) t += std::to_string(consts.at(c.p0 + j)) + ",";
       lit[c.dst] = t;
     } else if (c.op == K_CONCAT && c.dst != NONE && lit.count(c.b) && c.a != NONE && c.a < vwidth.size()) {
-      split[c.dst] = Split{c.a, lit[c.b]};
-    } else if (c.op == K_EQ && split.count(c.a) && split.count(c.b) && same(split[c.a], split[c.b])) {
-      const uint32_t ha = split[c.a].h, hb = split[c.b].h;
-      c.a = ha;
-      c.b = hb;
-      c.p1 = vwidth[ha];
+      const std::string t = lit[c.b];
+      const Split id = tid_of(t);
+      outc.push_back(std::move(c));
+      split[outc.back().dst] = Split{outc.back().a, id.t, id.tlit};
+      continue;
+    } else if (c.op == K_EQ && c.dst != NONE && split.count(c.a) && split.count(c.b) && hw(c.a) == hw(c.b)) {
+      const Split x = split[c.a], y = split[c.b];
+      changed = true;
+      if (x.tlit >= 0 && y.tlit >= 0 && x.tlit != y.tlit) {  // different literal tails: never equal
+        const uint32_t off = (uint32_t)consts.size();
+        consts.push_back(0u);
+        outc.push_back(VInstr{K_CONST, 1, c.dst, NONE, NONE, NONE, off, 0, {}});
+        continue;
+      }
+      c.a = x.h;
+      c.b = y.h;
+      c.p1 = vwidth[x.h];
+      if (!(x.tlit >= 0 && y.tlit >= 0)) {  // computed tail ids: both halves must agree
+        const uint32_t eh = fresh(1), et = fresh(1);
+        outc.push_back(VInstr{K_EQ, 1, eh, x.h, y.h, NONE, 0, vwidth[x.h], {}});
+        outc.push_back(VInstr{K_EQ, 1, et, x.t, y.t, NONE, 0, 32, {}});
+        outc.push_back(VInstr{K_AND, 1, c.dst, eh, et, NONE, 0, 1, {}});
+        continue;
+      }
     } else if (c.op == K_LOOKUP) {
-      // keys: the site key and every prior key
-      bool keys = split.count(c.a) > 0;
+      // keys: the site key and every prior key, all with one literal tail
+      bool keys = split.count(c.a) && split[c.a].tlit >= 0;
       for (size_t q = 0; keys && q < c.prior.size(); q += 2)
-        keys = split.count(c.prior[q]) && same(split[c.prior[q]], split[c.a]);
+        keys = split.count(c.prior[q]) && split[c.prior[q]].tlit == split[c.a].tlit && hw(c.prior[q]) == hw(c.a);
       if (keys) {
+        changed = true;
         const Split ka = split[c.a];
         for (size_t q = 0; q < c.prior.size(); q += 2) c.prior[q] = split[c.prior[q]].h;
         c.a = ka.h;
@@ -2008,39 +2064,64 @@ std::vector<uint32_t> narrow_literal_tails(std::vector<VInstr>& code, std::vecto
       }
       // values: the default and every prior value
       bool vals = c.dst != NONE && split.count(c.p0);
-      for (size_t q = 1; vals && q < c.prior.size(); q += 2)
-        vals = split.count(c.prior[q]) && same(split[c.prior[q]], split[c.p0]);
+      bool one_tail = vals;
+      for (size_t q = 1; vals && q < c.prior.size(); q += 2) {
+        vals = split.count(c.prior[q]) && hw(c.prior[q]) == hw(c.p0);
+        one_tail = one_tail && vals && split[c.prior[q]].tlit >= 0 && split[c.prior[q]].tlit == split[c.p0].tlit;
+      }
+      one_tail = one_tail && split[c.p0].tlit >= 0;
       if (vals) {
         const Split d0 = split[c.p0];
         VInstr n = c;
-        n.dst = (uint32_t)vwidth.size();
-        vwidth.push_back(vwidth[d0.h]);
+        n.dst = fresh(vwidth[d0.h]);
         n.wd = vwidth[d0.h];
         n.p0 = d0.h;
         for (size_t q = 1; q < n.prior.size(); q += 2) n.prior[q] = split[n.prior[q]].h;
-        split[c.dst] = Split{n.dst, d0.t};
-        twinned.push_back(c.dst);
+        Split r{n.dst, d0.t, d0.tlit};
         outc.push_back(c);
         outc.push_back(std::move(n));
+        if (!one_tail) {
+          VInstr t = c;
+          t.dst = fresh(32);
+          t.wd = 32;
+          t.p0 = d0.t;
+          for (size_t q = 1; q < t.prior.size(); q += 2) t.prior[q] = split[t.prior[q]].t;
+          r.t = t.dst;
+          r.tlit = -1;
+          outc.push_back(std::move(t));
+        }
+        split[c.dst] = r;
+        twinned.push_back(c.dst);
         continue;
       }
-    } else if (c.op == K_ITE && c.dst != NONE && split.count(c.b) && split.count(c.c) &&
-               same(split[c.b], split[c.c])) {
+    } else if (c.op == K_ITE && c.dst != NONE && split.count(c.b) && split.count(c.c) && hw(c.b) == hw(c.c)) {
+      const Split x = split[c.b], y = split[c.c];
       VInstr n = c;
-      n.dst = (uint32_t)vwidth.size();
-      vwidth.push_back(vwidth[split[c.b].h]);
-      n.wd = vwidth[n.dst];
-      n.b = split[c.b].h;
-      n.c = split[c.c].h;
-      split[c.dst] = Split{n.dst, split[c.b].t};
-      twinned.push_back(c.dst);
+      n.dst = fresh(vwidth[x.h]);
+      n.wd = vwidth[x.h];
+      n.b = x.h;
+      n.c = y.h;
+      Split r{n.dst, x.t, x.tlit};
       outc.push_back(c);
       outc.push_back(std::move(n));
+      if (!(x.tlit >= 0 && x.tlit == y.tlit)) {
+        VInstr t = c;
+        t.dst = fresh(32);
+        t.wd = 32;
+        t.b = x.t;
+        t.c = y.t;
+        r.t = t.dst;
+        r.tlit = -1;
+        outc.push_back(std::move(t));
+      }
+      split[c.dst] = r;
+      twinned.push_back(c.dst);
       continue;
     }
     outc.push_back(std::move(c));
   }
   code.swap(outc);
+  changed = changed || !twinned.empty();
   return twinned;
 }
 
@@ -2114,7 +2195,8 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
       code.push_back(std::move(v));
     }
     std::vector<VInstr> wide = code;
-    const std::vector<uint32_t> twinned = narrow_literal_tails(code, vwidth, out.consts);
+    bool narrowed = false;
+    (void)narrow_literal_tails(code, vwidth, out.consts, narrowed);
     const size_t nw = vwidth.size();  // with the narrow twins' values
     // dead code: keep asserts (unless dropped: the model read-back of a known hit), watches
     // and whatever they transitively use
@@ -2149,18 +2231,12 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
       return kept;
     };
     std::vector<VInstr> kept = dce(code);
-    // the JIT folds literal limbs by itself, so it gains from the narrow form only where the wide
-    // values die; where a wide one stays live (a LOOKUP over keys with different literal tails
-    // still reads it: C4) its narrow twin is extra work there, and the JIT keeps the wide program
-    bool wide_live = false;
-    if (!twinned.empty()) {
-      std::vector<char> tw(nw, 0);
-      for (uint32_t v : twinned) tw[v] = 1;
-      for (const VInstr& c : kept) wide_live = wide_live || (c.dst != NONE && c.dst < nw && tw[c.dst]);
-    }
+    // the JIT keeps the wide program: it folds literal limbs by itself, and a wide value that stays
+    // live next to its narrow twin (a LOOKUP over keys with different tails still reads it: C4) is
+    // extra work there; measured on the compiled kernels: C2 -1.9 %, C4 +0.4 % narrowed
     const uint64_t ops = in.limb_ops;  // algorithmic work is the query's, not what survives
     out.limb_ops = 0;
-    if (wide_live) {
+    if (narrowed) {
       std::vector<VInstr> kept_wide = dce(wide);
       allocate(kept_wide, vwidth, out, &kept);
     } else {

@@ -69,6 +69,10 @@ struct Lowered {
   std::vector<Instr> vcode;           // LOOKUP: p0 = default vid, p1 = offset into vaux
   std::vector<uint32_t> vaux;         // LOOKUP prior lists: pairs (key vid, value vid)
   std::vector<uint32_t> vwidth;       // width of each value id
+  // the interpreter's SSA program where it differs from vcode (narrowed literal-tail keys),
+  // before fusion and slots; empty: the same as vcode
+  std::vector<Instr> ivcode;
+  std::vector<uint32_t> ivaux;
 };
 
 // Parse + validate + lower. Returns MG_OK or an MG_E_* code with `err` set.

@@ -189,17 +189,20 @@ def check_program_gen(blob: bytes, gen_blob: np.ndarray) -> ProgramInfo:
 
 MG_SPEC_MAGIC = 0x43455053
 MG_SPEC_KEEP_WATCH = 1
+MG_SPEC_INTERP = 2
 
 
-def specialized_program(blob: bytes, gen_blob: Optional[np.ndarray] = None, keep_watch: bool = False) -> dict:
+def specialized_program(blob: bytes, gen_blob: Optional[np.ndarray] = None, keep_watch: bool = False,
+                        interp: bool = False) -> dict:
     """Host-only ``mg_program_specialized``: the lowered, specialised program a search (with a
     generator) or an eval (without) runs, in SSA form — ``code`` (n x 8 uint32:
-    op, width, dst, a, b, c, p0, p1), ``consts``, ``aux``, ``widths``, ``n_coords``."""
+    op, width, dst, a, b, c, p0, p1), ``consts``, ``aux``, ``widths``, ``n_coords``.  ``interp``:
+    the interpreter's program (literal-tail keys narrowed) instead of the compiled kernel's."""
     lib = load_library()
     g = None if gen_blob is None else np.ascontiguousarray(gen_blob, dtype=np.uint32)
     gp = _ptr(g, C.c_uint32) if g is not None else None
     gn = 0 if g is None else g.size
-    flags = MG_SPEC_KEEP_WATCH if keep_watch else 0
+    flags = (MG_SPEC_KEEP_WATCH if keep_watch else 0) | (MG_SPEC_INTERP if interp else 0)
     n = C.c_size_t()
     _check(lib.mg_program_specialized(_u8(blob), len(blob), gp, gn, flags, None, 0, C.byref(n)))
     w = np.zeros(n.value, dtype=np.uint32)

@@ -31,13 +31,15 @@ def _coord_words(P):
     return sum(ssa.limbs(c.width) for c in P.coords)
 
 
+@pytest.mark.parametrize("interp", [False, True], ids=["jit", "interp"])
 @pytest.mark.parametrize("keep_watch", [False, True], ids=["search", "watch"])
 @pytest.mark.parametrize("name", sorted(workloads.WORKLOADS), ids=workloads.test_id)
-def test_specialised_search_program_keeps_verdicts(name, keep_watch):
+def test_specialised_search_program_keeps_verdicts(name, keep_watch, interp):
+    """``interp``: the interpreter's program (literal-tail keys narrowed), else the compiled kernel's."""
     rng = random.Random(zlib.crc32(name.encode()) ^ 0x5BEC)
     P, blob = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
     pb = P.to_bytes()
-    spec = native.specialized_program(pb, blob, keep_watch=keep_watch)
+    spec = native.specialized_program(pb, blob, keep_watch=keep_watch, interp=interp)
     widths = [c.width for c in P.coords]
     n = N if name != "sha3_keyed_mapping" else 96
     for start in (0, rng.getrandbits(63) | 1):
@@ -110,13 +112,16 @@ def test_literal_tail_keys_are_narrowed():
     cs = literal_tail_query()
     P, blob = search.prepare([c.raw for c in cs])
     pb = P.to_bytes()
-    spec = native.specialized_program(pb, blob)
+    spec = native.specialized_program(pb, blob, interp=True)
     eq512 = [r for r in spec["code"] if int(r[0]) == kops.K_EQ and int(r[7]) == 512]
     assert not eq512, "a comparison of literal-tail keys was not narrowed"
+    wide = native.specialized_program(pb, blob)  # the compiled kernel keeps the wide program
+    assert [r for r in wide["code"] if int(r[0]) == kops.K_EQ and int(r[7]) == 512]
     rng = random.Random(0x7A11)
     for start in (0, rng.getrandbits(63) | 1):
         seed = rng.getrandbits(32)
         soa = cport.gen_soa(pb, blob, seed, start, N, _coord_words(P))
         want = cport.search(pb, blob, seed, start, N, threads=4, verdicts=True)[2]
-        got = kops.verdicts(spec, soa, [c.width for c in P.coords], N)
-        assert np.array_equal(got, want)
+        for prog in (spec, wide):
+            got = kops.verdicts(prog, soa, [c.width for c in P.coords], N)
+            assert np.array_equal(got, want)

@@ -1,0 +1,13 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r3r_pytest.log 2>&1 || { tail -30 gpurun_out/r3r_pytest.log; exit 1; }
+tail -2 gpurun_out/r3r_pytest.log
+: > gpurun_out/r3r_interp_ab.jsonl
+for V in "MYTHGPU_NARROW_TAILS=1" "MYTHGPU_NARROW_TAILS=0" "MYTHGPU_INTERP_LDS_MAX=192"; do
+  for W in etherstore_reentrancy walletlibrary_kill token_transfer_underflow; do
+    env $V timeout -k 10 120 python bench.py --workload $W --engine interp --candidates 4194304 --no-stream --no-eval --no-cpu-baseline --no-ttfm > gpurun_out/r3r_i.json 2>/dev/null || exit 1
+    python3 -c "import json; d=json.load(open('gpurun_out/r3r_i.json')); print(json.dumps({'engine':'interp','workload':'$W','env':'$V','value':d['value']}))" >> gpurun_out/r3r_interp_ab.jsonl
+  done
+done
+cat gpurun_out/r3r_interp_ab.jsonl
+bash tools/r3_ab.sh r3r "narrow=" "wide=MYTHGPU_NARROW_TAILS=0" && cat gpurun_out/r3r_ab.jsonl
