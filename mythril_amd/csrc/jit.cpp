@@ -14,6 +14,7 @@
 
 #include <amd_comgr/amd_comgr.h>
 
+#include <algorithm>
 #include <chrono>
 #include <mutex>
 
@@ -315,6 +316,73 @@ struct Gen {
   std::map<uint32_t, std::string> coord_var;  // coordinate -> prefix of its generated (final) limbs
   int tmp_id = 0;
 
+  // Dictionary gathers one group ahead (search kernel).  A MIXED coordinate whose DICT alternative
+  // gathers from global memory loads its entry where its value is needed, so a wave waits out the
+  // load every group it chose DICT (C3: two 256-bit gathers from a 74-entry table, half the wave
+  // cycles waiting).  Instead the group loop carries the next group's key: at the top of group k
+  // the wave hashes group k+1's choice word and, if it chose DICT, its lanes' entries and issues
+  // the loads; group k's own entries arrived during group k-1.  Same values (a pure function of
+  // group and coordinate), one fmix64 per group as before.  Opt-in (MYTHGPU_JIT_PREFETCH=1): C3
+  // measured 12 % SLOWER with it (profiles/r03_ab_prefetch.jsonl) — the loop-carried entries cost a
+  // register copy per limb and group, and the gathers were not what C3 waits on.
+  std::vector<uint32_t> pf;  // coordinates prefetched
+  bool pf_active = false;    // emitting the search kernel's body: read the prefetched registers
+  void plan_prefetch() {
+    pf.clear();
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_PREFETCH");
+      return g && g[0] == '1';
+    }();
+    if (!specs || !on || lane_keys()) return;
+    for (uint32_t c = 0; c < specs->size() && c < P.coord_width.size(); c++) {
+      const GenSpec& sp = (*specs)[c];
+      if ((sp.kind & 0xFFu) != MG_GEN_MIXED || coord_dead(c)) continue;
+      const uint32_t pd = sp.p[1] ? (sp.p[2] >> 16) : 0u, n = sp.p[1], w = P.coord_width[c];
+      if (!pd || n <= select_dict_max() || Lw(w) > 8 || dict_lds.count(sp.p[0])) continue;
+      if (!packed_dict(sp.p[0], n, w, "e").empty()) continue;
+      pf.push_back(c);
+    }
+  }
+  void emit_prefetch_decls() {
+    for (uint32_t c : pf) {
+      o << "  uint32_t pfh" << c << " = 0u";
+      for (uint32_t j = 0; j < Lw(P.coord_width[c]); j++) o << ", pf" << c << "_" << j << " = 0u";
+      o << ";\n";
+    }
+  }
+  // the loads for the group whose key is Gn
+  void emit_prefetch(const char* Gn) {
+    if (pf.empty()) return;
+    o << "  { GKeys kn; { const uint64_t K = " << Gn << " ^ LK;\n"
+         "    kn.klo = (uint32_t)K; kn.khi = (uint32_t)(K >> 32); kn.glo = (uint32_t)" << Gn
+      << "; kn.ghi = (uint32_t)(" << Gn << " >> 32); }\n";
+    for (uint32_t c : pf) {
+      const GenSpec& sp = (*specs)[c];
+      const uint32_t pc = sp.p[3] != MG_NONE ? (sp.p[2] & 0xFFFFu) : 0u;
+      const uint32_t pd = sp.p[2] >> 16;
+      const uint32_t lo = pc << 16, hi = pc + pd;
+      o << "    { const uint32_t wsn = gwsel(kn, " << c << "u);\n"
+        << "      if (" << (pc ? "wsn >= " + hex(lo) : std::string("true")) << " && "
+        << (hi >= 65536u ? std::string("true") : "wsn < " + hex(hi << 16)) << ") {\n"
+        << "        pfh" << c << " = grnd(kn, " << c << "u, 0xFFFFu);\n"
+        << "        const uint32_t e = ((pfh" << c << " >> 16) * " << sp.p[1] << "u) >> 16;\n";
+      const std::string pre = "pf" + std::to_string(c) + "_";
+      dict_limbs(sp.p[0], sp.p[1], P.coord_width[c], "e", [&](uint32_t j) { return pre + std::to_string(j); },
+                 "        ");
+      o << "      } }\n";
+    }
+    o << "  }\n";
+  }
+  // at the top of a group: this group's prefetched values, before the next group's loads overwrite them
+  void emit_prefetch_take() {
+    for (uint32_t c : pf) {
+      o << "  const uint32_t ch" << c << " = pfh" << c;
+      for (uint32_t j = 0; j < Lw(P.coord_width[c]); j++) o << ", cv" << c << "_" << j << " = pf" << c << "_" << j;
+      o << ";\n";
+    }
+  }
+  bool prefetched(uint32_t c) const { return pf_active && std::find(pf.begin(), pf.end(), c) != pf.end(); }
+
   std::string gen_coord_value(uint32_t c) {
     auto it = coord_var.find(c);
     if (it != coord_var.end()) return it->second;
@@ -460,9 +528,14 @@ struct Gen {
         }
         if (pd) {
           branch(below(pc + pd));
-          o << "    " << hdecl << "\n";
-          o << "    const uint32_t e = ((h >> 16) * " << sp.p[1] << "u) >> 16;\n";
-          dict_limbs(sp.p[0], sp.p[1], width, "e", lim, "    ");
+          if (prefetched(c)) {  // loaded one group ahead (plan_prefetch)
+            o << "    const uint32_t h = ch" << c << ";\n";
+            for (uint32_t j = 0; j < L; j++) o << "    " << lim(j) << " = cv" << c << "_" << j << ";\n";
+          } else {
+            o << "    " << hdecl << "\n";
+            o << "    const uint32_t e = ((h >> 16) * " << sp.p[1] << "u) >> 16;\n";
+            dict_limbs(sp.p[0], sp.p[1], width, "e", lim, "    ");
+          }
           delta(true);
           finish();
         }
@@ -990,8 +1063,14 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "      ? (uint32_t)gleft / (uint32_t)gstride + 1u : (uint32_t)(gleft / gstride + 1u);\n"
        "  const uint32_t kpf = (g0 == 0u && (start & 63u)) ? 0u : 0xFFFFFFFFu;\n"
        "  const uint32_t kpl = ((end & 63u) && nk && g0 + (uint64_t)(nk - 1u) * gstride == ngroups - 1u) ? nk - 1u : 0xFFFFFFFFu;\n"
-       "  uint64_t gbase = a0 + (g0 << 6);\n"
-       "  for (uint32_t kk = 0u; kk < nk; kk++, gbase += gstride << 6) {\n"
+       "  uint64_t gbase = a0 + (g0 << 6);\n";
+  g.plan_prefetch();
+  if (!g.pf.empty()) {
+    o << "  uint64_t Gn = fmix64((gbase >> 6) ^ sg);  // the key of the wave's next group (prefetch)\n";
+    g.emit_prefetch_decls();
+    g.emit_prefetch("Gn");
+  }
+  o << "  for (uint32_t kk = 0u; kk < nk; kk++, gbase += gstride << 6) {\n"
        "  if (early) {\n"
        "    const unsigned long long cur = __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
        "    const uint64_t cu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) | "
@@ -1001,13 +1080,22 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  // a group wholly inside [start, end) (every group of a call but its first and last) needs no\n"
        "  // per-lane bounds\n"
        "  const bool full = kk != kpf && kk != kpl;\n";
-  g.emit_group_keys("kk", "g0 + (uint64_t)kk * gstride", "gstride");
+  if (g.pf.empty()) {
+    g.emit_group_keys("kk", "g0 + (uint64_t)kk * gstride", "gstride");
+  } else {
+    o << "  const uint64_t G = Gn;\n";
+    g.emit_prefetch_take();
+    o << "  Gn = fmix64(((gbase >> 6) + gstride) ^ sg);\n";
+    g.emit_prefetch("Gn");
+  }
   o << "  GKeys ky;\n"
        "  { const uint64_t K = G ^ LK;\n"
        "    ky.klo = (uint32_t)K; ky.khi = (uint32_t)(K >> 32); ky.glo = (uint32_t)G; ky.ghi = (uint32_t)(G >> 32); }\n"
        "  uint32_t verdict = 1u;\n";
   g.decls();
+  g.pf_active = true;
   g.body(true);
+  g.pf_active = false;
   o << "  mg_next:\n"
        "  { unsigned long long m = __ballot(verdict != 0u);\n"
        "    if (!full) { const uint64_t idx = gbase + lane; m &= __ballot(idx >= start && idx < end); }\n"
