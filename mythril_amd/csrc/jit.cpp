@@ -1040,7 +1040,8 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        ;
   g.emit_dict_prologue();
   o << "  __shared__ unsigned long long mg_blk[2];  // the block's first hit and hit count\n"
-       "  if (tid == 0u) { mg_blk[0] = ~0ull; mg_blk[1] = 0ull; }\n"
+       "  __shared__ uint32_t mg_blk_n;  // waves of the block that have added theirs\n"
+       "  if (tid == 0u) { mg_blk[0] = ~0ull; mg_blk[1] = 0ull; mg_blk_n = 0u; }\n"
        "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"workgroup\");\n"
        "  __builtin_amdgcn_s_barrier();\n"
        "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"workgroup\");\n";
@@ -1109,20 +1110,20 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "      }\n"
        "    } }\n"
        "  }\n"
-       "  // the block's four waves combine in LDS, then one thread publishes: the end-of-wave global\n"
-       "  // atomics on one address from every wave serialised in the launch's tail; a first hit that\n"
-       "  // cannot lower the current minimum is not published at all\n"
+       "  // the block's four waves combine in LDS and the last of them to finish publishes: the\n"
+       "  // end-of-wave global atomics on one address from every wave serialised in the launch's tail;\n"
+       "  // a first hit that cannot lower the current minimum is not published at all.  No barrier:\n"
+       "  // issue arbitration favours a SIMD's oldest wave, so a block's waves finish staggered and\n"
+       "  // the first ones would idle there until the last\n"
        "  if (lane == 0u) {\n"
        "    if (wave_best != ~0ull) __hip_atomic_fetch_min(&mg_blk[0], (unsigned long long)wave_best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
        "    if (wave_hits) __hip_atomic_fetch_add(&mg_blk[1], (unsigned long long)wave_hits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
-       "  }\n"
-       "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"workgroup\");\n"
-       "  __builtin_amdgcn_s_barrier();\n"
-       "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"workgroup\");\n"
-       "  if (tid == 0u) {\n"
-       "    const unsigned long long bb = mg_blk[0], bh = mg_blk[1];\n"
-       "    if (bb != ~0ull && bb < __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(hit, bb);\n"
-       "    if (bh) atomicAdd(hit + 1, bh);\n"
+       "    if (__hip_atomic_fetch_add(&mg_blk_n, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 3u) {\n"
+       "      const unsigned long long bb = __hip_atomic_load(&mg_blk[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
+       "      const unsigned long long bh = __hip_atomic_load(&mg_blk[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
+       "      if (bb != ~0ull && bb < __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(hit, bb);\n"
+       "      if (bh) atomicAdd(hit + 1, bh);\n"
+       "    }\n"
        "  }\n}\n\n";
   }
   if (want_gen) {
