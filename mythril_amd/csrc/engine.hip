@@ -43,6 +43,13 @@ constexpr int kWave = 64;
 constexpr size_t kCaptureBytes = 64ull << 20;  // watch-row capture buffer (mg_search), per device
 // value file in LDS up to this many words per lane (160: 40 KiB per wave), else in global memory;
 // MYTHGPU_INTERP_LDS_MAX overrides (at most 255: 64 KiB per one-wave block)
+// The hit buffer: [0] the first hit, [1] a hit count, then kHitStripes more counts, one per
+// 128-byte line (u64 index kHitStride * (1 + s)).  A search kernel adds a wave's (or block's) hits
+// to the stripe of its block: every wave of a launch finishes in its last few percent and their
+// adds on one address serialised there; the host sums the stripes.
+constexpr uint32_t kHitStripes = 16, kHitStride = 16;
+constexpr uint32_t kHitWords = kHitStride * (1 + kHitStripes);
+
 static uint32_t lds_words_max() {
   static const uint32_t n = [] {
     const char* g = getenv("MYTHGPU_INTERP_LDS_MAX");
@@ -692,8 +699,12 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
     }
   }
   if (MODE == MODE_SEARCH && threadIdx.x == 0) {
-    if (wave_best != ~0ull) atomicMin(k.first_hit, (unsigned long long)wave_best);
-    if (wave_hits) atomicAdd(k.hits, (unsigned long long)wave_hits);
+    // a first hit that cannot lower the current minimum is not published; the count goes to the
+    // block's stripe (kHitStripes)
+    if (wave_best != ~0ull &&
+        wave_best < __hip_atomic_load(k.first_hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMin(k.first_hit, (unsigned long long)wave_best);
+    if (wave_hits) atomicAdd(k.hits + kHitStride * (1u + (blockIdx.x % kHitStripes)) - 1u, (unsigned long long)wave_hits);
   }
 }
 
@@ -1129,15 +1140,15 @@ static int launch_wait(Engine& e, mg_stats_t& st, uint64_t count) {
 
 // reset e's hit buffer before a search launch (async, from pinned memory)
 static int arm_hits(Engine& e) {
-  e.h_hit[0] = ~0ull;
-  e.h_hit[1] = 0ull;
-  HIPCHK(hipMemcpyAsync(e.d_hit, e.h_hit, 2 * sizeof(unsigned long long), hipMemcpyHostToDevice, e.stream));
+  // h_hit[0, kHitWords): the armed image (first = ~0, counts 0), written once at init
+  HIPCHK(hipMemcpyAsync(e.d_hit, e.h_hit, kHitWords * sizeof(unsigned long long), hipMemcpyHostToDevice, e.stream));
   return MG_OK;
 }
 
 // queue the hit buffer's read-back behind e's last launch (async); collect_hits waits for it
 static int fetch_hits(Engine& e) {
-  HIPCHK(hipMemcpyAsync(e.h_hit + 2, e.d_hit, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e.stream));
+  HIPCHK(hipMemcpyAsync(e.h_hit + kHitWords, e.d_hit, kHitWords * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                        e.stream));
   HIPCHK(hipEventRecord(e.ev2, e.stream));
   return MG_OK;
 }
@@ -1152,8 +1163,10 @@ static int collect_hits(Engine& e, mg_stats_t& st, uint64_t count, unsigned long
   st.kernel_ms_total += ms;
   st.candidates += count;
   st.last_candidates = count;
-  res[0] = e.h_hit[2];
-  res[1] = e.h_hit[3];
+  const unsigned long long* r = e.h_hit + kHitWords;
+  res[0] = r[0];
+  res[1] = r[1];
+  for (uint32_t q = 1; q <= kHitStripes; q++) res[1] += r[kHitStride * q];
   return MG_OK;
 }
 
@@ -1209,8 +1222,10 @@ static int init_dev(Engine& e, int dev) {
   HIPCHK(hipEventCreate(&e.ev0));
   HIPCHK(hipEventCreate(&e.ev1));
   HIPCHK(hipEventCreateWithFlags(&e.ev2, hipEventDisableTiming));
-  HIPCHK(hipMalloc((void**)&e.d_hit, 2 * sizeof(unsigned long long)));
-  HIPCHK(hipHostMalloc((void**)&e.h_hit, 4 * sizeof(unsigned long long), hipHostMallocDefault));
+  HIPCHK(hipMalloc((void**)&e.d_hit, kHitWords * sizeof(unsigned long long)));
+  HIPCHK(hipHostMalloc((void**)&e.h_hit, 2 * kHitWords * sizeof(unsigned long long), hipHostMallocDefault));
+  std::memset(e.h_hit, 0, 2 * kHitWords * sizeof(unsigned long long));
+  e.h_hit[0] = ~0ull;  // the armed image (arm_hits)
   // the model-capture buffer of latency-bound searches (mg_search), allocated up front so that no
   // query's time to first model includes the allocation
   HIPCHK(hipMalloc((void**)&e.d_capture, kCaptureBytes));
@@ -1975,15 +1990,16 @@ namespace mg {
 // `nblk` is the kernel's grid-size argument (the JIT kernels read no dispatch packet)
 static int jit_launch_async(Engine& e, hipFunction_t f, int nb, uint64_t count, void** args, uint32_t& nblk) {
   const uint64_t want = (count + 255) / 256;
-  // MYTHGPU_JIT_BPC (default 32) 256-lane blocks per CU, i.e. 32 waves per SIMD over the
+  // MYTHGPU_JIT_BPC (default 64) 256-lane blocks per CU, i.e. 64 waves per SIMD over the
   // launch, whatever the occupancy (`nb`, unused here: the API answers 4 blocks/CU for a
-  // 52-VGPR kernel the hardware runs 8 deep); the waves loop over aligned index groups.
-  // Measured (tools/grid_sweep.sh, 2^28 candidates): 16/CU leaves a tail where the oldest waves
-  // of each SIMD have finished (C4 -8 %, C5 -3 %, C2 -2 %), 64/CU and more pays per-wave start-up
-  // and end-of-wave atomics (C3 +50 %, C2 +40 % at 128/CU).
+  // 52-VGPR kernel the hardware runs 8 deep); the waves loop over aligned index groups.  Fewer
+  // blocks leave a tail where the oldest waves of each SIMD have finished (16/CU: C4 -8 %, C5 -3 %,
+  // C2 -2 %); more paid per-block start-up and the end-of-block publish, until the block's hits
+  // went to a count stripe with no barrier (profiles/r03_ab_bpc_*.jsonl: 64 vs 32 per CU, kernel
+  // time C2 -2.0 %, C4 -0.9 %, C1 -1.1 %, C3 -0.8 %; before the stripes C3 was 17 % slower at 64).
   static const uint64_t bpc = [] {
     const char* g = getenv("MYTHGPU_JIT_BPC");
-    return (uint64_t)std::max(1, g ? atoi(g) : 32);
+    return (uint64_t)std::max(1, g ? atoi(g) : 64);
   }();
   (void)nb;
   const uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * bpc;

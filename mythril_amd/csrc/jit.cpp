@@ -1122,7 +1122,7 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "      const unsigned long long bb = __hip_atomic_load(&mg_blk[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
        "      const unsigned long long bh = __hip_atomic_load(&mg_blk[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);\n"
        "      if (bb != ~0ull && bb < __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(hit, bb);\n"
-       "      if (bh) atomicAdd(hit + 1, bh);\n"
+       "      if (bh) atomicAdd(hit + 16u * (1u + (bid & 15u)), bh);  // the block's count stripe (engine.hip kHitStripes)\n"
        "    }\n"
        "  }\n}\n\n";
   }
