@@ -314,7 +314,8 @@ uint32_t assign_slots(const std::vector<VInstr>& code, uint32_t n_hoisted, const
     }
     ocode.push_back(in);
     for (uint32_t v : dies[k]) al.release(slot[v], L_of(vwidth[v]));
-    if (getenv("MYTHGPU_DEBUG_ALLOC") && al.high() > dbg_high) {
+    static const bool debug_alloc = getenv("MYTHGPU_DEBUG_ALLOC") != nullptr;
+    if (debug_alloc && al.high() > dbg_high) {
       dbg_high = al.high();
       size_t live = 0;
       std::string s;

@@ -222,3 +222,27 @@ def test_jit_verdicts_at_high_indices():
             eng.jit_free(jh)
             eng.free_gen(gh)
             eng.free(prog)
+
+
+@pytest.mark.parametrize("name", ["suicide_kill", "bectoken_batch_overflow"], ids=workloads.test_id)
+def test_hit_counts_over_many_blocks(engine, name):
+    """A launch of hundreds of blocks: the hit count is summed on the host from 16 count stripes
+    (engine.hip kHitStripes) and the first hit is the minimum over every block's publish — both must
+    equal the C port's over the same 2^18 candidates, for the compiled kernel and the interpreter."""
+    from oracle import cport
+
+    roots = [c.raw for c in workloads.WORKLOADS[name]()]
+    P, blob = search.prepare(roots)
+    prog = engine.load(P.to_bytes())
+    gh = engine.load_gen(prog, blob)
+    jit = engine.jit_compile(prog, gh)
+    try:
+        start, n = (1 << 40) + 12345, 1 << 18
+        want = cport.search(P.to_bytes(), blob, 5, start, n, threads=16)[:2]
+        assert want[1] > 0
+        assert engine.jit_search(jit, 5, start, n, early_exit=False) == want
+        assert engine.search(prog, gh, 5, start, n, early_exit=False) == want
+    finally:
+        engine.jit_free(jit)
+        engine.free_gen(gh)
+        engine.free(prog)
