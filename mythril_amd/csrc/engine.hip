@@ -1085,7 +1085,12 @@ template <int MODE>
 static int launch_async(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   // GEN / SEARCH sweep whole aligned 64-index groups (k_run)
   const uint64_t lanes = MODE == MODE_EVAL ? count : (k.start + count) - (k.start & ~63ull);
-  const uint32_t grid = grid_for(e, lanes, p.lds, p.low.value_words, p.heavy);
+  // A launch of at most two waves per CU (a query's first, latency-bound pass) keeps its value file
+  // in LDS even past lds_words_max() — up to 64 KiB per one-wave block: the words the global
+  // file would fetch from L2 at every operand are what such a launch waits on, and it needs no
+  // occupancy.  Larger launches trade the other way (C4 at 255: 20 % slower).
+  const bool lds = p.lds || (p.low.value_words <= 255u && lanes <= (uint64_t)std::max(e.cu_count, 1) * 2u * kWave);
+  const uint32_t grid = grid_for(e, lanes, lds, p.low.value_words, p.heavy);
   k.sk = seed_lane_key(k.seed);
   k.sg = seed_group_key(k.seed);
   k.code = p.d_code;
@@ -1104,17 +1109,17 @@ static int launch_async(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   }();
   if (prefetch) k.flags |= kFlagPrefetch;
   k.stride = (uint64_t)grid * kWave;
-  if (!p.lds) {
+  if (!lds) {
     const size_t need = (size_t)p.low.value_words * k.stride * 4;
     int rc = ensure_scratch(e, need);
     if (rc) return rc;
     k.scratch = e.d_scratch;
   }
-  const size_t shmem = p.lds ? (size_t)p.low.value_words * kWave * 4 : 0;
+  const size_t shmem = lds ? (size_t)p.low.value_words * kWave * 4 : 0;
   HIPCHK(hipEventRecord(e.ev0, e.stream));
-  if (p.lds && p.heavy)
+  if (lds && p.heavy)
     hipLaunchKernelGGL((k_run<VFLds, MODE, true>), dim3(grid), dim3(kWave), shmem, e.stream, k);
-  else if (p.lds)
+  else if (lds)
     hipLaunchKernelGGL((k_run<VFLds, MODE, false>), dim3(grid), dim3(kWave), shmem, e.stream, k);
   else if (p.heavy)
     hipLaunchKernelGGL((k_run<VFGlobal, MODE, true>), dim3(grid), dim3(kWave), 0, e.stream, k);

@@ -388,6 +388,7 @@ void allocate(const std::vector<VInstr>& vlist, const std::vector<uint32_t>& vwi
   std::vector<std::vector<VInstr>> orders;
   if (sink_on) orders.push_back(sink_inputs(fused, nv));
   orders.push_back(fused);
+
   bool have = false;
   for (const auto& code : orders) {
     for (int hz = hoist ? 1 : 0; hz >= 0; hz--) {
@@ -411,6 +412,8 @@ void allocate(const std::vector<VInstr>& vlist, const std::vector<uint32_t>& vwi
     }
   }
   out.vwidth = vwidth;
+  static const bool debug_words = getenv("MYTHGPU_DEBUG_ALLOC") != nullptr;
+  if (debug_words) fprintf(stderr, "value_words %u n_hoisted %u instrs %zu\n", out.value_words, out.n_hoisted, out.code.size());
 }
 
 }  // namespace
