@@ -95,7 +95,8 @@ struct KArgs {
   uint32_t pc0;              // code[0, pc0): hoisted K_CONSTs, run once per thread (Lowered::n_hoisted)
 };
 
-constexpr uint32_t kFlagPrefetch = 1u << 16;  // KArgs::flags: warm the scalar cache first (launch_async)
+constexpr uint32_t kFlagPrefetch = 1u << 16;
+constexpr int kTierLight = 0, kTierMid = 1, kTierHeavy = 2;  // KArgs::flags: warm the scalar cache first (launch_async)
 
 // uniform struct reads through the constant address space (scalar loads)
 __device__ __forceinline__ GenSpec ld_spec(const KArgs& k, uint32_t c) {
@@ -406,10 +407,12 @@ __device__ __forceinline__ uint32_t compare(const VF& vf, uint32_t op, uint32_t 
   return (op == K_ULT || op == K_SLT) ? (uint32_t)lt : (uint32_t)le;
 }
 
-// HEAVY = false: a program with no MUL/DIV/REM/shift/EXP/UMUL_NOOVF/KECCAK (most LASER
-// queries): those handlers hold ~200 VGPRs of 256-bit temporaries, so leaving them out
-// of the kernel lets several times more waves hide the LDS and scalar-load latency.
-template <class VF, int MODE, bool HEAVY>
+// TIER: the handlers a program needs.  kTierLight: no MUL/DIV/REM/shift/EXP/UMUL_NOOVF/KECCAK
+// (most LASER queries; 47 VGPRs); kTierMid adds MUL, UMUL_NOOVF and the shifts (the overflow
+// checks of arithmetic); kTierHeavy adds division, EXP and Keccak, whose 256-bit temporaries
+// hold ~220 VGPRs (two waves per SIMD).  Leaving handlers out lets more waves hide the LDS and
+// scalar-load latency.
+template <class VF, int MODE, int TIER>
 __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, uint64_t i, const GKeys& key,
                                                 bool early, bool active) {
   uint32_t verdict = 1;
@@ -538,7 +541,7 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
         break;
       }
       case K_MUL: {
-        if constexpr (HEAVY) {
+        if constexpr (TIER >= kTierMid) {
           W8 r = mul8(ld8(vf, in.a, L), ld8(vf, in.b, L));
           canon8(r, W);
           st8(vf, in.dst, L, r);
@@ -546,21 +549,21 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
         break;
       }
       case K_UMUL_NOOVF: {
-        if constexpr (HEAVY) {
+        if constexpr (TIER >= kTierMid) {
           const uint32_t wa = in.p1, La = (wa + 31) >> 5;
           vf.at(in.dst) = umul_noovf8(ld8(vf, in.a, La), ld8(vf, in.b, La), wa);
         }
         break;
       }
-      case K_UDIV: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_udiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_UREM: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_urem(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_SDIV: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_sdiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_SREM: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_srem(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_SMOD: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_smod(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_SHL: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_shl(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_LSHR: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_lshr(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_ASHR: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_ashr(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_EXP: if constexpr (HEAVY) { st8(vf, in.dst, L, bv_exp(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_UDIV: if constexpr (TIER >= kTierHeavy) { st8(vf, in.dst, L, bv_udiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_UREM: if constexpr (TIER >= kTierHeavy) { st8(vf, in.dst, L, bv_urem(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_SDIV: if constexpr (TIER >= kTierHeavy) { st8(vf, in.dst, L, bv_sdiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_SREM: if constexpr (TIER >= kTierHeavy) { st8(vf, in.dst, L, bv_srem(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_SMOD: if constexpr (TIER >= kTierHeavy) { st8(vf, in.dst, L, bv_smod(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_SHL: if constexpr (TIER >= kTierMid) { st8(vf, in.dst, L, bv_shl(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_LSHR: if constexpr (TIER >= kTierMid) { st8(vf, in.dst, L, bv_lshr(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_ASHR: if constexpr (TIER >= kTierMid) { st8(vf, in.dst, L, bv_ashr(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_EXP: if constexpr (TIER >= kTierHeavy) { st8(vf, in.dst, L, bv_exp(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
       case K_LOOKUP: {
         const uint32_t Lk = (in.b + 31) >> 5;
         uint32_t src = in.p0;
@@ -581,7 +584,7 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
         if (in.a == MG_NONE) {
           // keccak256("") — the constant of keccak_function_manager.py:75-81
           for (uint32_t j = 0; j < 8; j++) vf.at(in.dst + j) = kEmptyKeccak[j];
-        } else if constexpr (HEAVY) {
+        } else if constexpr (TIER >= kTierHeavy) {
           do_keccak(vf, in);
         }
         break;
@@ -619,7 +622,7 @@ __global__ void __launch_bounds__(256) k_gather_rows(const uint32_t* __restrict_
   if (r < rows) dst[r] = src[(uint64_t)r * kWave];
 }
 
-template <class VF, int MODE, bool HEAVY>
+template <class VF, int MODE, int TIER>
 __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
   extern __shared__ uint32_t lds[];
   VF vf(lds, k);
@@ -682,7 +685,7 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
     // every lane), so the compiler sees G as wave-uniform: the MIXED alternatives are scalar branches
     // and the generator specs scalar loads (from idx, G looked per-lane: divergent branches, vector loads)
     if (MODE != MODE_EVAL) key = gen_keys_lk(a0 + base, lk, k.sg);
-    uint32_t v = run_program<VF, MODE, HEAVY>(k, vf, i, key, early, active);
+    uint32_t v = run_program<VF, MODE, TIER>(k, vf, i, key, early, active);
     v = active ? v : 0u;
     if (MODE == MODE_SEARCH) {
       const unsigned long long m = __ballot(v != 0);
@@ -749,7 +752,7 @@ thread_local std::string g_err;
 struct DevProgram {
   Lowered low;
   std::string src;  // the program bytes (key of the specialisation cache)
-  bool heavy = true;  // has MUL/DIV/REM/shift/EXP/UMUL_NOOVF/KECCAK: the full interpreter
+  int tier = 2;  // interpreter variant: kTierLight / kTierMid / kTierHeavy (run_program)
   bool uploaded = false;
   void* buf = nullptr;  // pooled device buffer holding the four arrays below
   size_t cap = 0;
@@ -1001,12 +1004,19 @@ static void free_gen_buffers(Engine& e, DevGen& g) {
 // instructions, literals, lookup lists and coordinate widths in ONE pooled buffer, one copy
 static int upload_code(Engine& e, DevProgram& p) {
   p.lds = p.low.value_words <= lds_words_max();
-  p.heavy = false;
+  // MYTHGPU_INTERP_TIERS=0: light or heavy only (the mid variant folded into heavy)
+  static const bool tiers = [] {
+    const char* g = getenv("MYTHGPU_INTERP_TIERS");
+    return !(g && g[0] == '0');
+  }();
+  p.tier = kTierLight;
   for (const Instr& in : p.low.code) {
     switch (in.op) {
-      case K_MUL: case K_UDIV: case K_UREM: case K_SDIV: case K_SREM: case K_SMOD: case K_SHL: case K_LSHR:
-      case K_ASHR: case K_EXP: case K_UMUL_NOOVF: p.heavy = true; break;
-      case K_KECCAK: if (in.a != MG_NONE) p.heavy = true; break;
+      case K_MUL: case K_SHL: case K_LSHR: case K_ASHR: case K_UMUL_NOOVF:
+        p.tier = std::max(p.tier, tiers ? kTierMid : kTierHeavy);
+        break;
+      case K_UDIV: case K_UREM: case K_SDIV: case K_SREM: case K_SMOD: case K_EXP: p.tier = kTierHeavy; break;
+      case K_KECCAK: if (in.a != MG_NONE) p.tier = kTierHeavy; break;
       default: break;
     }
   }
@@ -1067,10 +1077,10 @@ static int ensure_scratch(Engine& e, size_t bytes) {
 
 // grid: enough waves to fill 256 CUs several times over, never more than needed.
 // Resident waves per CU: the LDS value file (160 KiB per CU) and the VGPRs of the
-// kernel variant (heavy ~230: 2 waves/SIMD; light ~55: 8 waves/SIMD).
-static uint32_t grid_for(const Engine& e, uint64_t count, bool lds, uint32_t value_words, bool heavy) {
+// kernel variant (heavy ~230: 2 waves/SIMD; mid: 4; light ~50: 8 waves/SIMD).
+static uint32_t grid_for(const Engine& e, uint64_t count, bool lds, uint32_t value_words, int tier) {
   uint64_t want = (count + kWave - 1) / kWave;
-  uint32_t waves_per_cu = heavy ? 8 : 32;
+  uint32_t waves_per_cu = tier == kTierHeavy ? 8 : tier == kTierMid ? 16 : 32;
   if (lds) {
     const uint32_t bytes = value_words * kWave * 4;
     waves_per_cu = std::max<uint32_t>(1, std::min<uint32_t>(waves_per_cu, (160u * 1024u) / std::max<uint32_t>(bytes, 1)));
@@ -1090,7 +1100,7 @@ static int launch_async(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   // file would fetch from L2 at every operand are what such a launch waits on, and it needs no
   // occupancy.  Larger launches trade the other way (C4 at 255: 20 % slower).
   const bool lds = p.lds || (p.low.value_words <= 255u && lanes <= (uint64_t)std::max(e.cu_count, 1) * 2u * kWave);
-  const uint32_t grid = grid_for(e, lanes, lds, p.low.value_words, p.heavy);
+  const uint32_t grid = grid_for(e, lanes, lds, p.low.value_words, p.tier);
   k.sk = seed_lane_key(k.seed);
   k.sg = seed_group_key(k.seed);
   k.code = p.d_code;
@@ -1117,14 +1127,16 @@ static int launch_async(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   }
   const size_t shmem = lds ? (size_t)p.low.value_words * kWave * 4 : 0;
   HIPCHK(hipEventRecord(e.ev0, e.stream));
-  if (lds && p.heavy)
-    hipLaunchKernelGGL((k_run<VFLds, MODE, true>), dim3(grid), dim3(kWave), shmem, e.stream, k);
-  else if (lds)
-    hipLaunchKernelGGL((k_run<VFLds, MODE, false>), dim3(grid), dim3(kWave), shmem, e.stream, k);
-  else if (p.heavy)
-    hipLaunchKernelGGL((k_run<VFGlobal, MODE, true>), dim3(grid), dim3(kWave), 0, e.stream, k);
-  else
-    hipLaunchKernelGGL((k_run<VFGlobal, MODE, false>), dim3(grid), dim3(kWave), 0, e.stream, k);
+  const dim3 g(grid), b(kWave);
+  if (lds) {
+    if (p.tier == kTierHeavy) hipLaunchKernelGGL((k_run<VFLds, MODE, kTierHeavy>), g, b, shmem, e.stream, k);
+    else if (p.tier == kTierMid) hipLaunchKernelGGL((k_run<VFLds, MODE, kTierMid>), g, b, shmem, e.stream, k);
+    else hipLaunchKernelGGL((k_run<VFLds, MODE, kTierLight>), g, b, shmem, e.stream, k);
+  } else {
+    if (p.tier == kTierHeavy) hipLaunchKernelGGL((k_run<VFGlobal, MODE, kTierHeavy>), g, b, 0, e.stream, k);
+    else if (p.tier == kTierMid) hipLaunchKernelGGL((k_run<VFGlobal, MODE, kTierMid>), g, b, 0, e.stream, k);
+    else hipLaunchKernelGGL((k_run<VFGlobal, MODE, kTierLight>), g, b, 0, e.stream, k);
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e.ev1, e.stream));
   return MG_OK;
@@ -1847,7 +1859,7 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
       // watch rows, so a hit's model needs no second pass (read_assignment); the capture buffer
       // is blocks x watch_words x 64 words
       const DevProgram& pw = dg.spec_watch;
-      const uint32_t grid_w = grid_for(e, lanes, pw.lds, pw.low.value_words, pw.heavy);
+      const uint32_t grid_w = grid_for(e, lanes, pw.lds, pw.low.value_words, pw.tier);
       const bool capture = assign_out && ww && pw.uploaded && lanes <= (uint64_t)grid_w * kWave &&
                            (uint64_t)grid_w * ww * kWave * 4u <= kCaptureBytes;
       int rc = MG_OK;
