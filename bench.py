@@ -60,9 +60,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="token_transfer_underflow")
-    ap.add_argument("--candidates", type=int, default=1 << 28,
-                    help="candidates per GPU per step (~3 ms on C2, so the per-step host sync and RCCL "
-                         "exchange cost ~1-2 %% of a step)")
+    ap.add_argument("--candidates", type=int, default=1 << 30,
+                    help="candidates per GPU per step (~6 ms on C2: SURVEY §8(e) sizes an epoch at 5-10 ms "
+                         "per GPU, so the per-step host sync and the RCCL exchange stay ~1 %% of a step "
+                         "at 8 GPUs)")
     ap.add_argument("--seed", type=int, default=0x6D797468)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
