@@ -11,4 +11,4 @@ for W in suicide_kill token_transfer_underflow etherstore_reentrancy bectoken_ba
   done
 done
 cat gpurun_out/r3o_interp_ab.jsonl
-bash tools/r3_ab.sh r3o "narrow=" "wide=MYTHGPU_NARROW_TAILS=0" && cat gpurun_out/r3o_ab.jsonl
+bash tools/runs/r3_ab.sh r3o "narrow=" "wide=MYTHGPU_NARROW_TAILS=0" && cat gpurun_out/r3o_ab.jsonl

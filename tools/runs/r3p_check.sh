@@ -10,4 +10,4 @@ for V in "160" "255"; do
   done
 done
 cat gpurun_out/r3p_interp_ab.jsonl
-bash tools/r3_ab.sh r3p "base=" && cat gpurun_out/r3p_ab.jsonl
+bash tools/runs/r3_ab.sh r3p "base=" && cat gpurun_out/r3p_ab.jsonl

@@ -10,4 +10,4 @@ for V in "MYTHGPU_NARROW_TAILS=1" "MYTHGPU_NARROW_TAILS=0" "MYTHGPU_INTERP_LDS_M
   done
 done
 cat gpurun_out/r3r_interp_ab.jsonl
-bash tools/r3_ab.sh r3r "narrow=" "wide=MYTHGPU_NARROW_TAILS=0" && cat gpurun_out/r3r_ab.jsonl
+bash tools/runs/r3_ab.sh r3r "narrow=" "wide=MYTHGPU_NARROW_TAILS=0" && cat gpurun_out/r3r_ab.jsonl
