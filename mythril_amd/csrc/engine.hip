@@ -2014,10 +2014,13 @@ static int jit_launch_async(Engine& e, hipFunction_t f, int nb, uint64_t count, 
   // C2 -2 %); more paid per-block start-up and the end-of-block publish, until the block's hits
   // went to a count stripe with no barrier (profiles/r03_ab_bpc_*.jsonl: 64 vs 32 per CU, kernel
   // time C2 -2.0 %, C4 -0.9 %, C1 -1.1 %, C3 -0.8 %; before the stripes C3 was 17 % slower at 64).
-  static const uint64_t bpc = [] {
+  // Launches past 2^29 candidates take 128 per CU (each wave still sweeps ~128 groups): the C2 step
+  // of 2^30, 64 -> 128 per CU: +1.3 %, 32: -2.5 % (profiles/r03_ab_bpc_2p30.jsonl)
+  static const int bpc_env = [] {
     const char* g = getenv("MYTHGPU_JIT_BPC");
-    return (uint64_t)std::max(1, g ? atoi(g) : 64);
+    return g ? std::max(1, atoi(g)) : 0;
   }();
+  const uint64_t bpc = bpc_env ? (uint64_t)bpc_env : (count > (1ull << 29) ? 128u : 64u);
   (void)nb;
   const uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * bpc;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
