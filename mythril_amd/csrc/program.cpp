@@ -332,7 +332,7 @@ uint32_t assign_slots(const std::vector<VInstr>& code, uint32_t n_hoisted, const
 }
 
 void allocate(const std::vector<VInstr>& vlist, const std::vector<uint32_t>& vwidth, Lowered& out,
-              const std::vector<VInstr>* slot_list = nullptr) {
+              const std::vector<VInstr>* slot_list = nullptr, bool search_orders = true) {
   const uint32_t NONE = MG_NONE;
   const size_t nv = vwidth.size();
   out.vcode.clear();
@@ -386,12 +386,12 @@ void allocate(const std::vector<VInstr>& vlist, const std::vector<uint32_t>& vwi
     return !(g && g[0] == '0');
   }();
   std::vector<std::vector<VInstr>> orders;
-  if (sink_on) orders.push_back(sink_inputs(fused, nv));
+  if (sink_on && search_orders) orders.push_back(sink_inputs(fused, nv));
   orders.push_back(fused);
 
   bool have = false;
   for (const auto& code : orders) {
-    for (int hz = hoist ? 1 : 0; hz >= 0; hz--) {
+    for (int hz = hoist && search_orders ? 1 : 0; hz >= 0; hz--) {
       std::vector<VInstr> h = code;
       uint32_t nh = 0;
       if (hz) {
@@ -854,7 +854,10 @@ int lower_program(const uint8_t* blob, size_t len, Lowered& out, std::string& er
     out.watch_words = wrow;
     out.max_width = max_w;
 
-    allocate(code, vwidth, out);
+    // the unlowered program's own slot code only serves explicit-coordinate evaluation on the
+    // interpreter (mg_eval; searches run a specialisation): no search over slot orders (for C4's
+    // 2,500 instructions that search took two thirds of the lowering)
+    allocate(code, vwidth, out, nullptr, /*search_orders=*/false);
     return MG_OK;
   } catch (const Fail& f) {
     err = f.msg;
@@ -1992,7 +1995,13 @@ std::vector<uint32_t> narrow_literal_tails(std::vector<VInstr>& code, std::vecto
   std::vector<uint32_t> twinned;  // wide values that got a narrow twin
   if (!on) return twinned;
   const uint32_t NONE = MG_NONE;
-  std::map<uint32_t, std::string> lit;    // K_CONST value id -> its literal (width + words)
+  std::map<uint32_t, std::pair<uint32_t, uint32_t>> lit;  // K_CONST value id -> (width, const offset)
+  auto lit_key = [&](uint32_t v) {  // the literal as a string key (width + words), built on demand
+    const auto& wo = lit.at(v);
+    std::string t = std::to_string(wo.first) + ":";
+    for (uint32_t j = 0; j < Lw(wo.first); j++) t += std::to_string(consts.at(wo.second + j)) + ",";
+    return t;
+  };
   std::map<std::string, uint32_t> tails;  // literal tail -> its id
   std::map<uint32_t, uint32_t> tid_vid;   // tail id -> the value id of its 32-bit literal
   struct Split {
@@ -2026,11 +2035,9 @@ std::vector<uint32_t> narrow_literal_tails(std::vector<VInstr>& code, std::vecto
   auto hw = [&](uint32_t v) { return vwidth[split.at(v).h]; };
   for (VInstr& c : code) {
     if (c.op == K_CONST && c.dst != NONE && c.dst < vwidth.size()) {
-      std::string t = std::to_string(c.wd) + ":";
-      for (uint32_t j = 0; j < Lw(c.wd); j++) t += std::to_string(consts.at(c.p0 + j)) + ",";
-      lit[c.dst] = t;
+      lit[c.dst] = {c.wd, c.p0};
     } else if (c.op == K_CONCAT && c.dst != NONE && lit.count(c.b) && c.a != NONE && c.a < vwidth.size()) {
-      const std::string t = lit[c.b];
+      const std::string t = lit_key(c.b);
       const Split id = tid_of(t);
       outc.push_back(std::move(c));
       split[outc.back().dst] = Split{outc.back().a, id.t, id.tlit};
