@@ -97,6 +97,9 @@ def load_pmc(pmc_dir: str, workload: str, sha: str, candidates: int):
 
 def main():
     args = parse()
+    # code objects left on disk by an earlier process (tests, a previous bench) would hide the
+    # compile in the cold numbers: the engine's on-disk code-object cache is off for the bench
+    os.environ.setdefault("MYTHGPU_JIT_DISK_CACHE", "0")
     # stdout carries exactly the one JSON line: native libraries print to fd 1 on their own
     # (RCCL's version banner at communicator set-up), so fd 1 goes to stderr for the run and the
     # line is written to the saved stdout
@@ -151,15 +154,17 @@ def main():
     sha = None
     if args.engine == "jit":
         sha = hashlib.sha256(native.jit_source(P.to_bytes(), blob).encode()).hexdigest()[:16]
-        # cold compile: comgr's on-disk cache off, so a kernel compiled by an earlier process
-        # (tests, a previous bench) is not reported as a compile cost
-        prev = os.environ.get("AMD_COMGR_CACHE")
-        os.environ["AMD_COMGR_CACHE"] = "0"
+        # cold compile: comgr's on-disk cache and the engine's code-object cache off, so a
+        # kernel compiled by an earlier process (tests, a previous bench) is not reported as a
+        # compile cost
+        prev = {k: os.environ.get(k) for k in ("AMD_COMGR_CACHE", "MYTHGPU_JIT_DISK_CACHE")}
+        os.environ.update({k: "0" for k in prev})
         jit = eng.jit_compile(prog, gh)
-        if prev is None:
-            os.environ.pop("AMD_COMGR_CACHE")
-        else:
-            os.environ["AMD_COMGR_CACHE"] = prev
+        for k, v in prev.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
         compile_ms = eng.jit_info(jit)[0]
 
     from mythril_amd.distributed import chunk_start, first_hit_allreduce

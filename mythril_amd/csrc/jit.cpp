@@ -9,12 +9,16 @@
 #include <signal.h>
 #include <spawn.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
 #include <amd_comgr/amd_comgr.h>
 
+#include <hip/hip_version.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <mutex>
 
@@ -1635,15 +1639,138 @@ void jit_compiler_preload() {
   (void)rtc();
 }
 
+// ---------------------------------------------------------------------------
+// On-disk code-object cache, shared by every process of one user: a query shape compiled once
+// (~0.15 s of comgr on the box) loads from disk in later Mythril runs (re-analysis, CI, one
+// contract's several entry points).  comgr's own cache (AMD_COMGR_CACHE) already skips most of
+// the compile of a known source (C2: 392 -> 15 ms on the host); this one also skips the helper
+// process and comgr altogether (a hit costs one file read).  The key is everything that
+// decides the code object: the source, the compiler-relevant environment (AMD_COMGR_* /
+// MYTHGPU_JIT* bar the controls of the caches, the timing switch and the helper's path), the
+// compiler choice and this library's build (HIP version, build time).  File <dir>/<h1><h2>.co
+// = 24-B header (magic, key length, h1) + the ELF code object; written to a temporary name and
+// renamed, so readers never see a partial file.  Any failure — no directory, a short or
+// foreign file — is a miss and never an error.
+//   MYTHGPU_JIT_DISK_CACHE=<dir>  cache directory (default ${XDG_CACHE_HOME:-$HOME/.cache}/mythgpu/jit)
+//   MYTHGPU_JIT_DISK_CACHE=0      off
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr uint64_t kCoMagic = 0x31304F43474D594Dull;  // "MYMGCO01"
+
+std::string disk_cache_dir() {
+  const char* d = getenv("MYTHGPU_JIT_DISK_CACHE");
+  if (d) return (d[0] == 0 || (d[0] == '0' && d[1] == 0)) ? std::string() : std::string(d);
+  if (const char* x = getenv("XDG_CACHE_HOME"); x && x[0]) return std::string(x) + "/mythgpu/jit";
+  if (const char* h = getenv("HOME"); h && h[0]) return std::string(h) + "/.cache/mythgpu/jit";
+  return std::string();
+}
+
+uint64_t key_hash(const std::string& s, uint64_t seed) {
+  uint64_t h = 0xCBF29CE484222325ull ^ seed;
+  for (unsigned char c : s) h = (h ^ c) * 0x100000001B3ull;
+  h ^= h >> 33;
+  h *= 0xFF51AFD7ED558CCDull;
+  h ^= h >> 33;
+  return h;
+}
+
+std::string compile_key(const std::string& src) {
+  std::string k = src;
+  k += "\n//mythgpu-jit-key\n";
+  for (char** e = environ; e && *e; e++)
+    if ((!std::strncmp(*e, "AMD_COMGR_", 10) || !std::strncmp(*e, "MYTHGPU_JIT", 11)) &&
+        std::strncmp(*e, "MYTHGPU_JIT_DISK_CACHE=", 23) && std::strncmp(*e, "MYTHGPU_JIT_CACHE=", 18) &&
+        std::strncmp(*e, "MYTHGPU_JIT_TIMING=", 19) && std::strncmp(*e, "MYTHGPU_JITD=", 13) &&
+        std::strncmp(*e, "AMD_COMGR_CACHE", 15)) {
+      k += *e;
+      k.push_back('\n');
+    }
+  k += "isolate=" + std::to_string(isolated() ? 1 : 0) + "\n";
+  k += "hip=" + std::to_string(HIP_VERSION) + " built=" __DATE__ " " __TIME__ "\n";
+  return k;
+}
+
+bool mkdirs(const std::string& dir) {
+  for (size_t p = 1; p <= dir.size(); p++) {
+    if (p == dir.size() || dir[p] == '/') {
+      const std::string part = dir.substr(0, p);
+      if (mkdir(part.c_str(), 0700) != 0 && errno != EEXIST) return false;
+    }
+  }
+  return true;
+}
+
+bool disk_load(const std::string& path, uint64_t klen, uint64_t h1, std::vector<char>& code) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  uint64_t hdr[3] = {0, 0, 0};
+  bool ok = fread(hdr, 8, 3, f) == 3 && hdr[0] == kCoMagic && hdr[1] == klen && hdr[2] == h1;
+  if (ok) {
+    fseek(f, 0, SEEK_END);
+    const long end = ftell(f);
+    ok = end > 24 + 4;
+    if (ok) {
+      std::vector<char> buf((size_t)end - 24);
+      fseek(f, 24, SEEK_SET);
+      ok = fread(buf.data(), 1, buf.size(), f) == buf.size() && !std::memcmp(buf.data(), "\x7f" "ELF", 4);
+      if (ok) code.swap(buf);
+    }
+  }
+  fclose(f);
+  return ok;
+}
+
+void disk_store(const std::string& dir, const std::string& path, uint64_t klen, uint64_t h1,
+                const std::vector<char>& code) {
+  if (!mkdirs(dir)) return;
+  static std::atomic<uint64_t> seq{0};
+  const std::string tmp = path + ".tmp." + std::to_string(getpid()) + "." + std::to_string(seq++);
+  FILE* f = fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  const uint64_t hdr[3] = {kCoMagic, klen, h1};
+  const bool ok = fwrite(hdr, 8, 3, f) == 3 && fwrite(code.data(), 1, code.size(), f) == code.size();
+  if (fclose(f) == 0 && ok && rename(tmp.c_str(), path.c_str()) == 0) return;
+  (void)unlink(tmp.c_str());
+}
+
+}  // namespace
+
 int jit_compile(const std::string& src, std::vector<char>& code, std::string& log) {
+  const std::string dir = disk_cache_dir();
+  const bool timing = getenv("MYTHGPU_JIT_TIMING") != nullptr;
+  std::string path;
+  uint64_t klen = 0, h1 = 0;
+  if (!dir.empty()) {
+    const std::string key = compile_key(src);
+    klen = key.size();
+    h1 = key_hash(key, 0);
+    char name[40];
+    snprintf(name, sizeof name, "%016llx%016llx.co", (unsigned long long)h1,
+             (unsigned long long)key_hash(key, 0x9E3779B97F4A7C15ull));
+    path = dir + "/" + name;
+    if (disk_load(path, klen, h1, code)) {
+      if (timing) fprintf(stderr, "mythgpu: JIT code object from the disk cache %s\n", path.c_str());
+      return MG_OK;
+    }
+  }
+  int rc = MG_E_UNSUPPORTED;
+  bool done = false;
   if (isolated()) {
     bool available = true;
-    const int rc = helper_compile(src, code, log, available);
-    if (available) return rc;
-    static std::once_flag warn;
-    std::call_once(warn, [&] { fprintf(stderr, "mythgpu: %s; compiling in-process\n", helper().why.c_str()); });
+    rc = helper_compile(src, code, log, available);
+    done = available;
+    if (!available) {
+      static std::once_flag warn;
+      std::call_once(warn, [&] { fprintf(stderr, "mythgpu: %s; compiling in-process\n", helper().why.c_str()); });
+    }
   }
-  return jit_compile_local(src, code, log);
+  if (!done) rc = jit_compile_local(src, code, log);
+  if (rc == MG_OK && !path.empty()) {
+    disk_store(dir, path, klen, h1, code);
+    if (timing) fprintf(stderr, "mythgpu: JIT code object stored in the disk cache %s\n", path.c_str());
+  }
+  return rc;
 }
 
 int jit_compile_local(const std::string& src, std::vector<char>& code, std::string& log) {

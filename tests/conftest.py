@@ -7,6 +7,9 @@ import pytest
 ROOT = Path(__file__).resolve().parent.parent
 if str(ROOT) not in sys.path:
     sys.path.insert(0, str(ROOT))
+# tests compile their kernels afresh (the engine's on-disk code-object cache is off unless a
+# test turns it on for a child process: test_jit_disk_cache.py)
+os.environ.setdefault("MYTHGPU_JIT_DISK_CACHE", "0")
 
 
 def pytest_configure(config):
