@@ -399,7 +399,12 @@ def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5):
 
     cs = workloads.WORKLOADS[workload]()
     P, _ = search.prepare([c.raw for c in cs])
+    # verdicts only (mg_jit_eval_dev without a watch buffer): the program without the model
+    # watch rows, whose eval kernel walks the SoA rows with one pointer (jit.cpp K_COORD)
+    prev = P.watch
+    P.set_watch([])
     blob = P.to_bytes()
+    P.set_watch(prev)
     prog = eng.load(blob)
     info = eng.info(prog)
     jh = eng.jit_compile(prog, 0)
@@ -424,7 +429,7 @@ def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5):
         sat = int(ver.sum().item())
         src = native.jit_source(blob)
         sha = hashlib.sha256(src.encode()).hexdigest()[:16]
-        rows_read = len(set(re.findall(r"soa\[\(uint64_t\)(\d+)u \* n \+ i\]", src)))
+        rows_read = len(set(re.findall(r"soa\[\(uint64_t\)(\d+)u \* n \+ i\]|// soa row (\d+)", src)))
     finally:
         eng.jit_free(jh)
         eng.free(prog)

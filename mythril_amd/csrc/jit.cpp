@@ -773,8 +773,22 @@ struct Gen {
         if (search) {
           gen_value(in.p0, "v" + std::to_string(d));
         } else {
-          for (uint32_t j = 0; j < L; j++)
-            o << "  " << v(d, j) << " = soa[(uint64_t)" << (in.p1 + j) << "u * n + i];\n";
+          for (uint32_t j = 0; j < L; j++) {
+            if (!P.watch_words) {
+              // no watch rows: one pointer walks the SoA rows (the loads come in row order, at the
+              // loop's top level), each load a 64-bit add of a small multiple of n to the previous
+              // address.  With soa[K * n + i] LLVM hoists every row's K * n out of the candidate
+              // loop into SGPR pairs and spills them to VGPR lanes (C4: ~970 v_readlane +
+              // ~970 v_writelane per candidate).  A program with watch rows keeps the indexed form
+              // (its per-store branches compile too slowly around the walking pointer's barriers)
+              const int64_t step = (int64_t)(in.p1 + j) - (int64_t)soa_row;
+              if (step) o << "  sp_ += (long long)" << step << " * (long long)n; __asm__ volatile(\"\" : \"+v\"(sp_));\n";
+              o << "  " << v(d, j) << " = *sp_;  // soa row " << (in.p1 + j) << "\n";
+              soa_row = in.p1 + j;
+            } else {
+              o << "  " << v(d, j) << " = soa[(uint64_t)" << (in.p1 + j) << "u * n + i];\n";
+            }
+          }
         }
         break;
       case K_ADD:
@@ -983,6 +997,8 @@ struct Gen {
 
   // P is specialised (program.cpp specialize_program): decided compares are literals,
   // aliases are renamed away and dead instructions are gone
+  uint32_t soa_row = 0;  // eval kernel without watch rows: the SoA row sp_ points at
+
   void body(bool search) {
     coord_var.clear();  // generated-coordinate names are per kernel
     // MYTHGPU_JIT_GEN_ONLY=1 (diagnostic, search kernels): only the candidate generator, its
@@ -1004,6 +1020,7 @@ struct Gen {
       o << "  verdict &= (uint32_t)(fold_ == 0x9E3779B9u); }\n";
       return;
     }
+    soa_row = 0;  // eval: sp_ = soa + i addresses row 0
     for (const Instr& in : P.vcode) emit(in, search, !search);
   }
 };
@@ -1161,12 +1178,17 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  }\n}\n\n";
   }
   if (want_eval) {
-  // eval kernel (explicit SoA coordinates, verdicts, optional watch rows)
+  // eval kernel (explicit SoA coordinates, verdicts, optional watch rows).  GU32: a
+  // global-address-space word, so the walking row pointer stays global_load (a generic pointer
+  // through the asm barrier would become flat); declared here, so search kernels' sources (and
+  // the SHAs their profiles are matched by) do not change
+  o << "typedef uint32_t __attribute__((address_space(1))) GU32;\n";
   o << "extern \"C\" __global__ void " << lb << " mgj_eval(const uint32_t* __restrict__ soa, uint64_t n, "
        "uint8_t* __restrict__ verdict_out, uint32_t* __restrict__ watch, uint32_t nblk) {\n"
        "  const uint64_t stride = (uint64_t)nblk * 256u;\n"
        "  for (uint64_t i = (uint64_t)__builtin_amdgcn_workgroup_id_x() * 256u + __builtin_amdgcn_workitem_id_x(); i < n; i += stride) {\n"
-       "  uint32_t verdict = 1u;\n";
+       "  uint32_t verdict = 1u;\n"
+       "  const GU32* sp_ = (const GU32*)((uint64_t)soa + i * 4ull);\n";
   g.decls();
   g.body(false);
   o << "  verdict_out[i] = (uint8_t)verdict;\n  }\n}\n";
