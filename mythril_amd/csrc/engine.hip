@@ -950,6 +950,18 @@ Engine& E() {
     }                                                                              \
   } while (0)
 
+// The engine's primary device made current on the calling thread.  The z3 race calls the
+// engine from two threads (the search on the GPU worker, mg_keccak256 from LASER's thread) and
+// only the thread that ran mg_init had the device set: with MYTHGPU_DEVICE / LOCAL_RANK != 0
+// the other one's hipMallocs landed on GPU 0 while its kernels ran on e.stream of GPU k.
+// Every entry point that touches the device takes one after the engine lock.
+struct OnDevice {
+  explicit OnDevice(const Engine& e) {
+    int d = -1;
+    if (e.device >= 0 && (hipGetDevice(&d) != hipSuccess || d != e.device)) (void)hipSetDevice(e.device);
+  }
+};
+
 static int set_err(int code, const std::string& m) {
   g_err = m;
   return code;
@@ -1266,6 +1278,7 @@ extern "C" {
 int mg_init(uint32_t device_mask) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   if (e.init) return MG_OK;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return set_err(MG_E_NODEVICE, "no HIP device");
@@ -1324,6 +1337,7 @@ int mg_split_range(uint64_t start, uint64_t count, uint32_t n_dev, uint64_t* sta
 void mg_shutdown(void) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   {
     // stop the compile thread (a compile in flight finishes first; its result is dropped)
     std::unique_lock<std::mutex> jl(e.jit_mu);
@@ -1474,6 +1488,7 @@ int mg_program_specialized(const uint8_t* ssa, size_t len, const uint32_t* gen_b
 int mg_program_load(const uint8_t* ssa, size_t len, uint64_t* handle) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   if (!e.init) return set_err(MG_E_NOTINIT, "mg_init not called");
   auto p = std::make_unique<DevProgram>();
   p->src.assign((const char*)ssa, len);
@@ -1513,6 +1528,7 @@ static DevProgram* find_prog(Engine& e, uint64_t h) {
 int mg_program_info(uint64_t prog, mg_program_info_t* info) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   DevProgram* p = find_prog(e, prog);
   if (!p) return set_err(MG_E_INVALID, "bad program handle");
   fill_info(*p, info);
@@ -1522,6 +1538,7 @@ int mg_program_info(uint64_t prog, mg_program_info_t* info) {
 int mg_gen_info(uint64_t gen, mg_program_info_t* info) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   auto it = e.gens.find(gen);
   if (it == e.gens.end()) return set_err(MG_E_INVALID, "bad generator handle");
   fill_info(it->second->spec, info);
@@ -1531,6 +1548,7 @@ int mg_gen_info(uint64_t gen, mg_program_info_t* info) {
 int mg_program_free(uint64_t prog) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   auto it = e.progs.find(prog);
   if (it == e.progs.end()) return set_err(MG_E_INVALID, "bad program handle");
   free_code(e, *it->second);
@@ -1579,6 +1597,7 @@ extern "C" {
 int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* gen_handle) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   DevProgram* p = find_prog(e, prog);
   if (!p) return set_err(MG_E_INVALID, "bad program handle");
   std::vector<GenSpec> specs;
@@ -1646,6 +1665,7 @@ int mg_gen_load(uint64_t prog, const uint32_t* blob, size_t n_words, uint64_t* g
 int mg_gen_free(uint64_t gen) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   auto it = e.gens.find(gen);
   if (it == e.gens.end()) return set_err(MG_E_INVALID, "bad generator handle");
   for (size_t i = 0; i < g_devs.size(); i++) {
@@ -1665,6 +1685,7 @@ int mg_gen_free(uint64_t gen) {
 int mg_eval_dev(uint64_t prog, const uint32_t* d_soa, uint64_t n, uint8_t* d_verdict, uint32_t* d_watch) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   DevProgram* p = find_prog(e, prog);
   if (!p) return set_err(MG_E_INVALID, "bad program handle");
   if (!p->uploaded) {
@@ -1684,6 +1705,7 @@ int mg_eval(uint64_t prog, const uint32_t* soa, uint64_t n, uint8_t* verdict_out
   DevProgram* p;
   {
     std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
     if (!e.init) return set_err(MG_E_NOTINIT, "mg_init not called");
     p = find_prog(e, prog);
     if (!p) return set_err(MG_E_INVALID, "bad program handle");
@@ -1712,6 +1734,7 @@ int mg_eval_generated(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start
                       uint32_t* watch_out) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   DevProgram* p = find_prog(e, prog);
   if (!p) return set_err(MG_E_INVALID, "bad program handle");
   auto it = e.gens.find(gen);
@@ -1797,6 +1820,7 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
               uint64_t* first_hit, uint64_t* n_hits, uint32_t* assign_out) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   DevProgram* p = find_prog(e, prog);
   if (!p) return set_err(MG_E_INVALID, "bad program handle");
   auto it = e.gens.find(gen);
@@ -1923,6 +1947,7 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
 int mg_keccak256(const uint8_t* msgs, const uint32_t* lens, uint64_t n, uint8_t* out32) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   if (!e.init) return set_err(MG_E_NOTINIT, "mg_init not called");
   if (n == 0) return MG_OK;
   std::vector<uint64_t> offs(n);
@@ -1964,6 +1989,7 @@ int mg_keccak256(const uint8_t* msgs, const uint32_t* lens, uint64_t n, uint8_t*
 int mg_stats(mg_stats_t* out) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   *out = e.stats;
   return MG_OK;
 }
@@ -1971,6 +1997,7 @@ int mg_stats(mg_stats_t* out) {
 int mg_stats_reset(void) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   mg_stats_t keep = e.stats;
   std::memset(&e.stats, 0, sizeof(e.stats));
   e.stats.device = keep.device;
@@ -1981,6 +2008,7 @@ int mg_stats_reset(void) {
 }
 
 int mg_dev_alloc(size_t bytes, void** dptr) {
+  OnDevice od_(E());
   HIPCHK(hipMalloc(dptr, std::max<size_t>(bytes, 1)));
   return MG_OK;
 }
@@ -2100,6 +2128,7 @@ int mg_jit_helper_pid(void) { return jit_helper_pid(); }
 int mg_cache_clear(void) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   e.lower_cache.clear();
   e.lower_order.clear();
   e.spec_cache.clear();
@@ -2187,17 +2216,27 @@ static void jit_worker_main(Engine* ep, int device) {
     lk.unlock();
     int rc = MG_OK;
     std::string log;
-    bool compiled = false;
+    bool compiled = false, from_disk = false;
     if (!j && code.empty()) {
-      rc = jit_compile(src, code, log);
+      rc = jit_compile(src, code, log, &from_disk);
       compiled = rc == MG_OK;
     }
     std::string err;
     if (rc != MG_OK) {
       err = "JIT compile failed: " + log.substr(0, 4000);
     } else if (!j) {
-      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       rc = load_jit(code, *t, ms, j);
+      if (rc != MG_OK && from_disk) {
+        // a disk-cache entry that passes the header checks but does not load (a truncated write
+        // renamed on a full disk, a runtime upgrade without a rebuild): drop it and compile once
+        jit_disk_evict(src);
+        code.clear();
+        rc = jit_compile(src, code, log, &from_disk);
+        ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (rc == MG_OK) rc = load_jit(code, *t, ms, j);
+        else g_err = "JIT compile failed: " + log.substr(0, 4000);
+      }
       if (rc != MG_OK) {
         err = g_err;
       } else {
@@ -2322,6 +2361,7 @@ extern "C" {
 int mg_jit_compile_ex(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* jit_handle) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   uint64_t ticket = 0;
   int rc = submit_jit(e, prog, gen, flags, &ticket);
   if (rc) return rc;
@@ -2331,12 +2371,14 @@ int mg_jit_compile_ex(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* jit
 int mg_jit_compile_async(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* ticket) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   return submit_jit(e, prog, gen, flags, ticket);
 }
 
 int mg_jit_poll(uint64_t ticket, int32_t wait_ms, uint64_t* jit_handle) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   return poll_jit(e, ticket, wait_ms, jit_handle);
 }
 
@@ -2359,6 +2401,7 @@ int mg_jit_cancel(uint64_t ticket) {
 int mg_jit_info(uint64_t jit, double* compile_ms, int* blocks_per_cu) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   auto it = e.jits.find(jit);
   if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
   if (compile_ms) *compile_ms = it->second->compile_ms;
@@ -2369,6 +2412,7 @@ int mg_jit_info(uint64_t jit, double* compile_ms, int* blocks_per_cu) {
 int mg_jit_free(uint64_t jit) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   auto it = e.jits.find(jit);
   if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
   release_jit(*it->second);
@@ -2388,6 +2432,7 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
                   uint64_t* n_hits, uint32_t* assign_out) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   auto it = e.jits.find(jit);
   if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
   DevJit& j = *it->second;
@@ -2463,6 +2508,7 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
 int mg_jit_verdicts(uint64_t jit, uint64_t seed, uint64_t start, uint64_t n, uint8_t* verdict_out) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   auto it = e.jits.find(jit);
   if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
   DevJit& j = *it->second;
@@ -2488,6 +2534,7 @@ int mg_jit_verdicts(uint64_t jit, uint64_t seed, uint64_t start, uint64_t n, uin
 int mg_jit_eval_dev(uint64_t jit, const uint32_t* d_soa, uint64_t n, uint8_t* d_verdict, uint32_t* d_watch) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
   auto it = e.jits.find(jit);
   if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
   DevJit& j = *it->second;
@@ -2502,6 +2549,7 @@ int mg_jit_eval(uint64_t jit, const uint32_t* soa, uint64_t n, uint8_t* verdict_
   DevProgram* p;
   {
     std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
     auto it = e.jits.find(jit);
     if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
     p = find_prog(e, it->second->prog);

@@ -1756,23 +1756,35 @@ void disk_store(const std::string& dir, const std::string& path, uint64_t klen, 
   (void)unlink(tmp.c_str());
 }
 
+std::string disk_path(const std::string& dir, const std::string& key) {
+  char name[40];
+  snprintf(name, sizeof name, "%016llx%016llx.co", (unsigned long long)key_hash(key, 0),
+           (unsigned long long)key_hash(key, 0x9E3779B97F4A7C15ull));
+  return dir + "/" + name;
+}
+
 }  // namespace
 
-int jit_compile(const std::string& src, std::vector<char>& code, std::string& log) {
+void jit_disk_evict(const std::string& src) {
+  const std::string dir = disk_cache_dir();
+  if (dir.empty()) return;
+  (void)unlink(disk_path(dir, compile_key(src)).c_str());
+}
+
+int jit_compile(const std::string& src, std::vector<char>& code, std::string& log, bool* from_disk) {
   const std::string dir = disk_cache_dir();
   const bool timing = getenv("MYTHGPU_JIT_TIMING") != nullptr;
   std::string path;
   uint64_t klen = 0, h1 = 0;
+  if (from_disk) *from_disk = false;
   if (!dir.empty()) {
     const std::string key = compile_key(src);
     klen = key.size();
     h1 = key_hash(key, 0);
-    char name[40];
-    snprintf(name, sizeof name, "%016llx%016llx.co", (unsigned long long)h1,
-             (unsigned long long)key_hash(key, 0x9E3779B97F4A7C15ull));
-    path = dir + "/" + name;
+    path = disk_path(dir, key);
     if (disk_load(path, klen, h1, code)) {
       if (timing) fprintf(stderr, "mythgpu: JIT code object from the disk cache %s\n", path.c_str());
+      if (from_disk) *from_disk = true;
       return MG_OK;
     }
   }

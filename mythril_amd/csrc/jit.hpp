@@ -21,7 +21,10 @@ void jit_compiler_preload();
 // compile for gfx950 -> code object bytes. MG_OK or MG_E_*; `log` gets the compiler log.  By
 // default through the compiler helper process (mythgpu_jitd): a compiler abort there fails the
 // compile, not the caller.  jit_compile_local: comgr (or hipRTC) in this process.
-int jit_compile(const std::string& src, std::vector<char>& code, std::string& log);
+// from_disk (nullable): set when the code object came from the on-disk cache
+int jit_compile(const std::string& src, std::vector<char>& code, std::string& log, bool* from_disk = nullptr);
+// drop the on-disk cache entry of `src` (a code object the runtime refused to load)
+void jit_disk_evict(const std::string& src);
 int jit_compile_local(const std::string& src, std::vector<char>& code, std::string& log);
 
 // the helper process: stop it (end of input; it exits), and its pid (-1 none yet, -2 died)

@@ -81,13 +81,16 @@ class HookStats:
         self.race_z3_time = 0.0   # z3 check seconds of those
         self.race_overhead = 0.0  # hook wall time beyond z3's own, summed over them
         self.negative_hits = 0    # repeats of a GPU-missed unsat/unknown tuple sent straight to z3
+        self.z3_queued_ms = 0.0   # raced z3 checks' waits for a worker (interrupted checks lingering)
+        self.z3_unknown_beside_interrupted = 0  # z3 unknowns while an interrupted check still ran
 
     def __repr__(self):
         return (f"mythgpu: {self.queries} queries, {self.gpu_models} GPU models, {self.fallbacks} to z3 "
                 f"({self.unsupported} unsupported, {self.errors} errors, {self.rejected} rejected), "
                 f"{self.candidates} candidates in {self.gpu_time:.3f} s; {self.races} raced, "
                 f"{self.z3_answers} by z3 (+{self.race_overhead * 1e3:.1f} ms over z3), "
-                f"{self.negative_hits} negative-cache repeats")
+                f"{self.negative_hits} negative-cache repeats, {self.z3_unknown_beside_interrupted} z3 unknown "
+                f"beside an interrupted check")
 
 
 STATS = HookStats()
@@ -108,7 +111,9 @@ def _solver_statistics():
 def _record(dt: float, answered: bool) -> None:
     """Feed the hook's work into LASER's ``SolverStatistics`` (what ``--solver-log`` /
     the statistics report print): a query the GPU answered never reaches the
-    ``stat_smt_query``-wrapped z3 check, so it is counted here, with its time; the GPU
+    ``stat_smt_query``-wrapped z3 check, so it is counted here, with its time (the hook's
+    wall time); a query z3 answered in the race is counted with z3's own check seconds, as
+    ``stat_smt_query`` times only the check (``solver_statistics.py:16-22``).  The GPU
     counters ride along as extra attributes of the same singleton."""
     st = _solver_statistics()
     if st is None:
@@ -164,6 +169,10 @@ NEGATIVE = NegativeCache()
 # thread waits for the first answer.  Two z3 workers: an interrupted check that is slow to
 # notice ``Z3_interrupt`` does not hold up the next query's.
 _Z3_POOL = ThreadPoolExecutor(max_workers=2, thread_name_prefix="mythgpu-z3")
+# z3 checks the GPU beat that are still running (``Z3_interrupt`` is noticed at z3's next
+# checkpoint): a new check starts only on a free worker, so at most two of them compete with it
+_LINGER = threading.Lock()
+_LINGERING = [0]
 _GPU_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="mythgpu-gpu")
 # longest single launch while racing: after z3 answers, the engine is free within this
 RACE_LAUNCH_S = 0.002
@@ -183,21 +192,42 @@ class Z3Race:
         self.timeout_ms = max(1, int(timeout_ms))
         self.result = None
         self.model = None
-        self.seconds = 0.0
+        self.seconds = 0.0        # z3's own check, from its real start (what stat_smt_query times)
+        self.queued_ms = 0.0      # submission -> a free worker
+        self.beside_interrupted = 0  # interrupted checks still running when this one started
+        self.submitted = time.perf_counter()
+        self._interrupted = False
+        self._finished = False
 
     def run(self):
         z3 = self.z3
-        t0 = time.perf_counter()
-        s = z3.Optimize(ctx=self.ctx)
-        s.set("timeout", self.timeout_ms)
-        s.add(*self.raws)
-        self.result = s.check()
-        if self.result == z3.sat:
-            self.model = s.model()
-        self.seconds = time.perf_counter() - t0
+        t_start = time.perf_counter()
+        self.queued_ms = (t_start - self.submitted) * 1e3
+        with _LINGER:
+            self.beside_interrupted = _LINGERING[0]
+        try:
+            s = z3.Optimize(ctx=self.ctx)
+            # the budget left of the reference's timeout: a check that waited for a worker (two
+            # interrupted checks still running) does not end past the query's wall-clock budget
+            s.set("timeout", max(1, self.timeout_ms - int(self.queued_ms)))
+            s.add(*self.raws)
+            t0 = time.perf_counter()
+            self.result = s.check()
+            self.seconds = time.perf_counter() - t0
+            if self.result == z3.sat:
+                self.model = s.model()
+        finally:
+            with _LINGER:
+                self._finished = True
+                if self._interrupted:
+                    _LINGERING[0] -= 1
         return self
 
     def interrupt(self) -> None:
+        with _LINGER:
+            if not self._finished and not self._interrupted:
+                self._interrupted = True
+                _LINGERING[0] += 1
         try:
             self.ctx.interrupt()
         except Exception:  # pragma: no cover - the check already ended
@@ -221,7 +251,11 @@ def race(gpu_job, z3_job, confirm):
                 res = f_gpu.result()
             except Exception as e:
                 _count_error(e)
-            model = confirm(res)
+            model = None
+            try:  # a z3 error re-checking the hit, or a model that does not decode: z3's answer stands
+                model = confirm(res)
+            except Exception as e:
+                _count_error(e)
             if model is not None:
                 z3_job.interrupt()
                 return "gpu", model
@@ -359,13 +393,28 @@ def _race(original, constraints, enforce_execution_time):
     dt = time.perf_counter() - t0
     STATS.race_z3_time += r.seconds
     STATS.race_overhead += max(0.0, dt - r.seconds)
-    _record(dt, True)
+    STATS.z3_queued_ms += r.queued_ms
+    if r.result == z3.unknown and r.beside_interrupted:
+        STATS.z3_unknown_beside_interrupted += 1
+    _record(r.seconds, True)
     if r.result == z3.sat:
         return Model([r.model.translate(z3.main_ctx())])
-    NEGATIVE.add(constraints)
+    # the negative cache keeps unsat, and unknown only at the full solver timeout: a budget cut
+    # by the execution timeout (or by a wait for a worker) may be what made z3 give up
+    if r.result == z3.unsat or (r.queued_ms < 1.0 and total >= _full_timeout()):
+        NEGATIVE.add(constraints)
     if r.result == z3.unknown:
         log.debug("Timeout encountered while solving expression using z3")
     raise _unsat_error()
+
+
+def _full_timeout() -> float:
+    try:
+        from mythril.support.support_args import args  # type: ignore
+
+        return float(args.solver_timeout)
+    except Exception:
+        return float("inf")
 
 
 def _gpu_search(terms, budget_s, cancel):

@@ -594,12 +594,15 @@ class Solver:
 class Optimize(Solver):
     DELAY = 0.0
     ANSWER = None  # None: check the assertions like Solver (all symbols 0 unless pinned)
+    LINGER = 0.0   # seconds an interrupted check keeps running before it notices
     calls = []
 
     def check(self, *args):
         t0 = time.perf_counter()
+        linger = Optimize.LINGER
         interrupted = self.ctx.interrupted.wait(Optimize.DELAY) if Optimize.DELAY > 0 else False
         if interrupted:
+            time.sleep(linger)
             r = unknown
         elif Optimize.ANSWER is not None:
             r = Optimize.ANSWER

@@ -69,3 +69,32 @@ def test_replace_with_actual_sha_on_gpu(engine):
     txs = [{"input": "0xa9059cbb" + "%064x" % h_val}]
     replace_with_actual_sha(txs, model, km)
     assert txs[0]["input"] == "0xa9059cbb" + oracle_keccak(a_val.to_bytes(32, "big")).hex()
+
+
+@pytest.mark.gpu
+def test_engine_calls_from_two_threads(engine):
+    """The z3 race's thread layout: a search on one worker thread while another
+    thread hashes through ``mg_keccak256`` — neither thread ran ``mg_init``, and every entry
+    point makes the engine's device current on its calling thread (``OnDevice``)."""
+    import threading
+
+    from mythril_amd import search, workloads
+
+    roots = [c.raw for c in workloads.WORKLOADS["token_transfer_underflow"]()]
+    out = {}
+
+    def hashing():
+        msgs = [bytes([k]) * k for k in range(1, 40)]
+        out["k"] = (engine.keccak256(msgs), [oracle_keccak(m) for m in msgs])
+
+    def searching():
+        out["s"] = search.search(engine, roots, jit="never", timeout_s=5)
+
+    ts = [threading.Thread(target=hashing), threading.Thread(target=searching)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    got, want = out["k"]
+    assert [bytes(g) for g in got] == want
+    assert out["s"].index is not None

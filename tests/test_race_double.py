@@ -132,3 +132,52 @@ def test_race_reference_path_when_nothing_to_race(mythril_standin, monkeypatch):
     assert hooked(tuple(_query())) == "z3-model"
     assert plugin.STATS.unsupported == 1 and len(S.calls) == 3 and not z3.Optimize.calls
     assert not S.state.budgets  # the GPU never searched
+
+
+def test_race_solver_time_is_z3_check_time(mythril_standin):
+    """``SolverStatistics.solver_time`` gets z3's own check seconds for a z3-answered race (what
+    ``stat_smt_query`` times, ``solver_statistics.py:16-22``), not the hook's wall time."""
+    S = mythril_standin
+    z3.Optimize.DELAY, z3.Optimize.ANSWER = 0.03, z3.unsat
+    S.state.result, S.state.delay = SearchResult(None, 0, 1 << 20, 0.01), 0.01
+    hooked = plugin.gpu_first(S.original)
+    before = _Stats().solver_time
+    with pytest.raises(_UnsatError):
+        hooked(tuple(_query()))
+    check_s = z3.Optimize.calls[-1][2]
+    assert _Stats().solver_time - before == pytest.approx(check_s, abs=2e-4)
+
+
+def test_race_lingering_interrupted_checks(mythril_standin):
+    """Two checks the GPU beat keep running after ``Z3_interrupt`` (LINGER): the next query's z3
+    check waits for a worker, its timeout is what is left of the query budget, and an
+    ``unknown`` it returns beside an interrupted check is counted."""
+    S = mythril_standin
+    z3.Optimize.DELAY, z3.Optimize.ANSWER, z3.Optimize.LINGER = 5.0, z3.sat, 0.15
+    S.state.result = _hit()
+    hooked = plugin.gpu_first(S.original)
+    for k in range(2):
+        hooked(tuple(_query()))  # GPU wins twice; both z3 checks linger 150 ms
+    assert plugin.STATS.gpu_models == 2
+    z3.Optimize.DELAY, z3.Optimize.ANSWER, z3.Optimize.LINGER = 0.01, z3.unknown, 0.0
+    S.state.result = SearchResult(None, 0, 1 << 20, 0.001)
+    cs = tuple(_query())
+    with pytest.raises(_UnsatError):
+        hooked(cs)
+    assert _wait_for(lambda: len(z3.Optimize.calls) == 3)
+    timeout = min(c[1] for c in z3.Optimize.calls)
+    assert timeout <= 9_500 - 100  # queued ~150 ms behind the lingering pair
+    assert plugin.STATS.z3_queued_ms >= 100
+    # the first lingering check ended as this one started, the second was still running
+    assert plugin.STATS.z3_unknown_beside_interrupted == 1
+    assert cs not in plugin.NEGATIVE  # an unknown on a cut budget is not cached
+
+
+def test_race_confirm_error_waits_for_z3(mythril_standin, monkeypatch):
+    """A z3 error while re-checking a GPU hit is counted and z3's own answer is returned."""
+    S = mythril_standin
+    z3.Optimize.DELAY, z3.Optimize.ANSWER = 0.02, z3.sat
+    S.state.result = _hit()
+    monkeypatch.setattr(z3bridge, "pin_model", lambda *a, **k: (_ for _ in ()).throw(RuntimeError("z3")))
+    m = plugin.gpu_first(S.original)(tuple(_query()))
+    assert m.raw[0].env == ({}, {}, {}) and plugin.STATS.errors == 1 and plugin.STATS.gpu_models == 0

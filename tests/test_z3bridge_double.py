@@ -36,11 +36,11 @@ def fz3(monkeypatch):
     monkeypatch.setattr(z3bridge, "_OPS", None)
     z3.Solver.instances.clear()
     z3.Solver.FORCE = None
-    z3.Optimize.DELAY, z3.Optimize.ANSWER = 0.0, None
+    z3.Optimize.DELAY, z3.Optimize.ANSWER, z3.Optimize.LINGER = 0.0, None, 0.0
     z3.Optimize.calls.clear()
     yield z3
     z3.Solver.FORCE = None
-    z3.Optimize.DELAY, z3.Optimize.ANSWER = 0.0, None
+    z3.Optimize.DELAY, z3.Optimize.ANSWER, z3.Optimize.LINGER = 0.0, None, 0.0
 
 
 # ---------------------------------------------------------------------------------------
