@@ -291,9 +291,16 @@ int mg_jit_helper_pid(void);
 /* host-only: the specialised source (search kernel if gen_blob, else eval kernel), optionally hipRTC-compiled */
 int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words, int compile,
                           char* buf, size_t cap, size_t* out_len);
+/* host-only: the first tier's assembly (search + gen kernels), optionally assembled */
+int mg_program_jit_asm(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words, int compile,
+                       char* buf, size_t cap, size_t* out_len);
 int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle);
-/* flags: MG_JIT_GEN_VERDICTS also builds mgj_gen (per-candidate verdicts, mg_jit_verdicts) */
+/* flags: MG_JIT_GEN_VERDICTS also builds mgj_gen (per-candidate verdicts, mg_jit_verdicts);
+ * MG_JIT_ASM builds the first tier instead: the same kernels emitted as gfx950 assembly with the
+ * engine's own register allocation, assembled and linked in a few ms (clang + LLVM take ~140 ms);
+ * MG_E_UNSUPPORTED for programs outside it (division, EXP, Keccak, variable shifts, UMUL_NOOVF) */
 #define MG_JIT_GEN_VERDICTS 1u
+#define MG_JIT_ASM 2u
 int mg_jit_compile_ex(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* jit_handle);
 int mg_jit_verdicts(uint64_t jit, uint64_t seed, uint64_t start, uint64_t n, uint8_t* verdict_out);
 /* Asynchronous compile on the engine's compile thread (outside the engine lock: searches on

@@ -18,7 +18,7 @@ LIB = PKG / "libmythgpu.so"
 JITD = PKG / "mythgpu_jitd"  # the JIT compiler process (csrc/jitd.cpp), next to the library
 JITD_SOURCES = [CSRC / "jitd.cpp", CSRC / "jit.cpp", CSRC / "program.cpp"]
 
-SOURCES = [CSRC / "engine.hip", CSRC / "program.cpp", CSRC / "jit.cpp"]
+SOURCES = [CSRC / "engine.hip", CSRC / "program.cpp", CSRC / "jit.cpp", CSRC / "jit_asm.cpp"]
 HEADERS = [CSRC / "bv_device.h", CSRC / "keccak_device.h", CSRC / "gen_device.h", CSRC / "jit_device.h", CSRC / "program.hpp",
            CSRC / "jit.hpp", INCLUDE / "mythgpu.h"]
 PRELUDE_PARTS = [CSRC / "bv_device.h", CSRC / "keccak_device.h", CSRC / "gen_device.h", CSRC / "jit_device.h"]

@@ -2048,7 +2048,19 @@ static int jit_launch_async(Engine& e, hipFunction_t f, int nb, uint64_t count, 
     const char* g = getenv("MYTHGPU_JIT_BPC");
     return g ? std::max(1, atoi(g)) : 0;
   }();
-  const uint64_t bpc = bpc_env ? (uint64_t)bpc_env : (count > (1ull << 29) ? 128u : 64u);
+  // Small launches: every wave still sweeps at least MYTHGPU_JIT_MIN_GROUPS (default 16) groups of
+  // 64 candidates, so its start-up (lane key, dictionary staging) and its end-of-wave publish are
+  // amortised — at 64 blocks per CU a 2^24 launch gave each wave 4 groups (C2 60 G/s against 175
+  // at 2^28, profiles/r03_config_sweeps.jsonl)
+  static const uint64_t min_groups = [] {
+    const char* g = getenv("MYTHGPU_JIT_MIN_GROUPS");
+    return g ? (uint64_t)std::max(0, atoi(g)) : 16ull;
+  }();
+  uint64_t bpc = bpc_env ? (uint64_t)bpc_env : (count > (1ull << 29) ? 128u : 64u);
+  if (!bpc_env && min_groups) {
+    const uint64_t waves_cu = std::max<uint64_t>(1, ((count + 63) / 64) / (min_groups * (uint64_t)std::max(e.cu_count, 1)));
+    bpc = std::max<uint64_t>(1, std::min(bpc, waves_cu / 4));
+  }
   (void)nb;
   const uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * bpc;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
@@ -2117,6 +2129,38 @@ int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_bl
     std::string log;
     rc = jit_compile(src, code, log);
     if (rc) return set_err(rc, "JIT compile failed: " + log.substr(0, 4000));
+  }
+  return MG_OK;
+}
+
+int mg_program_jit_asm(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words, int compile,
+                       char* buf, size_t cap, size_t* out_len) {
+  if (!gen_blob) return set_err(MG_E_INVALID, "the assembly tier needs a generator");
+  Lowered low;
+  std::string err;
+  int rc = lower_program(ssa, len, low, err);
+  if (rc) return set_err(rc, err);
+  std::vector<GenSpec> specs;
+  std::vector<uint32_t> consts;
+  rc = parse_gen(low, gen_blob, gen_words, specs, consts, err);
+  if (rc) return set_err(rc, err);
+  Lowered sp;
+  rc = specialize_program(low, &specs, &consts, sp, err, /*keep_watch=*/false);
+  if (rc) return set_err(rc, err);
+  std::string src;
+  rc = jit_asm_source(sp, specs, consts, JIT_SEARCH | JIT_GEN, src, err);
+  if (rc) return set_err(rc, "JIT assembly tier: " + err);
+  if (out_len) *out_len = src.size();
+  if (buf && cap) {
+    const size_t n = std::min(cap - 1, src.size());
+    std::memcpy(buf, src.data(), n);
+    buf[n] = 0;
+  }
+  if (compile) {
+    std::vector<char> code;
+    std::string log;
+    rc = jit_compile(src, code, log);
+    if (rc) return set_err(rc, "JIT assembly failed: " + log.substr(0, 4000));
   }
   return MG_OK;
 }
@@ -2191,8 +2235,23 @@ static void jit_worker_main(Engine* ep, int device) {
     lk.unlock();
     const auto t0 = std::chrono::steady_clock::now();
     const uint32_t kernels = t->has_gen ? (JIT_SEARCH | ((t->flags & MG_JIT_GEN_VERDICTS) ? JIT_GEN : 0u)) : JIT_EVAL;
-    const std::string src = t->has_gen ? jit_source(t->low, &t->specs, &t->consts, kernels)
-                                       : jit_source(t->low, nullptr, nullptr, kernels);
+    std::string src, asm_err;
+    int asm_rc = MG_OK;
+    if (t->flags & MG_JIT_ASM) {
+      // the first tier: assembly straight from the specialised program (jit_asm.cpp)
+      asm_rc = t->has_gen ? jit_asm_source(t->low, t->specs, t->consts, kernels, src, asm_err) : MG_E_UNSUPPORTED;
+      if (!t->has_gen) asm_err = "the assembly tier builds search kernels only";
+    } else {
+      src = t->has_gen ? jit_source(t->low, &t->specs, &t->consts, kernels) : jit_source(t->low, nullptr, nullptr, kernels);
+    }
+    if (asm_rc != MG_OK) {
+      lk.lock();
+      t->rc = asm_rc;
+      t->err = "JIT assembly tier: " + asm_err;
+      t->state = JitTicket::FAILED;
+      e.jit_done_cv.notify_all();
+      continue;
+    }
     std::unique_ptr<DevJit> j;
     std::vector<char> code;
     lk.lock();

@@ -1436,6 +1436,72 @@ int comgr_compile(const std::string& src, std::vector<char>& code, std::string& 
   return rc;
 }
 
+// assembly (the first tier, jit_asm.cpp) -> relocatable -> code object
+int comgr_assemble(const std::string& src, std::vector<char>& code, std::string& log) {
+  Comgr& c = comgr();
+  amd_comgr_data_t src_d{0};
+  amd_comgr_data_set_t in{0}, rel{0}, exe{0};
+  amd_comgr_action_info_t ai{0};
+  int rc = MG_E_HIP;
+  auto collect_log = [&](amd_comgr_data_set_t set) {
+    size_t n = 0;
+    if (c.data_count(set, AMD_COMGR_DATA_KIND_LOG, &n) != AMD_COMGR_STATUS_SUCCESS) return;
+    for (size_t i = 0; i < n; i++) {
+      amd_comgr_data_t d;
+      if (c.data_get(set, AMD_COMGR_DATA_KIND_LOG, i, &d) != AMD_COMGR_STATUS_SUCCESS) continue;
+      size_t sz = 0;
+      if (c.get_data(d, &sz, nullptr) == AMD_COMGR_STATUS_SUCCESS && sz > 1) {
+        std::string t(sz, '\0');
+        c.get_data(d, &sz, &t[0]);
+        log += t;
+      }
+      c.release_data(d);
+    }
+  };
+  do {
+    if (c.create_data(AMD_COMGR_DATA_KIND_SOURCE, &src_d) || c.set_data(src_d, src.size(), src.data()) ||
+        c.set_data_name(src_d, "mythgpu_jit.s"))
+      break;
+    if (c.create_set(&in) || c.create_set(&rel) || c.create_set(&exe) || c.set_add(in, src_d)) break;
+    if (c.create_info(&ai) || c.set_language(ai, AMD_COMGR_LANGUAGE_NONE) ||
+        c.set_isa(ai, "amdgcn-amd-amdhsa--gfx950") || c.set_logging(ai, true))
+      break;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (c.do_action(AMD_COMGR_ACTION_ASSEMBLE_SOURCE_TO_RELOCATABLE, ai, in, rel)) {
+      collect_log(rel);
+      break;
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    if (c.do_action(AMD_COMGR_ACTION_LINK_RELOCATABLE_TO_EXECUTABLE, ai, rel, exe)) {
+      collect_log(exe);
+      break;
+    }
+    if (getenv("MYTHGPU_JIT_TIMING")) {
+      const auto t2 = std::chrono::steady_clock::now();
+      auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+      fprintf(stderr, "mythgpu jit asm: %zu bytes, assemble %.2f ms, link %.2f ms\n", src.size(), ms(t0, t1), ms(t1, t2));
+    }
+    log.clear();  // the driver's notes about unused options
+    size_t n = 0;
+    amd_comgr_data_t o;
+    if (c.data_count(exe, AMD_COMGR_DATA_KIND_EXECUTABLE, &n) || n != 1 ||
+        c.data_get(exe, AMD_COMGR_DATA_KIND_EXECUTABLE, 0, &o))
+      break;
+    size_t sz = 0;
+    if (c.get_data(o, &sz, nullptr) == AMD_COMGR_STATUS_SUCCESS && sz) {
+      code.resize(sz);
+      if (c.get_data(o, &sz, code.data()) == AMD_COMGR_STATUS_SUCCESS) rc = MG_OK;
+    }
+    c.release_data(o);
+  } while (false);
+  if (ai.handle) c.destroy_info(ai);
+  for (amd_comgr_data_set_t s : {in, rel, exe})
+    if (s.handle) c.destroy_set(s);
+  if (src_d.handle) c.release_data(src_d);
+  if (rc != MG_OK && log.empty()) log = "comgr assembly failed";
+  return rc;
+}
+
 int hiprtc_compile(const std::string& src, std::vector<char>& code, std::string& log) {
   Rtc& r = rtc();
   if (!r.ok) {
@@ -1811,7 +1877,14 @@ int jit_compile_local(const std::string& src, std::vector<char>& code, std::stri
   const char* which = getenv("MYTHGPU_JIT_COMPILER");
   const bool use_rtc = which && std::strcmp(which, "hiprtc") == 0;
   int rc;
-  if (!use_rtc && comgr().ok) {
+  const bool is_asm = src.compare(0, std::strlen(kAsmMarker), kAsmMarker) == 0;
+  if (is_asm) {
+    if (!comgr().ok) {
+      log = "comgr not available (the assembly tier needs it)";
+      return MG_E_UNSUPPORTED;
+    }
+    rc = comgr_assemble(src, code, log);
+  } else if (!use_rtc && comgr().ok) {
     rc = comgr_compile(src, code, log);
   } else {
     rc = hiprtc_compile(src, code, log);
@@ -1820,7 +1893,7 @@ int jit_compile_local(const std::string& src, std::vector<char>& code, std::stri
   // MYTHGPU_JIT_DUMP=<prefix>: keep the source and code object for offline disassembly
   if (const char* dump = getenv("MYTHGPU_JIT_DUMP")) {
     const std::string base(dump);
-    if (FILE* f = fopen((base + ".hip").c_str(), "wb")) {
+    if (FILE* f = fopen((base + (is_asm ? ".s" : ".hip")).c_str(), "wb")) {
       fwrite(src.data(), 1, src.size(), f);
       fclose(f);
     }

@@ -14,6 +14,14 @@ enum : uint32_t { JIT_SEARCH = 1, JIT_EVAL = 2, JIT_GEN = 4 };
 std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
                        uint32_t kernels);
 
+// The first tier (jit_asm.cpp): the same kernels (JIT_SEARCH, optionally JIT_GEN) as gfx950 assembly
+// with the emitter's own register allocation; assembled and linked by comgr in a few ms instead of
+// ~140 ms of clang + LLVM.  MG_E_UNSUPPORTED (err says why) for programs outside the tier.
+// Sources starting with kAsmMarker are assembled, not compiled, by jit_compile*.
+constexpr const char* kAsmMarker = "; mythgpu-asm";
+int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const std::vector<uint32_t>& gconsts,
+                   uint32_t kernels, std::string& out, std::string& err);
+
 // Load the JIT compiler library now (on the calling thread): its static destructors then
 // register before anything the caller registers with atexit afterwards.
 void jit_compiler_preload();

@@ -1,0 +1,2041 @@
+// JIT first tier: gfx950 assembly emitted straight from the specialised program.
+//
+// The HIP-source JIT (jit.cpp) costs ~140 ms of clang + LLVM per query on the box's host
+// (profiles/r04a_jit_phases.jsonl: C2 front end + optimiser 54 ms, machine code generation
+// 84 ms), longer than a hard query's whole search.  This emitter writes the same search kernel
+// (mgj_search; mgj_gen for per-candidate verdicts) as GCN assembly with its own register
+// allocation, so a compile is the emission (well under a millisecond) plus an assembler pass and
+// a link (comgr, a few ms).  The O3 kernel still compiles behind it and replaces it on the same
+// index stream (search.search); both compute the verdict of every index exactly as the
+// interpreter and the C port do (GEN3, include/mythgpu.h).
+//
+// Model of the code:
+//  * one wave = one aligned group of 64 candidate indices; EXEC stays all-ones inside the body
+//    (every choice the generator makes per group is an SGPR branch, every per-lane choice a
+//    v_cndmask), so no structurisation is needed;
+//  * a value of width w is ceil(w/32) limbs, each a literal or a VGPR (copies are aliases:
+//    VGPRs are reference-counted); limbs no user reads are never computed (demanded limbs,
+//    backward pass); a Bool is a 64-lane mask in an SGPR pair (compares write masks, ASSERT
+//    ANDs them into the verdict mask, ITE selects through VCC);
+//  * VCC carries the add/sub chains; gfx950 needs two wait states between a VALU write of an
+//    SGPR (VCC, a compare's mask) and a VALU read of it, which the emitter counts and pads with
+//    s_nop (LLVM's GCNHazardRecognizer does the same); a branch target is treated as a fresh
+//    write of every such SGPR;
+//  * no scalar stores and no scalar-cache writes anywhere: results leave through vector atomics.
+//
+// Programs outside this tier (division, EXP, Keccak, variable shifts, UMUL_NOOVF, values wider
+// than 2048 bits) get MG_E_UNSUPPORTED and stay with the interpreter until the O3 kernel is ready.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <set>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "jit.hpp"
+
+namespace mg {
+
+namespace {
+
+struct AsmFail {
+  std::string why;
+};
+[[noreturn]] void fail(const std::string& w) { throw AsmFail{w}; }
+
+inline uint32_t Lw(uint32_t w) { return (w + 31) / 32; }
+inline uint32_t topmask(uint32_t w) { return (w & 31) ? ((1u << (w & 31)) - 1u) : 0xFFFFFFFFu; }
+inline uint32_t gsalt(uint32_t c, uint32_t j) { return c * 0x9E3779B9u + j * 0x85EBCA6Bu + 0x27D4EB2Fu; }
+
+constexpr int kVCC = 106;  // vcc_lo in the hazard table (vcc_hi = 107)
+constexpr uint32_t kMaxLimbs = 64;
+
+enum LKind : uint8_t { LU, LL, LR };
+struct Limb {
+  LKind k = LU;
+  uint32_t v = 0;
+  bool lit() const { return k == LL; }
+  bool reg() const { return k == LR; }
+  bool operator==(const Limb& o) const { return k == o.k && v == o.v; }
+};
+inline Limb Lit(uint32_t x) { return Limb{LL, x}; }
+inline Limb Reg(uint32_t r) { return Limb{LR, r}; }
+
+// a 64-lane Bool: literal (all lanes equal) or an SGPR pair
+struct Mask {
+  int k = 0;  // 0 none, 1 literal, 2 pair
+  bool ones = false;
+  int s = -1;
+};
+
+struct Val {
+  std::vector<Limb> l;
+  Mask m;
+  uint32_t w = 0;
+  bool def = false;
+};
+
+std::string hexs(uint32_t x) {
+  char b[16];
+  snprintf(b, sizeof b, "0x%x", x);
+  return b;
+}
+// an integer operand: inline constants (-16..64) as decimal, others as a 32-bit literal
+bool inl(uint32_t x) {
+  const int32_t s = (int32_t)x;
+  return s >= -16 && s <= 64;
+}
+std::string imm(uint32_t x) { return inl(x) ? std::to_string((int32_t)x) : hexs(x); }
+std::string V(uint32_t r) { return "v" + std::to_string(r); }
+std::string S(uint32_t r) { return "s" + std::to_string(r); }
+std::string SP(uint32_t r) { return "s[" + std::to_string(r) + ":" + std::to_string(r + 1) + "]"; }
+std::string VP(uint32_t r) { return "v[" + std::to_string(r) + ":" + std::to_string(r + 1) + "]"; }
+
+// fixed registers
+// VGPRs: v0 tid, v1 lane, v2/v3 lane key (lo/hi), v4/v5 group-lane key K (lo/hi), v6 zero, v7 scratch,
+//        v[8:9] 64-bit scratch; the allocator hands out v10 and up
+// SGPRs: s[0:1] kernarg, s2 block id, s3 wave in block, s[4:5] gconsts, s[8:9] start, s[10:11] count,
+//        s[12:13] sk, s[14:15] sg, s[16:17] hit / verdict_out, s18 flags, s19 nblk, s[20:21] a0,
+//        s[22:23] end, s[24:25] ngroups, s[26:27] g, s28 gstride, s29 early, s[30:31] wave best,
+//        s[32:33] wave hits, s[34:35] gbase, s[36:37] G, s[38:39] verdict, s[40:41] temps,
+//        s[42:43] ~0 unless the launch stops early, s6 the group is full, s7 temp; pairs s[44:45] ..
+//        s[98:99] allocated
+constexpr int kV0 = 10;
+constexpr int kS0 = 44, kS1 = 100;
+
+class Emitter {
+ public:
+  std::ostringstream o;
+  int64_t pos = 0;
+  std::map<int, int64_t> vw;  // SGPR -> position of its last VALU write
+  int nlab = 0;
+  std::vector<int> vref = std::vector<int>(256, 0);
+  int vhigh = kV0;
+  std::vector<int> sref = std::vector<int>(kS1, 0);
+  int shigh = kS0;
+
+  // --- instruction streams with the gfx950 VALU-SGPR hazard --------------------------------
+  void valu(const std::string& s, std::initializer_list<int> rd = {}, std::initializer_list<int> wr = {}) {
+    int64_t need = 0;
+    for (int r : rd) {
+      auto it = vw.find(r);
+      if (it != vw.end()) need = std::max(need, it->second + 3 - pos);
+    }
+    if (need > 0) {
+      o << "  s_nop " << (need - 1) << "\n";
+      pos += need;
+    }
+    o << "  " << s << "\n";
+    pos++;
+    for (int r : wr) vw[r] = pos - 1;
+  }
+  void salu(const std::string& s, std::initializer_list<int> wr = {}) {
+    o << "  " << s << "\n";
+    pos++;
+    for (int r : wr) vw.erase(r);
+  }
+  // memory / wait / branch instructions: no wait-state credit; a VMEM reading an SGPR a VALU wrote
+  // needs five
+  void mem(const std::string& s, std::initializer_list<int> rd = {}) {
+    int64_t need = 0;
+    for (int r : rd) {
+      auto it = vw.find(r);
+      if (it != vw.end()) need = std::max(need, it->second + 6 - pos);
+    }
+    if (need > 0) {
+      o << "  s_nop " << (need - 1) << "\n";
+      pos += need;
+    }
+    o << "  " << s << "\n";
+  }
+  void ctl(const std::string& s) { o << "  " << s << "\n"; }
+  std::string newlab() { return ".Lm" + std::to_string(nlab++); }
+  void label(const std::string& L) {
+    o << L << ":\n";
+    for (auto& kv : vw) kv.second = std::max(kv.second, pos - 1);
+  }
+  static std::initializer_list<int> none() { return {}; }
+
+  // --- VGPRs ---------------------------------------------------------------------------------
+  uint32_t valloc() {
+    for (int r = kV0; r < 256; r++)
+      if (!vref[r]) {
+        vref[r] = 1;
+        vhigh = std::max(vhigh, r + 1);
+        return (uint32_t)r;
+      }
+    fail("out of VGPRs");
+  }
+  void retain(const Limb& l) {
+    if (l.reg() && (int)l.v >= kV0) vref[l.v]++;
+  }
+  void release(const Limb& l) {
+    if (l.reg() && (int)l.v >= kV0) {
+      if (--vref[l.v] < 0) fail("internal: VGPR released twice");
+    }
+  }
+  // --- SGPR pairs ----------------------------------------------------------------------------
+  int salloc() {
+    for (int r = kS0; r + 1 < kS1; r += 2)
+      if (!sref[r]) {
+        sref[r] = 1;
+        shigh = std::max(shigh, r + 2);
+        return r;
+      }
+    fail("out of SGPRs");
+  }
+  void sretain(const Mask& m) {
+    if (m.k == 2) sref[m.s]++;
+  }
+  void srelease(const Mask& m) {
+    if (m.k == 2 && --sref[m.s] < 0) fail("internal: SGPR pair released twice");
+  }
+};
+
+struct Gen {
+  const Lowered& P;
+  const std::vector<GenSpec>& specs;
+  const std::vector<uint32_t>& G;  // generator constants
+  Emitter E;
+  std::vector<Val> val;
+  std::vector<uint64_t> need;        // demanded limbs per value id (bit j = limb j)
+  std::vector<int32_t> last;         // last vcode index reading each value id
+  std::map<uint32_t, uint32_t> cval; // coordinate -> value id of its (latest) generated value
+  std::vector<int32_t> def;          // value id -> defining vcode index
+  std::vector<uint32_t> copysrc;     // vcode index of a MIXED K_COORD -> its COPY source's value id
+  bool gen_kernel = false;           // mgj_gen (verdict bytes) instead of mgj_search
+
+  Gen(const Lowered& p, const std::vector<GenSpec>& s, const std::vector<uint32_t>& g)
+      : P(p), specs(s), G(g), val(p.vwidth.size()), need(p.vwidth.size(), 0), last(p.vwidth.size(), -1),
+        def(p.vwidth.size(), -1) {}
+
+  // ---------------------------------------------------------------------------------------
+  // analysis
+  // ---------------------------------------------------------------------------------------
+  static uint64_t lowmask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
+  uint32_t L(uint32_t id) const { return Lw(P.vwidth[id]); }
+
+  // bits [p, p + n) of a value of width w -> its limbs
+  static uint64_t bit_limbs(uint32_t p, uint32_t n, uint32_t w) {
+    if (p >= w || n == 0) return 0;
+    const uint32_t e = std::min(w, p + n);
+    uint64_t m = 0;
+    for (uint32_t q = p / 32; q * 32 < e; q++) m |= 1ull << q;
+    return m;
+  }
+
+  void analyse() {
+    for (uint32_t id = 0; id < P.vwidth.size(); id++)
+      if (Lw(P.vwidth[id]) > kMaxLimbs) fail("value wider than 2048 bits");
+    for (size_t k = 0; k < P.vcode.size(); k++) {
+      const Instr& in = P.vcode[k];
+      if (in.dst != MG_NONE && in.dst < def.size() && def[in.dst] < 0) def[in.dst] = (int32_t)k;
+      switch (in.op) {
+        case K_CONST: case K_COORD: case K_ADD: case K_SUB: case K_NEG: case K_AND: case K_OR: case K_XOR:
+        case K_NOT: case K_ITE: case K_EQ: case K_ULT: case K_ULE: case K_SLT: case K_SLE: case K_CONCAT:
+        case K_EXTRACT: case K_ZEXT: case K_SEXT: case K_LOOKUP: case K_ASSERT: case K_COPY: case K_MUL:
+        case K_WATCH:
+          break;
+        default:
+          fail("op " + std::to_string(in.op) + " outside the assembly tier");
+      }
+    }
+    // uses (for liveness) and demanded limbs (backward)
+    auto use = [&](uint32_t id, size_t k) {
+      if (id != MG_NONE && id < last.size()) last[id] = std::max(last[id], (int32_t)k);
+    };
+    std::map<uint32_t, uint32_t> latest;  // coordinate -> value id, in program order
+    copysrc.assign(P.vcode.size(), MG_NONE);
+    for (size_t k = 0; k < P.vcode.size(); k++) {
+      const Instr& in = P.vcode[k];
+      switch (in.op) {
+        case K_CONST: case K_WATCH:
+          break;
+        case K_COORD: {
+          // a MIXED coordinate reads its COPY source's value if the program generated it before
+          const GenSpec& sp = specs.at(in.p0);
+          if ((sp.kind & 0xFFu) == MG_GEN_MIXED && sp.p[3] != MG_NONE && (sp.p[2] & 0xFFFFu)) {
+            auto it = latest.find(sp.p[3]);
+            if (it != latest.end()) {
+              use(it->second, k);
+              copysrc[k] = it->second;
+            }
+          }
+          latest[in.p0] = in.dst;
+          break;
+        }
+        case K_LOOKUP:
+          use(in.a, k);
+          use(in.p0, k);
+          for (uint32_t q = 0; q < 2 * in.c; q++) use(P.vaux[in.p1 + q], k);
+          break;
+        default:
+          use(in.a, k);
+          if (in.op != K_NOT && in.op != K_NEG && in.op != K_EXTRACT && in.op != K_ZEXT && in.op != K_SEXT &&
+              in.op != K_ASSERT && in.op != K_COPY)
+            use(in.b, k);
+          if (in.op == K_ITE) use(in.c, k);
+          break;
+      }
+    }
+    for (size_t kk = P.vcode.size(); kk-- > 0;) {
+      const Instr& in = P.vcode[kk];
+      const uint32_t d = in.dst;
+      const uint64_t nd = (d != MG_NONE && d < need.size()) ? need[d] : 0;
+      auto all = [&](uint32_t id) {
+        if (id != MG_NONE && id < need.size()) need[id] |= lowmask(L(id));
+      };
+      auto upto = [&](uint32_t id, uint64_t m) {  // limbs 0 .. top demanded limb of m
+        if (id == MG_NONE || id >= need.size() || !m) return;
+        const uint32_t top = 63 - (uint32_t)__builtin_clzll(m);
+        need[id] |= lowmask(top + 1) & lowmask(L(id));
+      };
+      auto same = [&](uint32_t id, uint64_t m) {
+        if (id != MG_NONE && id < need.size()) need[id] |= m & lowmask(L(id));
+      };
+      if (in.op == K_COORD && copysrc[kk] != MG_NONE) all(copysrc[kk]);  // copied whole
+      switch (in.op) {
+        case K_ASSERT: all(in.a); break;
+        case K_ADD: case K_SUB: case K_MUL: upto(in.a, nd); upto(in.b, nd); break;
+        case K_NEG: upto(in.a, nd); break;
+        case K_AND: case K_OR: case K_XOR: same(in.a, nd); same(in.b, nd); break;
+        case K_NOT: case K_COPY: same(in.a, nd); break;
+        case K_ITE: all(in.a); same(in.b, nd); same(in.c, nd); break;
+        case K_EQ: case K_ULT: case K_ULE: case K_SLT: case K_SLE: all(in.a); all(in.b); break;
+        case K_ZEXT: same(in.a, nd); break;
+        case K_SEXT: {
+          const uint32_t La = Lw(in.p1);
+          same(in.a, nd);
+          if (nd >> (La - 1)) need[in.a] |= 1ull << (La - 1);
+          break;
+        }
+        case K_EXTRACT:
+          for (uint32_t j = 0; j < 64; j++)
+            if (nd >> j & 1) need[in.a] |= bit_limbs(in.p0 + 32 * j, 32, in.p1);
+          break;
+        case K_CONCAT: {
+          const uint32_t wb = in.p1, W = in.wd;
+          for (uint32_t j = 0; j < 64; j++) {
+            if (!(nd >> j & 1)) continue;
+            const uint32_t p = 32 * j, e = std::min(W, p + 32);
+            if (p < wb) need[in.b] |= bit_limbs(p, std::min(e, wb) - p, wb);
+            if (e > wb) {
+              const uint32_t q = std::max(p, wb) - wb;
+              need[in.a] |= bit_limbs(q, e - std::max(p, wb), W - wb);
+            }
+          }
+          break;
+        }
+        case K_LOOKUP:
+          all(in.a);
+          same(in.p0, nd);
+          for (uint32_t q = 0; q < in.c; q++) {
+            all(P.vaux[in.p1 + 2 * q]);
+            same(P.vaux[in.p1 + 2 * q + 1], nd);
+          }
+          break;
+        default: break;
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------------------------------
+  // operand helpers
+  // ---------------------------------------------------------------------------------------
+  Emitter& e() { return E; }
+
+  // a VGPR holding limb l (a literal is moved into a fresh VGPR the caller releases)
+  Limb vreg(const Limb& l) {
+    if (l.reg()) {
+      E.retain(l);
+      return l;
+    }
+    const uint32_t r = E.valloc();
+    E.valu("v_mov_b32_e32 " + V(r) + ", " + imm(l.lit() ? l.v : 0u));
+    return Reg(r);
+  }
+  std::string src(const Limb& l) const {
+    if (l.k == LU) fail("internal: a limb the demand analysis dropped was read");
+    return l.lit() ? imm(l.v) : V(l.v);
+  }
+
+  // operand usable in a VOP3 slot: VGPR or inline constant (other literals go through a VGPR)
+  Limb v3(const Limb& l) {
+    if (l.lit() && inl(l.v)) return l;
+    return vreg(l);
+  }
+  void drop(const Limb& l) { E.release(l); }
+
+  Limb fresh() { return Reg(E.valloc()); }
+
+  // mask form of a Bool value
+  Mask mask_of(uint32_t id) {
+    Val& x = val[id];
+    if (x.m.k) return x.m;
+    const Limb l = x.l.empty() ? Lit(0) : x.l[0];
+    Mask m;
+    if (l.lit() || l.k == LU) {
+      m.k = 1;
+      m.ones = l.lit() && (l.v & 1u);
+    } else {
+      m.k = 2;
+      m.s = E.salloc();
+      E.valu("v_cmp_ne_u32_e64 " + SP(m.s) + ", 0, " + V(l.v), {}, {m.s, m.s + 1});
+    }
+    x.m = m;
+    return m;
+  }
+  // limb form of a Bool value
+  Limb limb_of_bool(uint32_t id) {
+    Val& x = val[id];
+    if (!x.l.empty() && x.l[0].k != LU) return x.l[0];
+    const Mask m = mask_of(id);
+    Limb l;
+    if (m.k == 1) {
+      l = Lit(m.ones ? 1u : 0u);
+    } else {
+      l = fresh();
+      E.valu("v_cndmask_b32_e64 " + V(l.v) + ", 0, 1, " + SP(m.s), {m.s, m.s + 1});
+    }
+    x.l.assign(1, l);
+    return l;
+  }
+  // limb j of value id (Bools through their limb form)
+  Limb limb(uint32_t id, uint32_t j) {
+    if (P.vwidth[id] == 1 && j == 0) return limb_of_bool(id);
+    const Val& x = val[id];
+    if (j >= x.l.size()) return Lit(0);
+    return x.l[j];
+  }
+  bool is_bool(uint32_t id) const { return P.vwidth[id] == 1; }
+
+  // ---------------------------------------------------------------------------------------
+  // limb arithmetic
+  // ---------------------------------------------------------------------------------------
+  // x + y (+ carry) over limbs lo..hi of the result; `carry` -1: in VCC, 0/1 known
+  // returns the result limbs; the carry out ends in VCC (or known)
+  std::vector<Limb> add_chain(const std::vector<Limb>& x, const std::vector<Limb>& y, uint32_t n, bool sub) {
+    std::vector<Limb> r(n);
+    int carry = 0;  // known 0/1, or -1 = VCC
+    for (uint32_t j = 0; j < n; j++) {
+      const Limb a = j < x.size() ? x[j] : Lit(0), b = j < y.size() ? y[j] : Lit(0);
+      if (a.lit() && b.lit() && carry >= 0) {
+        uint64_t t;
+        if (!sub) {
+          t = (uint64_t)a.v + b.v + (uint64_t)carry;
+          carry = (int)(t >> 32);
+        } else {
+          t = (uint64_t)a.v - b.v - (uint64_t)carry;
+          carry = ((uint64_t)a.v < (uint64_t)b.v + (uint64_t)carry) ? 1 : 0;
+        }
+        r[j] = Lit((uint32_t)t);
+        continue;
+      }
+      if (carry == 0 && ((!sub && a.lit() && a.v == 0) || (b.lit() && b.v == 0))) {
+        r[j] = (b.lit() && b.v == 0) ? a : b;  // x + 0, 0 + y, x - 0: no carry
+        E.retain(r[j]);
+        continue;
+      }
+      if (carry == 1) {
+        E.salu("s_mov_b64 vcc, -1", {kVCC, kVCC + 1});
+        carry = -1;
+      }
+      const Limb d = fresh();
+      if (carry == 0) {
+        if (!sub) {
+          const Limb s0 = b.reg() ? a : b, s1 = b.reg() ? b : a;  // src1 must be a VGPR
+          E.valu("v_add_co_u32_e32 " + V(d.v) + ", vcc, " + src(s0) + ", " + V(s1.v), {}, {kVCC, kVCC + 1});
+        } else if (b.reg()) {
+          E.valu("v_sub_co_u32_e32 " + V(d.v) + ", vcc, " + src(a) + ", " + V(b.v), {}, {kVCC, kVCC + 1});
+        } else {
+          E.valu("v_subrev_co_u32_e32 " + V(d.v) + ", vcc, " + src(b) + ", " + V(a.v), {}, {kVCC, kVCC + 1});
+        }
+      } else {
+        Limb aa = a, bb = b, tmp, tmp2;
+        if (!aa.reg() && !bb.reg()) {
+          if (bb.lit() && bb.v == 0) bb = Reg(6);  // the zero register
+          else if (!sub && aa.lit() && aa.v == 0) aa = Reg(6);
+          else {
+            tmp = vreg(bb);
+            bb = tmp;
+          }
+        }
+        // the carry-in (VCC) is on the constant bus: the other operand must not be a literal
+        if (aa.lit() && !inl(aa.v)) {
+          tmp2 = vreg(aa);
+          aa = tmp2;
+        } else if (bb.lit() && !inl(bb.v)) {
+          tmp2 = vreg(bb);
+          bb = tmp2;
+        }
+        if (!sub) {
+          const Limb s0 = bb.reg() ? aa : bb, s1 = bb.reg() ? bb : aa;
+          E.valu("v_addc_co_u32_e32 " + V(d.v) + ", vcc, " + src(s0) + ", " + V(s1.v) + ", vcc", {kVCC, kVCC + 1},
+                 {kVCC, kVCC + 1});
+        } else if (bb.reg()) {
+          E.valu("v_subb_co_u32_e32 " + V(d.v) + ", vcc, " + src(aa) + ", " + V(bb.v) + ", vcc", {kVCC, kVCC + 1},
+                 {kVCC, kVCC + 1});
+        } else {
+          E.valu("v_subbrev_co_u32_e32 " + V(d.v) + ", vcc, " + src(bb) + ", " + V(aa.v) + ", vcc", {kVCC, kVCC + 1},
+                 {kVCC, kVCC + 1});
+        }
+        drop(tmp);
+        drop(tmp2);
+      }
+      carry = -1;
+      r[j] = d;
+    }
+    last_carry = carry;
+    return r;
+  }
+  int last_carry = 0;
+
+  // d = x & m (m literal): folded, or one v_and_b32
+  Limb and_lit(const Limb& x, uint32_t m) {
+    if (x.lit()) return Lit(x.v & m);
+    if (m == 0) return Lit(0);
+    if (m == 0xFFFFFFFFu) {
+      E.retain(x);
+      return x;
+    }
+    const Limb d = fresh();
+    E.valu("v_and_b32_e32 " + V(d.v) + ", " + imm(m) + ", " + V(x.v));
+    return d;
+  }
+  // the top limb of a width-w result masked (the limb vector owns its registers)
+  void mask_top(std::vector<Limb>& r, uint32_t w) {
+    if (!(w & 31) || r.empty()) return;
+    Limb& t = r.back();
+    if (t.k == LU) return;
+    const Limb m = and_lit(t, topmask(w));
+    drop(t);
+    t = m;
+  }
+
+  // bits [p, p+n) (n <= 32) of the limb vector x (width w) at bit 0, zero above n
+  Limb bits(const std::vector<Limb>& x, uint32_t w, uint32_t p, uint32_t n) {
+    if (p >= w || n == 0) return Lit(0);
+    n = std::min(n, w - p);
+    const uint32_t q = p / 32, r = p % 32;
+    const Limb lo = q < x.size() ? x[q] : Lit(0);
+    const bool need_hi = r && r + n > 32 && (q + 1) * 32 < w;
+    const Limb hi = need_hi && q + 1 < x.size() ? x[q + 1] : Lit(0);
+    const bool clip = n < 32 && p + n < w;  // bits above n may be set
+    const uint32_t m = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    if (lo.k == LU || (need_hi && hi.k == LU)) fail("internal: a limb the demand analysis dropped was read");
+    if (!need_hi || (hi.lit() && hi.v == 0 && !r)) {
+      if (r == 0) {
+        if (!clip) {
+          E.retain(lo);
+          return lo;
+        }
+        return and_lit(lo, m);
+      }
+      if (lo.lit()) return Lit((lo.v >> r) & (clip ? m : 0xFFFFFFFFu));
+      const Limb d = fresh();
+      if (clip) E.valu("v_bfe_u32 " + V(d.v) + ", " + V(lo.v) + ", " + std::to_string(r) + ", " + std::to_string(n));
+      else E.valu("v_lshrrev_b32_e32 " + V(d.v) + ", " + std::to_string(r) + ", " + V(lo.v));
+      return d;
+    }
+    if (lo.lit() && hi.lit()) {
+      const uint32_t t = (uint32_t)((((uint64_t)hi.v << 32) | lo.v) >> r);
+      return Lit(clip ? (t & m) : t);
+    }
+    const Limb a = v3(hi), b = v3(lo);
+    const Limb d = fresh();
+    E.valu("v_alignbit_b32 " + V(d.v) + ", " + src(a) + ", " + src(b) + ", " + std::to_string(r));
+    drop(a);
+    drop(b);
+    if (!clip) return d;
+    const Limb c = and_lit(d, m);
+    drop(d);
+    return c;
+  }
+
+  // (hi << s) | lo, lo < 2^s
+  Limb shl_or(const Limb& hi, uint32_t s, const Limb& lo) {
+    if (hi.lit() && lo.lit()) return Lit((s < 32 ? hi.v << s : 0u) | lo.v);
+    if (hi.lit() && hi.v == 0) {
+      E.retain(lo);
+      return lo;
+    }
+    const Limb a = v3(hi), c = v3(lo);
+    const Limb d = fresh();
+    E.valu("v_lshl_or_b32 " + V(d.v) + ", " + src(a) + ", " + std::to_string(s) + ", " + src(c));
+    drop(a);
+    drop(c);
+    return d;
+  }
+
+  // XOR-OR reduction of the limb pairs -> mask (all lanes where every pair is equal)
+  Mask eq_mask(const std::vector<std::pair<Limb, Limb>>& prs) {
+    std::vector<Limb> diff;  // owned
+    for (const auto& pr : prs) {
+      const Limb a = pr.first, b = pr.second;
+      if (a.lit() && b.lit()) {
+        if (a.v != b.v) {
+          for (auto& d : diff) drop(d);
+          Mask m;
+          m.k = 1;
+          m.ones = false;
+          return m;
+        }
+        continue;
+      }
+      if (a == b) continue;
+      if (a.lit() && a.v == 0) {
+        E.retain(b);
+        diff.push_back(b);
+        continue;
+      }
+      if (b.lit() && b.v == 0) {
+        E.retain(a);
+        diff.push_back(a);
+        continue;
+      }
+      if (prs.size() == 1 || (diff.empty() && &pr == &prs.back())) {
+        // one pair only: one compare
+        const Limb s0 = b.reg() ? a : b, s1 = b.reg() ? b : a;
+        Mask m;
+        m.k = 2;
+        m.s = E.salloc();
+        if (s0.lit() && !inl(s0.v)) {
+          E.valu("v_cmp_eq_u32_e32 vcc, " + src(s0) + ", " + V(s1.v), {}, {kVCC, kVCC + 1});
+          E.salu("s_mov_b64 " + SP(m.s) + ", vcc", {m.s, m.s + 1});
+        } else {
+          E.valu("v_cmp_eq_u32_e64 " + SP(m.s) + ", " + src(s0) + ", " + V(s1.v), {}, {m.s, m.s + 1});
+        }
+        return m;
+      }
+      const Limb d = fresh();
+      const Limb s0 = b.reg() ? a : b, s1 = b.reg() ? b : a;
+      E.valu("v_xor_b32_e32 " + V(d.v) + ", " + src(s0) + ", " + V(s1.v));
+      diff.push_back(d);
+    }
+    Mask m;
+    if (diff.empty()) {
+      m.k = 1;
+      m.ones = true;
+      return m;
+    }
+    while (diff.size() > 1) {
+      std::vector<Limb> nx;
+      for (size_t i = 0; i < diff.size(); i += 3) {
+        const size_t k = std::min<size_t>(3, diff.size() - i);
+        if (k == 1) {
+          nx.push_back(diff[i]);
+          continue;
+        }
+        const Limb d = fresh();
+        if (k == 2) E.valu("v_or_b32_e32 " + V(d.v) + ", " + V(diff[i].v) + ", " + V(diff[i + 1].v));
+        else E.valu("v_or3_b32 " + V(d.v) + ", " + V(diff[i].v) + ", " + V(diff[i + 1].v) + ", " + V(diff[i + 2].v));
+        for (size_t t = 0; t < k; t++) drop(diff[i + t]);
+        nx.push_back(d);
+      }
+      diff.swap(nx);
+    }
+    m.k = 2;
+    m.s = E.salloc();
+    E.valu("v_cmp_eq_u32_e64 " + SP(m.s) + ", 0, " + V(diff[0].v), {}, {m.s, m.s + 1});
+    drop(diff[0]);
+    return m;
+  }
+
+  // x < y (unsigned) over La limbs, as a mask; sgn: the top limbs' bit (w-1)&31 flipped first
+  Mask lt_mask(std::vector<Limb> x, std::vector<Limb> y, uint32_t w, bool sgn) {
+    const uint32_t La = Lw(w);
+    x.resize(La, Lit(0));
+    y.resize(La, Lit(0));
+    std::vector<Limb> own;
+    if (sgn) {
+      const uint32_t f = 1u << ((w - 1) & 31);
+      for (auto* v : {&x, &y}) {
+        Limb& t = (*v)[La - 1];
+        if (t.lit()) {
+          t.v ^= f;
+        } else {
+          const Limb d = fresh();
+          E.valu("v_xor_b32_e32 " + V(d.v) + ", " + imm(f) + ", " + V(t.v));
+          t = d;
+          own.push_back(d);
+        }
+      }
+    }
+    Mask m;
+    // all-literal limbs from the top decide or drop out: find the lowest limb that matters
+    if (La == 1) {
+      const Limb a = x[0], b = y[0];
+      if (a.lit() && b.lit()) {
+        m.k = 1;
+        m.ones = a.v < b.v;
+      } else {
+        m.k = 2;
+        m.s = E.salloc();
+        if (b.reg()) {
+          if (a.lit() && !inl(a.v)) {
+            E.valu("v_cmp_lt_u32_e32 vcc, " + src(a) + ", " + V(b.v), {}, {kVCC, kVCC + 1});
+            E.salu("s_mov_b64 " + SP(m.s) + ", vcc", {m.s, m.s + 1});
+          } else {
+            E.valu("v_cmp_lt_u32_e64 " + SP(m.s) + ", " + src(a) + ", " + V(b.v), {}, {m.s, m.s + 1});
+          }
+        } else {
+          if (!inl(b.v)) {
+            E.valu("v_cmp_gt_u32_e32 vcc, " + src(b) + ", " + V(a.v), {}, {kVCC, kVCC + 1});
+            E.salu("s_mov_b64 " + SP(m.s) + ", vcc", {m.s, m.s + 1});
+          } else {
+            E.valu("v_cmp_gt_u32_e64 " + SP(m.s) + ", " + src(b) + ", " + V(a.v), {}, {m.s, m.s + 1});
+          }
+        }
+      }
+      for (auto& d : own) drop(d);
+      return m;
+    }
+    // borrow chain of x - y; the difference itself is thrown away (v7)
+    int borrow = 0;
+    for (uint32_t j = 0; j < La; j++) {
+      const Limb a = x[j], b = y[j];
+      if (a.lit() && b.lit() && borrow >= 0) {
+        borrow = ((uint64_t)a.v < (uint64_t)b.v + (uint64_t)borrow) ? 1 : 0;
+        continue;
+      }
+      if (borrow == 1) {
+        E.salu("s_mov_b64 vcc, -1", {kVCC, kVCC + 1});
+        borrow = -1;
+      }
+      if (borrow == 0) {
+        if (b.reg()) E.valu("v_sub_co_u32_e32 v7, vcc, " + src(a) + ", " + V(b.v), {}, {kVCC, kVCC + 1});
+        else E.valu("v_subrev_co_u32_e32 v7, vcc, " + src(b) + ", " + V(a.v), {}, {kVCC, kVCC + 1});
+      } else {
+        Limb aa = a, bb = b, tmp, tmp2;
+        if (!aa.reg() && !bb.reg()) {
+          tmp = vreg(bb);
+          bb = tmp;
+        }
+        if (aa.lit() && !inl(aa.v)) {  // VCC is on the constant bus
+          tmp2 = vreg(aa);
+          aa = tmp2;
+        } else if (bb.lit() && !inl(bb.v)) {
+          tmp2 = vreg(bb);
+          bb = tmp2;
+        }
+        if (bb.reg())
+          E.valu("v_subb_co_u32_e32 v7, vcc, " + src(aa) + ", " + V(bb.v) + ", vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
+        else
+          E.valu("v_subbrev_co_u32_e32 v7, vcc, " + src(bb) + ", " + V(aa.v) + ", vcc", {kVCC, kVCC + 1},
+                 {kVCC, kVCC + 1});
+        drop(tmp);
+        drop(tmp2);
+      }
+      borrow = -1;
+    }
+    for (auto& d : own) drop(d);
+    if (borrow >= 0) {
+      m.k = 1;
+      m.ones = borrow == 1;
+      return m;
+    }
+    m.k = 2;
+    m.s = E.salloc();
+    E.salu("s_mov_b64 " + SP(m.s) + ", vcc", {m.s, m.s + 1});
+    return m;
+  }
+
+  Mask mnot(const Mask& a) {
+    Mask m;
+    if (a.k == 1) {
+      m.k = 1;
+      m.ones = !a.ones;
+      return m;
+    }
+    m.k = 2;
+    m.s = E.salloc();
+    E.salu("s_not_b64 " + SP(m.s) + ", " + SP(a.s), {m.s, m.s + 1});
+    return m;
+  }
+  // and / or / xor of masks
+  Mask mop(const char* op, const Mask& a, const Mask& b) {
+    Mask m;
+    const std::string o = op;
+    if (a.k == 1 && b.k == 1) {
+      m.k = 1;
+      m.ones = o == "and" ? (a.ones && b.ones) : o == "or" ? (a.ones || b.ones) : (a.ones != b.ones);
+      return m;
+    }
+    if (a.k == 1 || b.k == 1) {
+      const Mask& l = a.k == 1 ? a : b;
+      const Mask& r = a.k == 1 ? b : a;
+      if ((o == "and" && l.ones) || (o == "or" && !l.ones) || (o == "xor" && !l.ones)) {
+        E.sretain(r);
+        return r;
+      }
+      if (o == "and" || o == "or") {
+        m.k = 1;
+        m.ones = o == "or";
+        return m;
+      }
+      return mnot(r);  // xor with all ones
+    }
+    m.k = 2;
+    m.s = E.salloc();
+    E.salu("s_" + o + "_b64 " + SP(m.s) + ", " + SP(a.s) + ", " + SP(b.s), {m.s, m.s + 1});
+    return m;
+  }
+
+  // per-limb select through VCC (= the mask, already moved there): c ? t : f
+  Limb sel(const Limb& t, const Limb& f) {
+    if (t == f) {
+      E.retain(t);
+      return t;
+    }
+    if (t.k == LU || f.k == LU) fail("internal: a limb the demand analysis dropped was read");
+    // VCC is on the constant bus already: a literal operand must come through a VGPR
+    Limb tt = t, ff = f, tmp, tmp2;
+    if (!tt.reg()) {
+      tmp = vreg(tt);
+      tt = tmp;
+    }
+    if (ff.lit() && !inl(ff.v)) {
+      tmp2 = vreg(ff);
+      ff = tmp2;
+    }
+    const Limb d = fresh();
+    E.valu("v_cndmask_b32_e32 " + V(d.v) + ", " + src(ff) + ", " + V(tt.v) + ", vcc", {kVCC, kVCC + 1});
+    drop(tmp);
+    drop(tmp2);
+    return d;
+  }
+  void mask_to_vcc(const Mask& m) {
+    if (m.k == 2) E.salu("s_mov_b64 vcc, " + SP(m.s), {kVCC, kVCC + 1});
+    else E.salu(std::string("s_mov_b64 vcc, ") + (m.ones ? "-1" : "0"), {kVCC, kVCC + 1});
+  }
+
+  // ---------------------------------------------------------------------------------------
+  // the candidate generator (GEN3, include/mythgpu.h; the same function as gen_value in
+  // jit.cpp, engine.hip and oracle/bveval.c)
+  // ---------------------------------------------------------------------------------------
+  // per-lane hash grnd(c, j) into a fresh VGPR
+  Limb grnd(uint32_t c, uint32_t j) {
+    const Limb d = fresh(), t = fresh();
+    E.valu("v_xor_b32_e32 " + V(d.v) + ", " + imm(gsalt(c, j)) + ", v4");
+    E.valu("v_xor_b32_sdwa " + V(d.v) + ", " + V(d.v) + ", " + V(d.v) +
+           " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1");
+    E.valu("v_mul_u32_u24_e32 " + V(d.v) + ", 0x9e3779, " + V(d.v));
+    E.valu("v_lshrrev_b32_e32 " + V(t.v) + ", 15, " + V(d.v));
+    E.valu("v_xad_u32 " + V(d.v) + ", " + V(t.v) + ", " + V(d.v) + ", v5");
+    drop(t);
+    return d;
+  }
+  // the group's choice word of coordinate c -> SGPR s
+  void gwsel(uint32_t c, int s) {
+    E.salu("s_xor_b32 " + S(s) + ", s36, " + hexs(gsalt(c, 0xFFFEu)), {s});
+    E.salu("s_mul_i32 " + S(s) + ", " + S(s) + ", 0x9e3779b1", {s});
+    E.salu("s_add_u32 " + S(s) + ", " + S(s) + ", s37", {s});
+  }
+  // UNIFORM raw limbs masked to `bits`
+  std::vector<Limb> uniform_limbs(uint32_t c, uint32_t Lc, uint32_t bits) {
+    const uint32_t n = std::min(Lc, (bits + 31) / 32);
+    std::vector<Limb> u(n);
+    for (uint32_t j = 0; j < n; j++) {
+      if (j < 2) {
+        u[j] = grnd(c, j);
+      } else {
+        const uint32_t s = (7u * j + 3u) % 31u + 1u;
+        const Limb d = fresh();
+        E.valu("v_alignbit_b32 " + V(d.v) + ", " + V(u[j - 1].v) + ", " + V(u[j - 2].v) + ", " + std::to_string(s));
+        E.valu("v_add_u32_e32 " + V(d.v) + ", " + V(u[j - 2].v) + ", " + V(d.v));
+        u[j] = d;
+      }
+    }
+    std::vector<Limb> r(Lc, Lit(0));
+    for (uint32_t j = 0; j < Lc; j++) {
+      const uint32_t lo = 32 * j;
+      const uint32_t m = lo >= bits ? 0u : (bits - lo >= 32 ? 0xFFFFFFFFu : ((1u << (bits - lo)) - 1u));
+      if (j >= n || m == 0) continue;
+      r[j] = and_lit(u[j], m);
+    }
+    for (auto& x : u) drop(x);
+    return r;
+  }
+  // lo + x for x < (maxadd << sh) + 1: the number of low limbs that can differ (jit.cpp reach_limbs)
+  static uint32_t reach_limbs(const uint32_t* lo, uint32_t Lc, uint64_t maxadd, uint32_t sh) {
+    std::vector<uint32_t> add(Lc + 3, 0u);
+    const uint32_t q = sh / 32, r = sh % 32;
+    const unsigned __int128 x = (unsigned __int128)maxadd << r;
+    for (uint32_t t = 0; t < 3 && q + t < Lc + 3; t++) add[q + t] = (uint32_t)(x >> (32 * t));
+    for (uint32_t j = Lc; j < Lc + 3; j++)
+      if (add[j]) return Lc;
+    uint64_t cy = 0;
+    uint32_t k = 0;
+    for (uint32_t j = 0; j < Lc; j++) {
+      const uint64_t t = (uint64_t)lo[j] + add[j] + cy;
+      if ((uint32_t)t != lo[j]) k = j + 1;
+      cy = t >> 32;
+    }
+    return cy ? Lc : k;
+  }
+  // lo (literal limbs) + off (limbs, low limbs only), chain over the first k limbs
+  std::vector<Limb> add_lit(const uint32_t* lo, uint32_t Lc, const std::vector<Limb>& off, uint32_t k) {
+    std::vector<Limb> a(k), b(k);
+    for (uint32_t j = 0; j < k; j++) {
+      a[j] = Lit(lo[j]);
+      b[j] = j < off.size() ? off[j] : Lit(0);
+    }
+    std::vector<Limb> r = add_chain(a, b, k, false);
+    r.resize(Lc);
+    for (uint32_t j = k; j < Lc; j++) r[j] = Lit(lo[j]);
+    return r;
+  }
+  // high 32 bits of x * c (c a literal)
+  Limb mulhi_lit(const Limb& x, uint32_t c) {
+    if (x.lit()) return Lit((uint32_t)(((uint64_t)x.v * c) >> 32));
+    const Limb d = fresh();
+    if (inl(c)) {
+      E.valu("v_mul_hi_u32 " + V(d.v) + ", " + V(x.v) + ", " + imm(c));
+    } else {
+      E.salu("s_mov_b32 s41, " + hexs(c), {41});
+      E.valu("v_mul_hi_u32 " + V(d.v) + ", " + V(x.v) + ", s41", {41});
+    }
+    return d;
+  }
+
+  // dictionary entry `idx` (VGPR) of the n-entry table at G[off] (width w)
+  std::vector<Limb> dict(uint32_t off, uint32_t n, uint32_t w, const Limb& idx) {
+    const uint32_t Lc = Lw(w);
+    std::vector<Limb> r(Lc, Lit(0));
+    if (w <= 32 && n && (uint64_t)n * w <= 32) {  // packed in one literal: one bit-field extract
+      uint32_t pack = 0;
+      const uint32_t m = w == 32 ? 0xFFFFFFFFu : ((1u << w) - 1u);
+      for (uint32_t e2 = 0; e2 < n; e2++) pack |= (G[off + e2] & m) << (e2 * w);
+      const Limb sh = fresh(), d = fresh();
+      E.valu("v_mul_u32_u24_e32 " + V(sh.v) + ", " + imm(w) + ", " + V(idx.v));
+      E.salu("s_mov_b32 s41, " + hexs(pack), {41});
+      E.valu("v_bfe_u32 " + V(d.v) + ", s41, " + V(sh.v) + ", " + std::to_string(w), {41});
+      drop(sh);
+      r[0] = d;
+      return r;
+    }
+    if (n <= 4) {  // selects over the entries' literals
+      std::vector<Mask> ms;
+      for (uint32_t e2 = 0; e2 + 1 < n; e2++) {
+        Mask m;
+        m.k = 2;
+        m.s = E.salloc();
+        E.valu("v_cmp_ne_u32_e64 " + SP(m.s) + ", " + std::to_string(e2) + ", " + V(idx.v), {}, {m.s, m.s + 1});
+        ms.push_back(m);
+      }
+      for (uint32_t j = 0; j < Lc; j++) {
+        bool same = true;
+        for (uint32_t e2 = 1; e2 < n && same; e2++) same = G[off + e2 * Lc + j] == G[off + j];
+        if (same) {
+          r[j] = Lit(G[off + j]);
+          continue;
+        }
+        Limb cur = vreg(Lit(G[off + (n - 1) * Lc + j]));
+        for (int32_t e2 = (int32_t)n - 2; e2 >= 0; e2--) {
+          const uint32_t lv = G[off + e2 * Lc + j];
+          // lanes whose index is not e2 keep cur (src1), the others take the literal (src0)
+          const Limb lvr = inl(lv) ? Lit(lv) : vreg(Lit(lv));  // VCC already uses the constant bus
+          const Limb d = fresh();
+          E.valu("v_cndmask_b32_e64 " + V(d.v) + ", " + src(lvr) + ", " + V(cur.v) + ", " + SP(ms[e2].s),
+                 {ms[e2].s, ms[e2].s + 1});
+          drop(lvr);
+          drop(cur);
+          cur = d;
+        }
+        r[j] = cur;
+      }
+      for (auto& m : ms) E.srelease(m);
+      return r;
+    }
+    // gathers from the generator constants (s[4:5]): byte offset (off + idx * Lc + j) * 4
+    const Limb vo = fresh();
+    E.valu("v_mul_u32_u24_e32 " + V(vo.v) + ", " + imm(4 * Lc) + ", " + V(idx.v));
+    bool any = false;
+    for (uint32_t j = 0; j < Lc; j++) {
+      bool same = true;
+      for (uint32_t e2 = 1; e2 < n && same; e2++) same = G[off + e2 * Lc + j] == G[off + j];
+      if (same) {
+        r[j] = Lit(G[off + j]);
+        continue;
+      }
+      const uint32_t byte = (off + j) * 4;
+      const Limb d = fresh();
+      if (byte < 4096) {
+        E.mem("global_load_dword " + V(d.v) + ", " + V(vo.v) + ", s[4:5] offset:" + std::to_string(byte));
+      } else {
+        const Limb t = fresh();
+        E.valu("v_add_u32_e32 " + V(t.v) + ", " + hexs(byte) + ", " + V(vo.v));
+        E.mem("global_load_dword " + V(d.v) + ", " + V(t.v) + ", s[4:5]");
+        drop(t);
+      }
+      r[j] = d;
+      any = true;
+    }
+    if (any) E.ctl("s_waitcnt vmcnt(0)");
+    drop(vo);
+    return r;
+  }
+
+  // e = ((h >> 16) * n) >> 16
+  Limb dict_index(const Limb& h, uint32_t n) {
+    const Limb e2 = fresh();
+    E.valu("v_lshrrev_b32_e32 " + V(e2.v) + ", 16, " + V(h.v));
+    E.valu("v_mul_u32_u24_e32 " + V(e2.v) + ", " + imm(n) + ", " + V(e2.v));
+    E.valu("v_lshrrev_b32_e32 " + V(e2.v) + ", 16, " + V(e2.v));
+    return e2;
+  }
+
+  // write limbs r into the preassigned registers out (MIXED branches), releasing r
+  void put(const std::vector<Limb>& out, std::vector<Limb>& r) {
+    for (size_t j = 0; j < out.size(); j++) {
+      const Limb x = j < r.size() ? r[j] : Lit(0);
+      if (!(x == out[j])) E.valu("v_mov_b32_e32 " + V(out[j].v) + ", " + src(x));
+      if (j < r.size()) drop(r[j]);
+    }
+    r.clear();
+  }
+
+  // +/-(1 + (h & 1)) on the registers out, when (ws & 0xFFFF) < pdelta (scalar branch)
+  void delta(const std::vector<Limb>& out, uint32_t c, uint32_t pdelta, int ws, const Limb* hknown) {
+    const std::string skip = E.newlab();
+    E.salu("s_and_b32 s40, " + S(ws) + ", 0xffff", {40});
+    E.salu("s_cmp_lt_u32 s40, " + imm(pdelta));
+    E.ctl("s_cbranch_scc0 " + skip);
+    Limb h = hknown ? *hknown : grnd(c, 0xFFFFu);
+    if (hknown) E.retain(h);
+    // mag = 1 + (h & 1); the sign sb = (h >> 1) & 1 as a mask; a0 = sb ? -mag : mag
+    const Limb mag = fresh(), neg = fresh();
+    Mask sb;
+    sb.k = 2;
+    sb.s = E.salloc();
+    E.valu("v_and_b32_e32 " + V(mag.v) + ", 1, " + V(h.v));
+    E.valu("v_add_u32_e32 " + V(mag.v) + ", 1, " + V(mag.v));
+    E.valu("v_bfe_u32 " + V(neg.v) + ", " + V(h.v) + ", 1, 1");
+    E.valu("v_cmp_ne_u32_e64 " + SP(sb.s) + ", 0, " + V(neg.v), {}, {sb.s, sb.s + 1});
+    E.valu("v_sub_u32_e32 " + V(neg.v) + ", 0, " + V(mag.v));
+    E.valu("v_cndmask_b32_e64 " + V(mag.v) + ", " + V(mag.v) + ", " + V(neg.v) + ", " + SP(sb.s), {sb.s, sb.s + 1});
+    drop(neg);
+    const uint32_t Lc = (uint32_t)out.size();
+    E.valu("v_add_co_u32_e32 " + V(out[0].v) + ", vcc, " + V(mag.v) + ", " + V(out[0].v), {}, {kVCC, kVCC + 1});
+    drop(mag);
+    if (Lc > 1) {
+      // the high limbs change only in lanes whose low-limb carry differs from the step's sign
+      const std::string done = E.newlab();
+      E.salu("s_xor_b64 s[40:41], vcc, " + SP(sb.s), {40, 41});
+      E.ctl("s_cbranch_scc0 " + done);
+      const Limb ah = fresh();
+      E.valu("v_cndmask_b32_e64 " + V(ah.v) + ", 0, -1, " + SP(sb.s), {sb.s, sb.s + 1});
+      for (uint32_t j = 1; j < Lc; j++)
+        E.valu("v_addc_co_u32_e32 " + V(out[j].v) + ", vcc, " + V(ah.v) + ", " + V(out[j].v) + ", vcc", {kVCC, kVCC + 1},
+               {kVCC, kVCC + 1});
+      drop(ah);
+      E.label(done);
+    }
+    E.srelease(sb);
+    drop(h);
+    E.label(skip);
+  }
+
+  // mask to the width and the clamp record (MIXED: per branch, in place on out)
+  void finish(const std::vector<Limb>& out, uint32_t width, uint32_t clamp) {
+    const uint32_t Lc = (uint32_t)out.size();
+    if (width & 31) E.valu("v_and_b32_e32 " + V(out[Lc - 1].v) + ", " + imm(topmask(width)) + ", " + V(out[Lc - 1].v));
+    if (!clamp) return;
+    const uint32_t r = clamp - 1;
+    const uint32_t span = G[r + Lc];
+    const uint32_t k = reach_limbs(&G[r], Lc, span ? span - 1u : 0xFFFFFFFFull, 0);
+    // in range: v - lo has no borrow, high limbs zero and low limb < span (span 0: 2^32)
+    std::vector<Limb> v(out.begin(), out.end()), lo(Lc);
+    for (uint32_t j = 0; j < Lc; j++) lo[j] = Lit(G[r + j]);
+    // difference limbs (owned) and the borrow
+    std::vector<Limb> dif = add_chain(v, lo, Lc, true);
+    Mask bad;
+    bad.k = 2;
+    bad.s = E.salloc();
+    E.salu("s_mov_b64 " + SP(bad.s) + ", vcc", {bad.s, bad.s + 1});  // borrow: v < lo
+    std::vector<std::pair<Limb, Limb>> hz;
+    for (uint32_t j = 1; j < Lc; j++) hz.push_back({dif[j], Lit(0)});
+    if (!hz.empty()) {
+      const Mask z = eq_mask(hz);  // high limbs of the difference zero
+      const Mask nz = mnot(z);
+      const Mask b2 = mop("or", bad, nz);
+      E.srelease(z);
+      E.srelease(nz);
+      E.srelease(bad);
+      bad = b2;
+    }
+    if (span) {
+      Mask ge;
+      ge.k = 2;
+      ge.s = E.salloc();
+      const Limb d0 = vreg(dif[0]);
+      E.salu("s_mov_b32 s41, " + hexs(span), {41});
+      E.valu("v_cmp_le_u32_e64 " + SP(ge.s) + ", s41, " + V(d0.v), {41}, {ge.s, ge.s + 1});
+      drop(d0);
+      const Mask b2 = mop("or", bad, ge);
+      E.srelease(ge);
+      E.srelease(bad);
+      bad = b2;
+    }
+    for (auto& d : dif) drop(d);
+    // clamped value lo + (span ? mulhi(v0, span) : v0)
+    std::vector<Limb> offv(1);
+    offv[0] = span ? mulhi_lit(out[0], span) : out[0];
+    if (!span) E.retain(out[0]);
+    std::vector<Limb> cl = add_lit(&G[r], Lc, offv, k);
+    drop(offv[0]);
+    mask_to_vcc(bad);
+    for (uint32_t j = 0; j < Lc; j++) {
+      // out = bad ? clamped : out
+      Limb t = cl[j], tmp;
+      if (!t.reg()) {
+        tmp = vreg(t);
+        t = tmp;
+      }
+      E.valu("v_cndmask_b32_e32 " + V(out[j].v) + ", " + V(out[j].v) + ", " + V(t.v) + ", vcc", {kVCC, kVCC + 1});
+      drop(tmp);
+      drop(cl[j]);
+    }
+    E.srelease(bad);
+  }
+
+  // fixed-bit record: v = (v & ~mask) | value
+  void fixbits(std::vector<Limb>& r, uint32_t fix, bool in_place) {
+    const uint32_t f = fix - 1, Lc = (uint32_t)r.size();
+    for (uint32_t j = 0; j < Lc; j++) {
+      const uint32_t m = G[f + j], v = G[f + Lc + j];
+      if (!m) continue;
+      if (in_place) {
+        if (m == 0xFFFFFFFFu) {
+          E.valu("v_mov_b32_e32 " + V(r[j].v) + ", " + imm(v));
+          continue;
+        }
+        E.valu("v_and_b32_e32 " + V(r[j].v) + ", " + imm(~m) + ", " + V(r[j].v));
+        if (v) E.valu("v_or_b32_e32 " + V(r[j].v) + ", " + imm(v) + ", " + V(r[j].v));
+        continue;
+      }
+      if (m == 0xFFFFFFFFu || r[j].lit()) {
+        const uint32_t x = r[j].lit() ? ((r[j].v & ~m) | v) : v;
+        drop(r[j]);
+        r[j] = Lit(x);
+        continue;
+      }
+      const Limb a = and_lit(r[j], ~m);
+      drop(r[j]);
+      r[j] = a;
+      if (v) {
+        const Limb d = fresh();
+        E.valu("v_or_b32_e32 " + V(d.v) + ", " + imm(v) + ", " + V(a.v));
+        drop(a);
+        r[j] = d;
+      }
+    }
+  }
+
+  // coordinate c's value (owned limbs)
+  std::vector<Limb> gen_value(uint32_t c) {
+    const GenSpec sp = specs.at(c);
+    const uint32_t fix = sp.kind >> 8, kind = sp.kind & 0xFFu;
+    const uint32_t width = P.coord_width.at(c), Lc = Lw(width);
+    std::vector<Limb> r;
+    switch (kind) {
+      case MG_GEN_MIXED: {
+        std::vector<Limb> out(Lc);
+        for (auto& x : out) x = fresh();
+        const uint32_t pc = sp.p[3] != MG_NONE ? (sp.p[2] & 0xFFFFu) : 0u;
+        const uint32_t pd = sp.p[1] ? (sp.p[2] >> 16) : 0u;
+        const uint32_t ps = sp.p[4] & 0xFFFFu;
+        const uint32_t small_bits = std::min(width, sp.p[4] >> 16);
+        const bool narrow = width <= MG_GEN_NARROW_BITS;
+        const int ws = E.salloc();  // the choice word (one SGPR of a pair)
+        gwsel(c, ws);
+        const std::string end = E.newlab();
+        auto uni = [&](uint32_t bitsn) {
+          std::vector<Limb> u;
+          if (narrow) {
+            const Limb h = grnd(c, 0xFFFFu);
+            u.assign(Lc, Lit(0));
+            const uint32_t m = bitsn >= 32 ? 0xFFFFFFFFu : ((1u << bitsn) - 1u);
+            u[0] = and_lit(h, m & 0xFFFFu);
+            drop(h);
+          } else {
+            u = uniform_limbs(c, Lc, bitsn);
+          }
+          put(out, u);
+        };
+        std::string next;
+        bool any = false;
+        auto branch = [&](uint32_t T) {  // take this alternative when ws < T << 16
+          if (any) {
+            E.ctl("s_branch " + end);
+            E.label(next);
+          }
+          any = true;
+          next = E.newlab();
+          if (T < 65536u) {
+            E.salu("s_cmp_lt_u32 " + S(ws) + ", " + hexs(T << 16));
+            E.ctl("s_cbranch_scc0 " + next);
+          }
+        };
+        if (pc) {
+          branch(pc);
+          std::vector<Limb> s;
+          auto it = cval.find(sp.p[3]);
+          if (it != cval.end()) {
+            s = val[it->second].l;
+            for (auto& x : s) E.retain(x);
+          } else {
+            s = gen_value(sp.p[3]);
+          }
+          put(out, s);
+          if (sp.p[5]) delta(out, c, sp.p[5], ws, nullptr);
+          finish(out, width, sp.p[6]);
+        }
+        if (pd) {
+          branch(pc + pd);
+          const Limb h = grnd(c, 0xFFFFu);
+          const Limb ix = dict_index(h, sp.p[1]);
+          std::vector<Limb> dv = dict(sp.p[0], sp.p[1], width, ix);
+          drop(ix);
+          put(out, dv);
+          if (sp.p[5]) delta(out, c, sp.p[5], ws, &h);
+          drop(h);
+          finish(out, width, sp.p[6]);
+        }
+        if (ps) {
+          branch(pc + pd + ps);
+          uni(small_bits);
+          finish(out, width, sp.p[6]);
+        }
+        if (any) {
+          E.ctl("s_branch " + end);
+          E.label(next);
+        }
+        uni(width);
+        finish(out, width, sp.p[6]);
+        E.label(end);
+        Mask wsm;
+        wsm.k = 2;
+        wsm.s = ws;
+        E.srelease(wsm);
+        if (width & 31) E.valu("v_and_b32_e32 " + V(out[Lc - 1].v) + ", " + imm(topmask(width)) + ", " + V(out[Lc - 1].v));
+        if (fix) fixbits(out, fix, true);
+        return out;
+      }
+      case MG_GEN_DICT: {
+        const Limb h = grnd(c, 0xFFFFu);
+        const Limb ix = dict_index(h, sp.p[1]);
+        drop(h);
+        r = dict(sp.p[0], sp.p[1], width, ix);
+        drop(ix);
+        break;
+      }
+      case MG_GEN_RANGE: {
+        const Limb rr = grnd(c, 0);
+        std::vector<Limb> off(1);
+        if (sp.p[1]) {
+          off[0] = mulhi_lit(rr, sp.p[1]);
+          drop(rr);
+        } else {
+          off[0] = rr;
+        }
+        const uint32_t k = reach_limbs(&G[sp.p[0]], Lc, sp.p[1] ? sp.p[1] - 1u : 0xFFFFFFFFull, 0);
+        r = add_lit(&G[sp.p[0]], Lc, off, k);
+        drop(off[0]);
+        break;
+      }
+      case MG_GEN_ALIGNED: {
+        const Limb rr = grnd(c, 0);
+        Limb m;
+        if (sp.p[2]) {
+          m = mulhi_lit(rr, sp.p[2]);
+          drop(rr);
+        } else {
+          m = rr;
+        }
+        const int32_t sh = (int32_t)sp.p[1];
+        const uint32_t k = reach_limbs(&G[sp.p[0]], Lc, sp.p[2] ? sp.p[2] - 1u : 0xFFFFFFFFull, (uint32_t)sh);
+        std::vector<Limb> mw(Lc, Lit(0));
+        for (uint32_t j = 0; j < Lc; j++) {
+          const int32_t bit0 = (int32_t)(j * 32) - sh;
+          if (bit0 <= -32 || bit0 >= 32) continue;
+          const Limb d = fresh();
+          if (bit0 < 0) E.valu("v_lshlrev_b32_e32 " + V(d.v) + ", " + std::to_string(-bit0) + ", " + V(m.v));
+          else if (bit0 > 0) E.valu("v_lshrrev_b32_e32 " + V(d.v) + ", " + std::to_string(bit0) + ", " + V(m.v));
+          else E.valu("v_mov_b32_e32 " + V(d.v) + ", " + V(m.v));
+          mw[j] = d;
+        }
+        drop(m);
+        r = add_lit(&G[sp.p[0]], Lc, mw, k);
+        for (auto& x : mw) drop(x);
+        break;
+      }
+      case MG_GEN_FIXED:
+        r.resize(Lc);
+        for (uint32_t j = 0; j < Lc; j++) r[j] = Lit(G[sp.p[0] + j]);
+        break;
+      default:  // UNIFORM / LAZY
+        r = uniform_limbs(c, Lc, 32 * Lc);
+        break;
+    }
+    if (width & 31) mask_top(r, width);
+    if (fix) fixbits(r, fix, false);
+    return r;
+  }
+
+  // ---------------------------------------------------------------------------------------
+  // the program
+  // ---------------------------------------------------------------------------------------
+  void set(uint32_t d, std::vector<Limb> l) {
+    Val& x = val[d];
+    // limbs nobody reads are dropped (never computed where possible)
+    for (size_t j = 0; j < l.size(); j++)
+      if (!(need[d] >> j & 1) && l[j].k != LU) {
+        drop(l[j]);
+        l[j] = Limb{};
+      }
+    x.l = std::move(l);
+    x.w = P.vwidth[d];
+    x.def = true;
+  }
+  void set_mask(uint32_t d, const Mask& m) {
+    Val& x = val[d];
+    x.m = m;
+    x.w = 1;
+    x.def = true;
+  }
+  void kill(uint32_t id) {
+    Val& x = val[id];
+    for (auto& l : x.l) drop(l);
+    x.l.clear();
+    E.srelease(x.m);
+    x.m = Mask{};
+  }
+  std::vector<Limb> limbs(uint32_t id, uint32_t n) {
+    std::vector<Limb> r(n);
+    for (uint32_t j = 0; j < n; j++) r[j] = limb(id, j);
+    return r;
+  }
+  uint32_t demanded(uint32_t d) const { return need[d] ? 64 - (uint32_t)__builtin_clzll(need[d]) : 0; }
+
+  void emit(const Instr& in, size_t k, const std::string& next) {
+    const uint32_t d = in.dst, W = in.wd, Ld = Lw(W);
+    switch (in.op) {
+      case K_CONST: {
+        std::vector<Limb> r(Ld);
+        for (uint32_t j = 0; j < Ld; j++) r[j] = Lit(P.consts[in.p0 + j]);
+        if (W == 1) {
+          Mask m;
+          m.k = 1;
+          m.ones = P.consts[in.p0] & 1u;
+          val[d].m = m;
+        }
+        set(d, r);
+        break;
+      }
+      case K_COORD: {
+        std::vector<Limb> r = gen_value(in.p0);
+        set(d, r);
+        cval[in.p0] = d;
+        break;
+      }
+      case K_ADD: case K_SUB: case K_NEG: {
+        const uint32_t n = std::min(Ld, demanded(d));
+        std::vector<Limb> x = in.op == K_NEG ? std::vector<Limb>(n, Lit(0)) : limbs(in.a, n);
+        std::vector<Limb> y = in.op == K_NEG ? limbs(in.a, n) : limbs(in.b, n);
+        std::vector<Limb> r = add_chain(x, y, n, in.op != K_ADD);
+        r.resize(Ld);
+        if (n == Ld) mask_top(r, W);
+        set(d, r);
+        break;
+      }
+      case K_MUL: {
+        const uint32_t n = std::min(Ld, demanded(d));
+        std::vector<Limb> a = limbs(in.a, n), b = limbs(in.b, n), acc(n, Lit(0));  // acc owns
+        for (uint32_t i = 0; i < n; i++) {
+          if (a[i].lit() && a[i].v == 0) continue;
+          std::vector<Limb> lo(n, Lit(0)), hi(n, Lit(0));
+          bool anyv = false;
+          for (uint32_t j = 0; i + j < n; j++) {
+            const Limb x = a[i], y = b[j];
+            if (y.lit() && y.v == 0) continue;
+            if (x.lit() && y.lit()) {
+              const uint64_t p = (uint64_t)x.v * y.v;
+              lo[i + j] = Lit((uint32_t)p);
+              if (i + j + 1 < n) hi[i + j + 1] = Lit((uint32_t)(p >> 32));
+              continue;
+            }
+            anyv = true;
+            // VOP3: literal operands through s41 (one SGPR per instruction)
+            const Limb vx = x.reg() ? x : y, ly = x.reg() ? y : x;
+            std::string so;
+            std::initializer_list<int> rd = {};
+            if (ly.lit() && !inl(ly.v)) {
+              E.salu("s_mov_b32 s41, " + hexs(ly.v), {41});
+              so = "s41";
+              rd = {41};
+            } else {
+              so = src(ly);
+            }
+            const Limb dl = fresh();
+            E.valu("v_mul_lo_u32 " + V(dl.v) + ", " + V(vx.v) + ", " + so, rd);
+            lo[i + j] = dl;
+            if (i + j + 1 < n) {
+              const Limb dh = fresh();
+              E.valu("v_mul_hi_u32 " + V(dh.v) + ", " + V(vx.v) + ", " + so, rd);
+              hi[i + j + 1] = dh;
+            }
+          }
+          (void)anyv;
+          std::vector<Limb> s1 = add_chain(acc, lo, n, false);
+          for (auto& t : acc) drop(t);
+          for (auto& t : lo) drop(t);
+          std::vector<Limb> s2 = add_chain(s1, hi, n, false);
+          for (auto& t : s1) drop(t);
+          for (auto& t : hi) drop(t);
+          acc = s2;
+        }
+        acc.resize(Ld);
+        if (n == Ld) mask_top(acc, W);
+        set(d, acc);
+        break;
+      }
+      case K_AND: case K_OR: case K_XOR: {
+        if (W == 1) {
+          const char* op = in.op == K_AND ? "and" : in.op == K_OR ? "or" : "xor";
+          set_mask(d, mop(op, mask_of(in.a), mask_of(in.b)));
+          break;
+        }
+        std::vector<Limb> r(Ld);
+        for (uint32_t j = 0; j < Ld; j++) {
+          if (!(need[d] >> j & 1)) continue;
+          const Limb a = limb(in.a, j), b = limb(in.b, j);
+          if (a.lit() && b.lit()) {
+            r[j] = Lit(in.op == K_AND ? (a.v & b.v) : in.op == K_OR ? (a.v | b.v) : (a.v ^ b.v));
+            continue;
+          }
+          const Limb l = a.lit() ? a : b, v = a.lit() ? b : a;
+          if (l.lit()) {
+            if ((in.op == K_AND && l.v == 0xFFFFFFFFu) || (in.op != K_AND && l.v == 0)) {
+              E.retain(v);
+              r[j] = v;
+              continue;
+            }
+            if (in.op == K_AND && l.v == 0) { r[j] = Lit(0); continue; }
+            if (in.op == K_OR && l.v == 0xFFFFFFFFu) { r[j] = Lit(0xFFFFFFFFu); continue; }
+          }
+          if (in.op != K_XOR && a == b) {
+            E.retain(a);
+            r[j] = a;
+            continue;
+          }
+          const char* op = in.op == K_AND ? "v_and_b32_e32 " : in.op == K_OR ? "v_or_b32_e32 " : "v_xor_b32_e32 ";
+          const Limb dd = fresh();
+          E.valu(op + V(dd.v) + ", " + src(l.lit() ? l : a) + ", " + V(l.lit() ? v.v : b.v));
+          r[j] = dd;
+        }
+        set(d, r);
+        break;
+      }
+      case K_NOT: {
+        if (W == 1) {
+          set_mask(d, mnot(mask_of(in.a)));
+          break;
+        }
+        std::vector<Limb> r(Ld);
+        for (uint32_t j = 0; j < Ld; j++) {
+          if (!(need[d] >> j & 1)) continue;
+          const Limb a = limb(in.a, j);
+          if (a.lit()) {
+            r[j] = Lit(~a.v);
+            continue;
+          }
+          const Limb dd = fresh();
+          E.valu("v_not_b32_e32 " + V(dd.v) + ", " + V(a.v));
+          r[j] = dd;
+        }
+        mask_top(r, W);
+        set(d, r);
+        break;
+      }
+      case K_COPY: {
+        if (W == 1 && val[in.a].m.k) {
+          E.sretain(val[in.a].m);
+          val[d].m = val[in.a].m;
+        }
+        std::vector<Limb> r = val[in.a].l;
+        for (auto& x : r) E.retain(x);
+        set(d, r);
+        break;
+      }
+      case K_ITE: {
+        const Mask c = mask_of(in.a);
+        if (W == 1) {
+          if (c.k == 1) {
+            const Mask x = mask_of(c.ones ? in.b : in.c);
+            E.sretain(x);
+            set_mask(d, x);
+            break;
+          }
+          const Mask t = mop("and", c, mask_of(in.b));
+          const Mask nc = mnot(c);
+          const Mask f = mop("and", nc, mask_of(in.c));
+          set_mask(d, mop("or", t, f));
+          E.srelease(t);
+          E.srelease(nc);
+          E.srelease(f);
+          break;
+        }
+        std::vector<Limb> r(Ld);
+        if (c.k == 1) {
+          for (uint32_t j = 0; j < Ld; j++) {
+            if (!(need[d] >> j & 1)) continue;
+            r[j] = limb(c.ones ? in.b : in.c, j);
+            E.retain(r[j]);
+          }
+          set(d, r);
+          break;
+        }
+        mask_to_vcc(c);
+        for (uint32_t j = 0; j < Ld; j++) {
+          if (!(need[d] >> j & 1)) continue;
+          r[j] = sel(limb(in.b, j), limb(in.c, j));
+        }
+        set(d, r);
+        break;
+      }
+      case K_EQ: {
+        const uint32_t La = Lw(in.p1);
+        if (in.p1 == 1) {
+          set_mask(d, mnot_xor(mask_of(in.a), mask_of(in.b)));
+          break;
+        }
+        std::vector<std::pair<Limb, Limb>> prs;
+        for (uint32_t j = 0; j < La; j++) prs.push_back({limb(in.a, j), limb(in.b, j)});
+        set_mask(d, eq_mask(prs));
+        break;
+      }
+      case K_ULT: case K_ULE: case K_SLT: case K_SLE: {
+        const uint32_t La = Lw(in.p1);
+        const bool sgn = in.op == K_SLT || in.op == K_SLE;
+        if (in.p1 == 1) {
+          // Bool compares: a < b unsigned = ~a & b ; signed: a (= -1) < b (= 0) = a & ~b
+          const Mask a = mask_of(in.a), b = mask_of(in.b);
+          Mask lt = sgn ? mop_andn(a, b) : mop_andn(b, a);
+          if (in.op == K_ULE || in.op == K_SLE) {
+            const Mask gt = sgn ? mop_andn(b, a) : mop_andn(a, b);
+            const Mask le = mnot(gt);
+            E.srelease(gt);
+            E.srelease(lt);
+            lt = le;
+          }
+          set_mask(d, lt);
+          break;
+        }
+        if (in.op == K_ULT || in.op == K_SLT) {
+          set_mask(d, lt_mask(limbs(in.a, La), limbs(in.b, La), in.p1, sgn));
+        } else {
+          const Mask gt = lt_mask(limbs(in.b, La), limbs(in.a, La), in.p1, sgn);
+          set_mask(d, mnot(gt));
+          E.srelease(gt);
+        }
+        break;
+      }
+      case K_CONCAT: {
+        const uint32_t wb = in.p1, wa = W - wb;
+        const std::vector<Limb> a = limbs(in.a, Lw(wa)), b = limbs(in.b, Lw(wb));
+        std::vector<Limb> r(Ld);
+        for (uint32_t j = 0; j < Ld; j++) {
+          if (!(need[d] >> j & 1)) continue;
+          const uint32_t p = 32 * j, e2 = std::min(W, p + 32);
+          if (e2 <= wb) {
+            r[j] = bits(b, wb, p, e2 - p);
+          } else if (p >= wb) {
+            r[j] = bits(a, wa, p - wb, e2 - p);
+          } else {
+            const uint32_t nb = wb - p;
+            const Limb lo = bits(b, wb, p, nb), hi = bits(a, wa, 0, e2 - wb);
+            r[j] = shl_or(hi, nb, lo);
+            drop(lo);
+            drop(hi);
+          }
+        }
+        set(d, r);
+        break;
+      }
+      case K_EXTRACT: {
+        const uint32_t wa = in.p1;
+        const std::vector<Limb> a = limbs(in.a, Lw(wa));
+        std::vector<Limb> r(Ld);
+        for (uint32_t j = 0; j < Ld; j++) {
+          if (!(need[d] >> j & 1)) continue;
+          r[j] = bits(a, wa, in.p0 + 32 * j, std::min(32u, W - 32 * j));
+        }
+        if (W == 1) {
+          set(d, r);
+          break;
+        }
+        set(d, r);
+        break;
+      }
+      case K_ZEXT: {
+        const uint32_t La = Lw(in.p1);
+        std::vector<Limb> r(Ld, Lit(0));
+        for (uint32_t j = 0; j < La && j < Ld; j++) {
+          if (!(need[d] >> j & 1)) continue;
+          r[j] = limb(in.a, j);
+          E.retain(r[j]);
+        }
+        set(d, r);
+        break;
+      }
+      case K_SEXT: {
+        const uint32_t wa = in.p1, La = Lw(wa);
+        std::vector<Limb> r(Ld);
+        for (uint32_t j = 0; j + 1 < La; j++) {
+          if (!(need[d] >> j & 1)) continue;
+          r[j] = limb(in.a, j);
+          E.retain(r[j]);
+        }
+        const Limb t = limb(in.a, La - 1);
+        Limb top, f;
+        if (t.lit()) {
+          const uint32_t s = (wa - 1) & 31;
+          const int32_t x = (int32_t)(t.v << (31 - s)) >> (31 - s);
+          top = Lit((uint32_t)x);
+          f = Lit(x < 0 ? 0xFFFFFFFFu : 0u);
+        } else {
+          if (wa & 31) {
+            top = fresh();
+            E.valu("v_bfe_i32 " + V(top.v) + ", " + V(t.v) + ", 0, " + std::to_string(wa & 31));
+          } else {
+            top = t;
+            E.retain(top);
+          }
+          f = fresh();
+          E.valu("v_ashrrev_i32_e32 " + V(f.v) + ", 31, " + V(top.v));
+        }
+        r[La - 1] = top;
+        for (uint32_t j = La; j < Ld; j++) {
+          r[j] = f;
+          E.retain(f);
+        }
+        drop(f);
+        mask_top(r, W);
+        set(d, r);
+        break;
+      }
+      case K_LOOKUP: {
+        const uint32_t Lk = Lw(in.b), n = in.c;
+        std::vector<Limb> cur(Ld);
+        for (uint32_t j = 0; j < Ld; j++) {
+          if (!(need[d] >> j & 1)) continue;
+          cur[j] = limb(in.p0, j);
+          E.retain(cur[j]);
+        }
+        for (int32_t p = (int32_t)n - 1; p >= 0; p--) {
+          const uint32_t kv = P.vaux[in.p1 + 2 * p], vv = P.vaux[in.p1 + 2 * p + 1];
+          std::vector<std::pair<Limb, Limb>> prs;
+          for (uint32_t j = 0; j < Lk; j++) prs.push_back({limb(in.a, j), limb(kv, j)});
+          const Mask h = eq_mask(prs);
+          if (h.k == 1) {
+            if (h.ones) {
+              for (uint32_t j = 0; j < Ld; j++) {
+                if (!(need[d] >> j & 1)) continue;
+                drop(cur[j]);
+                cur[j] = limb(vv, j);
+                E.retain(cur[j]);
+              }
+            }
+            continue;
+          }
+          mask_to_vcc(h);
+          for (uint32_t j = 0; j < Ld; j++) {
+            if (!(need[d] >> j & 1)) continue;
+            const Limb s = sel(limb(vv, j), cur[j]);
+            drop(cur[j]);
+            cur[j] = s;
+          }
+          E.srelease(h);
+        }
+        set(d, cur);
+        break;
+      }
+      case K_ASSERT: {
+        const Mask m = mask_of(in.a);
+        if (m.k == 1) {
+          if (!m.ones) E.salu("s_mov_b64 s[38:39], 0", {38, 39});
+        } else {
+          E.salu("s_and_b64 s[38:39], s[38:39], " + SP(m.s), {38, 39});
+        }
+        if (!gen_kernel) {
+          // early exit: s[42:43] is ~0 when the launch does not stop early, so the OR is zero only
+          // when every lane failed and the wave may leave
+          E.salu("s_or_b64 s[40:41], s[38:39], s[42:43]", {40, 41});
+          E.ctl("s_cbranch_scc0 " + next);
+        }
+        break;
+      }
+      case K_WATCH:
+        break;
+      default:
+        fail("op " + std::to_string(in.op) + " outside the assembly tier");
+    }
+    (void)k;
+  }
+  Mask mnot_xor(const Mask& a, const Mask& b) {
+    const Mask x = mop("xor", a, b);
+    const Mask r = mnot(x);
+    E.srelease(x);
+    return r;
+  }
+  // a & ~b
+  Mask mop_andn(const Mask& a, const Mask& b) {
+    const Mask nb = mnot(b);
+    const Mask r = mop("and", a, nb);
+    E.srelease(nb);
+    return r;
+  }
+
+  void body(const std::string& next) {
+    for (size_t k = 0; k < P.vcode.size(); k++) {
+      const Instr& in = P.vcode[k];
+      emit(in, k, next);
+      // values whose last reader is this instruction, and results nobody reads
+      auto done = [&](uint32_t id) {
+        if (id != MG_NONE && id < last.size() && last[id] <= (int32_t)k && val[id].def) {
+          kill(id);
+          val[id].def = false;
+        }
+      };
+      if (in.dst != MG_NONE && in.dst < last.size() && last[in.dst] < 0) done(in.dst);
+      switch (in.op) {
+        case K_CONST: case K_WATCH: break;
+        case K_COORD:
+          if (copysrc[k] != MG_NONE) done(copysrc[k]);
+          break;
+        case K_LOOKUP:
+          done(in.a);
+          done(in.p0);
+          for (uint32_t q = 0; q < 2 * in.c; q++) done(P.vaux[in.p1 + q]);
+          break;
+        default:
+          done(in.a);
+          if (in.b != MG_NONE) done(in.b);
+          if (in.op == K_ITE) done(in.c);
+          break;
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------------------------------
+  // the kernel around the body
+  // ---------------------------------------------------------------------------------------
+  // 64-bit fmix64 of s[x:x+1] in place (SALU; s40/s41 scratch)
+  void sfmix(int x) {
+    auto xs = [&]() {
+      E.salu("s_lshr_b32 s40, " + S(x + 1) + ", 1", {40});
+      E.salu("s_xor_b32 " + S(x) + ", " + S(x) + ", s40", {x});
+    };
+    auto mul = [&](uint32_t clo, uint32_t chi) {
+      E.salu("s_mul_hi_u32 s40, " + S(x) + ", " + hexs(clo), {40});
+      E.salu("s_mul_i32 s41, " + S(x) + ", " + hexs(chi), {41});
+      E.salu("s_add_u32 s40, s40, s41", {40});
+      E.salu("s_mul_i32 s41, " + S(x + 1) + ", " + hexs(clo), {41});
+      E.salu("s_add_u32 " + S(x + 1) + ", s40, s41", {x + 1});
+      E.salu("s_mul_i32 " + S(x) + ", " + S(x) + ", " + hexs(clo), {x});
+    };
+    xs();
+    mul(0xED558CCDu, 0xFF51AFD7u);
+    xs();
+    mul(0x1A85EC53u, 0xC4CEB9FEu);
+    xs();
+  }
+  // per-lane fmix64 of v[lo], v[hi] in place (VALU; constants through s40/s41)
+  void vfmix(int lo, int hi) {
+    const Limb t1 = fresh(), t2 = fresh();
+    auto xs = [&]() {
+      E.valu("v_lshrrev_b32_e32 " + V(t1.v) + ", 1, " + V(hi));
+      E.valu("v_xor_b32_e32 " + V(lo) + ", " + V(lo) + ", " + V(t1.v));
+    };
+    auto mul = [&](uint32_t clo, uint32_t chi) {
+      E.salu("s_mov_b32 s40, " + hexs(clo), {40});
+      E.salu("s_mov_b32 s41, " + hexs(chi), {41});
+      E.valu("v_mul_hi_u32 " + V(t1.v) + ", " + V(lo) + ", s40", {40});
+      E.valu("v_mul_lo_u32 " + V(t2.v) + ", " + V(lo) + ", s41", {41});
+      E.valu("v_add_u32_e32 " + V(t1.v) + ", " + V(t1.v) + ", " + V(t2.v));
+      E.valu("v_mul_lo_u32 " + V(t2.v) + ", " + V(hi) + ", s40", {40});
+      E.valu("v_add_u32_e32 " + V(hi) + ", " + V(t1.v) + ", " + V(t2.v));
+      E.valu("v_mul_lo_u32 " + V(lo) + ", " + V(lo) + ", s40", {40});
+    };
+    xs();
+    mul(0xED558CCDu, 0xFF51AFD7u);
+    xs();
+    mul(0x1A85EC53u, 0xC4CEB9FEu);
+    xs();
+    drop(t1);
+    drop(t2);
+  }
+
+  int labels = 0;  // label numbers continue across the kernels of one module
+  std::string kernel(const std::string& name) {
+    E = Emitter();
+    E.nlab = labels;
+    val.assign(P.vwidth.size(), Val{});
+    cval.clear();
+    auto& o = E.o;
+    o << "  .text\n  .globl " << name << "\n  .p2align 8\n  .type " << name << ",@function\n" << name << ":\n";
+    // kernel arguments: search (gconsts, start, count, sk, sg, hit, flags, nblk);
+    //                   gen    (gconsts, start, count, sk, sg, verdict_out, nblk)
+    E.ctl("s_load_dwordx2 s[4:5], s[0:1], 0x0");
+    E.ctl("s_load_dwordx8 s[8:15], s[0:1], 0x8");
+    if (gen_kernel) {
+      E.ctl("s_load_dwordx2 s[16:17], s[0:1], 0x28");
+      E.ctl("s_load_dword s19, s[0:1], 0x30");
+    } else {
+      E.ctl("s_load_dwordx4 s[16:19], s[0:1], 0x28");
+    }
+    E.valu("v_and_b32_e32 v1, 63, v0");
+    E.valu("v_mov_b32_e32 v6, 0");
+    E.valu("v_readfirstlane_b32 s3, v0", {}, {3});
+    E.salu("s_lshr_b32 s3, s3, 6", {3});
+    E.ctl("s_waitcnt lgkmcnt(0)");
+    if (gen_kernel) E.salu("s_mov_b32 s18, 0", {18});
+    E.salu("s_and_b32 s29, s18, 1", {29});
+    // s[42:43] = early ? 0 : ~0 (the early-exit test of every ASSERT)
+    E.salu("s_cmp_eq_u32 s29, 0");
+    E.salu("s_cselect_b64 s[42:43], -1, 0", {42, 43});
+    E.salu("s_and_b32 s20, s8, 0xffffffc0", {20});
+    E.salu("s_mov_b32 s21, s9", {21});
+    E.salu("s_add_u32 s22, s8, s10", {22});
+    E.salu("s_addc_u32 s23, s9, s11", {23});
+    E.salu("s_sub_u32 s24, s22, s20", {24});
+    E.salu("s_subb_u32 s25, s23, s21", {25});
+    E.salu("s_add_u32 s24, s24, 63", {24});
+    E.salu("s_addc_u32 s25, s25, 0", {25});
+    E.salu("s_lshr_b64 s[24:25], s[24:25], 6", {24, 25});
+    E.salu("s_lshl_b32 s26, s2, 2", {26});
+    E.salu("s_add_u32 s26, s26, s3", {26});
+    E.salu("s_mov_b32 s27, 0", {27});
+    E.salu("s_lshl_b32 s28, s19, 2", {28});
+    E.salu("s_mov_b64 s[30:31], -1", {30, 31});
+    E.salu("s_mov_b64 s[32:33], 0", {32, 33});
+    // the lane half of the lane key: fmix64(lane ^ sk)
+    E.valu("v_xor_b32_e32 v2, s12, v1", {12});
+    E.valu("v_mov_b32_e32 v3, s13", {13});
+    vfmix(2, 3);
+    const std::string loop = E.newlab(), exit_ = E.newlab(), next = E.newlab(), cont = E.newlab();
+    E.label(loop);
+    // g < ngroups ?
+    E.salu("s_sub_u32 s40, s26, s24", {40});
+    E.salu("s_subb_u32 s40, s27, s25", {40});
+    E.ctl("s_cbranch_scc0 " + exit_);
+    E.salu("s_lshl_b64 s[34:35], s[26:27], 6", {34, 35});
+    E.salu("s_add_u32 s34, s34, s20", {34});
+    E.salu("s_addc_u32 s35, s35, s21", {35});
+    if (!gen_kernel) {
+      // stop once the group lies at or above the current first hit
+      const std::string noearly = E.newlab();
+      E.salu("s_cmp_eq_u32 s29, 0");
+      E.ctl("s_cbranch_scc1 " + noearly);
+      E.mem("global_load_dwordx2 v[8:9], v6, s[16:17] sc1", {16, 17});
+      E.ctl("s_waitcnt vmcnt(0)");
+      E.valu("v_readfirstlane_b32 s40, v8", {}, {40});
+      E.valu("v_readfirstlane_b32 s41, v9", {}, {41});
+      E.salu("s_sub_u32 s40, s34, s40", {40});
+      E.salu("s_subb_u32 s40, s35, s41", {40});
+      E.ctl("s_cbranch_scc0 " + exit_);
+      E.label(noearly);
+    }
+    // full group (s6): gbase >= start and gbase + 64 <= end
+    E.salu("s_sub_u32 s40, s34, s8", {40});
+    E.salu("s_subb_u32 s40, s35, s9", {40});
+    E.salu("s_cselect_b32 s41, 0, 1", {41});
+    E.salu("s_add_u32 s40, s34, 64", {40});
+    E.salu("s_addc_u32 s7, s35, 0", {7});
+    E.salu("s_sub_u32 s40, s22, s40", {40});
+    E.salu("s_subb_u32 s40, s23, s7", {40});
+    E.salu("s_cselect_b32 s40, 0, 1", {40});
+    E.salu("s_and_b32 s6, s41, s40", {6});
+    // G = fmix64((gbase >> 6) ^ sg)
+    E.salu("s_lshr_b64 s[36:37], s[34:35], 6", {36, 37});
+    E.salu("s_xor_b64 s[36:37], s[36:37], s[14:15]", {36, 37});
+    sfmix(36);
+    E.valu("v_xor_b32_e32 v4, s36, v2", {36});
+    E.valu("v_xor_b32_e32 v5, s37, v3", {37});
+    E.salu("s_mov_b64 s[38:39], -1", {38, 39});
+    body(next);
+    for (int r = kV0; r < 256; r++)
+      if (E.vref[r]) fail("internal: VGPR v" + std::to_string(r) + " still held after the body");
+    E.label(next);
+    // m = verdict, restricted to [start, end) in a partial group
+    E.salu("s_mov_b64 s[40:41], s[38:39]", {40, 41});
+    {
+      const std::string fullg = E.newlab();
+      E.salu("s_cmp_eq_u32 s6, 0");
+      E.ctl("s_cbranch_scc0 " + fullg);
+      E.valu("v_add_co_u32_e32 v8, vcc, s34, v1", {34}, {kVCC, kVCC + 1});
+      E.valu("v_mov_b32_e32 v9, s35", {35});
+      E.valu("v_addc_co_u32_e32 v9, vcc, 0, v9, vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
+      E.valu("v_cmp_le_u64_e64 s[44:45], s[8:9], v[8:9]", {8, 9}, {44, 45});
+      E.valu("v_cmp_gt_u64_e64 s[46:47], s[22:23], v[8:9]", {22, 23}, {46, 47});
+      E.salu("s_and_b64 s[40:41], s[40:41], s[44:45]", {40, 41});
+      E.salu("s_and_b64 s[40:41], s[40:41], s[46:47]", {40, 41});
+      E.label(fullg);
+    }
+    if (gen_kernel) {
+      // verdict bytes of the lanes in range: verdict_out[gbase + lane - start]
+      E.salu("s_mov_b64 s[44:45], s[38:39]", {44, 45});
+      // lanes in range: the partial-group mask built above when not full (s[40:41] = verdict & range)
+      // recompute the range alone into exec
+      E.valu("v_add_co_u32_e32 v8, vcc, s34, v1", {34}, {kVCC, kVCC + 1});
+      E.valu("v_mov_b32_e32 v9, s35", {35});
+      E.valu("v_addc_co_u32_e32 v9, vcc, 0, v9, vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
+      E.valu("v_cmp_le_u64_e64 s[46:47], s[8:9], v[8:9]", {8, 9}, {46, 47});
+      E.valu("v_cmp_gt_u64_e64 s[48:49], s[22:23], v[8:9]", {22, 23}, {48, 49});
+      E.salu("s_and_b64 s[46:47], s[46:47], s[48:49]", {46, 47});
+      E.valu("v_cndmask_b32_e64 v7, 0, 1, s[44:45]", {44, 45});
+      E.salu("s_sub_u32 s50, s34, s8", {50});
+      E.salu("s_subb_u32 s51, s35, s9", {51});
+      E.salu("s_add_u32 s50, s50, s16", {50});
+      E.salu("s_addc_u32 s51, s51, s17", {51});
+      E.valu("v_add_co_u32_e32 v8, vcc, s50, v1", {50}, {kVCC, kVCC + 1});
+      E.valu("v_mov_b32_e32 v9, s51", {51});
+      E.valu("v_addc_co_u32_e32 v9, vcc, 0, v9, vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
+      E.salu("s_mov_b64 exec, s[46:47]");
+      E.mem("global_store_byte v[8:9], v7, off");
+      E.salu("s_mov_b64 exec, -1");
+    } else {
+      E.salu("s_cmp_eq_u64 s[40:41], 0");
+      E.ctl("s_cbranch_scc1 " + cont);
+      E.salu("s_ff1_i32_b64 s44, s[40:41]", {44});
+      E.salu("s_bcnt1_i32_b64 s45, s[40:41]", {45});
+      E.salu("s_add_u32 s32, s32, s45", {32});
+      E.salu("s_addc_u32 s33, s33, 0", {33});
+      E.salu("s_add_u32 s46, s34, s44", {46});
+      E.salu("s_addc_u32 s47, s35, 0", {47});
+      E.salu("s_sub_u32 s44, s46, s30", {44});
+      E.salu("s_subb_u32 s44, s47, s31", {44});
+      E.ctl("s_cbranch_scc0 " + cont);
+      E.salu("s_mov_b64 s[30:31], s[46:47]", {30, 31});
+      E.salu("s_cmp_eq_u32 s29, 0");
+      E.ctl("s_cbranch_scc1 " + cont);
+      E.salu("s_mov_b64 exec, 1");
+      E.valu("v_mov_b32_e32 v8, s46", {46});
+      E.valu("v_mov_b32_e32 v9, s47", {47});
+      E.mem("global_atomic_umin_x2 v6, v[8:9], s[16:17]", {16, 17});
+      E.salu("s_mov_b64 exec, -1");
+    }
+    E.label(cont);
+    E.salu("s_add_u32 s26, s26, s28", {26});
+    E.salu("s_addc_u32 s27, s27, 0", {27});
+    E.ctl("s_branch " + loop);
+    E.label(exit_);
+    if (!gen_kernel) {
+      const std::string nobest = E.newlab(), end = E.newlab();
+      E.salu("s_cmp_eq_u64 s[30:31], -1");
+      E.ctl("s_cbranch_scc1 " + nobest);
+      E.salu("s_mov_b64 exec, 1");
+      E.valu("v_mov_b32_e32 v8, s30", {30});
+      E.valu("v_mov_b32_e32 v9, s31", {31});
+      E.mem("global_atomic_umin_x2 v6, v[8:9], s[16:17]", {16, 17});
+      E.salu("s_mov_b64 exec, -1");
+      E.label(nobest);
+      E.salu("s_cmp_eq_u64 s[32:33], 0");
+      E.ctl("s_cbranch_scc1 " + end);
+      // the wave's count goes to its block's stripe (engine.hip kHitStripes: 16 x 128 B after the hit)
+      E.salu("s_and_b32 s40, s2, 15", {40});
+      E.salu("s_add_u32 s40, s40, 1", {40});
+      E.salu("s_lshl_b32 s40, s40, 7", {40});
+      E.salu("s_add_u32 s44, s16, s40", {44});
+      E.salu("s_addc_u32 s45, s17, 0", {45});
+      E.salu("s_mov_b64 exec, 1");
+      E.valu("v_mov_b32_e32 v8, s32", {32});
+      E.valu("v_mov_b32_e32 v9, s33", {33});
+      E.mem("global_atomic_add_x2 v6, v[8:9], s[44:45]", {44, 45});
+      E.label(end);
+    }
+    E.ctl("s_endpgm");
+    // descriptor
+    const int nv = std::max(E.vhigh, kV0), ns = std::max(E.shigh, 52);
+    const int accum = (nv + 3) / 4 * 4;
+    o << "  .section .rodata,\"a\",@progbits\n  .p2align 6, 0x0\n  .amdhsa_kernel " << name << "\n"
+      << "    .amdhsa_group_segment_fixed_size 0\n    .amdhsa_private_segment_fixed_size 0\n"
+      << "    .amdhsa_kernarg_size " << (gen_kernel ? 52 : 56) << "\n"
+      << "    .amdhsa_user_sgpr_count 2\n    .amdhsa_user_sgpr_kernarg_segment_ptr 1\n"
+      << "    .amdhsa_system_sgpr_workgroup_id_x 1\n    .amdhsa_system_vgpr_workitem_id 0\n"
+      << "    .amdhsa_next_free_vgpr " << nv << "\n    .amdhsa_next_free_sgpr " << ns << "\n"
+      << "    .amdhsa_accum_offset " << accum << "\n    .amdhsa_reserve_vcc 1\n"
+      << "    .amdhsa_float_denorm_mode_32 3\n    .amdhsa_float_denorm_mode_16_64 3\n"
+      << "  .end_amdhsa_kernel\n  .text\n";
+    labels = E.nlab;
+    meta_vgpr[name] = nv;
+    meta_sgpr[name] = ns + 6;
+    return o.str();
+  }
+  std::map<std::string, int> meta_vgpr, meta_sgpr;
+};
+
+std::string metadata(const std::map<std::string, int>& vg, const std::map<std::string, int>& sg, bool with_gen) {
+  std::ostringstream o;
+  auto arg = [&](uint32_t off, uint32_t size, const char* kind, bool global) {
+    o << "      - .offset: " << off << "\n        .size: " << size << "\n        .value_kind: " << kind << "\n";
+    if (global) o << "        .address_space: global\n";
+  };
+  o << "  .amdgpu_metadata\n---\namdhsa.kernels:\n";
+  for (const char* name : {"mgj_search", "mgj_gen"}) {
+    const bool gen = std::strcmp(name, "mgj_gen") == 0;
+    if (gen && !with_gen) continue;
+    o << "  - .args:\n";
+    arg(0, 8, "global_buffer", true);
+    for (uint32_t k = 0; k < 4; k++) arg(8 + 8 * k, 8, "by_value", false);
+    arg(40, 8, "global_buffer", true);
+    if (gen) {
+      arg(48, 4, "by_value", false);
+    } else {
+      arg(48, 4, "by_value", false);
+      arg(52, 4, "by_value", false);
+    }
+    o << "    .group_segment_fixed_size: 0\n    .kernarg_segment_align: 8\n"
+      << "    .kernarg_segment_size: " << (gen ? 52 : 56) << "\n    .max_flat_workgroup_size: 256\n"
+      << "    .name: " << name << "\n    .private_segment_fixed_size: 0\n"
+      << "    .sgpr_count: " << sg.at(name) << "\n    .sgpr_spill_count: 0\n"
+      << "    .symbol: " << name << ".kd\n    .uniform_work_group_size: 1\n    .uses_dynamic_stack: false\n"
+      << "    .vgpr_count: " << vg.at(name) << "\n    .vgpr_spill_count: 0\n    .wavefront_size: 64\n"
+      << "    .agpr_count: 0\n";
+  }
+  o << "amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n  .end_amdgpu_metadata\n";
+  return o.str();
+}
+
+}  // namespace
+
+int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const std::vector<uint32_t>& gconsts,
+                   uint32_t kernels, std::string& out, std::string& err) {
+  try {
+    Gen g(P, specs, gconsts);
+    g.analyse();
+    std::ostringstream o;
+    o << kAsmMarker << "\n  .amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"\n  .amdhsa_code_object_version 6\n";
+    g.gen_kernel = false;
+    o << g.kernel("mgj_search");
+    const bool with_gen = (kernels & JIT_GEN) != 0;
+    if (with_gen) {
+      g.gen_kernel = true;
+      o << g.kernel("mgj_gen");
+    }
+    o << metadata(g.meta_vgpr, g.meta_sgpr, with_gen);
+    out = o.str();
+    return MG_OK;
+  } catch (const AsmFail& f) {
+    err = f.why;
+    return MG_E_UNSUPPORTED;
+  } catch (const std::exception& x) {
+    err = std::string("assembly tier: ") + x.what();
+    return MG_E_UNSUPPORTED;
+  }
+}
+
+}  // namespace mg

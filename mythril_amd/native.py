@@ -26,6 +26,8 @@ MG_E_NODEVICE = -4
 MG_E_NOMEM = -5
 MG_E_NOTINIT = -6
 MG_SEARCH_EARLY_EXIT = 1
+MG_JIT_GEN_VERDICTS = 1
+MG_JIT_ASM = 2  # the first tier: gfx950 assembly emitted by the engine (jit_asm.cpp)
 NO_HIT = (1 << 64) - 1
 
 EXPORTS = [
@@ -33,7 +35,7 @@ EXPORTS = [
     "mg_program_specialized", "mg_program_load",
     "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_info", "mg_gen_free", "mg_eval", "mg_eval_dev",
     "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
-    "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_jit_compile", "mg_jit_compile_ex", "mg_jit_verdicts", "mg_jit_info",
+    "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_program_jit_asm", "mg_jit_compile", "mg_jit_compile_ex", "mg_jit_verdicts", "mg_jit_info",
     "mg_jit_compile_async", "mg_jit_poll", "mg_jit_cancel", "mg_jit_helper_pid", "mg_cache_clear", "mg_split_range",
     "mg_jit_free", "mg_jit_search", "mg_jit_eval", "mg_jit_eval_dev",
 ]
@@ -120,6 +122,8 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_dev_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
             "mg_program_jit_source": (C.c_int, [u8p, C.c_size_t, u32p, C.c_size_t, C.c_int, C.c_char_p,
                                                 C.c_size_t, C.POINTER(C.c_size_t)]),
+            "mg_program_jit_asm": (C.c_int, [u8p, C.c_size_t, u32p, C.c_size_t, C.c_int, C.c_char_p,
+                                             C.c_size_t, C.POINTER(C.c_size_t)]),
             "mg_jit_compile": (C.c_int, [C.c_uint64, C.c_uint64, u64p]),
             "mg_jit_compile_ex": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, u64p]),
             "mg_jit_verdicts": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, u8p]),
@@ -236,6 +240,20 @@ def jit_source(blob: bytes, gen_blob: Optional[np.ndarray] = None, compile: bool
     return buf.value.decode()
 
 
+def jit_asm(blob: bytes, gen_blob: np.ndarray, compile: bool = False) -> str:
+    """Host-only: the first tier's gfx950 assembly of a search program (mgj_search + mgj_gen),
+    optionally assembled and linked through comgr (no GPU).  Raises EngineUnsupported for
+    programs outside the tier."""
+    lib = load_library()
+    g = np.ascontiguousarray(gen_blob, dtype=np.uint32)
+    n = C.c_size_t()
+    _check(lib.mg_program_jit_asm(_u8(blob), len(blob), _ptr(g, C.c_uint32), g.size, 0, None, 0, C.byref(n)))
+    buf = C.create_string_buffer(n.value + 1)
+    _check(lib.mg_program_jit_asm(_u8(blob), len(blob), _ptr(g, C.c_uint32), g.size, 1 if compile else 0, buf,
+                                  n.value + 1, C.byref(n)))
+    return buf.value.decode()
+
+
 def split_range(start: int, count: int, n_dev: int):
     """Host-only ``mg_split_range``: the [start, start+count) slice each of ``n_dev`` devices
     sweeps in a multi-device ``mg_search`` — [(start_d, count_d)] in device order."""
@@ -347,15 +365,18 @@ class Engine:
         return (None if fh.value == NO_HIT else fh.value), nh.value
 
     # JIT-specialised kernels --------------------------------------
-    def jit_compile(self, prog: int, gen: int = 0, gen_verdicts: bool = False) -> int:
+    def jit_compile(self, prog: int, gen: int = 0, gen_verdicts: bool = False, asm: bool = False) -> int:
+        """``asm``: the first tier (assembly emitted by the engine; search programs only)."""
         h = C.c_uint64()
-        _check(self.lib.mg_jit_compile_ex(prog, gen, 1 if gen_verdicts else 0, C.byref(h)))
+        flags = (MG_JIT_GEN_VERDICTS if gen_verdicts else 0) | (MG_JIT_ASM if asm else 0)
+        _check(self.lib.mg_jit_compile_ex(prog, gen, flags, C.byref(h)))
         return h.value
 
-    def jit_compile_async(self, prog: int, gen: int = 0, gen_verdicts: bool = False) -> int:
+    def jit_compile_async(self, prog: int, gen: int = 0, gen_verdicts: bool = False, asm: bool = False) -> int:
         """Start compiling on the engine's compile thread; returns a ticket for :meth:`jit_poll`."""
         t = C.c_uint64()
-        _check(self.lib.mg_jit_compile_async(prog, gen, 1 if gen_verdicts else 0, C.byref(t)))
+        flags = (MG_JIT_GEN_VERDICTS if gen_verdicts else 0) | (MG_JIT_ASM if asm else 0)
+        _check(self.lib.mg_jit_compile_async(prog, gen, flags, C.byref(t)))
         return t.value
 
     def jit_poll(self, ticket: int, wait_ms: int = 0) -> Optional[int]:

@@ -17,6 +17,13 @@ SHA3 lengths, the DIV/MOD "divisor == 0" checks) are taken on the host by
 literal folding, exactly where LASER takes them with ``z3.simplify``; a decision
 that depends on an input raises :class:`ReplayUnsupported`.
 
+An input-dependent jump (a JUMP target or JUMPI condition computed from calldata) is followed
+along the concrete path when the caller passes ``follow`` (term -> its value under the request's
+concrete inputs, e.g. :func:`engine_follow`, which evaluates it on the GPU): the replay then takes
+that branch and records the decision as a path constraint (``ReplayResult.path``), so the program is
+exactly LASER's path condition plus the post-state of that path — as concolic execution takes the
+concrete branch (``transaction/concolic.py:15-62``).  Without ``follow`` such a request is refused.
+
 Two documented departures, both for concrete execution only: SHA3 of memory
 becomes the engine's real ``keccak256`` term (LASER hashes concrete data on the
 host, ``keccak_function_manager.py:44-57``), and EXP becomes ``bvexp`` (LASER
@@ -61,11 +68,12 @@ def disassemble(code: bytes):
 
 
 class ReplayResult:
-    def __init__(self, storage: S.BaseArray, halted: str, inputs: Dict[str, T.Term], touched):
+    def __init__(self, storage: S.BaseArray, halted: str, inputs: Dict[str, T.Term], touched, path=()):
         self.storage = storage
         self.halted = halted
         self.inputs = inputs
         self.touched = touched  # storage keys written (concrete ints where foldable)
+        self.path = list(path)  # Bool terms: the input-dependent decisions taken (``follow``)
 
     def storage_word(self, key: int) -> BitVec:
         """Post-state storage word at a concrete key (``account.storage[key]``)."""
@@ -136,7 +144,7 @@ class _Memory:
 
 
 def replay(code_hex: str, calldata: bytes = b"", pre_storage: Optional[Dict[int, int]] = None,
-           max_steps: int = 10000) -> ReplayResult:
+           max_steps: int = 10000, follow=None) -> ReplayResult:
     code = bytes.fromhex(code_hex)
     ins = disassemble(code)
     pc_index = {pc: k for k, (pc, _, _) in enumerate(ins)}
@@ -153,6 +161,22 @@ def replay(code_hex: str, calldata: bytes = b"", pre_storage: Optional[Dict[int,
     stack: List = []
     mem = _Memory()
     touched = []
+    path: List[T.Term] = []
+
+    def decide(x, what: str) -> int:
+        """A control decision: folded where LASER's simplify folds it, else followed along the
+        concrete path (``follow``) with the decision kept as a path constraint."""
+        x = _as_bv(x)
+        if x.value is not None:
+            return int(x.value)
+        if follow is None:
+            raise ReplayUnsupported(f"input-dependent {what}")
+        v = int(follow(x.raw)) & TT256M1
+        path.append(T.eq(x.raw, BVV(v, 256).raw))
+        return v
+
+    def result(halted: str) -> ReplayResult:
+        return ReplayResult(storage, halted, inputs, touched, path)
     k = 0
     steps = 0
 
@@ -165,7 +189,7 @@ def replay(code_hex: str, calldata: bytes = b"", pre_storage: Optional[Dict[int,
         if steps > max_steps:
             raise ReplayUnsupported("step limit")
         if k >= len(ins):
-            return ReplayResult(storage, "stop", inputs, touched)
+            return result("stop")
         pc, op, imm = ins[k]
         k += 1
         if 0x60 <= op <= 0x7F:                       # PUSHn
@@ -181,7 +205,7 @@ def replay(code_hex: str, calldata: bytes = b"", pre_storage: Optional[Dict[int,
                 raise ExceptionalHalt("stack underflow")
             stack[-1], stack[-n - 1] = stack[-n - 1], stack[-1]
         elif op == 0x00:                             # STOP
-            return ReplayResult(storage, "stop", inputs, touched)
+            return result("stop")
         elif op == 0x01:                             # ADD  instructions.py:433-441
             stack.append(_pop_bitvec(stack) + _pop_bitvec(stack))
         elif op == 0x02:                             # MUL  :464-477
@@ -288,8 +312,29 @@ def replay(code_hex: str, calldata: bytes = b"", pre_storage: Optional[Dict[int,
             stack.append(S.Concat([cd_byte(start + i) for i in range(32)]))
         elif op == 0x36:                             # CALLDATASIZE :791-807
             stack.append(size)
+        elif op == 0x37:                             # CALLDATACOPY :881-893, _calldata_copy_helper :810-878
+            mstart = _concrete(_as_bv(_pop(stack)), "CALLDATACOPY memory offset")
+            dstart = _as_bv(_pop(stack))
+            n = _concrete(_as_bv(_pop(stack)), "CALLDATACOPY size")
+            if n > 4096 or mstart > 1 << 20:
+                raise ReplayUnsupported("CALLDATACOPY size")
+            if n > 0:
+                mem.extend(mstart, n)
+                for i in range(n):
+                    mem.bytes[mstart + i] = cd_byte(dstart + i)
         elif op == 0x38:                             # CODESIZE
             stack.append(BVV(len(code), 256))
+        elif op == 0x39:                             # CODECOPY :1061-1165, _code_copy_helper :1167-1227
+            moff = _concrete(_as_bv(_pop(stack)), "CODECOPY memory offset")
+            coff = _concrete(_as_bv(_pop(stack)), "CODECOPY code offset")
+            n = _concrete(_as_bv(_pop(stack)), "CODECOPY size")
+            if n > 4096 or moff > 1 << 20:
+                raise ReplayUnsupported("CODECOPY size")
+            mem.extend(moff, n)
+            for i in range(n):
+                if coff + i >= len(code):  # the reference stops at the end of the code (memory kept)
+                    break
+                mem.bytes[moff + i] = BVV(code[coff + i], 8)
         elif op == 0x3A:                             # GASPRICE
             stack.append(BitVec(inputs["gasprice"]))
         elif op == 0x50:                             # POP
@@ -322,14 +367,14 @@ def replay(code_hex: str, calldata: bytes = b"", pre_storage: Optional[Dict[int,
             storage[idx] = _as_bv(val)
             touched.append(idx)
         elif op == 0x56:                             # JUMP
-            dest = _concrete(_as_bv(_pop(stack)), "JUMP target")
+            dest = decide(_pop(stack), "JUMP target")
             if dest not in jumpdests:
                 raise ExceptionalHalt("bad jump")
             k = pc_index[dest]
         elif op == 0x57:                             # JUMPI
-            dest = _concrete(_as_bv(_pop(stack)), "JUMPI target")
+            dest = decide(_pop(stack), "JUMPI target")
             cond = _pop(stack)
-            c = _concrete(_as_bv(cond), "JUMPI condition")
+            c = decide(cond, "JUMPI condition")
             if c != 0:
                 if dest not in jumpdests:
                     raise ExceptionalHalt("bad jump")
@@ -342,7 +387,10 @@ def replay(code_hex: str, calldata: bytes = b"", pre_storage: Optional[Dict[int,
             pass
         elif op == 0xF3:                             # RETURN
             _pop(stack), _pop(stack)
-            return ReplayResult(storage, "return", inputs, touched)
+            return result("return")
+        elif op == 0xFF:                             # SELFDESTRUCT :1823-1845 (ends the call; storage kept)
+            _pop(stack)
+            return result("selfdestruct")
         elif op == 0xFE:
             raise ExceptionalHalt("invalid opcode")
         else:
@@ -364,3 +412,36 @@ def replay_assignment(vec: dict):
     }
     arrays = {"calldata": ({i: b for i, b in enumerate(data)}, 0)}
     return scal, arrays
+
+
+def engine_follow(engine, scal: Dict[str, int], arrays=None):
+    """``follow`` for :func:`replay` through the product path: the decision term evaluated on the
+    GPU (``mg_eval``) under the request's concrete inputs — scalar coordinates by name, array sites
+    (``calldata[...]``) by the concrete byte at their key (the key itself evaluated the same way)."""
+    from . import ssa
+
+    arrays = arrays or {}
+
+    def value(term: T.Term) -> int:
+        P = ssa.flatten([T.BoolVal(True), T.eq(term, term)], extra=[term])
+        P.set_watch([P.term_node[term.id]])
+        assign = []
+        for c in P.coords:
+            if c.kind == ssa.COORD_SCALAR:
+                assign.append(scal.get(c.name, 0))
+            else:
+                assign.append(None)
+        for c in P.sites:  # a site's key is a term over the inputs: evaluate it first
+            key = value(P.node_term[P.site_key_node[c.index]])
+            table, dflt = arrays.get(c.name, ({}, 0))
+            assign[c.index] = table.get(key, dflt)
+        soa = ssa.soa_from_assignments(P, [assign])
+        prog = engine.load(P.to_bytes())
+        try:
+            info = engine.info(prog)
+            _, watch = engine.eval(prog, soa, 1, watch_words=info.watch_words)
+        finally:
+            engine.free(prog)
+        return ssa.limbs_to_int(watch[:, 0])
+
+    return value

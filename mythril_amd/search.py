@@ -20,6 +20,7 @@ Generator heuristics (per coordinate, all on device, pure functions of
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Dict, List, Optional, Sequence
 
@@ -428,6 +429,11 @@ def model_from_assignment(P: ssa.Program, assign: np.ndarray):
 # exponential average of the compiles this process measured (cold value from the bench:
 # ~0.2 s on the MI355X box's host through hipRTC, less through comgr)
 JIT_COMPILE_S = [0.15]
+# the same for the first tier (assembly emitted by the engine, jit_asm.cpp): emission + assembler
+# + link, a few ms
+JIT_ASM_COMPILE_S = [0.01]
+# MYTHGPU_JIT_ASM=0: no first tier (the interpreter runs until the O3 kernel is ready)
+JIT_ASM = os.environ.get("MYTHGPU_JIT_ASM", "1") != "0"
 # while a compile is pending, interpreter launches are cut to about this long so the search
 # switches to the compiled kernel soon after it is ready; in the first few ms after the submit they
 # are cut to JIT_FIRST_POLL_S, so a kernel the engine already holds (same source: LASER re-asks
@@ -471,12 +477,15 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
     hits = 0
     used = "interp"
     expected_compile = JIT_COMPILE_S[0] if jit_cost_s is None else jit_cost_s
+    expected_asm = JIT_ASM_COMPILE_S[0]
     assign = np.zeros(max(P.watch_words, 1), dtype=np.uint32) if want_model else None
     try:
         gh = engine.load_gen(prog, blob)
         timing["load_ms"] = (time.perf_counter() - th) * 1e3
         jh = None
-        ticket = None
+        ticket = None      # the O3 kernel's compile
+        ticket_asm = None  # the first tier's (assembly), submitted just before it
+        tier = None        # "asm" / "o3": the compiled kernel in use
         rate = None  # candidates/s of the kernel in use (last launch)
         try:
             if jit == "always":
@@ -484,7 +493,7 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                 try:
                     jh = engine.jit_compile(prog, gh)
                     timing["jit_compile_ms"] = (time.perf_counter() - tc) * 1e3
-                    used = "jit"
+                    used, tier = "jit", "o3"
                 except Exception:  # the JIT rejected this program: scan on the interpreter
                     jit = "never"
             start = 0
@@ -493,27 +502,54 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                 left = timeout_s - (now - t0)
                 if left <= 0 or (cancel is not None and cancel.is_set()):
                     break
+                if ticket_asm is not None:
+                    try:
+                        h = engine.jit_poll(ticket_asm)
+                    except Exception:  # outside the first tier: the interpreter until the O3 kernel
+                        ticket_asm, h = None, None
+                    if h is not None:
+                        ticket_asm = None
+                        took = now - tc
+                        JIT_ASM_COMPILE_S[0] = 0.5 * JIT_ASM_COMPILE_S[0] + 0.5 * took
+                        timing["jit_asm_compile_ms"] = took * 1e3
+                        if jh is None:
+                            jh, used, rate, tier = h, "jit", None, "asm"
+                            timing["jit_switch_ms"] = (now - t0) * 1e3  # when the search moved to a kernel
+                            timing["interp_candidates"] = scanned
+                            chunk = max(chunk, 1 << 22)
+                        else:
+                            engine.jit_free(h)
                 if ticket is not None:
                     try:
                         h = engine.jit_poll(ticket)
-                    except Exception:  # JIT unavailable for this program: stay on the interpreter
-                        ticket, jit = None, "never"
-                        h = None
+                    except Exception:  # JIT unavailable for this program: stay where we are
+                        ticket, h = None, None
+                        if jh is None:
+                            jit = "never"
                     if h is not None:
-                        ticket, jh, used, rate = None, h, "jit", None
+                        ticket = None
+                        if jh is not None:  # the O3 kernel replaces the first tier's on the same stream
+                            engine.jit_free(jh)
+                        else:
+                            timing["jit_switch_ms"] = (now - t0) * 1e3
+                            timing["interp_candidates"] = scanned
+                        jh, used, rate, tier = h, "jit", None, "o3"
                         took = now - tc
                         timing["jit_compile_ms"] = took * 1e3
-                        timing["jit_switch_ms"] = (now - t0) * 1e3  # when the search moved to the kernel
-                        timing["interp_candidates"] = scanned
+                        timing["o3_switch_ms"] = (now - t0) * 1e3
                         JIT_COMPILE_S[0] = 0.5 * JIT_COMPILE_S[0] + 0.5 * took
                         chunk = max(chunk, 1 << 22)
-                if jh is None and ticket is None and jit == "auto" and scanned > 0 and left > 1.2 * expected_compile:
+                if (jh is None and ticket is None and ticket_asm is None and jit == "auto" and scanned > 0
+                        and left > 1.2 * min(expected_compile, expected_asm if JIT_ASM else expected_compile)):
                     tc = time.perf_counter()
-                    ticket = engine.jit_compile_async(prog, gh)
+                    if JIT_ASM and left > 1.2 * expected_asm:
+                        ticket_asm = engine.jit_compile_async(prog, gh, asm=True)
+                    if left > 1.2 * expected_compile:
+                        ticket = engine.jit_compile_async(prog, gh)
                 n = min(chunk, max_candidates - scanned)
                 if rate:
                     cap_s = left
-                    if ticket is not None:
+                    if ticket is not None or ticket_asm is not None:
                         cap_s = min(left, JIT_FIRST_POLL_S if now - tc < 5 * JIT_FIRST_POLL_S else JIT_POLL_S)
                     if max_launch_s is not None:
                         cap_s = min(cap_s, max_launch_s)
@@ -536,6 +572,8 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                 # (x16 after the 2^12 capture launch: a query that misses there is not an easy one)
                 chunk = min(chunk * (16 if chunk < (1 << 16) else 4), 1 << 26 if jh is None else 1 << 30)
         finally:
+            if ticket_asm is not None:
+                engine.jit_cancel(ticket_asm)
             if ticket is not None:
                 engine.jit_cancel(ticket)
             if jh is not None:
@@ -546,6 +584,8 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
     dt = time.perf_counter() - t0
     res = SearchResult(hit, hits, scanned, dt)
     res.engine = used
+    if tier is not None:
+        timing["jit_tier"] = tier
     global LAST_ENGINE, LAST_RESULT
     LAST_ENGINE, LAST_RESULT = used, res
     if hit is not None and want_model:

@@ -1,0 +1,206 @@
+"""The JIT's first tier (``jit_asm.cpp``: gfx950 assembly emitted by the engine, MG_JIT_ASM) against
+the C port (``oracle/bveval.c``) on the same GEN3 candidate stream.
+
+* per-candidate verdicts of the tier's ``mgj_gen`` on random unaligned 63-bit windows (two with bit
+  31 of the low index word set), for every workload inside the tier, the bench's hard needle, the
+  literal-tail mapping keys and random programs over the tier's operators;
+* its ``mgj_search``: first hit and hit count of each window equal the C port's, and an early-exit
+  search from index 0 finds the same first hit as the O3 kernel and the interpreter;
+* the full-size property: the hard needle (~2^-24, first hit near index 3.2e8) found at the same
+  index by the tier and by the O3 kernel.
+
+Reference anchor: a candidate's verdict is ``Model.eval(And(constraints), model_completion=True)``
+(``mythril/laser/smt/model.py:45-59``) of the query ``get_model`` receives
+(``mythril/support/model.py:15-49``).
+"""
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+from mythril_amd import native, search, workloads
+from mythril_amd.smt import terms as T
+
+pytestmark = pytest.mark.gpu
+
+N = 2048
+OUTSIDE = {"bectoken_batch_overflow", "sha3_keyed_mapping"}  # UMUL_NOOVF / Keccak, EXP, SDIV
+
+
+def _windows(rng, k=4):
+    out = []
+    for w in range(k):
+        start = rng.getrandbits(63)
+        if w < 2:
+            start = (start & ~0xFFFFFFFF) | 0x80000000 | rng.getrandbits(31)
+        out.append(start | 1)
+    return out
+
+
+def _check(engine, name, roots, seeds=2, windows=4):
+    from oracle import cport
+
+    rng = random.Random(zlib.crc32(name.encode()) ^ 0x61736D)
+    P, blob = search.prepare(roots)
+    pb = P.to_bytes()
+    prog = engine.load(pb)
+    gh = engine.load_gen(prog, blob)
+    ja = engine.jit_compile(prog, gh, gen_verdicts=True, asm=True)
+    try:
+        for _ in range(seeds):
+            seed = rng.getrandbits(32)
+            for start in _windows(rng, windows):
+                cf, ch, want = cport.search(pb, blob, seed, start, N, threads=16, verdicts=True)
+                va = engine.jit_verdicts(ja, seed, start, N)
+                bad = np.nonzero(va != want)[0]
+                assert bad.size == 0, (f"{name}: asm tier {bad.size} mismatches, first at index {start + int(bad[0])} "
+                                       f"seed {seed} (asm {va[bad[0]]}, C port {want[bad[0]]})")
+                assert engine.jit_search(ja, seed, start, N, early_exit=False) == (cf, ch)
+                ef, _ = engine.jit_search(ja, seed, start, N, early_exit=True)
+                assert ef == cf
+    finally:
+        engine.jit_free(ja)
+        engine.free_gen(gh)
+        engine.free(prog)
+
+
+def _queries():
+    from tests.helpers import literal_tail_query
+    import bench
+
+    q = {n: (lambda n=n: [c.raw for c in workloads.WORKLOADS[n]()]) for n in sorted(workloads.WORKLOADS)
+         if n not in OUTSIDE}
+    q["hard_needle"] = lambda: bench.hard_query(workloads.WORKLOADS["token_transfer_underflow"]())
+    q["literal_tail_keys"] = lambda: [c.raw for c in literal_tail_query()]
+    return q
+
+
+@pytest.mark.parametrize("name", sorted(_queries()))
+def test_asm_tier_verdicts(engine, name):
+    _check(engine, name, _queries()[name]())
+
+
+# operators inside the tier
+_BIN = ["bvadd", "bvsub", "bvmul", "bvand", "bvor", "bvxor"]
+_CMP = ["bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge"]
+
+
+def _random_program(seed: int, n_ops: int = 36):
+    from tests.helpers import edge_value
+
+    rng = random.Random(seed)
+    pool = {}
+
+    def add(t):
+        pool.setdefault(t.width, []).append(t)
+        return t
+
+    for i, w in enumerate((256, 256, 160, 64, 32, 8, 1 + 7, 257, 512, 1)):
+        if w == 1:
+            continue
+        add(T.BitVecVar(f"a{seed}_{i}_{w}", w))
+        add(T.BitVecVal(edge_value(rng, w), w))
+    bools = [T.BoolVar(f"f{seed}")]
+    arr = T.ArrayVar("Storage", 256, 256)
+    fn = T.FuncDecl("keccak256_512", 512, 256)
+    for _ in range(n_ops):
+        kind = rng.random()
+        w = rng.choice([256, 256, 64, 160, 8, 32, 512])
+        src = pool.get(w) or [T.BitVecVal(0, w)]
+        a, b = rng.choice(src), rng.choice(src)
+        if kind < 0.35:
+            op = rng.choice(_BIN)
+            t = T.bvbin(op if not (op == "bvmul" and w > 256) else "bvadd", a, b)
+        elif kind < 0.45:
+            t = T.bvun(rng.choice(["bvnot", "bvneg"]), a)
+        elif kind < 0.60:
+            c = T.bvcmp(rng.choice(_CMP), a, b) if w <= 256 else T.eq(a, b)
+            bools.append(c)
+            continue
+        elif kind < 0.68:
+            t = T.ite(rng.choice(bools), a, b)
+        elif kind < 0.76:
+            hi = rng.randrange(w)
+            t = T.extract(hi, rng.randrange(hi + 1), a)
+        elif kind < 0.82:
+            w2 = rng.choice([8, 32, 96, 160, 256])
+            b2 = rng.choice(pool.get(w2) or [T.BitVecVal(1, w2)])
+            t = T.concat(a, b2) if a.width + w2 <= 1024 else a
+        elif kind < 0.88:
+            k = rng.choice([1, 8, 96, 256])
+            t = T.zero_extend(k, a) if rng.random() < 0.5 else T.sign_extend(k, a)
+        elif kind < 0.95:
+            idx = rng.choice(pool[256])
+            st = T.store(arr, rng.choice(pool[256]), rng.choice(pool[256])) if rng.random() < 0.5 else arr
+            t = T.select(st, idx)
+        else:
+            t = T.app(fn, T.concat(rng.choice(pool[256]), rng.choice(pool[256])))
+        add(t)
+        if t.width <= 256 and rng.random() < 0.3:
+            bools.append(T.eq(t, rng.choice(pool.get(t.width) or [t])))
+    for _ in range(3):
+        x, y = rng.choice(bools), rng.choice(bools)
+        bools.append(rng.choice([T.and_(x, y), T.or_(x, y), T.not_(x), T.xor_(x, y), T.eq(x, y)]))
+    # an OR of a few of them: satisfiable by many candidates, so verdicts carry information
+    return [T.or_(*rng.sample(bools, min(3, len(bools)))), T.or_(*rng.sample(bools, min(3, len(bools))))]
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_asm_tier_random_programs(engine, seed):
+    roots = _random_program(1000 + seed)
+    P, blob = search.prepare(roots)
+    try:
+        native.jit_asm(P.to_bytes(), blob)
+    except native.EngineUnsupported as e:
+        pytest.skip(f"outside the tier: {e}")
+    _check(engine, f"random{seed}", roots, seeds=1, windows=3)
+
+
+def test_asm_tier_first_hit_from_zero(engine):
+    """Early-exit searches from index 0 (the product's shape): the tier, the O3 kernel and the
+    interpreter report the same first hit on every workload inside the tier."""
+    for name in sorted(workloads.WORKLOADS):
+        if name in OUTSIDE:
+            continue
+        P, blob = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
+        prog = engine.load(P.to_bytes())
+        gh = engine.load_gen(prog, blob)
+        ja = engine.jit_compile(prog, gh, asm=True)
+        jo = engine.jit_compile(prog, gh)
+        try:
+            for count in (1 << 12, 1 << 20):
+                a = engine.jit_search(ja, 7, 0, count, early_exit=True)[0]
+                o = engine.jit_search(jo, 7, 0, count, early_exit=True)[0]
+                i = engine.search(prog, gh, 7, 0, count, early_exit=True)[0]
+                assert a == o == i, (name, count, a, o, i)
+        finally:
+            engine.jit_free(ja)
+            engine.jit_free(jo)
+            engine.free_gen(gh)
+            engine.free(prog)
+
+
+def test_asm_tier_hard_needle_full_size(engine):
+    """The bench's hard query at full size: the ~2^-24 needle near index 3.2e8, found at the same
+    index by the tier and by the O3 kernel (hit counts over the whole sweep agree too)."""
+    import bench
+
+    roots = bench.hard_query(workloads.WORKLOADS["token_transfer_underflow"]())
+    P, blob = search.prepare(roots)
+    prog = engine.load(P.to_bytes())
+    gh = engine.load_gen(prog, blob)
+    ja = engine.jit_compile(prog, gh, asm=True)
+    jo = engine.jit_compile(prog, gh)
+    try:
+        seed = 0x6D797468
+        n = 1 << 29
+        fa, ha = engine.jit_search(ja, seed, 0, n, early_exit=False)
+        fo, ho = engine.jit_search(jo, seed, 0, n, early_exit=False)
+        assert (fa, ha) == (fo, ho) and fa is not None
+        assert engine.jit_search(ja, seed, 0, n, early_exit=True)[0] == fa
+    finally:
+        engine.jit_free(ja)
+        engine.jit_free(jo)
+        engine.free_gen(gh)
+        engine.free(prog)

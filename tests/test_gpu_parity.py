@@ -44,7 +44,7 @@ def test_vmtests_replay_on_gpu(engine):
     """Concrete replay programs of every covered VMTests vector, evaluated on the GPU,
     reproduce the expected post-state storage words."""
     cases = vmtest_cases()
-    assert len(cases) >= 390
+    assert len(cases) == 429  # every non-ignored vector with a post-state (helpers.VMTEST_REFUSED)
     checked = 0
     for name, v, r in cases:
         keys = [int(k, 16) for k in v["post_storage"]]
@@ -52,7 +52,8 @@ def test_vmtests_replay_on_gpu(engine):
             continue
         words = [r.storage_word(k).raw for k in keys]
         truth = T.BoolVal(True)
-        P = ssa.flatten([truth] + [T.eq(w, w) for w in words])
+        # the path constraints of followed jumps are the query: they must hold (verdict 1)
+        P = ssa.flatten([truth] + list(r.path) + [T.eq(w, w) for w in words])
         P.set_watch([P.term_node[w.id] for w in words])
         scal, arrs = replay_assignment(v)
         assign = []
@@ -82,6 +83,25 @@ def test_vmtests_replay_on_gpu(engine):
             assert val == int(x, 16), (name, k)
             checked += 1
     assert checked >= 390
+
+
+def test_vmtests_jumps_followed_on_gpu(engine):
+    """The vectors whose jumps depend on calldata (DynamicJump_value*, TestNameRegistrator), followed
+    through the product path: ``replay.engine_follow`` evaluates every decision on the GPU, and the
+    replay takes the same branches and keeps the same path constraints as with the oracle."""
+    from mythril_amd.replay import engine_follow, replay
+
+    n = 0
+    for name, v, r in vmtest_cases():
+        if not r.path:
+            continue
+        scal, arrs = replay_assignment(v)
+        pre = {int(k, 16): int(x, 16) for k, x in v["pre_storage"].items()}
+        r2 = replay(v["code"], bytes.fromhex(v["data"]), pre, follow=engine_follow(engine, scal, arrs))
+        assert [T.to_sexpr(t) for t in r2.path] == [T.to_sexpr(t) for t in r.path], name
+        assert r2.halted == r.halted
+        n += 1
+    assert n >= 4
 
 
 @pytest.mark.parametrize("op", ["shl", "shr", "sar"])

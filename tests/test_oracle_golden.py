@@ -42,8 +42,11 @@ def test_eip145_vectors(op):
 
 
 def test_vmtests_post_storage():
+    """Every VMTests vector with a post-state (429: the reference's non-ignored set) replays to its
+    expected storage words; input-dependent jumps followed along the concrete path leave path
+    constraints that hold for the vector's inputs."""
     cases = vmtest_cases()
-    assert len(cases) >= 390
+    assert len(cases) == 429
     dirs = {}
     for name, v, r in cases:
         from mythril_amd.replay import replay_assignment
@@ -52,6 +55,8 @@ def test_vmtests_post_storage():
         m = OracleModel(scal, arrs)
         for k, x in v["post_storage"].items():
             assert evaluate(r.storage_word(int(k, 16)).raw, m) == int(x, 16), (name, k)
+        for c in r.path:
+            assert evaluate(c, m) == 1, name
         dirs[v["dir"]] = dirs.get(v["dir"], 0) + 1
     # every arithmetic / bitwise / sha3 vector with a post-state is covered
     assert dirs["vmArithmeticTest"] >= 190

@@ -125,3 +125,37 @@ def test_literal_tail_keys_are_narrowed():
         for prog in (spec, wide):
             got = kops.verdicts(prog, soa, [c.width for c in P.coords], N)
             assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("name", sorted(workloads.WORKLOADS))
+def test_asm_tier_assembles_on_host(name):
+    """The JIT's first tier (jit_asm.cpp) for every workload inside it: the emitted gfx950 assembly
+    (mgj_search + mgj_gen) assembles and links through comgr on the host.  Workloads outside it
+    (UMUL_NOOVF; Keccak, EXP, SDIV) are refused with MG_E_UNSUPPORTED, never miscompiled."""
+    roots = [c.raw for c in workloads.WORKLOADS[name]()]
+    P, blob = search.prepare(roots)
+    if name in ("bectoken_batch_overflow", "sha3_keyed_mapping"):
+        with pytest.raises(native.EngineUnsupported):
+            native.jit_asm(P.to_bytes(), blob)
+        return
+    src = native.jit_asm(P.to_bytes(), blob, compile=True)
+    assert src.startswith("; mythgpu-asm") and "mgj_search:" in src and "mgj_gen:" in src
+    # results leave through vector memory only: the only scalar-memory instructions are the
+    # kernel-argument loads
+    smem = [ln.split()[0] for ln in src.splitlines() if ln.strip().startswith("s_") and ("[0:1]" in ln)]
+    assert set(smem) <= {"s_load_dwordx2", "s_load_dwordx8", "s_load_dwordx4", "s_load_dword"}
+
+
+def test_asm_tier_random_programs_assemble_on_host():
+    """Random programs over the tier's operators (tests/test_gpu_asm.py) emit and assemble on the host."""
+    from tests.test_gpu_asm import _random_program
+
+    ok = 0
+    for seed in range(24):
+        P, blob = search.prepare(_random_program(1000 + seed))
+        try:
+            native.jit_asm(P.to_bytes(), blob, compile=True)
+            ok += 1
+        except native.EngineUnsupported:
+            pass
+    assert ok >= 20
