@@ -207,6 +207,37 @@ def main():
     dt = float(dt_t.item())
     kernel_ms = float(km_t.item())
 
+    # the JIT's first tier (gfx950 assembly emitted by the engine, jit_asm.cpp): its cold compile (comgr's
+    # cache off) and its rate at 2^28 candidates per launch on this workload; the product runs it from a
+    # few ms after a query's first miss until the O3 kernel above is ready
+    asm_tier = None
+    if rank == 0 and args.engine == "jit" and not args.no_ttfm:
+        prev_cc = os.environ.get("AMD_COMGR_CACHE")
+        os.environ["AMD_COMGR_CACHE"] = "0"
+        t1 = time.perf_counter()
+        try:
+            ja = eng.jit_compile(prog, gh, asm=True)
+            asm_tier = {"compile_ms_cold": (time.perf_counter() - t1) * 1e3}
+        except native.EngineUnsupported as e:
+            ja, asm_tier = None, {"unsupported": str(e)}
+        if prev_cc is None:
+            os.environ.pop("AMD_COMGR_CACHE")
+        else:
+            os.environ["AMD_COMGR_CACHE"] = prev_cc
+        if ja is not None:
+            na = 1 << 28
+            eng.jit_search(ja, args.seed, 0, na, early_exit=False)
+            eng.reset_stats()
+            for s_ in range(4):
+                eng.jit_search(ja, args.seed, (s_ + 1) * na, na, early_exit=False)
+            st_a = eng.stats()
+            km_a = st_a.kernel_ms_total / max(st_a.launches, 1)
+            o3 = eng.jit_search(jit, args.seed, na, na, early_exit=False) if jit is not None else None
+            asm_tier.update({"candidates_per_launch": na, "kernel_ms": km_a, "candidates_per_s": na / (km_a * 1e-3),
+                             "agrees_with_o3_on_a_launch": o3 == eng.jit_search(ja, args.seed, na, na,
+                                                                                early_exit=False)})
+            eng.jit_free(ja)
+
     # time to first model (early-exit search from index 0 + model read-back), rank 0 only
     ttfm_ms = None
     ttfm_breakdown = None
@@ -371,6 +402,7 @@ def main():
             "first_model_index": ttfm_index,
             "time_to_first_model_hard_ms": None if hard is None else hard["cold_ms"],
             "time_to_first_model_hard": hard,
+            "jit_asm_tier": asm_tier,
             "hits_in_timed_region": int(total_hits),
             "hit_rate_in_timed_region": total_hits / total,
             "dropin_stream": stream,

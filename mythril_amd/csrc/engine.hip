@@ -49,6 +49,22 @@ constexpr size_t kCaptureBytes = 64ull << 20;  // watch-row capture buffer (mg_s
 // adds on one address serialised there; the host sums the stripes.
 constexpr uint32_t kHitStripes = 16, kHitStride = 16;
 constexpr uint32_t kHitWords = kHitStride * (1 + kHitStripes);
+// After them (never armed, never read back) the device's peer line: [0] n, [1 + k] the hit word of
+// the k-th device whose slice lies above this one's (in-process multi-device searches).  A wave
+// that publishes an early-exit first hit also lowers those words, so their waves, all above the
+// hit, stop at their next group boundary instead of sweeping to the end of their slice (the host
+// min over the devices is unchanged: the lowest hit is in this device's own word).  Written by
+// mg_init; jit.cpp and jit_asm.cpp read it at the same offset (kPeerWord, 2,176 B).
+constexpr uint32_t kPeerWord = kHitWords, kPeerMax = 15;
+constexpr uint32_t kHitAlloc = kHitWords + 1 + kPeerMax;
+static_assert(kPeerWord == 272, "jit.cpp / jit_asm.cpp hard-code the peer line at 2,176 B");
+
+// an early-exit first hit to the devices above this one (the peer line)
+__device__ __forceinline__ void publish_peers(unsigned long long* hit, unsigned long long v) {
+  const unsigned long long* t = hit + kPeerWord;
+  const uint32_t np = (uint32_t)t[0];
+  for (uint32_t q = 0; q < np && q < kPeerMax; q++) atomicMin((unsigned long long*)t[1 + q], v);
+}
 
 static uint32_t lds_words_max() {
   static const uint32_t n = [] {
@@ -694,7 +710,10 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
         wave_hits += (uint64_t)__popcll(m);
         if (first < wave_best) {
           wave_best = first;
-          if (early && threadIdx.x == 0) atomicMin(k.first_hit, (unsigned long long)first);
+          if (early && threadIdx.x == 0) {
+            atomicMin(k.first_hit, (unsigned long long)first);
+            publish_peers(k.first_hit, (unsigned long long)first);
+          }
         }
       }
     } else if (active) {
@@ -1251,7 +1270,8 @@ static int init_dev(Engine& e, int dev) {
   HIPCHK(hipEventCreate(&e.ev0));
   HIPCHK(hipEventCreate(&e.ev1));
   HIPCHK(hipEventCreateWithFlags(&e.ev2, hipEventDisableTiming));
-  HIPCHK(hipMalloc((void**)&e.d_hit, kHitWords * sizeof(unsigned long long)));
+  HIPCHK(hipMalloc((void**)&e.d_hit, kHitAlloc * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(e.d_hit + kPeerWord, 0, (1 + kPeerMax) * sizeof(unsigned long long)));  // no peers
   HIPCHK(hipHostMalloc((void**)&e.h_hit, 2 * kHitWords * sizeof(unsigned long long), hipHostMallocDefault));
   std::memset(e.h_hit, 0, 2 * kHitWords * sizeof(unsigned long long));
   e.h_hit[0] = ~0ull;  // the armed image (arm_hits)
@@ -1313,6 +1333,32 @@ int mg_init(uint32_t device_mask) {
       return set_err(rc, "mg_init: device " + std::to_string(devs[i]) + ": " + why);
     }
     g_devs.push_back(s2);
+  }
+  // peer lines: device d stops devices d+1.. (their slices lie above its own).  Distinct physical
+  // devices need peer access (xGMI); where it cannot be enabled, that pair simply does not stop early
+  if (g_devs.size() > 1) {
+    for (size_t d = 0; d < g_devs.size(); d++) {
+      std::vector<unsigned long long> line(1 + kPeerMax, 0ull);
+      uint32_t np = 0;
+      for (size_t q = d + 1; q < g_devs.size() && np < kPeerMax; q++) {
+        const int a = g_devs[d]->device, b = g_devs[q]->device;
+        if (a != b) {
+          int can = 0;
+          if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) continue;
+          (void)hipSetDevice(a);
+          const hipError_t pe = hipDeviceEnablePeerAccess(b, 0);
+          if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) {
+            (void)hipGetLastError();
+            continue;
+          }
+        }
+        line[1 + np++] = (unsigned long long)(uintptr_t)g_devs[q]->d_hit;
+      }
+      line[0] = np;
+      HIPCHK(hipSetDevice(g_devs[d]->device));
+      HIPCHK(hipMemcpy(g_devs[d]->d_hit + kPeerWord, line.data(), line.size() * sizeof(unsigned long long),
+                       hipMemcpyHostToDevice));
+    }
   }
   HIPCHK(hipSetDevice(e.device));
   e.stats.n_devices = (uint32_t)g_devs.size();

@@ -1126,8 +1126,13 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "      wave_hits += (uint64_t)__popcll(m);\n"
        "      if (first < wave_best) {\n"
        "        wave_best = first;\n"
-       "        // publish at once when waves stop early on it; else once per wave at the end\n"
-       "        if (early && lane == 0u) atomicMin(hit, (unsigned long long)first);\n"
+       "        // publish at once when waves stop early on it (and to the devices whose slices lie above\n"
+       "        // this one's: the peer line at hit + 272, engine.hip kPeerWord); else once per wave at the end\n"
+       "        if (early && lane == 0u) {\n"
+       "          atomicMin(hit, (unsigned long long)first);\n"
+       "          const uint32_t np = (uint32_t)hit[272];\n"
+       "          for (uint32_t q = 0u; q < np && q < 15u; q++) atomicMin((unsigned long long*)hit[273u + q], (unsigned long long)first);\n"
+       "        }\n"
        "      }\n"
        "    } }\n"
        "  }\n"

@@ -1926,6 +1926,33 @@ struct Gen {
       E.valu("v_mov_b32_e32 v8, s46", {46});
       E.valu("v_mov_b32_e32 v9, s47", {47});
       E.mem("global_atomic_umin_x2 v6, v[8:9], s[16:17]", {16, 17});
+      // ... and to the devices whose slices lie above this one's: the peer line after the hit
+      // buffer (engine.hip kPeerWord: [272] count, [273 + k] their hit words)
+      {
+        const std::string ploop = E.newlab(), pdone = E.newlab();
+        E.mem("global_load_dwordx2 v[8:9], v6, s[16:17] offset:2176", {16, 17});
+        E.ctl("s_waitcnt vmcnt(0)");
+        E.valu("v_readfirstlane_b32 s48, v8", {}, {48});
+        E.salu("s_min_u32 s48, s48, 15", {48});
+        E.salu("s_cmp_eq_u32 s48, 0");
+        E.ctl("s_cbranch_scc1 " + pdone);
+        E.salu("s_mov_b32 s49, 0", {49});
+        E.label(ploop);
+        E.salu("s_lshl_b32 s52, s49, 3", {52});
+        E.salu("s_add_u32 s52, s52, 0x888", {52});  // 2,184 B: the first peer pointer
+        E.valu("v_mov_b32_e32 v7, s52", {52});
+        E.mem("global_load_dwordx2 v[8:9], v7, s[16:17]", {16, 17});
+        E.ctl("s_waitcnt vmcnt(0)");
+        E.valu("v_readfirstlane_b32 s50, v8", {}, {50});
+        E.valu("v_readfirstlane_b32 s51, v9", {}, {51});
+        E.valu("v_mov_b32_e32 v8, s46", {46});
+        E.valu("v_mov_b32_e32 v9, s47", {47});
+        E.mem("global_atomic_umin_x2 v6, v[8:9], s[50:51]", {50, 51});
+        E.salu("s_add_u32 s49, s49, 1", {49});
+        E.salu("s_cmp_lt_u32 s49, s48");
+        E.ctl("s_cbranch_scc1 " + ploop);
+        E.label(pdone);
+      }
       E.salu("s_mov_b64 exec, -1");
     }
     E.label(cont);
@@ -1959,7 +1986,7 @@ struct Gen {
     }
     E.ctl("s_endpgm");
     // descriptor
-    const int nv = std::max(E.vhigh, kV0), ns = std::max(E.shigh, 52);
+    const int nv = std::max(E.vhigh, kV0), ns = std::max(E.shigh, 56);
     const int accum = (nv + 3) / 4 * 4;
     o << "  .section .rodata,\"a\",@progbits\n  .p2align 6, 0x0\n  .amdhsa_kernel " << name << "\n"
       << "    .amdhsa_group_segment_fixed_size 0\n    .amdhsa_private_segment_fixed_size 0\n"

@@ -107,3 +107,70 @@ def test_time_to_first_model_at_four_devices(engine):
         engine.reinit(old_mask)
     assert i1 == i4 and len(i1) == 1
     assert t4 <= 1.10 * t1 + 50e-6, (t1, t4)
+
+
+def test_multidevice_stops_at_first_hit(engine):
+    """A mid-range needle (~2^-20) whose first hit lies in slice 0 of a 2^24 launch split over four
+    devices: the wave that finds it lowers the hit words of the devices above (engine.hip peer
+    line), so their waves stop at the next group instead of sweeping their whole slice.  Same index
+    as one device, on the O3 kernel, the first tier and the interpreter; the split launch's time
+    stays within 1.1x of one device's plus the three extra launches (25 us each)."""
+    import statistics
+    import time
+
+    from mythril_amd.smt import Extract, symbol_factory
+
+    x = symbol_factory.BitVecSym("md_needle_x", 256)
+    k = symbol_factory.BitVecVal(0x9E3779B97F4A7C15F39CC0605CEDC835, 256)
+    roots = [(Extract(19, 0, x * k) == symbol_factory.BitVecVal(0x5A5A5, 20)).raw]
+    P, blob = search.prepare(roots)
+    n = 1 << 24
+
+    def kernels():
+        prog = engine.load(P.to_bytes())
+        gh = engine.load_gen(prog, blob)
+        return prog, gh, {"o3": engine.jit_compile(prog, gh), "asm": engine.jit_compile(prog, gh, asm=True)}
+
+    def timed(fn, reps=15):
+        fn()
+        ts = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            r = fn()
+            ts.append(time.perf_counter() - t)
+        return statistics.median(ts), r
+
+    prog, gh, ks = kernels()
+    try:
+        seed = next(s for s in range(200)
+                    if (1 << 20) <= (engine.jit_search(ks["o3"], s, 0, n, early_exit=True)[0] or n) < (1 << 22))
+        one = {name: timed(lambda j=j: engine.jit_search(j, seed, 0, n, early_exit=True)[0]) for name, j in ks.items()}
+        one["interp"] = timed(lambda: engine.search(prog, gh, seed, 0, n, early_exit=True)[0], reps=5)
+    finally:
+        for j in ks.values():
+            engine.jit_free(j)
+        engine.free_gen(gh)
+        engine.free(prog)
+    old_mask = engine.mask
+    try:
+        os.environ["MYTHGPU_VIRTUAL_DEVICES"] = "4"
+        engine.reinit(1 << engine.device)
+        assert engine.n_devices == 4
+        prog, gh, ks = kernels()
+        try:
+            four = {name: timed(lambda j=j: engine.jit_search(j, seed, 0, n, early_exit=True)[0])
+                    for name, j in ks.items()}
+            four["interp"] = timed(lambda: engine.search(prog, gh, seed, 0, n, early_exit=True)[0], reps=5)
+        finally:
+            for j in ks.values():
+                engine.jit_free(j)
+            engine.free_gen(gh)
+            engine.free(prog)
+    finally:
+        os.environ.pop("MYTHGPU_VIRTUAL_DEVICES", None)
+        engine.reinit(old_mask)
+    for name in one:
+        (t1, i1), (t4, i4) = one[name], four[name]
+        assert i1 == i4 and i1 < (1 << 22), (name, i1, i4)
+        if name != "interp":
+            assert t4 <= 1.10 * t1 + 3 * 25e-6, (name, t1, t4)
