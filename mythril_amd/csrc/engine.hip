@@ -922,9 +922,12 @@ struct Engine {
   // searches keep launching while a query's kernel compiles (mg_jit_compile_async).  `jit_mu`
   // guards the members below; lock order: mu before jit_mu.
   std::mutex jit_mu;
-  bool jit_worker_running = false;  // detached thread; never outlives the (leaked) Engine
+  // two compile threads (detached; never outlive the leaked Engine), one per queue: [0] the O3
+  // kernels (clang + LLVM, ~140 ms), [1] the first tier (assembly, a few ms) — a first-tier request
+  // never waits behind an O3 compile, not even a cancelled one still in the compiler
+  int jit_workers = 0;
   bool jit_stop = false;
-  std::deque<std::shared_ptr<JitTicket>> jit_queue;
+  std::deque<std::shared_ptr<JitTicket>> jit_queue[2];
   std::unordered_map<uint64_t, std::shared_ptr<JitTicket>> tickets;
   std::condition_variable jit_cv, jit_done_cv;
   bool init = false;
@@ -1388,12 +1391,13 @@ void mg_shutdown(void) {
     // stop the compile thread (a compile in flight finishes first; its result is dropped)
     std::unique_lock<std::mutex> jl(e.jit_mu);
     e.jit_stop = true;
-    for (auto& t : e.jit_queue) t->cancelled = true;
+    for (auto& q : e.jit_queue)
+      for (auto& t : q) t->cancelled = true;
     for (auto& kv : e.tickets) kv.second->cancelled = true;
     e.jit_cv.notify_all();
-    e.jit_done_cv.wait(jl, [&] { return !e.jit_worker_running; });
+    e.jit_done_cv.wait(jl, [&] { return e.jit_workers == 0; });
     e.jit_stop = false;
-    e.jit_queue.clear();
+    for (auto& q : e.jit_queue) q.clear();
     for (auto& kv : e.tickets)
       if (kv.second->ready) release_jit(*kv.second->ready);
     e.tickets.clear();
@@ -2264,19 +2268,20 @@ static int load_jit(const std::vector<char>& code, const JitTicket& t, double co
   return MG_OK;
 }
 
-static void jit_worker_main(Engine* ep, int device) {
+static void jit_worker_main(Engine* ep, int device, int lane) {
   Engine& e = *ep;
   (void)hipSetDevice(device);
   std::unique_lock<std::mutex> lk(e.jit_mu);
+  auto& queue = e.jit_queue[lane];
   for (;;) {
-    e.jit_cv.wait(lk, [&] { return e.jit_stop || !e.jit_queue.empty(); });
+    e.jit_cv.wait(lk, [&] { return e.jit_stop || !queue.empty(); });
     if (e.jit_stop) {
-      e.jit_worker_running = false;
+      e.jit_workers--;
       e.jit_done_cv.notify_all();
       return;
     }
-    std::shared_ptr<JitTicket> t = e.jit_queue.front();
-    e.jit_queue.pop_front();
+    std::shared_ptr<JitTicket> t = queue.front();
+    queue.pop_front();
     if (t->cancelled) continue;
     lk.unlock();
     const auto t0 = std::chrono::steady_clock::now();
@@ -2386,10 +2391,11 @@ static void jit_atexit() {
   Engine& e = E();
   std::unique_lock<std::mutex> jl(e.jit_mu);
   e.jit_stop = true;
-  for (auto& t : e.jit_queue) t->cancelled = true;
+  for (auto& q : e.jit_queue)
+    for (auto& t : q) t->cancelled = true;
   for (auto& kv : e.tickets) kv.second->cancelled = true;
   e.jit_cv.notify_all();
-  e.jit_done_cv.wait_for(jl, std::chrono::seconds(10), [&] { return !e.jit_worker_running; });
+  e.jit_done_cv.wait_for(jl, std::chrono::seconds(10), [&] { return e.jit_workers == 0; });
 }
 
 // caller holds e.mu
@@ -2416,19 +2422,19 @@ static int submit_jit(Engine& e, uint64_t prog, uint64_t gen, uint32_t flags, ui
   }
   const uint64_t h = e.next_handle++;
   std::lock_guard<std::mutex> jl(e.jit_mu);
-  if (!e.jit_worker_running) {
+  if (e.jit_workers == 0) {
     static std::once_flag once;
     std::call_once(once, [] {
       jit_compiler_preload();
       std::atexit(jit_atexit);
     });
     if (const char* c = getenv("MYTHGPU_JIT_CACHE")) e.code_cache.cap = std::max(1, atoi(c));
-    std::thread(jit_worker_main, &e, e.device).detach();
-    e.jit_worker_running = true;
+    for (int lane = 0; lane < 2; lane++) std::thread(jit_worker_main, &e, e.device, lane).detach();
+    e.jit_workers = 2;
   }
   e.tickets[h] = t;
-  e.jit_queue.push_back(t);
-  e.jit_cv.notify_one();
+  e.jit_queue[(flags & MG_JIT_ASM) ? 1 : 0].push_back(t);
+  e.jit_cv.notify_all();
   *ticket = h;
   return MG_OK;
 }

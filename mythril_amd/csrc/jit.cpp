@@ -1566,9 +1566,11 @@ struct Helper {
   std::string why;
 };
 
-Helper& helper() {
-  static Helper* h = new Helper;  // leaked: usable from exit handlers
-  return *h;
+// two helper processes: [0] compiles (clang + LLVM), [1] assembles the first tier — an assembly
+// request never queues behind a ~140 ms compile in the other
+Helper& helper(int lane = 0) {
+  static Helper* h[2] = {new Helper, new Helper};  // leaked: usable from exit handlers
+  return *h[lane & 1];
 }
 
 bool send_all(int fd, const void* p, size_t n) {
@@ -1664,7 +1666,7 @@ std::string env_snapshot() {
 }
 
 int helper_compile(const std::string& src, std::vector<char>& code, std::string& log, bool& available) {
-  Helper& h = helper();
+  Helper& h = helper(src.compare(0, std::strlen(kAsmMarker), kAsmMarker) == 0 ? 1 : 0);
   std::lock_guard<std::mutex> g(h.mu);
   available = true;
   if (h.dead) {
@@ -1701,16 +1703,18 @@ int helper_compile(const std::string& src, std::vector<char>& code, std::string&
 }  // namespace
 
 void jit_helper_stop() {
-  Helper& h = helper();
-  std::lock_guard<std::mutex> g(h.mu);
-  if (h.fd >= 0) {
-    close(h.fd);  // the helper exits on end of input
-    h.fd = -1;
-  }
-  if (h.pid > 0) {
-    int status;
-    (void)waitpid(h.pid, &status, 0);
-    h.pid = -1;
+  for (int lane = 0; lane < 2; lane++) {
+    Helper& h = helper(lane);
+    std::lock_guard<std::mutex> g(h.mu);
+    if (h.fd >= 0) {
+      close(h.fd);  // the helper exits on end of input
+      h.fd = -1;
+    }
+    if (h.pid > 0) {
+      int status;
+      (void)waitpid(h.pid, &status, 0);
+      h.pid = -1;
+    }
   }
 }
 

@@ -112,6 +112,7 @@ class Emitter {
   std::map<int, int64_t> vw;  // SGPR -> position of its last VALU write
   int nlab = 0;
   std::vector<int> vref = std::vector<int>(256, 0);
+  int vfirst = kV0;  // the allocator's first VGPR: below it the fixed registers and the literal pool
   int vhigh = kV0;
   std::vector<int> sref = std::vector<int>(kS1, 0);
   int shigh = kS0;
@@ -160,7 +161,7 @@ class Emitter {
 
   // --- VGPRs ---------------------------------------------------------------------------------
   uint32_t valloc() {
-    for (int r = kV0; r < 256; r++)
+    for (int r = vfirst; r < 256; r++)
       if (!vref[r]) {
         vref[r] = 1;
         vhigh = std::max(vhigh, r + 1);
@@ -169,10 +170,10 @@ class Emitter {
     fail("out of VGPRs");
   }
   void retain(const Limb& l) {
-    if (l.reg() && (int)l.v >= kV0) vref[l.v]++;
+    if (l.reg() && (int)l.v >= vfirst) vref[l.v]++;
   }
   void release(const Limb& l) {
-    if (l.reg() && (int)l.v >= kV0) {
+    if (l.reg() && (int)l.v >= vfirst) {
       if (--vref[l.v] < 0) fail("internal: VGPR released twice");
     }
   }
@@ -352,10 +353,21 @@ struct Gen {
       E.retain(l);
       return l;
     }
+    const uint32_t x = l.lit() ? l.v : 0u;
+    if (x == 0) return Reg(6);  // the zero register
+    auto it = pool.find(x);
+    if (it != pool.end()) return Reg((uint32_t)it->second);  // loaded once, before the group loop
+    census[x]++;
     const uint32_t r = E.valloc();
-    E.valu("v_mov_b32_e32 " + V(r) + ", " + imm(l.lit() ? l.v : 0u));
+    E.valu("v_mov_b32_e32 " + V(r) + ", " + imm(x));
     return Reg(r);
   }
+  // Literal pool: literals a VGPR operand needs (select arms, carry-chain operands, dictionary
+  // entries) are moved into a VGPR at every use unless pooled — one VGPR each, loaded once per
+  // kernel before the group loop.  jit_asm_source emits twice: the first pass counts (census), the
+  // second pools the most used ones within the VGPR budget.
+  std::map<uint32_t, int> pool;        // literal -> its VGPR
+  std::map<uint32_t, uint32_t> census; // literal -> materialisations in the last emission
   std::string src(const Limb& l) const {
     if (l.k == LU) fail("internal: a limb the demand analysis dropped was read");
     return l.lit() ? imm(l.v) : V(l.v);
@@ -816,8 +828,8 @@ struct Gen {
   // jit.cpp, engine.hip and oracle/bveval.c)
   // ---------------------------------------------------------------------------------------
   // per-lane hash grnd(c, j) into a fresh VGPR
-  Limb grnd(uint32_t c, uint32_t j) {
-    const Limb d = fresh(), t = fresh();
+  Limb grnd(uint32_t c, uint32_t j, const Limb* into = nullptr) {
+    const Limb d = into ? *into : fresh(), t = fresh();
     E.valu("v_xor_b32_e32 " + V(d.v) + ", " + imm(gsalt(c, j)) + ", v4");
     E.valu("v_xor_b32_sdwa " + V(d.v) + ", " + V(d.v) + ", " + V(d.v) +
            " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1");
@@ -834,8 +846,29 @@ struct Gen {
     E.salu("s_add_u32 " + S(s) + ", " + S(s) + ", s37", {s});
   }
   // UNIFORM raw limbs masked to `bits`
-  std::vector<Limb> uniform_limbs(uint32_t c, uint32_t Lc, uint32_t bits) {
+  // tgt (MIXED branches): the coordinate's output registers, written directly (put then moves nothing)
+  std::vector<Limb> uniform_limbs(uint32_t c, uint32_t Lc, uint32_t bits, const std::vector<Limb>* tgt = nullptr) {
     const uint32_t n = std::min(Lc, (bits + 31) / 32);
+    if (tgt) {
+      std::vector<Limb> r(*tgt);
+      for (uint32_t j = 0; j < n; j++) {
+        if (j < 2) {
+          grnd(c, j, &r[j]);
+        } else {
+          const uint32_t s = (7u * j + 3u) % 31u + 1u;
+          E.valu("v_alignbit_b32 " + V(r[j].v) + ", " + V(r[j - 1].v) + ", " + V(r[j - 2].v) + ", " + std::to_string(s));
+          E.valu("v_add_u32_e32 " + V(r[j].v) + ", " + V(r[j - 2].v) + ", " + V(r[j].v));
+        }
+      }
+      // the raw chain is complete: mask the top limb in place, zero the limbs above
+      for (uint32_t j = 0; j < Lc; j++) {
+        const uint32_t lo = 32 * j;
+        const uint32_t m = lo >= bits ? 0u : (bits - lo >= 32 ? 0xFFFFFFFFu : ((1u << (bits - lo)) - 1u));
+        if (j >= n || m == 0) E.valu("v_mov_b32_e32 " + V(r[j].v) + ", 0");
+        else if (m != 0xFFFFFFFFu) E.valu("v_and_b32_e32 " + V(r[j].v) + ", " + imm(m) + ", " + V(r[j].v));
+      }
+      return r;
+    }
     std::vector<Limb> u(n);
     for (uint32_t j = 0; j < n; j++) {
       if (j < 2) {
@@ -901,14 +934,15 @@ struct Gen {
   }
 
   // dictionary entry `idx` (VGPR) of the n-entry table at G[off] (width w)
-  std::vector<Limb> dict(uint32_t off, uint32_t n, uint32_t w, const Limb& idx) {
+  std::vector<Limb> dict(uint32_t off, uint32_t n, uint32_t w, const Limb& idx, const std::vector<Limb>* tgt = nullptr) {
     const uint32_t Lc = Lw(w);
     std::vector<Limb> r(Lc, Lit(0));
+    auto dst = [&](uint32_t j) { return tgt ? (*tgt)[j] : fresh(); };
     if (w <= 32 && n && (uint64_t)n * w <= 32) {  // packed in one literal: one bit-field extract
       uint32_t pack = 0;
       const uint32_t m = w == 32 ? 0xFFFFFFFFu : ((1u << w) - 1u);
       for (uint32_t e2 = 0; e2 < n; e2++) pack |= (G[off + e2] & m) << (e2 * w);
-      const Limb sh = fresh(), d = fresh();
+      const Limb sh = fresh(), d = dst(0);
       E.valu("v_mul_u32_u24_e32 " + V(sh.v) + ", " + imm(w) + ", " + V(idx.v));
       E.salu("s_mov_b32 s41, " + hexs(pack), {41});
       E.valu("v_bfe_u32 " + V(d.v) + ", s41, " + V(sh.v) + ", " + std::to_string(w), {41});
@@ -937,7 +971,7 @@ struct Gen {
           const uint32_t lv = G[off + e2 * Lc + j];
           // lanes whose index is not e2 keep cur (src1), the others take the literal (src0)
           const Limb lvr = inl(lv) ? Lit(lv) : vreg(Lit(lv));  // VCC already uses the constant bus
-          const Limb d = fresh();
+          const Limb d = e2 == 0 ? dst(j) : fresh();
           E.valu("v_cndmask_b32_e64 " + V(d.v) + ", " + src(lvr) + ", " + V(cur.v) + ", " + SP(ms[e2].s),
                  {ms[e2].s, ms[e2].s + 1});
           drop(lvr);
@@ -961,7 +995,7 @@ struct Gen {
         continue;
       }
       const uint32_t byte = (off + j) * 4;
-      const Limb d = fresh();
+      const Limb d = dst(j);
       if (byte < 4096) {
         E.mem("global_load_dword " + V(d.v) + ", " + V(vo.v) + ", s[4:5] offset:" + std::to_string(byte));
       } else {
@@ -991,7 +1025,8 @@ struct Gen {
   void put(const std::vector<Limb>& out, std::vector<Limb>& r) {
     for (size_t j = 0; j < out.size(); j++) {
       const Limb x = j < r.size() ? r[j] : Lit(0);
-      if (!(x == out[j])) E.valu("v_mov_b32_e32 " + V(out[j].v) + ", " + src(x));
+      if (x == out[j]) continue;  // written in place (tgt): not a reference of its own
+      E.valu("v_mov_b32_e32 " + V(out[j].v) + ", " + src(x));
       if (j < r.size()) drop(r[j]);
     }
     r.clear();
@@ -1039,12 +1074,69 @@ struct Gen {
   }
 
   // mask to the width and the clamp record (MIXED: per branch, in place on out)
-  void finish(const std::vector<Limb>& out, uint32_t width, uint32_t clamp) {
+  // zero: limbs of out this branch knows to be zero (bit j = limb j)
+  void finish(const std::vector<Limb>& out, uint32_t width, uint32_t clamp, uint64_t zero = 0) {
     const uint32_t Lc = (uint32_t)out.size();
-    if (width & 31) E.valu("v_and_b32_e32 " + V(out[Lc - 1].v) + ", " + imm(topmask(width)) + ", " + V(out[Lc - 1].v));
+    if ((width & 31) && !(zero >> (Lc - 1) & 1))
+      E.valu("v_and_b32_e32 " + V(out[Lc - 1].v) + ", " + imm(topmask(width)) + ", " + V(out[Lc - 1].v));
     if (!clamp) return;
     const uint32_t r = clamp - 1;
     const uint32_t span = G[r + Lc];
+    bool lo_hi_zero = true;
+    for (uint32_t j = 1; j < Lc; j++) lo_hi_zero = lo_hi_zero && G[r + j] == 0;
+    if (lo_hi_zero && (span ? (uint64_t)G[r] + span <= (1ull << 32) : G[r] == 0)) {
+      // lo < 2^32 and lo + span <= 2^32: in range iff the high limbs are zero and v0 - lo0 < span
+      // (mod 2^32: a v0 below lo0 wraps to at least 2^32 - lo0 >= span) — no borrow chain
+      std::vector<std::pair<Limb, Limb>> hz;
+      for (uint32_t j = 1; j < Lc; j++)
+        if (!(zero >> j & 1)) hz.push_back({out[j], Lit(0)});
+      Mask bad;
+      bad.k = 1;
+      bad.ones = false;
+      if (!hz.empty()) {
+        const Mask z = eq_mask(hz);
+        bad = mnot(z);
+        E.srelease(z);
+      }
+      if (span) {
+        Mask ge;
+        ge.k = 2;
+        ge.s = E.salloc();
+        Limb d0 = out[0];
+        if (G[r]) {
+          d0 = fresh();
+          E.valu("v_subrev_u32_e32 " + V(d0.v) + ", " + imm(G[r]) + ", " + V(out[0].v));
+        }
+        if (inl(span)) {
+          E.valu("v_cmp_le_u32_e64 " + SP(ge.s) + ", " + imm(span) + ", " + V(d0.v), {}, {ge.s, ge.s + 1});
+        } else {
+          E.salu("s_mov_b32 s41, " + hexs(span), {41});
+          E.valu("v_cmp_le_u32_e64 " + SP(ge.s) + ", s41, " + V(d0.v), {41}, {ge.s, ge.s + 1});
+        }
+        if (G[r]) drop(d0);
+        const Mask b2 = mop("or", bad, ge);
+        E.srelease(ge);
+        E.srelease(bad);
+        bad = b2;
+      }
+      if (bad.k == 1 && !bad.ones) return;
+      // clamped: lo0 + (span ? mulhi(v0, span) : v0) in limb 0 (no carry: below 2^32), zeros above
+      Limb c0;
+      if (span) {
+        c0 = mulhi_lit(out[0], span);
+        if (G[r]) E.valu("v_add_u32_e32 " + V(c0.v) + ", " + imm(G[r]) + ", " + V(c0.v));
+      }
+      mask_to_vcc(bad);
+      if (span) {
+        E.valu("v_cndmask_b32_e32 " + V(out[0].v) + ", " + V(out[0].v) + ", " + V(c0.v) + ", vcc", {kVCC, kVCC + 1});
+        drop(c0);
+      }
+      for (uint32_t j = 1; j < Lc; j++)
+        if (!(zero >> j & 1))
+          E.valu("v_cndmask_b32_e32 " + V(out[j].v) + ", " + V(out[j].v) + ", v6, vcc", {kVCC, kVCC + 1});
+      E.srelease(bad);
+      return;
+    }
     const uint32_t k = reach_limbs(&G[r], Lc, span ? span - 1u : 0xFFFFFFFFull, 0);
     // in range: v - lo has no borrow, high limbs zero and low limb < span (span 0: 2^32)
     std::vector<Limb> v(out.begin(), out.end()), lo(Lc);
@@ -1161,7 +1253,7 @@ struct Gen {
             u[0] = and_lit(h, m & 0xFFFFu);
             drop(h);
           } else {
-            u = uniform_limbs(c, Lc, bitsn);
+            u = uniform_limbs(c, Lc, bitsn, &out);
           }
           put(out, u);
         };
@@ -1189,38 +1281,51 @@ struct Gen {
           } else {
             s = gen_value(sp.p[3]);
           }
+          uint64_t zero = 0;  // limbs the copied value has as literal zeros (a delta may change them)
+          for (uint32_t j = 0; j < Lc && !sp.p[5]; j++)
+            if (j < s.size() && s[j].lit() && s[j].v == 0) zero |= 1ull << j;
           put(out, s);
           if (sp.p[5]) delta(out, c, sp.p[5], ws, nullptr);
-          finish(out, width, sp.p[6]);
+          finish(out, width, sp.p[6], zero);
         }
         if (pd) {
           branch(pc + pd);
           const Limb h = grnd(c, 0xFFFFu);
           const Limb ix = dict_index(h, sp.p[1]);
-          std::vector<Limb> dv = dict(sp.p[0], sp.p[1], width, ix);
+          std::vector<Limb> dv = dict(sp.p[0], sp.p[1], width, ix, &out);
           drop(ix);
+          uint64_t zero = 0;  // limbs zero in every entry (a delta may change them)
+          for (uint32_t j = 0; j < Lc && !sp.p[5]; j++)
+            if (j < dv.size() && dv[j].lit() && dv[j].v == 0) zero |= 1ull << j;
           put(out, dv);
           if (sp.p[5]) delta(out, c, sp.p[5], ws, &h);
           drop(h);
-          finish(out, width, sp.p[6]);
+          finish(out, width, sp.p[6], zero);
         }
+        // limbs above `bitsn` are zero in the SMALL / UNIFORM values (narrow: everything above limb 0)
+        auto zeros = [&](uint32_t bitsn) {
+          uint64_t z = 0;
+          for (uint32_t j = 0; j < Lc; j++)
+            if ((narrow && j > 0) || 32 * j >= bitsn) z |= 1ull << j;
+          return z;
+        };
         if (ps) {
           branch(pc + pd + ps);
           uni(small_bits);
-          finish(out, width, sp.p[6]);
+          finish(out, width, sp.p[6], zeros(small_bits));
         }
         if (any) {
           E.ctl("s_branch " + end);
           E.label(next);
         }
         uni(width);
-        finish(out, width, sp.p[6]);
+        finish(out, width, sp.p[6], zeros(width));
         E.label(end);
         Mask wsm;
         wsm.k = 2;
         wsm.s = ws;
         E.srelease(wsm);
-        if (width & 31) E.valu("v_and_b32_e32 " + V(out[Lc - 1].v) + ", " + imm(topmask(width)) + ", " + V(out[Lc - 1].v));
+        // (every alternative masked its value to the width in finish)
         if (fix) fixbits(out, fix, true);
         return out;
       }
@@ -1783,6 +1888,9 @@ struct Gen {
   std::string kernel(const std::string& name) {
     E = Emitter();
     E.nlab = labels;
+    census.clear();
+    E.vfirst = kV0 + (int)pool.size();
+    E.vhigh = E.vfirst;
     val.assign(P.vwidth.size(), Val{});
     cval.clear();
     auto& o = E.o;
@@ -1822,6 +1930,7 @@ struct Gen {
     E.salu("s_lshl_b32 s28, s19, 2", {28});
     E.salu("s_mov_b64 s[30:31], -1", {30, 31});
     E.salu("s_mov_b64 s[32:33], 0", {32, 33});
+    for (const auto& kv : pool) E.valu("v_mov_b32_e32 " + V((uint32_t)kv.second) + ", " + imm(kv.first));
     // the lane half of the lane key: fmix64(lane ^ sk)
     E.valu("v_xor_b32_e32 v2, s12, v1", {12});
     E.valu("v_mov_b32_e32 v3, s13", {13});
@@ -1867,7 +1976,7 @@ struct Gen {
     E.valu("v_xor_b32_e32 v5, s37, v3", {37});
     E.salu("s_mov_b64 s[38:39], -1", {38, 39});
     body(next);
-    for (int r = kV0; r < 256; r++)
+    for (int r = E.vfirst; r < 256; r++)
       if (E.vref[r]) fail("internal: VGPR v" + std::to_string(r) + " still held after the body");
     E.label(next);
     // m = verdict, restricted to [start, end) in a partial group
@@ -2046,8 +2155,23 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
     g.analyse();
     std::ostringstream o;
     o << kAsmMarker << "\n  .amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"\n  .amdhsa_code_object_version 6\n";
+    // pass 1 counts the literals the kernel moves into VGPRs; pass 2 pools the most used ones, as long
+    // as the kernel stays within 96 VGPRs (5 waves per SIMD)
     g.gen_kernel = false;
-    o << g.kernel("mgj_search");
+    std::string ks = g.kernel("mgj_search");
+    if (!getenv("MYTHGPU_JIT_ASM_NOPOOL")) {
+      std::vector<std::pair<uint32_t, uint32_t>> by;  // (count, literal)
+      for (const auto& kv : g.census)
+        if (kv.second >= 2) by.push_back({kv.second, kv.first});
+      std::sort(by.begin(), by.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+      const int room = std::max(0, 96 - g.meta_vgpr["mgj_search"]);
+      for (size_t i = 0; i < by.size() && (int)i < room; i++) g.pool[by[i].second] = kV0 + (int)i;
+      if (!g.pool.empty()) {
+        g.labels = 0;
+        ks = g.kernel("mgj_search");
+      }
+    }
+    o << ks;
     const bool with_gen = (kernels & JIT_GEN) != 0;
     if (with_gen) {
       g.gen_kernel = true;
