@@ -75,8 +75,9 @@ def parse():
                     help="candidates per eval launch (HBM-resident SoA; C2: 1,241 B each)")
     ap.add_argument("--eval-only", action="store_true",
                     help="profiling pass: only the eval-kernel launches (tools/profile.sh eval)")
-    ap.add_argument("--engine", choices=["jit", "interp"], default="jit",
-                    help="jit: hipRTC-specialised search kernel; interp: the generic interpreter kernel")
+    ap.add_argument("--engine", choices=["jit", "asm", "interp"], default="jit",
+                    help="jit: the O3 query kernel (clang + LLVM through comgr); asm: the JIT's first tier "
+                         "(gfx950 assembly emitted by the engine); interp: the generic interpreter kernel")
     ap.add_argument("--pmc-dir", default=str(ROOT / "profiles"),
                     help="where tools/profile.sh summaries (pmc_<workload>*.json) are looked up by kernel SHA")
     return ap.parse_args()
@@ -152,6 +153,11 @@ def main():
     jit = None
     compile_ms = None
     sha = None
+    if args.engine == "asm":
+        sha = hashlib.sha256(native.jit_asm(P.to_bytes(), blob).encode()).hexdigest()[:16]
+        t1 = time.perf_counter()
+        jit = eng.jit_compile(prog, gh, asm=True)
+        compile_ms = (time.perf_counter() - t1) * 1e3
     if args.engine == "jit":
         sha = hashlib.sha256(native.jit_source(P.to_bytes(), blob).encode()).hexdigest()[:16]
         # cold compile: comgr's on-disk cache and the engine's code-object cache off, so a

@@ -2295,6 +2295,7 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
     } else {
       src = t->has_gen ? jit_source(t->low, &t->specs, &t->consts, kernels) : jit_source(t->low, nullptr, nullptr, kernels);
     }
+    const auto t_src = std::chrono::steady_clock::now();
     if (asm_rc != MG_OK) {
       lk.lock();
       t->rc = asm_rc;
@@ -2332,11 +2333,18 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
       compiled = rc == MG_OK;
     }
     std::string err;
+    const auto t_comp = std::chrono::steady_clock::now();
     if (rc != MG_OK) {
       err = "JIT compile failed: " + log.substr(0, 4000);
     } else if (!j) {
       double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       rc = load_jit(code, *t, ms, j);
+      if (getenv("MYTHGPU_JIT_TIMING")) {
+        auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        fprintf(stderr, "mythgpu jit worker (%s): source %.2f ms, compile %.2f ms, module load %.2f ms\n",
+                (t->flags & MG_JIT_ASM) ? "asm" : "o3", d(t0, t_src), d(t_src, t_comp),
+                d(t_comp, std::chrono::steady_clock::now()));
+      }
       if (rc != MG_OK && from_disk) {
         // a disk-cache entry that passes the header checks but does not load (a truncated write
         // renamed on a full disk, a runtime upgrade without a rebuild): drop it and compile once

@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 W=${1:-token_transfer_underflow}
 E=${2:-jit}
 N=${3:-268435456}
-if [ "$E" = "jit" ]; then D=gpurun_out/prof_$W; K=mgj_search; else D=gpurun_out/prof_${W}_$E; K=k_run; fi
+if [ "$E" = "jit" ]; then D=gpurun_out/prof_$W; K=mgj_search; elif [ "$E" = "asm" ]; then D=gpurun_out/prof_${W}_asm; K=mgj_search; else D=gpurun_out/prof_${W}_$E; K=k_run; fi
 rm -rf $D && mkdir -p $D
 B="python3 bench.py --workload $W --engine $E --candidates $N --no-cpu-baseline --no-ttfm --no-stream --no-eval"
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $D/trace -o run --output-format csv -- $B --steps 10 --warmup 2 > $D/trace.log 2>&1 || exit $?
