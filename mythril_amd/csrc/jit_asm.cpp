@@ -207,6 +207,13 @@ struct Gen {
   std::vector<int32_t> def;          // value id -> defining vcode index
   std::vector<uint32_t> copysrc;     // vcode index of a MIXED K_COORD -> its COPY source's value id
   bool gen_kernel = false;           // mgj_gen (verdict bytes) instead of mgj_search
+  // Dictionary tables staged in LDS by the prologue, limb-major ([limb][entry], so lanes that drew
+  // different entries hit different banks): a gather is then one ds_read per limb instead of a
+  // global load whose latency the wave waits out (18 VMEM reads per group on C2 before this)
+  std::map<uint32_t, uint32_t> lds_base;  // gconsts offset of a table -> LDS word offset
+  std::map<uint32_t, std::pair<uint32_t, uint32_t>> lds_shape;  // table -> (entries, limbs)
+  uint32_t lds_words = 0;
+  static constexpr uint32_t kLdsWords = 8192;  // 32 KiB per 256-lane block
 
   Gen(const Lowered& p, const std::vector<GenSpec>& s, const std::vector<uint32_t>& g)
       : P(p), specs(s), G(g), val(p.vwidth.size()), need(p.vwidth.size(), 0), last(p.vwidth.size(), -1),
@@ -243,6 +250,7 @@ struct Gen {
           fail("op " + std::to_string(in.op) + " outside the assembly tier");
       }
     }
+    plan_lds();
     // uses (for liveness) and demanded limbs (backward)
     auto use = [&](uint32_t id, size_t k) {
       if (id != MG_NONE && id < last.size()) last[id] = std::max(last[id], (int32_t)k);
@@ -340,6 +348,77 @@ struct Gen {
         default: break;
       }
     }
+  }
+
+  void plan_lds() {
+    // coordinates a search reads: the program's K_COORDs and, transitively, their COPY sources
+    std::vector<char> reach(specs.size(), 0);
+    std::vector<uint32_t> st;
+    for (const Instr& in : P.vcode)
+      if (in.op == K_COORD && in.p0 < reach.size() && !reach[in.p0]) {
+        reach[in.p0] = 1;
+        st.push_back(in.p0);
+      }
+    while (!st.empty()) {
+      const uint32_t x = st.back();
+      st.pop_back();
+      const GenSpec& sp = specs[x];
+      if ((sp.kind & 0xFFu) == MG_GEN_MIXED && sp.p[3] != MG_NONE && (sp.p[2] & 0xFFFFu) && sp.p[3] < reach.size() &&
+          !reach[sp.p[3]]) {
+        reach[sp.p[3]] = 1;
+        st.push_back(sp.p[3]);
+      }
+    }
+    for (uint32_t c = 0; c < specs.size() && c < P.coord_width.size(); c++) {
+      if (!reach[c]) continue;
+      const GenSpec& sp = specs[c];
+      const uint32_t kind = sp.kind & 0xFFu, n = sp.p[1], off = sp.p[0], w = P.coord_width[c], Lc = Lw(w);
+      const bool dict = kind == MG_GEN_DICT || (kind == MG_GEN_MIXED && n && (sp.p[2] >> 16));
+      if (!dict || n <= 4 || Lc > 16 || lds_base.count(off)) continue;
+      if (w <= 32 && (uint64_t)n * w <= 32) continue;  // packed into one literal
+      if ((size_t)off + (size_t)n * Lc > G.size() || lds_words + n * Lc > kLdsWords) continue;
+      lds_base[off] = lds_words;
+      lds_shape[off] = {n, Lc};
+      lds_words += n * Lc;
+    }
+  }
+
+  // prologue: every lane of the block copies words of the planned tables, then a barrier
+  void emit_lds_prologue() {
+    if (!lds_words) return;
+    for (const auto& kv : lds_base) {
+      const uint32_t off = kv.first, base = kv.second, n = lds_shape[off].first, Lc = lds_shape[off].second;
+      const uint32_t nL = n * Lc, M = (65536u + Lc - 1) / Lc;  // i / Lc = (i * M) >> 16 for i * Lc < 2^16
+      for (uint32_t it = 0; it * 256 < nL; it++) {
+        const Limb vi = fresh(), vt = fresh(), ve = fresh(), vj = fresh();
+        // word i = tid + 256 it, clamped to the last word (lanes past the table rewrite that one)
+        E.valu("v_add_u32_e32 " + V(vi.v) + ", " + imm(256 * it) + ", v0");
+        E.valu("v_min_u32_e32 " + V(vi.v) + ", " + imm(nL - 1) + ", " + V(vi.v));
+        E.valu("v_lshlrev_b32_e32 " + V(vt.v) + ", 2, " + V(vi.v));
+        if (off * 4 < 4096) {
+          E.mem("global_load_dword " + V(vt.v) + ", " + V(vt.v) + ", s[4:5] offset:" + std::to_string(off * 4));
+        } else {
+          E.valu("v_add_u32_e32 " + V(vt.v) + ", " + hexs(off * 4) + ", " + V(vt.v));
+          E.mem("global_load_dword " + V(vt.v) + ", " + V(vt.v) + ", s[4:5]");
+        }
+        E.valu("v_mul_u32_u24_e32 " + V(ve.v) + ", " + imm(M) + ", " + V(vi.v));
+        E.valu("v_lshrrev_b32_e32 " + V(ve.v) + ", 16, " + V(ve.v));       // entry e
+        E.valu("v_mul_u32_u24_e32 " + V(vj.v) + ", " + imm(Lc) + ", " + V(ve.v));
+        E.valu("v_sub_u32_e32 " + V(vj.v) + ", " + V(vi.v) + ", " + V(vj.v));  // limb j
+        E.valu("v_mul_u32_u24_e32 " + V(vj.v) + ", " + imm(n) + ", " + V(vj.v));
+        if (!inl(base)) E.salu("s_mov_b32 s41, " + hexs(base), {41});
+        E.valu("v_add3_u32 " + V(vj.v) + ", " + V(vj.v) + ", " + V(ve.v) + ", " + (inl(base) ? imm(base) : "s41"), {41});
+        E.valu("v_lshlrev_b32_e32 " + V(vj.v) + ", 2, " + V(vj.v));
+        E.ctl("s_waitcnt vmcnt(0)");
+        E.mem("ds_write_b32 " + V(vj.v) + ", " + V(vt.v));
+        drop(vi);
+        drop(vt);
+        drop(ve);
+        drop(vj);
+      }
+    }
+    E.ctl("s_waitcnt lgkmcnt(0)");
+    E.ctl("s_barrier");
   }
 
   // ---------------------------------------------------------------------------------------
@@ -981,6 +1060,27 @@ struct Gen {
         r[j] = cur;
       }
       for (auto& m : ms) E.srelease(m);
+      return r;
+    }
+    auto lb = lds_base.find(off);
+    if (lb != lds_base.end()) {  // from the LDS copy: word base + j * n + idx
+      const Limb va = fresh();
+      E.valu("v_lshlrev_b32_e32 " + V(va.v) + ", 2, " + V(idx.v));
+      bool any = false;
+      for (uint32_t j = 0; j < Lc; j++) {
+        bool same = true;
+        for (uint32_t e2 = 1; e2 < n && same; e2++) same = G[off + e2 * Lc + j] == G[off + j];
+        if (same) {
+          r[j] = Lit(G[off + j]);
+          continue;
+        }
+        const Limb d = dst(j);
+        E.mem("ds_read_b32 " + V(d.v) + ", " + V(va.v) + " offset:" + std::to_string((lb->second + j * n) * 4));
+        r[j] = d;
+        any = true;
+      }
+      if (any) E.ctl("s_waitcnt lgkmcnt(0)");
+      drop(va);
       return r;
     }
     // gathers from the generator constants (s[4:5]): byte offset (off + idx * Lc + j) * 4
@@ -1910,6 +2010,7 @@ struct Gen {
     E.valu("v_readfirstlane_b32 s3, v0", {}, {3});
     E.salu("s_lshr_b32 s3, s3, 6", {3});
     E.ctl("s_waitcnt lgkmcnt(0)");
+    emit_lds_prologue();
     if (gen_kernel) E.salu("s_mov_b32 s18, 0", {18});
     E.salu("s_and_b32 s29, s18, 1", {29});
     // s[42:43] = early ? 0 : ~0 (the early-exit test of every ASSERT)
@@ -2098,7 +2199,7 @@ struct Gen {
     const int nv = std::max(E.vhigh, kV0), ns = std::max(E.shigh, 56);
     const int accum = (nv + 3) / 4 * 4;
     o << "  .section .rodata,\"a\",@progbits\n  .p2align 6, 0x0\n  .amdhsa_kernel " << name << "\n"
-      << "    .amdhsa_group_segment_fixed_size 0\n    .amdhsa_private_segment_fixed_size 0\n"
+      << "    .amdhsa_group_segment_fixed_size " << lds_words * 4 << "\n    .amdhsa_private_segment_fixed_size 0\n"
       << "    .amdhsa_kernarg_size " << (gen_kernel ? 52 : 56) << "\n"
       << "    .amdhsa_user_sgpr_count 2\n    .amdhsa_user_sgpr_kernarg_segment_ptr 1\n"
       << "    .amdhsa_system_sgpr_workgroup_id_x 1\n    .amdhsa_system_vgpr_workitem_id 0\n"
@@ -2107,14 +2208,17 @@ struct Gen {
       << "    .amdhsa_float_denorm_mode_32 3\n    .amdhsa_float_denorm_mode_16_64 3\n"
       << "  .end_amdhsa_kernel\n  .text\n";
     labels = E.nlab;
+    meta_lds = lds_words * 4;
     meta_vgpr[name] = nv;
     meta_sgpr[name] = ns + 6;
     return o.str();
   }
   std::map<std::string, int> meta_vgpr, meta_sgpr;
+  uint32_t meta_lds = 0;
 };
 
-std::string metadata(const std::map<std::string, int>& vg, const std::map<std::string, int>& sg, bool with_gen) {
+std::string metadata(const std::map<std::string, int>& vg, const std::map<std::string, int>& sg, bool with_gen,
+                     uint32_t lds_bytes) {
   std::ostringstream o;
   auto arg = [&](uint32_t off, uint32_t size, const char* kind, bool global) {
     o << "      - .offset: " << off << "\n        .size: " << size << "\n        .value_kind: " << kind << "\n";
@@ -2134,7 +2238,7 @@ std::string metadata(const std::map<std::string, int>& vg, const std::map<std::s
       arg(48, 4, "by_value", false);
       arg(52, 4, "by_value", false);
     }
-    o << "    .group_segment_fixed_size: 0\n    .kernarg_segment_align: 8\n"
+    o << "    .group_segment_fixed_size: " << lds_bytes << "\n    .kernarg_segment_align: 8\n"
       << "    .kernarg_segment_size: " << (gen ? 52 : 56) << "\n    .max_flat_workgroup_size: 256\n"
       << "    .name: " << name << "\n    .private_segment_fixed_size: 0\n"
       << "    .sgpr_count: " << sg.at(name) << "\n    .sgpr_spill_count: 0\n"
@@ -2177,7 +2281,7 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
       g.gen_kernel = true;
       o << g.kernel("mgj_gen");
     }
-    o << metadata(g.meta_vgpr, g.meta_sgpr, with_gen);
+    o << metadata(g.meta_vgpr, g.meta_sgpr, with_gen, g.meta_lds);
     out = o.str();
     return MG_OK;
   } catch (const AsmFail& f) {
