@@ -347,6 +347,11 @@ def main():
     evals = None
     if rank == 0 and world == 1 and inproc == 1 and not args.no_eval:
         evals = [eval_roofline(eng, torch, w, args.eval_candidates, args.pmc_dir) for w in EVAL_WORKLOADS]
+        for w in EVAL_WORKLOADS:  # the first tier's eval kernel (jit_asm.cpp), where the program is inside it
+            try:
+                evals.append(eval_roofline(eng, torch, w, args.eval_candidates, args.pmc_dir, asm=True))
+            except native.EngineUnsupported as e:
+                evals.append({"workload": CONFIG_OF[w], "kernel": "mgj_eval first tier (asm)", "unsupported": str(e)})
 
     # CPU baseline: the C restatement over a bounded sample of the same candidates
     cpu = None
@@ -425,7 +430,7 @@ def main():
 EVAL_WORKLOADS = ("token_transfer_underflow", "walletlibrary_kill")
 
 
-def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5):
+def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5, asm=False):
     """``Model.eval`` batched (``laser/smt/model.py:45-59``): the compiled eval kernel
     (``mg_jit_eval_dev``) of the UNSPECIALISED program — no generator, no value ranges, every
     instruction evaluated — over n candidates whose coordinates are already in HBM as a
@@ -445,7 +450,11 @@ def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5):
     P.set_watch(prev)
     prog = eng.load(blob)
     info = eng.info(prog)
-    jh = eng.jit_compile(prog, 0)
+    try:
+        jh = eng.jit_compile(prog, 0, asm=asm)
+    except Exception:
+        eng.free(prog)
+        raise
     try:
         cw = int(info.coord_words)
         mask = np.zeros(cw, dtype=np.int64)
@@ -465,22 +474,23 @@ def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5):
         st = eng.stats()
         kernel_ms = st.kernel_ms_total / max(st.launches, 1)
         sat = int(ver.sum().item())
-        src = native.jit_source(blob)
+        src = native.jit_asm(blob) if asm else native.jit_source(blob)
         sha = hashlib.sha256(src.encode()).hexdigest()[:16]
-        rows_read = len(set(re.findall(r"soa\[\(uint64_t\)(\d+)u \* n \+ i\]|// soa row (\d+)", src)))
+        rows_read = len(set(re.findall(r"soa\[\(uint64_t\)(\d+)u \* n \+ i\]|// soa row (\d+)|; soa row (\d+)", src)))
     finally:
         eng.jit_free(jh)
         eng.free(prog)
     del soa, ver
     bpc = 4 * rows_read + 1
     gbs = n * bpc / (kernel_ms * 1e-3) / 1e9
-    out = {"workload": CONFIG_OF[workload], "kernel": "mgj_eval (unspecialised program)", "candidates_per_launch": n,
+    out = {"workload": CONFIG_OF[workload],
+           "kernel": "mgj_eval first tier (asm)" if asm else "mgj_eval (unspecialised program)", "candidates_per_launch": n,
            "program_instrs": int(info.n_instrs), "coord_words": cw, "soa_rows_read": rows_read,
            "bytes_per_candidate": bpc,
            "kernel_ms": kernel_ms, "candidates_per_s": n / (kernel_ms * 1e-3),
            "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS},
            "valu": None, "traffic": None, "sat_fraction": sat / n, "jit_source_sha16": sha}
-    pmc = load_pmc(pmc_dir, "eval_" + workload, sha, n)
+    pmc = load_pmc(pmc_dir, ("evalasm_" if asm else "eval_") + workload, sha, n)
     if pmc is not None:
         n_instr = pmc["derived"]["valu_wave_instructions_per_candidate"]
         achieved = n_instr * n / (kernel_ms * 1e-3) / 1e12

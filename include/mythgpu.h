@@ -291,7 +291,8 @@ int mg_jit_helper_pid(void);
 /* host-only: the specialised source (search kernel if gen_blob, else eval kernel), optionally hipRTC-compiled */
 int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words, int compile,
                           char* buf, size_t cap, size_t* out_len);
-/* host-only: the first tier's assembly (search + gen kernels), optionally assembled */
+/* host-only: the first tier's assembly (search + gen kernels with a generator blob, else the eval
+ * kernel), optionally assembled */
 int mg_program_jit_asm(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words, int compile,
                        char* buf, size_t cap, size_t* out_len);
 int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle);

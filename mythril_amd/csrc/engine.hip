@@ -834,6 +834,7 @@ struct DevJit {
   uint64_t prog = 0, gen = 0;
   int nb_search = 1, nb_eval = 1;
   double compile_ms = 0;
+  bool asm_tier = false;  // the first tier's kernels (jit_asm.cpp): an eval launch takes n < 2^30
 };
 
 // unload (or let go of) a JIT kernel's module
@@ -2185,20 +2186,23 @@ int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_bl
 
 int mg_program_jit_asm(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words, int compile,
                        char* buf, size_t cap, size_t* out_len) {
-  if (!gen_blob) return set_err(MG_E_INVALID, "the assembly tier needs a generator");
   Lowered low;
   std::string err;
   int rc = lower_program(ssa, len, low, err);
   if (rc) return set_err(rc, err);
   std::vector<GenSpec> specs;
   std::vector<uint32_t> consts;
-  rc = parse_gen(low, gen_blob, gen_words, specs, consts, err);
-  if (rc) return set_err(rc, err);
+  if (gen_blob) {
+    rc = parse_gen(low, gen_blob, gen_words, specs, consts, err);
+    if (rc) return set_err(rc, err);
+  }
   Lowered sp;
-  rc = specialize_program(low, &specs, &consts, sp, err, /*keep_watch=*/false);
+  // with a generator: the search + gen kernels; without: the eval kernel (watch rows kept)
+  rc = gen_blob ? specialize_program(low, &specs, &consts, sp, err, /*keep_watch=*/false)
+                : specialize_program(low, nullptr, nullptr, sp, err);
   if (rc) return set_err(rc, err);
   std::string src;
-  rc = jit_asm_source(sp, specs, consts, JIT_SEARCH | JIT_GEN, src, err);
+  rc = jit_asm_source(sp, specs, consts, gen_blob ? (JIT_SEARCH | JIT_GEN) : JIT_EVAL, src, err);
   if (rc) return set_err(rc, "JIT assembly tier: " + err);
   if (out_len) *out_len = src.size();
   if (buf && cap) {
@@ -2264,6 +2268,7 @@ static int load_jit(const std::vector<char>& code, const JitTicket& t, double co
   j->prog = t.prog;
   j->gen = t.gen;
   j->compile_ms = compile_ms;
+  j->asm_tier = (t.flags & MG_JIT_ASM) != 0;
   out = std::move(j);
   return MG_OK;
 }
@@ -2290,8 +2295,7 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
     int asm_rc = MG_OK;
     if (t->flags & MG_JIT_ASM) {
       // the first tier: assembly straight from the specialised program (jit_asm.cpp)
-      asm_rc = t->has_gen ? jit_asm_source(t->low, t->specs, t->consts, kernels, src, asm_err) : MG_E_UNSUPPORTED;
-      if (!t->has_gen) asm_err = "the assembly tier builds search kernels only";
+      asm_rc = jit_asm_source(t->low, t->specs, t->consts, kernels, src, asm_err);
     } else {
       src = t->has_gen ? jit_source(t->low, &t->specs, &t->consts, kernels) : jit_source(t->low, nullptr, nullptr, kernels);
     }
@@ -2321,6 +2325,7 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
         j->nb_eval = en->nb_eval;
         j->prog = t->prog;
         j->gen = t->gen;
+        j->asm_tier = (t->flags & MG_JIT_ASM) != 0;
         j->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       }
     }
@@ -2658,6 +2663,8 @@ int mg_jit_eval_dev(uint64_t jit, const uint32_t* d_soa, uint64_t n, uint8_t* d_
   if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
   DevJit& j = *it->second;
   if (!j.feval) return set_err(MG_E_INVALID, "jit was not compiled for eval (compile with gen = 0)");
+  if (j.asm_tier && n >= (1ull << 30))
+    return set_err(MG_E_UNSUPPORTED, "the first tier's eval kernel takes fewer than 2^30 candidates per call");
   uint32_t nblk = 0;
   void* args[] = {&d_soa, &n, &d_verdict, &d_watch, &nblk};
   return jit_launch(e, j.feval, j.nb_eval, n, args, nblk);

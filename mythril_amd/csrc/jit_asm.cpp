@@ -207,6 +207,7 @@ struct Gen {
   std::vector<int32_t> def;          // value id -> defining vcode index
   std::vector<uint32_t> copysrc;     // vcode index of a MIXED K_COORD -> its COPY source's value id
   bool gen_kernel = false;           // mgj_gen (verdict bytes) instead of mgj_search
+  bool eval_kernel = false;          // mgj_eval: coordinates from HBM-resident SoA rows (no generator)
   // Dictionary tables staged in LDS by the prologue, limb-major ([limb][entry], so lanes that drew
   // different entries hit different banks): a gather is then one ds_read per limb instead of a
   // global load whose latency the wave waits out (18 VMEM reads per group on C2 before this)
@@ -215,15 +216,106 @@ struct Gen {
   uint32_t lds_words = 0;
   static constexpr uint32_t kLdsWords = 8192;  // 32 KiB per 256-lane block
 
+  std::vector<Instr> code;            // the program in emission order (reorder())
   Gen(const Lowered& p, const std::vector<GenSpec>& s, const std::vector<uint32_t>& g)
       : P(p), specs(s), G(g), val(p.vwidth.size()), need(p.vwidth.size(), 0), last(p.vwidth.size(), -1),
-        def(p.vwidth.size(), -1) {}
+        def(p.vwidth.size(), -1), code(p.vcode) {}
+
+  // Emission order: every ASSERT / WATCH in program order, each preceded by the instructions it
+  // needs that are not emitted yet (operands first, depth-first).  A value is then computed just
+  // before its first use and a later constraint's work comes after an earlier one's early exit:
+  // shorter live ranges (C4's eval program peaked at 220 live VGPRs in program order) and less
+  // work per rejected group.  Verdicts do not depend on the order (an AND of the asserts).
+  void reorder() {
+    const std::vector<Instr>& v = P.vcode;
+    std::vector<int32_t> dix(P.vwidth.size(), -1);
+    for (size_t k = 0; k < v.size(); k++)
+      if (v[k].dst != MG_NONE && v[k].dst < dix.size() && dix[v[k].dst] < 0) dix[v[k].dst] = (int32_t)k;
+    std::map<uint32_t, int32_t> coord_at;  // coordinate -> its first K_COORD
+    for (size_t k = 0; k < v.size(); k++)
+      if (v[k].op == K_COORD && !coord_at.count(v[k].p0)) coord_at[v[k].p0] = (int32_t)k;
+    auto operands = [&](const Instr& in, std::vector<int32_t>& out) {
+      out.clear();
+      auto add = [&](uint32_t id) {
+        if (id != MG_NONE && id < dix.size() && dix[id] >= 0) out.push_back(dix[id]);
+      };
+      switch (in.op) {
+        case K_CONST: break;
+        case K_COORD:
+          if (!eval_kernel && in.p0 < specs.size()) {
+            const GenSpec& sp = specs[in.p0];
+            if ((sp.kind & 0xFFu) == MG_GEN_MIXED && sp.p[3] != MG_NONE && (sp.p[2] & 0xFFFFu)) {
+              auto it = coord_at.find(sp.p[3]);
+              if (it != coord_at.end()) out.push_back(it->second);
+            }
+          }
+          break;
+        case K_LOOKUP:
+          add(in.a);
+          add(in.p0);
+          for (uint32_t q = 0; q < 2 * in.c; q++) add(P.vaux[in.p1 + q]);
+          break;
+        case K_NOT: case K_NEG: case K_EXTRACT: case K_ZEXT: case K_SEXT: case K_ASSERT: case K_COPY: case K_WATCH:
+          add(in.a);
+          break;
+        case K_ITE:
+          add(in.a);
+          add(in.b);
+          add(in.c);
+          break;
+        default:
+          add(in.a);
+          add(in.b);
+          break;
+      }
+    };
+    std::vector<char> done(v.size(), 0);
+    std::vector<Instr> out;
+    out.reserve(v.size());
+    std::vector<int32_t> ops;
+    auto visit = [&](int32_t root) {
+      std::vector<std::pair<int32_t, size_t>> st{{root, 0}};  // (instruction, next operand)
+      std::vector<std::vector<int32_t>> opl;
+      opl.emplace_back();
+      operands(v[root], opl.back());
+      while (!st.empty()) {
+        auto& top = st.back();
+        if (done[top.first]) {
+          st.pop_back();
+          opl.pop_back();
+          continue;
+        }
+        if (top.second < opl.back().size()) {
+          const int32_t o = opl.back()[top.second++];
+          if (!done[o]) {
+            st.push_back({o, 0});
+            opl.emplace_back();
+            operands(v[o], opl.back());
+          }
+          continue;
+        }
+        done[top.first] = 1;
+        out.push_back(v[top.first]);
+        st.pop_back();
+        opl.pop_back();
+      }
+    };
+    for (size_t k = 0; k < v.size(); k++)
+      if (v[k].op == K_ASSERT || v[k].op == K_WATCH) visit((int32_t)k);
+    for (size_t k = 0; k < v.size(); k++)
+      if (!done[k]) visit((int32_t)k);
+    code.swap(out);
+  }
 
   // ---------------------------------------------------------------------------------------
   // analysis
   // ---------------------------------------------------------------------------------------
   static uint64_t lowmask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
   uint32_t L(uint32_t id) const { return Lw(P.vwidth[id]); }
+
+  const Instr* def_of(uint32_t id) const {
+    return (id < def.size() && def[id] >= 0) ? &code[def[id]] : nullptr;
+  }
 
   // bits [p, p + n) of a value of width w -> its limbs
   static uint64_t bit_limbs(uint32_t p, uint32_t n, uint32_t w) {
@@ -237,8 +329,9 @@ struct Gen {
   void analyse() {
     for (uint32_t id = 0; id < P.vwidth.size(); id++)
       if (Lw(P.vwidth[id]) > kMaxLimbs) fail("value wider than 2048 bits");
-    for (size_t k = 0; k < P.vcode.size(); k++) {
-      const Instr& in = P.vcode[k];
+    if (!getenv("MYTHGPU_JIT_ASM_NOREORDER")) reorder();
+    for (size_t k = 0; k < code.size(); k++) {
+      const Instr& in = code[k];
       if (in.dst != MG_NONE && in.dst < def.size() && def[in.dst] < 0) def[in.dst] = (int32_t)k;
       switch (in.op) {
         case K_CONST: case K_COORD: case K_ADD: case K_SUB: case K_NEG: case K_AND: case K_OR: case K_XOR:
@@ -246,23 +339,35 @@ struct Gen {
         case K_EXTRACT: case K_ZEXT: case K_SEXT: case K_LOOKUP: case K_ASSERT: case K_COPY: case K_MUL:
         case K_WATCH:
           break;
+        case K_UDIV: case K_UREM: {
+          // by a literal below 2^32 only (x / 86400, x / 10**k: a limb-serial 2/1 division)
+          const Instr* bd = def_of(in.b);
+          bool ok = bd && bd->op == K_CONST;
+          for (uint32_t j = 1; ok && j < Lw(in.wd); j++) ok = P.consts[bd->p0 + j] == 0;
+          if (!ok) fail("division by a non-literal or a literal of 32 bits or more: outside the assembly tier");
+          break;
+        }
         default:
           fail("op " + std::to_string(in.op) + " outside the assembly tier");
       }
     }
-    plan_lds();
+    if (!eval_kernel) plan_lds();
     // uses (for liveness) and demanded limbs (backward)
     auto use = [&](uint32_t id, size_t k) {
       if (id != MG_NONE && id < last.size()) last[id] = std::max(last[id], (int32_t)k);
     };
     std::map<uint32_t, uint32_t> latest;  // coordinate -> value id, in program order
-    copysrc.assign(P.vcode.size(), MG_NONE);
-    for (size_t k = 0; k < P.vcode.size(); k++) {
-      const Instr& in = P.vcode[k];
+    copysrc.assign(code.size(), MG_NONE);
+    for (size_t k = 0; k < code.size(); k++) {
+      const Instr& in = code[k];
       switch (in.op) {
-        case K_CONST: case K_WATCH:
+        case K_CONST:
+          break;
+        case K_WATCH:
+          if (eval_kernel) use(in.a, k);  // the eval kernel stores watched values (model read-back)
           break;
         case K_COORD: {
+          if (eval_kernel) break;
           // a MIXED coordinate reads its COPY source's value if the program generated it before
           const GenSpec& sp = specs.at(in.p0);
           if ((sp.kind & 0xFFu) == MG_GEN_MIXED && sp.p[3] != MG_NONE && (sp.p[2] & 0xFFFFu)) {
@@ -289,8 +394,8 @@ struct Gen {
           break;
       }
     }
-    for (size_t kk = P.vcode.size(); kk-- > 0;) {
-      const Instr& in = P.vcode[kk];
+    for (size_t kk = code.size(); kk-- > 0;) {
+      const Instr& in = code[kk];
       const uint32_t d = in.dst;
       const uint64_t nd = (d != MG_NONE && d < need.size()) ? need[d] : 0;
       auto all = [&](uint32_t id) {
@@ -307,7 +412,9 @@ struct Gen {
       if (in.op == K_COORD && copysrc[kk] != MG_NONE) all(copysrc[kk]);  // copied whole
       switch (in.op) {
         case K_ASSERT: all(in.a); break;
+        case K_WATCH: if (eval_kernel) all(in.a); break;
         case K_ADD: case K_SUB: case K_MUL: upto(in.a, nd); upto(in.b, nd); break;
+        case K_UDIV: case K_UREM: if (nd) { all(in.a); all(in.b); } break;
         case K_NEG: upto(in.a, nd); break;
         case K_AND: case K_OR: case K_XOR: same(in.a, nd); same(in.b, nd); break;
         case K_NOT: case K_COPY: same(in.a, nd); break;
@@ -354,7 +461,7 @@ struct Gen {
     // coordinates a search reads: the program's K_COORDs and, transitively, their COPY sources
     std::vector<char> reach(specs.size(), 0);
     std::vector<uint32_t> st;
-    for (const Instr& in : P.vcode)
+    for (const Instr& in : code)
       if (in.op == K_COORD && in.p0 < reach.size() && !reach[in.p0]) {
         reach[in.p0] = 1;
         st.push_back(in.p0);
@@ -1541,6 +1648,10 @@ struct Gen {
         break;
       }
       case K_COORD: {
+        if (eval_kernel) {
+          set(d, soa_limbs(in, d));
+          break;
+        }
         std::vector<Limb> r = gen_value(in.p0);
         set(d, r);
         cval[in.p0] = d;
@@ -1605,6 +1716,88 @@ struct Gen {
         acc.resize(Ld);
         if (n == Ld) mask_top(acc, W);
         set(d, acc);
+        break;
+      }
+      case K_UDIV: case K_UREM: {
+        const uint32_t dv = P.consts[def_of(in.b)->p0];
+        std::vector<Limb> x = limbs(in.a, Ld), r(Ld, Lit(0));
+        if (dv == 0) {  // SMT-LIB: x / 0 = ~0 (to the width), x % 0 = x
+          for (uint32_t j = 0; j < Ld; j++) {
+            if (in.op == K_UDIV) r[j] = Lit(j == Ld - 1 ? topmask(W) : 0xFFFFFFFFu);
+            else { r[j] = x[j]; E.retain(r[j]); }
+          }
+          set(d, r);
+          break;
+        }
+        // normalised divisor dn = dv << s (top bit set) and its reciprocal v = (2^64 - 1) / dn - 2^32;
+        // the dividend shifted by s into Ld + 1 limbs; then one Moller-Granlund 2/1 step per limb
+        const uint32_t sh = (uint32_t)__builtin_clz(dv), dn = dv << sh;
+        const uint32_t rv = (uint32_t)(~0ull / dn - (1ull << 32));
+        std::vector<Limb> xs(Ld + 1);
+        for (uint32_t j = 0; j <= Ld; j++) {
+          const Limb hi = j < Ld ? x[j] : Lit(0), lo = j ? x[j - 1] : Lit(0);
+          if (sh == 0) {
+            xs[j] = hi;
+            E.retain(hi);
+          } else {
+            xs[j] = bits(std::vector<Limb>{lo, hi}, 64, 32 - sh, 32);
+          }
+        }
+        Limb rem = xs[Ld];  // < 2^sh <= dn: the first step's high word
+        E.salu("s_mov_b32 s40, " + hexs(dn), {40});
+        E.salu("s_mov_b32 s41, " + hexs(rv), {41});
+        Mask mk;
+        mk.k = 2;
+        mk.s = E.salloc();
+        const std::string M = SP(mk.s);
+        for (int32_t j = (int32_t)Ld - 1; j >= 0; j--) {
+          const Limb u1 = vreg(rem), u0 = vreg(xs[j]);
+          drop(rem);
+          drop(xs[j]);
+          const Limb q0 = fresh(), q1 = fresh(), t = fresh(), rr = fresh();
+          // (q1:q0) = rv * u1 + (u1 + 1 : u0)
+          E.valu("v_mul_lo_u32 " + V(q0.v) + ", " + V(u1.v) + ", s41", {41});
+          E.valu("v_mul_hi_u32 " + V(q1.v) + ", " + V(u1.v) + ", s41", {41});
+          E.valu("v_add_co_u32_e32 " + V(q0.v) + ", vcc, " + V(q0.v) + ", " + V(u0.v), {}, {kVCC, kVCC + 1});
+          E.valu("v_addc_co_u32_e32 " + V(q1.v) + ", vcc, " + V(q1.v) + ", " + V(u1.v) + ", vcc", {kVCC, kVCC + 1},
+                 {kVCC, kVCC + 1});
+          E.valu("v_add_u32_e32 " + V(q1.v) + ", 1, " + V(q1.v));
+          // r = u0 - q1 * dn (mod 2^32)
+          E.valu("v_mul_lo_u32 " + V(t.v) + ", " + V(q1.v) + ", s40", {40});
+          E.valu("v_sub_u32_e32 " + V(rr.v) + ", " + V(u0.v) + ", " + V(t.v));
+          // r > q0: q1 - 1, r + dn
+          E.valu("v_cmp_gt_u32_e64 " + M + ", " + V(rr.v) + ", " + V(q0.v), {}, {mk.s, mk.s + 1});
+          E.valu("v_add_u32_e32 " + V(t.v) + ", -1, " + V(q1.v));
+          E.valu("v_add_u32_e32 " + V(q0.v) + ", s40, " + V(rr.v), {40});
+          E.valu("v_cndmask_b32_e64 " + V(q1.v) + ", " + V(q1.v) + ", " + V(t.v) + ", " + M, {mk.s, mk.s + 1});
+          E.valu("v_cndmask_b32_e64 " + V(rr.v) + ", " + V(rr.v) + ", " + V(q0.v) + ", " + M, {mk.s, mk.s + 1});
+          // r >= dn: q1 + 1, r - dn
+          E.valu("v_cmp_le_u32_e64 " + M + ", s40, " + V(rr.v), {40}, {mk.s, mk.s + 1});
+          E.valu("v_add_u32_e32 " + V(t.v) + ", 1, " + V(q1.v));
+          E.valu("v_subrev_u32_e32 " + V(q0.v) + ", s40, " + V(rr.v), {40});
+          E.valu("v_cndmask_b32_e64 " + V(q1.v) + ", " + V(q1.v) + ", " + V(t.v) + ", " + M, {mk.s, mk.s + 1});
+          E.valu("v_cndmask_b32_e64 " + V(rr.v) + ", " + V(rr.v) + ", " + V(q0.v) + ", " + M, {mk.s, mk.s + 1});
+          drop(u1);
+          drop(u0);
+          drop(q0);
+          drop(t);
+          if (in.op == K_UDIV) r[j] = q1;
+          else drop(q1);
+          rem = rr;
+        }
+        E.srelease(mk);
+        if (in.op == K_UREM) {
+          if (sh) {
+            const Limb d0 = fresh();
+            E.valu("v_lshrrev_b32_e32 " + V(d0.v) + ", " + std::to_string(sh) + ", " + V(rem.v));
+            drop(rem);
+            rem = d0;
+          }
+          r[0] = rem;
+        } else {
+          drop(rem);
+        }
+        set(d, r);
         break;
       }
       case K_AND: case K_OR: case K_XOR: {
@@ -1875,7 +2068,7 @@ struct Gen {
         } else {
           E.salu("s_and_b64 s[38:39], s[38:39], " + SP(m.s), {38, 39});
         }
-        if (!gen_kernel) {
+        if (!gen_kernel && !eval_kernel) {
           // early exit: s[42:43] is ~0 when the launch does not stop early, so the OR is zero only
           // when every lane failed and the wave may leave
           E.salu("s_or_b64 s[40:41], s[38:39], s[42:43]", {40, 41});
@@ -1884,6 +2077,22 @@ struct Gen {
         break;
       }
       case K_WATCH:
+        if (eval_kernel) {
+          // watch row p0 + j of candidate i: watch + ((p0 + j) * n + i) * 4, in-range lanes only
+          const uint32_t Lw_ = Lw(P.vwidth[in.a]);
+          E.salu("s_cmp_eq_u64 s[12:13], 0");  // no watch buffer: nothing to store
+          const std::string skip = E.newlab();
+          E.ctl("s_cbranch_scc1 " + skip);
+          E.salu("s_mov_b64 exec, s[24:25]");
+          for (uint32_t j = 0; j < Lw_; j++) {
+            const Limb x = vreg(limb(in.a, j));
+            row_ptr(in.p0 + j, 12);
+            E.mem("global_store_dword v8, " + V(x.v) + ", s[40:41]");
+            drop(x);
+          }
+          E.salu("s_mov_b64 exec, -1");
+          E.label(skip);
+        }
         break;
       default:
         fail("op " + std::to_string(in.op) + " outside the assembly tier");
@@ -1904,10 +2113,30 @@ struct Gen {
     return r;
   }
 
+  static bool debug_live() {
+    static const bool on = getenv("MYTHGPU_JIT_ASM_DEBUG") != nullptr;
+    return on;
+  }
   void body(const std::string& next) {
-    for (size_t k = 0; k < P.vcode.size(); k++) {
-      const Instr& in = P.vcode[k];
+    for (size_t k = 0; k < code.size(); k++) {
+      const Instr& in = code[k];
       emit(in, k, next);
+      if (debug_live()) {
+        int used = 0;
+        for (int r = E.vfirst; r < 256; r++) used += E.vref[r] > 0;
+        fprintf(stderr, "asm live %zu op %u w %u: %d VGPRs\n", k, in.op, in.wd, used);
+        static const long at = getenv("MYTHGPU_JIT_ASM_DEBUG_AT") ? atol(getenv("MYTHGPU_JIT_ASM_DEBUG_AT")) : -1;
+        if ((long)k == at) {
+          std::map<uint32_t, int> byop;
+          for (uint32_t id = 0; id < val.size(); id++) {
+            if (!val[id].def) continue;
+            int regs = 0;
+            for (const auto& l : val[id].l) regs += l.reg();
+            if (regs && def[id] >= 0) byop[code[def[id]].op] += regs;
+          }
+          for (const auto& kv : byop) fprintf(stderr, "  live from op %u: %d limbs\n", kv.first, kv.second);
+        }
+      }
       // values whose last reader is this instruction, and results nobody reads
       auto done = [&](uint32_t id) {
         if (id != MG_NONE && id < last.size() && last[id] <= (int32_t)k && val[id].def) {
@@ -1982,6 +2211,132 @@ struct Gen {
     xs();
     drop(t1);
     drop(t2);
+  }
+
+  // ---------------------------------------------------------------------------------------
+  // the eval kernel (mgj_eval): explicit coordinates from SoA rows [row][candidate] in HBM.
+  // One candidate per lane (i < 2^30: 32-bit lane offsets), a grid-stride loop; the program's
+  // coordinate rows are loaded in the order the program reads them, kPrefetch loads ahead of
+  // their use (loads complete in order, so each use waits with vmcnt for exactly its row)
+  // ---------------------------------------------------------------------------------------
+  // loads kept in flight ahead of their use (MYTHGPU_JIT_ASM_PREFETCH, default 24; at most 60: vmcnt)
+  static uint32_t prefetch_depth() {
+    static const uint32_t n = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_PREFETCH");
+      return g ? (uint32_t)std::max(1, std::min(60, atoi(g))) : 24u;
+    }();
+    return n;
+  }
+  std::vector<uint32_t> rows;           // SoA rows in the order the program reads them
+  std::vector<Limb> row_reg;            // registers of issued rows
+  size_t rows_issued = 0, rows_used = 0;
+
+  // s[dst:dst+1] (here s[40:41]) = base s[b:b+1] + row * n * 4 (n * 4 in s[14:15]... kept as s20 low / s21 high)
+  void row_ptr(uint32_t row, int b) {
+    E.salu("s_mul_i32 s40, s20, " + hexs(row), {40});
+    E.salu("s_mul_hi_u32 s41, s20, " + hexs(row), {41});
+    E.salu("s_mul_i32 s42, s21, " + hexs(row), {42});
+    E.salu("s_add_u32 s41, s41, s42", {41});
+    E.salu("s_add_u32 s40, s40, " + S(b), {40});
+    E.salu("s_addc_u32 s41, s41, " + S(b + 1), {41});
+  }
+  void issue_rows(size_t upto) {
+    while (rows_issued < rows.size() && rows_issued < upto) {
+      const Limb d = fresh();
+      row_ptr(rows[rows_issued], 4);
+      E.mem("global_load_dword " + V(d.v) + ", v2, s[40:41]  ; soa row " + std::to_string(rows[rows_issued]));
+      row_reg[rows_issued++] = d;
+    }
+  }
+  std::vector<Limb> soa_limbs(const Instr& in, uint32_t d) {
+    const uint32_t Lc = Lw(in.wd);
+    std::vector<Limb> r(Lc);
+    for (uint32_t j = 0; j < Lc; j++) {
+      if (!(need[d] >> j & 1)) continue;
+      if (rows_used >= rows.size() || rows[rows_used] != in.p1 + j) fail("internal: SoA row order");
+      issue_rows(rows_used + 1);
+      // loads return in order: wait until only the loads issued after this row are outstanding
+      const size_t after = rows_issued - rows_used - 1;
+      E.ctl("s_waitcnt vmcnt(" + std::to_string(std::min<size_t>(after, 63)) + ")");
+      r[j] = row_reg[rows_used++];
+      issue_rows(rows_used + prefetch_depth());  // keep that many loads in flight
+    }
+    return r;
+  }
+
+  std::string kernel_eval(const std::string& name) {
+    E = Emitter();
+    E.nlab = labels;
+    census.clear();
+    E.vfirst = kV0 + (int)pool.size();
+    E.vhigh = E.vfirst;
+    val.assign(P.vwidth.size(), Val{});
+    rows.clear();
+    for (const Instr& in : code)
+      if (in.op == K_COORD)
+        for (uint32_t j = 0; j < Lw(in.wd); j++)
+          if (in.dst < need.size() && (need[in.dst] >> j & 1)) rows.push_back(in.p1 + j);
+    row_reg.assign(rows.size(), Limb{});
+    auto& o = E.o;
+    o << "  .text\n  .globl " << name << "\n  .p2align 8\n  .type " << name << ",@function\n" << name << ":\n";
+    // arguments (soa, n, verdict_out, watch, nblk): s[4:5] soa, s[8:9] n, s[10:11] verdict, s[12:13] watch, s14 nblk
+    E.ctl("s_load_dwordx2 s[4:5], s[0:1], 0x0");
+    E.ctl("s_load_dwordx8 s[8:15], s[0:1], 0x8");
+    E.valu("v_and_b32_e32 v1, 63, v0");
+    E.valu("v_mov_b32_e32 v6, 0");
+    E.valu("v_readfirstlane_b32 s3, v0", {}, {3});
+    E.salu("s_lshr_b32 s3, s3, 6", {3});
+    E.ctl("s_waitcnt lgkmcnt(0)");
+    for (const auto& kv : pool) E.valu("v_mov_b32_e32 " + V((uint32_t)kv.second) + ", " + imm(kv.first));
+    // n * 4 (64-bit) in s[20:21]; the wave's first candidate s16 = block * 256 + wave * 64; stride s17
+    E.salu("s_lshl_b64 s[20:21], s[8:9], 2", {20, 21});
+    E.salu("s_lshl_b32 s16, s2, 8", {16});
+    E.salu("s_lshl_b32 s22, s3, 6", {22});
+    E.salu("s_add_u32 s16, s16, s22", {16});
+    E.salu("s_lshl_b32 s17, s14, 8", {17});
+    E.salu("s_add_u32 s23, s8, -1", {23});  // n - 1
+    const std::string loop = E.newlab(), exit_ = E.newlab();
+    E.label(loop);
+    E.salu("s_cmp_lt_u32 s16, s8");
+    E.ctl("s_cbranch_scc0 " + exit_);
+    // i = s16 + lane; v3 = i (store offset), v2 = 4 * min(i, n - 1) (load offset: lanes past n reread
+    // the last candidate and store nothing); s[24:25] = lanes with i < n
+    E.valu("v_add_u32_e32 v3, s16, v1", {16});
+    E.valu("v_min_u32_e32 v2, s23, v3", {23});
+    E.valu("v_lshlrev_b32_e32 v2, 2, v2");
+    E.valu("v_cmp_gt_u32_e64 s[24:25], s8, v3", {8}, {24, 25});
+    E.valu("v_lshlrev_b32_e32 v8, 2, v3");  // watch-row store offset 4 i
+    E.salu("s_mov_b64 s[38:39], -1", {38, 39});
+    rows_issued = rows_used = 0;
+    issue_rows(prefetch_depth());
+    body("");
+    if (rows_used != rows.size()) fail("internal: SoA rows left unread");
+    for (int r = E.vfirst; r < 256; r++)
+      if (E.vref[r]) fail("internal: VGPR v" + std::to_string(r) + " still held after the body");
+    // verdict byte of the lanes in range
+    E.valu("v_cndmask_b32_e64 v7, 0, 1, s[38:39]", {38, 39});
+    E.salu("s_mov_b64 exec, s[24:25]");
+    E.mem("global_store_byte v3, v7, s[10:11]");
+    E.salu("s_mov_b64 exec, -1");
+    E.salu("s_add_u32 s16, s16, s17", {16});
+    E.ctl("s_branch " + loop);
+    E.label(exit_);
+    E.ctl("s_endpgm");
+    const int nv = std::max(E.vhigh, kV0), ns = std::max(E.shigh, 56);
+    const int accum = (nv + 3) / 4 * 4;
+    o << "  .section .rodata,\"a\",@progbits\n  .p2align 6, 0x0\n  .amdhsa_kernel " << name << "\n"
+      << "    .amdhsa_group_segment_fixed_size 0\n    .amdhsa_private_segment_fixed_size 0\n"
+      << "    .amdhsa_kernarg_size 36\n"
+      << "    .amdhsa_user_sgpr_count 2\n    .amdhsa_user_sgpr_kernarg_segment_ptr 1\n"
+      << "    .amdhsa_system_sgpr_workgroup_id_x 1\n    .amdhsa_system_vgpr_workitem_id 0\n"
+      << "    .amdhsa_next_free_vgpr " << nv << "\n    .amdhsa_next_free_sgpr " << ns << "\n"
+      << "    .amdhsa_accum_offset " << accum << "\n    .amdhsa_reserve_vcc 1\n"
+      << "    .amdhsa_float_denorm_mode_32 3\n    .amdhsa_float_denorm_mode_16_64 3\n"
+      << "  .end_amdhsa_kernel\n  .text\n";
+    labels = E.nlab;
+    meta_vgpr[name] = nv;
+    meta_sgpr[name] = ns + 6;
+    return o.str();
   }
 
   int labels = 0;  // label numbers continue across the kernels of one module
@@ -2252,13 +2607,54 @@ std::string metadata(const std::map<std::string, int>& vg, const std::map<std::s
 
 }  // namespace
 
+std::string metadata_eval(int vg, int sg) {
+  std::ostringstream o;
+  auto arg = [&](uint32_t off, uint32_t size, const char* kind, bool global) {
+    o << "      - .offset: " << off << "\n        .size: " << size << "\n        .value_kind: " << kind << "\n";
+    if (global) o << "        .address_space: global\n";
+  };
+  o << "  .amdgpu_metadata\n---\namdhsa.kernels:\n  - .args:\n";
+  arg(0, 8, "global_buffer", true);
+  arg(8, 8, "by_value", false);
+  arg(16, 8, "global_buffer", true);
+  arg(24, 8, "global_buffer", true);
+  arg(32, 4, "by_value", false);
+  o << "    .group_segment_fixed_size: 0\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 36\n"
+    << "    .max_flat_workgroup_size: 256\n    .name: mgj_eval\n    .private_segment_fixed_size: 0\n"
+    << "    .sgpr_count: " << sg << "\n    .sgpr_spill_count: 0\n    .symbol: mgj_eval.kd\n"
+    << "    .uniform_work_group_size: 1\n    .uses_dynamic_stack: false\n    .vgpr_count: " << vg
+    << "\n    .vgpr_spill_count: 0\n    .wavefront_size: 64\n    .agpr_count: 0\n"
+    << "amdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n  .end_amdgpu_metadata\n";
+  return o.str();
+}
+
 int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const std::vector<uint32_t>& gconsts,
                    uint32_t kernels, std::string& out, std::string& err) {
   try {
     Gen g(P, specs, gconsts);
-    g.analyse();
     std::ostringstream o;
     o << kAsmMarker << "\n  .amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"\n  .amdhsa_code_object_version 6\n";
+    if (kernels & JIT_EVAL) {  // the eval kernel alone (no generator)
+      g.eval_kernel = true;
+      g.analyse();
+      std::string ks = g.kernel_eval("mgj_eval");
+      if (!getenv("MYTHGPU_JIT_ASM_NOPOOL")) {
+        std::vector<std::pair<uint32_t, uint32_t>> by;
+        for (const auto& kv : g.census)
+          if (kv.second >= 2) by.push_back({kv.second, kv.first});
+        std::sort(by.begin(), by.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+        const int room = std::max(0, 96 - g.meta_vgpr["mgj_eval"]);
+        for (size_t i = 0; i < by.size() && (int)i < room; i++) g.pool[by[i].second] = kV0 + (int)i;
+        if (!g.pool.empty()) {
+          g.labels = 0;
+          ks = g.kernel_eval("mgj_eval");
+        }
+      }
+      o << ks << metadata_eval(g.meta_vgpr["mgj_eval"], g.meta_sgpr["mgj_eval"]);
+      out = o.str();
+      return MG_OK;
+    }
+    g.analyse();
     // pass 1 counts the literals the kernel moves into VGPRs; pass 2 pools the most used ones, as long
     // as the kernel stays within 96 VGPRs (5 waves per SIMD)
     g.gen_kernel = false;

@@ -77,6 +77,9 @@ int main() {
     std::string src(sl, '\0');
     if (!read_all(0, &src[0], sl)) return 0;
     apply_env(env);
+    // the first tier's assembly: comgr's on-disk cache costs more than the assembler it would skip
+    // (the first write of an entry ~10 ms on the box against ~4 ms of assembly); off for it
+    if (src.compare(0, std::strlen(mg::kAsmMarker), mg::kAsmMarker) == 0) setenv("AMD_COMGR_CACHE", "0", 1);
     if (const char* f = getenv("MYTHGPU_JITD_FAULT"))
       if (!std::strcmp(f, "abort")) abort();
     std::vector<char> code;

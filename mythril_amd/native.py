@@ -240,17 +240,18 @@ def jit_source(blob: bytes, gen_blob: Optional[np.ndarray] = None, compile: bool
     return buf.value.decode()
 
 
-def jit_asm(blob: bytes, gen_blob: np.ndarray, compile: bool = False) -> str:
-    """Host-only: the first tier's gfx950 assembly of a search program (mgj_search + mgj_gen),
-    optionally assembled and linked through comgr (no GPU).  Raises EngineUnsupported for
-    programs outside the tier."""
+def jit_asm(blob: bytes, gen_blob: Optional[np.ndarray] = None, compile: bool = False) -> str:
+    """Host-only: the first tier's gfx950 assembly — of a search program (mgj_search + mgj_gen)
+    when a generator blob is given, else of the eval kernel (mgj_eval) — optionally assembled and
+    linked through comgr (no GPU).  Raises EngineUnsupported for programs outside the tier."""
     lib = load_library()
-    g = np.ascontiguousarray(gen_blob, dtype=np.uint32)
+    g = None if gen_blob is None else np.ascontiguousarray(gen_blob, dtype=np.uint32)
+    gp = _ptr(g, C.c_uint32) if g is not None else None
+    gn = 0 if g is None else g.size
     n = C.c_size_t()
-    _check(lib.mg_program_jit_asm(_u8(blob), len(blob), _ptr(g, C.c_uint32), g.size, 0, None, 0, C.byref(n)))
+    _check(lib.mg_program_jit_asm(_u8(blob), len(blob), gp, gn, 0, None, 0, C.byref(n)))
     buf = C.create_string_buffer(n.value + 1)
-    _check(lib.mg_program_jit_asm(_u8(blob), len(blob), _ptr(g, C.c_uint32), g.size, 1 if compile else 0, buf,
-                                  n.value + 1, C.byref(n)))
+    _check(lib.mg_program_jit_asm(_u8(blob), len(blob), gp, gn, 1 if compile else 0, buf, n.value + 1, C.byref(n)))
     return buf.value.decode()
 
 

@@ -204,3 +204,65 @@ def test_asm_tier_hard_needle_full_size(engine):
         engine.jit_free(jo)
         engine.free_gen(gh)
         engine.free(prog)
+
+
+# ---------------------------------------------------------------------------------------------
+# the first tier's eval kernel (mgj_eval from jit_asm.cpp): explicit SoA coordinates, watch rows
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("seed", range(16))
+def test_asm_eval_random_programs_terms(engine, seed):
+    """``Model.eval`` batched on the first tier's eval kernel: every watched term's value and every
+    verdict equal the Python oracle's on edge-value assignments (``oracle/bv.py``, the reference's
+    ``model.eval(..., model_completion=True)``), as the O3 eval kernel's do."""
+    from tests.helpers import gpu_eval_terms
+    from oracle.bv import evaluate_many
+
+    roots = _random_program(3000 + seed)
+    P0, _ = search.prepare(roots)
+    try:
+        native.jit_asm(P0.to_bytes(), None)
+    except native.EngineUnsupported as e:
+        pytest.skip(f"outside the tier: {e}")
+    watch = [t for t in T.postorder(roots) if t.sort[0] == "bv"][:24]
+    P, assigns, ver, vals, models = gpu_eval_terms(engine, roots, watch, n=200, seed=seed, asm=True)
+    for i, m in enumerate(models):
+        want = evaluate_many(list(roots) + watch, m)
+        assert ver[i] == int(all(want[:len(roots)])), (seed, i)
+        for k, t in enumerate(watch):
+            assert vals[i][t.id] == want[len(roots) + k], (seed, i, k)
+
+
+@pytest.mark.parametrize("name", ["token_transfer_underflow", "suicide_kill", "etherstore_reentrancy"])
+def test_asm_eval_workload_verdicts(engine, name):
+    """The unspecialised workload program on random SoA rows: the first tier's eval verdicts equal
+    the C port's (``oracle/bveval.c`` eval) and the O3 eval kernel's, at an n that leaves a partial
+    last wave."""
+    from oracle import cport
+
+    P, _ = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
+    P.set_watch([])
+    pb = P.to_bytes()
+    prog = engine.load(pb)
+    info = engine.info(prog)
+    n = 5000 + 37
+    rng = np.random.default_rng(7)
+    soa = rng.integers(0, 1 << 32, size=(int(info.coord_words), n), dtype=np.uint64).astype(np.uint32)
+    # mask each coordinate row to its width (the layout mg_eval expects)
+    from mythril_amd import ssa
+
+    offs = P.coord_row_offsets()
+    for c in P.coords:
+        for j in range(ssa.limbs(c.width)):
+            bits = min(32, c.width - 32 * j)
+            soa[offs[c.index] + j] &= np.uint32((1 << bits) - 1)
+    ja = engine.jit_compile(prog, 0, asm=True)
+    jo = engine.jit_compile(prog, 0)
+    try:
+        va, _ = engine.jit_eval(ja, soa, n)
+        vo, _ = engine.jit_eval(jo, soa, n)
+    finally:
+        engine.jit_free(ja)
+        engine.jit_free(jo)
+        engine.free(prog)
+    want = cport.eval_soa(pb, soa, n)
+    assert np.array_equal(va, want) and np.array_equal(vo, want)
