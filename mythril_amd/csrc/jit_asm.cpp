@@ -1481,8 +1481,14 @@ struct Gen {
         if (pc) {
           branch(pc);
           std::vector<Limb> s;
+          // the source's value when it is still live and whole (a copy chain's inner source may
+          // have been generated earlier and released after its last analysed use)
           auto it = cval.find(sp.p[3]);
-          if (it != cval.end()) {
+          if (debug_live() && it != cval.end())
+            fprintf(stderr, "asm copy source %u of %u: def %d need %llx\n", sp.p[3], c, (int)val[it->second].def,
+                    (unsigned long long)need[it->second]);
+          if (it != cval.end() && val[it->second].def &&
+              (need[it->second] & lowmask(L(it->second))) == lowmask(L(it->second))) {
             s = val[it->second].l;
             for (auto& x : s) E.retain(x);
           } else {
