@@ -319,6 +319,13 @@ int mg_jit_info(uint64_t jit, double* compile_ms, int* blocks_per_cu);
 int mg_jit_free(uint64_t jit);
 int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags, uint64_t* first_hit,
                   uint64_t* n_hits, uint32_t* assign_out);
+/* n independent searches of one kernel (seed q over [starts[q], starts[q] + counts[q])), each
+ * with its own hit buffer, launched back to back round-robin over four streams so one launch's
+ * tail overlaps the next one's start, one wait for all: SURVEY's C2 sweep (2^24 per launch,
+ * seeds 1..16) without a host round trip per launch.  first_hits[q] = ~0 when launch q found
+ * nothing.  Results equal n calls of mg_jit_search; over several devices it is those calls. */
+int mg_jit_search_many(uint64_t jit, uint32_t n, const uint64_t* seeds, const uint64_t* starts, const uint64_t* counts,
+                       uint32_t flags, uint64_t* first_hits, uint64_t* n_hits);
 int mg_jit_eval(uint64_t jit, const uint32_t* soa_coords, uint64_t n, uint8_t* verdict_out, uint32_t* watch_out);
 int mg_jit_eval_dev(uint64_t jit, const uint32_t* d_soa_coords, uint64_t n, uint8_t* d_verdict_out,
                     uint32_t* d_watch_out);

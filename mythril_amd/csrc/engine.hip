@@ -57,6 +57,9 @@ constexpr uint32_t kHitWords = kHitStride * (1 + kHitStripes);
 // mg_init; jit.cpp and jit_asm.cpp read it at the same offset (kPeerWord, 2,176 B).
 constexpr uint32_t kPeerWord = kHitWords, kPeerMax = 15;
 constexpr uint32_t kHitAlloc = kHitWords + 1 + kPeerMax;
+// mg_jit_search_many: launches per batch (one hit buffer each) and the streams they alternate on
+constexpr uint32_t kManySlots = 64;
+constexpr int kManyStreams = 4;
 static_assert(kPeerWord == 272, "jit.cpp / jit_asm.cpp hard-code the peer line at 2,176 B");
 
 // an early-exit first hit to the devices above this one (the peer line)
@@ -955,6 +958,12 @@ struct Engine {
   uint32_t* d_watch1 = nullptr;  // one candidate's watch rows (model read-back)
   size_t watch1_words = 0;
   uint8_t* d_ver1 = nullptr;
+  // mg_jit_search_many: kManySlots hit buffers (kHitAlloc words each, no peers) and their pinned
+  // armed image / read-back, and kManyStreams streams the launches round-robin over (created on first use)
+  unsigned long long* d_hitmany = nullptr;
+  unsigned long long* h_hitmany = nullptr;
+  hipStream_t xs[4] = {};
+  hipEvent_t xev[4] = {};
   mg_stats_t stats{};
 };
 
@@ -1452,6 +1461,16 @@ static void free_dev_buffers(Engine& e) {
   e.scratch_bytes = 0;
   (void)hipFree(e.d_hit);
   if (e.h_hit) (void)hipHostFree(e.h_hit);
+  if (e.d_hitmany) (void)hipFree(e.d_hitmany);
+  if (e.h_hitmany) (void)hipHostFree(e.h_hitmany);
+  e.d_hitmany = nullptr;
+  e.h_hitmany = nullptr;
+  for (int q = 0; q < 4; q++) {
+    if (e.xs[q]) (void)hipStreamDestroy(e.xs[q]);
+    if (e.xev[q]) (void)hipEventDestroy(e.xev[q]);
+    e.xs[q] = nullptr;
+    e.xev[q] = nullptr;
+  }
   if (e.h_watch1) (void)hipHostFree(e.h_watch1);
   e.h_hit = nullptr;
   e.h_watch1 = nullptr;
@@ -2084,7 +2103,7 @@ int mg_dev_download(void* dst, const void* dptr, size_t bytes) {
 namespace mg {
 
 // `nblk` is the kernel's grid-size argument (the JIT kernels read no dispatch packet)
-static int jit_launch_async(Engine& e, hipFunction_t f, int nb, uint64_t count, void** args, uint32_t& nblk) {
+static uint32_t jit_grid(const Engine& e, uint64_t count) {
   const uint64_t want = (count + 255) / 256;
   // MYTHGPU_JIT_BPC (default 64) 256-lane blocks per CU, i.e. 64 waves per SIMD over the
   // launch, whatever the occupancy (`nb`, unused here: the API answers 4 blocks/CU for a
@@ -2112,9 +2131,13 @@ static int jit_launch_async(Engine& e, hipFunction_t f, int nb, uint64_t count, 
     const uint64_t waves_cu = std::max<uint64_t>(1, ((count + 63) / 64) / (min_groups * (uint64_t)std::max(e.cu_count, 1)));
     bpc = std::max<uint64_t>(1, std::min(bpc, waves_cu / 4));
   }
-  (void)nb;
   const uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * bpc;
-  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+  return (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+}
+
+static int jit_launch_async(Engine& e, hipFunction_t f, int nb, uint64_t count, void** args, uint32_t& nblk) {
+  (void)nb;
+  const uint32_t grid = jit_grid(e, count);
   nblk = grid;
   HIPCHK(hipEventRecord(e.ev0, e.stream));
   HIPCHK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, e.stream, args, nullptr));
@@ -2626,6 +2649,91 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
   if (n_hits) *n_hits = res[1];
   e.stats.hits += res[1];
   if (assign_out && res[0] != ~0ull) return read_assignment(e, *git->second, seed, res[0], assign_out);
+  return MG_OK;
+}
+
+int mg_jit_search_many(uint64_t jit, uint32_t n, const uint64_t* seeds, const uint64_t* starts, const uint64_t* counts,
+                       uint32_t flags, uint64_t* first_hits, uint64_t* n_hits) {
+  if (n == 0) return MG_OK;
+  if (!seeds || !starts || !counts || !first_hits || !n_hits) return set_err(MG_E_INVALID, "mg_jit_search_many: null array");
+  Engine& e = E();
+  bool split = false;
+  for (uint32_t q = 0; q < n; q++) split = split || split_over_devices(counts[q]);
+  if (split) {  // several devices per launch: one mg_jit_search after the other
+    for (uint32_t q = 0; q < n; q++) {
+      const int rc = mg_jit_search(jit, seeds[q], starts[q], counts[q], flags, first_hits + q, n_hits + q, nullptr);
+      if (rc) return rc;
+    }
+    return MG_OK;
+  }
+  std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
+  auto it = e.jits.find(jit);
+  if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
+  DevJit& j = *it->second;
+  auto git = e.gens.find(j.gen);
+  if (!find_prog(e, j.prog) || git == e.gens.end() || !j.fsearch) return set_err(MG_E_INVALID, "jit was not compiled for search");
+  for (uint32_t q = 0; q < n; q++)
+    if (counts[q] > (1ull << 52)) return set_err(MG_E_INVALID, "mg_jit_search_many: more than 2^52 candidates in one launch");
+  if (!e.d_hitmany) {
+    HIPCHK(hipMalloc((void**)&e.d_hitmany, (size_t)kManySlots * kHitAlloc * sizeof(unsigned long long)));
+    HIPCHK(hipHostMalloc((void**)&e.h_hitmany, 2 * (size_t)kManySlots * kHitAlloc * sizeof(unsigned long long),
+                         hipHostMallocDefault));
+    std::memset(e.h_hitmany, 0, 2 * (size_t)kManySlots * kHitAlloc * sizeof(unsigned long long));
+    for (uint32_t q = 0; q < kManySlots; q++) e.h_hitmany[(size_t)q * kHitAlloc] = ~0ull;  // armed; peer count 0
+    for (int q = 0; q < kManyStreams; q++) {
+      HIPCHK(hipStreamCreateWithFlags(&e.xs[q], hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&e.xev[q], hipEventDisableTiming));
+    }
+  }
+  const uint32_t* gconsts = git->second->d_consts;
+  for (uint32_t b0 = 0; b0 < n; b0 += kManySlots) {
+    const uint32_t m = std::min<uint32_t>(kManySlots, n - b0);
+    const size_t bytes = (size_t)m * kHitAlloc * sizeof(unsigned long long);
+    unsigned long long* back = e.h_hitmany + (size_t)kManySlots * kHitAlloc;
+    // arm m slots with one copy on the engine stream; the launch streams wait for it
+    HIPCHK(hipEventRecord(e.ev0, e.stream));
+    HIPCHK(hipMemcpyAsync(e.d_hitmany, e.h_hitmany, bytes, hipMemcpyHostToDevice, e.stream));
+    HIPCHK(hipEventRecord(e.ev2, e.stream));
+    for (int q = 0; q < kManyStreams; q++) HIPCHK(hipStreamWaitEvent(e.xs[q], e.ev2, 0));
+    uint64_t total = 0;
+    for (uint32_t q = 0; q < m; q++) {
+      uint64_t start = starts[b0 + q], count = counts[b0 + q];
+      uint64_t sk = seed_lane_key(seeds[b0 + q]), sg = seed_group_key(seeds[b0 + q]);
+      unsigned long long* hitp = e.d_hitmany + (size_t)q * kHitAlloc;
+      uint32_t f = flags;
+      const uint64_t lanes = (start + count) - (start & ~63ull);
+      uint32_t nblk = jit_grid(e, lanes);
+      void* args[] = {&gconsts, &start, &count, &sk, &sg, &hitp, &f, &nblk};
+      total += count;
+      if (count == 0) continue;
+      // hipModuleLaunchKernel copies the argument values at the call
+      HIPCHK(hipModuleLaunchKernel(j.fsearch, nblk, 1, 1, 256, 1, 1, 0, e.xs[q % kManyStreams], args, nullptr));
+    }
+    for (int q = 0; q < kManyStreams; q++) {
+      HIPCHK(hipEventRecord(e.xev[q], e.xs[q]));
+      HIPCHK(hipStreamWaitEvent(e.stream, e.xev[q], 0));
+    }
+    HIPCHK(hipEventRecord(e.ev1, e.stream));
+    HIPCHK(hipMemcpyAsync(back, e.d_hitmany, bytes, hipMemcpyDeviceToHost, e.stream));
+    HIPCHK(hipEventRecord(e.ev2, e.stream));
+    HIPCHK(hipEventSynchronize(e.ev2));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e.ev0, e.ev1));
+    e.stats.launches += m;
+    e.stats.last_kernel_ms = ms;  // the batch's arm .. last kernel
+    e.stats.kernel_ms_total += ms;
+    e.stats.candidates += total;
+    e.stats.last_candidates = total;
+    for (uint32_t q = 0; q < m; q++) {
+      const unsigned long long* r = back + (size_t)q * kHitAlloc;
+      uint64_t h = r[1];
+      for (uint32_t t = 1; t <= kHitStripes; t++) h += r[kHitStride * t];
+      first_hits[b0 + q] = counts[b0 + q] ? r[0] : ~0ull;
+      n_hits[b0 + q] = counts[b0 + q] ? h : 0;
+      e.stats.hits += n_hits[b0 + q];
+    }
+  }
   return MG_OK;
 }
 

@@ -2152,7 +2152,10 @@ struct Gen {
       };
       if (in.dst != MG_NONE && in.dst < last.size() && last[in.dst] < 0) done(in.dst);
       switch (in.op) {
-        case K_CONST: case K_WATCH: break;
+        case K_CONST: break;
+        case K_WATCH:
+          if (eval_kernel) done(in.a);  // a value read last by its watch row store
+          break;
         case K_COORD:
           if (copysrc[k] != MG_NONE) done(copysrc[k]);
           break;

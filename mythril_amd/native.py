@@ -37,7 +37,7 @@ EXPORTS = [
     "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
     "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_program_jit_asm", "mg_jit_compile", "mg_jit_compile_ex", "mg_jit_verdicts", "mg_jit_info",
     "mg_jit_compile_async", "mg_jit_poll", "mg_jit_cancel", "mg_jit_helper_pid", "mg_cache_clear", "mg_split_range",
-    "mg_jit_free", "mg_jit_search", "mg_jit_eval", "mg_jit_eval_dev",
+    "mg_jit_free", "mg_jit_search", "mg_jit_search_many", "mg_jit_eval", "mg_jit_eval_dev",
 ]
 
 
@@ -136,6 +136,7 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_split_range": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, u64p, u64p]),
             "mg_jit_free": (C.c_int, [C.c_uint64]),
             "mg_jit_search": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, u64p, u64p, u32p]),
+            "mg_jit_search_many": (C.c_int, [C.c_uint64, C.c_uint32, u64p, u64p, u64p, C.c_uint32, u64p, u64p]),
             "mg_jit_eval": (C.c_int, [C.c_uint64, u32p, C.c_uint64, u8p, u32p]),
             "mg_jit_eval_dev": (C.c_int, [C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
         }
@@ -415,6 +416,22 @@ class Engine:
         ap = _ptr(assign, C.c_uint32) if assign is not None else None
         _check(self.lib.mg_jit_search(jit, seed, start, count, flags, C.byref(fh), C.byref(nh), ap))
         return (None if fh.value == NO_HIT else fh.value), nh.value
+
+    def jit_search_many(self, jit: int, seeds, starts, counts, early_exit: bool = False):
+        """Independent searches (seed, start, count) of one kernel in one call (mg_jit_search_many):
+        [(first_hit or None, hits)] in order."""
+        n = len(seeds)
+        s = np.ascontiguousarray(seeds, dtype=np.uint64)
+        a = np.ascontiguousarray(starts, dtype=np.uint64)
+        c = np.ascontiguousarray(counts, dtype=np.uint64)
+        if not (len(a) == len(c) == n):
+            raise ValueError("seeds, starts and counts differ in length")
+        fh = np.zeros(n, dtype=np.uint64)
+        nh = np.zeros(n, dtype=np.uint64)
+        flags = MG_SEARCH_EARLY_EXIT if early_exit else 0
+        _check(self.lib.mg_jit_search_many(jit, n, _ptr(s, C.c_uint64), _ptr(a, C.c_uint64), _ptr(c, C.c_uint64),
+                                           flags, _ptr(fh, C.c_uint64), _ptr(nh, C.c_uint64)))
+        return [(None if int(f) == NO_HIT else int(f), int(h)) for f, h in zip(fh, nh)]
 
     def jit_eval(self, jit: int, soa: np.ndarray, n: int, watch_words: int = 0):
         soa = np.ascontiguousarray(soa, dtype=np.uint32)

@@ -159,3 +159,22 @@ def test_asm_tier_random_programs_assemble_on_host():
         except native.EngineUnsupported:
             pass
     assert ok >= 20
+
+
+def test_asm_eval_with_watch_rows_assembles_on_host():
+    """The first tier's eval kernel (mgj_eval) with watch rows, as ``gpu_eval_terms`` builds it (24
+    watched terms + the model read-back rows): emits and assembles for every random program; a value
+    read last by its watch store is released (an earlier build leaked its registers and refused)."""
+    from mythril_amd import ssa
+    from mythril_amd.search import model_watch
+    from mythril_amd.smt import terms as T
+    from tests.test_gpu_asm import _random_program
+
+    for seed in range(16):
+        roots = _random_program(3000 + seed)
+        watch = [t for t in T.postorder(roots) if t.sort[0] == "bv"][:24]
+        P = ssa.flatten(list(roots), extra=list(watch))
+        me, _ = model_watch(P)
+        P.set_watch([P.term_node[t.id] for t in watch] + me)
+        src = native.jit_asm(P.to_bytes(), None, compile=True)
+        assert "mgj_eval:" in src
