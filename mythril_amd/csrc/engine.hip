@@ -1375,6 +1375,16 @@ int mg_init(uint32_t device_mask) {
   }
   HIPCHK(hipSetDevice(e.device));
   e.stats.n_devices = (uint32_t)g_devs.size();
+  std::thread([] {  // helpers up (and the first tier's assembler warm) before the first query needs them
+    Lowered P;
+    P.vwidth = {1};
+    P.consts = {1};
+    P.vcode = {Instr{K_CONST, 1, 0, MG_NONE, MG_NONE, MG_NONE, 0, 0},
+               Instr{K_ASSERT, 1, MG_NONE, 0, MG_NONE, MG_NONE, 0, 0}};
+    std::string src, err;
+    if (jit_asm_source(P, {}, {}, JIT_EVAL, src, err) != MG_OK) src.clear();
+    jit_helper_warm(src);
+  }).detach();
   return MG_OK;
 }
 

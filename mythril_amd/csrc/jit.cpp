@@ -1729,6 +1729,25 @@ static bool isolated() {
   return !(v && v[0] == '0');
 }
 
+void jit_helper_warm(const std::string& asm_src) {
+  const char* w = getenv("MYTHGPU_JIT_WARM");
+  if (!isolated() || (w && w[0] == '0')) return;
+  // the first tier's helper: started, and `asm_src` (a tiny kernel) assembled and linked through
+  // it, so the process start-up, comgr's load and LLVM's AMDGPU target set-up are paid here and
+  // not by the first query's first-tier compile (cold 11.9 ms against ~4.6 ms warm on the box,
+  // profiles/r04h_bench.json)
+  if (!asm_src.empty()) {
+    std::vector<char> code;
+    std::string log;
+    bool available = true;
+    (void)helper_compile(asm_src, code, log, available);
+  }
+  // the compiler's helper: started only (its first compile loads comgr)
+  Helper& h = helper(0);
+  std::lock_guard<std::mutex> g(h.mu);
+  if (h.fd < 0 && !h.dead) (void)helper_start(h);
+}
+
 void jit_compiler_preload() {
   if (isolated()) return;  // the compiler lives in the helper process
   const char* which = getenv("MYTHGPU_JIT_COMPILER");

@@ -25,6 +25,9 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
 // Load the JIT compiler library now (on the calling thread): its static destructors then
 // register before anything the caller registers with atexit afterwards.
 void jit_compiler_preload();
+// start the compile helpers and warm the first tier's by assembling `asm_src` (a tiny kernel) —
+// mg_init runs it on a detached thread; MYTHGPU_JIT_WARM=0 or in-process compiles: nothing
+void jit_helper_warm(const std::string& asm_src);
 
 // compile for gfx950 -> code object bytes. MG_OK or MG_E_*; `log` gets the compiler log.  By
 // default through the compiler helper process (mythgpu_jitd): a compiler abort there fails the

@@ -2228,17 +2228,28 @@ struct Gen {
   // coordinate rows are loaded in the order the program reads them, kPrefetch loads ahead of
   // their use (loads complete in order, so each use waits with vmcnt for exactly its row)
   // ---------------------------------------------------------------------------------------
-  // loads kept in flight ahead of their use (MYTHGPU_JIT_ASM_PREFETCH, default 24; at most 60: vmcnt)
-  static uint32_t prefetch_depth() {
+  // loads kept in flight ahead of their use: MYTHGPU_JIT_ASM_PREFETCH fixes it (at most 60: vmcnt);
+  // by default jit_asm_source sizes it to the registers the kernel's occupancy leaves (eval_depth)
+  static uint32_t prefetch_env() {
     static const uint32_t n = [] {
       const char* g = getenv("MYTHGPU_JIT_ASM_PREFETCH");
-      return g ? (uint32_t)std::max(1, std::min(60, atoi(g))) : 24u;
+      return g ? (uint32_t)std::max(1, std::min(60, atoi(g))) : 0u;
     }();
     return n;
   }
+  uint32_t depth = 24;
+  uint32_t prefetch_depth() const { return depth; }
   std::vector<uint32_t> rows;           // SoA rows in the order the program reads them
   std::vector<Limb> row_reg;            // registers of issued rows
   size_t rows_issued = 0, rows_used = 0;
+  // Across groups: the first `ring` rows of the NEXT group are loaded into fixed registers (ring_reg,
+  // held for the whole kernel) while this group's last rows are consumed, offsets in vnext, so the
+  // queue never drains at a group boundary.  A ring row's value is copied out when consumed.
+  // row_seq: issue position of each row among this iteration's loads (ring rows: before it, -ring..-1)
+  std::vector<Limb> ring_reg;
+  Limb vnext;
+  std::vector<long> row_seq;
+  long loads = 0;
 
   // s[dst:dst+1] (here s[40:41]) = base s[b:b+1] + row * n * 4 (n * 4 in s[14:15]... kept as s20 low / s21 high)
   void row_ptr(uint32_t row, int b) {
@@ -2254,6 +2265,7 @@ struct Gen {
       const Limb d = fresh();
       row_ptr(rows[rows_issued], 4);
       E.mem("global_load_dword " + V(d.v) + ", v2, s[40:41]  ; soa row " + std::to_string(rows[rows_issued]));
+      row_seq[rows_issued] = loads++;
       row_reg[rows_issued++] = d;
     }
   }
@@ -2265,10 +2277,26 @@ struct Gen {
       if (rows_used >= rows.size() || rows[rows_used] != in.p1 + j) fail("internal: SoA row order");
       issue_rows(rows_used + 1);
       // loads return in order: wait until only the loads issued after this row are outstanding
-      const size_t after = rows_issued - rows_used - 1;
-      E.ctl("s_waitcnt vmcnt(" + std::to_string(std::min<size_t>(after, 63)) + ")");
-      r[j] = row_reg[rows_used++];
+      // (stores are not counted: the watch stores are conditional; an uncounted younger store only
+      // makes the wait longer)
+      const long after = loads - row_seq[rows_used] - 1;
+      E.ctl("s_waitcnt vmcnt(" + std::to_string(std::min<long>(std::max<long>(after, 0), 63)) + ")");
+      const size_t p = rows_used++;
+      if (p < ring_reg.size()) {  // a ring register: copied out, reloaded for the next group below
+        r[j] = fresh();
+        E.valu("v_mov_b32_e32 " + V(r[j].v) + ", " + V(ring_reg[p].v));
+      } else {
+        r[j] = row_reg[p];
+      }
       issue_rows(rows_used + prefetch_depth());  // keep that many loads in flight
+      const size_t M = rows.size(), R = ring_reg.size();
+      if (p + R >= M) {  // the next group's ring row p + R - M (clamped offsets: always in bounds)
+        const size_t q = p + R - M;
+        row_ptr(rows[q], 4);
+        E.mem("global_load_dword " + V(ring_reg[q].v) + ", " + V(vnext.v) + ", s[40:41]  ; soa row " + std::to_string(rows[q]) +
+              " (next group)");
+        loads++;
+      }
     }
     return r;
   }
@@ -2286,6 +2314,7 @@ struct Gen {
         for (uint32_t j = 0; j < Lw(in.wd); j++)
           if (in.dst < need.size() && (need[in.dst] >> j & 1)) rows.push_back(in.p1 + j);
     row_reg.assign(rows.size(), Limb{});
+    row_seq.assign(rows.size(), 0);
     auto& o = E.o;
     o << "  .text\n  .globl " << name << "\n  .p2align 8\n  .type " << name << ",@function\n" << name << ":\n";
     // arguments (soa, n, verdict_out, watch, nblk): s[4:5] soa, s[8:9] n, s[10:11] verdict, s[12:13] watch, s14 nblk
@@ -2305,21 +2334,42 @@ struct Gen {
     E.salu("s_lshl_b32 s17, s14, 8", {17});
     E.salu("s_add_u32 s23, s8, -1", {23});  // n - 1
     const std::string loop = E.newlab(), exit_ = E.newlab();
+    // the ring: the first rows of the wave's first group, loaded before the loop
+    ring_reg.clear();
+    for (size_t q = 0; q < std::min<size_t>(prefetch_depth(), rows.size()); q++) ring_reg.push_back(fresh());
+    vnext = fresh();
+    E.salu("s_cmp_lt_u32 s16, s8");
+    E.ctl("s_cbranch_scc0 " + exit_);
+    E.valu("v_add_u32_e32 v3, s16, v1", {16});
+    E.valu("v_min_u32_e32 v2, s23, v3", {23});
+    E.valu("v_lshlrev_b32_e32 v2, 2, v2");
+    for (size_t q = 0; q < ring_reg.size(); q++) {
+      row_ptr(rows[q], 4);
+      E.mem("global_load_dword " + V(ring_reg[q].v) + ", v2, s[40:41]  ; soa row " + std::to_string(rows[q]) + " (first group)");
+    }
     E.label(loop);
     E.salu("s_cmp_lt_u32 s16, s8");
     E.ctl("s_cbranch_scc0 " + exit_);
     // i = s16 + lane; v3 = i (store offset), v2 = 4 * min(i, n - 1) (load offset: lanes past n reread
-    // the last candidate and store nothing); s[24:25] = lanes with i < n
+    // the last candidate and store nothing); s[24:25] = lanes with i < n; vnext: the same for i + stride
     E.valu("v_add_u32_e32 v3, s16, v1", {16});
     E.valu("v_min_u32_e32 v2, s23, v3", {23});
     E.valu("v_lshlrev_b32_e32 v2, 2, v2");
+    E.valu("v_add_u32_e32 " + V(vnext.v) + ", s17, v3", {17});
+    E.valu("v_min_u32_e32 " + V(vnext.v) + ", s23, " + V(vnext.v), {23});
+    E.valu("v_lshlrev_b32_e32 " + V(vnext.v) + ", 2, " + V(vnext.v));
     E.valu("v_cmp_gt_u32_e64 s[24:25], s8, v3", {8}, {24, 25});
     E.valu("v_lshlrev_b32_e32 v8, 2, v3");  // watch-row store offset 4 i
     E.salu("s_mov_b64 s[38:39], -1", {38, 39});
-    rows_issued = rows_used = 0;
-    issue_rows(prefetch_depth());
+    rows_issued = ring_reg.size();
+    rows_used = 0;
+    loads = 0;
+    for (size_t q = 0; q < ring_reg.size(); q++) row_seq[q] = (long)q - (long)ring_reg.size();
     body("");
     if (rows_used != rows.size()) fail("internal: SoA rows left unread");
+    for (const Limb& l : ring_reg) drop(l);
+    drop(vnext);
+    ring_reg.clear();
     for (int r = E.vfirst; r < 256; r++)
       if (E.vref[r]) fail("internal: VGPR v" + std::to_string(r) + " still held after the body");
     // verdict byte of the lanes in range
@@ -2330,6 +2380,7 @@ struct Gen {
     E.salu("s_add_u32 s16, s16, s17", {16});
     E.ctl("s_branch " + loop);
     E.label(exit_);
+    E.ctl("s_waitcnt vmcnt(0)");  // the last iteration's loads for a group past n
     E.ctl("s_endpgm");
     const int nv = std::max(E.vhigh, kV0), ns = std::max(E.shigh, 56);
     const int accum = (nv + 3) / 4 * 4;
@@ -2646,7 +2697,34 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
     if (kernels & JIT_EVAL) {  // the eval kernel alone (no generator)
       g.eval_kernel = true;
       g.analyse();
+      // The HBM stream is latency-bound (rows in flight per wave x waves per SIMD): the row queue gets
+      // the registers the kernel's occupancy step leaves (C2: 44 rows at 4 waves per SIMD; C4: ~40 at 2).
+      // MYTHGPU_JIT_ASM_PREFETCH fixes the depth instead.
+      g.depth = Gen::prefetch_env() ? Gen::prefetch_env() : 8u;
       std::string ks = g.kernel_eval("mgj_eval");
+      if (!Gen::prefetch_env()) {
+        const int nv = g.meta_vgpr["mgj_eval"];
+        const int waves = std::max(1, std::min(8, 512 / ((nv + 7) / 8 * 8)));
+        const int budget = std::min(256, 512 / waves / 8 * 8);
+        for (int d = std::min(60, 8 + budget - nv); d > 8; d -= 4) {
+          g.depth = (uint32_t)d;
+          g.labels = 0;
+          try {
+            std::string k2 = g.kernel_eval("mgj_eval");
+            if (g.meta_vgpr["mgj_eval"] <= budget) {
+              ks = k2;
+              break;
+            }
+          } catch (const AsmFail&) {  // out of VGPRs at this depth: a shallower one
+            g.meta_vgpr["mgj_eval"] = 1 << 20;
+          }
+        }
+        if (g.meta_vgpr["mgj_eval"] > budget) {  // none fitted: the depth-8 kernel again
+          g.depth = 8;
+          g.labels = 0;
+          ks = g.kernel_eval("mgj_eval");
+        }
+      }
       if (!getenv("MYTHGPU_JIT_ASM_NOPOOL")) {
         std::vector<std::pair<uint32_t, uint32_t>> by;
         for (const auto& kv : g.census)

@@ -232,11 +232,14 @@ def test_asm_eval_random_programs_terms(engine, seed):
             assert vals[i][t.id] == want[len(roots) + k], (seed, i, k)
 
 
-@pytest.mark.parametrize("name", ["token_transfer_underflow", "suicide_kill", "etherstore_reentrancy"])
-def test_asm_eval_workload_verdicts(engine, name):
+@pytest.mark.parametrize("n", [5000 + 37, (1 << 18) + 37])
+@pytest.mark.parametrize("name", ["token_transfer_underflow", "suicide_kill", "etherstore_reentrancy",
+                                  "walletlibrary_kill"])
+def test_asm_eval_workload_verdicts(engine, name, n):
     """The unspecialised workload program on random SoA rows: the first tier's eval verdicts equal
     the C port's (``oracle/bveval.c`` eval) and the O3 eval kernel's, at an n that leaves a partial
-    last wave."""
+    last wave; at 2^18 + 37 every wave sweeps several groups, so the next group's rows loaded while
+    the current group finishes (the cross-group row ring) are exercised."""
     from oracle import cport
 
     P, _ = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
@@ -244,7 +247,6 @@ def test_asm_eval_workload_verdicts(engine, name):
     pb = P.to_bytes()
     prog = engine.load(pb)
     info = engine.info(prog)
-    n = 5000 + 37
     rng = np.random.default_rng(7)
     soa = rng.integers(0, 1 << 32, size=(int(info.coord_words), n), dtype=np.uint64).astype(np.uint32)
     # mask each coordinate row to its width (the layout mg_eval expects)
