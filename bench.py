@@ -346,12 +346,16 @@ def main():
     # the eval kernel's own roofline (unspecialised C2 and C4 programs on HBM-resident SoA inputs)
     evals = None
     if rank == 0 and world == 1 and inproc == 1 and not args.no_eval:
-        evals = [eval_roofline(eng, torch, w, args.eval_candidates, args.pmc_dir) for w in EVAL_WORKLOADS]
-        for w in EVAL_WORKLOADS:  # the first tier's eval kernel (jit_asm.cpp), where the program is inside it
-            try:
-                evals.append(eval_roofline(eng, torch, w, args.eval_candidates, args.pmc_dir, asm=True))
-            except native.EngineUnsupported as e:
-                evals.append({"workload": CONFIG_OF[w], "kernel": "mgj_eval first tier (asm)", "unsupported": str(e)})
+        evals = []
+        # the O3 and first-tier (jit_asm.cpp) eval kernels, each on the [row][candidate] SoA and on the
+        # tiled SoA (MG_JIT_SOA_TILED: a group's rows in one block)
+        for asm in (False, True):
+            for tiled in (False, True):
+                for w in EVAL_WORKLOADS:
+                    try:
+                        evals.append(eval_roofline(eng, torch, w, args.eval_candidates, args.pmc_dir, asm=asm, tiled=tiled))
+                    except native.EngineUnsupported as e:
+                        evals.append({"workload": CONFIG_OF[w], "kernel": eval_kernel_name(asm, tiled), "unsupported": str(e)})
 
     # CPU baseline: the C restatement over a bounded sample of the same candidates
     cpu = None
@@ -430,7 +434,11 @@ def main():
 EVAL_WORKLOADS = ("token_transfer_underflow", "walletlibrary_kill")
 
 
-def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5, asm=False):
+def eval_kernel_name(asm, tiled):
+    return ("mgj_eval first tier (asm)" if asm else "mgj_eval (unspecialised program)") + (", tiled SoA" if tiled else "")
+
+
+def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5, asm=False, tiled=False):
     """``Model.eval`` batched (``laser/smt/model.py:45-59``): the compiled eval kernel
     (``mg_jit_eval_dev``) of the UNSPECIALISED program — no generator, no value ranges, every
     instruction evaluated — over n candidates whose coordinates are already in HBM as a
@@ -451,7 +459,7 @@ def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5, asm=False):
     prog = eng.load(blob)
     info = eng.info(prog)
     try:
-        jh = eng.jit_compile(prog, 0, asm=asm)
+        jh = eng.jit_compile(prog, 0, asm=asm, tiled=tiled)
     except Exception:
         eng.free(prog)
         raise
@@ -465,6 +473,8 @@ def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5, asm=False):
                 mask[offs[c.index] + j] = (1 << bits) - 1
         soa = torch.randint(-(1 << 31), (1 << 31) - 1, (cw, n), dtype=torch.int32, device="cuda")
         soa &= torch.from_numpy(mask.astype(np.uint32).view(np.int32)).to("cuda")[:, None]
+        if tiled:
+            soa = native.tile_soa(soa)
         ver = torch.empty(n, dtype=torch.uint8, device="cuda")
         torch.cuda.synchronize()
         eng.jit_eval_dev(jh, soa.data_ptr(), n, ver.data_ptr())  # warm-up (module load, caches)
@@ -474,7 +484,7 @@ def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5, asm=False):
         st = eng.stats()
         kernel_ms = st.kernel_ms_total / max(st.launches, 1)
         sat = int(ver.sum().item())
-        src = native.jit_asm(blob) if asm else native.jit_source(blob)
+        src = native.jit_asm(blob, tiled=tiled) if asm else native.jit_source(blob, tiled=tiled)
         sha = hashlib.sha256(src.encode()).hexdigest()[:16]
         rows_read = len(set(re.findall(r"soa\[\(uint64_t\)(\d+)u \* n \+ i\]|// soa row (\d+)|; soa row (\d+)", src)))
     finally:
@@ -484,13 +494,13 @@ def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5, asm=False):
     bpc = 4 * rows_read + 1
     gbs = n * bpc / (kernel_ms * 1e-3) / 1e9
     out = {"workload": CONFIG_OF[workload],
-           "kernel": "mgj_eval first tier (asm)" if asm else "mgj_eval (unspecialised program)", "candidates_per_launch": n,
+           "kernel": eval_kernel_name(asm, tiled), "soa_layout": "tiled" if tiled else "row-major", "candidates_per_launch": n,
            "program_instrs": int(info.n_instrs), "coord_words": cw, "soa_rows_read": rows_read,
            "bytes_per_candidate": bpc,
            "kernel_ms": kernel_ms, "candidates_per_s": n / (kernel_ms * 1e-3),
            "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS},
            "valu": None, "traffic": None, "sat_fraction": sat / n, "jit_source_sha16": sha}
-    pmc = load_pmc(pmc_dir, ("evalasm_" if asm else "eval_") + workload, sha, n)
+    pmc = load_pmc(pmc_dir, ("evalasm_" if asm else "eval_") + ("tiled_" if tiled else "") + workload, sha, n)
     if pmc is not None:
         n_instr = pmc["derived"]["valu_wave_instructions_per_candidate"]
         achieved = n_instr * n / (kernel_ms * 1e-3) / 1e12

@@ -288,7 +288,9 @@ int mg_jit_helper_pid(void);
  * generator handle, the search kernel (mg_jit_search) specialised on it; with
  * gen = 0, the eval kernel (mg_jit_eval*).  It emits straight-line code (values in VGPRs, literals as immediates,
  * generator inlined).  Same semantics as mg_search / mg_eval. */
-/* host-only: the specialised source (search kernel if gen_blob, else eval kernel), optionally hipRTC-compiled */
+/* host-only: the specialised source (search kernel if gen_blob, else eval kernel); compile bit 0:
+ * also compile it, bit 1: the eval kernel for the tiled SoA (MG_JIT_SOA_TILED).  Same bits for
+ * mg_program_jit_asm. */
 int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words, int compile,
                           char* buf, size_t cap, size_t* out_len);
 /* host-only: the first tier's assembly (search + gen kernels with a generator blob, else the eval
@@ -299,9 +301,15 @@ int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle);
 /* flags: MG_JIT_GEN_VERDICTS also builds mgj_gen (per-candidate verdicts, mg_jit_verdicts);
  * MG_JIT_ASM builds the first tier instead: the same kernels emitted as gfx950 assembly with the
  * engine's own register allocation, assembled and linked in a few ms (clang + LLVM take ~140 ms);
- * MG_E_UNSUPPORTED for programs outside it (division, EXP, Keccak, variable shifts, UMUL_NOOVF) */
+ * MG_E_UNSUPPORTED for programs outside it (division other than by a literal of at most 32 bits,
+ * EXP, Keccak, variable shifts, UMUL_NOOVF).
+ * MG_JIT_SOA_TILED (eval kernel, gen = 0): the kernel reads a TILED SoA — coordinate limb row r of
+ * candidate i at word ((i / 64) * coord_words + r) * 64 + i % 64, so a group of 64 candidates has
+ * its rows in one contiguous block (coord_words * 256 bytes) — instead of [row][candidate].  The
+ * buffer holds ceil(n / 64) whole blocks (the last one padded).  Same verdicts and watch rows. */
 #define MG_JIT_GEN_VERDICTS 1u
 #define MG_JIT_ASM 2u
+#define MG_JIT_SOA_TILED 4u
 int mg_jit_compile_ex(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* jit_handle);
 int mg_jit_verdicts(uint64_t jit, uint64_t seed, uint64_t start, uint64_t n, uint8_t* verdict_out);
 /* Asynchronous compile on the engine's compile thread (outside the engine lock: searches on

@@ -838,6 +838,7 @@ struct DevJit {
   int nb_search = 1, nb_eval = 1;
   double compile_ms = 0;
   bool asm_tier = false;  // the first tier's kernels (jit_asm.cpp): an eval launch takes n < 2^30
+  bool tiled = false;     // eval kernel compiled for the tiled SoA (MG_JIT_SOA_TILED)
 };
 
 // unload (or let go of) a JIT kernel's module
@@ -2201,14 +2202,14 @@ int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_bl
                           /*keep_watch=*/gen_blob == nullptr);
   if (rc) return set_err(rc, err);
   const std::string src = gen_blob ? jit_source(sp, &specs, &consts, JIT_SEARCH)
-                                   : jit_source(sp, nullptr, nullptr, JIT_EVAL);
+                                   : jit_source(sp, nullptr, nullptr, JIT_EVAL | ((compile & 2) ? JIT_EVAL_TILED : 0u));
   if (out_len) *out_len = src.size();
   if (buf && cap) {
     const size_t n = std::min(cap - 1, src.size());
     std::memcpy(buf, src.data(), n);
     buf[n] = 0;
   }
-  if (compile) {
+  if (compile & 1) {
     std::vector<char> code;
     std::string log;
     rc = jit_compile(src, code, log);
@@ -2235,7 +2236,8 @@ int mg_program_jit_asm(const uint8_t* ssa, size_t len, const uint32_t* gen_blob,
                 : specialize_program(low, nullptr, nullptr, sp, err);
   if (rc) return set_err(rc, err);
   std::string src;
-  rc = jit_asm_source(sp, specs, consts, gen_blob ? (JIT_SEARCH | JIT_GEN) : JIT_EVAL, src, err);
+  rc = jit_asm_source(sp, specs, consts, gen_blob ? (JIT_SEARCH | JIT_GEN) : (JIT_EVAL | ((compile & 2) ? JIT_EVAL_TILED : 0u)),
+                      src, err);
   if (rc) return set_err(rc, "JIT assembly tier: " + err);
   if (out_len) *out_len = src.size();
   if (buf && cap) {
@@ -2243,7 +2245,7 @@ int mg_program_jit_asm(const uint8_t* ssa, size_t len, const uint32_t* gen_blob,
     std::memcpy(buf, src.data(), n);
     buf[n] = 0;
   }
-  if (compile) {
+  if (compile & 1) {
     std::vector<char> code;
     std::string log;
     rc = jit_compile(src, code, log);
@@ -2302,6 +2304,7 @@ static int load_jit(const std::vector<char>& code, const JitTicket& t, double co
   j->gen = t.gen;
   j->compile_ms = compile_ms;
   j->asm_tier = (t.flags & MG_JIT_ASM) != 0;
+  j->tiled = !t.has_gen && (t.flags & MG_JIT_SOA_TILED) != 0;
   out = std::move(j);
   return MG_OK;
 }
@@ -2323,7 +2326,8 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
     if (t->cancelled) continue;
     lk.unlock();
     const auto t0 = std::chrono::steady_clock::now();
-    const uint32_t kernels = t->has_gen ? (JIT_SEARCH | ((t->flags & MG_JIT_GEN_VERDICTS) ? JIT_GEN : 0u)) : JIT_EVAL;
+    const uint32_t kernels = t->has_gen ? (JIT_SEARCH | ((t->flags & MG_JIT_GEN_VERDICTS) ? JIT_GEN : 0u))
+                                        : (JIT_EVAL | ((t->flags & MG_JIT_SOA_TILED) ? JIT_EVAL_TILED : 0u));
     std::string src, asm_err;
     int asm_rc = MG_OK;
     if (t->flags & MG_JIT_ASM) {
@@ -2359,6 +2363,7 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
         j->prog = t->prog;
         j->gen = t->gen;
         j->asm_tier = (t->flags & MG_JIT_ASM) != 0;
+        j->tiled = !t->has_gen && (t->flags & MG_JIT_SOA_TILED) != 0;
         j->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       }
     }
@@ -2791,6 +2796,7 @@ int mg_jit_eval_dev(uint64_t jit, const uint32_t* d_soa, uint64_t n, uint8_t* d_
 int mg_jit_eval(uint64_t jit, const uint32_t* soa, uint64_t n, uint8_t* verdict_out, uint32_t* watch_out) {
   Engine& e = E();
   DevProgram* p;
+  bool tiled = false;
   {
     std::lock_guard<std::mutex> g(e.mu);
   OnDevice od_(e);
@@ -2798,16 +2804,19 @@ int mg_jit_eval(uint64_t jit, const uint32_t* soa, uint64_t n, uint8_t* verdict_
     if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
     p = find_prog(e, it->second->prog);
     if (!p) return set_err(MG_E_INVALID, "jit program was freed");
+    tiled = it->second->tiled;
   }
   if (n == 0) return MG_OK;
-  const size_t soa_bytes = (size_t)std::max<uint32_t>(p->low.coord_words, 1) * n * 4;
+  // a tiled SoA (MG_JIT_SOA_TILED) holds ceil(n / 64) whole 64-candidate blocks
+  const uint64_t soa_cols = tiled ? (n + 63) / 64 * 64 : n;
+  const size_t soa_bytes = (size_t)std::max<uint32_t>(p->low.coord_words, 1) * soa_cols * 4;
   const size_t watch_bytes = (size_t)p->low.watch_words * n * 4;
   uint32_t *d_soa = nullptr, *d_watch = nullptr;
   uint8_t* d_ver = nullptr;
   HIPCHK(hipMalloc((void**)&d_soa, soa_bytes));
   HIPCHK(hipMalloc((void**)&d_ver, n));
   if (watch_out && watch_bytes) HIPCHK(hipMalloc((void**)&d_watch, watch_bytes));
-  if (p->low.coord_words) HIPCHK(hipMemcpy(d_soa, soa, (size_t)p->low.coord_words * n * 4, hipMemcpyHostToDevice));
+  if (p->low.coord_words) HIPCHK(hipMemcpy(d_soa, soa, (size_t)p->low.coord_words * soa_cols * 4, hipMemcpyHostToDevice));
   int rc = mg_jit_eval_dev(jit, d_soa, n, d_ver, d_watch);
   if (rc == MG_OK) {
     HIPCHK(hipMemcpy(verdict_out, d_ver, n, hipMemcpyDeviceToHost));

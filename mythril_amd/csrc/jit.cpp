@@ -782,11 +782,15 @@ struct Gen {
               // ~970 v_writelane per candidate).  A program with watch rows keeps the indexed form
               // (its per-store branches compile too slowly around the walking pointer's barriers)
               const int64_t step = (int64_t)(in.p1 + j) - (int64_t)soa_row;
-              if (step) o << "  sp_ += (long long)" << step << " * (long long)n; __asm__ volatile(\"\" : \"+v\"(sp_));\n";
+              if (step && tiled) o << "  sp_ += " << step * 64 << "ll; __asm__ volatile(\"\" : \"+v\"(sp_));\n";
+              else if (step) o << "  sp_ += (long long)" << step << " * (long long)n; __asm__ volatile(\"\" : \"+v\"(sp_));\n";
               o << "  " << v(d, j) << " = *sp_;  // soa row " << (in.p1 + j) << "\n";
               soa_row = in.p1 + j;
             } else {
-              o << "  " << v(d, j) << " = soa[(uint64_t)" << (in.p1 + j) << "u * n + i];\n";
+              if (tiled)
+                o << "  " << v(d, j) << " = soa[((i >> 6) * " << P.coord_words << "ull + " << (in.p1 + j) << "ull) * 64ull + (i & 63ull)];\n";
+              else
+                o << "  " << v(d, j) << " = soa[(uint64_t)" << (in.p1 + j) << "u * n + i];\n";
             }
           }
         }
@@ -998,6 +1002,9 @@ struct Gen {
   // P is specialised (program.cpp specialize_program): decided compares are literals,
   // aliases are renamed away and dead instructions are gone
   uint32_t soa_row = 0;  // eval kernel without watch rows: the SoA row sp_ points at
+  // MG_JIT_SOA_TILED: row r of candidate i at ((i / 64) * coord_words + r) * 64 + i % 64 (a group's
+  // rows contiguous; jit_asm.cpp "Tiled SoA"): the walking pointer steps 64 words per row
+  bool tiled = false;
 
   void body(bool search) {
     coord_var.clear();  // generated-coordinate names are per kernel
@@ -1031,6 +1038,7 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
                        uint32_t kernels) {
   const bool want_search = kernels & JIT_SEARCH, want_eval = kernels & JIT_EVAL, want_gen = kernels & JIT_GEN;
   Gen g(P, specs, gconsts);
+  g.tiled = (kernels & JIT_EVAL_TILED) != 0;
   g.plan_dict_lds();
   g.plan_dict_gv();
   g.plan_ws_slots();
@@ -1193,7 +1201,9 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "  const uint64_t stride = (uint64_t)nblk * 256u;\n"
        "  for (uint64_t i = (uint64_t)__builtin_amdgcn_workgroup_id_x() * 256u + __builtin_amdgcn_workitem_id_x(); i < n; i += stride) {\n"
        "  uint32_t verdict = 1u;\n"
-       "  const GU32* sp_ = (const GU32*)((uint64_t)soa + i * 4ull);\n";
+       << (g.tiled ? "  const GU32* sp_ = (const GU32*)((uint64_t)soa + (((i >> 6) * " + std::to_string(P.coord_words) +
+                       "ull * 64ull) + (i & 63ull)) * 4ull);  // tiled SoA\n"
+                 : std::string("  const GU32* sp_ = (const GU32*)((uint64_t)soa + i * 4ull);\n"));
   g.decls();
   g.body(false);
   o << "  verdict_out[i] = (uint8_t)verdict;\n  }\n}\n";

@@ -10,7 +10,7 @@ namespace mg {
 // HIP source of the requested kernels: mgj_search (generator + first hit), mgj_gen
 // (per-candidate verdicts of generated candidates) and mgj_eval (SoA inputs).
 // `specs`/`gconsts` (nullable) specialise the generator at codegen time.
-enum : uint32_t { JIT_SEARCH = 1, JIT_EVAL = 2, JIT_GEN = 4 };
+enum : uint32_t { JIT_SEARCH = 1, JIT_EVAL = 2, JIT_GEN = 4, JIT_EVAL_TILED = 8 };
 std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
                        uint32_t kernels);
 

@@ -2248,6 +2248,12 @@ struct Gen {
   // row_seq: issue position of each row among this iteration's loads (ring rows: before it, -ring..-1)
   std::vector<Limb> ring_reg;
   Limb vnext;
+  // Tiled SoA (MG_JIT_SOA_TILED): candidate i's row r at ((i / 64) * coord_words + r) * 64 + i % 64 —
+  // a group's rows are one contiguous block (C4: 243 x 256 B), so a wave's loads stay inside one
+  // page (the row-major layout put them 4 n bytes apart: 7.7 % UTCL1 translation misses on C4)
+  // and each row's address is the group base + an immediate.  s[26:27] this group's block, s[28:29]
+  // the next group's (clamped to the last block)
+  bool tiled = false;
   std::vector<long> row_seq;
   long loads = 0;
 
@@ -2260,11 +2266,36 @@ struct Gen {
     E.salu("s_add_u32 s40, s40, " + S(b), {40});
     E.salu("s_addc_u32 s41, s41, " + S(b + 1), {41});
   }
+  // the load of SoA row `row` of the group whose block base is s[b:b+1] (tiled) or of the candidates
+  // at offsets `voff` (row-major: s[4:5] + row * n * 4)
+  void load_row(const Limb& d, uint32_t row, int b, const std::string& voff, const std::string& note) {
+    if (tiled) {
+      const uint64_t byte = (uint64_t)row * 256u, hi = byte & ~4095ull;
+      std::string base = "s[" + std::to_string(b) + ":" + std::to_string(b + 1) + "]";
+      if (hi) {
+        E.salu("s_add_u32 s40, " + S(b) + ", " + hexs((uint32_t)hi), {40});
+        E.salu("s_addc_u32 s41, " + S(b + 1) + ", 0", {41});
+        base = "s[40:41]";
+      }
+      E.mem("global_load_dword " + V(d.v) + ", v2, " + base + " offset:" + std::to_string(byte & 4095u) +
+            "  ; soa row " + std::to_string(row) + note);
+    } else {
+      row_ptr(row, 4);
+      E.mem("global_load_dword " + V(d.v) + ", " + voff + ", s[40:41]  ; soa row " + std::to_string(row) + note);
+    }
+  }
+  // s[d:d+1] = soa + g * coord_words * 256 for the group index in s[g]
+  void block_base(int d, int g) {
+    const uint32_t stride = P.coord_words * 256u;
+    E.salu("s_mul_i32 " + S(d) + ", " + S(g) + ", " + hexs(stride), {d});
+    E.salu("s_mul_hi_u32 " + S(d + 1) + ", " + S(g) + ", " + hexs(stride), {d + 1});
+    E.salu("s_add_u32 " + S(d) + ", " + S(d) + ", s4", {d});
+    E.salu("s_addc_u32 " + S(d + 1) + ", " + S(d + 1) + ", s5", {d + 1});
+  }
   void issue_rows(size_t upto) {
     while (rows_issued < rows.size() && rows_issued < upto) {
       const Limb d = fresh();
-      row_ptr(rows[rows_issued], 4);
-      E.mem("global_load_dword " + V(d.v) + ", v2, s[40:41]  ; soa row " + std::to_string(rows[rows_issued]));
+      load_row(d, rows[rows_issued], 26, "v2", "");
       row_seq[rows_issued] = loads++;
       row_reg[rows_issued++] = d;
     }
@@ -2292,9 +2323,7 @@ struct Gen {
       const size_t M = rows.size(), R = ring_reg.size();
       if (p + R >= M) {  // the next group's ring row p + R - M (clamped offsets: always in bounds)
         const size_t q = p + R - M;
-        row_ptr(rows[q], 4);
-        E.mem("global_load_dword " + V(ring_reg[q].v) + ", " + V(vnext.v) + ", s[40:41]  ; soa row " + std::to_string(rows[q]) +
-              " (next group)");
+        load_row(ring_reg[q], rows[q], 28, V(vnext.v), " (next group)");
         loads++;
       }
     }
@@ -2337,27 +2366,46 @@ struct Gen {
     // the ring: the first rows of the wave's first group, loaded before the loop
     ring_reg.clear();
     for (size_t q = 0; q < std::min<size_t>(prefetch_depth(), rows.size()); q++) ring_reg.push_back(fresh());
-    vnext = fresh();
+    vnext = tiled ? Limb{} : fresh();
+    if (tiled) {  // s31 = last group index, s32 = the grid stride in groups
+      E.salu("s_add_u32 s31, s8, 63", {31});
+      E.salu("s_lshr_b32 s31, s31, 6", {31});
+      E.salu("s_add_u32 s31, s31, -1", {31});
+      E.salu("s_lshr_b32 s32, s17, 6", {32});
+    }
     E.salu("s_cmp_lt_u32 s16, s8");
     E.ctl("s_cbranch_scc0 " + exit_);
     E.valu("v_add_u32_e32 v3, s16, v1", {16});
-    E.valu("v_min_u32_e32 v2, s23, v3", {23});
-    E.valu("v_lshlrev_b32_e32 v2, 2, v2");
-    for (size_t q = 0; q < ring_reg.size(); q++) {
-      row_ptr(rows[q], 4);
-      E.mem("global_load_dword " + V(ring_reg[q].v) + ", v2, s[40:41]  ; soa row " + std::to_string(rows[q]) + " (first group)");
+    if (tiled) {
+      E.valu("v_lshlrev_b32_e32 v2, 2, v1");  // lane * 4 inside the group's 256-byte row
+      E.salu("s_lshr_b32 s30, s16, 6", {30});
+      block_base(26, 30);
+    } else {
+      E.valu("v_min_u32_e32 v2, s23, v3", {23});
+      E.valu("v_lshlrev_b32_e32 v2, 2, v2");
     }
+    for (size_t q = 0; q < ring_reg.size(); q++) load_row(ring_reg[q], rows[q], 26, "v2", " (first group)");
     E.label(loop);
     E.salu("s_cmp_lt_u32 s16, s8");
     E.ctl("s_cbranch_scc0 " + exit_);
     // i = s16 + lane; v3 = i (store offset), v2 = 4 * min(i, n - 1) (load offset: lanes past n reread
     // the last candidate and store nothing); s[24:25] = lanes with i < n; vnext: the same for i + stride
+    // (tiled: v2 = 4 * lane, the blocks of this group and the next in s[26:27] / s[28:29]; the last
+    // block is whole in memory, so lanes past n read its padding)
     E.valu("v_add_u32_e32 v3, s16, v1", {16});
-    E.valu("v_min_u32_e32 v2, s23, v3", {23});
-    E.valu("v_lshlrev_b32_e32 v2, 2, v2");
-    E.valu("v_add_u32_e32 " + V(vnext.v) + ", s17, v3", {17});
-    E.valu("v_min_u32_e32 " + V(vnext.v) + ", s23, " + V(vnext.v), {23});
-    E.valu("v_lshlrev_b32_e32 " + V(vnext.v) + ", 2, " + V(vnext.v));
+    if (tiled) {
+      E.salu("s_lshr_b32 s30, s16, 6", {30});
+      block_base(26, 30);
+      E.salu("s_add_u32 s33, s30, s32", {33});
+      E.salu("s_min_u32 s33, s33, s31", {33});
+      block_base(28, 33);
+    } else {
+      E.valu("v_min_u32_e32 v2, s23, v3", {23});
+      E.valu("v_lshlrev_b32_e32 v2, 2, v2");
+      E.valu("v_add_u32_e32 " + V(vnext.v) + ", s17, v3", {17});
+      E.valu("v_min_u32_e32 " + V(vnext.v) + ", s23, " + V(vnext.v), {23});
+      E.valu("v_lshlrev_b32_e32 " + V(vnext.v) + ", 2, " + V(vnext.v));
+    }
     E.valu("v_cmp_gt_u32_e64 s[24:25], s8, v3", {8}, {24, 25});
     E.valu("v_lshlrev_b32_e32 v8, 2, v3");  // watch-row store offset 4 i
     E.salu("s_mov_b64 s[38:39], -1", {38, 39});
@@ -2368,7 +2416,7 @@ struct Gen {
     body("");
     if (rows_used != rows.size()) fail("internal: SoA rows left unread");
     for (const Limb& l : ring_reg) drop(l);
-    drop(vnext);
+    if (!tiled) drop(vnext);
     ring_reg.clear();
     for (int r = E.vfirst; r < 256; r++)
       if (E.vref[r]) fail("internal: VGPR v" + std::to_string(r) + " still held after the body");
@@ -2696,6 +2744,7 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
     o << kAsmMarker << "\n  .amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"\n  .amdhsa_code_object_version 6\n";
     if (kernels & JIT_EVAL) {  // the eval kernel alone (no generator)
       g.eval_kernel = true;
+      g.tiled = (kernels & JIT_EVAL_TILED) || getenv("MYTHGPU_JIT_ASM_TILED");
       g.analyse();
       // The HBM stream is latency-bound (rows in flight per wave x waves per SIMD): the row queue gets
       // the registers the kernel's occupancy step leaves (C2: 44 rows at 4 waves per SIMD; C4: ~40 at 2).

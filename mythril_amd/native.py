@@ -28,6 +28,22 @@ MG_E_NOTINIT = -6
 MG_SEARCH_EARLY_EXIT = 1
 MG_JIT_GEN_VERDICTS = 1
 MG_JIT_ASM = 2  # the first tier: gfx950 assembly emitted by the engine (jit_asm.cpp)
+MG_JIT_SOA_TILED = 4  # eval kernels read the tiled SoA (tile_soa)
+
+
+def tile_soa(soa):
+    """[row][candidate] SoA (rows x n, numpy or torch) -> the tiled layout MG_JIT_SOA_TILED kernels
+    read: word ((i // 64) * rows + r) * 64 + i % 64 (the last 64-candidate block zero-padded)."""
+    rows, n = soa.shape
+    blocks = (n + 63) // 64
+    pad = blocks * 64 - n
+    if hasattr(soa, "permute"):  # torch
+        import torch
+
+        x = torch.nn.functional.pad(soa, (0, pad)) if pad else soa
+        return x.reshape(rows, blocks, 64).permute(1, 0, 2).contiguous()
+    x = np.pad(soa, ((0, 0), (0, pad))) if pad else soa
+    return np.ascontiguousarray(x.reshape(rows, blocks, 64).transpose(1, 0, 2))
 NO_HIT = (1 << 64) - 1
 
 EXPORTS = [
@@ -226,7 +242,7 @@ def specialized_program(blob: bytes, gen_blob: Optional[np.ndarray] = None, keep
     return {"code": code, "consts": consts, "aux": aux, "widths": widths, "n_coords": ncoord}
 
 
-def jit_source(blob: bytes, gen_blob: Optional[np.ndarray] = None, compile: bool = False) -> str:
+def jit_source(blob: bytes, gen_blob: Optional[np.ndarray] = None, compile: bool = False, tiled: bool = False) -> str:
     """Host-only: the specialised HIP source of a program — the search kernel when a
     generator blob is given, else the eval kernel — optionally hipRTC-compiled (no GPU)."""
     lib = load_library()
@@ -234,14 +250,14 @@ def jit_source(blob: bytes, gen_blob: Optional[np.ndarray] = None, compile: bool
     gp = _ptr(g, C.c_uint32) if g is not None else None
     gn = 0 if g is None else g.size
     n = C.c_size_t()
-    _check(lib.mg_program_jit_source(_u8(blob), len(blob), gp, gn, 0, None, 0, C.byref(n)))
+    _check(lib.mg_program_jit_source(_u8(blob), len(blob), gp, gn, 2 if tiled else 0, None, 0, C.byref(n)))
     buf = C.create_string_buffer(n.value + 1)
-    _check(lib.mg_program_jit_source(_u8(blob), len(blob), gp, gn, 1 if compile else 0, buf, n.value + 1,
-                                     C.byref(n)))
+    _check(lib.mg_program_jit_source(_u8(blob), len(blob), gp, gn, (1 if compile else 0) | (2 if tiled else 0), buf,
+                                     n.value + 1, C.byref(n)))
     return buf.value.decode()
 
 
-def jit_asm(blob: bytes, gen_blob: Optional[np.ndarray] = None, compile: bool = False) -> str:
+def jit_asm(blob: bytes, gen_blob: Optional[np.ndarray] = None, compile: bool = False, tiled: bool = False) -> str:
     """Host-only: the first tier's gfx950 assembly — of a search program (mgj_search + mgj_gen)
     when a generator blob is given, else of the eval kernel (mgj_eval) — optionally assembled and
     linked through comgr (no GPU).  Raises EngineUnsupported for programs outside the tier."""
@@ -250,9 +266,10 @@ def jit_asm(blob: bytes, gen_blob: Optional[np.ndarray] = None, compile: bool = 
     gp = _ptr(g, C.c_uint32) if g is not None else None
     gn = 0 if g is None else g.size
     n = C.c_size_t()
-    _check(lib.mg_program_jit_asm(_u8(blob), len(blob), gp, gn, 0, None, 0, C.byref(n)))
+    _check(lib.mg_program_jit_asm(_u8(blob), len(blob), gp, gn, 2 if tiled else 0, None, 0, C.byref(n)))
     buf = C.create_string_buffer(n.value + 1)
-    _check(lib.mg_program_jit_asm(_u8(blob), len(blob), gp, gn, 1 if compile else 0, buf, n.value + 1, C.byref(n)))
+    _check(lib.mg_program_jit_asm(_u8(blob), len(blob), gp, gn, (1 if compile else 0) | (2 if tiled else 0), buf,
+                                  n.value + 1, C.byref(n)))
     return buf.value.decode()
 
 
@@ -367,10 +384,12 @@ class Engine:
         return (None if fh.value == NO_HIT else fh.value), nh.value
 
     # JIT-specialised kernels --------------------------------------
-    def jit_compile(self, prog: int, gen: int = 0, gen_verdicts: bool = False, asm: bool = False) -> int:
-        """``asm``: the first tier (assembly emitted by the engine; search programs only)."""
+    def jit_compile(self, prog: int, gen: int = 0, gen_verdicts: bool = False, asm: bool = False,
+                    tiled: bool = False) -> int:
+        """``asm``: the first tier (assembly emitted by the engine).  ``tiled`` (eval kernels): the
+        kernel reads the tiled SoA (:func:`tile_soa`; MG_JIT_SOA_TILED in mythgpu.h)."""
         h = C.c_uint64()
-        flags = (MG_JIT_GEN_VERDICTS if gen_verdicts else 0) | (MG_JIT_ASM if asm else 0)
+        flags = (MG_JIT_GEN_VERDICTS if gen_verdicts else 0) | (MG_JIT_ASM if asm else 0) | (MG_JIT_SOA_TILED if tiled else 0)
         _check(self.lib.mg_jit_compile_ex(prog, gen, flags, C.byref(h)))
         return h.value
 

@@ -178,7 +178,7 @@ def lift_literals(terms: Sequence[T.Term], min_width: int = 8):
 
 
 def gpu_eval_terms(engine, roots: Sequence[T.Term], watch_terms: Sequence[T.Term], assigns=None, n=64, seed=0,
-                   jit: bool = False, asm: bool = False):
+                   jit: bool = False, asm: bool = False, tiled: bool = False):
     """Evaluate on the GPU (the interpreter, or with ``jit`` the hipRTC-specialised eval kernel
     on the same runtime SoA inputs); returns (P, assigns, verdicts, per-candidate dict
     term-id -> value, per-candidate oracle models)."""
@@ -201,9 +201,12 @@ def gpu_eval_terms(engine, roots: Sequence[T.Term], watch_terms: Sequence[T.Term
     try:
         info = engine.info(prog)
         if jit or asm:
-            jh = engine.jit_compile(prog, 0, asm=asm)
+            jh = engine.jit_compile(prog, 0, asm=asm, tiled=tiled)
             try:
-                ver, watch = engine.jit_eval(jh, soa, len(assigns), watch_words=info.watch_words)
+                from mythril_amd.native import tile_soa
+
+                ver, watch = engine.jit_eval(jh, tile_soa(soa) if tiled else soa, len(assigns),
+                                             watch_words=info.watch_words)
             finally:
                 engine.jit_free(jh)
         else:

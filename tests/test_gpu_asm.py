@@ -211,6 +211,16 @@ def test_asm_tier_hard_needle_full_size(engine):
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("seed", range(16))
 def test_asm_eval_random_programs_terms(engine, seed):
+    _eval_terms(engine, seed, tiled=False)
+
+
+@pytest.mark.parametrize("seed", range(0, 16, 3))
+def test_asm_eval_random_programs_terms_tiled(engine, seed):
+    """The same on the tiled SoA (MG_JIT_SOA_TILED): watch rows and verdicts unchanged."""
+    _eval_terms(engine, seed, tiled=True)
+
+
+def _eval_terms(engine, seed, tiled):
     """``Model.eval`` batched on the first tier's eval kernel: every watched term's value and every
     verdict equal the Python oracle's on edge-value assignments (``oracle/bv.py``, the reference's
     ``model.eval(..., model_completion=True)``), as the O3 eval kernel's do."""
@@ -224,7 +234,7 @@ def test_asm_eval_random_programs_terms(engine, seed):
     except native.EngineUnsupported as e:
         pytest.skip(f"outside the tier: {e}")
     watch = [t for t in T.postorder(roots) if t.sort[0] == "bv"][:24]
-    P, assigns, ver, vals, models = gpu_eval_terms(engine, roots, watch, n=200, seed=seed, asm=True)
+    P, assigns, ver, vals, models = gpu_eval_terms(engine, roots, watch, n=200, seed=seed, asm=True, tiled=tiled)
     for i, m in enumerate(models):
         want = evaluate_many(list(roots) + watch, m)
         assert ver[i] == int(all(want[:len(roots)])), (seed, i)
@@ -232,14 +242,17 @@ def test_asm_eval_random_programs_terms(engine, seed):
             assert vals[i][t.id] == want[len(roots) + k], (seed, i, k)
 
 
+@pytest.mark.parametrize("tiled", [False, True])
 @pytest.mark.parametrize("n", [5000 + 37, (1 << 18) + 37])
 @pytest.mark.parametrize("name", ["token_transfer_underflow", "suicide_kill", "etherstore_reentrancy",
                                   "walletlibrary_kill"])
-def test_asm_eval_workload_verdicts(engine, name, n):
+def test_asm_eval_workload_verdicts(engine, name, n, tiled):
     """The unspecialised workload program on random SoA rows: the first tier's eval verdicts equal
     the C port's (``oracle/bveval.c`` eval) and the O3 eval kernel's, at an n that leaves a partial
     last wave; at 2^18 + 37 every wave sweeps several groups, so the next group's rows loaded while
-    the current group finishes (the cross-group row ring) are exercised."""
+    the current group finishes (the cross-group row ring) are exercised.  ``tiled``: both kernels
+    compiled for the tiled SoA (MG_JIT_SOA_TILED) read the same data re-laid (native.tile_soa),
+    against the C port on the row-major original."""
     from oracle import cport
 
     P, _ = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
@@ -257,11 +270,12 @@ def test_asm_eval_workload_verdicts(engine, name, n):
         for j in range(ssa.limbs(c.width)):
             bits = min(32, c.width - 32 * j)
             soa[offs[c.index] + j] &= np.uint32((1 << bits) - 1)
-    ja = engine.jit_compile(prog, 0, asm=True)
-    jo = engine.jit_compile(prog, 0)
+    ja = engine.jit_compile(prog, 0, asm=True, tiled=tiled)
+    jo = engine.jit_compile(prog, 0, tiled=tiled)
+    src = native.tile_soa(soa) if tiled else soa
     try:
-        va, _ = engine.jit_eval(ja, soa, n)
-        vo, _ = engine.jit_eval(jo, soa, n)
+        va, _ = engine.jit_eval(ja, src, n)
+        vo, _ = engine.jit_eval(jo, src, n)
     finally:
         engine.jit_free(ja)
         engine.jit_free(jo)
