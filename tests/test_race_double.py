@@ -49,7 +49,9 @@ def test_race_unsat_costs_only_z3_time(mythril_standin):
     assert not S.calls  # the reference's path never ran: z3 answered once, in the race
     # the race ran the reference's check: its timeout, on a worker thread
     name, timeout, _, result = z3.Optimize.calls[-1]
-    assert name.startswith("mythgpu-z3") and timeout == 9_500 and result is z3.unsat  # min(solver_timeout, remaining - 500)
+    # min(solver_timeout, remaining - 500), less the time the check waited for a z3 worker (a few
+    # ms when the machine is loaded)
+    assert name.startswith("mythgpu-z3") and 9_300 <= timeout <= 9_500 and result is z3.unsat
     assert plugin.STATS.z3_answers == 7 and plugin.STATS.races == 7
     assert _Stats().query_count == 7  # counted where stat_smt_query would have counted it
 
