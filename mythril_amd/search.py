@@ -550,7 +550,11 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                 if rate:
                     cap_s = left
                     if ticket is not None or ticket_asm is not None:
-                        cap_s = min(left, JIT_FIRST_POLL_S if now - tc < 5 * JIT_FIRST_POLL_S else JIT_POLL_S)
+                        # 1-ms launches while the first tier is due (a few ms; measured cadence: a 10-ms
+                        # launch started at 5 ms turned a 5.5-ms compile into a 15-ms switch)
+                        short = now - tc < max(5 * JIT_FIRST_POLL_S,
+                                               4 * expected_asm if ticket_asm is not None else 0.0)
+                        cap_s = min(left, JIT_FIRST_POLL_S if short else JIT_POLL_S)
                     if max_launch_s is not None:
                         cap_s = min(cap_s, max_launch_s)
                     n = max(1, min(n, int(rate * cap_s)))
