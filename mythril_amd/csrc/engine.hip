@@ -431,10 +431,27 @@ __device__ __forceinline__ uint32_t compare(const VF& vf, uint32_t op, uint32_t 
 // checks of arithmetic); kTierHeavy adds division, EXP and Keccak, whose 256-bit temporaries
 // hold ~220 VGPRs (two waves per SIMD).  Leaving handlers out lets more waves hide the LDS and
 // scalar-load latency.
-template <class VF, int MODE, int TIER>
-__device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, uint64_t i, const GKeys& key,
-                                                bool early, bool active) {
-  uint32_t verdict = 1;
+// One wave evaluates KG groups of 64 candidates per program pass: every dispatched instruction (its
+// scalar fetch, decode and jump) runs its handler once per group, on the group's slice of the value
+// file (VFG: slot-major, [slot][group][lane]).  verdict[g], i[g], key[g], active[g] are per group.
+template <class VF, int KG>
+struct VFG {
+  VF f;
+  uint32_t g;
+  __device__ __forceinline__ uint32_t& at(uint32_t w) const { return f.at(w * KG + g); }
+};
+
+#define MG_FOR_G(...)                                   \
+  _Pragma("unroll") for (uint32_t g = 0; g < (uint32_t)KG; g++) { \
+    const VFG<VF, KG> vf{vf0, g};                       \
+    __VA_ARGS__                                         \
+  }
+
+template <class VF, int MODE, int TIER, int KG>
+__device__ __forceinline__ void run_program(const KArgs& k, const VF& vf0, const uint64_t* i, const GKeys* key,
+                                            bool early, const bool* active, uint32_t* verdict) {
+#pragma unroll
+  for (int g = 0; g < KG; g++) verdict[g] = 1;
   const uint32_t n_instr = k.n_instr;
   // the next instruction's scalar load is issued before this one executes, so its latency
   // overlaps this instruction's LDS traffic instead of adding to it (the code buffer has
@@ -449,179 +466,213 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
     switch (in.op) {
       case K_CONST: {
         const auto* c = cst(k.consts) + in.p0;
-        MG_LIMBS(L, vf.at(in.dst + j) = c[j];);
+        MG_FOR_G(MG_LIMBS(L, vf.at(in.dst + j) = c[j];););
         break;
       }
       case K_COORD: {
         if (MODE == MODE_EVAL) {
-          MG_LIMBS(L, vf.at(in.dst + j) = k.soa[(uint64_t)(in.p1 + j) * k.count + i];);
+          MG_FOR_G(MG_LIMBS(L, vf.at(in.dst + j) = k.soa[(uint64_t)(in.p1 + j) * k.count + i[g]];););
         } else {
-          gen_coord<VF>(k, vf, in.dst, in.p0, W, key);
+          MG_FOR_G(gen_coord<VFG<VF, KG>>(k, vf, in.dst, in.p0, W, key[g]););
         }
         break;
       }
       case K_COPY: {
-        MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j););
+        MG_FOR_G(MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j);););
         break;
       }
       case K_ADD: {
-        uint32_t c = 0;
-        MG_LIMBS(L, vf.at(in.dst + j) = __builtin_addc(vf.at(in.a + j), vf.at(in.b + j), c, &c););
-        write_masked(vf, in.dst, L, W);
+        MG_FOR_G({
+          uint32_t c = 0;
+          MG_LIMBS(L, vf.at(in.dst + j) = __builtin_addc(vf.at(in.a + j), vf.at(in.b + j), c, &c););
+          write_masked(vf, in.dst, L, W);
+        });
         break;
       }
       case K_SUB: {
-        uint32_t c = 0;
-        MG_LIMBS(L, vf.at(in.dst + j) = __builtin_subc(vf.at(in.a + j), vf.at(in.b + j), c, &c););
-        write_masked(vf, in.dst, L, W);
+        MG_FOR_G({
+          uint32_t c = 0;
+          MG_LIMBS(L, vf.at(in.dst + j) = __builtin_subc(vf.at(in.a + j), vf.at(in.b + j), c, &c););
+          write_masked(vf, in.dst, L, W);
+        });
         break;
       }
       case K_NEG: {
-        uint32_t c = 0;
-        MG_LIMBS(L, vf.at(in.dst + j) = __builtin_subc(0u, vf.at(in.a + j), c, &c););
-        write_masked(vf, in.dst, L, W);
+        MG_FOR_G({
+          uint32_t c = 0;
+          MG_LIMBS(L, vf.at(in.dst + j) = __builtin_subc(0u, vf.at(in.a + j), c, &c););
+          write_masked(vf, in.dst, L, W);
+        });
         break;
       }
       case K_AND:
-        MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) & vf.at(in.b + j););
+        MG_FOR_G(MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) & vf.at(in.b + j);););
         break;
       case K_OR:
-        MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) | vf.at(in.b + j););
+        MG_FOR_G(MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) | vf.at(in.b + j);););
         break;
       case K_XOR:
-        MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) ^ vf.at(in.b + j););
+        MG_FOR_G(MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) ^ vf.at(in.b + j);););
         break;
       case K_NOT:
-        MG_LIMBS(L, vf.at(in.dst + j) = ~vf.at(in.a + j););
-        write_masked(vf, in.dst, L, W);
+        MG_FOR_G({
+          MG_LIMBS(L, vf.at(in.dst + j) = ~vf.at(in.a + j););
+          write_masked(vf, in.dst, L, W);
+        });
         break;
       case K_ITE: {
-        const bool c = vf.at(in.a) != 0;
-        MG_LIMBS(L, vf.at(in.dst + j) = c ? vf.at(in.b + j) : vf.at(in.c + j););
+        MG_FOR_G({
+          const bool c = vf.at(in.a) != 0;
+          MG_LIMBS(L, vf.at(in.dst + j) = c ? vf.at(in.b + j) : vf.at(in.c + j););
+        });
         break;
       }
       case K_EQ: {
         const uint32_t La = (in.p1 + 31) >> 5;
-        uint32_t d = 0;
-        MG_LIMBS(La, d |= vf.at(in.a + j) ^ vf.at(in.b + j););
-        vf.at(in.dst) = d == 0;
+        MG_FOR_G({
+          uint32_t d = 0;
+          MG_LIMBS(La, d |= vf.at(in.a + j) ^ vf.at(in.b + j););
+          vf.at(in.dst) = d == 0;
+        });
         break;
       }
       case K_ULT:
       case K_ULE:
       case K_SLT:
       case K_SLE:
-        vf.at(in.dst) = compare(vf, in.op, in.a, in.b, in.p1);
+        MG_FOR_G(vf.at(in.dst) = compare(vf, in.op, in.a, in.b, in.p1););
         break;
       case K_ASSERT_CMP: {
         // a compare whose one use was this assert (program.cpp: fuse_asserts)
-        verdict &= compare(vf, in.p0 & 0xFFu, in.a, in.b, in.p1) ^ (in.p0 >> 8);
-        if (early && __builtin_amdgcn_readfirstlane((uint32_t)(__ballot(verdict != 0) != 0ull)) == 0u) stop = true;
+        uint64_t any = 0;
+        MG_FOR_G({
+          verdict[g] &= compare(vf, in.p0 & 0xFFu, in.a, in.b, in.p1) ^ (in.p0 >> 8);
+          any |= __ballot(verdict[g] != 0);
+        });
+        if (early && __builtin_amdgcn_readfirstlane((uint32_t)(any != 0ull)) == 0u) stop = true;
         break;
       }
       case K_CONCAT: {
         // dst = a:b, width(b) = p1
         const uint32_t wb = in.p1, wa = W - wb;
-        for (uint32_t j = 0; j < L; j++) {
-          const uint32_t p = j * 32;
-          uint32_t v = bits32(vf, in.b, wb, p);
-          if (p + 32 > wb) {
-            v |= (p >= wb) ? bits32(vf, in.a, wa, p - wb) : (bits32(vf, in.a, wa, 0) << (wb - p));
+        MG_FOR_G({
+          for (uint32_t j = 0; j < L; j++) {
+            const uint32_t p = j * 32;
+            uint32_t v = bits32(vf, in.b, wb, p);
+            if (p + 32 > wb) {
+              v |= (p >= wb) ? bits32(vf, in.a, wa, p - wb) : (bits32(vf, in.a, wa, 0) << (wb - p));
+            }
+            vf.at(in.dst + j) = v;
           }
-          vf.at(in.dst + j) = v;
-        }
-        write_masked(vf, in.dst, L, W);
+          write_masked(vf, in.dst, L, W);
+        });
         break;
       }
       case K_EXTRACT: {
-        if (L == 1) {
-          vf.at(in.dst) = bits32(vf, in.a, in.p1, in.p0);
-        } else {
-          for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = bits32(vf, in.a, in.p1, in.p0 + j * 32);
-        }
-        write_masked(vf, in.dst, L, W);
+        MG_FOR_G({
+          if (L == 1) {
+            vf.at(in.dst) = bits32(vf, in.a, in.p1, in.p0);
+          } else {
+            for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = bits32(vf, in.a, in.p1, in.p0 + j * 32);
+          }
+          write_masked(vf, in.dst, L, W);
+        });
         break;
       }
       case K_ZEXT:
       case K_SEXT: {
         const uint32_t wa = in.p1, La = (wa + 31) >> 5;
-        uint32_t fill = 0;
-        if (in.op == K_SEXT) fill = ((vf.at(in.a + La - 1) >> ((wa - 1) & 31)) & 1u) ? 0xFFFFFFFFu : 0u;
         const uint32_t tm = top_mask(wa);
-        MG_LIMBS(L, {
-          uint32_t v = fill;
-          if (j < La) {
-            v = vf.at(in.a + j);
-            if (j == La - 1) v = (v & tm) | (fill & ~tm);
-          }
-          vf.at(in.dst + j) = v;
+        MG_FOR_G({
+          uint32_t fill = 0;
+          if (in.op == K_SEXT) fill = ((vf.at(in.a + La - 1) >> ((wa - 1) & 31)) & 1u) ? 0xFFFFFFFFu : 0u;
+          MG_LIMBS(L, {
+            uint32_t v = fill;
+            if (j < La) {
+              v = vf.at(in.a + j);
+              if (j == La - 1) v = (v & tm) | (fill & ~tm);
+            }
+            vf.at(in.dst + j) = v;
+          });
+          write_masked(vf, in.dst, L, W);
         });
-        write_masked(vf, in.dst, L, W);
         break;
       }
       case K_MUL: {
         if constexpr (TIER >= kTierMid) {
-          W8 r = mul8(ld8(vf, in.a, L), ld8(vf, in.b, L));
-          canon8(r, W);
-          st8(vf, in.dst, L, r);
+          MG_FOR_G({
+            W8 r = mul8(ld8(vf, in.a, L), ld8(vf, in.b, L));
+            canon8(r, W);
+            st8(vf, in.dst, L, r);
+          });
         }
         break;
       }
       case K_UMUL_NOOVF: {
         if constexpr (TIER >= kTierMid) {
           const uint32_t wa = in.p1, La = (wa + 31) >> 5;
-          vf.at(in.dst) = umul_noovf8(ld8(vf, in.a, La), ld8(vf, in.b, La), wa);
+          MG_FOR_G(vf.at(in.dst) = umul_noovf8(ld8(vf, in.a, La), ld8(vf, in.b, La), wa););
         }
         break;
       }
-      case K_UDIV: if constexpr (TIER >= kTierHeavy) { st8(vf, in.dst, L, bv_udiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_UREM: if constexpr (TIER >= kTierHeavy) { st8(vf, in.dst, L, bv_urem(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_SDIV: if constexpr (TIER >= kTierHeavy) { st8(vf, in.dst, L, bv_sdiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_SREM: if constexpr (TIER >= kTierHeavy) { st8(vf, in.dst, L, bv_srem(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_SMOD: if constexpr (TIER >= kTierHeavy) { st8(vf, in.dst, L, bv_smod(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_SHL: if constexpr (TIER >= kTierMid) { st8(vf, in.dst, L, bv_shl(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_LSHR: if constexpr (TIER >= kTierMid) { st8(vf, in.dst, L, bv_lshr(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_ASHR: if constexpr (TIER >= kTierMid) { st8(vf, in.dst, L, bv_ashr(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
-      case K_EXP: if constexpr (TIER >= kTierHeavy) { st8(vf, in.dst, L, bv_exp(ld8(vf, in.a, L), ld8(vf, in.b, L), W)); } break;
+      case K_UDIV: if constexpr (TIER >= kTierHeavy) { MG_FOR_G(st8(vf, in.dst, L, bv_udiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W));); } break;
+      case K_UREM: if constexpr (TIER >= kTierHeavy) { MG_FOR_G(st8(vf, in.dst, L, bv_urem(ld8(vf, in.a, L), ld8(vf, in.b, L), W));); } break;
+      case K_SDIV: if constexpr (TIER >= kTierHeavy) { MG_FOR_G(st8(vf, in.dst, L, bv_sdiv(ld8(vf, in.a, L), ld8(vf, in.b, L), W));); } break;
+      case K_SREM: if constexpr (TIER >= kTierHeavy) { MG_FOR_G(st8(vf, in.dst, L, bv_srem(ld8(vf, in.a, L), ld8(vf, in.b, L), W));); } break;
+      case K_SMOD: if constexpr (TIER >= kTierHeavy) { MG_FOR_G(st8(vf, in.dst, L, bv_smod(ld8(vf, in.a, L), ld8(vf, in.b, L), W));); } break;
+      case K_SHL: if constexpr (TIER >= kTierMid) { MG_FOR_G(st8(vf, in.dst, L, bv_shl(ld8(vf, in.a, L), ld8(vf, in.b, L), W));); } break;
+      case K_LSHR: if constexpr (TIER >= kTierMid) { MG_FOR_G(st8(vf, in.dst, L, bv_lshr(ld8(vf, in.a, L), ld8(vf, in.b, L), W));); } break;
+      case K_ASHR: if constexpr (TIER >= kTierMid) { MG_FOR_G(st8(vf, in.dst, L, bv_ashr(ld8(vf, in.a, L), ld8(vf, in.b, L), W));); } break;
+      case K_EXP: if constexpr (TIER >= kTierHeavy) { MG_FOR_G(st8(vf, in.dst, L, bv_exp(ld8(vf, in.a, L), ld8(vf, in.b, L), W));); } break;
       case K_LOOKUP: {
         const uint32_t Lk = (in.b + 31) >> 5;
-        uint32_t src = in.p0;
-        bool found = false;
-        for (uint32_t p = 0; p < in.c; p++) {
-          const uint32_t ko = cst(k.aux)[in.p1 + 2 * p], vo = cst(k.aux)[in.p1 + 2 * p + 1];
-          uint32_t d = 0;
-          MG_LIMBS(Lk, d |= vf.at(in.a + j) ^ vf.at(ko + j););
-          const bool hit = !found && d == 0;
-          src = hit ? vo : src;
-          found = found || hit;
-        }
-        // src differs per lane: gather the limbs from the selected slot
-        MG_LIMBS(L, vf.at(in.dst + j) = vf.at(src + j););
+        MG_FOR_G({
+          uint32_t src = in.p0;
+          bool found = false;
+          for (uint32_t p = 0; p < in.c; p++) {
+            const uint32_t ko = cst(k.aux)[in.p1 + 2 * p], vo = cst(k.aux)[in.p1 + 2 * p + 1];
+            uint32_t d = 0;
+            MG_LIMBS(Lk, d |= vf.at(in.a + j) ^ vf.at(ko + j););
+            const bool hit = !found && d == 0;
+            src = hit ? vo : src;
+            found = found || hit;
+          }
+          // src differs per lane: gather the limbs from the selected slot
+          MG_LIMBS(L, vf.at(in.dst + j) = vf.at(src + j););
+        });
         break;
       }
       case K_KECCAK: {
         if (in.a == MG_NONE) {
           // keccak256("") — the constant of keccak_function_manager.py:75-81
-          for (uint32_t j = 0; j < 8; j++) vf.at(in.dst + j) = kEmptyKeccak[j];
+          MG_FOR_G(for (uint32_t j = 0; j < 8; j++) vf.at(in.dst + j) = kEmptyKeccak[j];);
         } else if constexpr (TIER >= kTierHeavy) {
-          do_keccak(vf, in);
+          MG_FOR_G(do_keccak(vf, in););
         }
         break;
       }
       case K_ASSERT: {
-        verdict &= vf.at(in.a);
-        // every lane failed: stop (verdict is 0 everywhere).  A loop flag, not a return: a second
-        // loop exit made the compiler keep pc in a VGPR (vector address math + readfirstlane per
-        // fetch); readfirstlane makes the flag's uniformity explicit
-        if (early && __builtin_amdgcn_readfirstlane((uint32_t)(__ballot(verdict != 0) != 0ull)) == 0u) stop = true;
+        // every lane of every group failed: stop (verdicts are 0 everywhere).  A loop flag, not a
+        // return: a second loop exit made the compiler keep pc in a VGPR (vector address math +
+        // readfirstlane per fetch); readfirstlane makes the flag's uniformity explicit
+        uint64_t any = 0;
+        MG_FOR_G({
+          verdict[g] &= vf.at(in.a);
+          any |= __ballot(verdict[g] != 0);
+        });
+        if (early && __builtin_amdgcn_readfirstlane((uint32_t)(any != 0ull)) == 0u) stop = true;
         break;
       }
       case K_WATCH: {
-        if (MODE != MODE_SEARCH && k.watch && active) {
-          for (uint32_t j = 0; j < L; j++) k.watch[(uint64_t)(in.p0 + j) * k.count + i] = vf.at(in.a + j);
+        if (MODE != MODE_SEARCH && k.watch) {
+          MG_FOR_G({
+            if (active[g])
+              for (uint32_t j = 0; j < L; j++) k.watch[(uint64_t)(in.p0 + j) * k.count + i[g]] = vf.at(in.a + j);
+          });
         } else if (MODE == MODE_SEARCH && k.watch) {
-          // capture launch (one group per block): every lane's watch rows, [block][row][lane],
+          // capture launch (one group per block, KG = 1): every lane's watch rows, [block][row][lane],
           // so the first hit's model is read back without a second program pass
+          const VFG<VF, KG> vf{vf0, 0};
           uint32_t* w = k.watch + ((uint64_t)blockIdx.x * k.watch_words + in.p0) * kWave + threadIdx.x;
           for (uint32_t j = 0; j < L; j++) w[(uint64_t)j * kWave] = vf.at(in.a + j);
         }
@@ -631,7 +682,6 @@ __device__ __forceinline__ uint32_t run_program(const KArgs& k, const VF& vf, ui
         break;
     }
   }
-  return verdict;
 }
 
 // one lane's column of a capture block: dst[r] = src[r * 64] (mg_search model read-back)
@@ -641,16 +691,17 @@ __global__ void __launch_bounds__(256) k_gather_rows(const uint32_t* __restrict_
   if (r < rows) dst[r] = src[(uint64_t)r * kWave];
 }
 
-template <class VF, int MODE, int TIER>
+template <class VF, int MODE, int TIER, int KG>
 __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
   extern __shared__ uint32_t lds[];
-  VF vf(lds, k);
+  VF vf0(lds, k);
   // EVAL sweeps rows [0, count); GEN / SEARCH sweep the aligned 64-index groups that
   // cover [start, start + count), one group per wave (the GEN3 group key is per wave)
   const uint64_t a0 = (MODE == MODE_EVAL) ? 0ull : (k.start & ~63ull);
   const uint64_t end = k.start + k.count;
   const uint64_t total = (MODE == MODE_EVAL) ? k.count : (end - a0);
-  const uint64_t step = (uint64_t)gridDim.x * kWave;
+  // KG groups per wave per pass (run_program): a wave's pass covers KG * 64 consecutive indices
+  const uint64_t step = (uint64_t)gridDim.x * kWave * KG;
   const bool early = (MODE == MODE_SEARCH) && (k.flags & MG_SEARCH_EARLY_EXIT);
   uint64_t wave_best = ~0ull, wave_hits = 0;  // wave-uniform; published once per wave
   // idx & 63 == threadIdx.x & 63 below (a0 and base are multiples of 64): the lane half of
@@ -681,14 +732,20 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
     const Instr in = ld_instr(k, pc);
     const uint32_t L = (in.wd + 31) >> 5;
     const auto* c = cst(k.consts) + in.p0;
-    MG_LIMBS(L, vf.at(in.dst + j) = c[j];);
+    MG_FOR_G(MG_LIMBS(L, vf.at(in.dst + j) = c[j];););
   }
-  for (uint64_t base = (uint64_t)blockIdx.x * kWave; base < total; base += step) {
-    const uint64_t off = base + threadIdx.x;
-    const uint64_t idx = a0 + off;  // candidate index (GEN / SEARCH)
-    const bool active = (MODE == MODE_EVAL) ? off < total : (idx >= k.start && idx < end);
-    // EVAL: SoA row; GEN: output row (only written by active lanes)
-    const uint64_t i = (MODE == MODE_EVAL) ? (active ? off : total - 1) : (idx - k.start);
+  for (uint64_t base = (uint64_t)blockIdx.x * kWave * KG; base < total; base += step) {
+    bool active[KG];
+    uint64_t i[KG];
+    GKeys key[KG];
+#pragma unroll
+    for (int g = 0; g < KG; g++) {
+      const uint64_t off = base + (uint64_t)g * kWave + threadIdx.x;
+      const uint64_t idx = a0 + off;  // candidate index (GEN / SEARCH)
+      active[g] = (MODE == MODE_EVAL) ? off < total : (idx >= k.start && idx < end);
+      // EVAL: SoA row; GEN: output row (only written by active lanes)
+      i[g] = (MODE == MODE_EVAL) ? (active[g] ? off : total - 1) : (idx - k.start);
+    }
     if (early) {
       // every candidate below the current first hit is still evaluated, so the
       // final minimum is exact; waves entirely above it stop
@@ -699,28 +756,32 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
                              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cur);
       if (a0 + base >= cur_u) break;
     }
-    GKeys key{};
-    // the group key from the wave's group base (a0 + base, a multiple of 64: idx >> 6 is the same for
+    // each group's key from its base (a0 + base + 64 g, a multiple of 64: idx >> 6 is the same for
     // every lane), so the compiler sees G as wave-uniform: the MIXED alternatives are scalar branches
     // and the generator specs scalar loads (from idx, G looked per-lane: divergent branches, vector loads)
-    if (MODE != MODE_EVAL) key = gen_keys_lk(a0 + base, lk, k.sg);
-    uint32_t v = run_program<VF, MODE, TIER>(k, vf, i, key, early, active);
-    v = active ? v : 0u;
-    if (MODE == MODE_SEARCH) {
-      const unsigned long long m = __ballot(v != 0);
-      if (m) {
-        const uint64_t first = a0 + base + (uint64_t)(__ffsll((long long)m) - 1);
-        wave_hits += (uint64_t)__popcll(m);
-        if (first < wave_best) {
-          wave_best = first;
-          if (early && threadIdx.x == 0) {
-            atomicMin(k.first_hit, (unsigned long long)first);
-            publish_peers(k.first_hit, (unsigned long long)first);
+#pragma unroll
+    for (int g = 0; g < KG; g++) key[g] = MODE != MODE_EVAL ? gen_keys_lk(a0 + base + (uint64_t)g * kWave, lk, k.sg) : GKeys{};
+    uint32_t v[KG];
+    run_program<VF, MODE, TIER, KG>(k, vf0, i, key, early, active, v);
+#pragma unroll
+    for (int g = 0; g < KG; g++) {
+      v[g] = active[g] ? v[g] : 0u;
+      if (MODE == MODE_SEARCH) {
+        const unsigned long long m = __ballot(v[g] != 0);
+        if (m) {
+          const uint64_t first = a0 + base + (uint64_t)g * kWave + (uint64_t)(__ffsll((long long)m) - 1);
+          wave_hits += (uint64_t)__popcll(m);
+          if (first < wave_best) {
+            wave_best = first;
+            if (early && threadIdx.x == 0) {
+              atomicMin(k.first_hit, (unsigned long long)first);
+              publish_peers(k.first_hit, (unsigned long long)first);
+            }
           }
         }
+      } else if (active[g]) {
+        k.verdict[i[g]] = (uint8_t)v[g];
       }
-    } else if (active) {
-      k.verdict[i] = (uint8_t)v;
     }
   }
   if (MODE == MODE_SEARCH && threadIdx.x == 0) {
@@ -1123,15 +1184,35 @@ static int ensure_scratch(Engine& e, size_t bytes) {
 // grid: enough waves to fill 256 CUs several times over, never more than needed.
 // Resident waves per CU: the LDS value file (160 KiB per CU) and the VGPRs of the
 // kernel variant (heavy ~230: 2 waves/SIMD; mid: 4; light ~50: 8 waves/SIMD).
-static uint32_t grid_for(const Engine& e, uint64_t count, bool lds, uint32_t value_words, int tier) {
-  uint64_t want = (count + kWave - 1) / kWave;
+static uint32_t grid_for(const Engine& e, uint64_t count, bool lds, uint32_t value_words, int tier, int kg = 1) {
+  uint64_t want = (count + (uint64_t)kWave * kg - 1) / ((uint64_t)kWave * kg);
   uint32_t waves_per_cu = tier == kTierHeavy ? 8 : tier == kTierMid ? 16 : 32;
   if (lds) {
-    const uint32_t bytes = value_words * kWave * 4;
+    const uint32_t bytes = value_words * kWave * 4 * (uint32_t)kg;
     waves_per_cu = std::max<uint32_t>(1, std::min<uint32_t>(waves_per_cu, (160u * 1024u) / std::max<uint32_t>(bytes, 1)));
   }
   uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * waves_per_cu * 4;
   return (uint32_t)std::max<uint64_t>(1, std::min(want, cap));
+}
+
+// k_run's groups per wave per pass: MYTHGPU_INTERP_KG=2|4 where allowed, else 1.  Measured at 2^22
+// per launch (profiles/r04n_interp_kg.jsonl): KG 2 / 4 cost C2 35 % / 63 % (5.18 -> 3.35 / 1.94
+// G/s), C1 21 % / 53 %, C3 15 % / 44 %, C4 (its file is in global memory: KG 1) unchanged — the
+// interpreter waits on LDS and scalar-load latency, which only more resident waves hide, and KG
+// divides the waves an LDS-resident value file leaves per CU; the dispatch it amortises is not the
+// limiter.  So the default stays 1.
+static int interp_kg(int mode, bool lds, bool capture, int tier, uint32_t value_words, uint64_t lanes, int cus) {
+  static const int forced = [] {
+    const char* g = getenv("MYTHGPU_INTERP_KG");
+    const int v = g ? atoi(g) : 0;
+    return v == 1 || v == 2 || v == 4 ? v : 0;
+  }();
+  if (mode == MODE_EVAL || !lds || capture || tier == kTierHeavy) return 1;
+  int kg = forced ? forced : 1;
+  while (kg > 1 && (value_words * (uint32_t)kg * kWave * 4u > 160u * 1024u ||
+                    lanes < (uint64_t)std::max(cus, 1) * 4u * kWave * (uint64_t)kg))
+    kg /= 2;
+  return kg;
 }
 
 // enqueue one interpreter launch on e's stream (e's device must be current); bracketed by
@@ -1145,7 +1226,11 @@ static int launch_async(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   // file would fetch from L2 at every operand are what such a launch waits on, and it needs no
   // occupancy.  Larger launches trade the other way (C4 at 255: 20 % slower).
   const bool lds = p.lds || (p.low.value_words <= 255u && lanes <= (uint64_t)std::max(e.cu_count, 1) * 2u * kWave);
-  const uint32_t grid = grid_for(e, lanes, lds, p.low.value_words, p.tier);
+  // groups per wave per program pass (k_run KG): one dispatched instruction serves KG x 64 candidates,
+  // at KG x the value file in LDS.  Search / gen launches with the file in LDS, no capture, not the
+  // heavy tier (its 256-bit temporaries), and a launch big enough to fill the chip at KG
+  const int kg = interp_kg(MODE, lds, k.watch != nullptr, p.tier, p.low.value_words, lanes, e.cu_count);
+  const uint32_t grid = grid_for(e, lanes, lds, p.low.value_words, p.tier, kg);
   k.sk = seed_lane_key(k.seed);
   k.sg = seed_group_key(k.seed);
   k.code = p.d_code;
@@ -1170,18 +1255,36 @@ static int launch_async(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
     if (rc) return rc;
     k.scratch = e.d_scratch;
   }
-  const size_t shmem = lds ? (size_t)p.low.value_words * kWave * 4 : 0;
+  const size_t shmem = lds ? (size_t)p.low.value_words * kWave * 4 * kg : 0;
   HIPCHK(hipEventRecord(e.ev0, e.stream));
   const dim3 g(grid), b(kWave);
+#define MG_RUN(VFT, TIERC, KGC) hipLaunchKernelGGL((k_run<VFT, MODE, TIERC, KGC>), g, b, shmem, e.stream, k)
   if (lds) {
-    if (p.tier == kTierHeavy) hipLaunchKernelGGL((k_run<VFLds, MODE, kTierHeavy>), g, b, shmem, e.stream, k);
-    else if (p.tier == kTierMid) hipLaunchKernelGGL((k_run<VFLds, MODE, kTierMid>), g, b, shmem, e.stream, k);
-    else hipLaunchKernelGGL((k_run<VFLds, MODE, kTierLight>), g, b, shmem, e.stream, k);
+    if (p.tier == kTierHeavy) {
+      MG_RUN(VFLds, kTierHeavy, 1);
+    } else if (p.tier == kTierMid) {
+      if constexpr (MODE != MODE_EVAL) {
+        if (kg == 4) MG_RUN(VFLds, kTierMid, 4);
+        else if (kg == 2) MG_RUN(VFLds, kTierMid, 2);
+        else MG_RUN(VFLds, kTierMid, 1);
+      } else {
+        MG_RUN(VFLds, kTierMid, 1);
+      }
+    } else {
+      if constexpr (MODE != MODE_EVAL) {
+        if (kg == 4) MG_RUN(VFLds, kTierLight, 4);
+        else if (kg == 2) MG_RUN(VFLds, kTierLight, 2);
+        else MG_RUN(VFLds, kTierLight, 1);
+      } else {
+        MG_RUN(VFLds, kTierLight, 1);
+      }
+    }
   } else {
-    if (p.tier == kTierHeavy) hipLaunchKernelGGL((k_run<VFGlobal, MODE, kTierHeavy>), g, b, 0, e.stream, k);
-    else if (p.tier == kTierMid) hipLaunchKernelGGL((k_run<VFGlobal, MODE, kTierMid>), g, b, 0, e.stream, k);
-    else hipLaunchKernelGGL((k_run<VFGlobal, MODE, kTierLight>), g, b, 0, e.stream, k);
+    if (p.tier == kTierHeavy) MG_RUN(VFGlobal, kTierHeavy, 1);
+    else if (p.tier == kTierMid) MG_RUN(VFGlobal, kTierMid, 1);
+    else MG_RUN(VFGlobal, kTierLight, 1);
   }
+#undef MG_RUN
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e.ev1, e.stream));
   return MG_OK;
