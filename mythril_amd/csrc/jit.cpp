@@ -774,7 +774,7 @@ struct Gen {
           gen_value(in.p0, "v" + std::to_string(d));
         } else {
           for (uint32_t j = 0; j < L; j++) {
-            if (!P.watch_words) {
+            if (!P.watch_words || walk_watch()) {
               // no watch rows: one pointer walks the SoA rows (the loads come in row order, at the
               // loop's top level), each load a 64-bit add of a small multiple of n to the previous
               // address.  With soa[K * n + i] LLVM hoists every row's K * n out of the candidate
@@ -955,9 +955,25 @@ struct Gen {
         if (search) o << "  if (early && __ballot(verdict != 0u) == 0ull) goto mg_next;\n";
         break;
       case K_WATCH:
-        if (eval_watch)
-          for (uint32_t j = 0; j < L; j++)
-            o << "  if (watch) watch[(uint64_t)" << (in.p0 + j) << "u * n + i] = " << v(in.a, j) << ";\n";
+        if (eval_watch) {
+          for (uint32_t j = 0; j < L; j++) {
+            if (walk_watch()) {
+              // the watch rows through a walking pointer too: indexed stores had LLVM hoist every
+              // row's K * n into SGPR pairs and spill them to VGPR lanes (C4: 974 v_readlane +
+              // 972 v_writelane)
+              const int64_t step = (int64_t)(in.p0 + j) - (int64_t)watch_row;
+              // n through an opaque copy: step * n is then computed at the store, not hoisted out of
+              // the candidate loop into one SGPR pair per row (54 v_writelane spills on C4)
+              if (step)
+                o << "  { uint64_t n_ = n; __asm__ volatile(\"\" : \"+s\"(n_)); wp_ += (long long)" << step
+                  << " * (long long)n_; __asm__ volatile(\"\" : \"+v\"(wp_)); }\n";
+              o << "  if (watch) *wp_ = " << v(in.a, j) << ";\n";
+              watch_row = in.p0 + j;
+            } else {
+              o << "  if (watch) watch[(uint64_t)" << (in.p0 + j) << "u * n + i] = " << v(in.a, j) << ";\n";
+            }
+          }
+        }
         break;
       case K_COPY:
         for (uint32_t j = 0; j < L; j++) o << "  " << v(d, j) << " = " << v(in.a, j) << ";\n";
@@ -1002,6 +1018,16 @@ struct Gen {
   // P is specialised (program.cpp specialize_program): decided compares are literals,
   // aliases are renamed away and dead instructions are gone
   uint32_t soa_row = 0;  // eval kernel without watch rows: the SoA row sp_ points at
+  uint32_t watch_row = 0;  // the watch row wp_ points at
+  // eval kernels with watch rows walk their SoA and watch rows with pointers too (MYTHGPU_JIT_WATCH_INDEXED=1:
+  // the indexed form)
+  static bool walk_watch() {
+    static const bool indexed = [] {
+      const char* g = getenv("MYTHGPU_JIT_WATCH_INDEXED");
+      return g && g[0] == '1';
+    }();
+    return !indexed;
+  }
   // MG_JIT_SOA_TILED: row r of candidate i at ((i / 64) * coord_words + r) * 64 + i % 64 (a group's
   // rows contiguous; jit_asm.cpp "Tiled SoA"): the walking pointer steps 64 words per row
   bool tiled = false;
@@ -1028,6 +1054,7 @@ struct Gen {
       return;
     }
     soa_row = 0;  // eval: sp_ = soa + i addresses row 0
+    watch_row = 0;
     for (const Instr& in : P.vcode) emit(in, search, !search);
   }
 };
@@ -1204,6 +1231,7 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        << (g.tiled ? "  const GU32* sp_ = (const GU32*)((uint64_t)soa + (((i >> 6) * " + std::to_string(P.coord_words) +
                        "ull * 64ull) + (i & 63ull)) * 4ull);  // tiled SoA\n"
                  : std::string("  const GU32* sp_ = (const GU32*)((uint64_t)soa + i * 4ull);\n"));
+  if (P.watch_words && Gen::walk_watch()) o << "  GU32* wp_ = (GU32*)((uint64_t)watch + i * 4ull);\n";
   g.decls();
   g.body(false);
   o << "  verdict_out[i] = (uint8_t)verdict;\n  }\n}\n";
