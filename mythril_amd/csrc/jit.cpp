@@ -1019,14 +1019,17 @@ struct Gen {
   // aliases are renamed away and dead instructions are gone
   uint32_t soa_row = 0;  // eval kernel without watch rows: the SoA row sp_ points at
   uint32_t watch_row = 0;  // the watch row wp_ points at
-  // eval kernels with watch rows walk their SoA and watch rows with pointers too (MYTHGPU_JIT_WATCH_INDEXED=1:
-  // the indexed form)
+  // MYTHGPU_JIT_WATCH_WALK=1: eval kernels with watch rows walk their SoA and watch rows with
+  // pointers too.  It removes the K * n spills (C4: 974 v_readlane + 972 v_writelane -> 18 + 18, static
+  // VALU 5,059 -> 3,114) but LLVM takes far longer over the per-store branches: a VMTests replay kernel
+  // (TestNameRegistrator, 8 watch words) went from 184 s to past 300 s on this host.  So it is opt-in;
+  // the spill-free watch-row kernel is the first tier's (jit_asm.cpp: its own register allocation)
   static bool walk_watch() {
-    static const bool indexed = [] {
-      const char* g = getenv("MYTHGPU_JIT_WATCH_INDEXED");
+    static const bool walk = [] {
+      const char* g = getenv("MYTHGPU_JIT_WATCH_WALK");
       return g && g[0] == '1';
     }();
-    return !indexed;
+    return walk;
   }
   // MG_JIT_SOA_TILED: row r of candidate i at ((i / 64) * coord_words + r) * 64 + i % 64 (a group's
   // rows contiguous; jit_asm.cpp "Tiled SoA"): the walking pointer steps 64 words per row
