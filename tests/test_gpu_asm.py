@@ -256,8 +256,12 @@ def test_asm_eval_workload_verdicts(engine, name, n, tiled):
     from oracle import cport
 
     P, _ = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
+    # the verdicts-only program; search.prepare's Program is the flatten cache's, so its watch list
+    # (the model read-back rows later searches of this workload decode) is put back
+    prev = P.watch
     P.set_watch([])
     pb = P.to_bytes()
+    P.set_watch(prev)
     prog = engine.load(pb)
     info = engine.info(prog)
     rng = np.random.default_rng(7)
