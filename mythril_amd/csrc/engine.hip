@@ -1374,6 +1374,40 @@ static bool split_over_devices(uint64_t count) {
   return g_devs.size() > 1 && count / g_devs.size() >= split_min_per_device();
 }
 
+// One empty launch of every interpreter variant the engine launches by default (and of the capture
+// gather and Keccak kernels) at initialisation: the runtime loads a kernel's code on its first launch,
+// ~2 ms that the first query of the process paid inside its time to first model (the first k_run
+// launch of a process took 1.96 ms against 0.057 ms after, profiles/r04u_cold.jsonl).  An empty
+// launch touches no memory: count 0 leaves k_run's group loop empty, rows / n 0 the others.
+template <int MODE>
+static void warm_run(Engine& e) {
+  KArgs k{};
+  const dim3 g(1), b(kWave);
+  hipLaunchKernelGGL((k_run<VFLds, MODE, kTierLight, 1>), g, b, 0, e.stream, k);
+  hipLaunchKernelGGL((k_run<VFLds, MODE, kTierMid, 1>), g, b, 0, e.stream, k);
+  hipLaunchKernelGGL((k_run<VFLds, MODE, kTierHeavy, 1>), g, b, 0, e.stream, k);
+  hipLaunchKernelGGL((k_run<VFGlobal, MODE, kTierLight, 1>), g, b, 0, e.stream, k);
+  hipLaunchKernelGGL((k_run<VFGlobal, MODE, kTierMid, 1>), g, b, 0, e.stream, k);
+  hipLaunchKernelGGL((k_run<VFGlobal, MODE, kTierHeavy, 1>), g, b, 0, e.stream, k);
+}
+
+static int warm_kernels(Engine& e) {
+  static const bool off = [] {
+    const char* g = getenv("MYTHGPU_WARM_KERNELS");
+    return g && g[0] == '0';
+  }();
+  if (off) return MG_OK;
+  warm_run<MODE_EVAL>(e);
+  warm_run<MODE_GEN>(e);
+  warm_run<MODE_SEARCH>(e);
+  hipLaunchKernelGGL(k_gather_rows, dim3(1), dim3(256), 0, e.stream, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u);
+  hipLaunchKernelGGL(k_keccak, dim3(1), dim3(256), 0, e.stream, (const uint8_t*)nullptr, (const uint64_t*)nullptr,
+                     (const uint32_t*)nullptr, (uint64_t)0, (uint8_t*)nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(e.stream));
+  return MG_OK;
+}
+
 static int init_dev(Engine& e, int dev) {
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, dev));
@@ -1403,7 +1437,7 @@ static int init_dev(Engine& e, int dev) {
   e.stats.cu_count = e.cu_count;
   e.stats.clock_mhz = e.clock_mhz;
   e.init = true;
-  return MG_OK;
+  return warm_kernels(e);
 }
 
 static void free_dev_buffers(Engine& e);
