@@ -337,7 +337,7 @@ struct Gen {
         case K_CONST: case K_COORD: case K_ADD: case K_SUB: case K_NEG: case K_AND: case K_OR: case K_XOR:
         case K_NOT: case K_ITE: case K_EQ: case K_ULT: case K_ULE: case K_SLT: case K_SLE: case K_CONCAT:
         case K_EXTRACT: case K_ZEXT: case K_SEXT: case K_LOOKUP: case K_ASSERT: case K_COPY: case K_MUL:
-        case K_WATCH:
+        case K_WATCH: case K_UMUL_NOOVF:
           break;
         case K_UDIV: case K_UREM: {
           // by a literal below 2^32 only (x / 86400, x / 10**k: a limb-serial 2/1 division)
@@ -415,6 +415,7 @@ struct Gen {
         case K_WATCH: if (eval_kernel) all(in.a); break;
         case K_ADD: case K_SUB: case K_MUL: upto(in.a, nd); upto(in.b, nd); break;
         case K_UDIV: case K_UREM: if (nd) { all(in.a); all(in.b); } break;
+        case K_UMUL_NOOVF: all(in.a); all(in.b); break;
         case K_NEG: upto(in.a, nd); break;
         case K_AND: case K_OR: case K_XOR: same(in.a, nd); same(in.b, nd); break;
         case K_NOT: case K_COPY: same(in.a, nd); break;
@@ -1722,6 +1723,68 @@ struct Gen {
         acc.resize(Ld);
         if (n == Ld) mask_top(acc, W);
         set(d, acc);
+        break;
+      }
+      case K_UMUL_NOOVF: {
+        // the full 2La-limb product (schoolbook; zero literal limbs skipped: LASER's overflow checks
+        // multiply a small count by a word), then "no bit at or above wa" as one zero test
+        const uint32_t wa = in.p1, La = Lw(wa), n = 2 * La;
+        std::vector<Limb> a = limbs(in.a, La), b = limbs(in.b, La), acc(n, Lit(0));  // acc owns
+        for (uint32_t i = 0; i < La; i++) {
+          if (a[i].lit() && a[i].v == 0) continue;
+          std::vector<Limb> lo(n, Lit(0)), hi(n, Lit(0));
+          for (uint32_t j = 0; j < La; j++) {
+            const Limb x = a[i], y = b[j];
+            if (y.lit() && y.v == 0) continue;
+            if (x.lit() && y.lit()) {
+              const uint64_t p = (uint64_t)x.v * y.v;
+              lo[i + j] = Lit((uint32_t)p);
+              hi[i + j + 1] = Lit((uint32_t)(p >> 32));
+              continue;
+            }
+            const Limb vx = x.reg() ? x : y, ly = x.reg() ? y : x;
+            std::string so;
+            std::initializer_list<int> rd = {};
+            if (ly.lit() && !inl(ly.v)) {
+              E.salu("s_mov_b32 s41, " + hexs(ly.v), {41});
+              so = "s41";
+              rd = {41};
+            } else {
+              so = src(ly);
+            }
+            const Limb dl = fresh(), dh = fresh();
+            E.valu("v_mul_lo_u32 " + V(dl.v) + ", " + V(vx.v) + ", " + so, rd);
+            E.valu("v_mul_hi_u32 " + V(dh.v) + ", " + V(vx.v) + ", " + so, rd);
+            lo[i + j] = dl;
+            hi[i + j + 1] = dh;
+          }
+          std::vector<Limb> s1 = add_chain(acc, lo, n, false);
+          for (auto& t : acc) drop(t);
+          for (auto& t : lo) drop(t);
+          std::vector<Limb> s2 = add_chain(s1, hi, n, false);
+          for (auto& t : s1) drop(t);
+          for (auto& t : hi) drop(t);
+          acc = s2;
+        }
+        std::vector<std::pair<Limb, Limb>> prs;
+        std::vector<Limb> tmp;  // owned
+        for (uint32_t q = 0; q < n; q++) {
+          const uint32_t bit0 = 32 * q;
+          const uint32_t m = bit0 + 32 <= wa ? 0u : (bit0 >= wa ? 0xFFFFFFFFu : ~((1u << (wa - bit0)) - 1u));
+          if (!m) continue;
+          if (acc[q].lit()) {
+            prs.push_back({Lit(acc[q].v & m), Lit(0)});
+          } else if (m == 0xFFFFFFFFu) {
+            prs.push_back({acc[q], Lit(0)});
+          } else {
+            const Limb t = and_lit(acc[q], m);
+            tmp.push_back(t);
+            prs.push_back({t, Lit(0)});
+          }
+        }
+        set_mask(d, eq_mask(prs));
+        for (auto& t : tmp) drop(t);
+        for (auto& t : acc) drop(t);
         break;
       }
       case K_UDIV: case K_UREM: {

@@ -25,7 +25,7 @@ from mythril_amd.smt import terms as T
 pytestmark = pytest.mark.gpu
 
 N = 2048
-OUTSIDE = {"bectoken_batch_overflow", "sha3_keyed_mapping"}  # UMUL_NOOVF / Keccak, EXP, SDIV
+OUTSIDE = {"sha3_keyed_mapping"}  # Keccak, EXP, SDIV
 
 
 def _windows(rng, k=4):
@@ -83,7 +83,7 @@ def test_asm_tier_verdicts(engine, name):
 
 # operators inside the tier
 _BIN = ["bvadd", "bvsub", "bvmul", "bvand", "bvor", "bvxor"]
-_CMP = ["bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge"]
+_CMP = ["bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge", "bvumul_noovfl"]
 
 
 def _random_program(seed: int, n_ops: int = 36):

@@ -130,11 +130,11 @@ def test_literal_tail_keys_are_narrowed():
 @pytest.mark.parametrize("name", sorted(workloads.WORKLOADS))
 def test_asm_tier_assembles_on_host(name):
     """The JIT's first tier (jit_asm.cpp) for every workload inside it: the emitted gfx950 assembly
-    (mgj_search + mgj_gen) assembles and links through comgr on the host.  Workloads outside it
-    (UMUL_NOOVF; Keccak, EXP, SDIV) are refused with MG_E_UNSUPPORTED, never miscompiled."""
+    (mgj_search + mgj_gen) assembles and links through comgr on the host.  A workload outside it
+    (C5: Keccak, EXP, SDIV) is refused with MG_E_UNSUPPORTED, never miscompiled."""
     roots = [c.raw for c in workloads.WORKLOADS[name]()]
     P, blob = search.prepare(roots)
-    if name in ("bectoken_batch_overflow", "sha3_keyed_mapping"):
+    if name == "sha3_keyed_mapping":
         with pytest.raises(native.EngineUnsupported):
             native.jit_asm(P.to_bytes(), blob)
         return
