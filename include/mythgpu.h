@@ -302,7 +302,7 @@ int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle);
  * MG_JIT_ASM builds the first tier instead: the same kernels emitted as gfx950 assembly with the
  * engine's own register allocation, assembled and linked in a few ms (clang + LLVM take ~140 ms);
  * MG_E_UNSUPPORTED for programs outside it (division other than by a literal of at most 32 bits,
- * EXP, Keccak, variable shifts, UMUL_NOOVF).
+ * EXP, Keccak, variable shifts).
  * MG_JIT_SOA_TILED (eval kernel, gen = 0): the kernel reads a TILED SoA — coordinate limb row r of
  * candidate i at word ((i / 64) * coord_words + r) * 64 + i % 64, so a group of 64 candidates has
  * its rows in one contiguous block (coord_words * 256 bytes) — instead of [row][candidate].  The
