@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <set>
 #include <sstream>
@@ -1146,6 +1147,35 @@ struct Gen {
         E.valu("v_cmp_ne_u32_e64 " + SP(m.s) + ", " + std::to_string(e2) + ", " + V(idx.v), {}, {m.s, m.s + 1});
         ms.push_back(m);
       }
+      // the select chain over entries e..n-1 of limb j, shared between limbs whose entries agree there
+      // (the actor dictionary: two of three addresses repeat one word in every limb)
+      std::map<std::vector<uint32_t>, Limb> memo;  // each entry holds one reference
+      std::function<Limb(uint32_t, uint32_t)> chain = [&](uint32_t j, uint32_t e) -> Limb {
+        std::vector<uint32_t> key{e};
+        for (uint32_t k = e; k < n; k++) key.push_back(G[off + k * Lc + j]);
+        auto it = memo.find(key);
+        if (it != memo.end()) {
+          E.retain(it->second);
+          return it->second;
+        }
+        Limb cur;
+        if (e + 1 == n) {
+          cur = vreg(Lit(G[off + e * Lc + j]));
+        } else {
+          const Limb rest = chain(j, e + 1);
+          const uint32_t lv = G[off + e * Lc + j];
+          // lanes whose index is not e keep rest (src1), the others take the literal (src0)
+          const Limb lvr = inl(lv) ? Lit(lv) : vreg(Lit(lv));  // VCC already uses the constant bus
+          cur = fresh();
+          E.valu("v_cndmask_b32_e64 " + V(cur.v) + ", " + src(lvr) + ", " + V(rest.v) + ", " + SP(ms[e].s),
+                 {ms[e].s, ms[e].s + 1});
+          drop(lvr);
+          drop(rest);
+        }
+        memo[key] = cur;
+        E.retain(cur);
+        return cur;
+      };
       for (uint32_t j = 0; j < Lc; j++) {
         bool same = true;
         for (uint32_t e2 = 1; e2 < n && same; e2++) same = G[off + e2 * Lc + j] == G[off + j];
@@ -1153,20 +1183,17 @@ struct Gen {
           r[j] = Lit(G[off + j]);
           continue;
         }
-        Limb cur = vreg(Lit(G[off + (n - 1) * Lc + j]));
-        for (int32_t e2 = (int32_t)n - 2; e2 >= 0; e2--) {
-          const uint32_t lv = G[off + e2 * Lc + j];
-          // lanes whose index is not e2 keep cur (src1), the others take the literal (src0)
-          const Limb lvr = inl(lv) ? Lit(lv) : vreg(Lit(lv));  // VCC already uses the constant bus
-          const Limb d = e2 == 0 ? dst(j) : fresh();
-          E.valu("v_cndmask_b32_e64 " + V(d.v) + ", " + src(lvr) + ", " + V(cur.v) + ", " + SP(ms[e2].s),
-                 {ms[e2].s, ms[e2].s + 1});
-          drop(lvr);
-          drop(cur);
-          cur = d;
-        }
-        r[j] = cur;
+        const Limb rest = chain(j, 1);
+        const uint32_t lv = G[off + j];
+        const Limb lvr = inl(lv) ? Lit(lv) : vreg(Lit(lv));
+        const Limb d = dst(j);
+        E.valu("v_cndmask_b32_e64 " + V(d.v) + ", " + src(lvr) + ", " + V(rest.v) + ", " + SP(ms[0].s),
+               {ms[0].s, ms[0].s + 1});
+        drop(lvr);
+        drop(rest);
+        r[j] = d;
       }
+      for (auto& kv : memo) drop(kv.second);
       for (auto& m : ms) E.srelease(m);
       return r;
     }

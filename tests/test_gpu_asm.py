@@ -286,3 +286,47 @@ def test_asm_eval_workload_verdicts(engine, name, n, tiled):
         engine.free(prog)
     want = cport.eval_soa(pb, soa, n)
     assert np.array_equal(va, want) and np.array_equal(vo, want)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 200])
+def test_eval_tiled_small_n(engine, n):
+    """The tiled SoA at sizes around one 64-candidate block (the last block padded): both eval
+    kernels' verdicts equal the C port's on the row-major original."""
+    from oracle import cport
+    from mythril_amd import ssa
+
+    P, _ = search.prepare([c.raw for c in workloads.WORKLOADS["suicide_kill"]()])
+    prev = P.watch
+    P.set_watch([])
+    pb = P.to_bytes()
+    P.set_watch(prev)
+    prog = engine.load(pb)
+    info = engine.info(prog)
+    rng = np.random.default_rng(n)
+    soa = rng.integers(0, 1 << 32, size=(int(info.coord_words), n), dtype=np.uint64).astype(np.uint32)
+    offs = P.coord_row_offsets()
+    for c in P.coords:
+        for j in range(ssa.limbs(c.width)):
+            bits = min(32, c.width - 32 * j)
+            soa[offs[c.index] + j] &= np.uint32((1 << bits) - 1)
+    want = cport.eval_soa(pb, soa, n)
+    try:
+        for asm in (False, True):
+            jh = engine.jit_compile(prog, 0, asm=asm, tiled=True)
+            try:
+                v, _ = engine.jit_eval(jh, native.tile_soa(soa), n)
+            finally:
+                engine.jit_free(jh)
+            assert np.array_equal(v, want), (asm, n)
+    finally:
+        engine.free(prog)
+
+
+@pytest.mark.parametrize("wa", [8, 32, 64, 160, 256])
+def test_asm_tier_umul_noovf(engine, wa):
+    """bvumul_noovfl at several widths on the first tier: per-candidate verdicts equal the C port's
+    (the generator's small, dictionary and uniform draws give products on both sides of 2^wa)."""
+    x, y = T.BitVecVar(f"mx{wa}", wa), T.BitVecVar(f"my{wa}", wa)
+    z = T.BitVecVar(f"mz{wa}", wa)
+    roots = [T.or_(T.bvcmp("bvumul_noovfl", x, y), T.bvcmp("bvumul_noovfl", z, T.BitVecVal(3, wa)))]
+    _check(engine, f"umul{wa}", roots, seeds=2, windows=3)

@@ -39,3 +39,39 @@ def test_search_many_equals_single_calls(engine, name, asm):
         engine.jit_free(j)
         engine.free_gen(gh)
         engine.free(prog)
+
+
+def test_search_many_over_virtual_devices(engine):
+    """Four logical devices (MYTHGPU_VIRTUAL_DEVICES): launches big enough to split go through
+    mg_jit_search one after the other (every device's slice, host min / sum), small ones through the
+    batch on the primary device; both give one mg_jit_search's answers."""
+    import os
+
+    P, blob = search.prepare([c.raw for c in workloads.WORKLOADS["token_transfer_underflow"]()])
+    old_mask = engine.mask
+    seeds, starts, counts = [3, 4, 5], [0, 1 << 33, 77], [1 << 22, 1 << 21, 4096]
+    try:
+        prog = engine.load(P.to_bytes())
+        gh = engine.load_gen(prog, blob)
+        j = engine.jit_compile(prog, gh)
+        want = [engine.jit_search(j, s, a, c, early_exit=False) for s, a, c in zip(seeds, starts, counts)]
+        engine.jit_free(j)
+        engine.free_gen(gh)
+        engine.free(prog)
+        os.environ["MYTHGPU_VIRTUAL_DEVICES"] = "4"
+        engine.reinit(1 << engine.device)
+        assert engine.n_devices == 4
+        prog = engine.load(P.to_bytes())
+        gh = engine.load_gen(prog, blob)
+        j = engine.jit_compile(prog, gh)
+        try:
+            assert engine.jit_search_many(j, seeds, starts, counts) == want
+            assert engine.jit_search_many(j, seeds[2:], starts[2:], counts[2:]) == want[2:]
+        finally:
+            engine.jit_free(j)
+            engine.free_gen(gh)
+            engine.free(prog)
+    finally:
+        os.environ.pop("MYTHGPU_VIRTUAL_DEVICES", None)
+        engine.reinit(old_mask)
+    assert engine.n_devices == 1
