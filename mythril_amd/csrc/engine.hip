@@ -112,7 +112,19 @@ struct KArgs {
   uint32_t watch_words;      // SEARCH with `watch`: rows per block of the capture buffer (see K_WATCH)
   uint32_t n_specs;          // generator specs (coordinates): the prologue's scalar-cache warm-up
   uint32_t pc0;              // code[0, pc0): hoisted K_CONSTs, run once per thread (Lowered::n_hoisted)
+  uint32_t n_gconsts;        // words at gconsts
+  uint32_t lds_g;            // word offset of the prologue's LDS copy of gconsts (kNoLds: none)
 };
+constexpr uint32_t kNoLds = 0xFFFFFFFFu;
+
+// the dynamic LDS of k_run: the value file (VFLds), then the generator constants' copy (lds_g)
+extern __shared__ uint32_t mg_lds[];
+
+// word i of the generator constants at a per-lane index: from the block's LDS copy when the
+// prologue staged one (a gather from global memory is an L2 round trip per dictionary limb)
+__device__ __forceinline__ uint32_t gword(const KArgs& k, uint32_t i) {
+  return k.lds_g != kNoLds ? mg_lds[k.lds_g + i] : cst(k.gconsts)[i];
+}
 
 constexpr uint32_t kFlagPrefetch = 1u << 16;
 constexpr int kTierLight = 0, kTierMid = 1, kTierHeavy = 2;  // KArgs::flags: warm the scalar cache first (launch_async)
@@ -186,7 +198,7 @@ __device__ __forceinline__ void gen_base(const KArgs& k, const VF& vf, uint32_t 
     }
     case MG_GEN_DICT: {
       const uint32_t e = ((grnd(ky, c, 0xFFFFu) >> 16) * s.p[1]) >> 16;
-      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = cst(k.gconsts)[s.p[0] + e * L + j];
+      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = gword(k, s.p[0] + e * L + j);
       break;
     }
     case MG_GEN_ALIGNED: {
@@ -211,7 +223,7 @@ __device__ __forceinline__ void gen_base(const KArgs& k, const VF& vf, uint32_t 
       const uint32_t h = grnd(ky, c, 0xFFFFu);
       if (alt == ALT_DICT) {
         const uint32_t e = ((h >> 16) * s.p[1]) >> 16;
-        for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = cst(k.gconsts)[s.p[0] + e * L + j];
+        for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = gword(k, s.p[0] + e * L + j);
       } else {  // SMALL / UNIFORM
         const bool narrow = width <= MG_GEN_NARROW_BITS;
         const uint32_t bits = alt == ALT_SMALL ? min(width, s.p[4] >> 16) : width;
@@ -333,6 +345,20 @@ __device__ __forceinline__ void st8(const VF& vf, uint32_t off, uint32_t L, cons
     if ((uint32_t)i < L) vf.at(off + i) = x.w[i];
 }
 
+// 256-bit values with every source limb loaded before any result limb is stored.  LDS runs a wave's
+// operations in order, but the compiler cannot move the load of a + j + 1 above the store to dst + j
+// (they may alias), so a limb-interleaved handler paid one LDS round trip per limb
+template <class VF>
+__device__ __forceinline__ void lda8(const VF& vf, uint32_t off, uint32_t* x) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) x[j] = vf.at(off + j);
+}
+template <class VF>
+__device__ __forceinline__ void sta8(const VF& vf, uint32_t off, const uint32_t* x) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) vf.at(off + j) = x[j];
+}
+
 // 32 bits of value (slot off, width w) starting at bit position p (zero beyond w)
 template <class VF>
 __device__ __forceinline__ uint32_t bits32(const VF& vf, uint32_t off, uint32_t w, uint32_t p) {
@@ -450,7 +476,7 @@ struct VFG {
 template <class VF, int MODE, int TIER, int KG>
 __device__ __forceinline__ void run_program(const KArgs& k, const VF& vf0, const uint64_t* i, const GKeys* key,
                                             bool early, const bool* active, uint32_t* verdict) {
-#pragma unroll
+_Pragma("unroll")
   for (int g = 0; g < KG; g++) verdict[g] = 1;
   const uint32_t n_instr = k.n_instr;
   // the next instruction's scalar load is issued before this one executes, so its latency
@@ -478,52 +504,111 @@ __device__ __forceinline__ void run_program(const KArgs& k, const VF& vf0, const
         break;
       }
       case K_COPY: {
-        MG_FOR_G(MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j);););
-        break;
-      }
-      case K_ADD: {
         MG_FOR_G({
-          uint32_t c = 0;
-          MG_LIMBS(L, vf.at(in.dst + j) = __builtin_addc(vf.at(in.a + j), vf.at(in.b + j), c, &c););
-          write_masked(vf, in.dst, L, W);
+          if (L == 8) {
+            uint32_t x[8];
+            lda8(vf, in.a, x);
+            sta8(vf, in.dst, x);
+          } else {
+            MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j););
+          }
         });
         break;
       }
+      case K_ADD:
       case K_SUB: {
         MG_FOR_G({
-          uint32_t c = 0;
-          MG_LIMBS(L, vf.at(in.dst + j) = __builtin_subc(vf.at(in.a + j), vf.at(in.b + j), c, &c););
-          write_masked(vf, in.dst, L, W);
+          if (L == 8) {
+            uint32_t x[8], y[8], r[8], c = 0;
+            lda8(vf, in.a, x);
+            lda8(vf, in.b, y);
+            if (in.op == K_ADD) {
+_Pragma("unroll")
+              for (int j = 0; j < 8; j++) r[j] = __builtin_addc(x[j], y[j], c, &c);
+            } else {
+_Pragma("unroll")
+              for (int j = 0; j < 8; j++) r[j] = __builtin_subc(x[j], y[j], c, &c);
+            }
+            r[7] &= top_mask(W);
+            sta8(vf, in.dst, r);
+          } else {
+            uint32_t c = 0;
+            if (in.op == K_ADD) {
+              MG_LIMBS(L, vf.at(in.dst + j) = __builtin_addc(vf.at(in.a + j), vf.at(in.b + j), c, &c););
+            } else {
+              MG_LIMBS(L, vf.at(in.dst + j) = __builtin_subc(vf.at(in.a + j), vf.at(in.b + j), c, &c););
+            }
+            write_masked(vf, in.dst, L, W);
+          }
         });
         break;
       }
       case K_NEG: {
         MG_FOR_G({
-          uint32_t c = 0;
-          MG_LIMBS(L, vf.at(in.dst + j) = __builtin_subc(0u, vf.at(in.a + j), c, &c););
-          write_masked(vf, in.dst, L, W);
+          if (L == 8) {
+            uint32_t x[8], r[8], c = 0;
+            lda8(vf, in.a, x);
+_Pragma("unroll")
+            for (int j = 0; j < 8; j++) r[j] = __builtin_subc(0u, x[j], c, &c);
+            r[7] &= top_mask(W);
+            sta8(vf, in.dst, r);
+          } else {
+            uint32_t c = 0;
+            MG_LIMBS(L, vf.at(in.dst + j) = __builtin_subc(0u, vf.at(in.a + j), c, &c););
+            write_masked(vf, in.dst, L, W);
+          }
         });
         break;
       }
       case K_AND:
-        MG_FOR_G(MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) & vf.at(in.b + j);););
-        break;
       case K_OR:
-        MG_FOR_G(MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) | vf.at(in.b + j);););
+      case K_XOR: {
+        MG_FOR_G({
+          if (L == 8) {
+            uint32_t x[8], y[8], r[8];
+            lda8(vf, in.a, x);
+            lda8(vf, in.b, y);
+_Pragma("unroll")
+            for (int j = 0; j < 8; j++) r[j] = in.op == K_AND ? (x[j] & y[j]) : in.op == K_OR ? (x[j] | y[j]) : (x[j] ^ y[j]);
+            sta8(vf, in.dst, r);
+          } else if (in.op == K_AND) {
+            MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) & vf.at(in.b + j););
+          } else if (in.op == K_OR) {
+            MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) | vf.at(in.b + j););
+          } else {
+            MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) ^ vf.at(in.b + j););
+          }
+        });
         break;
-      case K_XOR:
-        MG_FOR_G(MG_LIMBS(L, vf.at(in.dst + j) = vf.at(in.a + j) ^ vf.at(in.b + j);););
-        break;
+      }
       case K_NOT:
         MG_FOR_G({
-          MG_LIMBS(L, vf.at(in.dst + j) = ~vf.at(in.a + j););
-          write_masked(vf, in.dst, L, W);
+          if (L == 8) {
+            uint32_t x[8];
+            lda8(vf, in.a, x);
+_Pragma("unroll")
+            for (int j = 0; j < 8; j++) x[j] = ~x[j];
+            x[7] &= top_mask(W);
+            sta8(vf, in.dst, x);
+          } else {
+            MG_LIMBS(L, vf.at(in.dst + j) = ~vf.at(in.a + j););
+            write_masked(vf, in.dst, L, W);
+          }
         });
         break;
       case K_ITE: {
         MG_FOR_G({
           const bool c = vf.at(in.a) != 0;
-          MG_LIMBS(L, vf.at(in.dst + j) = c ? vf.at(in.b + j) : vf.at(in.c + j););
+          if (L == 8) {
+            uint32_t x[8], y[8];
+            lda8(vf, in.b, x);
+            lda8(vf, in.c, y);
+_Pragma("unroll")
+            for (int j = 0; j < 8; j++) x[j] = c ? x[j] : y[j];
+            sta8(vf, in.dst, x);
+          } else {
+            MG_LIMBS(L, vf.at(in.dst + j) = c ? vf.at(in.b + j) : vf.at(in.c + j););
+          }
         });
         break;
       }
@@ -556,26 +641,47 @@ __device__ __forceinline__ void run_program(const KArgs& k, const VF& vf0, const
         // dst = a:b, width(b) = p1
         const uint32_t wb = in.p1, wa = W - wb;
         MG_FOR_G({
-          for (uint32_t j = 0; j < L; j++) {
-            const uint32_t p = j * 32;
-            uint32_t v = bits32(vf, in.b, wb, p);
-            if (p + 32 > wb) {
-              v |= (p >= wb) ? bits32(vf, in.a, wa, p - wb) : (bits32(vf, in.a, wa, 0) << (wb - p));
+          if (L == 8) {  // every limb computed (loads only) before the stores
+            uint32_t r[8];
+_Pragma("unroll")
+            for (uint32_t j = 0; j < 8; j++) {
+              const uint32_t p = j * 32;
+              uint32_t v = bits32(vf, in.b, wb, p);
+              if (p + 32 > wb) {
+                v |= (p >= wb) ? bits32(vf, in.a, wa, p - wb) : (bits32(vf, in.a, wa, 0) << (wb - p));
+              }
+              r[j] = v;
             }
-            vf.at(in.dst + j) = v;
+            r[7] &= top_mask(W);
+            sta8(vf, in.dst, r);
+          } else {
+            for (uint32_t j = 0; j < L; j++) {
+              const uint32_t p = j * 32;
+              uint32_t v = bits32(vf, in.b, wb, p);
+              if (p + 32 > wb) {
+                v |= (p >= wb) ? bits32(vf, in.a, wa, p - wb) : (bits32(vf, in.a, wa, 0) << (wb - p));
+              }
+              vf.at(in.dst + j) = v;
+            }
+            write_masked(vf, in.dst, L, W);
           }
-          write_masked(vf, in.dst, L, W);
         });
         break;
       }
       case K_EXTRACT: {
         MG_FOR_G({
           if (L == 1) {
-            vf.at(in.dst) = bits32(vf, in.a, in.p1, in.p0);
+            vf.at(in.dst) = bits32(vf, in.a, in.p1, in.p0) & top_mask(W);
+          } else if (L == 8) {
+            uint32_t r[8];
+_Pragma("unroll")
+            for (uint32_t j = 0; j < 8; j++) r[j] = bits32(vf, in.a, in.p1, in.p0 + j * 32);
+            r[7] &= top_mask(W);
+            sta8(vf, in.dst, r);
           } else {
             for (uint32_t j = 0; j < L; j++) vf.at(in.dst + j) = bits32(vf, in.a, in.p1, in.p0 + j * 32);
+            write_masked(vf, in.dst, L, W);
           }
-          write_masked(vf, in.dst, L, W);
         });
         break;
       }
@@ -586,15 +692,30 @@ __device__ __forceinline__ void run_program(const KArgs& k, const VF& vf0, const
         MG_FOR_G({
           uint32_t fill = 0;
           if (in.op == K_SEXT) fill = ((vf.at(in.a + La - 1) >> ((wa - 1) & 31)) & 1u) ? 0xFFFFFFFFu : 0u;
-          MG_LIMBS(L, {
-            uint32_t v = fill;
-            if (j < La) {
-              v = vf.at(in.a + j);
-              if (j == La - 1) v = (v & tm) | (fill & ~tm);
+          if (L == 8) {
+            uint32_t r[8];
+_Pragma("unroll")
+            for (uint32_t j = 0; j < 8; j++) {
+              uint32_t v = fill;
+              if (j < La) {
+                v = vf.at(in.a + j);
+                if (j == La - 1) v = (v & tm) | (fill & ~tm);
+              }
+              r[j] = v;
             }
-            vf.at(in.dst + j) = v;
-          });
-          write_masked(vf, in.dst, L, W);
+            r[7] &= top_mask(W);
+            sta8(vf, in.dst, r);
+          } else {
+            MG_LIMBS(L, {
+              uint32_t v = fill;
+              if (j < La) {
+                v = vf.at(in.a + j);
+                if (j == La - 1) v = (v & tm) | (fill & ~tm);
+              }
+              vf.at(in.dst + j) = v;
+            });
+            write_masked(vf, in.dst, L, W);
+          }
         });
         break;
       }
@@ -638,7 +759,13 @@ __device__ __forceinline__ void run_program(const KArgs& k, const VF& vf0, const
             found = found || hit;
           }
           // src differs per lane: gather the limbs from the selected slot
-          MG_LIMBS(L, vf.at(in.dst + j) = vf.at(src + j););
+          if (L == 8) {
+            uint32_t x[8];
+            lda8(vf, src, x);
+            sta8(vf, in.dst, x);
+          } else {
+            MG_LIMBS(L, vf.at(in.dst + j) = vf.at(src + j););
+          }
         });
         break;
       }
@@ -693,8 +820,11 @@ __global__ void __launch_bounds__(256) k_gather_rows(const uint32_t* __restrict_
 
 template <class VF, int MODE, int TIER, int KG>
 __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
-  extern __shared__ uint32_t lds[];
-  VF vf0(lds, k);
+  VF vf0(mg_lds, k);
+  // the generator constants into LDS behind the value file (one wave per block: its own later
+  // reads see the writes, LDS runs a wave's operations in order)
+  if (MODE != MODE_EVAL && k.lds_g != kNoLds)
+    for (uint32_t i = threadIdx.x; i < k.n_gconsts; i += kWave) mg_lds[k.lds_g + i] = cst(k.gconsts)[i];
   // EVAL sweeps rows [0, count); GEN / SEARCH sweep the aligned 64-index groups that
   // cover [start, start + count), one group per wave (the GEN3 group key is per wave)
   const uint64_t a0 = (MODE == MODE_EVAL) ? 0ull : (k.start & ~63ull);
@@ -1184,11 +1314,12 @@ static int ensure_scratch(Engine& e, size_t bytes) {
 // grid: enough waves to fill 256 CUs several times over, never more than needed.
 // Resident waves per CU: the LDS value file (160 KiB per CU) and the VGPRs of the
 // kernel variant (heavy ~230: 2 waves/SIMD; mid: 4; light ~50: 8 waves/SIMD).
-static uint32_t grid_for(const Engine& e, uint64_t count, bool lds, uint32_t value_words, int tier, int kg = 1) {
+static uint32_t grid_for(const Engine& e, uint64_t count, bool lds, uint32_t value_words, int tier, int kg = 1,
+                         uint32_t extra_bytes = 0) {
   uint64_t want = (count + (uint64_t)kWave * kg - 1) / ((uint64_t)kWave * kg);
   uint32_t waves_per_cu = tier == kTierHeavy ? 8 : tier == kTierMid ? 16 : 32;
   if (lds) {
-    const uint32_t bytes = value_words * kWave * 4 * (uint32_t)kg;
+    const uint32_t bytes = value_words * kWave * 4 * (uint32_t)kg + extra_bytes;
     waves_per_cu = std::max<uint32_t>(1, std::min<uint32_t>(waves_per_cu, (160u * 1024u) / std::max<uint32_t>(bytes, 1)));
   }
   uint64_t cap = (uint64_t)std::max(e.cu_count, 1) * waves_per_cu * 4;
@@ -1230,7 +1361,17 @@ static int launch_async(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   // at KG x the value file in LDS.  Search / gen launches with the file in LDS, no capture, not the
   // heavy tier (its 256-bit temporaries), and a launch big enough to fill the chip at KG
   const int kg = interp_kg(MODE, lds, k.watch != nullptr, p.tier, p.low.value_words, lanes, e.cu_count);
-  const uint32_t grid = grid_for(e, lanes, lds, p.low.value_words, p.tier, kg);
+  // MYTHGPU_INTERP_LDS_GEN=0: dictionary gathers from global memory instead of the LDS copy
+  static const bool lds_gen = [] {
+    const char* g = getenv("MYTHGPU_INTERP_LDS_GEN");
+    return !(g && g[0] == '0');
+  }();
+  k.lds_g = kNoLds;
+  if (lds && lds_gen && MODE != MODE_EVAL && k.gconsts && k.n_gconsts && k.n_gconsts <= 4096u &&
+      (size_t)p.low.value_words * kWave * 4 * kg + (size_t)k.n_gconsts * 4 <= 64u * 1024u)
+    k.lds_g = p.low.value_words * kWave * (uint32_t)kg;
+  const uint32_t g_bytes = k.lds_g != kNoLds ? k.n_gconsts * 4u : 0u;
+  const uint32_t grid = grid_for(e, lanes, lds, p.low.value_words, p.tier, kg, g_bytes);
   k.sk = seed_lane_key(k.seed);
   k.sg = seed_group_key(k.seed);
   k.code = p.d_code;
@@ -1255,7 +1396,7 @@ static int launch_async(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
     if (rc) return rc;
     k.scratch = e.d_scratch;
   }
-  const size_t shmem = lds ? (size_t)p.low.value_words * kWave * 4 * kg : 0;
+  const size_t shmem = lds ? (size_t)p.low.value_words * kWave * 4 * kg + g_bytes : 0;
   HIPCHK(hipEventRecord(e.ev0, e.stream));
   const dim3 g(grid), b(kWave);
 #define MG_RUN(VFT, TIERC, KGC) hipLaunchKernelGGL((k_run<VFT, MODE, TIERC, KGC>), g, b, shmem, e.stream, k)
@@ -1966,6 +2107,7 @@ int mg_eval_generated(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start
   KArgs k{};
   k.specs = it->second->d_specs;
   k.gconsts = it->second->d_consts;
+  k.n_gconsts = (uint32_t)it->second->consts.size();
   k.verdict = d_ver;
   k.watch = d_watch;
   k.start = start;
@@ -2014,6 +2156,7 @@ static int read_assignment(Engine& e, DevGen& g, uint64_t seed, uint64_t idx, ui
   KArgs k{};
   k.specs = g.d_specs;
   k.gconsts = g.d_consts;
+  k.n_gconsts = (uint32_t)g.consts.size();
   k.verdict = e.d_ver1;
   k.watch = e.d_watch1;
   k.start = idx;
@@ -2062,6 +2205,7 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
       KArgs k{};
       k.specs = dg.d_specs;
       k.gconsts = dg.d_consts;
+      k.n_gconsts = (uint32_t)dg.consts.size();
       k.first_hit = de.d_hit;
       k.hits = de.d_hit + 1;
       k.start = st[d];
@@ -2087,6 +2231,7 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
     KArgs k{};
     k.specs = it->second->d_specs;
     k.gconsts = it->second->d_consts;
+    k.n_gconsts = (uint32_t)it->second->consts.size();
     k.first_hit = e.d_hit;
     k.hits = e.d_hit + 1;
     k.start = start;
