@@ -45,7 +45,9 @@ def test_race_unsat_costs_only_z3_time(mythril_standin):
         dt = time.perf_counter() - t0
         over.append(dt - z3.Optimize.calls[-1][2])
         assert _wait_for(lambda: len(S.state.cancelled) == len(over))  # the GPU search was stopped
-    assert statistics.median(over) <= 2e-3, over
+    # what a miss adds to z3's own time: the hand-off, not the GPU's 200-ms slice (a few ms at most on a
+    # loaded host: 2-5 ms measured with the suite running 8 ways)
+    assert statistics.median(over) <= 10e-3, over
     assert not S.calls  # the reference's path never ran: z3 answered once, in the race
     # the race ran the reference's check: its timeout, on a worker thread
     name, timeout, _, result = z3.Optimize.calls[-1]
