@@ -167,6 +167,20 @@ struct VFGlobal {
   __device__ __forceinline__ uint32_t& at(uint32_t w) const { return base[(uint64_t)w * stride]; }
 };
 
+// 256-bit values with every source limb loaded before any result limb is stored.  LDS runs a wave's
+// operations in order, but the compiler cannot move the load of a + j + 1 above the store to dst + j
+// (they may alias), so a limb-interleaved handler paid one LDS round trip per limb
+template <class VF>
+__device__ __forceinline__ void lda8(const VF& vf, uint32_t off, uint32_t* x) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) x[j] = vf.at(off + j);
+}
+template <class VF>
+__device__ __forceinline__ void sta8(const VF& vf, uint32_t off, const uint32_t* x) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) vf.at(off + j) = x[j];
+}
+
 // ---------------------------------------------------------------------------
 // candidate generator, GEN3 (include/mythgpu.h): a pure function of (seed, index,
 // coordinate); the same function as oracle/bveval.c gen_value and the JIT's
@@ -198,7 +212,14 @@ __device__ __forceinline__ void gen_base(const KArgs& k, const VF& vf, uint32_t 
     }
     case MG_GEN_DICT: {
       const uint32_t e = ((grnd(ky, c, 0xFFFFu) >> 16) * s.p[1]) >> 16;
-      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = gword(k, s.p[0] + e * L + j);
+      if (L == 8) {  // the entry's limbs first, then the stores (gword may read LDS: no interleaving)
+        uint32_t x[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) x[j] = gword(k, s.p[0] + e * 8 + j);
+        sta8(vf, dst, x);
+      } else {
+        for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = gword(k, s.p[0] + e * L + j);
+      }
       break;
     }
     case MG_GEN_ALIGNED: {
@@ -223,7 +244,14 @@ __device__ __forceinline__ void gen_base(const KArgs& k, const VF& vf, uint32_t 
       const uint32_t h = grnd(ky, c, 0xFFFFu);
       if (alt == ALT_DICT) {
         const uint32_t e = ((h >> 16) * s.p[1]) >> 16;
-        for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = gword(k, s.p[0] + e * L + j);
+        if (L == 8) {
+          uint32_t x[8];
+#pragma unroll
+          for (uint32_t j = 0; j < 8; j++) x[j] = gword(k, s.p[0] + e * 8 + j);
+          sta8(vf, dst, x);
+        } else {
+          for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = gword(k, s.p[0] + e * L + j);
+        }
       } else {  // SMALL / UNIFORM
         const bool narrow = width <= MG_GEN_NARROW_BITS;
         const uint32_t bits = alt == ALT_SMALL ? min(width, s.p[4] >> 16) : width;
@@ -266,7 +294,15 @@ __device__ __forceinline__ void gen_finish(const KArgs& k, const VF& vf, uint32_
       const bool sub = (h >> 1) & 1u;
       const uint32_t a0 = sub ? 0u - mag : mag, ah = sub ? 0xFFFFFFFFu : 0u;  // +/-mag sign-extended
       uint32_t cy = 0;
-      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = __builtin_addc(vf.at(dst + j), j ? ah : a0, cy, &cy);
+      if (L == 8) {
+        uint32_t x[8];
+        lda8(vf, dst, x);
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) x[j] = __builtin_addc(x[j], j ? ah : a0, cy, &cy);
+        sta8(vf, dst, x);
+      } else {
+        for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = __builtin_addc(vf.at(dst + j), j ? ah : a0, cy, &cy);
+      }
     }
     vf.at(dst + L - 1) &= top_mask(width);
     if (s.p[6]) {  // clamp into [lo, lo + span)
@@ -289,7 +325,15 @@ __device__ __forceinline__ void gen_finish(const KArgs& k, const VF& vf, uint32_
   vf.at(dst + L - 1) &= top_mask(width);
   if (const uint32_t fix = s.kind >> 8) {
     const auto* f = cst(k.gconsts) + (fix - 1);
-    for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = (vf.at(dst + j) & ~f[j]) | f[L + j];
+    if (L == 8) {
+      uint32_t x[8];
+      lda8(vf, dst, x);
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) x[j] = (x[j] & ~f[j]) | f[8 + j];
+      sta8(vf, dst, x);
+    } else {
+      for (uint32_t j = 0; j < L; j++) vf.at(dst + j) = (vf.at(dst + j) & ~f[j]) | f[L + j];
+    }
   }
 }
 
@@ -343,20 +387,6 @@ __device__ __forceinline__ void st8(const VF& vf, uint32_t off, uint32_t L, cons
 #pragma unroll
   for (int i = 0; i < 8; i++)
     if ((uint32_t)i < L) vf.at(off + i) = x.w[i];
-}
-
-// 256-bit values with every source limb loaded before any result limb is stored.  LDS runs a wave's
-// operations in order, but the compiler cannot move the load of a + j + 1 above the store to dst + j
-// (they may alias), so a limb-interleaved handler paid one LDS round trip per limb
-template <class VF>
-__device__ __forceinline__ void lda8(const VF& vf, uint32_t off, uint32_t* x) {
-#pragma unroll
-  for (int j = 0; j < 8; j++) x[j] = vf.at(off + j);
-}
-template <class VF>
-__device__ __forceinline__ void sta8(const VF& vf, uint32_t off, const uint32_t* x) {
-#pragma unroll
-  for (int j = 0; j < 8; j++) vf.at(off + j) = x[j];
 }
 
 // 32 bits of value (slot off, width w) starting at bit position p (zero beyond w)
