@@ -200,13 +200,15 @@ def _extend(st: "_FlatState", terms: Sequence[T.Term], lazy_inverse: bool) -> No
     P = st.P
     scalar_coord, table_of, fwd_arg = st.scalar_coord, st.table_of, st.fwd_arg
 
+    nodes, node_width, node_term, term_node = P.nodes, P.node_width, P.node_term, P.term_node
+
     def new_node(op, width, a=MG_NONE, b=MG_NONE, c=MG_NONE, p0=0, p1=0, p2=0, term=None):
         if width > MG_MAX_WIDTH:
             raise Unsupported(f"width {width} > {MG_MAX_WIDTH}")
-        P.nodes.append([OPS[op], width, a, b, c, p0, p1, p2])
-        P.node_width.append(width)
-        P.node_term.append(term)
-        return len(P.nodes) - 1
+        nodes.append([OPS[op], width, a, b, c, p0, p1, p2])
+        node_width.append(width)
+        node_term.append(term)
+        return len(nodes) - 1
 
     def const_node(v: int, w: int, term=None):
         off = len(P.consts)
@@ -238,10 +240,12 @@ def _extend(st: "_FlatState", terms: Sequence[T.Term], lazy_inverse: bool) -> No
             # forward UF apps, for lazy inverse defaults; the argument of an inverse
             # app is visited before it (children first), so one pass suffices
             fwd_arg[t.id] = t.args[0].id
+    def nid(x):
+        return term_node[x.id]
+
     for t in order:
         n = None
         op = t.op
-        nid = lambda x: P.term_node[x.id]
         if op in ("bvconst", "boolconst"):
             n = const_node(T.const_value(t), t.width, term=t)
         elif op in ("bvvar", "boolvar"):
