@@ -1391,10 +1391,13 @@ static int launch_async(Engine& e, DevProgram& p, KArgs k, uint64_t count) {
   // at KG x the value file in LDS.  Search / gen launches with the file in LDS, no capture, not the
   // heavy tier (its 256-bit temporaries), and a launch big enough to fill the chip at KG
   const int kg = interp_kg(MODE, lds, k.watch != nullptr, p.tier, p.low.value_words, lanes, e.cu_count);
-  // MYTHGPU_INTERP_LDS_GEN=0: dictionary gathers from global memory instead of the LDS copy
+  // MYTHGPU_INTERP_LDS_GEN=1: the prologue copies the generator constants into LDS and dictionary
+  // entries are read from there.  Measured slower at 2^22 per launch (profiles/r04z_interp_loadall.jsonl:
+  // C2 6.00 -> 5.54 G/s, etherstore 11.1 -> 9.2, C3 23.4 -> 20.5; the copy per block and the smaller
+  // occupancy cost more than the L2 gathers), so off by default
   static const bool lds_gen = [] {
     const char* g = getenv("MYTHGPU_INTERP_LDS_GEN");
-    return !(g && g[0] == '0');
+    return g && g[0] == '1';
   }();
   k.lds_g = kNoLds;
   if (lds && lds_gen && MODE != MODE_EVAL && k.gconsts && k.n_gconsts && k.n_gconsts <= 4096u &&
