@@ -3038,7 +3038,11 @@ int mg_jit_search_many(uint64_t jit, uint32_t n, const uint64_t* seeds, const ui
       total += count;
       if (count == 0) continue;
       // hipModuleLaunchKernel copies the argument values at the call
-      HIPCHK(hipModuleLaunchKernel(j.fsearch, nblk, 1, 1, 256, 1, 1, 0, e.xs[q % kManyStreams], args, nullptr));
+      const hipError_t le = hipModuleLaunchKernel(j.fsearch, nblk, 1, 1, 256, 1, 1, 0, e.xs[q % kManyStreams], args, nullptr);
+      if (le != hipSuccess) {  // the launches already queued finish before the slots are reused
+        for (int s2 = 0; s2 < kManyStreams; s2++) (void)hipStreamSynchronize(e.xs[s2]);
+        return set_err(MG_E_HIP, std::string("mg_jit_search_many: ") + hipGetErrorString(le));
+      }
     }
     for (int q = 0; q < kManyStreams; q++) {
       HIPCHK(hipEventRecord(e.xev[q], e.xs[q]));
@@ -3128,6 +3132,14 @@ int mg_jit_eval(uint64_t jit, const uint32_t* soa, uint64_t n, uint8_t* verdict_
   const size_t watch_bytes = (size_t)p->low.watch_words * n * 4;
   uint32_t *d_soa = nullptr, *d_watch = nullptr;
   uint8_t* d_ver = nullptr;
+  // freed on every return, the early error returns of HIPCHK included
+  struct Frees {
+    void** p[3];
+    ~Frees() {
+      for (void** q : p)
+        if (*q) (void)hipFree(*q);
+    }
+  } frees_{{(void**)&d_soa, (void**)&d_ver, (void**)&d_watch}};
   HIPCHK(hipMalloc((void**)&d_soa, soa_bytes));
   HIPCHK(hipMalloc((void**)&d_ver, n));
   if (watch_out && watch_bytes) HIPCHK(hipMalloc((void**)&d_watch, watch_bytes));
@@ -3137,9 +3149,6 @@ int mg_jit_eval(uint64_t jit, const uint32_t* soa, uint64_t n, uint8_t* verdict_
     HIPCHK(hipMemcpy(verdict_out, d_ver, n, hipMemcpyDeviceToHost));
     if (d_watch) HIPCHK(hipMemcpy(watch_out, d_watch, watch_bytes, hipMemcpyDeviceToHost));
   }
-  (void)hipFree(d_soa);
-  (void)hipFree(d_ver);
-  if (d_watch) (void)hipFree(d_watch);
   return rc;
 }
 
