@@ -395,6 +395,19 @@ struct Gen {
           break;
       }
     }
+    // MYTHGPU_JIT_ASM_GEN_ONLY=1 (diagnostic, search kernels): only the generator — every coordinate
+    // generated whole, nothing else evaluated (verdict 1): the generator's share of the kernel's VALU
+    if (gen_only() && !eval_kernel) {
+      std::vector<Instr> g;
+      for (const Instr& in : code)
+        if (in.op == K_COORD) g.push_back(in);
+      code.swap(g);
+      def.assign(P.vwidth.size(), -1);
+      for (size_t k = 0; k < code.size(); k++) def[code[k].dst] = (int32_t)k;
+      copysrc.assign(code.size(), MG_NONE);
+      last.assign(P.vwidth.size(), -1);
+      for (const Instr& in : code) need[in.dst] = lowmask(L(in.dst));
+    }
     for (size_t kk = code.size(); kk-- > 0;) {
       const Instr& in = code[kk];
       const uint32_t d = in.dst;
@@ -2209,6 +2222,13 @@ struct Gen {
     return r;
   }
 
+  static bool gen_only() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_GEN_ONLY");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
   static bool debug_live() {
     static const bool on = getenv("MYTHGPU_JIT_ASM_DEBUG") != nullptr;
     return on;
