@@ -783,7 +783,7 @@ struct Gen {
   }
 
   // XOR-OR reduction of the limb pairs -> mask (all lanes where every pair is equal)
-  Mask eq_mask(const std::vector<std::pair<Limb, Limb>>& prs) {
+  Mask eq_mask(const std::vector<std::pair<Limb, Limb>>& prs, Limb* keep = nullptr) {
     std::vector<Limb> diff;  // owned
     for (const auto& pr : prs) {
       const Limb a = pr.first, b = pr.second;
@@ -852,8 +852,43 @@ struct Gen {
     m.k = 2;
     m.s = E.salloc();
     E.valu("v_cmp_eq_u32_e64 " + SP(m.s) + ", 0, " + V(diff[0].v), {}, {m.s, m.s + 1});
-    drop(diff[0]);
+    if (keep) *keep = diff[0];  // the caller holds the reduced difference (eq_ids' cache)
+    else drop(diff[0]);
     return m;
+  }
+
+  // a == b over the first Lk limbs of values a and b.  The reduced difference (OR of the limbs' XORs)
+  // is kept while both values live: LASER's constraints compare the same keys again and again (a
+  // keccak site's key against every prior site in each LOOKUP, and in the EQs of the injectivity
+  // conditions), and a repeat then costs one compare
+  std::map<std::pair<uint32_t, uint32_t>, Limb> eqdiff;  // each entry holds one reference
+  Mask eq_ids(uint32_t a, uint32_t b, uint32_t Lk) {
+    const auto key = std::minmax(a, b);
+    auto it = eqdiff.find(key);
+    if (it != eqdiff.end()) {
+      Mask m;
+      m.k = 2;
+      m.s = E.salloc();
+      E.valu("v_cmp_eq_u32_e64 " + SP(m.s) + ", 0, " + V(it->second.v), {}, {m.s, m.s + 1});
+      return m;
+    }
+    std::vector<std::pair<Limb, Limb>> prs;
+    for (uint32_t j = 0; j < Lk; j++) prs.push_back({limb(a, j), limb(b, j)});
+    Limb keep{};
+    const Mask m = eq_mask(prs, &keep);
+    if (keep.reg()) eqdiff[key] = keep;
+    return m;
+  }
+  // value `id` is dead: the cached differences it took part in go
+  void eq_forget(uint32_t id) {
+    for (auto it = eqdiff.begin(); it != eqdiff.end();) {
+      if (it->first.first == id || it->first.second == id) {
+        drop(it->second);
+        it = eqdiff.erase(it);
+      } else {
+        ++it;
+      }
+    }
   }
 
   // x < y (unsigned) over La limbs, as a mask; sgn: the top limbs' bit (w-1)&31 flipped first
@@ -2019,9 +2054,11 @@ struct Gen {
           set_mask(d, mnot_xor(mask_of(in.a), mask_of(in.b)));
           break;
         }
-        std::vector<std::pair<Limb, Limb>> prs;
-        for (uint32_t j = 0; j < La; j++) prs.push_back({limb(in.a, j), limb(in.b, j)});
-        set_mask(d, eq_mask(prs));
+        set_mask(d, no_eq_cache() ? [&] {
+          std::vector<std::pair<Limb, Limb>> prs;
+          for (uint32_t j = 0; j < La; j++) prs.push_back({limb(in.a, j), limb(in.b, j)});
+          return eq_mask(prs);
+        }() : eq_ids(in.a, in.b, La));
         break;
       }
       case K_ULT: case K_ULE: case K_SLT: case K_SLE: {
@@ -2144,9 +2181,14 @@ struct Gen {
         }
         for (int32_t p = (int32_t)n - 1; p >= 0; p--) {
           const uint32_t kv = P.vaux[in.p1 + 2 * p], vv = P.vaux[in.p1 + 2 * p + 1];
-          std::vector<std::pair<Limb, Limb>> prs;
-          for (uint32_t j = 0; j < Lk; j++) prs.push_back({limb(in.a, j), limb(kv, j)});
-          const Mask h = eq_mask(prs);
+          Mask h;
+          if (no_eq_cache()) {
+            std::vector<std::pair<Limb, Limb>> prs;
+            for (uint32_t j = 0; j < Lk; j++) prs.push_back({limb(in.a, j), limb(kv, j)});
+            h = eq_mask(prs);
+          } else {
+            h = eq_ids(in.a, kv, Lk);
+          }
           if (h.k == 1) {
             if (h.ones) {
               for (uint32_t j = 0; j < Ld; j++) {
@@ -2222,6 +2264,13 @@ struct Gen {
     return r;
   }
 
+  static bool no_eq_cache() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_EQ_CACHE");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
   static bool gen_only() {
     static const bool on = [] {
       const char* g = getenv("MYTHGPU_JIT_ASM_GEN_ONLY");
@@ -2258,6 +2307,7 @@ struct Gen {
         if (id != MG_NONE && id < last.size() && last[id] <= (int32_t)k && val[id].def) {
           kill(id);
           val[id].def = false;
+          if (!eqdiff.empty()) eq_forget(id);
         }
       };
       if (in.dst != MG_NONE && in.dst < last.size() && last[in.dst] < 0) done(in.dst);
@@ -2281,6 +2331,8 @@ struct Gen {
           break;
       }
     }
+    for (auto& kv : eqdiff) drop(kv.second);  // values live to the end of the body
+    eqdiff.clear();
   }
 
   // ---------------------------------------------------------------------------------------
