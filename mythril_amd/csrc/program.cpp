@@ -159,6 +159,107 @@ void for_each_use(const VInstr& c, F&& f) {
   }
 }
 
+// The compare of a lookup's result, pushed into the lookup (the compiled kernels' list only):
+//   EQ(LOOKUP(k; (k_q, v_q)...; d), x)  ->  LOOKUP(k; (k_q, EQ(v_q, x))...; EQ(d, x))  of width 1
+// where the LOOKUP has no other reader.  Exact: the lookup selects one of the v_q / d, and the
+// compare of the selected value is the selected compare.  LASER's keccak bookkeeping asserts this
+// shape once per hashed site (the inverse map's entry for keccak(x) is x: the default is x itself,
+// so EQ(d, x) is a literal 1, and the priors' values are keys the program already compares).
+// Kept where it removes work: the n x L limb selects and the width-L compare go; a compare of a
+// value with itself is a literal, and a pair the program already compares (an EQ, or a LOOKUP key
+// test: LLVM's CSE and the first tier's difference cache share those) is counted free.
+// MYTHGPU_EQ_PUSHDOWN=0: off.
+std::vector<VInstr> push_eq_into_lookup(const std::vector<VInstr>& code, std::vector<uint32_t>& vwidth,
+                                        std::vector<uint32_t>& consts, bool* changed) {
+  static const bool on = [] {
+    const char* g = getenv("MYTHGPU_EQ_PUSHDOWN");
+    return !(g && g[0] == '0');
+  }();
+  *changed = false;
+  if (!on) return code;
+  const uint32_t NONE = MG_NONE;
+  const size_t nv = vwidth.size();
+  std::vector<uint32_t> uses(nv, 0);
+  std::vector<int32_t> defk(nv, -1);
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> eq_of;  // compared pair -> EQ result (NONE: a key test)
+  auto pair = [](uint32_t a, uint32_t b) { return a < b ? std::make_pair(a, b) : std::make_pair(b, a); };
+  for (size_t k = 0; k < code.size(); k++) {
+    const VInstr& c = code[k];
+    if (c.dst != NONE && c.dst < nv) defk[c.dst] = (int32_t)k;
+    for_each_use(c, [&](uint32_t x) {
+      if (x < nv) uses[x]++;
+    });
+    if (c.op == K_EQ) eq_of.emplace(pair(c.a, c.b), c.dst);
+    if (c.op == K_LOOKUP)
+      for (size_t q = 0; q + 1 < c.prior.size(); q += 2) eq_of.emplace(pair(c.a, c.prior[q]), NONE);
+  }
+  std::vector<char> drop(code.size(), 0);
+  std::vector<std::vector<VInstr>> at(code.size());  // replacement of an EQ
+  for (size_t k = 0; k < code.size(); k++) {
+    const VInstr& e = code[k];
+    if (e.op != K_EQ || e.dst == NONE) continue;
+    uint32_t lk = NONE, x = NONE;
+    for (int side = 0; side < 2 && lk == NONE; side++) {
+      const uint32_t s = side ? e.b : e.a, o = side ? e.a : e.b;
+      if (s < nv && defk[s] >= 0 && code[(size_t)defk[s]].op == K_LOOKUP && uses[s] == 1 && !drop[(size_t)defk[s]]) {
+        lk = s;
+        x = o;
+      }
+    }
+    if (lk == NONE) continue;
+    const VInstr& L = code[(size_t)defk[lk]];
+    const uint32_t n = L.c, W = L.wd, Lw = L_of(W);
+    std::vector<uint32_t> vals;
+    for (uint32_t q = 0; q < n; q++) vals.push_back(L.prior[2 * q + 1]);
+    vals.push_back(L.p0);
+    uint64_t cost_new = n;
+    for (uint32_t v : vals)
+      if (v != x && !eq_of.count(pair(v, x))) cost_new += 2ull * Lw;
+    const uint64_t cost_old = (uint64_t)n * Lw + 2ull * Lw;
+    if (cost_new >= cost_old) continue;
+    std::vector<VInstr> rep;
+    uint32_t one = NONE;
+    auto eq_id = [&](uint32_t v) -> uint32_t {
+      if (v == x) {
+        if (one == NONE) {
+          one = (uint32_t)vwidth.size();
+          vwidth.push_back(1);
+          rep.push_back(VInstr{K_CONST, 1, one, NONE, NONE, NONE, (uint32_t)consts.size(), 0, {}});
+          consts.push_back(1u);
+        }
+        return one;
+      }
+      auto it = eq_of.find(pair(v, x));
+      if (it != eq_of.end() && it->second != NONE && defk[it->second] >= 0 && (size_t)defk[it->second] < k)
+        return it->second;  // an EQ of the same pair, earlier in the list
+      const uint32_t id = (uint32_t)vwidth.size();
+      vwidth.push_back(1);
+      rep.push_back(VInstr{K_EQ, 1, id, v, x, NONE, e.p0, e.p1, {}});
+      eq_of[pair(v, x)] = NONE;  // compared from here on (not reusable as a value: defined here)
+      return id;
+    };
+    VInstr nl{K_LOOKUP, 1, e.dst, L.a, L.b, n, NONE, 0, {}};
+    for (uint32_t q = 0; q < n; q++) {
+      nl.prior.push_back(L.prior[2 * q]);
+      nl.prior.push_back(eq_id(vals[q]));
+    }
+    nl.p0 = eq_id(L.p0);
+    rep.push_back(std::move(nl));
+    drop[(size_t)defk[lk]] = 1;
+    drop[k] = 1;
+    at[k] = std::move(rep);
+    *changed = true;
+  }
+  if (!*changed) return code;
+  std::vector<VInstr> out;
+  out.reserve(code.size() + 8);
+  for (size_t k = 0; k < code.size(); k++) {
+    if (!drop[k]) out.push_back(code[k]);
+    for (auto& r : at[k]) out.push_back(std::move(r));
+  }
+  return out;
+}
+
 // K_COORD / K_CONST moved to just before their first use (order among them kept)
 std::vector<VInstr> sink_inputs(const std::vector<VInstr>& code, size_t nv) {
   std::vector<int64_t> first(nv, -1);
@@ -2247,11 +2348,18 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
     // extra work there; measured on the compiled kernels: C2 -1.9 %, C4 +0.4 % narrowed
     const uint64_t ops = in.limb_ops;  // algorithmic work is the query's, not what survives
     out.limb_ops = 0;
+    // the compiled kernels' list also takes the lookup-compare pushdown; the interpreter's slot code
+    // does not (each pushed compare is one more dispatch there)
+    bool pushed = false;
     if (narrowed) {
-      std::vector<VInstr> kept_wide = dce(wide);
+      std::vector<VInstr> kept_wide = push_eq_into_lookup(dce(wide), vwidth, out.consts, &pushed);
       allocate(kept_wide, vwidth, out, &kept);
     } else {
-      allocate(kept, vwidth, out);
+      std::vector<VInstr> jit_list = push_eq_into_lookup(kept, vwidth, out.consts, &pushed);
+      if (pushed)
+        allocate(jit_list, vwidth, out, &kept);
+      else
+        allocate(kept, vwidth, out);
     }
     out.limb_ops = ops;
     return MG_OK;
