@@ -161,11 +161,12 @@ void for_each_use(const VInstr& c, F&& f) {
 
 // The compare of a lookup's result, pushed into the lookup (the compiled kernels' list only):
 //   EQ(LOOKUP(k; (k_q, v_q)...; d), x)  ->  LOOKUP(k; (k_q, EQ(v_q, x))...; EQ(d, x))  of width 1
-// where the LOOKUP has no other reader.  Exact: the lookup selects one of the v_q / d, and the
-// compare of the selected value is the selected compare.  LASER's keccak bookkeeping asserts this
-// shape once per hashed site (the inverse map's entry for keccak(x) is x: the default is x itself,
-// so EQ(d, x) is a literal 1, and the priors' values are keys the program already compares).
-// Kept where it removes work: the n x L limb selects and the width-L compare go; a compare of a
+// (the LOOKUP itself goes when nothing else reads it).  Exact: the lookup selects one of the
+// v_q / d, and the compare of the selected value is the selected compare.  LASER's keccak
+// bookkeeping asserts this shape once per hashed site (the inverse map's entry for keccak(x) is x:
+// the default is x itself, so EQ(d, x) is a literal 1, and the priors' values are keys the program
+// already compares).  Kept where it removes work: the width-L compare goes, and the n x L limb
+// selects too when the LOOKUP goes; a compare of a
 // value with itself is a literal, and a pair the program already compares (an EQ, or a LOOKUP key
 // test: LLVM's CSE and the first tier's difference cache share those) is counted free.
 // MYTHGPU_EQ_PUSHDOWN=0: off.
@@ -201,7 +202,7 @@ std::vector<VInstr> push_eq_into_lookup(const std::vector<VInstr>& code, std::ve
     uint32_t lk = NONE, x = NONE;
     for (int side = 0; side < 2 && lk == NONE; side++) {
       const uint32_t s = side ? e.b : e.a, o = side ? e.a : e.b;
-      if (s < nv && defk[s] >= 0 && code[(size_t)defk[s]].op == K_LOOKUP && uses[s] == 1 && !drop[(size_t)defk[s]]) {
+      if (s < nv && defk[s] >= 0 && code[(size_t)defk[s]].op == K_LOOKUP && !drop[(size_t)defk[s]]) {
         lk = s;
         x = o;
       }
@@ -215,7 +216,9 @@ std::vector<VInstr> push_eq_into_lookup(const std::vector<VInstr>& code, std::ve
     uint64_t cost_new = n;
     for (uint32_t v : vals)
       if (v != x && !eq_of.count(pair(v, x))) cost_new += 2ull * Lw;
-    const uint64_t cost_old = (uint64_t)n * Lw + 2ull * Lw;
+    // a lookup read elsewhere too stays: then only the compare goes
+    const bool single = uses[lk] == 1;
+    const uint64_t cost_old = (single ? (uint64_t)n * Lw : 0ull) + 2ull * Lw;
     if (cost_new >= cost_old) continue;
     std::vector<VInstr> rep;
     uint32_t one = NONE;
@@ -245,7 +248,7 @@ std::vector<VInstr> push_eq_into_lookup(const std::vector<VInstr>& code, std::ve
     }
     nl.p0 = eq_id(L.p0);
     rep.push_back(std::move(nl));
-    drop[(size_t)defk[lk]] = 1;
+    if (single) drop[(size_t)defk[lk]] = 1;
     drop[k] = 1;
     at[k] = std::move(rep);
     *changed = true;
