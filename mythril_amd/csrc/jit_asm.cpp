@@ -2283,6 +2283,7 @@ struct Gen {
     return on;
   }
   void body(const std::string& next) {
+    eqdiff.clear();  // a kernel abandoned midway (AsmFail: out of VGPRs at this depth) left its entries
     for (size_t k = 0; k < code.size(); k++) {
       const Instr& in = code[k];
       emit(in, k, next);

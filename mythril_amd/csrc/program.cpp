@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <set>
 #include <cstdio>
 #include <cstdlib>
 
@@ -157,6 +158,76 @@ void for_each_use(const VInstr& c, F&& f) {
     use(c.b);
     use(c.c);
   }
+}
+
+// Lookups read only under the else-side of ITE(EQ(x, y), ...) guards (the compiled kernels' list
+// only): LASER's storage reads are ITE chains over the writes' keys, ending in the mapping's own
+// lookup, so the lookup tests keys the guards above it have already found unequal.  Along an
+// else-chain of single-reader ITEs whose conditions are EQs, a single-reader LOOKUP drops each prior
+// whose key test (key, k_q) is one of those pairs — that prior cannot match there — and with no
+// prior left it is a COPY of its default.  Exact: the dropped tests are false wherever the value is
+// read.  MYTHGPU_ITE_PRUNE=0: off.
+std::vector<VInstr> prune_guarded_lookups(const std::vector<VInstr>& code_in, size_t nv, bool* changed) {
+  static const bool on = [] {
+    const char* g = getenv("MYTHGPU_ITE_PRUNE");
+    return !(g && g[0] == '0');
+  }();
+  *changed = false;
+  if (!on) return code_in;
+  const uint32_t NONE = MG_NONE;
+  std::vector<VInstr> code = code_in;
+  auto pair = [](uint32_t a, uint32_t b) { return a < b ? std::make_pair(a, b) : std::make_pair(b, a); };
+  for (int round = 0; round < 4; round++) {
+    std::vector<uint32_t> uses(nv, 0);
+    std::vector<int32_t> defk(nv, -1);
+    for (size_t k = 0; k < code.size(); k++) {
+      const VInstr& c = code[k];
+      if (c.dst != NONE && c.dst < nv) defk[c.dst] = (int32_t)k;
+      for_each_use(c, [&](uint32_t x) {
+        if (x < nv) uses[x]++;
+      });
+    }
+    auto def = [&](uint32_t v) -> VInstr* { return v < nv && defk[v] >= 0 ? &code[(size_t)defk[v]] : nullptr; };
+    bool any = false;
+    for (size_t k = code.size(); k-- > 0;) {
+      if (code[k].op != K_ITE) continue;
+      std::set<std::pair<uint32_t, uint32_t>> ne;  // pairs known unequal on the else side
+      const VInstr* ite = &code[k];
+      while (true) {
+        const VInstr* cd = def(ite->a);
+        if (!cd || cd->op != K_EQ) break;
+        ne.insert(pair(cd->a, cd->b));
+        const uint32_t e = ite->c;
+        VInstr* ed = def(e);
+        if (!ed || uses[e] != 1) break;
+        if (ed->op == K_ITE) {
+          ite = ed;
+          continue;
+        }
+        if (ed->op == K_LOOKUP) {
+          std::vector<uint32_t> keep;
+          for (size_t q = 0; q + 1 < ed->prior.size(); q += 2)
+            if (!ne.count(pair(ed->a, ed->prior[q]))) {
+              keep.push_back(ed->prior[q]);
+              keep.push_back(ed->prior[q + 1]);
+            }
+          if (keep.size() != ed->prior.size()) {
+            any = true;
+            if (keep.empty()) {
+              *ed = VInstr{K_COPY, ed->wd, ed->dst, ed->p0, NONE, NONE, 0, 0, {}};
+            } else {
+              ed->prior = std::move(keep);
+              ed->c = (uint32_t)(ed->prior.size() / 2);
+            }
+          }
+        }
+        break;
+      }
+    }
+    if (!any) break;
+    *changed = true;
+  }
+  return code;
 }
 
 // The compare of a lookup's result, pushed into the lookup (the compiled kernels' list only):
@@ -2353,13 +2424,18 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
     out.limb_ops = 0;
     // the compiled kernels' list also takes the lookup-compare pushdown; the interpreter's slot code
     // does not (each pushed compare is one more dispatch there)
-    bool pushed = false;
+    bool pushed = false, pruned = false;
+    auto jit_rewrites = [&](const std::vector<VInstr>& list) {
+      std::vector<VInstr> r = prune_guarded_lookups(list, vwidth.size(), &pruned);
+      if (pruned) r = dce(r);  // before the pushdown, whose new values dce's table does not cover
+      return push_eq_into_lookup(r, vwidth, out.consts, &pushed);
+    };
     if (narrowed) {
-      std::vector<VInstr> kept_wide = push_eq_into_lookup(dce(wide), vwidth, out.consts, &pushed);
+      std::vector<VInstr> kept_wide = jit_rewrites(dce(wide));
       allocate(kept_wide, vwidth, out, &kept);
     } else {
-      std::vector<VInstr> jit_list = push_eq_into_lookup(kept, vwidth, out.consts, &pushed);
-      if (pushed)
+      std::vector<VInstr> jit_list = jit_rewrites(kept);
+      if (pushed || pruned)
         allocate(jit_list, vwidth, out, &kept);
       else
         allocate(kept, vwidth, out);

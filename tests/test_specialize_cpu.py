@@ -161,6 +161,24 @@ def test_asm_tier_random_programs_assemble_on_host():
     assert ok >= 20
 
 
+@pytest.mark.parametrize("name", [w for w in workloads.WORKLOADS if w != "sha3_keyed_mapping"])
+def test_asm_eval_workloads_assemble_on_host(name):
+    """The first tier's eval kernel of every workload inside the tier, verdicts only and with the
+    model watch rows, row-major and tiled SoA: emits (the occupancy-sized row queue tries several
+    depths, abandoning a kernel that runs out of registers midway) and assembles.  An abandoned
+    kernel's cached compare differences once leaked into the next attempt (C4: VGPR released twice)."""
+    P, _ = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
+    prev = P.watch
+    try:
+        for watch in (False, True):
+            P.set_watch(prev if watch else [])
+            for tiled in (False, True):
+                src = native.jit_asm(P.to_bytes(), None, compile=True, tiled=tiled)
+                assert "mgj_eval:" in src
+    finally:
+        P.set_watch(prev)
+
+
 def test_asm_eval_with_watch_rows_assembles_on_host():
     """The first tier's eval kernel (mgj_eval) with watch rows, as ``gpu_eval_terms`` builds it (24
     watched terms + the model read-back rows): emits and assembles for every random program; a value
