@@ -196,3 +196,40 @@ def test_asm_eval_with_watch_rows_assembles_on_host():
         P.set_watch([P.term_node[t.id] for t in watch] + me)
         src = native.jit_asm(P.to_bytes(), None, compile=True)
         assert "mgj_eval:" in src
+
+
+def test_lookup_compare_pushdown_fires_and_keeps_verdicts():
+    """``program.cpp: push_eq_into_lookup`` (the compiled kernels' program only): LASER's keccak
+    bookkeeping asserts ``EQ(LOOKUP(k; (k_q, v_q)...; x), x)`` once per hashed site, which becomes a
+    width-1 LOOKUP over the priors' compares.  C2 and C4 carry that shape: their compiled program has
+    width-1 LOOKUPs and fewer wide ones than the interpreter's (which keeps the original form), and
+    on C2 the interpreter's has none of width 1.  Verdicts against the C port: the workload tests
+    above (``jit``)."""
+    K_LOOKUP = 30
+    for name in ("token_transfer_underflow", "walletlibrary_kill"):
+        P, blob = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
+        jit = native.specialized_program(P.to_bytes(), blob)["code"]
+        itp = native.specialized_program(P.to_bytes(), blob, interp=True)["code"]
+        narrow = lambda code: int(np.sum((code[:, 0] == K_LOOKUP) & (code[:, 1] == 1)))
+        wide = lambda code: int(np.sum((code[:, 0] == K_LOOKUP) & (code[:, 1] > 1)))
+        assert narrow(jit) > 0, name
+        assert wide(jit) < wide(itp), name
+        if name == "token_transfer_underflow":
+            assert narrow(itp) == 0
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_rewritten_random_programs_keep_verdicts(seed):
+    """Random programs over the tier's operators (``tests/test_gpu_asm.py``: LOOKUP sites, ITE chains,
+    EQs), specialised for their generator: the compiled kernels' program — with the compare
+    pushdown and the guarded-lookup pruning — gives the C port's verdicts on the unspecialised one."""
+    from tests.test_gpu_asm import _random_program
+
+    P, blob = search.prepare(_random_program(7000 + seed))
+    pb = P.to_bytes()
+    spec = native.specialized_program(pb, blob)
+    widths = [c.width for c in P.coords]
+    soa = cport.gen_soa(pb, blob, 11 + seed, 0, N, _coord_words(P))
+    want = cport.search(pb, blob, 11 + seed, 0, N, threads=4, verdicts=True)[2]
+    got = kops.verdicts(spec, soa, widths, N)
+    assert np.array_equal(got, want)
