@@ -2173,6 +2173,40 @@ struct Gen {
       }
       case K_LOOKUP: {
         const uint32_t Lk = Lw(in.b), n = in.c;
+        auto key_test = [&](uint32_t kv) -> Mask {
+          if (!no_eq_cache()) return eq_ids(in.a, kv, Lk);
+          std::vector<std::pair<Limb, Limb>> prs;
+          for (uint32_t j = 0; j < Lk; j++) prs.push_back({limb(in.a, j), limb(kv, j)});
+          return eq_mask(prs);
+        };
+        if (in.wd == 1 && !no_bool_lookup()) {
+          // a Bool lookup (the specialiser's compare pushdown): selects of lane masks on the scalar
+          // unit, no limb materialised
+          Mask cur = mask_of(in.p0);
+          E.sretain(cur);
+          for (int32_t p = (int32_t)n - 1; p >= 0; p--) {
+            const uint32_t kv = P.vaux[in.p1 + 2 * p], vv = P.vaux[in.p1 + 2 * p + 1];
+            const Mask h = key_test(kv);
+            if (h.k == 1) {
+              if (h.ones) {
+                E.srelease(cur);
+                cur = mask_of(vv);
+                E.sretain(cur);
+              }
+              continue;
+            }
+            const Mask t = mop("and", h, mask_of(vv));
+            const Mask f = mop_andn(cur, h);
+            const Mask nc = mop("or", t, f);
+            E.srelease(t);
+            E.srelease(f);
+            E.srelease(cur);
+            E.srelease(h);
+            cur = nc;
+          }
+          set_mask(d, cur);
+          break;
+        }
         std::vector<Limb> cur(Ld);
         for (uint32_t j = 0; j < Ld; j++) {
           if (!(need[d] >> j & 1)) continue;
@@ -2264,6 +2298,14 @@ struct Gen {
     return r;
   }
 
+  // MYTHGPU_JIT_ASM_NO_BOOL_LOOKUP=1: a Bool lookup selects limbs like any other
+  static bool no_bool_lookup() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_BOOL_LOOKUP");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
   static bool no_eq_cache() {
     static const bool on = [] {
       const char* g = getenv("MYTHGPU_JIT_ASM_NO_EQ_CACHE");
