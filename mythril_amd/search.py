@@ -486,6 +486,7 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
         ticket = None      # the O3 kernel's compile
         ticket_asm = None  # the first tier's (assembly), submitted just before it
         tier = None        # "asm" / "o3": the compiled kernel in use
+        asm_tried = o3_tried = False
         rate = None  # candidates/s of the kernel in use (last launch)
         try:
             if jit == "always":
@@ -539,13 +540,19 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                         timing["o3_switch_ms"] = (now - t0) * 1e3
                         JIT_COMPILE_S[0] = 0.5 * JIT_COMPILE_S[0] + 0.5 * took
                         chunk = max(chunk, 1 << 22)
+                # each tier is submitted at most once per search: a first tier that refused this
+                # program (outside its vocabulary) is not asked again while the O3 kernel is not due
+                want_asm = JIT_ASM and not asm_tried and left > 1.2 * expected_asm
+                want_o3 = not o3_tried and left > 1.2 * expected_compile
                 if (jh is None and ticket is None and ticket_asm is None and jit == "auto" and scanned > 0
-                        and left > 1.2 * min(expected_compile, expected_asm if JIT_ASM else expected_compile)):
+                        and (want_asm or want_o3)):
                     tc = time.perf_counter()
-                    if JIT_ASM and left > 1.2 * expected_asm:
+                    if want_asm:
                         ticket_asm = engine.jit_compile_async(prog, gh, asm=True)
-                    if left > 1.2 * expected_compile:
+                        asm_tried = True
+                    if want_o3:
                         ticket = engine.jit_compile_async(prog, gh)
+                        o3_tried = True
                 n = min(chunk, max_candidates - scanned)
                 if rate:
                     cap_s = left
