@@ -57,6 +57,7 @@ enum LKind : uint8_t { LU, LL, LR };
 struct Limb {
   LKind k = LU;
   uint32_t v = 0;
+  uint32_t g = 0;  // allocation tag of an allocated VGPR (Emitter::vgen), checked under MYTHGPU_JIT_ASM_CHECK
   bool lit() const { return k == LL; }
   bool reg() const { return k == LR; }
   bool operator==(const Limb& o) const { return k == o.k && v == o.v; }
@@ -113,6 +114,25 @@ class Emitter {
   std::map<int, int64_t> vw;  // SGPR -> position of its last VALU write
   int nlab = 0;
   std::vector<int> vref = std::vector<int>(256, 0);
+  // MYTHGPU_JIT_ASM_CHECK=1: every allocation of a VGPR gets a fresh tag, every limb the tag of the
+  // allocation it was computed into; a read, retain or release of a limb whose register has since
+  // been released or handed out again fails the emission (a lifetime bug of the allocator, which
+  // would otherwise read another value's register in the kernel)
+  std::vector<uint32_t> vgen = std::vector<uint32_t>(256, 0);
+  uint32_t gen_ctr = 0;
+  static bool check_on() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_CHECK");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
+  void check(const Limb& l) const {
+    if (!check_on() || !l.reg() || (int)l.v < vfirst) return;
+    if (l.g == 0) fail("internal: an allocated VGPR v" + std::to_string(l.v) + " without its allocation tag");
+    if (vref[l.v] <= 0 || vgen[l.v] != l.g)
+      fail("internal: v" + std::to_string(l.v) + " used after its register was released or reallocated");
+  }
   int vfirst = kV0;  // the allocator's first VGPR: below it the fixed registers and the literal pool
   int vhigh = kV0;
   std::vector<int> sref = std::vector<int>(kS1, 0);
@@ -165,15 +185,18 @@ class Emitter {
     for (int r = vfirst; r < 256; r++)
       if (!vref[r]) {
         vref[r] = 1;
+        vgen[r] = ++gen_ctr;
         vhigh = std::max(vhigh, r + 1);
         return (uint32_t)r;
       }
     fail("out of VGPRs");
   }
   void retain(const Limb& l) {
+    check(l);
     if (l.reg() && (int)l.v >= vfirst) vref[l.v]++;
   }
   void release(const Limb& l) {
+    check(l);
     if (l.reg() && (int)l.v >= vfirst) {
       if (--vref[l.v] < 0) fail("internal: VGPR released twice");
     }
@@ -514,25 +537,25 @@ struct Gen {
       for (uint32_t it = 0; it * 256 < nL; it++) {
         const Limb vi = fresh(), vt = fresh(), ve = fresh(), vj = fresh();
         // word i = tid + 256 it, clamped to the last word (lanes past the table rewrite that one)
-        E.valu("v_add_u32_e32 " + V(vi.v) + ", " + imm(256 * it) + ", v0");
-        E.valu("v_min_u32_e32 " + V(vi.v) + ", " + imm(nL - 1) + ", " + V(vi.v));
-        E.valu("v_lshlrev_b32_e32 " + V(vt.v) + ", 2, " + V(vi.v));
+        E.valu("v_add_u32_e32 " + VL(vi) + ", " + imm(256 * it) + ", v0");
+        E.valu("v_min_u32_e32 " + VL(vi) + ", " + imm(nL - 1) + ", " + VL(vi));
+        E.valu("v_lshlrev_b32_e32 " + VL(vt) + ", 2, " + VL(vi));
         if (off * 4 < 4096) {
-          E.mem("global_load_dword " + V(vt.v) + ", " + V(vt.v) + ", s[4:5] offset:" + std::to_string(off * 4));
+          E.mem("global_load_dword " + VL(vt) + ", " + VL(vt) + ", s[4:5] offset:" + std::to_string(off * 4));
         } else {
-          E.valu("v_add_u32_e32 " + V(vt.v) + ", " + hexs(off * 4) + ", " + V(vt.v));
-          E.mem("global_load_dword " + V(vt.v) + ", " + V(vt.v) + ", s[4:5]");
+          E.valu("v_add_u32_e32 " + VL(vt) + ", " + hexs(off * 4) + ", " + VL(vt));
+          E.mem("global_load_dword " + VL(vt) + ", " + VL(vt) + ", s[4:5]");
         }
-        E.valu("v_mul_u32_u24_e32 " + V(ve.v) + ", " + imm(M) + ", " + V(vi.v));
-        E.valu("v_lshrrev_b32_e32 " + V(ve.v) + ", 16, " + V(ve.v));       // entry e
-        E.valu("v_mul_u32_u24_e32 " + V(vj.v) + ", " + imm(Lc) + ", " + V(ve.v));
-        E.valu("v_sub_u32_e32 " + V(vj.v) + ", " + V(vi.v) + ", " + V(vj.v));  // limb j
-        E.valu("v_mul_u32_u24_e32 " + V(vj.v) + ", " + imm(n) + ", " + V(vj.v));
+        E.valu("v_mul_u32_u24_e32 " + VL(ve) + ", " + imm(M) + ", " + VL(vi));
+        E.valu("v_lshrrev_b32_e32 " + VL(ve) + ", 16, " + VL(ve));       // entry e
+        E.valu("v_mul_u32_u24_e32 " + VL(vj) + ", " + imm(Lc) + ", " + VL(ve));
+        E.valu("v_sub_u32_e32 " + VL(vj) + ", " + VL(vi) + ", " + VL(vj));  // limb j
+        E.valu("v_mul_u32_u24_e32 " + VL(vj) + ", " + imm(n) + ", " + VL(vj));
         if (!inl(base)) E.salu("s_mov_b32 s41, " + hexs(base), {41});
-        E.valu("v_add3_u32 " + V(vj.v) + ", " + V(vj.v) + ", " + V(ve.v) + ", " + (inl(base) ? imm(base) : "s41"), {41});
-        E.valu("v_lshlrev_b32_e32 " + V(vj.v) + ", 2, " + V(vj.v));
+        E.valu("v_add3_u32 " + VL(vj) + ", " + VL(vj) + ", " + VL(ve) + ", " + (inl(base) ? imm(base) : "s41"), {41});
+        E.valu("v_lshlrev_b32_e32 " + VL(vj) + ", 2, " + VL(vj));
         E.ctl("s_waitcnt vmcnt(0)");
-        E.mem("ds_write_b32 " + V(vj.v) + ", " + V(vt.v));
+        E.mem("ds_write_b32 " + VL(vj) + ", " + VL(vt));
         drop(vi);
         drop(vt);
         drop(ve);
@@ -559,9 +582,9 @@ struct Gen {
     auto it = pool.find(x);
     if (it != pool.end()) return Reg((uint32_t)it->second);  // loaded once, before the group loop
     census[x]++;
-    const uint32_t r = E.valloc();
-    E.valu("v_mov_b32_e32 " + V(r) + ", " + imm(x));
-    return Reg(r);
+    const Limb r = fresh();
+    E.valu("v_mov_b32_e32 " + VL(r) + ", " + imm(x));
+    return r;
   }
   // Literal pool: literals a VGPR operand needs (select arms, carry-chain operands, dictionary
   // entries) are moved into a VGPR at every use unless pooled — one VGPR each, loaded once per
@@ -571,7 +594,8 @@ struct Gen {
   std::map<uint32_t, uint32_t> census; // literal -> materialisations in the last emission
   std::string src(const Limb& l) const {
     if (l.k == LU) fail("internal: a limb the demand analysis dropped was read");
-    return l.lit() ? imm(l.v) : V(l.v);
+    E.check(l);
+    return l.lit() ? imm(l.v) : VL(l);
   }
 
   // operand usable in a VOP3 slot: VGPR or inline constant (other literals go through a VGPR)
@@ -581,7 +605,15 @@ struct Gen {
   }
   void drop(const Limb& l) { E.release(l); }
 
-  Limb fresh() { return Reg(E.valloc()); }
+  Limb fresh() {
+    const uint32_t r = E.valloc();
+    return Limb{LR, r, E.vgen[r]};
+  }
+  // the register name of a limb, checked against its allocation (MYTHGPU_JIT_ASM_CHECK)
+  std::string VL(const Limb& l) const {
+    E.check(l);
+    return V(l.v);
+  }
 
   // mask form of a Bool value
   Mask mask_of(uint32_t id) {
@@ -595,7 +627,7 @@ struct Gen {
     } else {
       m.k = 2;
       m.s = E.salloc();
-      E.valu("v_cmp_ne_u32_e64 " + SP(m.s) + ", 0, " + V(l.v), {}, {m.s, m.s + 1});
+      E.valu("v_cmp_ne_u32_e64 " + SP(m.s) + ", 0, " + VL(l), {}, {m.s, m.s + 1});
     }
     x.m = m;
     return m;
@@ -610,7 +642,7 @@ struct Gen {
       l = Lit(m.ones ? 1u : 0u);
     } else {
       l = fresh();
-      E.valu("v_cndmask_b32_e64 " + V(l.v) + ", 0, 1, " + SP(m.s), {m.s, m.s + 1});
+      E.valu("v_cndmask_b32_e64 " + VL(l) + ", 0, 1, " + SP(m.s), {m.s, m.s + 1});
     }
     x.l.assign(1, l);
     return l;
@@ -659,11 +691,11 @@ struct Gen {
       if (carry == 0) {
         if (!sub) {
           const Limb s0 = b.reg() ? a : b, s1 = b.reg() ? b : a;  // src1 must be a VGPR
-          E.valu("v_add_co_u32_e32 " + V(d.v) + ", vcc, " + src(s0) + ", " + V(s1.v), {}, {kVCC, kVCC + 1});
+          E.valu("v_add_co_u32_e32 " + VL(d) + ", vcc, " + src(s0) + ", " + VL(s1), {}, {kVCC, kVCC + 1});
         } else if (b.reg()) {
-          E.valu("v_sub_co_u32_e32 " + V(d.v) + ", vcc, " + src(a) + ", " + V(b.v), {}, {kVCC, kVCC + 1});
+          E.valu("v_sub_co_u32_e32 " + VL(d) + ", vcc, " + src(a) + ", " + VL(b), {}, {kVCC, kVCC + 1});
         } else {
-          E.valu("v_subrev_co_u32_e32 " + V(d.v) + ", vcc, " + src(b) + ", " + V(a.v), {}, {kVCC, kVCC + 1});
+          E.valu("v_subrev_co_u32_e32 " + VL(d) + ", vcc, " + src(b) + ", " + VL(a), {}, {kVCC, kVCC + 1});
         }
       } else {
         Limb aa = a, bb = b, tmp, tmp2;
@@ -685,13 +717,13 @@ struct Gen {
         }
         if (!sub) {
           const Limb s0 = bb.reg() ? aa : bb, s1 = bb.reg() ? bb : aa;
-          E.valu("v_addc_co_u32_e32 " + V(d.v) + ", vcc, " + src(s0) + ", " + V(s1.v) + ", vcc", {kVCC, kVCC + 1},
+          E.valu("v_addc_co_u32_e32 " + VL(d) + ", vcc, " + src(s0) + ", " + VL(s1) + ", vcc", {kVCC, kVCC + 1},
                  {kVCC, kVCC + 1});
         } else if (bb.reg()) {
-          E.valu("v_subb_co_u32_e32 " + V(d.v) + ", vcc, " + src(aa) + ", " + V(bb.v) + ", vcc", {kVCC, kVCC + 1},
+          E.valu("v_subb_co_u32_e32 " + VL(d) + ", vcc, " + src(aa) + ", " + VL(bb) + ", vcc", {kVCC, kVCC + 1},
                  {kVCC, kVCC + 1});
         } else {
-          E.valu("v_subbrev_co_u32_e32 " + V(d.v) + ", vcc, " + src(bb) + ", " + V(aa.v) + ", vcc", {kVCC, kVCC + 1},
+          E.valu("v_subbrev_co_u32_e32 " + VL(d) + ", vcc, " + src(bb) + ", " + VL(aa) + ", vcc", {kVCC, kVCC + 1},
                  {kVCC, kVCC + 1});
         }
         drop(tmp);
@@ -714,7 +746,7 @@ struct Gen {
       return x;
     }
     const Limb d = fresh();
-    E.valu("v_and_b32_e32 " + V(d.v) + ", " + imm(m) + ", " + V(x.v));
+    E.valu("v_and_b32_e32 " + VL(d) + ", " + imm(m) + ", " + VL(x));
     return d;
   }
   // the top limb of a width-w result masked (the limb vector owns its registers)
@@ -748,8 +780,8 @@ struct Gen {
       }
       if (lo.lit()) return Lit((lo.v >> r) & (clip ? m : 0xFFFFFFFFu));
       const Limb d = fresh();
-      if (clip) E.valu("v_bfe_u32 " + V(d.v) + ", " + V(lo.v) + ", " + std::to_string(r) + ", " + std::to_string(n));
-      else E.valu("v_lshrrev_b32_e32 " + V(d.v) + ", " + std::to_string(r) + ", " + V(lo.v));
+      if (clip) E.valu("v_bfe_u32 " + VL(d) + ", " + VL(lo) + ", " + std::to_string(r) + ", " + std::to_string(n));
+      else E.valu("v_lshrrev_b32_e32 " + VL(d) + ", " + std::to_string(r) + ", " + VL(lo));
       return d;
     }
     if (lo.lit() && hi.lit()) {
@@ -758,7 +790,7 @@ struct Gen {
     }
     const Limb a = v3(hi), b = v3(lo);
     const Limb d = fresh();
-    E.valu("v_alignbit_b32 " + V(d.v) + ", " + src(a) + ", " + src(b) + ", " + std::to_string(r));
+    E.valu("v_alignbit_b32 " + VL(d) + ", " + src(a) + ", " + src(b) + ", " + std::to_string(r));
     drop(a);
     drop(b);
     if (!clip) return d;
@@ -776,7 +808,7 @@ struct Gen {
     }
     const Limb a = v3(hi), c = v3(lo);
     const Limb d = fresh();
-    E.valu("v_lshl_or_b32 " + V(d.v) + ", " + src(a) + ", " + std::to_string(s) + ", " + src(c));
+    E.valu("v_lshl_or_b32 " + VL(d) + ", " + src(a) + ", " + std::to_string(s) + ", " + src(c));
     drop(a);
     drop(c);
     return d;
@@ -815,16 +847,16 @@ struct Gen {
         m.k = 2;
         m.s = E.salloc();
         if (s0.lit() && !inl(s0.v)) {
-          E.valu("v_cmp_eq_u32_e32 vcc, " + src(s0) + ", " + V(s1.v), {}, {kVCC, kVCC + 1});
+          E.valu("v_cmp_eq_u32_e32 vcc, " + src(s0) + ", " + VL(s1), {}, {kVCC, kVCC + 1});
           E.salu("s_mov_b64 " + SP(m.s) + ", vcc", {m.s, m.s + 1});
         } else {
-          E.valu("v_cmp_eq_u32_e64 " + SP(m.s) + ", " + src(s0) + ", " + V(s1.v), {}, {m.s, m.s + 1});
+          E.valu("v_cmp_eq_u32_e64 " + SP(m.s) + ", " + src(s0) + ", " + VL(s1), {}, {m.s, m.s + 1});
         }
         return m;
       }
       const Limb d = fresh();
       const Limb s0 = b.reg() ? a : b, s1 = b.reg() ? b : a;
-      E.valu("v_xor_b32_e32 " + V(d.v) + ", " + src(s0) + ", " + V(s1.v));
+      E.valu("v_xor_b32_e32 " + VL(d) + ", " + src(s0) + ", " + VL(s1));
       diff.push_back(d);
     }
     Mask m;
@@ -842,8 +874,8 @@ struct Gen {
           continue;
         }
         const Limb d = fresh();
-        if (k == 2) E.valu("v_or_b32_e32 " + V(d.v) + ", " + V(diff[i].v) + ", " + V(diff[i + 1].v));
-        else E.valu("v_or3_b32 " + V(d.v) + ", " + V(diff[i].v) + ", " + V(diff[i + 1].v) + ", " + V(diff[i + 2].v));
+        if (k == 2) E.valu("v_or_b32_e32 " + VL(d) + ", " + VL(diff[i]) + ", " + VL(diff[i + 1]));
+        else E.valu("v_or3_b32 " + VL(d) + ", " + VL(diff[i]) + ", " + VL(diff[i + 1]) + ", " + VL(diff[i + 2]));
         for (size_t t = 0; t < k; t++) drop(diff[i + t]);
         nx.push_back(d);
       }
@@ -851,7 +883,7 @@ struct Gen {
     }
     m.k = 2;
     m.s = E.salloc();
-    E.valu("v_cmp_eq_u32_e64 " + SP(m.s) + ", 0, " + V(diff[0].v), {}, {m.s, m.s + 1});
+    E.valu("v_cmp_eq_u32_e64 " + SP(m.s) + ", 0, " + VL(diff[0]), {}, {m.s, m.s + 1});
     if (keep) *keep = diff[0];  // the caller holds the reduced difference (eq_ids' cache)
     else drop(diff[0]);
     return m;
@@ -869,7 +901,7 @@ struct Gen {
       Mask m;
       m.k = 2;
       m.s = E.salloc();
-      E.valu("v_cmp_eq_u32_e64 " + SP(m.s) + ", 0, " + V(it->second.v), {}, {m.s, m.s + 1});
+      E.valu("v_cmp_eq_u32_e64 " + SP(m.s) + ", 0, " + VL(it->second), {}, {m.s, m.s + 1});
       return m;
     }
     std::vector<std::pair<Limb, Limb>> prs;
@@ -905,7 +937,7 @@ struct Gen {
           t.v ^= f;
         } else {
           const Limb d = fresh();
-          E.valu("v_xor_b32_e32 " + V(d.v) + ", " + imm(f) + ", " + V(t.v));
+          E.valu("v_xor_b32_e32 " + VL(d) + ", " + imm(f) + ", " + VL(t));
           t = d;
           own.push_back(d);
         }
@@ -923,17 +955,17 @@ struct Gen {
         m.s = E.salloc();
         if (b.reg()) {
           if (a.lit() && !inl(a.v)) {
-            E.valu("v_cmp_lt_u32_e32 vcc, " + src(a) + ", " + V(b.v), {}, {kVCC, kVCC + 1});
+            E.valu("v_cmp_lt_u32_e32 vcc, " + src(a) + ", " + VL(b), {}, {kVCC, kVCC + 1});
             E.salu("s_mov_b64 " + SP(m.s) + ", vcc", {m.s, m.s + 1});
           } else {
-            E.valu("v_cmp_lt_u32_e64 " + SP(m.s) + ", " + src(a) + ", " + V(b.v), {}, {m.s, m.s + 1});
+            E.valu("v_cmp_lt_u32_e64 " + SP(m.s) + ", " + src(a) + ", " + VL(b), {}, {m.s, m.s + 1});
           }
         } else {
           if (!inl(b.v)) {
-            E.valu("v_cmp_gt_u32_e32 vcc, " + src(b) + ", " + V(a.v), {}, {kVCC, kVCC + 1});
+            E.valu("v_cmp_gt_u32_e32 vcc, " + src(b) + ", " + VL(a), {}, {kVCC, kVCC + 1});
             E.salu("s_mov_b64 " + SP(m.s) + ", vcc", {m.s, m.s + 1});
           } else {
-            E.valu("v_cmp_gt_u32_e64 " + SP(m.s) + ", " + src(b) + ", " + V(a.v), {}, {m.s, m.s + 1});
+            E.valu("v_cmp_gt_u32_e64 " + SP(m.s) + ", " + src(b) + ", " + VL(a), {}, {m.s, m.s + 1});
           }
         }
       }
@@ -953,8 +985,8 @@ struct Gen {
         borrow = -1;
       }
       if (borrow == 0) {
-        if (b.reg()) E.valu("v_sub_co_u32_e32 v7, vcc, " + src(a) + ", " + V(b.v), {}, {kVCC, kVCC + 1});
-        else E.valu("v_subrev_co_u32_e32 v7, vcc, " + src(b) + ", " + V(a.v), {}, {kVCC, kVCC + 1});
+        if (b.reg()) E.valu("v_sub_co_u32_e32 v7, vcc, " + src(a) + ", " + VL(b), {}, {kVCC, kVCC + 1});
+        else E.valu("v_subrev_co_u32_e32 v7, vcc, " + src(b) + ", " + VL(a), {}, {kVCC, kVCC + 1});
       } else {
         Limb aa = a, bb = b, tmp, tmp2;
         if (!aa.reg() && !bb.reg()) {
@@ -969,9 +1001,9 @@ struct Gen {
           bb = tmp2;
         }
         if (bb.reg())
-          E.valu("v_subb_co_u32_e32 v7, vcc, " + src(aa) + ", " + V(bb.v) + ", vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
+          E.valu("v_subb_co_u32_e32 v7, vcc, " + src(aa) + ", " + VL(bb) + ", vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
         else
-          E.valu("v_subbrev_co_u32_e32 v7, vcc, " + src(bb) + ", " + V(aa.v) + ", vcc", {kVCC, kVCC + 1},
+          E.valu("v_subbrev_co_u32_e32 v7, vcc, " + src(bb) + ", " + VL(aa) + ", vcc", {kVCC, kVCC + 1},
                  {kVCC, kVCC + 1});
         drop(tmp);
         drop(tmp2);
@@ -1049,7 +1081,7 @@ struct Gen {
       ff = tmp2;
     }
     const Limb d = fresh();
-    E.valu("v_cndmask_b32_e32 " + V(d.v) + ", " + src(ff) + ", " + V(tt.v) + ", vcc", {kVCC, kVCC + 1});
+    E.valu("v_cndmask_b32_e32 " + VL(d) + ", " + src(ff) + ", " + VL(tt) + ", vcc", {kVCC, kVCC + 1});
     drop(tmp);
     drop(tmp2);
     return d;
@@ -1066,12 +1098,12 @@ struct Gen {
   // per-lane hash grnd(c, j) into a fresh VGPR
   Limb grnd(uint32_t c, uint32_t j, const Limb* into = nullptr) {
     const Limb d = into ? *into : fresh(), t = fresh();
-    E.valu("v_xor_b32_e32 " + V(d.v) + ", " + imm(gsalt(c, j)) + ", v4");
-    E.valu("v_xor_b32_sdwa " + V(d.v) + ", " + V(d.v) + ", " + V(d.v) +
+    E.valu("v_xor_b32_e32 " + VL(d) + ", " + imm(gsalt(c, j)) + ", v4");
+    E.valu("v_xor_b32_sdwa " + VL(d) + ", " + VL(d) + ", " + VL(d) +
            " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1");
-    E.valu("v_mul_u32_u24_e32 " + V(d.v) + ", 0x9e3779, " + V(d.v));
-    E.valu("v_lshrrev_b32_e32 " + V(t.v) + ", 15, " + V(d.v));
-    E.valu("v_xad_u32 " + V(d.v) + ", " + V(t.v) + ", " + V(d.v) + ", v5");
+    E.valu("v_mul_u32_u24_e32 " + VL(d) + ", 0x9e3779, " + VL(d));
+    E.valu("v_lshrrev_b32_e32 " + VL(t) + ", 15, " + VL(d));
+    E.valu("v_xad_u32 " + VL(d) + ", " + VL(t) + ", " + VL(d) + ", v5");
     drop(t);
     return d;
   }
@@ -1092,16 +1124,16 @@ struct Gen {
           grnd(c, j, &r[j]);
         } else {
           const uint32_t s = (7u * j + 3u) % 31u + 1u;
-          E.valu("v_alignbit_b32 " + V(r[j].v) + ", " + V(r[j - 1].v) + ", " + V(r[j - 2].v) + ", " + std::to_string(s));
-          E.valu("v_add_u32_e32 " + V(r[j].v) + ", " + V(r[j - 2].v) + ", " + V(r[j].v));
+          E.valu("v_alignbit_b32 " + VL(r[j]) + ", " + VL(r[j - 1]) + ", " + VL(r[j - 2]) + ", " + std::to_string(s));
+          E.valu("v_add_u32_e32 " + VL(r[j]) + ", " + VL(r[j - 2]) + ", " + VL(r[j]));
         }
       }
       // the raw chain is complete: mask the top limb in place, zero the limbs above
       for (uint32_t j = 0; j < Lc; j++) {
         const uint32_t lo = 32 * j;
         const uint32_t m = lo >= bits ? 0u : (bits - lo >= 32 ? 0xFFFFFFFFu : ((1u << (bits - lo)) - 1u));
-        if (j >= n || m == 0) E.valu("v_mov_b32_e32 " + V(r[j].v) + ", 0");
-        else if (m != 0xFFFFFFFFu) E.valu("v_and_b32_e32 " + V(r[j].v) + ", " + imm(m) + ", " + V(r[j].v));
+        if (j >= n || m == 0) E.valu("v_mov_b32_e32 " + VL(r[j]) + ", 0");
+        else if (m != 0xFFFFFFFFu) E.valu("v_and_b32_e32 " + VL(r[j]) + ", " + imm(m) + ", " + VL(r[j]));
       }
       return r;
     }
@@ -1112,8 +1144,8 @@ struct Gen {
       } else {
         const uint32_t s = (7u * j + 3u) % 31u + 1u;
         const Limb d = fresh();
-        E.valu("v_alignbit_b32 " + V(d.v) + ", " + V(u[j - 1].v) + ", " + V(u[j - 2].v) + ", " + std::to_string(s));
-        E.valu("v_add_u32_e32 " + V(d.v) + ", " + V(u[j - 2].v) + ", " + V(d.v));
+        E.valu("v_alignbit_b32 " + VL(d) + ", " + VL(u[j - 1]) + ", " + VL(u[j - 2]) + ", " + std::to_string(s));
+        E.valu("v_add_u32_e32 " + VL(d) + ", " + VL(u[j - 2]) + ", " + VL(d));
         u[j] = d;
       }
     }
@@ -1161,10 +1193,10 @@ struct Gen {
     if (x.lit()) return Lit((uint32_t)(((uint64_t)x.v * c) >> 32));
     const Limb d = fresh();
     if (inl(c)) {
-      E.valu("v_mul_hi_u32 " + V(d.v) + ", " + V(x.v) + ", " + imm(c));
+      E.valu("v_mul_hi_u32 " + VL(d) + ", " + VL(x) + ", " + imm(c));
     } else {
       E.salu("s_mov_b32 s41, " + hexs(c), {41});
-      E.valu("v_mul_hi_u32 " + V(d.v) + ", " + V(x.v) + ", s41", {41});
+      E.valu("v_mul_hi_u32 " + VL(d) + ", " + VL(x) + ", s41", {41});
     }
     return d;
   }
@@ -1179,9 +1211,9 @@ struct Gen {
       const uint32_t m = w == 32 ? 0xFFFFFFFFu : ((1u << w) - 1u);
       for (uint32_t e2 = 0; e2 < n; e2++) pack |= (G[off + e2] & m) << (e2 * w);
       const Limb sh = fresh(), d = dst(0);
-      E.valu("v_mul_u32_u24_e32 " + V(sh.v) + ", " + imm(w) + ", " + V(idx.v));
+      E.valu("v_mul_u32_u24_e32 " + VL(sh) + ", " + imm(w) + ", " + VL(idx));
       E.salu("s_mov_b32 s41, " + hexs(pack), {41});
-      E.valu("v_bfe_u32 " + V(d.v) + ", s41, " + V(sh.v) + ", " + std::to_string(w), {41});
+      E.valu("v_bfe_u32 " + VL(d) + ", s41, " + VL(sh) + ", " + std::to_string(w), {41});
       drop(sh);
       r[0] = d;
       return r;
@@ -1192,7 +1224,7 @@ struct Gen {
         Mask m;
         m.k = 2;
         m.s = E.salloc();
-        E.valu("v_cmp_ne_u32_e64 " + SP(m.s) + ", " + std::to_string(e2) + ", " + V(idx.v), {}, {m.s, m.s + 1});
+        E.valu("v_cmp_ne_u32_e64 " + SP(m.s) + ", " + std::to_string(e2) + ", " + VL(idx), {}, {m.s, m.s + 1});
         ms.push_back(m);
       }
       // the select chain over entries e..n-1 of limb j, shared between limbs whose entries agree there
@@ -1215,7 +1247,7 @@ struct Gen {
           // lanes whose index is not e keep rest (src1), the others take the literal (src0)
           const Limb lvr = inl(lv) ? Lit(lv) : vreg(Lit(lv));  // VCC already uses the constant bus
           cur = fresh();
-          E.valu("v_cndmask_b32_e64 " + V(cur.v) + ", " + src(lvr) + ", " + V(rest.v) + ", " + SP(ms[e].s),
+          E.valu("v_cndmask_b32_e64 " + VL(cur) + ", " + src(lvr) + ", " + VL(rest) + ", " + SP(ms[e].s),
                  {ms[e].s, ms[e].s + 1});
           drop(lvr);
           drop(rest);
@@ -1235,7 +1267,7 @@ struct Gen {
         const uint32_t lv = G[off + j];
         const Limb lvr = inl(lv) ? Lit(lv) : vreg(Lit(lv));
         const Limb d = dst(j);
-        E.valu("v_cndmask_b32_e64 " + V(d.v) + ", " + src(lvr) + ", " + V(rest.v) + ", " + SP(ms[0].s),
+        E.valu("v_cndmask_b32_e64 " + VL(d) + ", " + src(lvr) + ", " + VL(rest) + ", " + SP(ms[0].s),
                {ms[0].s, ms[0].s + 1});
         drop(lvr);
         drop(rest);
@@ -1248,7 +1280,7 @@ struct Gen {
     auto lb = lds_base.find(off);
     if (lb != lds_base.end()) {  // from the LDS copy: word base + j * n + idx
       const Limb va = fresh();
-      E.valu("v_lshlrev_b32_e32 " + V(va.v) + ", 2, " + V(idx.v));
+      E.valu("v_lshlrev_b32_e32 " + VL(va) + ", 2, " + VL(idx));
       bool any = false;
       for (uint32_t j = 0; j < Lc; j++) {
         bool same = true;
@@ -1258,7 +1290,7 @@ struct Gen {
           continue;
         }
         const Limb d = dst(j);
-        E.mem("ds_read_b32 " + V(d.v) + ", " + V(va.v) + " offset:" + std::to_string((lb->second + j * n) * 4));
+        E.mem("ds_read_b32 " + VL(d) + ", " + VL(va) + " offset:" + std::to_string((lb->second + j * n) * 4));
         r[j] = d;
         any = true;
       }
@@ -1268,7 +1300,7 @@ struct Gen {
     }
     // gathers from the generator constants (s[4:5]): byte offset (off + idx * Lc + j) * 4
     const Limb vo = fresh();
-    E.valu("v_mul_u32_u24_e32 " + V(vo.v) + ", " + imm(4 * Lc) + ", " + V(idx.v));
+    E.valu("v_mul_u32_u24_e32 " + VL(vo) + ", " + imm(4 * Lc) + ", " + VL(idx));
     bool any = false;
     for (uint32_t j = 0; j < Lc; j++) {
       bool same = true;
@@ -1280,11 +1312,11 @@ struct Gen {
       const uint32_t byte = (off + j) * 4;
       const Limb d = dst(j);
       if (byte < 4096) {
-        E.mem("global_load_dword " + V(d.v) + ", " + V(vo.v) + ", s[4:5] offset:" + std::to_string(byte));
+        E.mem("global_load_dword " + VL(d) + ", " + VL(vo) + ", s[4:5] offset:" + std::to_string(byte));
       } else {
         const Limb t = fresh();
-        E.valu("v_add_u32_e32 " + V(t.v) + ", " + hexs(byte) + ", " + V(vo.v));
-        E.mem("global_load_dword " + V(d.v) + ", " + V(t.v) + ", s[4:5]");
+        E.valu("v_add_u32_e32 " + VL(t) + ", " + hexs(byte) + ", " + VL(vo));
+        E.mem("global_load_dword " + VL(d) + ", " + VL(t) + ", s[4:5]");
         drop(t);
       }
       r[j] = d;
@@ -1298,9 +1330,9 @@ struct Gen {
   // e = ((h >> 16) * n) >> 16
   Limb dict_index(const Limb& h, uint32_t n) {
     const Limb e2 = fresh();
-    E.valu("v_lshrrev_b32_e32 " + V(e2.v) + ", 16, " + V(h.v));
-    E.valu("v_mul_u32_u24_e32 " + V(e2.v) + ", " + imm(n) + ", " + V(e2.v));
-    E.valu("v_lshrrev_b32_e32 " + V(e2.v) + ", 16, " + V(e2.v));
+    E.valu("v_lshrrev_b32_e32 " + VL(e2) + ", 16, " + VL(h));
+    E.valu("v_mul_u32_u24_e32 " + VL(e2) + ", " + imm(n) + ", " + VL(e2));
+    E.valu("v_lshrrev_b32_e32 " + VL(e2) + ", 16, " + VL(e2));
     return e2;
   }
 
@@ -1309,7 +1341,7 @@ struct Gen {
     for (size_t j = 0; j < out.size(); j++) {
       const Limb x = j < r.size() ? r[j] : Lit(0);
       if (x == out[j]) continue;  // written in place (tgt): not a reference of its own
-      E.valu("v_mov_b32_e32 " + V(out[j].v) + ", " + src(x));
+      E.valu("v_mov_b32_e32 " + VL(out[j]) + ", " + src(x));
       if (j < r.size()) drop(r[j]);
     }
     r.clear();
@@ -1328,15 +1360,15 @@ struct Gen {
     Mask sb;
     sb.k = 2;
     sb.s = E.salloc();
-    E.valu("v_and_b32_e32 " + V(mag.v) + ", 1, " + V(h.v));
-    E.valu("v_add_u32_e32 " + V(mag.v) + ", 1, " + V(mag.v));
-    E.valu("v_bfe_u32 " + V(neg.v) + ", " + V(h.v) + ", 1, 1");
-    E.valu("v_cmp_ne_u32_e64 " + SP(sb.s) + ", 0, " + V(neg.v), {}, {sb.s, sb.s + 1});
-    E.valu("v_sub_u32_e32 " + V(neg.v) + ", 0, " + V(mag.v));
-    E.valu("v_cndmask_b32_e64 " + V(mag.v) + ", " + V(mag.v) + ", " + V(neg.v) + ", " + SP(sb.s), {sb.s, sb.s + 1});
+    E.valu("v_and_b32_e32 " + VL(mag) + ", 1, " + VL(h));
+    E.valu("v_add_u32_e32 " + VL(mag) + ", 1, " + VL(mag));
+    E.valu("v_bfe_u32 " + VL(neg) + ", " + VL(h) + ", 1, 1");
+    E.valu("v_cmp_ne_u32_e64 " + SP(sb.s) + ", 0, " + VL(neg), {}, {sb.s, sb.s + 1});
+    E.valu("v_sub_u32_e32 " + VL(neg) + ", 0, " + VL(mag));
+    E.valu("v_cndmask_b32_e64 " + VL(mag) + ", " + VL(mag) + ", " + VL(neg) + ", " + SP(sb.s), {sb.s, sb.s + 1});
     drop(neg);
     const uint32_t Lc = (uint32_t)out.size();
-    E.valu("v_add_co_u32_e32 " + V(out[0].v) + ", vcc, " + V(mag.v) + ", " + V(out[0].v), {}, {kVCC, kVCC + 1});
+    E.valu("v_add_co_u32_e32 " + VL(out[0]) + ", vcc, " + VL(mag) + ", " + VL(out[0]), {}, {kVCC, kVCC + 1});
     drop(mag);
     if (Lc > 1) {
       // the high limbs change only in lanes whose low-limb carry differs from the step's sign
@@ -1344,9 +1376,9 @@ struct Gen {
       E.salu("s_xor_b64 s[40:41], vcc, " + SP(sb.s), {40, 41});
       E.ctl("s_cbranch_scc0 " + done);
       const Limb ah = fresh();
-      E.valu("v_cndmask_b32_e64 " + V(ah.v) + ", 0, -1, " + SP(sb.s), {sb.s, sb.s + 1});
+      E.valu("v_cndmask_b32_e64 " + VL(ah) + ", 0, -1, " + SP(sb.s), {sb.s, sb.s + 1});
       for (uint32_t j = 1; j < Lc; j++)
-        E.valu("v_addc_co_u32_e32 " + V(out[j].v) + ", vcc, " + V(ah.v) + ", " + V(out[j].v) + ", vcc", {kVCC, kVCC + 1},
+        E.valu("v_addc_co_u32_e32 " + VL(out[j]) + ", vcc, " + VL(ah) + ", " + VL(out[j]) + ", vcc", {kVCC, kVCC + 1},
                {kVCC, kVCC + 1});
       drop(ah);
       E.label(done);
@@ -1361,7 +1393,7 @@ struct Gen {
   void finish(const std::vector<Limb>& out, uint32_t width, uint32_t clamp, uint64_t zero = 0) {
     const uint32_t Lc = (uint32_t)out.size();
     if ((width & 31) && !(zero >> (Lc - 1) & 1))
-      E.valu("v_and_b32_e32 " + V(out[Lc - 1].v) + ", " + imm(topmask(width)) + ", " + V(out[Lc - 1].v));
+      E.valu("v_and_b32_e32 " + VL(out[Lc - 1]) + ", " + imm(topmask(width)) + ", " + VL(out[Lc - 1]));
     if (!clamp) return;
     const uint32_t r = clamp - 1;
     const uint32_t span = G[r + Lc];
@@ -1388,13 +1420,13 @@ struct Gen {
         Limb d0 = out[0];
         if (G[r]) {
           d0 = fresh();
-          E.valu("v_subrev_u32_e32 " + V(d0.v) + ", " + imm(G[r]) + ", " + V(out[0].v));
+          E.valu("v_subrev_u32_e32 " + VL(d0) + ", " + imm(G[r]) + ", " + VL(out[0]));
         }
         if (inl(span)) {
-          E.valu("v_cmp_le_u32_e64 " + SP(ge.s) + ", " + imm(span) + ", " + V(d0.v), {}, {ge.s, ge.s + 1});
+          E.valu("v_cmp_le_u32_e64 " + SP(ge.s) + ", " + imm(span) + ", " + VL(d0), {}, {ge.s, ge.s + 1});
         } else {
           E.salu("s_mov_b32 s41, " + hexs(span), {41});
-          E.valu("v_cmp_le_u32_e64 " + SP(ge.s) + ", s41, " + V(d0.v), {41}, {ge.s, ge.s + 1});
+          E.valu("v_cmp_le_u32_e64 " + SP(ge.s) + ", s41, " + VL(d0), {41}, {ge.s, ge.s + 1});
         }
         if (G[r]) drop(d0);
         const Mask b2 = mop("or", bad, ge);
@@ -1407,16 +1439,16 @@ struct Gen {
       Limb c0;
       if (span) {
         c0 = mulhi_lit(out[0], span);
-        if (G[r]) E.valu("v_add_u32_e32 " + V(c0.v) + ", " + imm(G[r]) + ", " + V(c0.v));
+        if (G[r]) E.valu("v_add_u32_e32 " + VL(c0) + ", " + imm(G[r]) + ", " + VL(c0));
       }
       mask_to_vcc(bad);
       if (span) {
-        E.valu("v_cndmask_b32_e32 " + V(out[0].v) + ", " + V(out[0].v) + ", " + V(c0.v) + ", vcc", {kVCC, kVCC + 1});
+        E.valu("v_cndmask_b32_e32 " + VL(out[0]) + ", " + VL(out[0]) + ", " + VL(c0) + ", vcc", {kVCC, kVCC + 1});
         drop(c0);
       }
       for (uint32_t j = 1; j < Lc; j++)
         if (!(zero >> j & 1))
-          E.valu("v_cndmask_b32_e32 " + V(out[j].v) + ", " + V(out[j].v) + ", v6, vcc", {kVCC, kVCC + 1});
+          E.valu("v_cndmask_b32_e32 " + VL(out[j]) + ", " + VL(out[j]) + ", v6, vcc", {kVCC, kVCC + 1});
       E.srelease(bad);
       return;
     }
@@ -1447,7 +1479,7 @@ struct Gen {
       ge.s = E.salloc();
       const Limb d0 = vreg(dif[0]);
       E.salu("s_mov_b32 s41, " + hexs(span), {41});
-      E.valu("v_cmp_le_u32_e64 " + SP(ge.s) + ", s41, " + V(d0.v), {41}, {ge.s, ge.s + 1});
+      E.valu("v_cmp_le_u32_e64 " + SP(ge.s) + ", s41, " + VL(d0), {41}, {ge.s, ge.s + 1});
       drop(d0);
       const Mask b2 = mop("or", bad, ge);
       E.srelease(ge);
@@ -1469,7 +1501,7 @@ struct Gen {
         tmp = vreg(t);
         t = tmp;
       }
-      E.valu("v_cndmask_b32_e32 " + V(out[j].v) + ", " + V(out[j].v) + ", " + V(t.v) + ", vcc", {kVCC, kVCC + 1});
+      E.valu("v_cndmask_b32_e32 " + VL(out[j]) + ", " + VL(out[j]) + ", " + VL(t) + ", vcc", {kVCC, kVCC + 1});
       drop(tmp);
       drop(cl[j]);
     }
@@ -1484,11 +1516,11 @@ struct Gen {
       if (!m) continue;
       if (in_place) {
         if (m == 0xFFFFFFFFu) {
-          E.valu("v_mov_b32_e32 " + V(r[j].v) + ", " + imm(v));
+          E.valu("v_mov_b32_e32 " + VL(r[j]) + ", " + imm(v));
           continue;
         }
-        E.valu("v_and_b32_e32 " + V(r[j].v) + ", " + imm(~m) + ", " + V(r[j].v));
-        if (v) E.valu("v_or_b32_e32 " + V(r[j].v) + ", " + imm(v) + ", " + V(r[j].v));
+        E.valu("v_and_b32_e32 " + VL(r[j]) + ", " + imm(~m) + ", " + VL(r[j]));
+        if (v) E.valu("v_or_b32_e32 " + VL(r[j]) + ", " + imm(v) + ", " + VL(r[j]));
         continue;
       }
       if (m == 0xFFFFFFFFu || r[j].lit()) {
@@ -1502,7 +1534,7 @@ struct Gen {
       r[j] = a;
       if (v) {
         const Limb d = fresh();
-        E.valu("v_or_b32_e32 " + V(d.v) + ", " + imm(v) + ", " + V(a.v));
+        E.valu("v_or_b32_e32 " + VL(d) + ", " + imm(v) + ", " + VL(a));
         drop(a);
         r[j] = d;
       }
@@ -1656,9 +1688,9 @@ struct Gen {
           const int32_t bit0 = (int32_t)(j * 32) - sh;
           if (bit0 <= -32 || bit0 >= 32) continue;
           const Limb d = fresh();
-          if (bit0 < 0) E.valu("v_lshlrev_b32_e32 " + V(d.v) + ", " + std::to_string(-bit0) + ", " + V(m.v));
-          else if (bit0 > 0) E.valu("v_lshrrev_b32_e32 " + V(d.v) + ", " + std::to_string(bit0) + ", " + V(m.v));
-          else E.valu("v_mov_b32_e32 " + V(d.v) + ", " + V(m.v));
+          if (bit0 < 0) E.valu("v_lshlrev_b32_e32 " + VL(d) + ", " + std::to_string(-bit0) + ", " + VL(m));
+          else if (bit0 > 0) E.valu("v_lshrrev_b32_e32 " + VL(d) + ", " + std::to_string(bit0) + ", " + VL(m));
+          else E.valu("v_mov_b32_e32 " + VL(d) + ", " + VL(m));
           mw[j] = d;
         }
         drop(m);
@@ -1769,20 +1801,23 @@ struct Gen {
             // VOP3: literal operands through s41 (one SGPR per instruction)
             const Limb vx = x.reg() ? x : y, ly = x.reg() ? y : x;
             std::string so;
-            std::initializer_list<int> rd = {};
-            if (ly.lit() && !inl(ly.v)) {
+            // a literal operand goes through s41 (read by the multiplies: an SGPR the hazard table
+            // tracks; a temporary initializer_list here would dangle)
+            const bool via_s41 = ly.lit() && !inl(ly.v);
+            if (via_s41) {
               E.salu("s_mov_b32 s41, " + hexs(ly.v), {41});
               so = "s41";
-              rd = {41};
             } else {
               so = src(ly);
             }
             const Limb dl = fresh();
-            E.valu("v_mul_lo_u32 " + V(dl.v) + ", " + V(vx.v) + ", " + so, rd);
+            if (via_s41) E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so, {41});
+            else E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so);
             lo[i + j] = dl;
             if (i + j + 1 < n) {
               const Limb dh = fresh();
-              E.valu("v_mul_hi_u32 " + V(dh.v) + ", " + V(vx.v) + ", " + so, rd);
+              if (via_s41) E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so, {41});
+              else E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so);
               hi[i + j + 1] = dh;
             }
           }
@@ -1819,17 +1854,21 @@ struct Gen {
             }
             const Limb vx = x.reg() ? x : y, ly = x.reg() ? y : x;
             std::string so;
-            std::initializer_list<int> rd = {};
-            if (ly.lit() && !inl(ly.v)) {
+            const bool via_s41 = ly.lit() && !inl(ly.v);
+            if (via_s41) {
               E.salu("s_mov_b32 s41, " + hexs(ly.v), {41});
               so = "s41";
-              rd = {41};
             } else {
               so = src(ly);
             }
             const Limb dl = fresh(), dh = fresh();
-            E.valu("v_mul_lo_u32 " + V(dl.v) + ", " + V(vx.v) + ", " + so, rd);
-            E.valu("v_mul_hi_u32 " + V(dh.v) + ", " + V(vx.v) + ", " + so, rd);
+            if (via_s41) {
+              E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so, {41});
+              E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so, {41});
+            } else {
+              E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so);
+              E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so);
+            }
             lo[i + j] = dl;
             hi[i + j + 1] = dh;
           }
@@ -1900,27 +1939,27 @@ struct Gen {
           drop(xs[j]);
           const Limb q0 = fresh(), q1 = fresh(), t = fresh(), rr = fresh();
           // (q1:q0) = rv * u1 + (u1 + 1 : u0)
-          E.valu("v_mul_lo_u32 " + V(q0.v) + ", " + V(u1.v) + ", s41", {41});
-          E.valu("v_mul_hi_u32 " + V(q1.v) + ", " + V(u1.v) + ", s41", {41});
-          E.valu("v_add_co_u32_e32 " + V(q0.v) + ", vcc, " + V(q0.v) + ", " + V(u0.v), {}, {kVCC, kVCC + 1});
-          E.valu("v_addc_co_u32_e32 " + V(q1.v) + ", vcc, " + V(q1.v) + ", " + V(u1.v) + ", vcc", {kVCC, kVCC + 1},
+          E.valu("v_mul_lo_u32 " + VL(q0) + ", " + VL(u1) + ", s41", {41});
+          E.valu("v_mul_hi_u32 " + VL(q1) + ", " + VL(u1) + ", s41", {41});
+          E.valu("v_add_co_u32_e32 " + VL(q0) + ", vcc, " + VL(q0) + ", " + VL(u0), {}, {kVCC, kVCC + 1});
+          E.valu("v_addc_co_u32_e32 " + VL(q1) + ", vcc, " + VL(q1) + ", " + VL(u1) + ", vcc", {kVCC, kVCC + 1},
                  {kVCC, kVCC + 1});
-          E.valu("v_add_u32_e32 " + V(q1.v) + ", 1, " + V(q1.v));
+          E.valu("v_add_u32_e32 " + VL(q1) + ", 1, " + VL(q1));
           // r = u0 - q1 * dn (mod 2^32)
-          E.valu("v_mul_lo_u32 " + V(t.v) + ", " + V(q1.v) + ", s40", {40});
-          E.valu("v_sub_u32_e32 " + V(rr.v) + ", " + V(u0.v) + ", " + V(t.v));
+          E.valu("v_mul_lo_u32 " + VL(t) + ", " + VL(q1) + ", s40", {40});
+          E.valu("v_sub_u32_e32 " + VL(rr) + ", " + VL(u0) + ", " + VL(t));
           // r > q0: q1 - 1, r + dn
-          E.valu("v_cmp_gt_u32_e64 " + M + ", " + V(rr.v) + ", " + V(q0.v), {}, {mk.s, mk.s + 1});
-          E.valu("v_add_u32_e32 " + V(t.v) + ", -1, " + V(q1.v));
-          E.valu("v_add_u32_e32 " + V(q0.v) + ", s40, " + V(rr.v), {40});
-          E.valu("v_cndmask_b32_e64 " + V(q1.v) + ", " + V(q1.v) + ", " + V(t.v) + ", " + M, {mk.s, mk.s + 1});
-          E.valu("v_cndmask_b32_e64 " + V(rr.v) + ", " + V(rr.v) + ", " + V(q0.v) + ", " + M, {mk.s, mk.s + 1});
+          E.valu("v_cmp_gt_u32_e64 " + M + ", " + VL(rr) + ", " + VL(q0), {}, {mk.s, mk.s + 1});
+          E.valu("v_add_u32_e32 " + VL(t) + ", -1, " + VL(q1));
+          E.valu("v_add_u32_e32 " + VL(q0) + ", s40, " + VL(rr), {40});
+          E.valu("v_cndmask_b32_e64 " + VL(q1) + ", " + VL(q1) + ", " + VL(t) + ", " + M, {mk.s, mk.s + 1});
+          E.valu("v_cndmask_b32_e64 " + VL(rr) + ", " + VL(rr) + ", " + VL(q0) + ", " + M, {mk.s, mk.s + 1});
           // r >= dn: q1 + 1, r - dn
-          E.valu("v_cmp_le_u32_e64 " + M + ", s40, " + V(rr.v), {40}, {mk.s, mk.s + 1});
-          E.valu("v_add_u32_e32 " + V(t.v) + ", 1, " + V(q1.v));
-          E.valu("v_subrev_u32_e32 " + V(q0.v) + ", s40, " + V(rr.v), {40});
-          E.valu("v_cndmask_b32_e64 " + V(q1.v) + ", " + V(q1.v) + ", " + V(t.v) + ", " + M, {mk.s, mk.s + 1});
-          E.valu("v_cndmask_b32_e64 " + V(rr.v) + ", " + V(rr.v) + ", " + V(q0.v) + ", " + M, {mk.s, mk.s + 1});
+          E.valu("v_cmp_le_u32_e64 " + M + ", s40, " + VL(rr), {40}, {mk.s, mk.s + 1});
+          E.valu("v_add_u32_e32 " + VL(t) + ", 1, " + VL(q1));
+          E.valu("v_subrev_u32_e32 " + VL(q0) + ", s40, " + VL(rr), {40});
+          E.valu("v_cndmask_b32_e64 " + VL(q1) + ", " + VL(q1) + ", " + VL(t) + ", " + M, {mk.s, mk.s + 1});
+          E.valu("v_cndmask_b32_e64 " + VL(rr) + ", " + VL(rr) + ", " + VL(q0) + ", " + M, {mk.s, mk.s + 1});
           drop(u1);
           drop(u0);
           drop(q0);
@@ -1933,7 +1972,7 @@ struct Gen {
         if (in.op == K_UREM) {
           if (sh) {
             const Limb d0 = fresh();
-            E.valu("v_lshrrev_b32_e32 " + V(d0.v) + ", " + std::to_string(sh) + ", " + V(rem.v));
+            E.valu("v_lshrrev_b32_e32 " + VL(d0) + ", " + std::to_string(sh) + ", " + VL(rem));
             drop(rem);
             rem = d0;
           }
@@ -1975,7 +2014,7 @@ struct Gen {
           }
           const char* op = in.op == K_AND ? "v_and_b32_e32 " : in.op == K_OR ? "v_or_b32_e32 " : "v_xor_b32_e32 ";
           const Limb dd = fresh();
-          E.valu(op + V(dd.v) + ", " + src(l.lit() ? l : a) + ", " + V(l.lit() ? v.v : b.v));
+          E.valu(op + VL(dd) + ", " + src(l.lit() ? l : a) + ", " + VL(l.lit() ? v : b));
           r[j] = dd;
         }
         set(d, r);
@@ -1995,7 +2034,7 @@ struct Gen {
             continue;
           }
           const Limb dd = fresh();
-          E.valu("v_not_b32_e32 " + V(dd.v) + ", " + V(a.v));
+          E.valu("v_not_b32_e32 " + VL(dd) + ", " + VL(a));
           r[j] = dd;
         }
         mask_top(r, W);
@@ -2153,13 +2192,13 @@ struct Gen {
         } else {
           if (wa & 31) {
             top = fresh();
-            E.valu("v_bfe_i32 " + V(top.v) + ", " + V(t.v) + ", 0, " + std::to_string(wa & 31));
+            E.valu("v_bfe_i32 " + VL(top) + ", " + VL(t) + ", 0, " + std::to_string(wa & 31));
           } else {
             top = t;
             E.retain(top);
           }
           f = fresh();
-          E.valu("v_ashrrev_i32_e32 " + V(f.v) + ", 31, " + V(top.v));
+          E.valu("v_ashrrev_i32_e32 " + VL(f) + ", 31, " + VL(top));
         }
         r[La - 1] = top;
         for (uint32_t j = La; j < Ld; j++) {
@@ -2272,7 +2311,7 @@ struct Gen {
           for (uint32_t j = 0; j < Lw_; j++) {
             const Limb x = vreg(limb(in.a, j));
             row_ptr(in.p0 + j, 12);
-            E.mem("global_store_dword v8, " + V(x.v) + ", s[40:41]");
+            E.mem("global_store_dword v8, " + VL(x) + ", s[40:41]");
             drop(x);
           }
           E.salu("s_mov_b64 exec, -1");
@@ -2405,17 +2444,17 @@ struct Gen {
   void vfmix(int lo, int hi) {
     const Limb t1 = fresh(), t2 = fresh();
     auto xs = [&]() {
-      E.valu("v_lshrrev_b32_e32 " + V(t1.v) + ", 1, " + V(hi));
-      E.valu("v_xor_b32_e32 " + V(lo) + ", " + V(lo) + ", " + V(t1.v));
+      E.valu("v_lshrrev_b32_e32 " + VL(t1) + ", 1, " + V(hi));
+      E.valu("v_xor_b32_e32 " + V(lo) + ", " + V(lo) + ", " + VL(t1));
     };
     auto mul = [&](uint32_t clo, uint32_t chi) {
       E.salu("s_mov_b32 s40, " + hexs(clo), {40});
       E.salu("s_mov_b32 s41, " + hexs(chi), {41});
-      E.valu("v_mul_hi_u32 " + V(t1.v) + ", " + V(lo) + ", s40", {40});
-      E.valu("v_mul_lo_u32 " + V(t2.v) + ", " + V(lo) + ", s41", {41});
-      E.valu("v_add_u32_e32 " + V(t1.v) + ", " + V(t1.v) + ", " + V(t2.v));
-      E.valu("v_mul_lo_u32 " + V(t2.v) + ", " + V(hi) + ", s40", {40});
-      E.valu("v_add_u32_e32 " + V(hi) + ", " + V(t1.v) + ", " + V(t2.v));
+      E.valu("v_mul_hi_u32 " + VL(t1) + ", " + V(lo) + ", s40", {40});
+      E.valu("v_mul_lo_u32 " + VL(t2) + ", " + V(lo) + ", s41", {41});
+      E.valu("v_add_u32_e32 " + VL(t1) + ", " + VL(t1) + ", " + VL(t2));
+      E.valu("v_mul_lo_u32 " + VL(t2) + ", " + V(hi) + ", s40", {40});
+      E.valu("v_add_u32_e32 " + V(hi) + ", " + VL(t1) + ", " + VL(t2));
       E.valu("v_mul_lo_u32 " + V(lo) + ", " + V(lo) + ", s40", {40});
     };
     xs();
@@ -2482,11 +2521,11 @@ struct Gen {
         E.salu("s_addc_u32 s41, " + S(b + 1) + ", 0", {41});
         base = "s[40:41]";
       }
-      E.mem("global_load_dword " + V(d.v) + ", v2, " + base + " offset:" + std::to_string(byte & 4095u) +
+      E.mem("global_load_dword " + VL(d) + ", v2, " + base + " offset:" + std::to_string(byte & 4095u) +
             "  ; soa row " + std::to_string(row) + note);
     } else {
       row_ptr(row, 4);
-      E.mem("global_load_dword " + V(d.v) + ", " + voff + ", s[40:41]  ; soa row " + std::to_string(row) + note);
+      E.mem("global_load_dword " + VL(d) + ", " + voff + ", s[40:41]  ; soa row " + std::to_string(row) + note);
     }
   }
   // s[d:d+1] = soa + g * coord_words * 256 for the group index in s[g]
@@ -2520,7 +2559,7 @@ struct Gen {
       const size_t p = rows_used++;
       if (p < ring_reg.size()) {  // a ring register: copied out, reloaded for the next group below
         r[j] = fresh();
-        E.valu("v_mov_b32_e32 " + V(r[j].v) + ", " + V(ring_reg[p].v));
+        E.valu("v_mov_b32_e32 " + VL(r[j]) + ", " + VL(ring_reg[p]));
       } else {
         r[j] = row_reg[p];
       }
@@ -2528,7 +2567,7 @@ struct Gen {
       const size_t M = rows.size(), R = ring_reg.size();
       if (p + R >= M) {  // the next group's ring row p + R - M (clamped offsets: always in bounds)
         const size_t q = p + R - M;
-        load_row(ring_reg[q], rows[q], 28, V(vnext.v), " (next group)");
+        load_row(ring_reg[q], rows[q], 28, VL(vnext), " (next group)");
         loads++;
       }
     }
@@ -2607,9 +2646,9 @@ struct Gen {
     } else {
       E.valu("v_min_u32_e32 v2, s23, v3", {23});
       E.valu("v_lshlrev_b32_e32 v2, 2, v2");
-      E.valu("v_add_u32_e32 " + V(vnext.v) + ", s17, v3", {17});
-      E.valu("v_min_u32_e32 " + V(vnext.v) + ", s23, " + V(vnext.v), {23});
-      E.valu("v_lshlrev_b32_e32 " + V(vnext.v) + ", 2, " + V(vnext.v));
+      E.valu("v_add_u32_e32 " + VL(vnext) + ", s17, v3", {17});
+      E.valu("v_min_u32_e32 " + VL(vnext) + ", s23, " + VL(vnext), {23});
+      E.valu("v_lshlrev_b32_e32 " + VL(vnext) + ", 2, " + VL(vnext));
     }
     E.valu("v_cmp_gt_u32_e64 s[24:25], s8, v3", {8}, {24, 25});
     E.valu("v_lshlrev_b32_e32 v8, 2, v3");  // watch-row store offset 4 i

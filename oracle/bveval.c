@@ -163,9 +163,13 @@ static void vneg(val_t* r, const val_t* a, uint32_t width) {
 }
 
 static void vsub(val_t* r, const val_t* a, const val_t* b, uint32_t width) {
-  val_t nb;
-  vneg(&nb, b, MAXW * 64);
-  vadd(r, a, &nb, width);
+  uint64_t br = 0;
+  for (int i = 0; i < MAXW; i++) {
+    const uint64_t x = a->w[i], y = b->w[i];
+    r->w[i] = x - y - br;
+    br = (x < y) || (x - y < br);
+  }
+  vmask(r, width);
 }
 
 static void vmul(val_t* r, const val_t* a, const val_t* b, uint32_t width, val_t* hi) {
@@ -205,7 +209,21 @@ static void vshl1(val_t* a) {
 static void vdivrem(const val_t* a, const val_t* b, uint32_t width, val_t* q, val_t* r) {
   vzero(q);
   vzero(r);
-  for (int i = (int)width - 1; i >= 0; i--) {
+  int small = b->w[0] != 0;
+  for (int i = 1; i < MAXW && small; i++) small = b->w[i] == 0;
+  if (small) { /* a one-word divisor: schoolbook division by 64-bit digits */
+    unsigned __int128 rem = 0;
+    for (int i = nw(width) - 1; i >= 0; i--) {
+      const unsigned __int128 cur = (rem << 64) | a->w[i];
+      q->w[i] = (uint64_t)(cur / b->w[0]);
+      rem = cur % b->w[0];
+    }
+    r->w[0] = (uint64_t)rem;
+    return;
+  }
+  int top = (int)width - 1; /* the dividend's leading zeros leave r = 0 and their quotient bits 0 */
+  while (top >= 0 && !vbit(a, (uint32_t)top)) top--;
+  for (int i = top; i >= 0; i--) {
     vshl1(r);
     r->w[0] |= (uint64_t)vbit(a, (uint32_t)i);
     if (!vult(r, b)) {
@@ -217,20 +235,36 @@ static void vdivrem(const val_t* a, const val_t* b, uint32_t width, val_t* q, va
   }
 }
 
+/* shifts by whole words and a bit remainder; the operand is masked to the width first */
 static void vshl(val_t* r, const val_t* a, uint64_t s, uint32_t width) {
   vzero(r);
   if (s >= width) return;
-  for (uint32_t i = 0; i + s < width; i++)
-    if (vbit(a, i)) r->w[(i + s) / 64] |= 1ull << ((i + s) % 64);
+  val_t t = *a;
+  vmask(&t, width);
+  const int q = (int)(s / 64), b = (int)(s % 64);
+  for (int i = MAXW - 1; i >= q; i--) {
+    uint64_t x = t.w[i - q] << b;
+    if (b && i - q >= 1) x |= t.w[i - q - 1] >> (64 - b);
+    r->w[i] = x;
+  }
+  vmask(r, width);
 }
 
 static void vshr(val_t* r, const val_t* a, uint64_t s, uint32_t width, int fill) {
   vzero(r);
-  for (uint32_t i = 0; i < width; i++) {
-    uint64_t src = i + s;
-    int bit = src < width ? vbit(a, (uint32_t)src) : fill;
-    if (bit) r->w[i / 64] |= 1ull << (i % 64);
+  val_t t = *a;
+  vmask(&t, width);
+  if (s < width) {
+    const int q = (int)(s / 64), b = (int)(s % 64);
+    for (int i = 0; i + q < MAXW; i++) {
+      uint64_t x = t.w[i + q] >> b;
+      if (b && i + q + 1 < MAXW) x |= t.w[i + q + 1] << (64 - b);
+      r->w[i] = x;
+    }
   }
+  if (fill) /* bits [width - s, width) take the sign */
+    for (uint32_t i = s < width ? width - (uint32_t)s : 0; i < width; i++) r->w[i / 64] |= 1ull << (i % 64);
+  vmask(r, width);
 }
 
 static uint64_t vsmall(const val_t* b, uint32_t cap) {

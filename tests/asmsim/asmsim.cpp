@@ -1,0 +1,1199 @@
+// CPU simulator of the first JIT tier's gfx950 instruction subset (see asmsim.hpp).  Test
+// infrastructure only.
+#include "asmsim.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <deque>
+#include <sstream>
+#include <unordered_map>
+
+namespace asmsim {
+
+namespace {
+
+[[noreturn]] void err(const std::string& w) { throw SimError{w}; }
+
+#define OPS(X)                                                                                                    \
+  X(s_mov_b32) X(s_mov_b64) X(s_add_u32) X(s_addc_u32) X(s_sub_u32) X(s_subb_u32) X(s_add_i32) X(s_sub_i32)       \
+  X(s_mul_i32) X(s_mul_hi_u32) X(s_lshl_b32) X(s_lshr_b32) X(s_ashr_i32) X(s_lshl_b64) X(s_lshr_b64)              \
+  X(s_and_b32) X(s_or_b32) X(s_xor_b32) X(s_andn2_b32) X(s_and_b64) X(s_or_b64) X(s_xor_b64) X(s_andn2_b64)       \
+  X(s_orn2_b64) X(s_nor_b64) X(s_xnor_b64) X(s_not_b32) X(s_not_b64) X(s_min_u32) X(s_max_u32) X(s_cselect_b32)   \
+  X(s_cselect_b64) X(s_cmp_eq_u32) X(s_cmp_lg_u32) X(s_cmp_lt_u32) X(s_cmp_le_u32) X(s_cmp_gt_u32)                 \
+  X(s_cmp_ge_u32) X(s_cmp_eq_u64) X(s_cmp_lg_u64) X(s_ff1_i32_b64) X(s_bcnt1_i32_b64) X(s_ff1_i32_b32)           \
+  X(s_flbit_i32_b32) X(s_bfe_u32)                                                                                 \
+  X(s_cbranch_scc0) X(s_cbranch_scc1) X(s_cbranch_vccz) X(s_cbranch_vccnz) X(s_cbranch_execz) X(s_branch)         \
+  X(s_nop) X(s_waitcnt) X(s_barrier) X(s_endpgm)                                                                  \
+  X(s_load_dword) X(s_load_dwordx2) X(s_load_dwordx4) X(s_load_dwordx8)                                           \
+  X(v_mov_b32) X(v_add_u32) X(v_sub_u32) X(v_subrev_u32) X(v_add_co_u32) X(v_addc_co_u32) X(v_sub_co_u32)        \
+  X(v_subrev_co_u32) X(v_subb_co_u32) X(v_subbrev_co_u32) X(v_and_b32) X(v_or_b32) X(v_xor_b32) X(v_not_b32)     \
+  X(v_lshlrev_b32) X(v_lshrrev_b32) X(v_ashrrev_i32) X(v_min_u32) X(v_max_u32) X(v_mul_u32_u24) X(v_mul_lo_u32)  \
+  X(v_mul_hi_u32) X(v_cndmask_b32) X(v_cmp_eq_u32) X(v_cmp_ne_u32) X(v_cmp_lt_u32) X(v_cmp_le_u32)                \
+  X(v_cmp_gt_u32) X(v_cmp_ge_u32) X(v_cmp_eq_i32) X(v_cmp_ne_i32) X(v_cmp_lt_i32) X(v_cmp_le_i32) X(v_cmp_gt_i32) \
+  X(v_cmp_ge_i32) X(v_cmp_eq_u64) X(v_cmp_ne_u64) X(v_cmp_lt_u64) X(v_cmp_le_u64) X(v_cmp_gt_u64) X(v_cmp_ge_u64) \
+  X(v_bfe_u32) X(v_bfe_i32) X(v_alignbit_b32) X(v_lshl_or_b32) X(v_add3_u32) X(v_or3_b32) X(v_xad_u32)           \
+  X(v_and_or_b32) X(v_lshl_add_u32) X(v_add_lshl_u32) X(v_bitop3_b32) X(v_readfirstlane_b32) X(v_lshlrev_b64)     \
+  X(v_lshrrev_b64) X(v_ffbh_u32) X(v_ffbl_b32) X(v_perm_b32) X(v_mad_u32_u24) X(v_mad_u64_u32) X(v_bfi_b32)       \
+  X(v_cvt_f32_u32) X(v_rcp_iflag_f32) X(v_cvt_u32_f32) X(v_mul_f32) X(v_readlane_b32) X(v_writelane_b32)          \
+  X(global_load_dword) X(global_load_dwordx2) X(global_load_dwordx4) X(global_store_byte) X(global_store_dword)  \
+  X(global_atomic_umin_x2) X(global_atomic_add_x2) X(ds_read_b32) X(ds_write_b32) X(ds_read_b64) X(ds_write_b64)  \
+  X(ds_read2_b32)
+
+enum Op {
+#define X_ENUM(n) OP_##n,
+  OPS(X_ENUM)
+#undef X_ENUM
+      OP_COUNT
+};
+const char* kNames[] = {
+#define X_NAME(n) #n,
+    OPS(X_NAME)
+#undef X_NAME
+};
+
+// encodings: 0 none/VOP3-only, 1 _e32, 2 _e64, 3 _sdwa
+struct OpKey {
+  int op, enc;
+};
+
+const std::unordered_map<std::string, int>& names() {
+  static const std::unordered_map<std::string, int> m = [] {
+    std::unordered_map<std::string, int> r;
+    for (int i = 0; i < OP_COUNT; i++) r[kNames[i]] = i;
+    return r;
+  }();
+  return m;
+}
+
+std::string trim(const std::string& s) {
+  size_t a = 0, b = s.size();
+  while (a < b && isspace((unsigned char)s[a])) a++;
+  while (b > a && isspace((unsigned char)s[b - 1])) b--;
+  return s.substr(a, b - a);
+}
+
+bool parse_int(const std::string& t, int64_t& v) {
+  if (t.empty()) return false;
+  const char* p = t.c_str();
+  char* e = nullptr;
+  bool neg = false;
+  if (*p == '-') {
+    neg = true;
+    p++;
+  }
+  if (!isdigit((unsigned char)*p)) return false;
+  unsigned long long x = strtoull(p, &e, 0);
+  if (*e) return false;
+  v = neg ? -(int64_t)x : (int64_t)x;
+  return true;
+}
+
+Opd operand(const std::string& t0) {
+  const std::string t = trim(t0);
+  Opd o;
+  auto reg = [&](char c, OKind k) -> bool {
+    if (t.size() < 2 || t[0] != c) return false;
+    if (t[1] == '[') {
+      const size_t colon = t.find(':'), close = t.find(']');
+      if (colon == std::string::npos || close == std::string::npos) err("bad register range " + t);
+      const int a = atoi(t.substr(2, colon - 2).c_str()), b = atoi(t.substr(colon + 1, close - colon - 1).c_str());
+      o.k = k;
+      o.r = a;
+      o.n = b - a + 1;
+      return true;
+    }
+    for (size_t i = 1; i < t.size(); i++)
+      if (!isdigit((unsigned char)t[i])) return false;
+    o.k = k;
+    o.r = atoi(t.c_str() + 1);
+    o.n = 1;
+    return true;
+  };
+  if (t == "vcc") {
+    o.k = O_S;
+    o.r = 106;
+    o.n = 2;
+    return o;
+  }
+  if (t == "vcc_lo") {
+    o.k = O_S;
+    o.r = 106;
+    return o;
+  }
+  if (t == "vcc_hi") {
+    o.k = O_S;
+    o.r = 107;
+    return o;
+  }
+  if (t == "exec") {
+    o.k = O_EXEC;
+    o.n = 2;
+    return o;
+  }
+  if (t == "off") {
+    o.k = O_OFF;
+    return o;
+  }
+  if (reg('v', O_V) || reg('s', O_S)) return o;
+  int64_t v;
+  if (parse_int(t, v)) {
+    o.k = O_IMM;
+    o.imm = (uint64_t)v;
+    o.inl = v >= -16 && v <= 64;
+    return o;
+  }
+  err("unknown operand '" + t + "'");
+}
+
+}  // namespace
+
+Module parse(const std::string& text) {
+  Module m;
+  std::unordered_map<std::string, int> labels;
+  std::vector<std::pair<size_t, std::string>> fix;  // instruction -> label to resolve
+  std::istringstream in(text);
+  std::string line;
+  bool meta = false;
+  std::string cur_kd;
+  while (std::getline(in, line)) {
+    const size_t sc = line.find(';');
+    const std::string raw = line;
+    if (sc != std::string::npos) line = line.substr(0, sc);
+    std::string t = trim(line);
+    if (t.empty()) continue;
+    if (t == ".amdgpu_metadata") {
+      meta = true;
+      continue;
+    }
+    if (t == ".end_amdgpu_metadata") {
+      meta = false;
+      continue;
+    }
+    if (meta) continue;
+    if (t[0] == '.') {
+      if (t.rfind(".amdhsa_kernel ", 0) == 0) cur_kd = trim(t.substr(15));
+      if (t.rfind(".amdhsa_group_segment_fixed_size", 0) == 0 && !cur_kd.empty())
+        m.kernels[cur_kd].lds_bytes = (uint32_t)atol(trim(t.substr(32)).c_str());
+      if (t == ".end_amdhsa_kernel") cur_kd.clear();
+      if (t.back() == ':' && t.find(' ') == std::string::npos) labels[t.substr(0, t.size() - 1)] = (int)m.code.size();
+      continue;
+    }
+    if (t.back() == ':' && t.find(' ') == std::string::npos) {
+      const std::string L = t.substr(0, t.size() - 1);
+      labels[L] = (int)m.code.size();
+      if (L[0] != '.') m.kernels[L].entry = m.code.size();
+      continue;
+    }
+    Ins ins;
+    ins.text = trim(raw);
+    const size_t sp = t.find_first_of(" \t");
+    std::string mn = sp == std::string::npos ? t : t.substr(0, sp);
+    std::string rest = sp == std::string::npos ? "" : trim(t.substr(sp));
+    int enc = 0;
+    auto strip = [&](const char* suf, int e) {
+      const size_t n = strlen(suf);
+      if (mn.size() > n && mn.compare(mn.size() - n, n, suf) == 0) {
+        mn = mn.substr(0, mn.size() - n);
+        enc = e;
+      }
+    };
+    strip("_e32", 1);
+    strip("_e64", 2);
+    strip("_sdwa", 3);
+    auto it = names().find(mn);
+    if (it == names().end()) err("unknown instruction '" + ins.text + "'");
+    ins.op = it->second;
+    ins.a.reserve(6);
+    // enc in the first operand slot's spare bits: kept in offset's companion (vmcnt unused)
+    if (ins.op == OP_s_waitcnt) {
+      std::istringstream ws(rest);
+      std::string tok;
+      while (ws >> tok) {
+        const size_t lp = tok.find('('), rp = tok.find(')');
+        if (lp == std::string::npos || rp == std::string::npos) err("bad s_waitcnt " + ins.text);
+        const int n = atoi(tok.substr(lp + 1, rp - lp - 1).c_str());
+        if (tok.rfind("vmcnt", 0) == 0) ins.vmcnt = n;
+        else if (tok.rfind("lgkmcnt", 0) == 0) ins.lgkmcnt = n;
+        else err("bad s_waitcnt " + ins.text);
+      }
+      m.code.push_back(ins);
+      continue;
+    }
+    if (ins.op == OP_s_cbranch_scc0 || ins.op == OP_s_cbranch_scc1 || ins.op == OP_s_branch ||
+        ins.op == OP_s_cbranch_vccz || ins.op == OP_s_cbranch_vccnz || ins.op == OP_s_cbranch_execz) {
+      fix.push_back({m.code.size(), rest});
+      m.code.push_back(ins);
+      continue;
+    }
+    // operands separated by commas; modifiers (offset:N, sc0/sc1/nt, sdwa selects) after the last
+    std::vector<std::string> parts;
+    {
+      std::string cur;
+      for (char c : rest) {
+        if (c == ',') {
+          parts.push_back(cur);
+          cur.clear();
+        } else {
+          cur += c;
+        }
+      }
+      if (!trim(cur).empty() || !parts.empty()) parts.push_back(cur);
+    }
+    if (!parts.empty()) {
+      std::istringstream ls(parts.back());
+      std::string first, tok;
+      ls >> first;
+      std::vector<std::string> mods;
+      while (ls >> tok) mods.push_back(tok);
+      // a lone modifier list after an operand ("s[4:5] offset:8")
+      parts.back() = first;
+      for (const std::string& md : mods) {
+        if (md.rfind("offset:", 0) == 0) {
+          int64_t v;
+          if (!parse_int(md.substr(7), v)) err("bad offset " + ins.text);
+          ins.offset = v;
+        } else if (md == "sc0" || md == "sc1" || md == "nt") {
+          // cache policy bits: no effect on a single-device simulation
+        } else if (md.rfind("src1_sel:", 0) == 0) {
+          const std::string s = md.substr(9);
+          if (s == "WORD_1") ins.sdwa_src1_word1 = 1;
+          else if (s != "DWORD") err("unsupported sdwa select " + ins.text);
+        } else if (md == "dst_sel:DWORD" || md == "dst_unused:UNUSED_PAD" || md == "src0_sel:DWORD") {
+        } else {
+          err("unsupported modifier '" + md + "' in " + ins.text);
+        }
+      }
+    }
+    for (const std::string& p : parts) ins.a.push_back(operand(p));
+    ins.enc = enc;
+    m.code.push_back(ins);
+  }
+  for (auto& f : fix) {
+    auto it = labels.find(trim(f.second));
+    if (it == labels.end()) err("unknown label " + f.second);
+    m.code[f.first].target = it->second;
+  }
+  return m;
+}
+
+uint64_t Memory::add(size_t bytes, const void* init) {
+  Buffer b;
+  b.base = (uint64_t)(bufs.size() + 1) << 36;
+  b.data.assign(bytes, 0);
+  if (init && bytes) memcpy(b.data.data(), init, bytes);
+  bufs.push_back(std::move(b));
+  return bufs.back().base;
+}
+
+uint8_t* Memory::at(uint64_t addr, size_t n) {
+  const uint64_t k = (addr >> 36);
+  if (k == 0 || k > bufs.size()) {
+    std::ostringstream o;
+    o << "access to 0x" << std::hex << addr << " outside every buffer";
+    err(o.str());
+  }
+  Buffer& b = bufs[k - 1];
+  const uint64_t off = addr - b.base;
+  if (off + n > b.data.size()) {
+    std::ostringstream o;
+    o << "access at byte " << off << " (+" << n << ") of a " << b.data.size() << "-byte buffer";
+    err(o.str());
+  }
+  return b.data.data() + off;
+}
+
+Buffer& Memory::of(uint64_t base) {
+  for (auto& b : bufs)
+    if (b.base == base) return b;
+  err("no buffer at that base");
+}
+
+namespace {
+
+constexpr int kNS = 108;  // s0..s105, vcc = s106:107
+
+struct Pend {
+  std::vector<int> v, s;
+};
+
+struct Wave {
+  uint32_t v[256][64];
+  bool vinit[256];
+  uint32_t s[kNS];
+  bool sinit[kNS];
+  int64_t sw[kNS];  // slot of the last VALU write
+  int vpend[256];
+  int spend[kNS];
+  std::deque<Pend> vm, lgkm;
+  uint64_t exec = ~0ull;
+  bool scc = false;
+  size_t pc = 0;
+  int64_t slot = 0;
+  bool done = false, barrier = false;
+  int id = 0;
+};
+
+struct Ctx {
+  const Module& M;
+  Memory& mem;
+  std::vector<uint8_t> lds;
+  Stats* st;
+  int block = 0;
+};
+
+[[noreturn]] void fail(const Wave& w, const Ctx& c, const Ins& in, const std::string& what) {
+  std::ostringstream o;
+  o << what << " [block " << c.block << " wave " << w.id << " pc " << w.pc << ": " << in.text << "]";
+  err(o.str());
+}
+
+// --- register access with the checks ---------------------------------------------------------
+inline void chk_v_read(const Wave& w, const Ctx& c, const Ins& in, int r) {
+  if (r < 0 || r > 255) fail(w, c, in, "VGPR out of range");
+  if (w.vpend[r]) fail(w, c, in, "read of v" + std::to_string(r) + " with a load in flight");
+  if (!w.vinit[r]) fail(w, c, in, "read of v" + std::to_string(r) + " before any write");
+}
+inline void chk_s_read(const Wave& w, const Ctx& c, const Ins& in, int r) {
+  if (r < 0 || r >= kNS) fail(w, c, in, "SGPR out of range");
+  if (w.spend[r]) fail(w, c, in, "read of s" + std::to_string(r) + " with a load in flight");
+  if (!w.sinit[r]) fail(w, c, in, "read of s" + std::to_string(r) + " before any write");
+}
+inline void chk_v_write(const Wave& w, const Ctx& c, const Ins& in, int r) {
+  if (r < 0 || r > 255) fail(w, c, in, "VGPR out of range");
+  if (w.vpend[r]) fail(w, c, in, "write of v" + std::to_string(r) + " with a load into it in flight");
+}
+inline void chk_s_write(const Wave& w, const Ctx& c, const Ins& in, int r) {
+  if (r < 0 || r >= kNS) fail(w, c, in, "SGPR out of range");
+  if (w.spend[r]) fail(w, c, in, "write of s" + std::to_string(r) + " with a load into it in flight");
+}
+
+uint32_t sread(Wave& w, const Ctx& c, const Ins& in, const Opd& o) {
+  switch (o.k) {
+    case O_S: chk_s_read(w, c, in, o.r); return w.s[o.r];
+    case O_IMM: return (uint32_t)o.imm;
+    case O_EXEC: return (uint32_t)w.exec;
+    default: fail(w, c, in, "bad scalar operand");
+  }
+}
+uint64_t sread64(Wave& w, const Ctx& c, const Ins& in, const Opd& o) {
+  switch (o.k) {
+    case O_S:
+      if (o.n != 2) fail(w, c, in, "64-bit scalar operand is not a pair");
+      chk_s_read(w, c, in, o.r);
+      chk_s_read(w, c, in, o.r + 1);
+      return (uint64_t)w.s[o.r] | ((uint64_t)w.s[o.r + 1] << 32);
+    case O_IMM:
+      if (!o.inl) fail(w, c, in, "32-bit literal in a 64-bit scalar operand");
+      return (uint64_t)(int64_t)(int32_t)(uint32_t)o.imm;
+    case O_EXEC: return w.exec;
+    default: fail(w, c, in, "bad scalar operand");
+  }
+}
+void swrite(Wave& w, const Ctx& c, const Ins& in, const Opd& o, uint32_t v) {
+  if (o.k == O_EXEC) {
+    w.exec = (w.exec & ~0xFFFFFFFFull) | v;
+    return;
+  }
+  if (o.k != O_S) fail(w, c, in, "bad scalar destination");
+  chk_s_write(w, c, in, o.r);
+  w.s[o.r] = v;
+  w.sinit[o.r] = true;
+  w.sw[o.r] = -1000;  // an SALU write: no VALU hazard on the new value
+}
+void swrite64(Wave& w, const Ctx& c, const Ins& in, const Opd& o, uint64_t v) {
+  if (o.k == O_EXEC) {
+    w.exec = v;
+    return;
+  }
+  if (o.k != O_S || o.n != 2) fail(w, c, in, "bad 64-bit scalar destination");
+  chk_s_write(w, c, in, o.r);
+  chk_s_write(w, c, in, o.r + 1);
+  w.s[o.r] = (uint32_t)v;
+  w.s[o.r + 1] = (uint32_t)(v >> 32);
+  w.sinit[o.r] = w.sinit[o.r + 1] = true;
+  w.sw[o.r] = w.sw[o.r + 1] = -1000;
+}
+
+// a VALU source: per-lane reader after the checks (done once per instruction)
+struct Src {
+  const uint32_t* vec = nullptr;
+  const uint32_t* vec_hi = nullptr;
+  uint64_t k = 0;
+  bool scalar = true;
+  uint32_t lo(int l) const { return scalar ? (uint32_t)k : vec[l]; }
+  uint64_t v64(int l) const { return scalar ? k : ((uint64_t)vec[l] | (vec_hi ? (uint64_t)vec_hi[l] << 32 : 0ull)); }
+};
+
+struct ValuCheck {
+  int sgpr[4];
+  int ns = 0;
+  int literals = 0;
+  void sg(int r) {
+    for (int i = 0; i < ns; i++)
+      if (sgpr[i] == r) return;
+    if (ns < 4) sgpr[ns++] = r;
+  }
+};
+
+Src vsrc(Wave& w, const Ctx& c, const Ins& in, const Opd& o, bool wide, ValuCheck& vc, bool vop3) {
+  Src s;
+  switch (o.k) {
+    case O_V:
+      chk_v_read(w, c, in, o.r);
+      s.scalar = false;
+      s.vec = w.v[o.r];
+      if (wide) {
+        if (o.n != 2) fail(w, c, in, "64-bit VALU operand is not a pair");
+        chk_v_read(w, c, in, o.r + 1);
+        s.vec_hi = w.v[o.r + 1];
+      }
+      return s;
+    case O_S:
+      chk_s_read(w, c, in, o.r);
+      vc.sg(o.r);
+      if (w.slot - w.sw[o.r] < 3) fail(w, c, in, "VALU reads s" + std::to_string(o.r) + " within 2 wait states of a VALU write");
+      s.k = w.s[o.r];
+      if (wide) {
+        if (o.n != 2) fail(w, c, in, "64-bit VALU operand is not a pair");
+        chk_s_read(w, c, in, o.r + 1);
+        if (w.slot - w.sw[o.r + 1] < 3) fail(w, c, in, "VALU reads an SGPR within 2 wait states of a VALU write");
+        s.k |= (uint64_t)w.s[o.r + 1] << 32;
+      }
+      return s;
+    case O_IMM:
+      if (!o.inl) {
+        if (vop3) fail(w, c, in, "32-bit literal in a VOP3 encoding");
+        vc.literals++;
+      }
+      s.k = wide && o.inl ? (uint64_t)(int64_t)(int32_t)(uint32_t)o.imm : (uint32_t)o.imm;
+      return s;
+    case O_EXEC:
+      s.k = wide ? w.exec : (uint32_t)w.exec;
+      return s;
+    default:
+      fail(w, c, in, "bad VALU operand");
+  }
+}
+
+// implicit VCC read by a VALU (carry-in, e32 select)
+uint64_t vcc_read(Wave& w, const Ctx& c, const Ins& in, ValuCheck& vc) {
+  chk_s_read(w, c, in, 106);
+  chk_s_read(w, c, in, 107);
+  if (w.slot - w.sw[106] < 3 || w.slot - w.sw[107] < 3) fail(w, c, in, "VALU reads VCC within 2 wait states of a VALU write");
+  vc.sg(106);
+  return (uint64_t)w.s[106] | ((uint64_t)w.s[107] << 32);
+}
+uint64_t mask_read(Wave& w, const Ctx& c, const Ins& in, const Opd& o, ValuCheck& vc) {
+  if (o.k != O_S || o.n != 2) fail(w, c, in, "lane mask operand is not an SGPR pair");
+  chk_s_read(w, c, in, o.r);
+  chk_s_read(w, c, in, o.r + 1);
+  if (w.slot - w.sw[o.r] < 3 || w.slot - w.sw[o.r + 1] < 3)
+    fail(w, c, in, "VALU reads s[" + std::to_string(o.r) + "] within 2 wait states of a VALU write");
+  vc.sg(o.r);
+  return (uint64_t)w.s[o.r] | ((uint64_t)w.s[o.r + 1] << 32);
+}
+void mask_write(Wave& w, const Ctx& c, const Ins& in, const Opd& o, uint64_t m) {
+  if (o.k != O_S || o.n != 2) fail(w, c, in, "lane mask destination is not an SGPR pair");
+  chk_s_write(w, c, in, o.r);
+  chk_s_write(w, c, in, o.r + 1);
+  w.s[o.r] = (uint32_t)m;
+  w.s[o.r + 1] = (uint32_t)(m >> 32);
+  w.sinit[o.r] = w.sinit[o.r + 1] = true;
+  w.sw[o.r] = w.sw[o.r + 1] = w.slot;
+}
+uint32_t* vdst(Wave& w, const Ctx& c, const Ins& in, const Opd& o, int k = 0) {
+  if (o.k != O_V) fail(w, c, in, "VALU destination is not a VGPR");
+  chk_v_write(w, c, in, o.r + k);
+  w.vinit[o.r + k] = true;
+  return w.v[o.r + k];
+}
+
+void vmem_sgpr(Wave& w, const Ctx& c, const Ins& in, const Opd& o) {
+  if (o.k != O_S) return;
+  for (int q = 0; q < o.n; q++) {
+    chk_s_read(w, c, in, o.r + q);
+    if (w.slot - w.sw[o.r + q] < 6) fail(w, c, in, "VMEM reads an SGPR within 5 wait states of a VALU write");
+  }
+}
+
+void retire(Wave& w, std::deque<Pend>& q, int keep) {
+  while ((int)q.size() > keep) {
+    for (int r : q.front().v) w.vpend[r]--;
+    for (int r : q.front().s) w.spend[r]--;
+    q.pop_front();
+  }
+}
+
+uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c, uint32_t t) {
+  uint32_t r = 0;
+  for (int i = 0; i < 32; i++) {
+    const uint32_t idx = ((a >> i & 1) << 2) | ((b >> i & 1) << 1) | (c >> i & 1);
+    r |= ((t >> idx) & 1u) << i;
+  }
+  return r;
+}
+
+// one instruction of wave w; returns false when the wave stops (end or barrier)
+bool step(Wave& w, Ctx& c) {
+  const Ins& in = c.M.code.at(w.pc);
+  const auto& a = in.a;
+  const int enc = in.enc;
+  w.slot++;
+  if (c.st) c.st->insts++;
+  auto need = [&](size_t n) {
+    if (a.size() != n) fail(w, c, in, "expected " + std::to_string(n) + " operands");
+  };
+  size_t next = w.pc + 1;
+  const int op = in.op;
+  // ---- scalar ------------------------------------------------------------------------------
+  if (op <= OP_s_bfe_u32) {
+    if (c.st) c.st->salu++;
+    uint64_t r = 0;
+    switch (op) {
+      case OP_s_mov_b32: need(2); swrite(w, c, in, a[0], sread(w, c, in, a[1])); break;
+      case OP_s_mov_b64: need(2); swrite64(w, c, in, a[0], sread64(w, c, in, a[1])); break;
+      case OP_s_add_u32: {
+        need(3);
+        const uint64_t t = (uint64_t)sread(w, c, in, a[1]) + sread(w, c, in, a[2]);
+        w.scc = t >> 32;
+        swrite(w, c, in, a[0], (uint32_t)t);
+        break;
+      }
+      case OP_s_addc_u32: {
+        need(3);
+        const uint64_t t = (uint64_t)sread(w, c, in, a[1]) + sread(w, c, in, a[2]) + (w.scc ? 1 : 0);
+        w.scc = t >> 32;
+        swrite(w, c, in, a[0], (uint32_t)t);
+        break;
+      }
+      case OP_s_sub_u32: {
+        need(3);
+        const uint32_t x = sread(w, c, in, a[1]), y = sread(w, c, in, a[2]);
+        w.scc = y > x;
+        swrite(w, c, in, a[0], x - y);
+        break;
+      }
+      case OP_s_subb_u32: {
+        need(3);
+        const uint32_t x = sread(w, c, in, a[1]), y = sread(w, c, in, a[2]);
+        const uint64_t b = (uint64_t)y + (w.scc ? 1 : 0);
+        w.scc = b > x;
+        swrite(w, c, in, a[0], (uint32_t)(x - b));
+        break;
+      }
+      case OP_s_add_i32: case OP_s_sub_i32: {
+        need(3);
+        const int32_t x = (int32_t)sread(w, c, in, a[1]), y = (int32_t)sread(w, c, in, a[2]);
+        const int64_t t = op == OP_s_add_i32 ? (int64_t)x + y : (int64_t)x - y;
+        w.scc = t != (int64_t)(int32_t)t;
+        swrite(w, c, in, a[0], (uint32_t)t);
+        break;
+      }
+      case OP_s_mul_i32: need(3); swrite(w, c, in, a[0], sread(w, c, in, a[1]) * sread(w, c, in, a[2])); break;
+      case OP_s_mul_hi_u32:
+        need(3);
+        swrite(w, c, in, a[0], (uint32_t)(((uint64_t)sread(w, c, in, a[1]) * sread(w, c, in, a[2])) >> 32));
+        break;
+      case OP_s_lshl_b32: need(3); r = (uint32_t)(sread(w, c, in, a[1]) << (sread(w, c, in, a[2]) & 31)); w.scc = r != 0; swrite(w, c, in, a[0], (uint32_t)r); break;
+      case OP_s_lshr_b32: need(3); r = sread(w, c, in, a[1]) >> (sread(w, c, in, a[2]) & 31); w.scc = r != 0; swrite(w, c, in, a[0], (uint32_t)r); break;
+      case OP_s_ashr_i32: need(3); r = (uint32_t)((int32_t)sread(w, c, in, a[1]) >> (sread(w, c, in, a[2]) & 31)); w.scc = r != 0; swrite(w, c, in, a[0], (uint32_t)r); break;
+      case OP_s_lshl_b64: need(3); r = sread64(w, c, in, a[1]) << (sread(w, c, in, a[2]) & 63); w.scc = r != 0; swrite64(w, c, in, a[0], r); break;
+      case OP_s_lshr_b64: need(3); r = sread64(w, c, in, a[1]) >> (sread(w, c, in, a[2]) & 63); w.scc = r != 0; swrite64(w, c, in, a[0], r); break;
+      case OP_s_and_b32: case OP_s_or_b32: case OP_s_xor_b32: case OP_s_andn2_b32: {
+        need(3);
+        const uint32_t x = sread(w, c, in, a[1]), y = sread(w, c, in, a[2]);
+        r = op == OP_s_and_b32 ? (x & y) : op == OP_s_or_b32 ? (x | y) : op == OP_s_xor_b32 ? (x ^ y) : (x & ~y);
+        w.scc = (uint32_t)r != 0;
+        swrite(w, c, in, a[0], (uint32_t)r);
+        break;
+      }
+      case OP_s_and_b64: case OP_s_or_b64: case OP_s_xor_b64: case OP_s_andn2_b64: case OP_s_orn2_b64:
+      case OP_s_nor_b64: case OP_s_xnor_b64: {
+        need(3);
+        const uint64_t x = sread64(w, c, in, a[1]), y = sread64(w, c, in, a[2]);
+        switch (op) {
+          case OP_s_and_b64: r = x & y; break;
+          case OP_s_or_b64: r = x | y; break;
+          case OP_s_xor_b64: r = x ^ y; break;
+          case OP_s_andn2_b64: r = x & ~y; break;
+          case OP_s_orn2_b64: r = x | ~y; break;
+          case OP_s_nor_b64: r = ~(x | y); break;
+          default: r = ~(x ^ y); break;
+        }
+        w.scc = r != 0;
+        swrite64(w, c, in, a[0], r);
+        break;
+      }
+      case OP_s_not_b32: need(2); r = ~sread(w, c, in, a[1]) & 0xFFFFFFFFu; w.scc = r != 0; swrite(w, c, in, a[0], (uint32_t)r); break;
+      case OP_s_not_b64: need(2); r = ~sread64(w, c, in, a[1]); w.scc = r != 0; swrite64(w, c, in, a[0], r); break;
+      case OP_s_min_u32: case OP_s_max_u32: {
+        need(3);
+        const uint32_t x = sread(w, c, in, a[1]), y = sread(w, c, in, a[2]);
+        const bool first = op == OP_s_min_u32 ? x < y : x > y;
+        w.scc = first;
+        swrite(w, c, in, a[0], first ? x : y);
+        break;
+      }
+      case OP_s_cselect_b32: need(3); { const uint32_t x = sread(w, c, in, a[1]), y = sread(w, c, in, a[2]); swrite(w, c, in, a[0], w.scc ? x : y); } break;
+      case OP_s_cselect_b64: need(3); { const uint64_t x = sread64(w, c, in, a[1]), y = sread64(w, c, in, a[2]); swrite64(w, c, in, a[0], w.scc ? x : y); } break;
+      case OP_s_cmp_eq_u32: need(2); w.scc = sread(w, c, in, a[0]) == sread(w, c, in, a[1]); break;
+      case OP_s_cmp_lg_u32: need(2); w.scc = sread(w, c, in, a[0]) != sread(w, c, in, a[1]); break;
+      case OP_s_cmp_lt_u32: need(2); w.scc = sread(w, c, in, a[0]) < sread(w, c, in, a[1]); break;
+      case OP_s_cmp_le_u32: need(2); w.scc = sread(w, c, in, a[0]) <= sread(w, c, in, a[1]); break;
+      case OP_s_cmp_gt_u32: need(2); w.scc = sread(w, c, in, a[0]) > sread(w, c, in, a[1]); break;
+      case OP_s_cmp_ge_u32: need(2); w.scc = sread(w, c, in, a[0]) >= sread(w, c, in, a[1]); break;
+      case OP_s_cmp_eq_u64: need(2); w.scc = sread64(w, c, in, a[0]) == sread64(w, c, in, a[1]); break;
+      case OP_s_cmp_lg_u64: need(2); w.scc = sread64(w, c, in, a[0]) != sread64(w, c, in, a[1]); break;
+      case OP_s_ff1_i32_b64: { need(2); const uint64_t x = sread64(w, c, in, a[1]); swrite(w, c, in, a[0], x ? (uint32_t)__builtin_ctzll(x) : 0xFFFFFFFFu); break; }
+      case OP_s_ff1_i32_b32: { need(2); const uint32_t x = sread(w, c, in, a[1]); swrite(w, c, in, a[0], x ? (uint32_t)__builtin_ctz(x) : 0xFFFFFFFFu); break; }
+      case OP_s_flbit_i32_b32: { need(2); const uint32_t x = sread(w, c, in, a[1]); swrite(w, c, in, a[0], x ? (uint32_t)__builtin_clz(x) : 0xFFFFFFFFu); break; }
+      case OP_s_bcnt1_i32_b64: { need(2); r = (uint32_t)__builtin_popcountll(sread64(w, c, in, a[1])); w.scc = r != 0; swrite(w, c, in, a[0], (uint32_t)r); break; }
+      case OP_s_bfe_u32: {
+        need(3);
+        const uint32_t x = sread(w, c, in, a[1]), f = sread(w, c, in, a[2]);
+        const uint32_t off = f & 31, wd = (f >> 16) & 127;
+        r = wd == 0 ? 0 : (wd >= 32 ? (x >> off) : ((x >> off) & ((1u << wd) - 1u)));
+        w.scc = r != 0;
+        swrite(w, c, in, a[0], (uint32_t)r);
+        break;
+      }
+    }
+    w.pc = next;
+    return true;
+  }
+  // ---- control ---------------------------------------------------------------------------
+  switch (op) {
+    case OP_s_cbranch_scc0: if (!w.scc) next = in.target; w.pc = next; return true;
+    case OP_s_cbranch_scc1: if (w.scc) next = in.target; w.pc = next; return true;
+    case OP_s_cbranch_vccz: case OP_s_cbranch_vccnz: {
+      chk_s_read(w, c, in, 106);
+      chk_s_read(w, c, in, 107);
+      const bool z = ((uint64_t)w.s[106] | ((uint64_t)w.s[107] << 32)) == 0;
+      if (z == (op == OP_s_cbranch_vccz)) next = in.target;
+      w.pc = next;
+      return true;
+    }
+    case OP_s_cbranch_execz: if (!w.exec) next = in.target; w.pc = next; return true;
+    case OP_s_branch: w.pc = in.target; return true;
+    case OP_s_nop: {
+      need(1);
+      if (a[0].k != O_IMM || a[0].imm > 15) fail(w, c, in, "bad s_nop");
+      w.slot += (int64_t)a[0].imm;  // N + 1 wait states in all
+      w.pc = next;
+      return true;
+    }
+    case OP_s_waitcnt:
+      if (in.vmcnt >= 0) retire(w, w.vm, in.vmcnt);
+      if (in.lgkmcnt >= 0) retire(w, w.lgkm, in.lgkmcnt);
+      w.pc = next;
+      return true;
+    case OP_s_barrier:
+      w.pc = next;
+      w.barrier = true;
+      return false;
+    case OP_s_endpgm:
+      w.done = true;
+      return false;
+    case OP_s_load_dword: case OP_s_load_dwordx2: case OP_s_load_dwordx4: case OP_s_load_dwordx8: {
+      need(3);
+      const int n = op == OP_s_load_dword ? 1 : op == OP_s_load_dwordx2 ? 2 : op == OP_s_load_dwordx4 ? 4 : 8;
+      if (a[0].k != O_S || a[0].n != n || a[1].k != O_S || a[1].n != 2 || a[2].k != O_IMM)
+        fail(w, c, in, "bad s_load operands");
+      const uint64_t base = sread64(w, c, in, a[1]) + a[2].imm;
+      const uint8_t* p = c.mem.at(base, 4u * n);
+      Pend pd;
+      for (int q = 0; q < n; q++) {
+        const int r = a[0].r + q;
+        if (r >= kNS) fail(w, c, in, "SGPR out of range");
+        memcpy(&w.s[r], p + 4 * q, 4);
+        w.sinit[r] = true;
+        w.spend[r]++;
+        pd.s.push_back(r);
+      }
+      w.lgkm.push_back(pd);
+      w.pc = next;
+      return true;
+    }
+    default: break;
+  }
+  // ---- memory ---------------------------------------------------------------------------
+  if (op >= OP_global_load_dword) {
+    if (c.st) (op >= OP_ds_read_b32 ? c.st->lds : c.st->vmem)++;
+    if (op >= OP_ds_read_b32) {
+      auto lds_at = [&](uint32_t addr, uint32_t n) -> uint8_t* {
+        if ((addr & (n >= 4 ? 3u : n - 1u)) != 0) fail(w, c, in, "misaligned LDS access");
+        if ((uint64_t)addr + n > c.lds.size()) fail(w, c, in, "LDS access past the kernel's allocation");
+        return c.lds.data() + addr;
+      };
+      if (op == OP_ds_read_b32 || op == OP_ds_read_b64) {
+        need(2);
+        const int nw = op == OP_ds_read_b32 ? 1 : 2;
+        ValuCheck vc;
+        const Src ad = vsrc(w, c, in, a[1], false, vc, true);
+        Pend pd;
+        for (int q = 0; q < nw; q++) {
+          uint32_t* d = vdst(w, c, in, a[0], q);
+          for (int l = 0; l < 64; l++)
+            if (w.exec >> l & 1) memcpy(&d[l], lds_at(ad.lo(l) + (uint32_t)in.offset + 4 * q, 4), 4);
+          pd.v.push_back(a[0].r + q);
+          w.vpend[a[0].r + q]++;
+        }
+        w.lgkm.push_back(pd);
+      } else if (op == OP_ds_write_b32 || op == OP_ds_write_b64) {
+        need(2);
+        const int nw = op == OP_ds_write_b32 ? 1 : 2;
+        ValuCheck vc;
+        const Src ad = vsrc(w, c, in, a[0], false, vc, true);
+        const Src dv = vsrc(w, c, in, a[1], nw == 2, vc, true);
+        for (int l = 0; l < 64; l++) {
+          if (!(w.exec >> l & 1)) continue;
+          const uint64_t x = dv.v64(l);
+          for (int q = 0; q < nw; q++) {
+            const uint32_t y = (uint32_t)(x >> (32 * q));
+            memcpy(lds_at(ad.lo(l) + (uint32_t)in.offset + 4 * q, 4), &y, 4);
+          }
+        }
+        w.lgkm.push_back(Pend{});
+      } else {
+        fail(w, c, in, "unsupported LDS instruction");
+      }
+      w.pc = next;
+      return true;
+    }
+    // global: vaddr + saddr (32-bit lane offsets) or a 64-bit vaddr with "off"
+    const bool store = op == OP_global_store_byte || op == OP_global_store_dword;
+    const bool atomic = op == OP_global_atomic_umin_x2 || op == OP_global_atomic_add_x2;
+    const bool load = !store && !atomic;
+    need(3);
+    const Opd& vaddr = load ? a[1] : a[0];
+    const Opd& sa = a[2];
+    ValuCheck vc;
+    if (vaddr.k != O_V) fail(w, c, in, "global address is not a VGPR");
+    const bool off = sa.k == O_OFF;
+    const Src av = vsrc(w, c, in, vaddr, off, vc, true);
+    if (off && vaddr.n != 2) fail(w, c, in, "64-bit address is not a VGPR pair");
+    uint64_t sb = 0;
+    if (!off) {
+      if (sa.k != O_S || sa.n != 2) fail(w, c, in, "global base is not an SGPR pair");
+      vmem_sgpr(w, c, in, sa);
+      sb = (uint64_t)w.s[sa.r] | ((uint64_t)w.s[sa.r + 1] << 32);
+    }
+    if (in.offset < -4096 || in.offset > 4095) fail(w, c, in, "global offset outside 13 signed bits");
+    auto addr = [&](int l) -> uint64_t { return (off ? av.v64(l) : sb + av.lo(l)) + (uint64_t)in.offset; };
+    if (load) {
+      const int nw = op == OP_global_load_dword ? 1 : op == OP_global_load_dwordx2 ? 2 : 4;
+      if (a[0].k != O_V || a[0].n != nw) fail(w, c, in, "load destination width");
+      Pend pd;
+      std::vector<uint32_t*> ds;
+      for (int q = 0; q < nw; q++) ds.push_back(vdst(w, c, in, a[0], q));
+      for (int l = 0; l < 64; l++) {
+        if (!(w.exec >> l & 1)) continue;
+        const uint8_t* p = c.mem.at(addr(l), 4u * nw);
+        for (int q = 0; q < nw; q++) memcpy(&ds[q][l], p + 4 * q, 4);
+      }
+      for (int q = 0; q < nw; q++) {
+        pd.v.push_back(a[0].r + q);
+        w.vpend[a[0].r + q]++;
+      }
+      w.vm.push_back(pd);
+    } else if (store) {
+      const Src dv = vsrc(w, c, in, a[1], false, vc, true);
+      for (int l = 0; l < 64; l++) {
+        if (!(w.exec >> l & 1)) continue;
+        const uint32_t x = dv.lo(l);
+        if (op == OP_global_store_byte) *c.mem.at(addr(l), 1) = (uint8_t)x;
+        else memcpy(c.mem.at(addr(l), 4), &x, 4);
+      }
+      w.vm.push_back(Pend{});
+    } else {
+      const Src dv = vsrc(w, c, in, a[1], true, vc, true);
+      for (int l = 0; l < 64; l++) {
+        if (!(w.exec >> l & 1)) continue;
+        const uint64_t ad = addr(l);
+        if (ad & 7) fail(w, c, in, "misaligned 64-bit atomic");
+        uint64_t cur;
+        uint8_t* p = c.mem.at(ad, 8);
+        memcpy(&cur, p, 8);
+        const uint64_t x = dv.v64(l);
+        cur = op == OP_global_atomic_umin_x2 ? std::min(cur, x) : cur + x;
+        memcpy(p, &cur, 8);
+      }
+      w.vm.push_back(Pend{});
+    }
+    w.pc = next;
+    return true;
+  }
+  // ---- vector ALU -------------------------------------------------------------------------
+  if (c.st) c.st->valu++;
+  const bool vop3 = enc != 1;  // VOP3 and SDWA take no 32-bit literal
+  ValuCheck vc;
+  const uint64_t ex = w.exec;
+  auto lanes = [&](auto f) {
+    for (int l = 0; l < 64; l++)
+      if (ex >> l & 1) f(l);
+  };
+  auto e32_src1 = [&](const Opd& o) {
+    if (enc == 1 && o.k != O_V) fail(w, c, in, "VOP2/VOPC src1 must be a VGPR");
+  };
+  switch (op) {
+    case OP_v_mov_b32: {
+      need(2);
+      const Src s = vsrc(w, c, in, a[1], false, vc, vop3);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      lanes([&](int l) { d[l] = s.lo(l); });
+      break;
+    }
+    case OP_v_readfirstlane_b32: {
+      need(2);
+      const Src s = vsrc(w, c, in, a[1], false, vc, true);
+      const int l = ex ? __builtin_ctzll(ex) : 0;
+      if (a[0].k != O_S) fail(w, c, in, "readfirstlane destination");
+      chk_s_write(w, c, in, a[0].r);
+      w.s[a[0].r] = s.lo(l);
+      w.sinit[a[0].r] = true;
+      w.sw[a[0].r] = w.slot;
+      break;
+    }
+    case OP_v_add_u32: case OP_v_sub_u32: case OP_v_subrev_u32: case OP_v_and_b32: case OP_v_or_b32:
+    case OP_v_xor_b32: case OP_v_lshlrev_b32: case OP_v_lshrrev_b32: case OP_v_ashrrev_i32: case OP_v_min_u32:
+    case OP_v_max_u32: case OP_v_mul_u32_u24: case OP_v_mul_lo_u32: case OP_v_mul_hi_u32: {
+      need(3);
+      e32_src1(a[2]);
+      const Src x = vsrc(w, c, in, a[1], false, vc, vop3), y = vsrc(w, c, in, a[2], false, vc, vop3);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      const bool sd = enc == 3;
+      lanes([&](int l) {
+        const uint32_t p = x.lo(l), q = sd && in.sdwa_src1_word1 ? (y.lo(l) >> 16) : y.lo(l);
+        uint32_t r = 0;
+        switch (op) {
+          case OP_v_add_u32: r = p + q; break;
+          case OP_v_sub_u32: r = p - q; break;
+          case OP_v_subrev_u32: r = q - p; break;
+          case OP_v_and_b32: r = p & q; break;
+          case OP_v_or_b32: r = p | q; break;
+          case OP_v_xor_b32: r = p ^ q; break;
+          case OP_v_lshlrev_b32: r = q << (p & 31); break;
+          case OP_v_lshrrev_b32: r = q >> (p & 31); break;
+          case OP_v_ashrrev_i32: r = (uint32_t)((int32_t)q >> (p & 31)); break;
+          case OP_v_min_u32: r = std::min(p, q); break;
+          case OP_v_max_u32: r = std::max(p, q); break;
+          case OP_v_mul_u32_u24: r = (p & 0xFFFFFFu) * (q & 0xFFFFFFu); break;
+          case OP_v_mul_lo_u32: r = p * q; break;
+          default: r = (uint32_t)(((uint64_t)p * q) >> 32); break;
+        }
+        d[l] = r;
+      });
+      break;
+    }
+    case OP_v_not_b32: case OP_v_ffbh_u32: case OP_v_ffbl_b32: case OP_v_cvt_f32_u32: case OP_v_rcp_iflag_f32:
+    case OP_v_cvt_u32_f32: {
+      need(2);
+      const Src x = vsrc(w, c, in, a[1], false, vc, vop3);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      lanes([&](int l) {
+        const uint32_t p = x.lo(l);
+        uint32_t r;
+        float f;
+        switch (op) {
+          case OP_v_not_b32: r = ~p; break;
+          case OP_v_ffbh_u32: r = p ? (uint32_t)__builtin_clz(p) : 0xFFFFFFFFu; break;
+          case OP_v_ffbl_b32: r = p ? (uint32_t)__builtin_ctz(p) : 0xFFFFFFFFu; break;
+          case OP_v_cvt_f32_u32: f = (float)p; memcpy(&r, &f, 4); break;
+          case OP_v_rcp_iflag_f32: memcpy(&f, &p, 4); f = 1.0f / f; memcpy(&r, &f, 4); break;
+          default: memcpy(&f, &p, 4); r = f <= 0 ? 0u : (f >= 4294967296.0f ? 0xFFFFFFFFu : (uint32_t)f); break;
+        }
+        d[l] = r;
+      });
+      break;
+    }
+    case OP_v_add_co_u32: case OP_v_sub_co_u32: case OP_v_subrev_co_u32: {
+      need(4);
+      e32_src1(a[3]);
+      if (enc == 1 && !(a[1].k == O_S && a[1].r == 106 && a[1].n == 2)) fail(w, c, in, "e32 carry-out must be vcc");
+      const Src x = vsrc(w, c, in, a[2], false, vc, vop3), y = vsrc(w, c, in, a[3], false, vc, vop3);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      uint64_t m = 0;
+      lanes([&](int l) {
+        const uint32_t p = x.lo(l), q = y.lo(l);
+        if (op == OP_v_add_co_u32) {
+          const uint64_t t = (uint64_t)p + q;
+          d[l] = (uint32_t)t;
+          m |= (t >> 32) << l;
+        } else {
+          const uint32_t u = op == OP_v_sub_co_u32 ? p : q, v = op == OP_v_sub_co_u32 ? q : p;
+          d[l] = u - v;
+          m |= (uint64_t)(v > u) << l;
+        }
+      });
+      mask_write(w, c, in, a[1], m);
+      break;
+    }
+    case OP_v_addc_co_u32: case OP_v_subb_co_u32: case OP_v_subbrev_co_u32: {
+      need(5);
+      e32_src1(a[3]);
+      if (enc == 1 && !(a[1].k == O_S && a[1].r == 106 && a[4].k == O_S && a[4].r == 106))
+        fail(w, c, in, "e32 carry operands must be vcc");
+      const Src x = vsrc(w, c, in, a[2], false, vc, vop3), y = vsrc(w, c, in, a[3], false, vc, vop3);
+      const uint64_t cin = enc == 1 ? vcc_read(w, c, in, vc) : mask_read(w, c, in, a[4], vc);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      uint64_t m = 0;
+      lanes([&](int l) {
+        const uint32_t p = x.lo(l), q = y.lo(l), ci = (uint32_t)(cin >> l & 1);
+        if (op == OP_v_addc_co_u32) {
+          const uint64_t t = (uint64_t)p + q + ci;
+          d[l] = (uint32_t)t;
+          m |= (t >> 32) << l;
+        } else {
+          const uint32_t u = op == OP_v_subb_co_u32 ? p : q, v = op == OP_v_subb_co_u32 ? q : p;
+          const uint64_t b = (uint64_t)v + ci;
+          d[l] = (uint32_t)(u - b);
+          m |= (uint64_t)(b > u) << l;
+        }
+      });
+      mask_write(w, c, in, a[1], m);
+      break;
+    }
+    case OP_v_cndmask_b32: {
+      need(4);
+      e32_src1(a[2]);
+      const Src x = vsrc(w, c, in, a[1], false, vc, vop3), y = vsrc(w, c, in, a[2], false, vc, vop3);
+      uint64_t m;
+      if (enc == 1) {
+        if (!(a[3].k == O_S && a[3].r == 106)) fail(w, c, in, "e32 select must be vcc");
+        m = vcc_read(w, c, in, vc);
+      } else {
+        m = mask_read(w, c, in, a[3], vc);
+      }
+      uint32_t* d = vdst(w, c, in, a[0]);
+      lanes([&](int l) { d[l] = (m >> l & 1) ? y.lo(l) : x.lo(l); });
+      break;
+    }
+    case OP_v_cmp_eq_u32: case OP_v_cmp_ne_u32: case OP_v_cmp_lt_u32: case OP_v_cmp_le_u32: case OP_v_cmp_gt_u32:
+    case OP_v_cmp_ge_u32: case OP_v_cmp_eq_i32: case OP_v_cmp_ne_i32: case OP_v_cmp_lt_i32: case OP_v_cmp_le_i32:
+    case OP_v_cmp_gt_i32: case OP_v_cmp_ge_i32: case OP_v_cmp_eq_u64: case OP_v_cmp_ne_u64: case OP_v_cmp_lt_u64:
+    case OP_v_cmp_le_u64: case OP_v_cmp_gt_u64: case OP_v_cmp_ge_u64: {
+      need(3);
+      e32_src1(a[2]);
+      if (enc == 1 && !(a[0].k == O_S && a[0].r == 106 && a[0].n == 2)) fail(w, c, in, "e32 compare must write vcc");
+      const bool wide = op >= OP_v_cmp_eq_u64;
+      const Src x = vsrc(w, c, in, a[1], wide, vc, vop3), y = vsrc(w, c, in, a[2], wide, vc, vop3);
+      uint64_t m = 0;
+      lanes([&](int l) {
+        bool r;
+        if (wide) {
+          const uint64_t p = x.v64(l), q = y.v64(l);
+          switch (op) {
+            case OP_v_cmp_eq_u64: r = p == q; break;
+            case OP_v_cmp_ne_u64: r = p != q; break;
+            case OP_v_cmp_lt_u64: r = p < q; break;
+            case OP_v_cmp_le_u64: r = p <= q; break;
+            case OP_v_cmp_gt_u64: r = p > q; break;
+            default: r = p >= q; break;
+          }
+        } else if (op >= OP_v_cmp_eq_i32) {
+          const int32_t p = (int32_t)x.lo(l), q = (int32_t)y.lo(l);
+          switch (op) {
+            case OP_v_cmp_eq_i32: r = p == q; break;
+            case OP_v_cmp_ne_i32: r = p != q; break;
+            case OP_v_cmp_lt_i32: r = p < q; break;
+            case OP_v_cmp_le_i32: r = p <= q; break;
+            case OP_v_cmp_gt_i32: r = p > q; break;
+            default: r = p >= q; break;
+          }
+        } else {
+          const uint32_t p = x.lo(l), q = y.lo(l);
+          switch (op) {
+            case OP_v_cmp_eq_u32: r = p == q; break;
+            case OP_v_cmp_ne_u32: r = p != q; break;
+            case OP_v_cmp_lt_u32: r = p < q; break;
+            case OP_v_cmp_le_u32: r = p <= q; break;
+            case OP_v_cmp_gt_u32: r = p > q; break;
+            default: r = p >= q; break;
+          }
+        }
+        m |= (uint64_t)r << l;
+      });
+      mask_write(w, c, in, a[0], m);
+      break;
+    }
+    case OP_v_bfe_u32: case OP_v_bfe_i32: case OP_v_alignbit_b32: case OP_v_lshl_or_b32: case OP_v_add3_u32:
+    case OP_v_or3_b32: case OP_v_xad_u32: case OP_v_and_or_b32: case OP_v_lshl_add_u32: case OP_v_add_lshl_u32:
+    case OP_v_perm_b32: case OP_v_mad_u32_u24: case OP_v_bfi_b32: {
+      need(4);
+      const Src x = vsrc(w, c, in, a[1], false, vc, true), y = vsrc(w, c, in, a[2], false, vc, true),
+                z = vsrc(w, c, in, a[3], false, vc, true);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      lanes([&](int l) {
+        const uint32_t p = x.lo(l), q = y.lo(l), s = z.lo(l);
+        uint32_t r = 0;
+        switch (op) {
+          case OP_v_bfe_u32: {
+            const uint32_t o = q & 31, n = s & 31;
+            r = n == 0 ? 0 : (p >> o) & ((1u << n) - 1u);
+            break;
+          }
+          case OP_v_bfe_i32: {
+            const uint32_t o = q & 31, n = s & 31;
+            if (n == 0) {
+              r = 0;
+            } else {
+              const uint32_t f = (p >> o) & ((1u << n) - 1u);
+              r = (uint32_t)((int32_t)(f << (32 - n)) >> (32 - n));
+            }
+            break;
+          }
+          case OP_v_alignbit_b32: r = (uint32_t)((((uint64_t)p << 32) | q) >> (s & 31)); break;
+          case OP_v_lshl_or_b32: r = (p << (q & 31)) | s; break;
+          case OP_v_add3_u32: r = p + q + s; break;
+          case OP_v_or3_b32: r = p | q | s; break;
+          case OP_v_xad_u32: r = (p ^ q) + s; break;
+          case OP_v_and_or_b32: r = (p & q) | s; break;
+          case OP_v_lshl_add_u32: r = (p << (q & 31)) + s; break;
+          case OP_v_add_lshl_u32: r = (p + q) << (s & 31); break;
+          case OP_v_mad_u32_u24: r = (p & 0xFFFFFFu) * (q & 0xFFFFFFu) + s; break;
+          case OP_v_bfi_b32: r = (p & q) | (~p & s); break;
+          default: {  // v_perm_b32: byte selects from {p, q}
+            const uint64_t cat = ((uint64_t)p << 32) | q;
+            for (int b = 0; b < 4; b++) {
+              const uint32_t sel = (s >> (8 * b)) & 0xFF;
+              uint32_t byte;
+              if (sel < 8) byte = (uint32_t)(cat >> (8 * sel)) & 0xFF;
+              else if (sel == 12) byte = 0;
+              else if (sel > 12) byte = 0xFF;
+              else fail(w, c, in, "unsupported v_perm selector");
+              r |= byte << (8 * b);
+            }
+            break;
+          }
+        }
+        d[l] = r;
+      });
+      break;
+    }
+    case OP_v_bitop3_b32: {
+      // v_bitop3_b32 d, a, b, c bitop3:0xNN (the table as a fourth operand here)
+      need(5);
+      const Src x = vsrc(w, c, in, a[1], false, vc, true), y = vsrc(w, c, in, a[2], false, vc, true),
+                z = vsrc(w, c, in, a[3], false, vc, true);
+      if (a[4].k != O_IMM) fail(w, c, in, "bitop3 table");
+      const uint32_t t = (uint32_t)a[4].imm & 0xFF;
+      uint32_t* d = vdst(w, c, in, a[0]);
+      lanes([&](int l) { d[l] = bitop3(x.lo(l), y.lo(l), z.lo(l), t); });
+      break;
+    }
+    case OP_v_lshlrev_b64: case OP_v_lshrrev_b64: {
+      need(3);
+      const Src x = vsrc(w, c, in, a[1], false, vc, true), y = vsrc(w, c, in, a[2], true, vc, true);
+      if (a[0].k != O_V || a[0].n != 2) fail(w, c, in, "64-bit shift destination");
+      uint32_t* d0 = vdst(w, c, in, a[0], 0);
+      uint32_t* d1 = vdst(w, c, in, a[0], 1);
+      lanes([&](int l) {
+        const uint64_t v = y.v64(l);
+        const uint32_t s = x.lo(l) & 63;
+        const uint64_t r = op == OP_v_lshlrev_b64 ? v << s : v >> s;
+        d0[l] = (uint32_t)r;
+        d1[l] = (uint32_t)(r >> 32);
+      });
+      break;
+    }
+    case OP_v_mad_u64_u32: {
+      // v_mad_u64_u32 v[d:d+1], s[c:c+1], a, b, v[e:e+1]: d = a * b + e, carry-out to the pair
+      need(5);
+      const Src x = vsrc(w, c, in, a[2], false, vc, true), y = vsrc(w, c, in, a[3], false, vc, true),
+                z = vsrc(w, c, in, a[4], true, vc, true);
+      uint32_t* d0 = vdst(w, c, in, a[0], 0);
+      uint32_t* d1 = vdst(w, c, in, a[0], 1);
+      uint64_t m = 0;
+      lanes([&](int l) {
+        const unsigned __int128 t = (unsigned __int128)x.lo(l) * y.lo(l) + z.v64(l);
+        d0[l] = (uint32_t)t;
+        d1[l] = (uint32_t)(t >> 32);
+        m |= (uint64_t)(t >> 64 & 1) << l;
+      });
+      mask_write(w, c, in, a[1], m);
+      break;
+    }
+    case OP_v_mul_f32: {
+      need(3);
+      const Src x = vsrc(w, c, in, a[1], false, vc, vop3), y = vsrc(w, c, in, a[2], false, vc, vop3);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      lanes([&](int l) {
+        float p, q;
+        uint32_t pu = x.lo(l), qu = y.lo(l);
+        memcpy(&p, &pu, 4);
+        memcpy(&q, &qu, 4);
+        const float r = p * q;
+        memcpy(&d[l], &r, 4);
+      });
+      break;
+    }
+    default:
+      fail(w, c, in, "instruction not simulated");
+  }
+  if (vc.ns + vc.literals > 1) fail(w, c, in, "constant bus: more than one SGPR or literal read");
+  w.pc = next;
+  return true;
+}
+
+}  // namespace
+
+void launch(const Module& m, const std::string& kernel, Memory& mem, uint64_t kernarg, uint32_t nblk, Stats* stats,
+            uint64_t max_steps) {
+  auto kit = m.kernels.find(kernel);
+  if (kit == m.kernels.end()) err("no kernel " + kernel);
+  uint64_t steps = 0;
+  std::vector<Wave> waves(4);
+  for (uint32_t b = 0; b < nblk; b++) {
+    Ctx c{m, mem, std::vector<uint8_t>(kit->second.lds_bytes, 0), stats, (int)b};
+    for (int q = 0; q < 4; q++) {
+      Wave& w = waves[q];
+      memset(w.vinit, 0, sizeof w.vinit);
+      memset(w.sinit, 0, sizeof w.sinit);
+      memset(w.vpend, 0, sizeof w.vpend);
+      memset(w.spend, 0, sizeof w.spend);
+      for (int r = 0; r < kNS; r++) w.sw[r] = -1000;
+      w.vm.clear();
+      w.lgkm.clear();
+      w.exec = ~0ull;
+      w.scc = false;
+      w.pc = kit->second.entry;
+      w.slot = 0;
+      w.done = w.barrier = false;
+      w.id = q;
+      for (int l = 0; l < 64; l++) w.v[0][l] = (uint32_t)(64 * q + l);
+      w.vinit[0] = true;
+      w.s[0] = (uint32_t)kernarg;
+      w.s[1] = (uint32_t)(kernarg >> 32);
+      w.s[2] = b;
+      w.sinit[0] = w.sinit[1] = w.sinit[2] = true;
+      if (stats) stats->waves++;
+    }
+    for (;;) {
+      bool progress = false;
+      for (int q = 0; q < 4; q++) {
+        Wave& w = waves[q];
+        if (w.done || w.barrier) continue;
+        progress = true;
+        while (step(w, c)) {
+          if (++steps > max_steps) err("step budget exhausted (a wave that never exits?)");
+        }
+      }
+      bool all = true, any_wait = false;
+      for (auto& w : waves) {
+        all = all && w.done;
+        any_wait = any_wait || w.barrier;
+      }
+      if (all) break;
+      if (!progress || any_wait) {
+        bool every = true;
+        for (auto& w : waves) every = every && (w.done || w.barrier);
+        if (every)
+          for (auto& w : waves) w.barrier = false;
+        else if (!progress)
+          err("deadlock at a barrier");
+      }
+    }
+  }
+}
+
+}  // namespace asmsim

@@ -1,0 +1,83 @@
+// A CPU simulator of the gfx950 instruction subset the first JIT tier emits
+// (mythril_amd/csrc/jit_asm.cpp) — test infrastructure only, never linked into the product.
+//
+// It runs the emitted kernels (mgj_search, mgj_gen, mgj_eval) wave by wave on the host, 64 lanes
+// per wave, four waves per 256-lane block, with a flat 64-bit memory of the buffers the engine
+// would pass, so the first tier's output can be compared per candidate with the C port
+// (oracle/bveval.c) on any number of programs without a GPU.  Besides the arithmetic it checks
+// the rules the emitter claims to keep; any violation is an error, not a wrong verdict:
+//   * a VGPR or SGPR read (or overwritten) while a load into it is still in flight (vmcnt /
+//     lgkmcnt not waited for), loads returning in issue order per counter;
+//   * a VALU read of an SGPR (VCC included) fewer than 2 wait states after a VALU wrote it, and a
+//     VMEM read of an SGPR fewer than 5 after a VALU wrote it (s_nop N = N + 1 wait states);
+//   * the constant bus: one SGPR or literal per VALU instruction (implicit VCC included), no
+//     32-bit literal in a VOP3 encoding;
+//   * an access outside every buffer, or outside the kernel's LDS allocation;
+//   * a read of a VGPR no instruction wrote in this wave;
+//   * a kernel that runs more than a step budget (a wave that never exits).
+#pragma once
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace asmsim {
+
+struct SimError {
+  std::string what;
+};
+
+enum OKind : uint8_t { O_NONE, O_V, O_S, O_IMM, O_EXEC, O_OFF };
+struct Opd {
+  OKind k = O_NONE;
+  int r = 0;       // register number (vcc = s106)
+  int n = 1;       // registers (a pair: 2)
+  uint64_t imm = 0;
+  bool inl = false;  // an inline constant (-16..64)
+};
+
+struct Ins {
+  int op = 0;
+  std::vector<Opd> a;
+  int64_t offset = 0;   // offset:N
+  int vmcnt = -1, lgkmcnt = -1;  // s_waitcnt
+  int sdwa_src1_word1 = 0;
+  int enc = 0;          // 0 VOP3-only / none, 1 _e32, 2 _e64, 3 _sdwa
+  int target = -1;      // branch target (instruction index)
+  std::string text;     // the source line (diagnostics)
+};
+
+struct Kernel {
+  size_t entry = 0;
+  uint32_t lds_bytes = 0;
+};
+
+struct Module {
+  std::vector<Ins> code;
+  std::map<std::string, Kernel> kernels;
+};
+
+// parse the emitter's assembly text (throws SimError on anything unknown)
+Module parse(const std::string& text);
+
+struct Buffer {
+  uint64_t base = 0;
+  std::vector<uint8_t> data;
+};
+
+struct Memory {
+  std::vector<Buffer> bufs;
+  uint64_t add(size_t bytes, const void* init = nullptr);  // returns the base address
+  uint8_t* at(uint64_t addr, size_t n);
+  Buffer& of(uint64_t base);
+};
+
+struct Stats {
+  uint64_t insts = 0, valu = 0, salu = 0, vmem = 0, lds = 0, waves = 0;
+};
+
+// run `kernel` over `nblk` 256-lane blocks; kernarg: the argument block's address
+void launch(const Module& m, const std::string& kernel, Memory& mem, uint64_t kernarg, uint32_t nblk,
+            Stats* stats = nullptr, uint64_t max_steps = 400000000ull);
+
+}  // namespace asmsim

@@ -1,0 +1,343 @@
+"""The first JIT tier (``mythril_amd/csrc/jit_asm.cpp``) against the C port on the CPU, at depth.
+
+``tests/asmsim/`` is an instruction-level simulator of the gfx950 subset the tier emits: it runs
+``mgj_gen``, ``mgj_search`` and ``mgj_eval`` wave by wave and also checks the emitter's own
+claims — no register read while a load into it is in flight (vmcnt / lgkmcnt), the VALU->SGPR->VALU
+and VALU->SGPR->VMEM wait states, the constant-bus and literal rules, every access inside a
+buffer or the kernel's LDS, no read of a never-written VGPR.  The driver (``asmsim_main.cpp``)
+emits the kernels exactly as ``mg_jit_compile_ex`` does and compares, per record:
+
+* ``mgj_gen`` verdicts per candidate with the C port's (``oracle/bveval.c``, the unspecialised
+  program) on a random 63-bit window; ``mgj_search``'s first hit and hit count; the early-exit
+  first hit, and that the hit was also lowered into a peer device's hit word;
+* ``mgj_eval`` verdicts (row-major and tiled SoA) on random coordinate rows.
+
+The emitter and the specialiser run under AddressSanitizer + UndefinedBehaviorSanitizer (g++;
+the simulator and the C port, test infrastructure, at -O2).  Programs: ``MYTHGPU_SIMFUZZ_N``
+(default 10,000) LASER-shaped queries (``tests/lasergen.py``: dispatchers, actor sets, keccak-keyed
+mappings with many-prior inverse lookups and literal-slot tails, Store chains, wrap predicates, ITE
+guards, symbol equalities that make MIXED coordinates copy each other in chains), split over four
+emitter configurations (the lookup-compare pushdown and the guarded-lookup pruning on and off, the
+difference cache and Bool lookups off, no literal pool), plus random programs over the tier's
+operators and the workloads at several windows.
+
+Reference anchor: a candidate's verdict is ``Model.eval(And(constraints), model_completion=True)``
+(``mythril/laser/smt/model.py:45-59``) of the query ``get_model`` receives
+(``mythril/support/model.py:15-49``).
+"""
+import multiprocessing as mp
+import os
+import random
+import shutil
+import struct
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+N_FUZZ = int(os.environ.get("MYTHGPU_SIMFUZZ_N", "10000"))
+WORKERS = max(1, min(8, os.cpu_count() or 1))
+CONFIGS = [
+    {},
+    {"MYTHGPU_EQ_PUSHDOWN": "0", "MYTHGPU_ITE_PRUNE": "0"},
+    {"MYTHGPU_JIT_ASM_NO_EQ_CACHE": "1", "MYTHGPU_JIT_ASM_NO_BOOL_LOOKUP": "1"},
+    {"MYTHGPU_JIT_ASM_NOPOOL": "1", "MYTHGPU_EQ_PUSHDOWN": "1"},
+]
+
+
+def _build(out: Path, sanitize: bool) -> Path:
+    from mythril_amd import build
+
+    build.write_prelude()
+    cxx, cc = shutil.which("g++"), shutil.which("gcc")
+    if cxx is None or cc is None:
+        pytest.skip("g++/gcc not available")
+    out.mkdir(parents=True, exist_ok=True)
+    san = ["-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+           "-fno-omit-frame-pointer"] if sanitize else ["-O2"]
+    jobs = []
+    objs = []
+    # the product's emitter and specialiser (under the sanitizers), the checker and the simulator
+    for src, flags, lang in [
+        ("mythril_amd/csrc/program.cpp", san, cxx), ("mythril_amd/csrc/jit_asm.cpp", san, cxx),
+        ("tests/asmsim/asmsim_main.cpp", san, cxx), ("tests/asmsim/asmsim.cpp", ["-O2"], cxx),
+        ("oracle/bveval.c", ["-O2"], cc),
+    ] + ([] if sanitize else [("mythril_amd/csrc/jit.cpp", ["-O2"], cxx)]):
+        o = out / (Path(src).name + ".o")
+        cmd = [lang] + (["-std=c++17"] if lang == cxx else []) + flags + [
+            "-I/opt/rocm/include", f"-I{ROOT}", "-c", str(ROOT / src), "-o", str(o)]
+        if not sanitize:
+            cmd.append("-DASMSIM_ASSEMBLER")
+        jobs.append(subprocess.Popen(cmd, stderr=subprocess.PIPE, text=True))
+        objs.append(str(o))
+    for j in jobs:
+        _, e = j.communicate(timeout=900)
+        assert j.returncode == 0, e[-3000:]
+    exe = out / ("asmsim_asan" if sanitize else "asmsim")
+    r = subprocess.run([cxx] + san + objs + ["-ldl", "-o", str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return exe
+
+
+SOURCES = ["mythril_amd/csrc/program.cpp", "mythril_amd/csrc/program.hpp", "mythril_amd/csrc/jit_asm.cpp",
+           "mythril_amd/csrc/jit.hpp", "include/mythgpu.h", "tests/asmsim/asmsim_main.cpp", "tests/asmsim/asmsim.cpp",
+           "tests/asmsim/asmsim.hpp", "oracle/bveval.c"]
+
+
+def _cached(tmp_path_factory, sanitize: bool) -> Path:
+    """A driver build, cached under /tmp by a hash of its sources (a rebuild costs ~40 s)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for s in SOURCES + (["mythril_amd/csrc/jit.cpp"] if not sanitize else []):
+        h.update((ROOT / s).read_bytes())
+    cache = Path("/tmp") / f"mythgpu-asmsim-{h.hexdigest()[:16]}"
+    name = "asmsim_asan" if sanitize else "asmsim"
+    exe = cache / name
+    if exe.exists():
+        return exe
+    built = _build(tmp_path_factory.mktemp(name), sanitize=sanitize)
+    cache.mkdir(parents=True, exist_ok=True)
+    shutil.copy2(built, cache / (name + ".tmp"))
+    os.replace(cache / (name + ".tmp"), exe)
+    return exe
+
+
+@pytest.fixture(scope="module")
+def sim(tmp_path_factory):
+    """The differential driver (emitter, simulator and C port at -O2; comgr's assembler linked)."""
+    return _cached(tmp_path_factory, sanitize=False)
+
+
+@pytest.fixture(scope="module")
+def sim_asan(tmp_path_factory):
+    """The emitter and the specialiser under ASan + UBSan (run with ASMSIM_EMIT_ONLY=1)."""
+    return _cached(tmp_path_factory, sanitize=True)
+
+
+def record(kind, pb: bytes, blob, seed: int, start: int, count: int, flags: int = 0) -> bytes:
+    out = struct.pack("<II", kind, len(pb)) + pb
+    if blob is None:
+        out += struct.pack("<I", 0xFFFFFFFF)
+    else:
+        g = np.asarray(blob, dtype=np.uint32)
+        out += struct.pack("<I", len(g)) + g.tobytes()
+    return out + struct.pack("<QQII", seed, start, count, flags)
+
+
+def run_sim(exe: Path, records: bytes, env_extra=None, timeout=1500):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    env.update(env_extra or {})
+    r = subprocess.run([str(exe)], input=records, capture_output=True, env=env, timeout=timeout)
+    out = r.stdout.decode(errors="replace")
+    err = r.stderr.decode(errors="replace")
+    lines = out.strip().splitlines()
+    summary = dict(kv.split("=") for kv in lines[-1].split()) if lines and "records=" in lines[-1] else {}
+    return r.returncode, summary, lines[:-1], err
+
+
+def _fuzz_records(lo: int, hi: int, full: bool = False) -> bytes:
+    from mythril_amd import search
+    from tests.lasergen import laser_query
+
+    recs = []
+    for s in range(lo, hi):
+        roots = laser_query(s, full=full)
+        P, blob = search.prepare(roots)
+        rng = random.Random(s * 7919 + 1)
+        start = rng.getrandbits(63)
+        if s % 3 == 0:
+            start = (start & ~0xFFFFFFFF) | 0x80000000 | rng.getrandbits(31)  # bit 31 of the low word set
+        if s % 5 == 0:
+            start = rng.getrandbits(12)  # from near index 0 (the product's early-exit shape)
+        # every 25th kernel also goes through comgr's assembler and linker (encodings, operand rules)
+        recs.append(record(0, P.to_bytes(), blob, rng.getrandbits(32), start, 640 if s % 10 == 0 else 256,
+                           flags=int(s % 25 == 0)))
+    return b"".join(recs)
+
+
+def _fuzz_worker(args):
+    exe, asan, lo, hi, cfg = args
+    recs = _fuzz_records(lo, hi)
+    env = dict(CONFIGS[cfg], MYTHGPU_JIT_ASM_CHECK="1")
+    out = []
+    for e, extra in ((asan, {"ASMSIM_EMIT_ONLY": "1"}), (exe, {})):
+        rc, summary, bad, err = run_sim(Path(e), recs, dict(env, **extra))
+        out.append((rc, summary, bad[:5], err[-3000:], cfg))
+    return out
+
+
+def _check(results, n_expected):
+    total = {"records": 0, "ok": 0, "outside": 0}
+    for rc, summary, bad, err, cfg in results:
+        assert summary, f"config {CONFIGS[cfg]}: no summary (rc {rc})\n{err}"
+        assert rc == 0 and "Sanitizer" not in err and "runtime error" not in err, \
+            f"config {CONFIGS[cfg]}: {summary}\n" + "\n".join(bad) + "\n" + err
+        for k in total:
+            total[k] += int(summary[k])
+    assert total["records"] == n_expected
+    return total
+
+
+def test_asm_tier_laser_fuzz_under_asan(sim, sim_asan):
+    """>= 10,000 LASER-shaped queries: every first-tier verdict, first hit and hit count equals the
+    C port's, with no simulator rule broken, no lifetime violation from the emitter's own checker
+    (MYTHGPU_JIT_ASM_CHECK) and no sanitizer report from the emitter and the specialiser."""
+    n = N_FUZZ
+    step = max(1, n // (WORKERS * 4))
+    tasks = [(str(sim), str(sim_asan), lo, min(n, lo + step), (lo // step) % len(CONFIGS))
+             for lo in range(0, n, step)]
+    with mp.get_context("fork").Pool(WORKERS) as pool:
+        results = pool.map(_fuzz_worker, tasks, chunksize=1)
+    asan_total = _check([r[0] for r in results], n)
+    total = _check([r[1] for r in results], n)
+    print("laser fuzz:", total, "emitter under ASan:", asan_total)
+    # the queries are LASER's vocabulary, inside the tier by construction
+    assert total["ok"] == n and asan_total["ok"] == n, (total, asan_total)
+
+
+def _tier_records(lo, hi, full=False) -> bytes:
+    from mythril_amd import search
+    from tests.helpers import random_tier_program
+
+    recs = []
+    for s in range(lo, hi):
+        roots = random_tier_program(10_000 + s, full=full)
+        P, blob = search.prepare(roots)
+        rng = random.Random(s)
+        recs.append(record(0, P.to_bytes(), blob, rng.getrandbits(32), rng.getrandbits(63), 192))
+        # the eval kernel on the same program (watch list off: verdict rows only)
+        prev = P.watch
+        P.set_watch([])
+        pb = P.to_bytes()
+        P.set_watch(prev)
+        recs.append(record(1 + (s & 1), pb, None, rng.getrandbits(32), 0, 64 * rng.randint(1, 5) + rng.randrange(64)))
+    return b"".join(recs)
+
+
+def _tier_worker(args):
+    exe, lo, hi, cfg = args
+    rc, summary, bad, err = run_sim(Path(exe), _tier_records(lo, hi), dict(CONFIGS[cfg], MYTHGPU_JIT_ASM_CHECK="1"))
+    return rc, summary, bad[:5], err[-3000:], cfg
+
+
+def test_asm_tier_random_programs_sim(sim):
+    """Random programs over the tier's operators (every width from 8 to 512, ITE, Extract/Concat,
+    Zero/SignExt, array Select/Store, UF applications, bvumul_noovfl): search, gen and eval
+    kernels against the C port."""
+    n = int(os.environ.get("MYTHGPU_SIMFUZZ_TIER_N", "1000"))
+    step = max(1, n // (WORKERS * 2))
+    tasks = [(str(sim), lo, min(n, lo + step), (lo // step) % len(CONFIGS)) for lo in range(0, n, step)]
+    with mp.get_context("fork").Pool(WORKERS) as pool:
+        results = pool.map(_tier_worker, tasks, chunksize=1)
+    total = _check(results, 2 * n)
+    print("tier programs:", total)
+    assert total["ok"] >= 2 * n * 0.9, total
+
+
+def test_asm_tier_workloads_sim(sim):
+    """The workloads inside the tier and the bench's hard needle: search/gen at windows with bit 31
+    of the low word set and from index 0, and the eval kernel (row-major and tiled) over several
+    64-candidate groups per wave (the cross-group row ring)."""
+    import bench
+    from mythril_amd import search, workloads
+
+    recs = []
+    queries = {n: [c.raw for c in workloads.WORKLOADS[n]()] for n in workloads.WORKLOADS}
+    queries["hard_needle"] = bench.hard_query(workloads.WORKLOADS["token_transfer_underflow"]())
+    rng = random.Random(5)
+    n_search = 0
+    for name, roots in sorted(queries.items()):
+        P, blob = search.prepare(roots)
+        pb = P.to_bytes()
+        for start in (0, 0x80000001 | (rng.getrandbits(30) << 33), rng.getrandbits(63)):
+            recs.append(record(0, pb, blob, rng.getrandbits(32), start, 4096))
+            n_search += 1
+        prev = P.watch
+        P.set_watch([])
+        pe = P.to_bytes()
+        P.set_watch(prev)
+        for kind in (1, 2):
+            recs.append(record(kind, pe, None, rng.getrandbits(32), 0, 64 * 9 + 37))
+    rc, summary, bad, err = run_sim(sim, b"".join(recs), {"MYTHGPU_JIT_ASM_CHECK": "1"})
+    assert rc == 0, f"{summary}\n" + "\n".join(bad) + "\n" + err[-3000:]
+    # sha3_keyed_mapping (Keccak, EXP, SDIV) is the one workload outside the tier today
+    assert int(summary["ok"]) + int(summary["outside"]) == len(recs)
+    assert int(summary["ok"]) >= len(recs) - 5
+
+
+def _mutants(tmp_path: Path, mutants) -> dict:
+    """Drivers built with textual edits {name: {file: (old, new)}} of their sources (no sanitizers);
+    the unedited objects are compiled once and shared, everything in parallel."""
+    srcs = ("mythril_amd/csrc/program.cpp", "mythril_amd/csrc/jit_asm.cpp", "tests/asmsim/asmsim_main.cpp",
+            "tests/asmsim/asmsim.cpp", "oracle/bveval.c")
+    jobs, objs = [], {}
+
+    def compile_(path: Path, o: Path, src: str):
+        lang = ["gcc"] if src.endswith(".c") else ["g++", "-std=c++17"]
+        jobs.append(subprocess.Popen(lang + ["-O1", f"-I{ROOT}", f"-I{ROOT / Path(src).parent}", "-I/opt/rocm/include",
+                                             "-c", str(path), "-o", str(o)], stderr=subprocess.PIPE, text=True))
+
+    for src in srcs:
+        if any(src not in e for e in mutants.values()):
+            o = tmp_path / f"base_{Path(src).name}.o"
+            compile_(ROOT / src, o, src)
+            objs[src] = o
+    per = {}
+    for name, edits in mutants.items():
+        per[name] = []
+        for src in srcs:
+            if src not in edits:
+                continue
+            text = (ROOT / src).read_text()
+            old, new = edits[src]
+            assert old in text, (src, old)
+            path = tmp_path / f"{name}_{Path(src).name}"
+            path.write_text(text.replace(old, new))
+            o = tmp_path / f"{name}_{Path(src).name}.o"
+            compile_(path, o, src)
+            per[name].append((src, o))
+    for j in jobs:
+        _, e = j.communicate(timeout=900)
+        assert j.returncode == 0, e[-2000:]
+    out = {}
+    for name, own in per.items():
+        mine = dict(objs)
+        mine.update(dict(own))
+        exe = tmp_path / name
+        subprocess.run(["g++"] + [str(mine[s]) for s in srcs] + ["-ldl", "-o", str(exe)], check=True)
+        out[name] = exe
+    return out
+
+
+def test_the_checks_have_teeth(sim, tmp_path):
+    """The differential catches what it is for.  (1) An emitter with round 4's COPY-liveness bug put
+    back (a MIXED coordinate's COPY branch reusing a copy source the depth-first order had already
+    released; it gave false SATs on etherstore on the GPU) fails on etherstore.  (2) A simulator
+    whose subtract-with-borrow is wrong reports mismatches: the emitter and the simulator do not
+    merely agree with themselves."""
+    from mythril_amd import search, workloads
+
+    def recs(name, n=4, count=4096):
+        P, blob = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
+        rng = random.Random(1)
+        return b"".join(record(0, P.to_bytes(), blob, rng.getrandbits(32), rng.getrandbits(63), count)
+                        for _ in range(n))
+
+    eth = recs("etherstore_reentrancy")
+    rc, good, _, _ = run_sim(sim, eth, {"MYTHGPU_JIT_ASM_CHECK": "1"})
+    assert rc == 0 and int(good["mismatch"]) == 0, good
+    exes = _mutants(tmp_path, {
+        "copy_bug": {"mythril_amd/csrc/jit_asm.cpp": ("if (it != cval.end() && val[it->second].def &&",
+                                                      "if (it != cval.end() &&")},
+        "sub_bug": {"tests/asmsim/asmsim.cpp": ("d[l] = (uint32_t)(u - b);", "d[l] = (uint32_t)(u - b + 1);")},
+    })
+    rc, summary, lines, _ = run_sim(exes["copy_bug"], eth)
+    assert rc != 0 and int(summary["mismatch"]) > 0, (summary, lines)
+    mixed = recs("token_transfer_underflow", 1, 1024) + recs("walletlibrary_kill", 1, 1024) + \
+        recs("bectoken_batch_overflow", 1, 1024)
+    rc, summary, lines, _ = run_sim(exes["sub_bug"], mixed)
+    assert rc != 0 and int(summary["mismatch"]) > 0, (summary, lines)

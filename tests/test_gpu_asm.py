@@ -81,69 +81,10 @@ def test_asm_tier_verdicts(engine, name):
     _check(engine, name, _queries()[name]())
 
 
-# operators inside the tier
-_BIN = ["bvadd", "bvsub", "bvmul", "bvand", "bvor", "bvxor"]
-_CMP = ["bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge", "bvumul_noovfl"]
-
-
 def _random_program(seed: int, n_ops: int = 36):
-    from tests.helpers import edge_value
+    from tests.helpers import random_tier_program
 
-    rng = random.Random(seed)
-    pool = {}
-
-    def add(t):
-        pool.setdefault(t.width, []).append(t)
-        return t
-
-    for i, w in enumerate((256, 256, 160, 64, 32, 8, 1 + 7, 257, 512, 1)):
-        if w == 1:
-            continue
-        add(T.BitVecVar(f"a{seed}_{i}_{w}", w))
-        add(T.BitVecVal(edge_value(rng, w), w))
-    bools = [T.BoolVar(f"f{seed}")]
-    arr = T.ArrayVar("Storage", 256, 256)
-    fn = T.FuncDecl("keccak256_512", 512, 256)
-    for _ in range(n_ops):
-        kind = rng.random()
-        w = rng.choice([256, 256, 64, 160, 8, 32, 512])
-        src = pool.get(w) or [T.BitVecVal(0, w)]
-        a, b = rng.choice(src), rng.choice(src)
-        if kind < 0.35:
-            op = rng.choice(_BIN)
-            t = T.bvbin(op if not (op == "bvmul" and w > 256) else "bvadd", a, b)
-        elif kind < 0.45:
-            t = T.bvun(rng.choice(["bvnot", "bvneg"]), a)
-        elif kind < 0.60:
-            c = T.bvcmp(rng.choice(_CMP), a, b) if w <= 256 else T.eq(a, b)
-            bools.append(c)
-            continue
-        elif kind < 0.68:
-            t = T.ite(rng.choice(bools), a, b)
-        elif kind < 0.76:
-            hi = rng.randrange(w)
-            t = T.extract(hi, rng.randrange(hi + 1), a)
-        elif kind < 0.82:
-            w2 = rng.choice([8, 32, 96, 160, 256])
-            b2 = rng.choice(pool.get(w2) or [T.BitVecVal(1, w2)])
-            t = T.concat(a, b2) if a.width + w2 <= 1024 else a
-        elif kind < 0.88:
-            k = rng.choice([1, 8, 96, 256])
-            t = T.zero_extend(k, a) if rng.random() < 0.5 else T.sign_extend(k, a)
-        elif kind < 0.95:
-            idx = rng.choice(pool[256])
-            st = T.store(arr, rng.choice(pool[256]), rng.choice(pool[256])) if rng.random() < 0.5 else arr
-            t = T.select(st, idx)
-        else:
-            t = T.app(fn, T.concat(rng.choice(pool[256]), rng.choice(pool[256])))
-        add(t)
-        if t.width <= 256 and rng.random() < 0.3:
-            bools.append(T.eq(t, rng.choice(pool.get(t.width) or [t])))
-    for _ in range(3):
-        x, y = rng.choice(bools), rng.choice(bools)
-        bools.append(rng.choice([T.and_(x, y), T.or_(x, y), T.not_(x), T.xor_(x, y), T.eq(x, y)]))
-    # an OR of a few of them: satisfiable by many candidates, so verdicts carry information
-    return [T.or_(*rng.sample(bools, min(3, len(bools)))), T.or_(*rng.sample(bools, min(3, len(bools))))]
+    return random_tier_program(seed, n_ops)
 
 
 @pytest.mark.parametrize("seed", range(24))
