@@ -363,14 +363,13 @@ struct Gen {
         case K_EXTRACT: case K_ZEXT: case K_SEXT: case K_LOOKUP: case K_ASSERT: case K_COPY: case K_MUL:
         case K_WATCH: case K_UMUL_NOOVF:
           break;
-        case K_UDIV: case K_UREM: {
-          // by a literal below 2^32 only (x / 86400, x / 10**k: a limb-serial 2/1 division)
-          const Instr* bd = def_of(in.b);
-          bool ok = bd && bd->op == K_CONST;
-          for (uint32_t j = 1; ok && j < Lw(in.wd); j++) ok = P.consts[bd->p0 + j] == 0;
-          if (!ok) fail("division by a non-literal or a literal of 32 bits or more: outside the assembly tier");
+        case K_UDIV: case K_UREM: case K_SDIV: case K_SREM: case K_SMOD: case K_SHL: case K_LSHR: case K_ASHR:
+        case K_EXP:
+          // data-dependent operators (widths <= 256 after lowering): div_lit / udivrem / shift_var / exp_var
+          if (in.wd > 256) fail("arithmetic wider than 256 bits");
           break;
-        }
+        case K_KECCAK:
+          break;
         default:
           fail("op " + std::to_string(in.op) + " outside the assembly tier");
       }
@@ -451,7 +450,14 @@ struct Gen {
         case K_ASSERT: all(in.a); break;
         case K_WATCH: if (eval_kernel) all(in.a); break;
         case K_ADD: case K_SUB: case K_MUL: upto(in.a, nd); upto(in.b, nd); break;
-        case K_UDIV: case K_UREM: if (nd) { all(in.a); all(in.b); } break;
+        case K_UDIV: case K_UREM: case K_SDIV: case K_SREM: case K_SMOD: case K_SHL: case K_LSHR: case K_ASHR:
+        case K_EXP:
+          if (nd) {
+            all(in.a);
+            all(in.b);
+          }
+          break;
+        case K_KECCAK: if (nd && in.a != MG_NONE) all(in.a); break;
         case K_UMUL_NOOVF: all(in.a); all(in.b); break;
         case K_NEG: upto(in.a, nd); break;
         case K_AND: case K_OR: case K_XOR: same(in.a, nd); same(in.b, nd); break;
@@ -1746,6 +1752,747 @@ struct Gen {
   }
   uint32_t demanded(uint32_t d) const { return need[d] ? 64 - (uint32_t)__builtin_clzll(need[d]) : 0; }
 
+  // ---------------------------------------------------------------------------------------
+  // data-dependent operators: variable shifts, division by a non-literal, EXP, Keccak-256.
+  // Values are <= 256 bits here (the lowering's bound), so they live in <= 8 limbs; loops are
+  // wave-uniform (trip counts are wave maxima found with ballots), per-lane work is predicated by
+  // EXEC inside the loop (division) or by selects, and loop-carried values sit in registers
+  // allocated before the loop and updated in place, so the allocator's state is the same at the
+  // back edge as at the head.  Semantics: SMT-LIB total division (x / 0 = ~0, x % 0 = x), shifts
+  // of w or more saturate, EVM EXP mod 2^w, Keccak-256 of the value's big-endian bytes.
+  // ---------------------------------------------------------------------------------------
+  // the divisor b is a literal below 2^32 (the limb-serial 2/1 path above)
+  bool lit_divisor(uint32_t b, uint32_t Ld) const {
+    const Instr* bd = def_of(b);
+    bool ok = bd && bd->op == K_CONST;
+    for (uint32_t j = 1; ok && j < Ld; j++) ok = P.consts[bd->p0 + j] == 0;
+    return ok;
+  }
+  void drop_all(std::vector<Limb>& v) {
+    for (auto& x : v) drop(x);
+    v.clear();
+  }
+  // fresh registers holding x[0..n) (literal or missing limbs as their value / zero): loop state
+  std::vector<Limb> own(const std::vector<Limb>& x, uint32_t n) {
+    std::vector<Limb> r(n);
+    for (uint32_t j = 0; j < n; j++) {
+      const Limb s = j < x.size() && x[j].k != LU ? x[j] : Lit(0);
+      r[j] = fresh();
+      E.valu("v_mov_b32_e32 " + VL(r[j]) + ", " + src(s));
+    }
+    return r;
+  }
+  // a scalar SGPR (one of a pair) for loop counters and wave maxima
+  int sreg() { return E.salloc(); }
+  void sfree(int s) {
+    Mask m;
+    m.k = 2;
+    m.s = s;
+    E.srelease(m);
+  }
+  Mask mask_new() {
+    Mask m;
+    m.k = 2;
+    m.s = E.salloc();
+    return m;
+  }
+  // d = m ? t : f for VGPR operands (f/t may be the zero register)
+  void vsel(const Limb& d, const Limb& f, const Limb& t, const Mask& m) {
+    E.valu("v_cndmask_b32_e64 " + VL(d) + ", " + VL(f) + ", " + VL(t) + ", " + SP(m.s), {m.s, m.s + 1});
+  }
+  // a mask from one VALU compare of a VGPR with an inline constant or SGPR s41 (literal)
+  Mask vcmp(const char* op, const Limb& a, uint32_t k) {
+    Mask m = mask_new();
+    if (inl(k)) {
+      E.valu(std::string("v_cmp_") + op + "_u32_e64 " + SP(m.s) + ", " + VL(a) + ", " + imm(k), {}, {m.s, m.s + 1});
+    } else {
+      E.salu("s_mov_b32 s41, " + hexs(k), {41});
+      E.valu(std::string("v_cmp_") + op + "_u32_e64 " + SP(m.s) + ", " + VL(a) + ", s41", {41}, {m.s, m.s + 1});
+    }
+    return m;
+  }
+
+  // bit length of a limb vector (0 for zero) into a fresh VGPR
+  Limb bitlen(const std::vector<Limb>& x) {
+    const Limb bl = fresh();
+    E.valu("v_mov_b32_e32 " + VL(bl) + ", 0");
+    for (uint32_t j = 0; j < x.size(); j++) {
+      const Limb l = x[j];
+      if (l.k == LU || (l.lit() && l.v == 0)) continue;
+      if (l.lit()) {
+        E.valu("v_mov_b32_e32 " + VL(bl) + ", " + imm(32 * j + 32 - (uint32_t)__builtin_clz(l.v)));
+        continue;
+      }
+      const Limb t = fresh();
+      E.valu("v_ffbh_u32_e32 " + VL(t) + ", " + VL(l));                      // leading zeros (~0 for 0)
+      E.valu("v_sub_u32_e32 " + VL(t) + ", " + imm(32 * j + 32) + ", " + VL(t));
+      const Mask nz = vcmp("ne", l, 0);
+      vsel(bl, bl, t, nz);
+      E.srelease(nz);
+      drop(t);
+    }
+    return bl;
+  }
+  // the wave-uniform maximum of a per-lane value v < 2^bits into SGPR s (ballot binary search)
+  void wave_max(const Limb& v, uint32_t bits, int s) {
+    const int c = sreg();
+    const Mask m = mask_new();
+    E.salu("s_mov_b32 " + S(s) + ", 0", {s});
+    for (int b = (int)bits - 1; b >= 0; b--) {
+      E.salu("s_add_u32 " + S(c) + ", " + S(s) + ", " + imm(1u << b), {c});
+      E.valu("v_cmp_ge_u32_e64 " + SP(m.s) + ", " + VL(v) + ", " + S(c), {c}, {m.s, m.s + 1});
+      E.salu("s_cmp_lg_u64 " + SP(m.s) + ", 0");
+      E.salu("s_cselect_b32 " + S(s) + ", " + S(c) + ", " + S(s), {s});
+    }
+    E.srelease(m);
+    sfree(c);
+  }
+
+  // ---- shifts ------------------------------------------------------------------------------
+  // x (owned registers, L limbs) shifted by whole limbs: q = s >> 5 per lane, barrel stages k =
+  // 1, 2, 4, ... (a select per limb each); left: towards higher limbs, zero fill; right: fill f
+  void limb_barrel(std::vector<Limb>& x, const Limb& s, bool left, const Limb& fill) {
+    const uint32_t Lx = (uint32_t)x.size();
+    const Limb q = fresh();
+    E.valu("v_lshrrev_b32_e32 " + VL(q) + ", 5, " + VL(s));
+    for (uint32_t k = 1; k <= Lx; k <<= 1) {
+      const Limb t = fresh();
+      E.valu("v_and_b32_e32 " + VL(t) + ", " + imm(k) + ", " + VL(q));
+      const Mask on = vcmp("ne", t, 0);
+      drop(t);
+      if (left) {
+        for (int i = (int)Lx - 1; i >= 0; i--) vsel(x[i], x[i], i >= (int)k ? x[i - k] : fill, on);
+      } else {
+        for (uint32_t i = 0; i < Lx; i++) vsel(x[i], x[i], i + k < Lx ? x[i + k] : fill, on);
+      }
+      E.srelease(on);
+    }
+    drop(q);
+  }
+  // x (owned) shifted within its limbs by s (a VGPR, 0 <= s <= 32 L): left or right with fill f
+  // (a VGPR: the zero register or a sign word)
+  void shift_limbs(std::vector<Limb>& x, const Limb& s, bool left, const Limb& fill) {
+    const uint32_t Lx = (uint32_t)x.size();
+    limb_barrel(x, s, left, fill);
+    const Limb b = fresh();
+    E.valu("v_and_b32_e32 " + VL(b) + ", 31, " + VL(s));
+    if (left) {
+      // x[i] = (x[i] << b) | (x[i-1] >> (32 - b)): alignbit by -b (mod 32), except b = 0
+      const Limb nb = fresh(), t = fresh();
+      E.valu("v_sub_u32_e32 " + VL(nb) + ", 0, " + VL(b));
+      const Mask z = vcmp("eq", b, 0);
+      for (int i = (int)Lx - 1; i >= 0; i--) {
+        E.valu("v_alignbit_b32 " + VL(t) + ", " + VL(x[i]) + ", " + (i ? VL(x[i - 1]) : std::string("0")) + ", " + VL(nb));
+        vsel(x[i], t, x[i], z);
+      }
+      E.srelease(z);
+      drop(nb);
+      drop(t);
+    } else {
+      for (uint32_t i = 0; i < Lx; i++)
+        E.valu("v_alignbit_b32 " + VL(x[i]) + ", " + VL(i + 1 < Lx ? x[i + 1] : fill) + ", " + VL(x[i]) + ", " + VL(b));
+    }
+    drop(b);
+  }
+  // the shift amount of value b saturated to W, in a fresh VGPR
+  Limb shift_amount(uint32_t bid, uint32_t W) {
+    const uint32_t Lb = L(bid);
+    const Limb b0 = limb(bid, 0), s = fresh();
+    if (b0.lit()) E.valu("v_mov_b32_e32 " + VL(s) + ", " + imm(std::min(b0.v, W)));
+    else E.valu("v_min_u32_e32 " + VL(s) + ", " + imm(W) + ", " + VL(b0));
+    std::vector<std::pair<Limb, Limb>> hz;
+    for (uint32_t j = 1; j < Lb; j++) hz.push_back({limb(bid, j), Lit(0)});
+    if (!hz.empty()) {
+      const Mask z = eq_mask(hz);  // every high limb zero
+      if (z.k == 1) {
+        if (!z.ones) E.valu("v_mov_b32_e32 " + VL(s) + ", " + imm(W));
+      } else {
+        const Limb wv = vreg(Lit(W));
+        vsel(s, wv, s, z);
+        drop(wv);
+      }
+      E.srelease(z);
+    }
+    return s;
+  }
+  // SHL / LSHR / ASHR of the width-W value a by value b
+  std::vector<Limb> shift_var(uint32_t op, const std::vector<Limb>& a, uint32_t bid, uint32_t W) {
+    const uint32_t La = Lw(W);
+    std::vector<Limb> x = own(a, La);
+    const Limb s = shift_amount(bid, W);
+    Limb fill = Reg(6);
+    if (op == K_ASHR) {
+      // sign-extend the top limb, the fill word is its sign
+      if (W & 31) E.valu("v_bfe_i32 " + VL(x[La - 1]) + ", " + VL(x[La - 1]) + ", 0, " + std::to_string(W & 31));
+      fill = fresh();
+      E.valu("v_ashrrev_i32_e32 " + VL(fill) + ", 31, " + VL(x[La - 1]));
+    }
+    shift_limbs(x, s, op == K_SHL, fill);
+    if (op == K_ASHR) drop(fill);
+    drop(s);
+    mask_top(x, W);
+    return x;
+  }
+
+  // ---- multiplication (low n limbs, schoolbook) ------------------------------------------------
+  std::vector<Limb> mul_lo(const std::vector<Limb>& a, const std::vector<Limb>& b, uint32_t n) {
+    std::vector<Limb> acc(n, Lit(0));  // owned
+    for (uint32_t i = 0; i < n; i++) {
+      const Limb x = i < a.size() ? a[i] : Lit(0);
+      if (x.lit() && x.v == 0) continue;
+      std::vector<Limb> lo(n, Lit(0)), hi(n, Lit(0));
+      for (uint32_t j = 0; i + j < n; j++) {
+        const Limb y = j < b.size() ? b[j] : Lit(0);
+        if (y.lit() && y.v == 0) continue;
+        if (x.lit() && y.lit()) {
+          const uint64_t p = (uint64_t)x.v * y.v;
+          lo[i + j] = Lit((uint32_t)p);
+          if (i + j + 1 < n) hi[i + j + 1] = Lit((uint32_t)(p >> 32));
+          continue;
+        }
+        const Limb vx = x.reg() ? x : y, ly = x.reg() ? y : x;
+        const bool via_s41 = ly.lit() && !inl(ly.v);
+        if (via_s41) E.salu("s_mov_b32 s41, " + hexs(ly.v), {41});
+        const std::string so = via_s41 ? std::string("s41") : src(ly);
+        const Limb dl = fresh();
+        if (via_s41) E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so, {41});
+        else E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so);
+        lo[i + j] = dl;
+        if (i + j + 1 < n) {
+          const Limb dh = fresh();
+          if (via_s41) E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so, {41});
+          else E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so);
+          hi[i + j + 1] = dh;
+        }
+      }
+      std::vector<Limb> s1 = add_chain(acc, lo, n, false);
+      for (auto& t : acc) drop(t);
+      for (auto& t : lo) drop(t);
+      std::vector<Limb> s2 = add_chain(s1, hi, n, false);
+      for (auto& t : s1) drop(t);
+      for (auto& t : hi) drop(t);
+      acc = s2;
+    }
+    return acc;
+  }
+  // dst[j] = v[j] (moves into loop-state registers; v released)
+  void assign(const std::vector<Limb>& dst, std::vector<Limb>& v) {
+    for (size_t j = 0; j < dst.size(); j++) {
+      const Limb x = j < v.size() && v[j].k != LU ? v[j] : Lit(0);
+      if (x == dst[j]) continue;
+      E.valu("v_mov_b32_e32 " + VL(dst[j]) + ", " + src(x));
+    }
+    drop_all(v);
+  }
+
+  // ---- division ------------------------------------------------------------------------------
+  // q, r of a / b (unsigned, width W) with SMT-LIB's total division: per lane, a restoring
+  // division over the quotient's bits only (la - lb + 1 of them, la / lb the bit lengths, as
+  // bv_device.h udivrem8), the remainder kept in NB limbs — NB the wave's widest divisor, one of
+  // 1 / 2 / 4 / L, a uniform branch — and the loop run for the wave's longest quotient with
+  // EXEC holding the lanes that still have steps
+  void udivrem(const std::vector<Limb>& a_in, const std::vector<Limb>& b_in, uint32_t W, std::vector<Limb>& q,
+               std::vector<Limb>& r) {
+    const uint32_t La = Lw(W), C = 32 * La;
+    std::vector<Limb> a = a_in, b = b_in;
+    a.resize(La, Lit(0));
+    b.resize(La, Lit(0));
+    const Limb la = bitlen(a), lb = bitlen(b);
+    // n = la >= lb ? la - lb + 1 : 0
+    const Limb n = fresh();
+    E.valu("v_sub_u32_e32 " + VL(n) + ", " + VL(la) + ", " + VL(lb));
+    E.valu("v_add_u32_e32 " + VL(n) + ", 1, " + VL(n));
+    {
+      Mask lt = mask_new();
+      E.valu("v_cmp_lt_u32_e64 " + SP(lt.s) + ", " + VL(la) + ", " + VL(lb), {}, {lt.s, lt.s + 1});
+      vsel(n, n, Reg(6), lt);
+      E.srelease(lt);
+    }
+    drop(la);
+    // rem = a >> n, quo = a << (C - n)
+    std::vector<Limb> rem = own(a, La), quo = own(a, La);
+    shift_limbs(rem, n, false, Reg(6));
+    {
+      const Limb cn = fresh();
+      E.valu("v_sub_u32_e32 " + VL(cn) + ", " + imm(C) + ", " + VL(n));
+      shift_limbs(quo, cn, true, Reg(6));
+      drop(cn);
+    }
+    // the divisor's limbs as registers for the subtraction
+    std::vector<Limb> bv(La);
+    for (uint32_t j = 0; j < La; j++) bv[j] = vreg(b[j]);
+    const int sN = sreg(), sIt = sreg();
+    wave_max(n, 9, sN);
+    // NB: the wave's widest divisor in limbs (ballots over the divisor's limbs)
+    const int sNB = sreg();
+    E.salu("s_mov_b32 " + S(sNB) + ", 1", {sNB});
+    {
+      const Mask m = mask_new();
+      for (uint32_t j = 1; j < La; j++) {
+        if (b[j].lit() && b[j].v == 0) continue;
+        if (b[j].lit()) {
+          E.salu("s_mov_b32 " + S(sNB) + ", " + imm(j + 1), {sNB});
+          continue;
+        }
+        E.valu("v_cmp_ne_u32_e64 " + SP(m.s) + ", 0, " + VL(bv[j]), {}, {m.s, m.s + 1});
+        E.salu("s_cmp_lg_u64 " + SP(m.s) + ", 0");
+        E.salu("s_cselect_b32 " + S(sNB) + ", " + imm(j + 1) + ", " + S(sNB), {sNB});
+      }
+      E.srelease(m);
+    }
+    std::vector<uint32_t> widths;
+    for (uint32_t nb : {1u, 2u, 4u, La})
+      if (nb <= La && std::find(widths.begin(), widths.end(), nb) == widths.end()) widths.push_back(nb);
+    const std::string done = E.newlab();
+    const Mask act = mask_new(), cm = mask_new(), ge = mask_new();
+    for (size_t vi = 0; vi < widths.size(); vi++) {
+      const uint32_t NB = widths[vi];
+      const std::string next = E.newlab(), loop = E.newlab(), end = E.newlab();
+      if (vi + 1 < widths.size()) {  // this variant serves the waves whose widest divisor has <= NB limbs
+        E.salu("s_cmp_gt_u32 " + S(sNB) + ", " + imm(NB));
+        E.ctl("s_cbranch_scc1 " + next);
+      }
+      E.salu("s_mov_b32 " + S(sIt) + ", 0", {sIt});
+      E.label(loop);
+      E.salu("s_cmp_ge_u32 " + S(sIt) + ", " + S(sN));
+      E.ctl("s_cbranch_scc1 " + end);
+      // lanes with a step left
+      E.salu("s_mov_b64 exec, -1");
+      E.valu("v_cmp_gt_u32_e64 " + SP(act.s) + ", " + VL(n) + ", " + S(sIt), {sIt}, {act.s, act.s + 1});
+      E.salu("s_mov_b64 exec, " + SP(act.s));
+      // (rem : quo) <<= 1: quo's top bit carries into rem, rem's top bit out (cm)
+      for (uint32_t i = 0; i < La; i++) {
+        if (i == 0) E.valu("v_add_co_u32_e32 " + VL(quo[0]) + ", vcc, " + VL(quo[0]) + ", " + VL(quo[0]), {}, {kVCC, kVCC + 1});
+        else E.valu("v_addc_co_u32_e32 " + VL(quo[i]) + ", vcc, " + VL(quo[i]) + ", " + VL(quo[i]) + ", vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
+      }
+      for (uint32_t i = 0; i < NB; i++)
+        E.valu("v_addc_co_u32_e32 " + VL(rem[i]) + ", vcc, " + VL(rem[i]) + ", " + VL(rem[i]) + ", vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
+      E.salu("s_mov_b64 " + SP(cm.s) + ", vcc", {cm.s, cm.s + 1});
+      // d = rem - b (NB limbs); ge = carry-out | no borrow
+      std::vector<Limb> dd(NB);
+      for (uint32_t i = 0; i < NB; i++) {
+        dd[i] = fresh();
+        if (i == 0) E.valu("v_sub_co_u32_e32 " + VL(dd[0]) + ", vcc, " + VL(rem[0]) + ", " + VL(bv[0]), {}, {kVCC, kVCC + 1});
+        else E.valu("v_subb_co_u32_e32 " + VL(dd[i]) + ", vcc, " + VL(rem[i]) + ", " + VL(bv[i]) + ", vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
+      }
+      E.salu("s_orn2_b64 " + SP(ge.s) + ", " + SP(cm.s) + ", vcc", {ge.s, ge.s + 1});
+      for (uint32_t i = 0; i < NB; i++) vsel(rem[i], rem[i], dd[i], ge);
+      drop_all(dd);
+      // the quotient bit
+      E.salu("s_mov_b64 vcc, " + SP(ge.s), {kVCC, kVCC + 1});
+      E.valu("v_addc_co_u32_e32 " + VL(quo[0]) + ", vcc, 0, " + VL(quo[0]) + ", vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
+      E.salu("s_add_u32 " + S(sIt) + ", " + S(sIt) + ", 1", {sIt});
+      E.ctl("s_branch " + loop);
+      E.label(end);
+      E.salu("s_mov_b64 exec, -1");
+      if (vi + 1 < widths.size()) {
+        E.ctl("s_branch " + done);
+        E.label(next);
+      }
+    }
+    E.label(done);
+    E.salu("s_mov_b64 exec, -1");
+    E.srelease(act);
+    E.srelease(cm);
+    E.srelease(ge);
+    sfree(sN);
+    sfree(sIt);
+    sfree(sNB);
+    drop(n);
+    for (auto& x : bv) drop(x);
+    // b == 0 (lb == 0): q = ~0 (to the width), r = a
+    {
+      const Mask z = vcmp("eq", lb, 0);
+      for (uint32_t i = 0; i < La; i++) {
+        const uint32_t ones = i == La - 1 ? topmask(W) : 0xFFFFFFFFu;
+        const Limb o = vreg(Lit(ones));
+        vsel(quo[i], quo[i], o, z);
+        drop(o);
+        const Limb ai = vreg(a[i]);
+        vsel(rem[i], rem[i], ai, z);
+        drop(ai);
+      }
+      E.srelease(z);
+    }
+    drop(lb);
+    q = quo;
+    r = rem;
+  }
+  // two's-complement negation of x (owned, in place) where mask m is set, to the width W
+  void neg_where(std::vector<Limb>& x, const Mask& m, uint32_t W) {
+    if (m.k == 1 && !m.ones) return;
+    std::vector<Limb> z(x.size(), Lit(0));
+    std::vector<Limb> ng = add_chain(z, x, (uint32_t)x.size(), true);
+    mask_top(ng, W);
+    for (size_t j = 0; j < x.size(); j++) {
+      const Limb t = vreg(ng[j]);
+      if (m.k == 1) E.valu("v_mov_b32_e32 " + VL(x[j]) + ", " + VL(t));
+      else vsel(x[j], x[j], t, m);
+      drop(t);
+    }
+    drop_all(ng);
+  }
+  // the sign of a width-W value (bit W-1) as a mask
+  Mask sign_mask(const std::vector<Limb>& x, uint32_t W) {
+    const Limb t = x[Lw(W) - 1];
+    if (t.lit()) {
+      Mask m;
+      m.k = 1;
+      m.ones = (t.v >> ((W - 1) & 31)) & 1u;
+      return m;
+    }
+    const Limb b = fresh();
+    E.valu("v_bfe_u32 " + VL(b) + ", " + VL(t) + ", " + std::to_string((W - 1) & 31) + ", 1");
+    const Mask m = vcmp("ne", b, 0);
+    drop(b);
+    return m;
+  }
+  // SDIV / SREM / SMOD by the msb case split (bv_device.h bv_sdiv / bv_srem / bv_smod)
+  std::vector<Limb> sdivrem(uint32_t op, const std::vector<Limb>& a_in, const std::vector<Limb>& b_in, uint32_t W) {
+    const uint32_t La = Lw(W);
+    std::vector<Limb> a = own(a_in, La), b = own(b_in, La);
+    const Mask ma = sign_mask(a, W), mb = sign_mask(b, W);
+    std::vector<Limb> aa = own(a, La), bb = own(b, La);
+    neg_where(aa, ma, W);
+    neg_where(bb, mb, W);
+    std::vector<Limb> q, r;
+    udivrem(aa, bb, W, q, r);
+    drop_all(aa);
+    drop_all(bb);
+    std::vector<Limb> out;
+    if (op == K_SDIV) {
+      drop_all(r);
+      const Mask x = mop("xor", ma, mb);
+      neg_where(q, x, W);
+      E.srelease(x);
+      out = q;
+    } else if (op == K_SREM) {
+      drop_all(q);
+      neg_where(r, ma, W);
+      out = r;
+    } else {
+      // SMOD: u = |a| urem |b|; u == 0 or both non-negative: u; a < 0 <= b: b - u;
+      // a >= 0 > b: u + b; both negative: -u
+      drop_all(q);
+      std::vector<std::pair<Limb, Limb>> zp;
+      for (uint32_t j = 0; j < La; j++) zp.push_back({r[j], Lit(0)});
+      const Mask uz = eq_mask(zp);
+      std::vector<Limb> bmu = add_chain(b, r, La, true);  // b - u
+      std::vector<Limb> upb = add_chain(r, b, La, false); // u + b
+      mask_top(bmu, W);
+      mask_top(upb, W);
+      std::vector<Limb> nu(La, Lit(0));
+      std::vector<Limb> negu = add_chain(nu, r, La, true);  // -u
+      mask_top(negu, W);
+      const Mask nmb = mnot(mb), nma = mnot(ma);
+      const Mask c1 = mop("and", ma, nmb), c2 = mop("and", nma, mb), c3 = mop("and", ma, mb);
+      for (uint32_t j = 0; j < La; j++) {
+        for (auto pr : {std::make_pair(&bmu, c1), std::make_pair(&upb, c2), std::make_pair(&negu, c3)}) {
+          if (pr.second.k == 1 && !pr.second.ones) continue;
+          const Limb t = vreg((*pr.first)[j]);
+          if (pr.second.k == 1) E.valu("v_mov_b32_e32 " + VL(r[j]) + ", " + VL(t));
+          else vsel(r[j], r[j], t, pr.second);
+          drop(t);
+        }
+      }
+      // u == 0: 0 (r is zero then unless a case above changed it: restore zero)
+      if (!(uz.k == 1 && !uz.ones))
+        for (uint32_t j = 0; j < La; j++) {
+          if (uz.k == 1) E.valu("v_mov_b32_e32 " + VL(r[j]) + ", 0");
+          else vsel(r[j], r[j], Reg(6), uz);
+        }
+      for (const Mask& m : {uz, nmb, nma, c1, c2, c3}) E.srelease(m);
+      drop_all(bmu);
+      drop_all(upb);
+      drop_all(negu);
+      out = r;
+    }
+    E.srelease(ma);
+    E.srelease(mb);
+    drop_all(a);
+    drop_all(b);
+    return out;
+  }
+
+  // ---- EXP -----------------------------------------------------------------------------------
+  // base^e mod 2^W, left-to-right over the exponent's 2-bit digits (bv_device.h bv_exp): the wave's
+  // longest exponent (ballots) fixes the step count; the exponent is pre-shifted so its top digit
+  // sits at the top; per step two squarings and, where some lane's digit is non-zero, a multiply
+  // by base^{1,2,3} (selected per lane)
+  std::vector<Limb> exp_var(const std::vector<Limb>& base_in, const std::vector<Limb>& e_in, uint32_t W) {
+    const uint32_t La = Lw(W), C = 32 * La;
+    std::vector<Limb> base = own(base_in, La), ex = own(e_in, La);
+    std::vector<Limb> r(La);
+    for (uint32_t j = 0; j < La; j++) {
+      r[j] = fresh();
+      E.valu("v_mov_b32_e32 " + VL(r[j]) + ", " + (j ? "0" : "1"));
+    }
+    std::vector<Limb> b2 = mul_lo(base, base, La), b3;
+    {
+      std::vector<Limb> t = mul_lo(b2, base, La);
+      b3 = own(t, La);
+      drop_all(t);
+      std::vector<Limb> t2 = own(b2, La);
+      drop_all(b2);
+      b2 = t2;
+    }
+    const Limb el = bitlen(ex);
+    const int sD = sreg();
+    wave_max(el, 9, sD);
+    drop(el);
+    // digits D = ceil(T / 2); ex <<= C - 2 D
+    E.salu("s_add_u32 " + S(sD) + ", " + S(sD) + ", 1", {sD});
+    E.salu("s_lshr_b32 " + S(sD) + ", " + S(sD) + ", 1", {sD});
+    {
+      const Limb sh = fresh();
+      E.salu("s_lshl_b32 s41, " + S(sD) + ", 1", {41});
+      E.salu("s_sub_u32 s41, " + imm(C) + ", s41", {41});
+      E.valu("v_mov_b32_e32 " + VL(sh) + ", s41", {41});
+      shift_limbs(ex, sh, true, Reg(6));
+      drop(sh);
+    }
+    const std::string loop = E.newlab(), end = E.newlab();
+    const Mask nz = mask_new();
+    E.label(loop);
+    E.salu("s_cmp_eq_u32 " + S(sD) + ", 0");
+    E.ctl("s_cbranch_scc1 " + end);
+    const Limb dg = fresh();
+    E.valu("v_lshrrev_b32_e32 " + VL(dg) + ", 30, " + VL(ex[La - 1]));
+    for (int i = (int)La - 1; i > 0; i--)
+      E.valu("v_alignbit_b32 " + VL(ex[i]) + ", " + VL(ex[i]) + ", " + VL(ex[i - 1]) + ", 30");
+    E.valu("v_lshlrev_b32_e32 " + VL(ex[0]) + ", 2, " + VL(ex[0]));
+    for (int sq = 0; sq < 2; sq++) {
+      std::vector<Limb> t = mul_lo(r, r, La);
+      assign(r, t);
+    }
+    {
+      const std::string skip = E.newlab();
+      E.valu("v_cmp_ne_u32_e64 " + SP(nz.s) + ", 0, " + VL(dg), {}, {nz.s, nz.s + 1});
+      E.salu("s_cmp_eq_u64 " + SP(nz.s) + ", 0");
+      E.ctl("s_cbranch_scc1 " + skip);
+      const Mask m1 = vcmp("eq", dg, 1), m2 = vcmp("eq", dg, 2);
+      std::vector<Limb> f(La);
+      for (uint32_t j = 0; j < La; j++) {
+        f[j] = fresh();
+        vsel(f[j], b3[j], b2[j], m2);
+        vsel(f[j], f[j], base[j], m1);
+      }
+      E.srelease(m1);
+      E.srelease(m2);
+      std::vector<Limb> p = mul_lo(r, f, La);
+      drop_all(f);
+      for (uint32_t j = 0; j < La; j++) {
+        const Limb t = vreg(p[j]);
+        vsel(r[j], r[j], t, nz);
+        drop(t);
+      }
+      drop_all(p);
+      E.label(skip);
+    }
+    drop(dg);
+    E.salu("s_add_u32 " + S(sD) + ", " + S(sD) + ", -1", {sD});
+    E.ctl("s_branch " + loop);
+    E.label(end);
+    E.srelease(nz);
+    sfree(sD);
+    drop_all(base);
+    drop_all(ex);
+    drop_all(b2);
+    drop_all(b3);
+    mask_top(r, W);
+    return r;
+  }
+
+  // ---- Keccak-256 ----------------------------------------------------------------------------
+  // keccak256 of the big-endian bytes of a width-w value (nbytes of them, pad10*1, rate 136 B),
+  // as keccak_value (jit_device.h) and oracle/bveval.c vkeccak.  State: 25 lanes as (lo, hi)
+  // VGPR halves; the permutation is a loop over rounds in three unrolled chunks of eight (the
+  // round constants built on the SALU from a packed 7-bit code per round); rho and pi rotate each
+  // lane into its destination in place along the pi cycle (one saved lane), chi keeps two saved
+  // lanes per row
+  static uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+  void keccak_f1600(std::vector<Limb>& st) {  // st: 50 owned registers, lane i = (st[2i], st[2i+1])
+    static const uint64_t RC[24] = {
+        0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
+        0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+        0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
+        0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
+        0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+        0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+    static const uint32_t kPos[7] = {0, 1, 3, 7, 15, 31, 63};
+    auto lo = [&](int i) { return st[2 * i]; };
+    auto hi = [&](int i) { return st[2 * i + 1]; };
+    const int sT = sreg(), sK = sreg(), sR = sreg();  // packed table (pair), round count, RC lo/hi
+    std::vector<Limb> c(10), rr(10);
+    for (auto& x : c) x = fresh();
+    for (auto& x : rr) x = fresh();
+    const Limb t0 = fresh(), t1 = fresh(), s0 = fresh(), s1 = fresh();
+    for (int chunk = 0; chunk < 3; chunk++) {
+      // 8 rounds x 7 bits: bit j of round k's code is RC bit kPos[j]
+      uint64_t packed = 0;
+      for (int k = 0; k < 8; k++) {
+        uint64_t code = 0, back = 0;
+        for (int j = 0; j < 7; j++) code |= ((RC[8 * chunk + k] >> kPos[j]) & 1ull) << j;
+        for (int j = 0; j < 7; j++) back |= ((code >> j) & 1ull) << kPos[j];
+        if (back != RC[8 * chunk + k]) fail("internal: a Keccak round constant outside the 7-bit code");
+        packed |= code << (7 * k);
+      }
+      E.salu("s_mov_b32 " + S(sT) + ", " + hexs((uint32_t)packed), {sT});
+      E.salu("s_mov_b32 " + S(sT + 1) + ", " + hexs((uint32_t)(packed >> 32)), {sT + 1});
+      E.salu("s_mov_b32 " + S(sK) + ", 8", {sK});
+      const std::string loop = E.newlab();
+      E.label(loop);
+      // theta: C[x] = xor of column x; a[x,y] ^= C[x-1] ^ rot(C[x+1], 1)
+      for (int x = 0; x < 5; x++)
+        for (int h = 0; h < 2; h++) {
+          auto L_ = [&](int i) { return h ? hi(i) : lo(i); };
+          const Limb d = c[2 * x + h];
+          E.valu("v_bitop3_b32 " + VL(d) + ", " + VL(L_(x)) + ", " + VL(L_(x + 5)) + ", " + VL(L_(x + 10)) + " bitop3:0x96");
+          E.valu("v_bitop3_b32 " + VL(d) + ", " + VL(d) + ", " + VL(L_(x + 15)) + ", " + VL(L_(x + 20)) + " bitop3:0x96");
+        }
+      for (int x = 0; x < 5; x++) {
+        E.valu("v_alignbit_b32 " + VL(rr[2 * x]) + ", " + VL(c[2 * x]) + ", " + VL(c[2 * x + 1]) + ", 31");
+        E.valu("v_alignbit_b32 " + VL(rr[2 * x + 1]) + ", " + VL(c[2 * x + 1]) + ", " + VL(c[2 * x]) + ", 31");
+      }
+      for (int y = 0; y < 25; y += 5)
+        for (int x = 0; x < 5; x++)
+          for (int h = 0; h < 2; h++) {
+            const Limb a = h ? hi(y + x) : lo(y + x);
+            E.valu("v_bitop3_b32 " + VL(a) + ", " + VL(a) + ", " + VL(c[2 * ((x + 4) % 5) + h]) + ", " +
+                   VL(rr[2 * ((x + 1) % 5) + h]) + " bitop3:0x96");
+          }
+      // rho + pi along the cycle 1 -> 10 -> 7 -> ... (dst = rot(src, r)), backwards in place
+      static const int kCyc[24] = {10, 7, 11, 17, 18, 3, 5, 16, 8, 21, 24, 4, 15, 23, 19, 13, 12, 2, 20, 14, 22, 9, 6, 1};
+      static const int kRot[24] = {1, 3, 6, 10, 15, 21, 28, 36, 45, 55, 2, 14, 27, 41, 56, 8, 25, 43, 62, 18, 39, 61, 20, 44};
+      auto rot_into = [&](const Limb& dl, const Limb& dh, const Limb& sl, const Limb& sh, int n) {
+        if (n < 32) {
+          E.valu("v_alignbit_b32 " + VL(dl) + ", " + VL(sl) + ", " + VL(sh) + ", " + std::to_string(32 - n));
+          E.valu("v_alignbit_b32 " + VL(dh) + ", " + VL(sh) + ", " + VL(sl) + ", " + std::to_string(32 - n));
+        } else {
+          E.valu("v_alignbit_b32 " + VL(dl) + ", " + VL(sh) + ", " + VL(sl) + ", " + std::to_string(64 - n));
+          E.valu("v_alignbit_b32 " + VL(dh) + ", " + VL(sl) + ", " + VL(sh) + ", " + std::to_string(64 - n));
+        }
+      };
+      // dst k = kCyc[k] receives rot(src k, kRot[k]) with src 0 = lane 1, src k = kCyc[k-1]
+      E.valu("v_mov_b32_e32 " + VL(t0) + ", " + VL(lo(1)));
+      E.valu("v_mov_b32_e32 " + VL(t1) + ", " + VL(hi(1)));
+      for (int k = 23; k >= 1; k--) rot_into(lo(kCyc[k]), hi(kCyc[k]), lo(kCyc[k - 1]), hi(kCyc[k - 1]), kRot[k]);
+      rot_into(lo(kCyc[0]), hi(kCyc[0]), t0, t1, kRot[0]);
+      // chi per row: a[x] ^= ~a[x+1] & a[x+2]; b0, b1 saved
+      for (int y = 0; y < 25; y += 5)
+        for (int h = 0; h < 2; h++) {
+          auto A = [&](int x) { return h ? hi(y + x) : lo(y + x); };
+          E.valu("v_mov_b32_e32 " + VL(s0) + ", " + VL(A(0)));
+          E.valu("v_mov_b32_e32 " + VL(s1) + ", " + VL(A(1)));
+          E.valu("v_bitop3_b32 " + VL(A(0)) + ", " + VL(A(0)) + ", " + VL(A(1)) + ", " + VL(A(2)) + " bitop3:0xd2");
+          E.valu("v_bitop3_b32 " + VL(A(1)) + ", " + VL(A(1)) + ", " + VL(A(2)) + ", " + VL(A(3)) + " bitop3:0xd2");
+          E.valu("v_bitop3_b32 " + VL(A(2)) + ", " + VL(A(2)) + ", " + VL(A(3)) + ", " + VL(A(4)) + " bitop3:0xd2");
+          E.valu("v_bitop3_b32 " + VL(A(3)) + ", " + VL(A(3)) + ", " + VL(A(4)) + ", " + VL(s0) + " bitop3:0xd2");
+          E.valu("v_bitop3_b32 " + VL(A(4)) + ", " + VL(A(4)) + ", " + VL(s0) + ", " + VL(s1) + " bitop3:0xd2");
+        }
+      // iota: RC from the round's 7-bit code (bit j -> RC bit kPos[j])
+      E.salu("s_and_b32 s40, " + S(sT) + ", 0x7f", {40});
+      E.salu("s_and_b32 " + S(sR) + ", s40, 3", {sR});  // positions 0 and 1
+      for (int j = 2; j < 6; j++) {
+        E.salu("s_and_b32 s41, s40, " + imm(1u << j), {41});
+        E.salu("s_lshl_b32 s41, s41, " + std::to_string(kPos[j] - j), {41});
+        E.salu("s_or_b32 " + S(sR) + ", " + S(sR) + ", s41", {sR});
+      }
+      E.salu("s_and_b32 s41, s40, 64", {41});
+      E.salu("s_lshl_b32 " + S(sR + 1) + ", s41, 25", {sR + 1});
+      E.valu("v_xor_b32_e32 " + VL(lo(0)) + ", " + S(sR) + ", " + VL(lo(0)));
+      E.valu("v_xor_b32_e32 " + VL(hi(0)) + ", " + S(sR + 1) + ", " + VL(hi(0)));
+      E.salu("s_lshr_b64 " + SP(sT) + ", " + SP(sT) + ", 7", {sT, sT + 1});
+      E.salu("s_add_u32 " + S(sK) + ", " + S(sK) + ", -1", {sK});
+      E.salu("s_cmp_lg_u32 " + S(sK) + ", 0");
+      E.ctl("s_cbranch_scc1 " + loop);
+    }
+    drop_all(c);
+    drop_all(rr);
+    drop(t0);
+    drop(t1);
+    drop(s0);
+    drop(s1);
+    sfree(sT);
+    sfree(sK);
+    sfree(sR);
+  }
+  std::vector<Limb> keccak(const std::vector<Limb>& v, uint32_t w, uint32_t nbytes) {
+    const uint32_t nblk = nbytes / 136 + 1;
+    std::vector<Limb> st(50);
+    // the big-endian chunk of the value starting at message byte m, as the little-endian word of
+    // the sponge (bytes m .. m+3); bytes past the value are zero
+    auto word_at = [&](uint32_t m) -> Limb {
+      if (m >= nbytes) return Lit(0);
+      const int64_t p = 8 * ((int64_t)nbytes - (int64_t)m - 4);  // value bit of the chunk's low byte
+      Limb f;
+      if (p >= 0) {
+        f = bits(v, w, (uint32_t)p, 32);
+      } else {
+        const uint32_t nb = (uint32_t)(nbytes - m);  // 1..3 valid bytes, the chunk's top bytes
+        const Limb g = bits(v, w, 0, 8 * nb);
+        if (g.lit()) {
+          f = Lit(g.v << (32 - 8 * nb));
+        } else {
+          f = fresh();
+          E.valu("v_lshlrev_b32_e32 " + VL(f) + ", " + std::to_string(32 - 8 * nb) + ", " + VL(g));
+        }
+        drop(g);
+      }
+      if (f.lit()) return Lit(bswap32(f.v));
+      const Limb d = fresh();
+      E.salu("s_mov_b32 s41, 0x10203", {41});
+      E.valu("v_perm_b32 " + VL(d) + ", " + VL(f) + ", " + VL(f) + ", s41", {41});
+      drop(f);
+      return d;
+    };
+    for (uint32_t blk = 0; blk < nblk; blk++) {
+      for (uint32_t h = 0; h < 34; h++) {
+        const uint32_t m = blk * 136 + 4 * h;
+        Limb x = word_at(m);
+        uint32_t pad = 0;
+        for (uint32_t k = 0; k < 4; k++) {
+          if (m + k == nbytes) pad |= 0x01u << (8 * k);
+          if (m + k == nblk * 136 - 1) pad |= 0x80u << (8 * k);
+        }
+        if (pad) {
+          if (x.lit()) {
+            x = Lit(x.v ^ pad);
+          } else {
+            const Limb d = fresh();
+            if (inl(pad)) E.valu("v_xor_b32_e32 " + VL(d) + ", " + imm(pad) + ", " + VL(x));
+            else E.valu("v_xor_b32_e32 " + VL(d) + ", " + hexs(pad) + ", " + VL(x));
+            drop(x);
+            x = d;
+          }
+        }
+        if (blk == 0) {
+          st[h] = fresh();
+          E.valu("v_mov_b32_e32 " + VL(st[h]) + ", " + src(x));
+        } else if (!(x.lit() && x.v == 0)) {
+          if (x.lit() && !inl(x.v)) E.valu("v_xor_b32_e32 " + VL(st[h]) + ", " + hexs(x.v) + ", " + VL(st[h]));
+          else E.valu("v_xor_b32_e32 " + VL(st[h]) + ", " + src(x) + ", " + VL(st[h]));
+        }
+        drop(x);
+      }
+      if (blk == 0)
+        for (uint32_t h = 34; h < 50; h++) {
+          st[h] = fresh();
+          E.valu("v_mov_b32_e32 " + VL(st[h]) + ", 0");
+        }
+      keccak_f1600(st);
+    }
+    // digest: value limb j = bswap(state half 7 - j)
+    std::vector<Limb> out(8);
+    E.salu("s_mov_b32 s41, 0x10203", {41});
+    for (uint32_t j = 0; j < 8; j++) {
+      out[j] = fresh();
+      E.valu("v_perm_b32 " + VL(out[j]) + ", " + VL(st[7 - j]) + ", " + VL(st[7 - j]) + ", s41", {41});
+    }
+    drop_all(st);
+    return out;
+  }
+
   void emit(const Instr& in, size_t k, const std::string& next) {
     const uint32_t d = in.dst, W = in.wd, Ld = Lw(W);
     switch (in.op) {
@@ -1901,7 +2648,57 @@ struct Gen {
         for (auto& t : acc) drop(t);
         break;
       }
+      case K_SHL: case K_LSHR: case K_ASHR: {
+        if (!need[d]) {
+          set(d, std::vector<Limb>(Ld));
+          break;
+        }
+        std::vector<Limb> r = shift_var(in.op, limbs(in.a, Ld), in.b, W);
+        set(d, r);
+        break;
+      }
+      case K_SDIV: case K_SREM: case K_SMOD: {
+        if (!need[d]) {
+          set(d, std::vector<Limb>(Ld));
+          break;
+        }
+        set(d, sdivrem(in.op, limbs(in.a, Ld), limbs(in.b, Ld), W));
+        break;
+      }
+      case K_EXP: {
+        if (!need[d]) {
+          set(d, std::vector<Limb>(Ld));
+          break;
+        }
+        set(d, exp_var(limbs(in.a, Ld), limbs(in.b, Ld), W));
+        break;
+      }
+      case K_KECCAK: {
+        if (!need[d]) {
+          set(d, std::vector<Limb>(Ld));
+          break;
+        }
+        set(d, keccak(in.a == MG_NONE ? std::vector<Limb>() : limbs(in.a, L(in.a)),
+                      in.a == MG_NONE ? 0u : P.vwidth[in.a], in.p0));
+        break;
+      }
       case K_UDIV: case K_UREM: {
+        if (!need[d]) {
+          set(d, std::vector<Limb>(Ld));
+          break;
+        }
+        if (!lit_divisor(in.b, Ld)) {
+          std::vector<Limb> q, r;
+          udivrem(limbs(in.a, Ld), limbs(in.b, Ld), W, q, r);
+          if (in.op == K_UDIV) {
+            drop_all(r);
+            set(d, q);
+          } else {
+            drop_all(q);
+            set(d, r);
+          }
+          break;
+        }
         const uint32_t dv = P.consts[def_of(in.b)->p0];
         std::vector<Limb> x = limbs(in.a, Ld), r(Ld, Lit(0));
         if (dv == 0) {  // SMT-LIB: x / 0 = ~0 (to the width), x % 0 = x

@@ -258,6 +258,10 @@ Module parse(const std::string& text) {
           const std::string s = md.substr(9);
           if (s == "WORD_1") ins.sdwa_src1_word1 = 1;
           else if (s != "DWORD") err("unsupported sdwa select " + ins.text);
+        } else if (md.rfind("bitop3:", 0) == 0) {
+          int64_t v;
+          if (!parse_int(md.substr(7), v) || v < 0 || v > 255) err("bad bitop3 table " + ins.text);
+          ins.bitop3 = (int)v;
         } else if (md == "dst_sel:DWORD" || md == "dst_unused:UNUSED_PAD" || md == "src0_sel:DWORD") {
         } else {
           err("unsupported modifier '" + md + "' in " + ins.text);
@@ -1071,12 +1075,12 @@ bool step(Wave& w, Ctx& c) {
       break;
     }
     case OP_v_bitop3_b32: {
-      // v_bitop3_b32 d, a, b, c bitop3:0xNN (the table as a fourth operand here)
-      need(5);
+      // v_bitop3_b32 d, a, b, c bitop3:0xNN: bit i of d is table[(a_i << 2) | (b_i << 1) | c_i]
+      need(4);
       const Src x = vsrc(w, c, in, a[1], false, vc, true), y = vsrc(w, c, in, a[2], false, vc, true),
                 z = vsrc(w, c, in, a[3], false, vc, true);
-      if (a[4].k != O_IMM) fail(w, c, in, "bitop3 table");
-      const uint32_t t = (uint32_t)a[4].imm & 0xFF;
+      if (in.bitop3 < 0) fail(w, c, in, "bitop3 without a table");
+      const uint32_t t = (uint32_t)in.bitop3;
       uint32_t* d = vdst(w, c, in, a[0]);
       lanes([&](int l) { d[l] = bitop3(x.lo(l), y.lo(l), z.lo(l), t); });
       break;

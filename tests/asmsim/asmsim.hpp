@@ -43,6 +43,7 @@ struct Ins {
   int vmcnt = -1, lgkmcnt = -1;  // s_waitcnt
   int sdwa_src1_word1 = 0;
   int enc = 0;          // 0 VOP3-only / none, 1 _e32, 2 _e64, 3 _sdwa
+  int bitop3 = -1;      // v_bitop3_b32's table
   int target = -1;      // branch target (instruction index)
   std::string text;     // the source line (diagnostics)
 };

@@ -100,6 +100,7 @@ std::string check_search(uint64_t rec, const std::vector<uint8_t>& prog, const s
   }
   if (rc == MG_E_UNSUPPORTED) {
     C.outside++;
+    if (getenv("ASMSIM_WHY")) fprintf(stderr, "outside the tier: %s\n", err.c_str());
     return "";
   }
   if (rc) return "jit_asm_source: " + err;
@@ -231,6 +232,7 @@ std::string check_eval(const std::vector<uint8_t>& prog, uint64_t seed, uint32_t
   const int rc = jit_asm_source(sp, {}, {}, JIT_EVAL | (tiled ? JIT_EVAL_TILED : 0u), src, err);
   if (rc == MG_E_UNSUPPORTED) {
     C.outside++;
+    if (getenv("ASMSIM_WHY")) fprintf(stderr, "outside the tier: %s\n", err.c_str());
     return "";
   }
   if (rc) return "jit_asm_source: " + err;

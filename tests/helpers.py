@@ -273,8 +273,8 @@ def random_tier_program(seed: int, n_ops: int = 36, full: bool = False):
         a, b = rng.choice(src), rng.choice(src)
         if full and kind < 0.12:
             op = rng.choice(_FULL_BIN)
-            t = T.bvbin(op, a, b) if w <= 512 else T.bvbin("bvadd", a, b)
-            if op in ("bvshl", "bvlshr", "bvashr") and rng.random() < 0.6:  # shift amounts that matter
+            t = T.bvbin(op, a, b) if w <= 256 else T.bvbin("bvadd", a, b)  # the lowering's bound
+            if w <= 256 and op in ("bvshl", "bvlshr", "bvashr") and rng.random() < 0.6:  # amounts that matter
                 t = T.bvbin(op, a, T.bvbin("bvand", b, T.BitVecVal(rng.choice([7, 63, 255, 511]), w)))
         elif full and kind < 0.16:
             t = T.bvexp(a, T.bvbin("bvand", b, T.BitVecVal(rng.choice([3, 15, 255]), w))) if w == 256 else a

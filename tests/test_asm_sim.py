@@ -140,12 +140,14 @@ def run_sim(exe: Path, records: bytes, env_extra=None, timeout=1500):
 
 
 def _fuzz_records(lo: int, hi: int, full: bool = False) -> bytes:
+    """LASER-shaped queries ``lo .. hi`` as search records (``full``: with symbolic division,
+    signed division / remainder, variable shifts, EXP and concrete Keccak)."""
     from mythril_amd import search
     from tests.lasergen import laser_query
 
     recs = []
     for s in range(lo, hi):
-        roots = laser_query(s, full=full)
+        roots = laser_query(s + (500_000 if full else 0), full=full)
         P, blob = search.prepare(roots)
         rng = random.Random(s * 7919 + 1)
         start = rng.getrandbits(63)
@@ -200,12 +202,13 @@ def test_asm_tier_laser_fuzz_under_asan(sim, sim_asan):
 
 
 def _tier_records(lo, hi, full=False) -> bytes:
+    """Random programs over the tier's operators as search + eval records."""
     from mythril_amd import search
     from tests.helpers import random_tier_program
 
     recs = []
     for s in range(lo, hi):
-        roots = random_tier_program(10_000 + s, full=full)
+        roots = random_tier_program(10_000 + s + (500_000 if full else 0), full=full)
         P, blob = search.prepare(roots)
         rng = random.Random(s)
         recs.append(record(0, P.to_bytes(), blob, rng.getrandbits(32), rng.getrandbits(63), 192))
@@ -267,6 +270,33 @@ def test_asm_tier_workloads_sim(sim):
     # sha3_keyed_mapping (Keccak, EXP, SDIV) is the one workload outside the tier today
     assert int(summary["ok"]) + int(summary["outside"]) == len(recs)
     assert int(summary["ok"]) >= len(recs) - 5
+
+
+def _full_worker(args):
+    exe, lo, hi, cfg, kind = args
+    recs = _fuzz_records(lo, hi, full=True) if kind == "laser" else _tier_records(lo, hi, full=True)
+    rc, summary, bad, err = run_sim(Path(exe), recs, dict(CONFIGS[cfg], MYTHGPU_JIT_ASM_CHECK="1"))
+    return rc, summary, bad[:5], err[-3000:], cfg
+
+
+def test_asm_tier_full_vocabulary_sim(sim):
+    """Round 5's vocabulary in the tier — symbolic UDIV/UREM, SDIV/SREM/SMOD, variable SHL/LSHR/ASHR,
+    EXP and Keccak-256 (one and several blocks) — per candidate equal to the C port on LASER-shaped
+    queries (``lasergen.laser_query(full=True)``) and random programs (search, gen and eval kernels)."""
+    n_l = int(os.environ.get("MYTHGPU_SIMFUZZ_FULL_N", "1000"))
+    n_t = n_l // 2
+    tasks = []
+    step = max(1, n_l // (WORKERS * 2))
+    tasks += [(str(sim), lo, min(n_l, lo + step), (lo // step) % len(CONFIGS), "laser") for lo in range(0, n_l, step)]
+    step = max(1, n_t // WORKERS)
+    tasks += [(str(sim), lo, min(n_t, lo + step), (lo // step) % len(CONFIGS), "tier") for lo in range(0, n_t, step)]
+    with mp.get_context("fork").Pool(WORKERS) as pool:
+        results = pool.map(_full_worker, tasks, chunksize=1)
+    total = _check(results, n_l + 2 * n_t)
+    print("full vocabulary:", total)
+    # a refusal is a fall-back (the interpreter keeps the query), never a wrong verdict; one
+    # program in ~2,000 keeps too many 256-bit values live around an EXP or Keccak (out of VGPRs)
+    assert total["ok"] >= 0.995 * (n_l + 2 * n_t), total
 
 
 def _mutants(tmp_path: Path, mutants) -> dict:

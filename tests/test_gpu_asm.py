@@ -25,7 +25,7 @@ from mythril_amd.smt import terms as T
 pytestmark = pytest.mark.gpu
 
 N = 2048
-OUTSIDE = {"sha3_keyed_mapping"}  # Keccak, EXP, SDIV
+OUTSIDE = set()  # since round 5 the tier takes Keccak, EXP, signed / symbolic division and variable shifts
 
 
 def _windows(rng, k=4):
@@ -81,21 +81,22 @@ def test_asm_tier_verdicts(engine, name):
     _check(engine, name, _queries()[name]())
 
 
-def _random_program(seed: int, n_ops: int = 36):
+def _random_program(seed: int, n_ops: int = 36, full: bool = False):
     from tests.helpers import random_tier_program
 
-    return random_tier_program(seed, n_ops)
+    return random_tier_program(seed, n_ops, full=full)
 
 
-@pytest.mark.parametrize("seed", range(24))
-def test_asm_tier_random_programs(engine, seed):
-    roots = _random_program(1000 + seed)
-    P, blob = search.prepare(roots)
-    try:
-        native.jit_asm(P.to_bytes(), blob)
-    except native.EngineUnsupported as e:
-        pytest.skip(f"outside the tier: {e}")
-    _check(engine, f"random{seed}", roots, seeds=1, windows=3)
+# 200 random programs (8 chunks of 25), every other one over the full vocabulary (symbolic
+# division and remainders, signed division, variable shifts, EXP, Keccak)
+@pytest.mark.parametrize("chunk", range(8))
+def test_asm_tier_random_programs(engine, chunk):
+    for k in range(25):
+        seed = 1000 + 25 * chunk + k
+        roots = _random_program(seed, full=bool(k & 1))
+        P, blob = search.prepare(roots)
+        native.jit_asm(P.to_bytes(), blob)  # inside the tier (raises otherwise)
+        _check(engine, f"random{seed}", roots, seeds=1, windows=2)
 
 
 def test_asm_tier_first_hit_from_zero(engine):
@@ -150,32 +151,25 @@ def test_asm_tier_hard_needle_full_size(engine):
 # ---------------------------------------------------------------------------------------------
 # the first tier's eval kernel (mgj_eval from jit_asm.cpp): explicit SoA coordinates, watch rows
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("seed", range(16))
-def test_asm_eval_random_programs_terms(engine, seed):
-    _eval_terms(engine, seed, tiled=False)
+# model read-back on the tier's eval kernel: 200 random programs (8 chunks of 25), watch rows
+@pytest.mark.parametrize("chunk", range(8))
+def test_asm_eval_random_programs_terms(engine, chunk):
+    for k in range(25):
+        _eval_terms(engine, 25 * chunk + k, tiled=bool(k % 3 == 0), n=48, full=bool(k & 1))
 
 
-@pytest.mark.parametrize("seed", range(0, 16, 3))
-def test_asm_eval_random_programs_terms_tiled(engine, seed):
-    """The same on the tiled SoA (MG_JIT_SOA_TILED): watch rows and verdicts unchanged."""
-    _eval_terms(engine, seed, tiled=True)
-
-
-def _eval_terms(engine, seed, tiled):
+def _eval_terms(engine, seed, tiled, n=200, full=False):
     """``Model.eval`` batched on the first tier's eval kernel: every watched term's value and every
     verdict equal the Python oracle's on edge-value assignments (``oracle/bv.py``, the reference's
     ``model.eval(..., model_completion=True)``), as the O3 eval kernel's do."""
     from tests.helpers import gpu_eval_terms
     from oracle.bv import evaluate_many
 
-    roots = _random_program(3000 + seed)
+    roots = _random_program(3000 + seed, full=full)
     P0, _ = search.prepare(roots)
-    try:
-        native.jit_asm(P0.to_bytes(), None)
-    except native.EngineUnsupported as e:
-        pytest.skip(f"outside the tier: {e}")
+    native.jit_asm(P0.to_bytes(), None)  # inside the tier (raises otherwise)
     watch = [t for t in T.postorder(roots) if t.sort[0] == "bv"][:24]
-    P, assigns, ver, vals, models = gpu_eval_terms(engine, roots, watch, n=200, seed=seed, asm=True, tiled=tiled)
+    P, assigns, ver, vals, models = gpu_eval_terms(engine, roots, watch, n=n, seed=seed, asm=True, tiled=tiled)
     for i, m in enumerate(models):
         want = evaluate_many(list(roots) + watch, m)
         assert ver[i] == int(all(want[:len(roots)])), (seed, i)
