@@ -280,7 +280,7 @@ def main():
     # timing, "warm" finds it in the code cache (the same query asked again)
     hard = None
     if rank == 0 and not args.no_ttfm:
-        hroots = hard_query(cs)
+        hroots = hard_query(cs, HARD_BITS.get(args.workload, 24))
         search.FLATTEN_CACHE = ssa.FlattenCache(aux_words=True)
         search._GEN_CACHE.clear()
         eng.cache_clear()
@@ -295,7 +295,8 @@ def main():
             if label == "cold":
                 hard["jit_compile_ms"] = rh.timing.get("jit_compile_ms")
             hard[f"{label}_timing"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in rh.timing.items()}
-        hard["needle"] = "Extract(23, 0, x * K) == C on a fresh 256-bit symbol x (~2^-24 per candidate)"
+        hb = HARD_BITS.get(args.workload, 24)
+        hard["needle"] = f"Extract({hb - 1}, 0, x * K) == C on a fresh 256-bit symbol x (~2^-{hb} per candidate)"
 
     # time to first model on ALL ranks: the compiled kernel sweeps epochs of `chunk` candidates per
     # rank from index 0, one all-reduce(MIN) per epoch (distributed.sharded_first_hit); the index found
@@ -512,16 +513,22 @@ def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5, asm=False, tiled=Fal
     return out
 
 
-def hard_query(cs):
-    """The workload's constraints plus a ~2^-24 needle: ``Extract(23, 0, x * K) == C`` on a fresh
-    256-bit symbol ``x`` (a path symbol would inherit the generator's dictionaries, which may
-    never reach the needle), so about one candidate in 2^24 of the workload's satisfying ones
+# needle bits of the hard query per workload: 24 (~2^-24) on top of the C1-C4 queries, which their
+# generators satisfy often; C5 itself holds about 1 candidate in 2^17, so its needle
+# is 8 bits: ~2^25 candidates to the first model either way
+HARD_BITS = {"sha3_keyed_mapping": 8}
+
+
+def hard_query(cs, bits: int = 24):
+    """The workload's constraints plus a ~2^-bits needle: ``Extract(bits-1, 0, x * K) == C`` on a
+    fresh 256-bit symbol ``x`` (a path symbol would inherit the generator's dictionaries, which may
+    never reach the needle), so about one candidate in 2^bits of the workload's satisfying ones
     satisfies the query."""
     from mythril_amd.smt import Extract, symbol_factory
 
     x = symbol_factory.BitVecSym("hard_x", 256)
     k = symbol_factory.BitVecVal(0x9E3779B97F4A7C15F39CC0605CEDC835, 256)
-    needle = Extract(23, 0, x * k) == symbol_factory.BitVecVal(0xA5C3E1, 24)
+    needle = Extract(bits - 1, 0, x * k) == symbol_factory.BitVecVal(0xA5C3E1 & ((1 << bits) - 1), bits)
     return [c.raw for c in cs] + [needle.raw]
 
 

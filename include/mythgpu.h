@@ -194,6 +194,10 @@ enum mg_gen_kind {
 
 /* search flags */
 #define MG_SEARCH_EARLY_EXIT 1u   /* stop lanes past the current first hit; skip waves whose roots all failed */
+/* set by the engine itself (callers need not): the launch's first-hit word may be lowered by waves on
+ * ANOTHER physical GPU (an in-process search split over devices), so kernels read it with system
+ * scope (gfx950: global_load ... sc0 sc1) instead of agent scope (sc1) */
+#define MG_SEARCH_SYSTEM_SCOPE 2u
 
 typedef struct mg_program_info {
   uint32_t n_nodes, n_instrs, n_coords, n_roots;
@@ -301,8 +305,11 @@ int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle);
 /* flags: MG_JIT_GEN_VERDICTS also builds mgj_gen (per-candidate verdicts, mg_jit_verdicts);
  * MG_JIT_ASM builds the first tier instead: the same kernels emitted as gfx950 assembly with the
  * engine's own register allocation, assembled and linked in a few ms (clang + LLVM take ~140 ms);
- * MG_E_UNSUPPORTED for programs outside it (division other than by a literal of at most 32 bits,
- * EXP, Keccak, variable shifts).
+ * MG_E_UNSUPPORTED for the rare program outside it (too many live 256-bit values for the VGPRs).
+ * An eval kernel WITH watch rows (model read-back, batched term evaluation) is the first tier's by
+ * default — no SGPR spills by construction (the O3 kernel's row stores spill) — and the O3 kernel
+ * only when the first tier refuses the program; MG_JIT_O3 asks for the O3 kernel (as does
+ * MYTHGPU_JIT_WATCH_TIER=o3).  mg_jit_info's MG_JIT_ASM bit tells which one was built.
  * MG_JIT_SOA_TILED (eval kernel, gen = 0): the kernel reads a TILED SoA — coordinate limb row r of
  * candidate i at word ((i / 64) * coord_words + r) * 64 + i % 64, so a group of 64 candidates has
  * its rows in one contiguous block (coord_words * 256 bytes) — instead of [row][candidate].  The
@@ -310,6 +317,7 @@ int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle);
 #define MG_JIT_GEN_VERDICTS 1u
 #define MG_JIT_ASM 2u
 #define MG_JIT_SOA_TILED 4u
+#define MG_JIT_O3 8u
 int mg_jit_compile_ex(uint64_t prog, uint64_t gen, uint32_t flags, uint64_t* jit_handle);
 int mg_jit_verdicts(uint64_t jit, uint64_t seed, uint64_t start, uint64_t n, uint8_t* verdict_out);
 /* Asynchronous compile on the engine's compile thread (outside the engine lock: searches on
@@ -324,6 +332,12 @@ int mg_jit_cancel(uint64_t ticket);
  * objects by source): the next query pays every pass again (cold-start measurement). */
 int mg_cache_clear(void);
 int mg_jit_info(uint64_t jit, double* compile_ms, int* blocks_per_cu);
+/* what a JIT handle was built as and the eval buffers it expects: *flags gets MG_JIT_ASM (the first
+ * tier's kernels), MG_JIT_SOA_TILED (its eval kernel reads the tiled SoA) and MG_JIT_GEN_VERDICTS
+ * (mgj_gen present); *coord_words / *watch_words the rows of the program's SoA and watch buffers, so
+ * a caller of mg_jit_eval can check its buffers (coord_words x n, or coord_words x ceil(n/64) x 64
+ * words when tiled).  Any out pointer may be null. */
+int mg_jit_layout(uint64_t jit, uint32_t* flags, uint32_t* coord_words, uint32_t* watch_words);
 int mg_jit_free(uint64_t jit);
 int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, uint32_t flags, uint64_t* first_hit,
                   uint64_t* n_hits, uint32_t* assign_out);

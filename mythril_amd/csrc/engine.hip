@@ -62,11 +62,20 @@ constexpr uint32_t kManySlots = 64;
 constexpr int kManyStreams = 4;
 static_assert(kPeerWord == 272, "jit.cpp / jit_asm.cpp hard-code the peer line at 2,176 B");
 
-// an early-exit first hit to the devices above this one (the peer line)
+// an early-exit first hit to the devices above this one (the peer line).  System scope (gfx950:
+// global_atomic_umin_x2 ... sc1): a peer's word may live on another GPU, in fine-grained memory
+// (mg_init allocates every hit buffer fine-grained when the mask spans physical devices), where the
+// atomic is performed at the owner's memory and its waves' system-scope loads see it
 __device__ __forceinline__ void publish_peers(unsigned long long* hit, unsigned long long v) {
   const unsigned long long* t = hit + kPeerWord;
   const uint32_t np = (uint32_t)t[0];
-  for (uint32_t q = 0; q < np && q < kPeerMax; q++) atomicMin((unsigned long long*)t[1 + q], v);
+  for (uint32_t q = 0; q < np && q < kPeerMax; q++)
+    __hip_atomic_fetch_min((unsigned long long*)t[1 + q], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// the launch's current first hit: agent scope, or system scope when peers on other GPUs lower it
+__device__ __forceinline__ unsigned long long read_first_hit(const unsigned long long* hit, uint32_t flags) {
+  if (flags & MG_SEARCH_SYSTEM_SCOPE) return __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 static uint32_t lds_words_max() {
@@ -909,7 +918,7 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
     if (early) {
       // every candidate below the current first hit is still evaluated, so the
       // final minimum is exact; waves entirely above it stop
-      const unsigned long long cur = __hip_atomic_load(k.first_hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long cur = read_first_hit(k.first_hit, k.flags);
       // readfirstlane returns int: widen through uint32_t, or a low word with bit 31 set would
       // sign-extend over the high word
       const uint64_t cur_u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) |
@@ -948,7 +957,7 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
     // a first hit that cannot lower the current minimum is not published; the count goes to the
     // block's stripe (kHitStripes)
     if (wave_best != ~0ull &&
-        wave_best < __hip_atomic_load(k.first_hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        wave_best < read_first_hit(k.first_hit, k.flags))
       atomicMin(k.first_hit, (unsigned long long)wave_best);
     if (wave_hits) atomicAdd(k.hits + kHitStride * (1u + (blockIdx.x % kHitStripes)) - 1u, (unsigned long long)wave_hits);
   }
@@ -1127,6 +1136,7 @@ struct JitTicket {
   std::vector<GenSpec> specs;
   std::vector<uint32_t> consts;
   bool cancelled = false;
+  bool asm_fallback = false;  // the first tier was chosen by default (watch rows): O3 if it refuses
   std::unique_ptr<DevJit> ready;  // loaded module, handed to Engine::jits by the poll
   int rc = MG_OK;
   std::string err;
@@ -1161,6 +1171,9 @@ struct Engine {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   int cu_count = 0, clock_mhz = 0;
+  // the mask spans physical devices: hit buffers are fine-grained and launches read them with
+  // system scope (MG_SEARCH_SYSTEM_SCOPE)
+  bool sys_scope = false;
   uint64_t next_handle = 1;
   std::unordered_map<uint64_t, std::unique_ptr<DevProgram>> progs;
   std::unordered_map<uint64_t, std::unique_ptr<DevGen>> gens;
@@ -1662,6 +1675,27 @@ int mg_init(uint32_t device_mask) {
   // peer lines: device d stops devices d+1.. (their slices lie above its own).  Distinct physical
   // devices need peer access (xGMI); where it cannot be enabled, that pair simply does not stop early
   if (g_devs.size() > 1) {
+    // Memory model of the stop words.  Each device's first-hit word is lowered by its own waves
+    // (agent-scope atomics) and by waves of the devices below it (the peer line).  When those are
+    // other GPUs, their atomics cross xGMI: the hit buffers are then allocated fine-grained
+    // (hipDeviceMallocFinegrained), peers publish with system-scope atomics (publish_peers; the
+    // kernels' sc1 atomics) which the owner's memory performs, and the owner's waves read the word
+    // with system-scope loads (MG_SEARCH_SYSTEM_SCOPE: sc0 sc1, which no cache level serves stale).
+    // Virtual devices on one GPU (MYTHGPU_VIRTUAL_DEVICES) keep coarse-grained buffers and agent
+    // scope.  A late or lost peer write costs only the early stop: the host takes the minimum over
+    // every device's word.
+    bool physical = false;
+    for (size_t d = 1; d < g_devs.size(); d++) physical = physical || g_devs[d]->device != g_devs[0]->device;
+    if (physical) {
+      for (Engine* de : g_devs) {
+        HIPCHK(hipSetDevice(de->device));
+        HIPCHK(hipFree(de->d_hit));
+        de->d_hit = nullptr;
+        HIPCHK(hipExtMallocWithFlags((void**)&de->d_hit, kHitAlloc * sizeof(unsigned long long), hipDeviceMallocFinegrained));
+        HIPCHK(hipMemset(de->d_hit, 0, kHitAlloc * sizeof(unsigned long long)));
+        de->sys_scope = true;
+      }
+    }
     for (size_t d = 0; d < g_devs.size(); d++) {
       std::vector<unsigned long long> line(1 + kPeerMax, 0ull);
       uint32_t np = 0;
@@ -2243,7 +2277,7 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
       k.hits = de.d_hit + 1;
       k.start = st[d];
       k.seed = seed;
-      k.flags = flags;
+      k.flags = flags | (de.sys_scope ? MG_SEARCH_SYSTEM_SCOPE : 0u);
       rc = launch_async<MODE_SEARCH>(de, dg.spec, k, ct[d]);
       if (rc == MG_OK) rc = fetch_hits(de);
     }
@@ -2648,6 +2682,11 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
     if (t->flags & MG_JIT_ASM) {
       // the first tier: assembly straight from the specialised program (jit_asm.cpp)
       asm_rc = jit_asm_source(t->low, t->specs, t->consts, kernels, src, asm_err);
+      if (asm_rc != MG_OK && t->asm_fallback) {  // chosen by default: the O3 kernel instead
+        t->flags &= ~MG_JIT_ASM;
+        asm_rc = MG_OK;
+        src = jit_source(t->low, nullptr, nullptr, kernels);
+      }
     } else {
       src = t->has_gen ? jit_source(t->low, &t->specs, &t->consts, kernels) : jit_source(t->low, nullptr, nullptr, kernels);
     }
@@ -2785,6 +2824,17 @@ static int submit_jit(Engine& e, uint64_t prog, uint64_t gen, uint32_t flags, ui
     std::string err;
     int rc = specialize_program(p->low, nullptr, nullptr, t->low, err);
     if (rc) return set_err(rc, err);
+    // watch rows (model read-back, batched term evaluation): the first tier's eval kernel stores them
+    // from the values' registers (no SGPR spills; the O3 kernel's indexed row stores spill hundreds of
+    // v_readlane / v_writelane on C4), and compiles in a few ms; O3 if the first tier refuses
+    static const bool o3_env = [] {
+      const char* w = getenv("MYTHGPU_JIT_WATCH_TIER");
+      return w && std::string(w) == "o3";
+    }();
+    if (t->low.watch_words && !(flags & (MG_JIT_ASM | MG_JIT_O3)) && !o3_env) {
+      t->flags |= MG_JIT_ASM;
+      t->asm_fallback = true;
+    }
   }
   const uint64_t h = e.next_handle++;
   std::lock_guard<std::mutex> jl(e.jit_mu);
@@ -2799,7 +2849,7 @@ static int submit_jit(Engine& e, uint64_t prog, uint64_t gen, uint32_t flags, ui
     e.jit_workers = 2;
   }
   e.tickets[h] = t;
-  e.jit_queue[(flags & MG_JIT_ASM) ? 1 : 0].push_back(t);
+  e.jit_queue[(t->flags & MG_JIT_ASM) ? 1 : 0].push_back(t);
   e.jit_cv.notify_all();
   *ticket = h;
   return MG_OK;
@@ -2886,6 +2936,21 @@ int mg_jit_info(uint64_t jit, double* compile_ms, int* blocks_per_cu) {
   return MG_OK;
 }
 
+int mg_jit_layout(uint64_t jit, uint32_t* flags, uint32_t* coord_words, uint32_t* watch_words) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  OnDevice od_(e);
+  auto it = e.jits.find(jit);
+  if (it == e.jits.end()) return set_err(MG_E_INVALID, "bad jit handle");
+  const DevJit& j = *it->second;
+  DevProgram* p = find_prog(e, j.prog);
+  if (!p) return set_err(MG_E_INVALID, "jit program was freed");
+  if (flags) *flags = (j.asm_tier ? MG_JIT_ASM : 0u) | (j.tiled ? MG_JIT_SOA_TILED : 0u) | (j.fgen ? MG_JIT_GEN_VERDICTS : 0u);
+  if (coord_words) *coord_words = p->low.coord_words;
+  if (watch_words) *watch_words = p->low.watch_words;
+  return MG_OK;
+}
+
 int mg_jit_free(uint64_t jit) {
   Engine& e = E();
   std::lock_guard<std::mutex> g(e.mu);
@@ -2942,7 +3007,7 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
       DevJit* dj = &j;
       if (d > 0 && (rc = jit_on(de, j, jit, &dj))) break;
       if ((rc = arm_hits(de))) break;
-      a[d] = A{dg.d_consts, st[d], ct[d], sk, sg, de.d_hit, flags, 0};
+      a[d] = A{dg.d_consts, st[d], ct[d], sk, sg, de.d_hit, flags | (de.sys_scope ? MG_SEARCH_SYSTEM_SCOPE : 0u), 0};
       void* args[] = {&a[d].gconsts, &a[d].start, &a[d].count, &a[d].sk, &a[d].sg, &a[d].hit, &a[d].flags, &a[d].nblk};
       const uint64_t lanes = (st[d] + ct[d]) - (st[d] & ~63ull);
       // hipModuleLaunchKernel copies the argument values at the call (nblk is set before it)

@@ -1132,7 +1132,9 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   }
   o << "  for (uint32_t kk = 0u; kk < nk; kk++, gbase += gstride << 6) {\n"
        "  if (early) {\n"
-       "    const unsigned long long cur = __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+       "    // system scope when peers on other GPUs lower this word (MG_SEARCH_SYSTEM_SCOPE, mg_init)\n"
+       "    const unsigned long long cur = (flags & 2u) ? __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)\n"
+       "                                               : __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
        "    const uint64_t cu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) | "
        "(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cur);\n"
        "    if (gbase >= cu) break;\n"
@@ -1169,7 +1171,9 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "        if (early && lane == 0u) {\n"
        "          atomicMin(hit, (unsigned long long)first);\n"
        "          const uint32_t np = (uint32_t)hit[272];\n"
-       "          for (uint32_t q = 0u; q < np && q < 15u; q++) atomicMin((unsigned long long*)hit[273u + q], (unsigned long long)first);\n"
+       "          for (uint32_t q = 0u; q < np && q < 15u; q++)\n"
+       "            __hip_atomic_fetch_min((unsigned long long*)hit[273u + q], (unsigned long long)first, __ATOMIC_RELAXED,\n"
+       "                                   __HIP_MEMORY_SCOPE_SYSTEM);\n"
        "        }\n"
        "      }\n"
        "    } }\n"

@@ -3554,7 +3554,18 @@ struct Gen {
       const std::string noearly = E.newlab();
       E.salu("s_cmp_eq_u32 s29, 0");
       E.ctl("s_cbranch_scc1 " + noearly);
-      E.mem("global_load_dwordx2 v[8:9], v6, s[16:17] sc1", {16, 17});
+      // agent scope, or system scope (sc0 sc1) when peers on other GPUs lower the word (flags bit 1,
+      // MG_SEARCH_SYSTEM_SCOPE: the engine sets it when the device mask spans physical GPUs)
+      {
+        const std::string sys = E.newlab(), got = E.newlab();
+        E.salu("s_and_b32 s40, s18, 2", {40});
+        E.ctl("s_cbranch_scc1 " + sys);
+        E.mem("global_load_dwordx2 v[8:9], v6, s[16:17] sc1", {16, 17});
+        E.ctl("s_branch " + got);
+        E.label(sys);
+        E.mem("global_load_dwordx2 v[8:9], v6, s[16:17] sc0 sc1", {16, 17});
+        E.label(got);
+      }
       E.ctl("s_waitcnt vmcnt(0)");
       E.valu("v_readfirstlane_b32 s40, v8", {}, {40});
       E.valu("v_readfirstlane_b32 s41, v9", {}, {41});
@@ -3661,7 +3672,7 @@ struct Gen {
         E.valu("v_readfirstlane_b32 s51, v9", {}, {51});
         E.valu("v_mov_b32_e32 v8, s46", {46});
         E.valu("v_mov_b32_e32 v9, s47", {47});
-        E.mem("global_atomic_umin_x2 v6, v[8:9], s[50:51]", {50, 51});
+        E.mem("global_atomic_umin_x2 v6, v[8:9], s[50:51] sc1", {50, 51});  // system scope: a peer GPU's word
         E.salu("s_add_u32 s49, s49, 1", {49});
         E.salu("s_cmp_lt_u32 s49, s48");
         E.ctl("s_cbranch_scc1 " + ploop);

@@ -29,6 +29,7 @@ MG_SEARCH_EARLY_EXIT = 1
 MG_JIT_GEN_VERDICTS = 1
 MG_JIT_ASM = 2  # the first tier: gfx950 assembly emitted by the engine (jit_asm.cpp)
 MG_JIT_SOA_TILED = 4  # eval kernels read the tiled SoA (tile_soa)
+MG_JIT_O3 = 8  # the O3 eval kernel even with watch rows (the first tier's is the default there)
 
 
 def tile_soa(soa):
@@ -51,7 +52,7 @@ EXPORTS = [
     "mg_program_specialized", "mg_program_load",
     "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_info", "mg_gen_free", "mg_eval", "mg_eval_dev",
     "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
-    "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_program_jit_asm", "mg_jit_compile", "mg_jit_compile_ex", "mg_jit_verdicts", "mg_jit_info",
+    "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_program_jit_asm", "mg_jit_compile", "mg_jit_compile_ex", "mg_jit_verdicts", "mg_jit_info", "mg_jit_layout",
     "mg_jit_compile_async", "mg_jit_poll", "mg_jit_cancel", "mg_jit_helper_pid", "mg_cache_clear", "mg_split_range",
     "mg_jit_free", "mg_jit_search", "mg_jit_search_many", "mg_jit_eval", "mg_jit_eval_dev",
 ]
@@ -144,6 +145,7 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_jit_compile_ex": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, u64p]),
             "mg_jit_verdicts": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, u8p]),
             "mg_jit_info": (C.c_int, [C.c_uint64, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+            "mg_jit_layout": (C.c_int, [C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
             "mg_jit_compile_async": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, u64p]),
             "mg_jit_poll": (C.c_int, [C.c_uint64, C.c_int32, u64p]),
             "mg_jit_cancel": (C.c_int, [C.c_uint64]),
@@ -385,11 +387,13 @@ class Engine:
 
     # JIT-specialised kernels --------------------------------------
     def jit_compile(self, prog: int, gen: int = 0, gen_verdicts: bool = False, asm: bool = False,
-                    tiled: bool = False) -> int:
+                    tiled: bool = False, o3: bool = False) -> int:
         """``asm``: the first tier (assembly emitted by the engine).  ``tiled`` (eval kernels): the
-        kernel reads the tiled SoA (:func:`tile_soa`; MG_JIT_SOA_TILED in mythgpu.h)."""
+        kernel reads the tiled SoA (:func:`tile_soa`; MG_JIT_SOA_TILED in mythgpu.h).  An eval kernel
+        with watch rows is the first tier's unless ``o3`` (MG_JIT_O3)."""
         h = C.c_uint64()
-        flags = (MG_JIT_GEN_VERDICTS if gen_verdicts else 0) | (MG_JIT_ASM if asm else 0) | (MG_JIT_SOA_TILED if tiled else 0)
+        flags = (MG_JIT_GEN_VERDICTS if gen_verdicts else 0) | (MG_JIT_ASM if asm else 0) | \
+            (MG_JIT_SOA_TILED if tiled else 0) | (MG_JIT_O3 if o3 else 0)
         _check(self.lib.mg_jit_compile_ex(prog, gen, flags, C.byref(h)))
         return h.value
 
@@ -425,6 +429,13 @@ class Engine:
         _check(self.lib.mg_jit_info(jit, C.byref(ms), C.byref(nb)))
         return ms.value, nb.value
 
+    def jit_layout(self, jit: int):
+        """(flags, coord_words, watch_words) of a JIT handle (mg_jit_layout): flags has MG_JIT_ASM for the
+        first tier's kernels, MG_JIT_SOA_TILED for an eval kernel that reads the tiled SoA."""
+        f, cw, ww = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        _check(self.lib.mg_jit_layout(jit, C.byref(f), C.byref(cw), C.byref(ww)))
+        return f.value, cw.value, ww.value
+
     def jit_free(self, jit: int):
         _check(self.lib.mg_jit_free(jit))
 
@@ -453,7 +464,21 @@ class Engine:
         return [(None if int(f) == NO_HIT else int(f), int(h)) for f, h in zip(fh, nh)]
 
     def jit_eval(self, jit: int, soa: np.ndarray, n: int, watch_words: int = 0):
+        """Verdicts (and watch rows) of n explicit candidates.  The SoA is checked against the kernel's
+        layout first: [coord_words][n] row-major, or tile_soa's (blocks, coord_words, 64) for a kernel
+        compiled ``tiled`` — mg_jit_eval copies coord_words x n (tiled: x ceil(n/64) x 64) words from it."""
+        flags, cw, _ = self.jit_layout(jit)
+        if flags & MG_JIT_SOA_TILED:
+            blocks = (n + 63) // 64
+            if getattr(soa, "ndim", 0) != 3 or tuple(soa.shape[1:]) != (cw, 64) or soa.shape[0] < blocks:
+                raise ValueError(f"tiled eval kernel: expected the tiled SoA ({blocks}, {cw}, 64) of tile_soa, "
+                                 f"got shape {getattr(soa, 'shape', None)}")
+        elif cw and (getattr(soa, "ndim", 0) != 2 or soa.shape[0] != cw or soa.shape[1] < n):
+            raise ValueError(f"eval kernel: expected the [row][candidate] SoA ({cw}, {n}), got shape "
+                             f"{getattr(soa, 'shape', None)}")
         soa = np.ascontiguousarray(soa, dtype=np.uint32)
+        if soa.shape[-1] != n and not (flags & MG_JIT_SOA_TILED):
+            soa = np.ascontiguousarray(soa[:, :n])
         ver = np.zeros(n, dtype=np.uint8)
         watch = np.zeros((max(watch_words, 1), n), dtype=np.uint32) if watch_words else None
         _check(self.lib.mg_jit_eval(jit, _ptr(soa, C.c_uint32), n, _ptr(ver, C.c_uint8),

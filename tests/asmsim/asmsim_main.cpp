@@ -185,7 +185,9 @@ std::string check_search(uint64_t rec, const std::vector<uint8_t>& prog, const s
       put64(ka, 24, sk);
       put64(ka, 32, sg);
       put64(ka, 40, h);
-      put32(ka, 48, early ? 1u : 0u);
+      // the early-exit pass reads the hit word with agent scope on even records and with system scope
+      // (MG_SEARCH_SYSTEM_SCOPE, a device mask spanning GPUs) on odd ones
+      put32(ka, 48, early ? ((rec & 1) ? 3u : 1u) : 0u);
       put32(ka, 52, nblk);
       const uint64_t kb = mem.add(ka.size(), ka.data());
       asmsim::launch(m, "mgj_search", mem, kb, nblk, early ? nullptr : &st);
@@ -218,7 +220,6 @@ std::string check_search(uint64_t rec, const std::vector<uint8_t>& prog, const s
   }
   C.valu += st.valu;
   C.cand += count;
-  (void)rec;
   return "";
 }
 

@@ -178,10 +178,10 @@ def lift_literals(terms: Sequence[T.Term], min_width: int = 8):
 
 
 def gpu_eval_terms(engine, roots: Sequence[T.Term], watch_terms: Sequence[T.Term], assigns=None, n=64, seed=0,
-                   jit: bool = False, asm: bool = False, tiled: bool = False):
-    """Evaluate on the GPU (the interpreter, or with ``jit`` the hipRTC-specialised eval kernel
-    on the same runtime SoA inputs); returns (P, assigns, verdicts, per-candidate dict
-    term-id -> value, per-candidate oracle models)."""
+                   jit: bool = False, asm: bool = False, tiled: bool = False, o3: bool = False):
+    """Evaluate on the GPU (the interpreter, or with ``jit`` the compiled eval kernel on the same
+    runtime SoA inputs: with watch rows the first tier's by default, ``o3`` the O3 kernel); returns
+    (P, assigns, verdicts, per-candidate dict term-id -> value, per-candidate oracle models)."""
     P = ssa.flatten(list(roots), extra=list(watch_terms))
     # watch every requested term that the program contains, plus the model read-back entries
     from mythril_amd.search import model_watch
@@ -201,7 +201,7 @@ def gpu_eval_terms(engine, roots: Sequence[T.Term], watch_terms: Sequence[T.Term
     try:
         info = engine.info(prog)
         if jit or asm:
-            jh = engine.jit_compile(prog, 0, asm=asm, tiled=tiled)
+            jh = engine.jit_compile(prog, 0, asm=asm, tiled=tiled, o3=o3)
             try:
                 from mythril_amd.native import tile_soa
 

@@ -14,13 +14,15 @@ from oracle.bv import OracleModel, evaluate
 pytestmark = pytest.mark.gpu
 
 
-def _eval_both(engine, P, assigns):
+def _eval_both(engine, P, assigns, o3=False):
+    """The interpreter's and a compiled eval kernel's verdicts and watch rows on the same SoA (with
+    watch rows the compiled kernel is the first tier's by default, ``o3``: the O3 kernel)."""
     soa = ssa.soa_from_assignments(P, assigns)
     prog = engine.load(P.to_bytes())
     try:
         info = engine.info(prog)
         v_i, w_i = engine.eval(prog, soa, len(assigns), watch_words=info.watch_words)
-        jit = engine.jit_compile(prog, 0)
+        jit = engine.jit_compile(prog, 0, o3=o3)
         try:
             v_j, w_j = engine.jit_eval(jit, soa, len(assigns), watch_words=info.watch_words)
         finally:
@@ -30,8 +32,9 @@ def _eval_both(engine, P, assigns):
     return v_i, w_i, v_j, w_j
 
 
+@pytest.mark.parametrize("o3", [False, True], ids=["default", "o3"])
 @pytest.mark.parametrize("seed", range(6))
-def test_jit_eval_matches_interpreter_random_dags(engine, seed):
+def test_jit_eval_matches_interpreter_random_dags(engine, seed, o3):
     rp = RandomProgram(500 + seed, n_ops=60)
     P = ssa.flatten([rp.root], extra=rp.terms)
     from mythril_amd.search import model_watch
@@ -152,12 +155,14 @@ def test_jit_narrow_widths_runtime_operands(engine):
 def test_jit_vmtests_literals_as_runtime_inputs(engine):
     """VMTests replay programs through the JIT eval kernel with every PUSH literal lifted
     into a runtime coordinate (tests/laser/evm_testsuite/evm_test.py:109-188 post-states):
-    this checks the kernel's arithmetic, not hipRTC's constant folder."""
+    this checks the kernel's arithmetic, not hipRTC's constant folder.  Every vector on the default
+    watch-row kernel (the first tier's since round 5: EXP, Keccak, signed and symbolic division,
+    variable shifts included) and every sixth also on the O3 kernel (MG_JIT_O3)."""
     from helpers import lift_literals
 
     cases = vmtest_cases()
     checked = 0
-    for name, v, r in cases:
+    for ci, (name, v, r) in enumerate(cases):
         keys = [int(k, 16) for k in v["post_storage"]]
         if not keys:
             continue
@@ -179,18 +184,22 @@ def test_jit_vmtests_literals_as_runtime_inputs(engine):
         prog = engine.load(P.to_bytes())
         try:
             info = engine.info(prog)
-            jh = engine.jit_compile(prog, 0)
-            try:
-                _, w_j = engine.jit_eval(jh, soa, 1, watch_words=info.watch_words)
-            finally:
-                engine.jit_free(jh)
+            outs = []
+            for o3 in ((False, True) if ci % 6 == 0 else (False,)):
+                jh = engine.jit_compile(prog, 0, o3=o3)
+                try:
+                    _, w_j = engine.jit_eval(jh, soa, 1, watch_words=info.watch_words)
+                finally:
+                    engine.jit_free(jh)
+                outs.append(w_j)
         finally:
             engine.free(prog)
-        row = 0
-        for k, x in v["post_storage"].items():
-            assert ssa.limbs_to_int(w_j[row:row + 8, 0]) == int(x, 16), (name, k)
-            row += 8
-            checked += 1
+        for w_j in outs:
+            row = 0
+            for k, x in v["post_storage"].items():
+                assert ssa.limbs_to_int(w_j[row:row + 8, 0]) == int(x, 16), (name, k)
+                row += 8
+        checked += len(v["post_storage"])
     assert checked >= 390
 
 

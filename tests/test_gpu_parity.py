@@ -358,7 +358,7 @@ def test_power_of_two_strength_reduction(engine):
     assert (wi == wj).all()
 
 
-@pytest.mark.parametrize("jit", [False, True])
+@pytest.mark.parametrize("jit", [False, True, "o3"])
 def test_division_operand_sizes(engine, jit):
     """udivrem8's paths (one-limb long division, quotient-bit loop with 2/4/8-limb
     remainders) under every mix of operand sizes within a wave: per-lane bit lengths of
@@ -382,7 +382,8 @@ def test_division_operand_sizes(engine, jit):
     assigns += [[rng.getrandbits(256), rng.choice([1, 2, 3, 7, 10, 0xFFFFFFFF, 0])] for _ in range(128)]
     edges = [0, 1, 2, 3, (1 << 255), (1 << 255) - 1, (1 << 256) - 1, (1 << 256) - 2, 1 << 128, (1 << 32) - 1, 1 << 32]
     assigns += [[x, y] for x in edges for y in edges]
-    P, _, ver, got, models = gpu_eval_terms(engine, [T.BoolVal(True)], terms, assigns, jit=jit)
+    # jit=True: the default watch-row kernel (the first tier's), "o3": the O3 kernel
+    P, _, ver, got, models = gpu_eval_terms(engine, [T.BoolVal(True)], terms, assigns, jit=bool(jit), o3=jit == "o3")
     for i, (x, y) in enumerate(assigns):
         want = evaluate_many(terms, OracleModel({"a": x, "b": y}))
         for t, w in zip(terms, want):
