@@ -62,6 +62,17 @@ constexpr uint32_t kManySlots = 64;
 constexpr int kManyStreams = 4;
 static_assert(kPeerWord == 272, "jit.cpp / jit_asm.cpp hard-code the peer line at 2,176 B");
 
+// mg_init's warm-up thread (helper processes started, one tiny kernel assembled): detached, counted
+// here, and waited for by mg_shutdown and the exit handler before they stop the helpers, so a
+// shutdown never races the warm-up's helper I/O
+static std::mutex g_warm_mu;
+static std::condition_variable g_warm_cv;
+static int g_warm_running = 0;
+static void wait_warm() {
+  std::unique_lock<std::mutex> wl(g_warm_mu);
+  g_warm_cv.wait_for(wl, std::chrono::seconds(30), [] { return g_warm_running == 0; });
+}
+
 // an early-exit first hit to the devices above this one (the peer line).  System scope (gfx950:
 // global_atomic_umin_x2 ... sc1): a peer's word may live on another GPU, in fine-grained memory
 // (mg_init allocates every hit buffer fine-grained when the mask spans physical devices), where the
@@ -1721,7 +1732,18 @@ int mg_init(uint32_t device_mask) {
   }
   HIPCHK(hipSetDevice(e.device));
   e.stats.n_devices = (uint32_t)g_devs.size();
+  {
+    std::lock_guard<std::mutex> wl(g_warm_mu);
+    g_warm_running++;
+  }
   std::thread([] {  // helpers up (and the first tier's assembler warm) before the first query needs them
+    struct Done {  // mg_shutdown / the exit handler wait for this before stopping the helpers
+      ~Done() {
+        std::lock_guard<std::mutex> wl(g_warm_mu);
+        g_warm_running--;
+        g_warm_cv.notify_all();
+      }
+    } done_;
     Lowered P;
     P.vwidth = {1};
     P.consts = {1};
@@ -1768,6 +1790,7 @@ void mg_shutdown(void) {
       if (kv.second->ready) release_jit(*kv.second->ready);
     e.tickets.clear();
   }
+  wait_warm();        // the warm-up's helper requests end before the helpers stop
   jit_helper_stop();  // the compiler process ends on end of input (started again on demand)
   if (!e.init) {
     for (auto& kv : e.jits) release_jit(*kv.second);
@@ -2793,6 +2816,7 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
 // process exit with a compile in flight: stop the compile thread before the compiler
 // library's static destructors run (registered after them, so it runs first)
 static void jit_atexit() {
+  wait_warm();
   Engine& e = E();
   std::unique_lock<std::mutex> jl(e.jit_mu);
   e.jit_stop = true;

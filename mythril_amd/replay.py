@@ -175,6 +175,19 @@ def replay(code_hex: str, calldata: bytes = b"", pre_storage: Optional[Dict[int,
         path.append(T.eq(x.raw, BVV(v, 256).raw))
         return v
 
+    def branch(cond) -> bool:
+        """A JUMPI condition: folded, or followed with LASER's branch constraint kept — ``cond != 0``
+        on the taken branch, ``cond == 0`` on the fall-through (``instructions.py:1565-1571``)."""
+        cond = _as_bv(cond)
+        if cond.value is not None:
+            return int(cond.value) != 0
+        if follow is None:
+            raise ReplayUnsupported("input-dependent JUMPI condition")
+        taken = (int(follow(cond.raw)) & TT256M1) != 0
+        zero = BVV(0, 256).raw
+        path.append(T.not_(T.eq(cond.raw, zero)) if taken else T.eq(cond.raw, zero))
+        return taken
+
     def result(halted: str) -> ReplayResult:
         return ReplayResult(storage, halted, inputs, touched, path)
     k = 0
@@ -371,11 +384,11 @@ def replay(code_hex: str, calldata: bytes = b"", pre_storage: Optional[Dict[int,
             if dest not in jumpdests:
                 raise ExceptionalHalt("bad jump")
             k = pc_index[dest]
-        elif op == 0x57:                             # JUMPI
-            dest = decide(_pop(stack), "JUMPI target")
-            cond = _pop(stack)
-            c = decide(cond, "JUMPI condition")
-            if c != 0:
+        elif op == 0x57:                             # JUMPI (:1523-1585)
+            target = _pop(stack)
+            c = branch(_pop(stack))
+            if c:  # the target is a decision only on the taken branch
+                dest = decide(target, "JUMPI target")
                 if dest not in jumpdests:
                     raise ExceptionalHalt("bad jump")
                 k = pc_index[dest]

@@ -80,3 +80,24 @@ def test_smt_division_semantics():
     assert evaluate((x % zero).raw, m) == 7
     mn = 1 << 255
     assert evaluate((x / BVV(M, 256)).raw, OracleModel({"x": mn})) == mn  # -2^255 / -1 wraps
+
+
+def test_jumpi_path_constraint_is_lasers():
+    """An input-dependent JUMPI followed along the concrete path records LASER's branch constraint —
+    ``cond != 0`` taken, ``cond == 0`` not taken (``instructions.py:1565-1571``) — and the target is a
+    decision only when the branch is taken.  Code: CALLDATALOAD(0) as the condition, JUMPI to 7."""
+    from mythril_amd.replay import replay
+    from mythril_amd.smt import terms as T
+
+    code = "600035600757005b00"  # PUSH1 0 CALLDATALOAD PUSH1 7 JUMPI STOP JUMPDEST STOP
+    for word, taken in ((5, True), (0, False)):
+        data = word.to_bytes(32, "big")
+        arrs = {"calldata": ({i: b for i, b in enumerate(data)}, 0)}
+        m = OracleModel({"calldatasize": 32}, arrs)
+        r = replay(code, data, follow=lambda t, m=m: evaluate(t, m))
+        assert len(r.path) == 1, r.path
+        c = r.path[0]
+        assert (c.op == "not") == taken, c.op  # Not(cond == 0) taken, cond == 0 not taken
+        assert evaluate(c, m) == 1
+        other = OracleModel({"calldatasize": 32}, {"calldata": ({31: 0 if taken else 9}, 0)})
+        assert evaluate(c, other) == 0  # the constraint is the branch, not the concrete value
