@@ -181,24 +181,30 @@ class Emitter {
   static std::initializer_list<int> none() { return {}; }
 
   // --- VGPRs ---------------------------------------------------------------------------------
+  std::function<bool()> on_pressure;  // drop cached values (value numbering); true if any went
   uint32_t valloc() {
-    for (int r = vfirst; r < 256; r++)
-      if (!vref[r]) {
-        vref[r] = 1;
-        vgen[r] = ++gen_ctr;
-        vhigh = std::max(vhigh, r + 1);
-        return (uint32_t)r;
-      }
+    for (int pass = 0; pass < 2; pass++) {
+      for (int r = vfirst; r < 256; r++)
+        if (!vref[r]) {
+          vref[r] = 1;
+          vgen[r] = ++gen_ctr;
+          vhigh = std::max(vhigh, r + 1);
+          return (uint32_t)r;
+        }
+      if (!on_pressure || !on_pressure()) break;
+    }
     fail("out of VGPRs");
   }
   void retain(const Limb& l) {
     check(l);
     if (l.reg() && (int)l.v >= vfirst) vref[l.v]++;
   }
+  std::function<void(uint32_t)> on_free;  // a register's allocation tag died (limb value numbering)
   void release(const Limb& l) {
     check(l);
     if (l.reg() && (int)l.v >= vfirst) {
       if (--vref[l.v] < 0) fail("internal: VGPR released twice");
+      if (vref[l.v] == 0 && on_free) on_free(vgen[l.v]);
     }
   }
   // --- SGPR pairs ----------------------------------------------------------------------------
@@ -577,6 +583,25 @@ struct Gen {
   // ---------------------------------------------------------------------------------------
   Emitter& e() { return E; }
 
+  // Code emitted under a condition (a MIXED alternative, a delta step, a division / EXP / Keccak
+  // loop) may not run on every path to a later use, so nothing computed there enters the value
+  // caches (xcache, litcache): cond counts the open conditional regions
+  int cond = 0;
+  struct CondScope {
+    Gen& g;
+    explicit CondScope(Gen& g_) : g(g_) { g.cond++; }
+    ~CondScope() { g.cond--; }
+  };
+  // literals materialised in VGPRs, reused while the current constraint's code is emitted (cleared at
+  // each ASSERT and under register pressure): a LOOKUP's select chain over a literal default or
+  // literal-tail keys moved the same literal into a VGPR once per limb and prior
+  std::map<uint32_t, Limb> litcache;  // each entry holds one reference
+  void litcache_clear() {
+    std::vector<Limb> held;
+    for (auto& kv : litcache) held.push_back(kv.second);
+    litcache.clear();
+    for (auto& d : held) drop(d);
+  }
   // a VGPR holding limb l (a literal is moved into a fresh VGPR the caller releases)
   Limb vreg(const Limb& l) {
     if (l.reg()) {
@@ -587,11 +612,24 @@ struct Gen {
     if (x == 0) return Reg(6);  // the zero register
     auto it = pool.find(x);
     if (it != pool.end()) return Reg((uint32_t)it->second);  // loaded once, before the group loop
+    const bool cache = !cond && !no_lvn() && lvn_on;
+    if (cache) {
+      auto c = litcache.find(x);
+      if (c != litcache.end()) {
+        E.retain(c->second);
+        return c->second;
+      }
+    }
     census[x]++;
     const Limb r = fresh();
     E.valu("v_mov_b32_e32 " + VL(r) + ", " + imm(x));
+    if (cache) {
+      E.retain(r);
+      litcache[x] = r;
+    }
     return r;
   }
+  bool lvn_on = false;  // the value caches are live only inside body()
   // Literal pool: literals a VGPR operand needs (select arms, carry-chain operands, dictionary
   // entries) are moved into a VGPR at every use unless pooled — one VGPR each, loaded once per
   // kernel before the group loop.  jit_asm_source emits twice: the first pass counts (census), the
@@ -860,10 +898,7 @@ struct Gen {
         }
         return m;
       }
-      const Limb d = fresh();
-      const Limb s0 = b.reg() ? a : b, s1 = b.reg() ? b : a;
-      E.valu("v_xor_b32_e32 " + VL(d) + ", " + src(s0) + ", " + VL(s1));
-      diff.push_back(d);
+      diff.push_back(xor_limb(a, b));
     }
     Mask m;
     if (diff.empty()) {
@@ -893,6 +928,65 @@ struct Gen {
     if (keep) *keep = diff[0];  // the caller holds the reduced difference (eq_ids' cache)
     else drop(diff[0]);
     return m;
+  }
+
+  // Limb value numbering of the compare differences: x ^ y of two limbs is kept while both limbs'
+  // registers hold the values they had (allocation tags), so keys that share limbs across values —
+  // Concat(sender, slot) vs Concat(sender, other slot), a COPY and its source, a key and the
+  // LOOKUP priors built from it — XOR each limb pair once.  Each entry holds one reference to its
+  // result; the entry goes when either operand's register is released for good (E.on_free).
+  static uint64_t lid(const Limb& l) { return l.lit() ? ((1ull << 63) | l.v) : (((uint64_t)l.g << 9) | l.v); }
+  std::map<std::pair<uint64_t, uint64_t>, Limb> xcache;
+  std::multimap<uint32_t, std::pair<uint64_t, uint64_t>> xby;  // operand tag -> entries
+  static bool no_lvn() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_LVN");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
+  Limb xor_limb(const Limb& a, const Limb& b) {
+    const Limb s0 = b.reg() ? a : b, s1 = b.reg() ? b : a;
+    const bool cacheable = lvn_on && !cond && !no_lvn() && (!s0.reg() || (int)s0.v < E.vfirst || s0.g) &&
+                           ((int)s1.v < E.vfirst || s1.g);
+    const uint64_t k0 = lid(s0), k1 = lid(s1);  // (std::minmax of temporaries would return dangling references)
+    const std::pair<uint64_t, uint64_t> key(std::min(k0, k1), std::max(k0, k1));
+    if (cacheable) {
+      auto it = xcache.find(key);
+      if (it != xcache.end()) {
+        E.retain(it->second);
+        return it->second;
+      }
+    }
+    const Limb d = fresh();
+    E.valu("v_xor_b32_e32 " + VL(d) + ", " + src(s0) + ", " + VL(s1));
+    if (cacheable) {
+      E.retain(d);
+      xcache[key] = d;
+      for (const Limb& o : {s0, s1})
+        if (o.reg() && (int)o.v >= E.vfirst) xby.insert({o.g, key});
+    }
+    return d;
+  }
+  void xcache_free(uint32_t g) {
+    auto r = xby.equal_range(g);
+    std::vector<std::pair<uint64_t, uint64_t>> keys;
+    for (auto it = r.first; it != r.second; ++it) keys.push_back(it->second);
+    xby.erase(r.first, r.second);
+    for (const auto& k : keys) {
+      auto it = xcache.find(k);
+      if (it == xcache.end()) continue;
+      const Limb d = it->second;
+      xcache.erase(it);
+      drop(d);  // may free d's register in turn
+    }
+  }
+  void xcache_clear() {
+    std::vector<Limb> held;
+    for (auto& kv : xcache) held.push_back(kv.second);
+    xcache.clear();
+    xby.clear();
+    for (auto& d : held) drop(d);
   }
 
   // a == b over the first Lk limbs of values a and b.  The reduced difference (OR of the limbs' XORs)
@@ -1355,6 +1449,7 @@ struct Gen {
 
   // +/-(1 + (h & 1)) on the registers out, when (ws & 0xFFFF) < pdelta (scalar branch)
   void delta(const std::vector<Limb>& out, uint32_t c, uint32_t pdelta, int ws, const Limb* hknown) {
+    CondScope cs_(*this);
     const std::string skip = E.newlab();
     E.salu("s_and_b32 s40, " + S(ws) + ", 0xffff", {40});
     E.salu("s_cmp_lt_u32 s40, " + imm(pdelta));
@@ -1555,6 +1650,7 @@ struct Gen {
     std::vector<Limb> r;
     switch (kind) {
       case MG_GEN_MIXED: {
+        CondScope cs_(*this);
         std::vector<Limb> out(Lc);
         for (auto& x : out) x = fresh();
         const uint32_t pc = sp.p[3] != MG_NONE ? (sp.p[2] & 0xFFFFu) : 0u;
@@ -1993,6 +2089,7 @@ struct Gen {
   // EXEC holding the lanes that still have steps
   void udivrem(const std::vector<Limb>& a_in, const std::vector<Limb>& b_in, uint32_t W, std::vector<Limb>& q,
                std::vector<Limb>& r) {
+    CondScope cs_(*this);
     const uint32_t La = Lw(W), C = 32 * La;
     std::vector<Limb> a = a_in, b = b_in;
     a.resize(La, Lit(0));
@@ -2220,6 +2317,7 @@ struct Gen {
   // sits at the top; per step two squarings and, where some lane's digit is non-zero, a multiply
   // by base^{1,2,3} (selected per lane)
   std::vector<Limb> exp_var(const std::vector<Limb>& base_in, const std::vector<Limb>& e_in, uint32_t W) {
+    CondScope cs_(*this);
     const uint32_t La = Lw(W), C = 32 * La;
     std::vector<Limb> base = own(base_in, La), ex = own(e_in, La);
     std::vector<Limb> r(La);
@@ -2312,6 +2410,7 @@ struct Gen {
   // lanes per row
   static uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
   void keccak_f1600(std::vector<Limb>& st) {  // st: 50 owned registers, lane i = (st[2i], st[2i+1])
+    CondScope cs_(*this);
     static const uint64_t RC[24] = {
         0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
         0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
@@ -3083,6 +3182,7 @@ struct Gen {
         break;
       }
       case K_ASSERT: {
+        litcache_clear();  // the next constraint's code starts; its literals are materialised anew
         const Mask m = mask_of(in.a);
         if (m.k == 1) {
           if (!m.ones) E.salu("s_mov_b64 s[38:39], 0", {38, 39});
@@ -3099,6 +3199,7 @@ struct Gen {
       }
       case K_WATCH:
         if (eval_kernel) {
+          CondScope cs_(*this);  // the stores are skipped without a watch buffer
           // watch row p0 + j of candidate i: watch + ((p0 + j) * n + i) * 4, in-range lanes only
           const uint32_t Lw_ = Lw(P.vwidth[in.a]);
           E.salu("s_cmp_eq_u64 s[12:13], 0");  // no watch buffer: nothing to store
@@ -3162,8 +3263,23 @@ struct Gen {
   }
   void body(const std::string& next) {
     eqdiff.clear();  // a kernel abandoned midway (AsmFail: out of VGPRs at this depth) left its entries
+    xcache.clear();
+    xby.clear();
+    litcache.clear();
+    E.on_free = [this](uint32_t g) { xcache_free(g); };
+    E.on_pressure = [this]() {
+      const bool any = !xcache.empty() || !litcache.empty();
+      xcache_clear();
+      litcache_clear();
+      return any;
+    };
+    lvn_on = true;
+    static const bool annotate = getenv("MYTHGPU_JIT_ASM_ANNOTATE") != nullptr;
     for (size_t k = 0; k < code.size(); k++) {
       const Instr& in = code[k];
+      if (annotate)
+        E.o << "  ; vcode " << k << " op " << in.op << " w " << in.wd << " dst " << in.dst << " a " << in.a << " b " << in.b
+            << "\n";
       emit(in, k, next);
       if (debug_live()) {
         int used = 0;
@@ -3212,6 +3328,11 @@ struct Gen {
     }
     for (auto& kv : eqdiff) drop(kv.second);  // values live to the end of the body
     eqdiff.clear();
+    xcache_clear();
+    litcache_clear();
+    lvn_on = false;
+    E.on_free = nullptr;
+    E.on_pressure = nullptr;
   }
 
   // ---------------------------------------------------------------------------------------

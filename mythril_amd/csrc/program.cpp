@@ -2405,6 +2405,7 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
     // dead code: keep asserts (unless dropped: the model read-back of a known hit), watches
     // and whatever they transitively use
     auto dce = [&](std::vector<VInstr>& list) {
+      const size_t nw = vwidth.size();  // the rewrites below add values
       std::vector<char> live(nw, 0), keep(list.size(), 0);
       for (size_t k = list.size(); k-- > 0;) {
         const VInstr& c = list[k];
@@ -2445,8 +2446,18 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
     bool pushed = false, pruned = false;
     auto jit_rewrites = [&](const std::vector<VInstr>& list) {
       std::vector<VInstr> r = prune_guarded_lookups(list, vwidth.size(), &pruned);
-      if (pruned) r = dce(r);  // before the pushdown, whose new values dce's table does not cover
-      return push_eq_into_lookup(r, vwidth, out.consts, &pushed);
+      if (pruned) r = dce(r);
+      // to a fixed point (bounded): a pushed compare of a lookup whose values are lookups in turn —
+      // LASER's nested keccak inverse maps (C4: the preimage of one hash compared with the preimage
+      // of another) — is pushed again, so the inner 512-bit select chains go too
+      for (int round = 0; round < 4; round++) {
+        bool again = false;
+        r = push_eq_into_lookup(r, vwidth, out.consts, &again);
+        if (!again) break;
+        pushed = true;
+        r = dce(r);
+      }
+      return r;
     };
     if (narrowed) {
       std::vector<VInstr> kept_wide = jit_rewrites(dce(wide));

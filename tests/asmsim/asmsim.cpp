@@ -155,9 +155,14 @@ Module parse(const std::string& text) {
   std::string line;
   bool meta = false;
   std::string cur_kd;
+  int cur_tag = -1;
   while (std::getline(in, line)) {
     const size_t sc = line.find(';');
     const std::string raw = line;
+    if (sc != std::string::npos && line.compare(sc, 8, "; vcode ") == 0) {
+      m.tags.push_back(trim(line.substr(sc + 2)));
+      cur_tag = (int)m.tags.size() - 1;
+    }
     if (sc != std::string::npos) line = line.substr(0, sc);
     std::string t = trim(line);
     if (t.empty()) continue;
@@ -186,6 +191,7 @@ Module parse(const std::string& text) {
     }
     Ins ins;
     ins.text = trim(raw);
+    ins.tag = cur_tag;
     const size_t sp = t.find_first_of(" \t");
     std::string mn = sp == std::string::npos ? t : t.substr(0, sp);
     std::string rest = sp == std::string::npos ? "" : trim(t.substr(sp));
@@ -828,7 +834,10 @@ bool step(Wave& w, Ctx& c) {
     return true;
   }
   // ---- vector ALU -------------------------------------------------------------------------
-  if (c.st) c.st->valu++;
+  if (c.st) {
+    c.st->valu++;
+    if (in.tag >= 0) c.st->valu_by_tag[in.tag]++;
+  }
   const bool vop3 = enc != 1;  // VOP3 and SDWA take no 32-bit literal
   ValuCheck vc;
   const uint64_t ex = w.exec;

@@ -46,6 +46,7 @@ struct Ins {
   int bitop3 = -1;      // v_bitop3_b32's table
   int target = -1;      // branch target (instruction index)
   std::string text;     // the source line (diagnostics)
+  int tag = -1;         // the "; vcode ..." annotation region it belongs to (MYTHGPU_JIT_ASM_ANNOTATE)
 };
 
 struct Kernel {
@@ -56,6 +57,7 @@ struct Kernel {
 struct Module {
   std::vector<Ins> code;
   std::map<std::string, Kernel> kernels;
+  std::vector<std::string> tags;  // annotation texts, by Ins::tag
 };
 
 // parse the emitter's assembly text (throws SimError on anything unknown)
@@ -75,6 +77,7 @@ struct Memory {
 
 struct Stats {
   uint64_t insts = 0, valu = 0, salu = 0, vmem = 0, lds = 0, waves = 0;
+  std::map<int, uint64_t> valu_by_tag;  // VALU wave-instructions per annotation region
 };
 
 // run `kernel` over `nblk` 256-lane blocks; kernarg: the argument block's address

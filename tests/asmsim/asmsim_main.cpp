@@ -190,7 +190,20 @@ std::string check_search(uint64_t rec, const std::vector<uint8_t>& prog, const s
       put32(ka, 48, early ? ((rec & 1) ? 3u : 1u) : 0u);
       put32(ka, 52, nblk);
       const uint64_t kb = mem.add(ka.size(), ka.data());
-      asmsim::launch(m, "mgj_search", mem, kb, nblk, early ? nullptr : &st);
+      asmsim::Stats sst;
+      asmsim::launch(m, "mgj_search", mem, kb, nblk, early ? nullptr : &sst);
+      if (!early) {
+        st.valu += sst.valu;
+        st.salu += sst.salu;
+        // ASMSIM_COUNT=1: the full-evaluation search launch's instructions per candidate (lane-
+        // instructions, as SQ_INSTS_VALU x 64 / candidates)
+        if (getenv("ASMSIM_COUNT")) {
+          printf("count record %llu: valu %.1f salu %.1f lds %.2f vmem %.2f per candidate\n", (unsigned long long)rec,
+                 64.0 * sst.valu / count, 64.0 * sst.salu / count, 64.0 * sst.lds / count, 64.0 * sst.vmem / count);
+          for (const auto& kv : sst.valu_by_tag)  // MYTHGPU_JIT_ASM_ANNOTATE=1: per program instruction
+            printf("count tag %s: %.2f\n", m.tags[kv.first].c_str(), 64.0 * kv.second / count);
+        }
+      }
       uint64_t r[kHitU64];
       memcpy(r, mem.of(h).data.data(), sizeof r);
       uint64_t hits = r[1];
@@ -230,7 +243,24 @@ std::string check_eval(const std::vector<uint8_t>& prog, uint64_t seed, uint32_t
   if (lower_program(prog.data(), prog.size(), low, err)) return "lower: " + err;
   if (specialize_program(low, nullptr, nullptr, sp, err)) return "specialise: " + err;
   std::string src;
-  const int rc = jit_asm_source(sp, {}, {}, JIT_EVAL | (tiled ? JIT_EVAL_TILED : 0u), src, err);
+  int rc = jit_asm_source(sp, {}, {}, JIT_EVAL | (tiled ? JIT_EVAL_TILED : 0u), src, err);
+  if (const char* f = getenv("ASMSIM_DUMP")) {  // debugging: the emitted text
+    if (FILE* fp = fopen(f, "wb")) {
+      fwrite(src.data(), 1, src.size(), fp);
+      fclose(fp);
+    }
+  }
+  if (const char* f = getenv("ASMSIM_SOURCE")) {  // debugging: simulate this text instead
+    FILE* fp = fopen(f, "rb");
+    if (fp) {
+      src.clear();
+      char buf[4096];
+      size_t n;
+      while ((n = fread(buf, 1, sizeof buf, fp)) > 0) src.append(buf, n);
+      fclose(fp);
+      rc = MG_OK;
+    }
+  }
   if (rc == MG_E_UNSUPPORTED) {
     C.outside++;
     if (getenv("ASMSIM_WHY")) fprintf(stderr, "outside the tier: %s\n", err.c_str());
