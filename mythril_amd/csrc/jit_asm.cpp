@@ -2118,6 +2118,29 @@ struct Gen {
     // the divisor's limbs as registers for the subtraction
     std::vector<Limb> bv(La);
     for (uint32_t j = 0; j < La; j++) bv[j] = vreg(b[j]);
+    // lanes whose divisor is one non-zero limb (x / 10**k, x / n for a small n): limb-serial long
+    // division instead (div_one_limb), and out of the bit-serial loop below (n = 0)
+    {
+      std::vector<std::pair<Limb, Limb>> hz;
+      for (uint32_t j = 1; j < La; j++) hz.push_back({b[j], Lit(0)});
+      const Mask hiz = hz.empty() ? Mask{1, true, -1} : eq_mask(hz);
+      Mask nz0;
+      if (b[0].lit()) {
+        nz0.k = 1;
+        nz0.ones = b[0].v != 0;
+      } else {
+        nz0 = vcmp("ne", bv[0], 0);
+      }
+      const Mask one = mop("and", hiz, nz0);
+      E.srelease(hiz);
+      E.srelease(nz0);
+      if (!(one.k == 1 && !one.ones)) {
+        div_one_limb(a, bv[0], quo, rem, one);
+        if (one.k == 1) E.valu("v_mov_b32_e32 " + VL(n) + ", 0");
+        else vsel(n, n, Reg(6), one);
+      }
+      E.srelease(one);
+    }
     const int sN = sreg(), sIt = sreg();
     wave_max(n, 9, sN);
     // NB: the wave's widest divisor in limbs (ballots over the divisor's limbs)
@@ -2215,6 +2238,100 @@ struct Gen {
     q = quo;
     r = rem;
   }
+  // quo / rem of the lanes in mask `one` (divisor d = one non-zero limb): normalised long division,
+  // one Moller-Granlund 2/1 step per limb (Moller & Granlund, "Improved division by invariant
+  // integers", IEEE TC 2011, Alg. 4; as bv_device.h udivrem8's one-limb path), with the per-lane
+  // reciprocal v = floor((2^64 - 1) / dn) - 2^32 of the normalised divisor dn computed exactly by 32
+  // restoring steps (the numerator (~dn : 2^32 - 1) over dn: the quotient has 32 bits).  EXEC holds
+  // the lanes of `one` throughout; quo / rem are written for them only
+  void div_one_limb(const std::vector<Limb>& a, const Limb& d0, std::vector<Limb>& quo, std::vector<Limb>& rem,
+                    const Mask& one) {
+    const uint32_t La = (uint32_t)quo.size();
+    const std::string skip = E.newlab();
+    if (one.k == 2) {
+      E.salu("s_mov_b64 exec, " + SP(one.s));
+      E.ctl("s_cbranch_execz " + skip);
+    }
+    const Limb sh = fresh(), dn = fresh(), rv = fresh(), rr = fresh(), t = fresh(), q0 = fresh(), q1 = fresh();
+    E.valu("v_ffbh_u32_e32 " + VL(sh) + ", " + VL(d0));
+    E.valu("v_lshlrev_b32_e32 " + VL(dn) + ", " + VL(sh) + ", " + VL(d0));
+    // rv = floor(((~dn) * 2^32 + 2^32 - 1) / dn): 32 steps of rem = 2 rem + 1, a carry-out or rem >= dn
+    // subtracts dn and sets the quotient bit
+    {
+      const Mask c = mask_new(), g = mask_new();
+      const int sK = sreg();
+      E.valu("v_not_b32_e32 " + VL(rr) + ", " + VL(dn));
+      E.valu("v_mov_b32_e32 " + VL(rv) + ", 0");
+      E.salu("s_mov_b32 " + S(sK) + ", 32", {sK});
+      const std::string loop = E.newlab();
+      E.label(loop);
+      E.valu("v_cmp_gt_i32_e64 " + SP(c.s) + ", 0, " + VL(rr), {}, {c.s, c.s + 1});  // top bit set
+      E.valu("v_lshl_or_b32 " + VL(rr) + ", " + VL(rr) + ", 1, 1");
+      E.valu("v_cmp_ge_u32_e64 " + SP(g.s) + ", " + VL(rr) + ", " + VL(dn), {}, {g.s, g.s + 1});
+      E.salu("s_or_b64 " + SP(g.s) + ", " + SP(g.s) + ", " + SP(c.s), {g.s, g.s + 1});
+      E.valu("v_sub_u32_e32 " + VL(t) + ", " + VL(rr) + ", " + VL(dn));
+      vsel(rr, rr, t, g);
+      E.salu("s_mov_b64 vcc, " + SP(g.s), {kVCC, kVCC + 1});
+      E.valu("v_addc_co_u32_e32 " + VL(rv) + ", vcc, " + VL(rv) + ", " + VL(rv) + ", vcc", {kVCC, kVCC + 1},
+             {kVCC, kVCC + 1});
+      E.salu("s_add_u32 " + S(sK) + ", " + S(sK) + ", -1", {sK});
+      E.salu("s_cmp_lg_u32 " + S(sK) + ", 0");
+      E.ctl("s_cbranch_scc1 " + loop);
+      E.srelease(c);
+      E.srelease(g);
+      sfree(sK);
+    }
+    // the dividend shifted left by sh into La + 1 limbs: xs[j] = ({a[j], a[j-1]} << sh) >> 32
+    const Limb nsh = fresh();
+    E.valu("v_sub_u32_e32 " + VL(nsh) + ", 0, " + VL(sh));
+    const Mask z = vcmp("eq", sh, 0);
+    std::vector<Limb> xs(La + 1);
+    for (uint32_t j = 0; j <= La; j++) {
+      const Limb hi = j < La ? vreg(a[j]) : Reg(6), lo = j ? vreg(a[j - 1]) : Reg(6);
+      xs[j] = fresh();
+      E.valu("v_alignbit_b32 " + VL(xs[j]) + ", " + VL(hi) + ", " + VL(lo) + ", " + VL(nsh));
+      vsel(xs[j], xs[j], hi, z);
+      drop(hi);
+      drop(lo);
+    }
+    E.srelease(z);
+    drop(nsh);
+    const Mask M = mask_new();
+    // the top word of the shifted dividend is below 2^sh <= dn: the first step's high word
+    E.valu("v_mov_b32_e32 " + VL(rr) + ", " + VL(xs[La]));
+    for (int32_t j = (int32_t)La - 1; j >= 0; j--) {
+      const Limb& u0 = xs[j];
+      // (q1:q0) = rv * rr + (rr + 1 : u0)
+      E.valu("v_mul_lo_u32 " + VL(q0) + ", " + VL(rr) + ", " + VL(rv));
+      E.valu("v_mul_hi_u32 " + VL(q1) + ", " + VL(rr) + ", " + VL(rv));
+      E.valu("v_add_co_u32_e32 " + VL(q0) + ", vcc, " + VL(q0) + ", " + VL(u0), {}, {kVCC, kVCC + 1});
+      E.valu("v_addc_co_u32_e32 " + VL(q1) + ", vcc, " + VL(q1) + ", " + VL(rr) + ", vcc", {kVCC, kVCC + 1},
+             {kVCC, kVCC + 1});
+      E.valu("v_add_u32_e32 " + VL(q1) + ", 1, " + VL(q1));
+      // r = u0 - q1 dn (mod 2^32); r > q0: q1 - 1, r + dn; then r >= dn: q1 + 1, r - dn
+      E.valu("v_mul_lo_u32 " + VL(t) + ", " + VL(q1) + ", " + VL(dn));
+      E.valu("v_sub_u32_e32 " + VL(rr) + ", " + VL(u0) + ", " + VL(t));
+      E.valu("v_cmp_gt_u32_e64 " + SP(M.s) + ", " + VL(rr) + ", " + VL(q0), {}, {M.s, M.s + 1});
+      E.valu("v_add_u32_e32 " + VL(t) + ", -1, " + VL(q1));
+      E.valu("v_add_u32_e32 " + VL(q0) + ", " + VL(dn) + ", " + VL(rr));
+      vsel(q1, q1, t, M);
+      vsel(rr, rr, q0, M);
+      E.valu("v_cmp_le_u32_e64 " + SP(M.s) + ", " + VL(dn) + ", " + VL(rr), {}, {M.s, M.s + 1});
+      E.valu("v_add_u32_e32 " + VL(t) + ", 1, " + VL(q1));
+      E.valu("v_sub_u32_e32 " + VL(q0) + ", " + VL(rr) + ", " + VL(dn));
+      vsel(q1, q1, t, M);
+      vsel(rr, rr, q0, M);
+      E.valu("v_mov_b32_e32 " + VL(quo[j]) + ", " + VL(q1));
+    }
+    E.srelease(M);
+    E.valu("v_lshrrev_b32_e32 " + VL(rem[0]) + ", " + VL(sh) + ", " + VL(rr));
+    for (uint32_t j = 1; j < La; j++) E.valu("v_mov_b32_e32 " + VL(rem[j]) + ", 0");
+    for (auto& x : xs) drop(x);
+    for (const Limb& x : {sh, dn, rv, rr, t, q0, q1}) drop(x);
+    E.label(skip);
+    E.salu("s_mov_b64 exec, -1");
+  }
+
   // two's-complement negation of x (owned, in place) where mask m is set, to the width W
   void neg_where(std::vector<Limb>& x, const Mask& m, uint32_t W) {
     if (m.k == 1 && !m.ones) return;
@@ -2426,6 +2543,11 @@ struct Gen {
     for (auto& x : c) x = fresh();
     for (auto& x : rr) x = fresh();
     const Limb t0 = fresh(), t1 = fresh(), s0 = fresh(), s1 = fresh();
+    // 24 rounds in one loop: the round constants as 7-bit codes, 8 rounds per packed table; tables
+    // 0..2 in three SGPR pairs, the current one shifted by 7 bits per round and replaced by the next
+    // every 8 rounds
+    const int sT1 = sreg(), sT2 = sreg();
+    const int tabs[3] = {sT, sT1, sT2};
     for (int chunk = 0; chunk < 3; chunk++) {
       // 8 rounds x 7 bits: bit j of round k's code is RC bit kPos[j]
       uint64_t packed = 0;
@@ -2436,9 +2558,12 @@ struct Gen {
         if (back != RC[8 * chunk + k]) fail("internal: a Keccak round constant outside the 7-bit code");
         packed |= code << (7 * k);
       }
-      E.salu("s_mov_b32 " + S(sT) + ", " + hexs((uint32_t)packed), {sT});
-      E.salu("s_mov_b32 " + S(sT + 1) + ", " + hexs((uint32_t)(packed >> 32)), {sT + 1});
-      E.salu("s_mov_b32 " + S(sK) + ", 8", {sK});
+      const int T = tabs[chunk];
+      E.salu("s_mov_b32 " + S(T) + ", " + hexs((uint32_t)packed), {T});
+      E.salu("s_mov_b32 " + S(T + 1) + ", " + hexs((uint32_t)(packed >> 32)), {T + 1});
+    }
+    E.salu("s_mov_b32 " + S(sK) + ", 24", {sK});
+    {
       const std::string loop = E.newlab();
       E.label(loop);
       // theta: C[x] = xor of column x; a[x,y] ^= C[x-1] ^ rot(C[x+1], 1)
@@ -2503,9 +2628,16 @@ struct Gen {
       E.valu("v_xor_b32_e32 " + VL(hi(0)) + ", " + S(sR + 1) + ", " + VL(hi(0)));
       E.salu("s_lshr_b64 " + SP(sT) + ", " + SP(sT) + ", 7", {sT, sT + 1});
       E.salu("s_add_u32 " + S(sK) + ", " + S(sK) + ", -1", {sK});
+      // every 8 rounds the next table (s_cselect keeps SCC)
+      E.salu("s_and_b32 s40, " + S(sK) + ", 7", {40});
+      E.salu("s_cmp_eq_u32 s40, 0");
+      E.salu("s_cselect_b64 " + SP(sT) + ", " + SP(sT1) + ", " + SP(sT), {sT, sT + 1});
+      E.salu("s_cselect_b64 " + SP(sT1) + ", " + SP(sT2) + ", " + SP(sT1), {sT1, sT1 + 1});
       E.salu("s_cmp_lg_u32 " + S(sK) + ", 0");
       E.ctl("s_cbranch_scc1 " + loop);
     }
+    sfree(sT1);
+    sfree(sT2);
     drop_all(c);
     drop_all(rr);
     drop(t0);
