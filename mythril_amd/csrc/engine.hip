@@ -1151,6 +1151,7 @@ struct JitTicket {
   std::unique_ptr<DevJit> ready;  // loaded module, handed to Engine::jits by the poll
   int rc = MG_OK;
   std::string err;
+  std::chrono::steady_clock::time_point submitted = std::chrono::steady_clock::now();  // MYTHGPU_JIT_TIMING
 };
 
 struct Engine {
@@ -2761,8 +2762,8 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
       rc = load_jit(code, *t, ms, j);
       if (getenv("MYTHGPU_JIT_TIMING")) {
         auto d = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        fprintf(stderr, "mythgpu jit worker (%s): source %.2f ms, compile %.2f ms, module load %.2f ms\n",
-                (t->flags & MG_JIT_ASM) ? "asm" : "o3", d(t0, t_src), d(t_src, t_comp),
+        fprintf(stderr, "mythgpu jit worker (%s): queued %.2f ms, source %.2f ms, compile %.2f ms, module load %.2f ms\n",
+                (t->flags & MG_JIT_ASM) ? "asm" : "o3", d(t->submitted, t0), d(t0, t_src), d(t_src, t_comp),
                 d(t_comp, std::chrono::steady_clock::now()));
       }
       if (rc != MG_OK && from_disk) {

@@ -182,18 +182,23 @@ class Emitter {
 
   // --- VGPRs ---------------------------------------------------------------------------------
   std::function<bool()> on_pressure;  // drop cached values (value numbering); true if any went
+  // The value caches may not raise the kernel's VGPR count past the occupancy step the kernel
+  // reaches without them (jit_asm_source): an allocation at or above vsoft first drops the caches.
+  // (C4: the literal cache alone took the search kernel from 98 to 134 VGPRs, 4 to 3 waves per SIMD.)
+  int vsoft = 256;
   uint32_t valloc() {
-    for (int pass = 0; pass < 2; pass++) {
-      for (int r = vfirst; r < 256; r++)
-        if (!vref[r]) {
-          vref[r] = 1;
-          vgen[r] = ++gen_ctr;
-          vhigh = std::max(vhigh, r + 1);
-          return (uint32_t)r;
-        }
-      if (!on_pressure || !on_pressure()) break;
+    for (;;) {
+      int r = vfirst;
+      while (r < 256 && vref[r]) r++;
+      // cache entries go one at a time (least recently used first) until a register below the limit
+      // is free or the caches are empty
+      if ((r >= 256 || r >= vsoft) && on_pressure && on_pressure()) continue;
+      if (r >= 256) fail("out of VGPRs");
+      vref[r] = 1;
+      vgen[r] = ++gen_ctr;
+      vhigh = std::max(vhigh, r + 1);
+      return (uint32_t)r;
     }
-    fail("out of VGPRs");
   }
   void retain(const Limb& l) {
     check(l);
@@ -208,13 +213,22 @@ class Emitter {
     }
   }
   // --- SGPR pairs ----------------------------------------------------------------------------
+  int sfree() const {  // SGPR pairs free
+    int n = 0;
+    for (int r = kS0; r + 1 < kS1; r += 2) n += !sref[r];
+    return n;
+  }
+  std::function<bool()> on_spressure;  // move a Bool value's mask to its VGPR form; true if one went
   int salloc() {
-    for (int r = kS0; r + 1 < kS1; r += 2)
-      if (!sref[r]) {
-        sref[r] = 1;
-        shigh = std::max(shigh, r + 2);
-        return r;
-      }
+    for (;;) {
+      for (int r = kS0; r + 1 < kS1; r += 2)
+        if (!sref[r]) {
+          sref[r] = 1;
+          shigh = std::max(shigh, r + 2);
+          return r;
+        }
+      if (!on_spressure || !on_spressure()) break;
+    }
     fail("out of SGPRs");
   }
   void sretain(const Mask& m) {
@@ -596,10 +610,16 @@ struct Gen {
   // each ASSERT and under register pressure): a LOOKUP's select chain over a literal default or
   // literal-tail keys moved the same literal into a VGPR once per limb and prior
   std::map<uint32_t, Limb> litcache;  // each entry holds one reference
+  // last use of each cache entry (eviction under the soft VGPR limit: least recently used first)
+  uint64_t tick = 0;
+  std::map<uint32_t, uint64_t> lit_last;
+  std::map<std::pair<uint64_t, uint64_t>, uint64_t> x_last;
+  std::map<std::pair<uint32_t, uint32_t>, uint64_t> eq_last;
   void litcache_clear() {
     std::vector<Limb> held;
     for (auto& kv : litcache) held.push_back(kv.second);
     litcache.clear();
+    lit_last.clear();
     for (auto& d : held) drop(d);
   }
   // a VGPR holding limb l (a literal is moved into a fresh VGPR the caller releases)
@@ -612,10 +632,11 @@ struct Gen {
     if (x == 0) return Reg(6);  // the zero register
     auto it = pool.find(x);
     if (it != pool.end()) return Reg((uint32_t)it->second);  // loaded once, before the group loop
-    const bool cache = !cond && !no_lvn() && lvn_on;
+    const bool cache = !cond && !no_lvn() && lvn_on && caches;
     if (cache) {
       auto c = litcache.find(x);
       if (c != litcache.end()) {
+        lit_last[x] = ++tick;
         E.retain(c->second);
         return c->second;
       }
@@ -626,10 +647,15 @@ struct Gen {
     if (cache) {
       E.retain(r);
       litcache[x] = r;
+      lit_last[x] = ++tick;
     }
     return r;
   }
   bool lvn_on = false;  // the value caches are live only inside body()
+  // jit_asm_source's first pass emits without the value caches (litcache, xcache, eqdiff): its VGPR
+  // count sets the occupancy step (vsoft) the cached second pass must stay within
+  bool caches = true;
+  int vsoft = 256;
   // Literal pool: literals a VGPR operand needs (select arms, carry-chain operands, dictionary
   // entries) are moved into a VGPR at every use unless pooled — one VGPR each, loaded once per
   // kernel before the group loop.  jit_asm_source emits twice: the first pass counts (census), the
@@ -708,8 +734,30 @@ struct Gen {
   std::vector<Limb> add_chain(const std::vector<Limb>& x, const std::vector<Limb>& y, uint32_t n, bool sub) {
     std::vector<Limb> r(n);
     int carry = 0;  // known 0/1, or -1 = VCC
+    Limb zz{};      // a subtraction's 0 - 0 - borrow limb (the same for every such limb above)
     for (uint32_t j = 0; j < n; j++) {
       const Limb a = j < x.size() ? x[j] : Lit(0), b = j < y.size() ? y[j] : Lit(0);
+      if (carry < 0 && a.lit() && a.v == 0 && b.lit() && b.v == 0) {
+        // zero limbs above a carry in VCC: an addition's limb is the carry and carries nothing on (the
+        // limbs above are literal zeros); a subtraction's is -borrow, borrowing on — one limb serves all
+        if (!sub) {
+          const Limb d = fresh();
+          E.valu("v_addc_co_u32_e32 " + VL(d) + ", vcc, 0, v6, vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
+          r[j] = d;
+          carry = 0;
+          continue;
+        }
+        if (!zz.reg()) {
+          zz = fresh();
+          E.valu("v_subb_co_u32_e32 " + VL(zz) + ", vcc, 0, v6, vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
+          r[j] = zz;
+        } else {
+          E.retain(zz);
+          r[j] = zz;
+        }
+        continue;
+      }
+      zz = Limb{};  // a different borrow from here on
       if (a.lit() && b.lit() && carry >= 0) {
         uint64_t t;
         if (!sub) {
@@ -858,9 +906,20 @@ struct Gen {
     return d;
   }
 
-  // XOR-OR reduction of the limb pairs -> mask (all lanes where every pair is equal)
+  // XOR-OR reduction of the limb pairs -> mask (all lanes where every pair is equal).  Pairs whose XOR
+  // the limb cache holds (xcache) are ORed in; the others accumulate one v_bitop3 each,
+  // acc = (a ^ b) | acc (a literal operand through s41), instead of an XOR each and an OR tree
+  // (MYTHGPU_JIT_ASM_EQ_BITOP3=0: XOR each pair, then OR3 trees)
+  static bool eq_bitop3() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_EQ_BITOP3");
+      return !(g && g[0] == '0');
+    }();
+    return on;
+  }
   Mask eq_mask(const std::vector<std::pair<Limb, Limb>>& prs, Limb* keep = nullptr) {
     std::vector<Limb> diff;  // owned
+    std::vector<std::pair<Limb, Limb>> raw;  // pairs for the bitop3 accumulation
     for (const auto& pr : prs) {
       const Limb a = pr.first, b = pr.second;
       if (a.lit() && b.lit()) {
@@ -884,7 +943,7 @@ struct Gen {
         diff.push_back(a);
         continue;
       }
-      if (prs.size() == 1 || (diff.empty() && &pr == &prs.back())) {
+      if (prs.size() == 1 || (diff.empty() && raw.empty() && &pr == &prs.back())) {
         // one pair only: one compare
         const Limb s0 = b.reg() ? a : b, s1 = b.reg() ? b : a;
         Mask m;
@@ -898,7 +957,43 @@ struct Gen {
         }
         return m;
       }
-      diff.push_back(xor_limb(a, b));
+      if (eq_bitop3()) {
+        Limb hit;
+        if (xcache_get(a, b, hit)) diff.push_back(hit);
+        else raw.push_back({a, b});
+      } else {
+        diff.push_back(xor_limb(a, b));
+      }
+    }
+    if (!raw.empty()) {
+      // acc = a0 ^ b0, then acc = (a ^ b) | acc per pair (bitop3 table 0xBE over (a, b, acc))
+      const auto& p0 = raw[0];
+      Limb acc = fresh();
+      {
+        const Limb s0 = p0.second.reg() ? p0.first : p0.second, s1 = p0.second.reg() ? p0.second : p0.first;
+        E.valu("v_xor_b32_e32 " + VL(acc) + ", " + src(s0) + ", " + VL(s1));
+      }
+      int64_t s41 = -1;  // the literal s41 holds
+      for (size_t i = 1; i < raw.size(); i++) {
+        const Limb x = raw[i].second.reg() ? raw[i].first : raw[i].second;  // a literal, if any
+        const Limb y = raw[i].second.reg() ? raw[i].second : raw[i].first;
+        std::string xs;
+        if (x.lit() && !inl(x.v)) {
+          if (s41 != (int64_t)x.v) {
+            E.salu("s_mov_b32 s41, " + hexs(x.v), {41});
+            s41 = x.v;
+          }
+          xs = "s41";
+        } else {
+          xs = src(x);
+        }
+        const Limb d = fresh();
+        if (xs == "s41") E.valu("v_bitop3_b32 " + VL(d) + ", " + VL(y) + ", s41, " + VL(acc) + " bitop3:0xbe", {41});
+        else E.valu("v_bitop3_b32 " + VL(d) + ", " + VL(y) + ", " + xs + ", " + VL(acc) + " bitop3:0xbe");
+        drop(acc);
+        acc = d;
+      }
+      diff.push_back(acc);
     }
     Mask m;
     if (diff.empty()) {
@@ -947,13 +1042,14 @@ struct Gen {
   }
   Limb xor_limb(const Limb& a, const Limb& b) {
     const Limb s0 = b.reg() ? a : b, s1 = b.reg() ? b : a;
-    const bool cacheable = lvn_on && !cond && !no_lvn() && (!s0.reg() || (int)s0.v < E.vfirst || s0.g) &&
+    const bool cacheable = lvn_on && caches && !cond && !no_lvn() && (!s0.reg() || (int)s0.v < E.vfirst || s0.g) &&
                            ((int)s1.v < E.vfirst || s1.g);
     const uint64_t k0 = lid(s0), k1 = lid(s1);  // (std::minmax of temporaries would return dangling references)
     const std::pair<uint64_t, uint64_t> key(std::min(k0, k1), std::max(k0, k1));
     if (cacheable) {
       auto it = xcache.find(key);
       if (it != xcache.end()) {
+        x_last[key] = ++tick;
         E.retain(it->second);
         return it->second;
       }
@@ -963,10 +1059,22 @@ struct Gen {
     if (cacheable) {
       E.retain(d);
       xcache[key] = d;
+      x_last[key] = ++tick;
       for (const Limb& o : {s0, s1})
         if (o.reg() && (int)o.v >= E.vfirst) xby.insert({o.g, key});
     }
     return d;
+  }
+  // the cached XOR of limbs a and b, if any (retained for the caller)
+  bool xcache_get(const Limb& a, const Limb& b, Limb& out) {
+    if (!(lvn_on && caches && !cond && !no_lvn())) return false;
+    const uint64_t k0 = lid(a), k1 = lid(b);
+    auto it = xcache.find({std::min(k0, k1), std::max(k0, k1)});
+    if (it == xcache.end()) return false;
+    x_last[it->first] = ++tick;
+    E.retain(it->second);
+    out = it->second;
+    return true;
   }
   void xcache_free(uint32_t g) {
     auto r = xby.equal_range(g);
@@ -998,6 +1106,7 @@ struct Gen {
     const auto key = std::minmax(a, b);
     auto it = eqdiff.find(key);
     if (it != eqdiff.end()) {
+      eq_last[key] = ++tick;
       Mask m;
       m.k = 2;
       m.s = E.salloc();
@@ -1008,8 +1117,89 @@ struct Gen {
     for (uint32_t j = 0; j < Lk; j++) prs.push_back({limb(a, j), limb(b, j)});
     Limb keep{};
     const Mask m = eq_mask(prs, &keep);
-    if (keep.reg()) eqdiff[key] = keep;
+    if (keep.reg() && caches) {
+      eqdiff[key] = keep;
+      eq_last[key] = ++tick;
+    }
+    else if (keep.reg()) drop(keep);
     return m;
+  }
+  // One cache entry goes, to make room under the soft VGPR limit: a literal first (a hit saves one
+  // v_mov), then an XOR (one v_xor), then a compare difference (a whole OR-reduction), least
+  // recently used first within each.  False when every cache is empty.
+  template <class M, class T>
+  static typename M::iterator lru(M& m, T& last) {
+    auto best = m.end();
+    uint64_t bt = ~0ull;
+    for (auto it = m.begin(); it != m.end(); ++it) {
+      auto l = last.find(it->first);
+      const uint64_t t = l == last.end() ? 0 : l->second;
+      if (t < bt) {
+        bt = t;
+        best = it;
+      }
+    }
+    return best;
+  }
+  bool evict_one() {
+    if (!litcache.empty()) {
+      auto it = lru(litcache, lit_last);
+      const Limb d = it->second;
+      lit_last.erase(it->first);
+      litcache.erase(it);
+      drop(d);
+      return true;
+    }
+    if (!xcache.empty()) {
+      auto it = lru(xcache, x_last);
+      const Limb d = it->second;
+      x_last.erase(it->first);
+      xcache.erase(it);  // its xby entries go stale: xcache_free skips keys no longer cached
+      drop(d);
+      return true;
+    }
+    if (!eqdiff.empty()) {
+      auto it = lru(eqdiff, eq_last);
+      const Limb d = it->second;
+      eq_last.erase(it->first);
+      eqdiff.erase(it);
+      drop(d);
+      return true;
+    }
+    return false;
+  }
+  // Out of SGPR pairs (the compare pushdown keeps many Bools live as lane masks): the mask of the Bool
+  // value read latest, and not by the instruction being emitted, moves to its VGPR form (one
+  // v_cndmask; a later reader compares it back)
+  size_t cur_k = 0;
+  bool spill_mask() {
+    if (cur_k >= code.size()) return false;
+    const Instr& in = code[cur_k];
+    auto operand = [&](uint32_t id) {
+      if (id == in.a || id == in.b || id == in.c) return true;
+      if (in.op == K_LOOKUP) {
+        if (id == in.p0) return true;
+        for (uint32_t q = 0; q < 2 * in.c; q++)
+          if (P.vaux[in.p1 + q] == id) return true;
+      }
+      return false;
+    };
+    int64_t best = -1;
+    int32_t bl = -1;
+    for (uint32_t id = 0; id < val.size(); id++) {
+      const Val& x = val[id];
+      if (!x.def || x.m.k != 2 || E.sref[x.m.s] != 1 || operand(id)) continue;
+      const int32_t lu = id < last.size() ? last[id] : -1;
+      if (lu > bl) {
+        bl = lu;
+        best = id;
+      }
+    }
+    if (best < 0) return false;
+    limb_of_bool((uint32_t)best);
+    E.srelease(val[best].m);
+    val[best].m = Mask{};
+    return true;
   }
   // value `id` is dead: the cached differences it took part in go
   void eq_forget(uint32_t id) {
@@ -1072,12 +1262,63 @@ struct Gen {
       for (auto& d : own) drop(d);
       return m;
     }
+    // a literal operand whose limbs above k are zero while the other's are registers (LASER's bounds
+    // checks: x <= 20, 0 < x): the high limbs only need a zero test, x < K = (x_hi == 0) & (x_lo < K_lo)
+    // and K < x = (x_hi != 0) | (K_lo < x_lo) — an OR-reduction instead of a borrow through every limb
+    if (!sgn) {
+      for (int side = 0; side < 2; side++) {
+        const std::vector<Limb>& kv = side ? x : y;  // the literal side
+        const std::vector<Limb>& rv = side ? y : x;
+        int k = -1;  // highest nonzero limb of the literal side
+        bool lit_all = true;
+        for (uint32_t j = 0; j < La; j++) {
+          if (!kv[j].lit()) lit_all = false;
+          else if (kv[j].v) k = (int)j;
+        }
+        if (!lit_all) continue;
+        std::vector<std::pair<Limb, Limb>> hz;
+        for (uint32_t j = (uint32_t)(k + 1); j < La; j++)
+          if (!(rv[j].lit() && rv[j].v == 0)) hz.push_back({rv[j], Lit(0)});
+        uint32_t regs = 0;
+        for (const auto& pr : hz) regs += pr.first.reg();
+        if (regs < 2) continue;
+        const uint32_t wl = 32u * (uint32_t)(k + 1);
+        std::vector<Limb> xl(x.begin(), x.begin() + (k + 1)), yl(y.begin(), y.begin() + (k + 1));
+        const Mask z = eq_mask(hz);  // the register side's high limbs are zero
+        Mask lo;
+        if (k < 0) {
+          lo.k = 1;
+          lo.ones = false;  // x_lo < y_lo over no limbs: 0 < 0
+        } else {
+          lo = lt_mask(xl, yl, wl, false);
+        }
+        Mask r;
+        if (side == 0) {  // x < K
+          r = mop("and", z, lo);
+        } else {          // K < x
+          const Mask nz = mnot(z);
+          r = mop("or", nz, lo);
+          E.srelease(nz);
+        }
+        E.srelease(z);
+        E.srelease(lo);
+        for (auto& d : own) drop(d);
+        return r;
+      }
+    }
     // borrow chain of x - y; the difference itself is thrown away (v7)
     int borrow = 0;
     for (uint32_t j = 0; j < La; j++) {
       const Limb a = x[j], b = y[j];
       if (a.lit() && b.lit() && borrow >= 0) {
         borrow = ((uint64_t)a.v < (uint64_t)b.v + (uint64_t)borrow) ? 1 : 0;
+        continue;
+      }
+      if (a.lit() && b.lit()) {
+        // a borrow in VCC through literal limbs: equal ones pass it on, a larger minuend absorbs it,
+        // a smaller one borrows regardless — no instruction
+        if (a.v > b.v) borrow = 0;
+        else if (a.v < b.v) borrow = 1;
         continue;
       }
       if (borrow == 1) {
@@ -1302,8 +1543,10 @@ struct Gen {
   }
 
   // dictionary entry `idx` (VGPR) of the n-entry table at G[off] (width w)
-  std::vector<Limb> dict(uint32_t off, uint32_t n, uint32_t w, const Limb& idx, const std::vector<Limb>* tgt = nullptr) {
-    const uint32_t Lc = Lw(w);
+  // (upto: only limbs below it — the others come back as literal zeros, unread by the caller)
+  std::vector<Limb> dict(uint32_t off, uint32_t n, uint32_t w, const Limb& idx, const std::vector<Limb>* tgt = nullptr,
+                         uint32_t upto = 64) {
+    const uint32_t Lc = Lw(w), Lu = std::min(Lc, upto);
     std::vector<Limb> r(Lc, Lit(0));
     auto dst = [&](uint32_t j) { return tgt ? (*tgt)[j] : fresh(); };
     if (w <= 32 && n && (uint64_t)n * w <= 32) {  // packed in one literal: one bit-field extract
@@ -1356,7 +1599,7 @@ struct Gen {
         E.retain(cur);
         return cur;
       };
-      for (uint32_t j = 0; j < Lc; j++) {
+      for (uint32_t j = 0; j < Lu; j++) {
         bool same = true;
         for (uint32_t e2 = 1; e2 < n && same; e2++) same = G[off + e2 * Lc + j] == G[off + j];
         if (same) {
@@ -1382,7 +1625,7 @@ struct Gen {
       const Limb va = fresh();
       E.valu("v_lshlrev_b32_e32 " + VL(va) + ", 2, " + VL(idx));
       bool any = false;
-      for (uint32_t j = 0; j < Lc; j++) {
+      for (uint32_t j = 0; j < Lu; j++) {
         bool same = true;
         for (uint32_t e2 = 1; e2 < n && same; e2++) same = G[off + e2 * Lc + j] == G[off + j];
         if (same) {
@@ -1402,7 +1645,7 @@ struct Gen {
     const Limb vo = fresh();
     E.valu("v_mul_u32_u24_e32 " + VL(vo) + ", " + imm(4 * Lc) + ", " + VL(idx));
     bool any = false;
-    for (uint32_t j = 0; j < Lc; j++) {
+    for (uint32_t j = 0; j < Lu; j++) {
       bool same = true;
       for (uint32_t e2 = 1; e2 < n && same; e2++) same = G[off + e2 * Lc + j] == G[off + j];
       if (same) {
@@ -1444,6 +1687,7 @@ struct Gen {
       E.valu("v_mov_b32_e32 " + VL(out[j]) + ", " + src(x));
       if (j < r.size()) drop(r[j]);
     }
+    for (size_t j = out.size(); j < r.size(); j++) drop(r[j]);  // limbs above the ones generated
     r.clear();
   }
 
@@ -1493,6 +1737,9 @@ struct Gen {
   // zero: limbs of out this branch knows to be zero (bit j = limb j)
   void finish(const std::vector<Limb>& out, uint32_t width, uint32_t clamp, uint64_t zero = 0) {
     const uint32_t Lc = (uint32_t)out.size();
+    // a MIXED value generated to fewer limbs than the width (gen_value's want) has no top limb to mask
+    // and no clamp (a clamp reads every limb: such values are generated whole)
+    if (Lc < Lw(width)) return;
     if ((width & 31) && !(zero >> (Lc - 1) & 1))
       E.valu("v_and_b32_e32 " + VL(out[Lc - 1]) + ", " + imm(topmask(width)) + ", " + VL(out[Lc - 1]));
     if (!clamp) return;
@@ -1642,16 +1889,31 @@ struct Gen {
     }
   }
 
-  // coordinate c's value (owned limbs)
-  std::vector<Limb> gen_value(uint32_t c) {
+  // coordinate c's value (owned limbs).  want: the limbs the caller reads (bit j = limb j); a MIXED
+  // value is generated only up to the highest of them that its fixed-bit record does not set whole
+  // (the limbs above come back as literals: zeros, or the record's bits) — the same value in every
+  // limb read, as each limb depends only on the limbs below it (carries, the UNIFORM chain) or on
+  // none (dictionary entries).  A clamp reads every limb: such values are generated whole.
+  // (C4: a COPY chain three MIXED levels deep whose every bit but one is fixed)
+  std::vector<Limb> gen_value(uint32_t c, uint64_t want = ~0ull) {
     const GenSpec sp = specs.at(c);
     const uint32_t fix = sp.kind >> 8, kind = sp.kind & 0xFFu;
     const uint32_t width = P.coord_width.at(c), Lc = Lw(width);
     std::vector<Limb> r;
     switch (kind) {
       case MG_GEN_MIXED: {
+        uint64_t wl = want & lowmask(Lc);
+        if (fix)
+          for (uint32_t j = 0; j < Lc; j++)
+            if (G[fix - 1 + j] == 0xFFFFFFFFu) wl &= ~(1ull << j);
+        const uint32_t Lg = (sp.p[6] || no_gen_want()) ? Lc : (wl ? 64u - (uint32_t)__builtin_clzll(wl) : 0u);
+        if (Lg == 0) {  // nothing the caller reads is generated: the record's bits
+          r.assign(Lc, Lit(0));
+          if (fix) fixbits(r, fix, false);
+          return r;
+        }
         CondScope cs_(*this);
-        std::vector<Limb> out(Lc);
+        std::vector<Limb> out(Lg);
         for (auto& x : out) x = fresh();
         const uint32_t pc = sp.p[3] != MG_NONE ? (sp.p[2] & 0xFFFFu) : 0u;
         const uint32_t pd = sp.p[1] ? (sp.p[2] >> 16) : 0u;
@@ -1670,7 +1932,7 @@ struct Gen {
             u[0] = and_lit(h, m & 0xFFFFu);
             drop(h);
           } else {
-            u = uniform_limbs(c, Lc, bitsn, &out);
+            u = uniform_limbs(c, Lg, bitsn, &out);
           }
           put(out, u);
         };
@@ -1702,7 +1964,7 @@ struct Gen {
             s = val[it->second].l;
             for (auto& x : s) E.retain(x);
           } else {
-            s = gen_value(sp.p[3]);
+            s = gen_value(sp.p[3], lowmask(Lg));
           }
           uint64_t zero = 0;  // limbs the copied value has as literal zeros (a delta may change them)
           for (uint32_t j = 0; j < Lc && !sp.p[5]; j++)
@@ -1715,7 +1977,7 @@ struct Gen {
           branch(pc + pd);
           const Limb h = grnd(c, 0xFFFFu);
           const Limb ix = dict_index(h, sp.p[1]);
-          std::vector<Limb> dv = dict(sp.p[0], sp.p[1], width, ix, &out);
+          std::vector<Limb> dv = dict(sp.p[0], sp.p[1], width, ix, &out, Lg);
           drop(ix);
           uint64_t zero = 0;  // limbs zero in every entry (a delta may change them)
           for (uint32_t j = 0; j < Lc && !sp.p[5]; j++)
@@ -1749,8 +2011,25 @@ struct Gen {
         wsm.s = ws;
         E.srelease(wsm);
         // (every alternative masked its value to the width in finish)
-        if (fix) fixbits(out, fix, true);
-        return out;
+        r.assign(Lc, Lit(0));
+        for (uint32_t j = 0; j < Lg; j++) r[j] = out[j];
+        if (fix) {
+          // the record's bits: in place on the generated limbs; a generated limb the record sets
+          // whole (below a wanted one) becomes its literal
+          const uint32_t f = fix - 1;
+          for (uint32_t j = 0; j < Lc; j++) {
+            const uint32_t m = G[f + j], v = G[f + Lc + j];
+            if (!m) continue;
+            if (!r[j].reg() || m == 0xFFFFFFFFu) {
+              drop(r[j]);
+              r[j] = Lit(v);
+              continue;
+            }
+            E.valu("v_and_b32_e32 " + VL(r[j]) + ", " + imm(~m) + ", " + VL(r[j]));
+            if (v) E.valu("v_or_b32_e32 " + VL(r[j]) + ", " + imm(v) + ", " + VL(r[j]));
+          }
+        }
+        return r;
       }
       case MG_GEN_DICT: {
         const Limb h = grnd(c, 0xFFFFu);
@@ -2744,7 +3023,7 @@ struct Gen {
           set(d, soa_limbs(in, d));
           break;
         }
-        std::vector<Limb> r = gen_value(in.p0);
+        std::vector<Limb> r = gen_value(in.p0, need[d]);
         set(d, r);
         cval[in.p0] = d;
         break;
@@ -2839,12 +3118,15 @@ struct Gen {
             } else {
               so = src(ly);
             }
-            const Limb dl = fresh(), dh = fresh();
+            // the product's limb 0 is the low half of a0 * b0 alone: it carries nothing into the limbs
+            // the test reads (at or above wa >= 32), so it is not computed
+            const bool lo_dead = i + j == 0 && wa >= 32;
+            const Limb dl = lo_dead ? Lit(0) : fresh(), dh = fresh();
             if (via_s41) {
-              E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so, {41});
+              if (!lo_dead) E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so, {41});
               E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so, {41});
             } else {
-              E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so);
+              if (!lo_dead) E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so);
               E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so);
             }
             lo[i + j] = dl;
@@ -3274,6 +3556,70 @@ struct Gen {
           set_mask(d, cur);
           break;
         }
+        // (the key tests and their run ORs stay in SGPR pairs over the limbs: only with room for them)
+        if (n >= 2 && n <= 5 && !no_lookup_runs() && E.sfree() >= (int)(n + n * (n - 1) / 2 + 4)) {
+          // The key tests first, then per limb the select chain with runs of priors holding the same
+          // limb (a key's literal tail, a zero, the same register) merged into one select under the OR
+          // of their tests: applied last to first, h_p ? v : (h_p-1 ? v : c) = (h_p | h_p-1) ? v : c.
+          // (C4: the keccak preimage lookups' limbs are mostly such runs.)
+          std::vector<Mask> hs;
+          std::vector<uint32_t> ps;  // the priors left, in application order (last prior first)
+          int base = -1;             // a prior that always matches: the chain starts at its value
+          for (int32_t p = (int32_t)n - 1; p >= 0; p--) {
+            const Mask h = key_test(P.vaux[in.p1 + 2 * p]);
+            if (h.k == 1) {
+              if (h.ones) {
+                for (auto& m : hs) E.srelease(m);
+                hs.clear();
+                ps.clear();
+                base = p;
+              }
+              continue;
+            }
+            hs.push_back(h);
+            ps.push_back((uint32_t)p);
+          }
+          const uint32_t dflt = base >= 0 ? P.vaux[in.p1 + 2 * base + 1] : in.p0;
+          std::map<std::pair<size_t, size_t>, Mask> ors;  // OR of hs[a..b]
+          auto run_mask = [&](size_t a, size_t b) -> Mask {
+            if (a == b) return hs[a];
+            auto it = ors.find({a, b});
+            if (it != ors.end()) return it->second;
+            const Mask prev = b - 1 == a ? hs[a] : ors.at({a, b - 1});
+            const Mask m = mop("or", prev, hs[b]);
+            ors[{a, b}] = m;
+            return m;
+          };
+          std::vector<Limb> res(Ld);
+          for (uint32_t j = 0; j < Ld; j++) {
+            if (!(need[d] >> j & 1)) continue;
+            Limb c = limb(dflt, j);
+            E.retain(c);
+            for (size_t a = 0; a < ps.size();) {
+              const Limb v = limb(P.vaux[in.p1 + 2 * ps[a] + 1], j);
+              size_t b = a;
+              while (b + 1 < ps.size() && limb(P.vaux[in.p1 + 2 * ps[b + 1] + 1], j) == v) b++;
+              if (!(v == c)) {
+                // run_mask memoises ORs; every run ending at b extends the one ending at b - 1
+                for (size_t q = a + 1; q < b; q++) run_mask(a, q);
+                const Mask m = run_mask(a, b);
+                const Limb t = v3(v), f = v3(c);
+                const Limb r = fresh();
+                E.valu("v_cndmask_b32_e64 " + VL(r) + ", " + src(f) + ", " + src(t) + ", " + SP(m.s), {m.s, m.s + 1});
+                drop(t);
+                drop(f);
+                drop(c);
+                c = r;
+              }
+              a = b + 1;
+            }
+            res[j] = c;
+          }
+          for (auto& kv : ors) E.srelease(kv.second);
+          for (auto& m : hs) E.srelease(m);
+          set(d, res);
+          break;
+        }
         std::vector<Limb> cur(Ld);
         for (uint32_t j = 0; j < Ld; j++) {
           if (!(need[d] >> j & 1)) continue;
@@ -3361,12 +3707,35 @@ struct Gen {
   }
   // a & ~b
   Mask mop_andn(const Mask& a, const Mask& b) {
+    if (a.k == 2 && b.k == 2) {  // one s_andn2_b64
+      Mask m;
+      m.k = 2;
+      m.s = E.salloc();
+      E.salu("s_andn2_b64 " + SP(m.s) + ", " + SP(a.s) + ", " + SP(b.s), {m.s, m.s + 1});
+      return m;
+    }
     const Mask nb = mnot(b);
     const Mask r = mop("and", a, nb);
     E.srelease(nb);
     return r;
   }
 
+  // MYTHGPU_JIT_ASM_NO_GEN_WANT=1: every MIXED coordinate generated whole
+  static bool no_gen_want() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_GEN_WANT");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
+  // MYTHGPU_JIT_ASM_NO_LOOKUP_RUNS=1: a lookup's select chain one prior at a time
+  static bool no_lookup_runs() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_LOOKUP_RUNS");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
   // MYTHGPU_JIT_ASM_NO_BOOL_LOOKUP=1: a Bool lookup selects limbs like any other
   static bool no_bool_lookup() {
     static const bool on = [] {
@@ -3398,17 +3767,17 @@ struct Gen {
     xcache.clear();
     xby.clear();
     litcache.clear();
+    lit_last.clear();
+    x_last.clear();
+    eq_last.clear();
     E.on_free = [this](uint32_t g) { xcache_free(g); };
-    E.on_pressure = [this]() {
-      const bool any = !xcache.empty() || !litcache.empty();
-      xcache_clear();
-      litcache_clear();
-      return any;
-    };
+    E.on_pressure = [this]() { return evict_one(); };
+    E.on_spressure = [this]() { return spill_mask(); };
     lvn_on = true;
     static const bool annotate = getenv("MYTHGPU_JIT_ASM_ANNOTATE") != nullptr;
     for (size_t k = 0; k < code.size(); k++) {
       const Instr& in = code[k];
+      cur_k = k;
       if (annotate)
         E.o << "  ; vcode " << k << " op " << in.op << " w " << in.wd << " dst " << in.dst << " a " << in.a << " b " << in.b
             << "\n";
@@ -3465,6 +3834,7 @@ struct Gen {
     lvn_on = false;
     E.on_free = nullptr;
     E.on_pressure = nullptr;
+    E.on_spressure = nullptr;
   }
 
   // ---------------------------------------------------------------------------------------
@@ -3627,6 +3997,7 @@ struct Gen {
   std::string kernel_eval(const std::string& name) {
     E = Emitter();
     E.nlab = labels;
+    E.vsoft = vsoft;
     census.clear();
     E.vfirst = kV0 + (int)pool.size();
     E.vhigh = E.vfirst;
@@ -3745,6 +4116,7 @@ struct Gen {
   std::string kernel(const std::string& name) {
     E = Emitter();
     E.nlab = labels;
+    E.vsoft = vsoft;
     census.clear();
     E.vfirst = kV0 + (int)pool.size();
     E.vhigh = E.vfirst;
@@ -4041,6 +4413,13 @@ std::string metadata_eval(int vg, int sg) {
   return o.str();
 }
 
+// the most VGPRs a kernel of `v` VGPRs may use and keep its waves per SIMD (512 per lane, in
+// granules of 8), and never below 96 (5 waves)
+static int occupancy_step(int v) {
+  const int waves = std::max(1, std::min(8, 512 / ((std::max(v, 1) + 7) / 8 * 8)));
+  return std::max(96, std::min(256, 512 / waves / 8 * 8));
+}
+
 int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const std::vector<uint32_t>& gconsts,
                    uint32_t kernels, std::string& out, std::string& err) {
   try {
@@ -4055,11 +4434,23 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
       // the registers the kernel's occupancy step leaves (C2: 44 rows at 4 waves per SIMD; C4: ~40 at 2).
       // MYTHGPU_JIT_ASM_PREFETCH fixes the depth instead.
       g.depth = Gen::prefetch_env() ? Gen::prefetch_env() : 8u;
-      std::string ks = g.kernel_eval("mgj_eval");
+      // the cache-free kernel's VGPRs set the occupancy step; the cached kernels stay within it
+      g.caches = false;
+      std::string ks;
+      int nv;
+      try {
+        ks = g.kernel_eval("mgj_eval");
+        nv = g.meta_vgpr["mgj_eval"];
+      } catch (const AsmFail&) {  // as for the search kernel: no soft limit
+        nv = 256;
+      }
+      const int waves = std::max(1, std::min(8, 512 / ((nv + 7) / 8 * 8)));
+      const int budget = std::min(256, 512 / waves / 8 * 8);
+      g.caches = true;
+      g.vsoft = budget;
+      g.labels = 0;
+      ks = g.kernel_eval("mgj_eval");
       if (!Gen::prefetch_env()) {
-        const int nv = g.meta_vgpr["mgj_eval"];
-        const int waves = std::max(1, std::min(8, 512 / ((nv + 7) / 8 * 8)));
-        const int budget = std::min(256, 512 / waves / 8 * 8);
         for (int d = std::min(60, 8 + budget - nv); d > 8; d -= 4) {
           g.depth = (uint32_t)d;
           g.labels = 0;
@@ -4096,21 +4487,33 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
       return MG_OK;
     }
     g.analyse();
-    // pass 1 counts the literals the kernel moves into VGPRs; pass 2 pools the most used ones, as long
-    // as the kernel stays within 96 VGPRs (5 waves per SIMD)
+    // pass 1, without the value caches, counts the literals the kernel moves into VGPRs and its VGPRs;
+    // pass 2 pools the most used literals and runs the caches within the occupancy step pass 1 reached
+    // (at least 96 VGPRs, 5 waves per SIMD)
     g.gen_kernel = false;
-    std::string ks = g.kernel("mgj_search");
-    if (!getenv("MYTHGPU_JIT_ASM_NOPOOL")) {
+    g.caches = false;
+    std::string ks;
+    int v0;
+    try {
+      ks = g.kernel("mgj_search");
+      v0 = g.meta_vgpr["mgj_search"];
+    } catch (const AsmFail&) {
+      // out of VGPRs without the caches (shared XOR limbs relieve pressure): no soft limit then
+      v0 = 256;
+      g.census.clear();
+    }
+    g.caches = true;
+    g.vsoft = occupancy_step(v0);
+    {
       std::vector<std::pair<uint32_t, uint32_t>> by;  // (count, literal)
-      for (const auto& kv : g.census)
-        if (kv.second >= 2) by.push_back({kv.second, kv.first});
+      if (!getenv("MYTHGPU_JIT_ASM_NOPOOL"))
+        for (const auto& kv : g.census)
+          if (kv.second >= 2) by.push_back({kv.second, kv.first});
       std::sort(by.begin(), by.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
-      const int room = std::max(0, 96 - g.meta_vgpr["mgj_search"]);
+      const int room = std::max(0, std::min(96, g.vsoft) - v0);
       for (size_t i = 0; i < by.size() && (int)i < room; i++) g.pool[by[i].second] = kV0 + (int)i;
-      if (!g.pool.empty()) {
-        g.labels = 0;
-        ks = g.kernel("mgj_search");
-      }
+      g.labels = 0;
+      ks = g.kernel("mgj_search");
     }
     o << ks;
     const bool with_gen = (kernels & JIT_GEN) != 0;

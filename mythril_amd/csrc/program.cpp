@@ -15,8 +15,10 @@
 
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <set>
+#include <tuple>
 #include <cstdio>
 #include <cstdlib>
 
@@ -240,7 +242,10 @@ std::vector<VInstr> prune_guarded_lookups(const std::vector<VInstr>& code_in, si
 // selects too when the LOOKUP goes; a compare of a
 // value with itself is a literal, and a pair the program already compares (an EQ, or a LOOKUP key
 // test: LLVM's CSE and the first tier's difference cache share those) is counted free.
-// The same for an ITE result (a lookup of one prior).  MYTHGPU_EQ_PUSHDOWN=0: off.
+// The same for an ITE result (a lookup of one prior), and for the ordered compares (ULT, ULE, SLT,
+// SLE) of a lookup or ITE with a literal: CMP(ITE(c, a, b), K) -> ITE(c, CMP(a, K), CMP(b, K)), operand
+// order kept — a storage read's bounds check then selects Bools instead of 256-bit words, and its
+// literal arms fold.  MYTHGPU_EQ_PUSHDOWN=0: off.
 std::vector<VInstr> push_eq_into_lookup(const std::vector<VInstr>& code, std::vector<uint32_t>& vwidth,
                                         std::vector<uint32_t>& consts, bool* changed) {
   static const bool on = [] {
@@ -254,6 +259,9 @@ std::vector<VInstr> push_eq_into_lookup(const std::vector<VInstr>& code, std::ve
   std::vector<uint32_t> uses(nv, 0);
   std::vector<int32_t> defk(nv, -1);
   std::map<std::pair<uint32_t, uint32_t>, uint32_t> eq_of;  // compared pair -> EQ result (NONE: a key test)
+  // ordered compares this pass created: (op, a, b) -> result (defined before any later reader: each
+  // replacement list is emitted at its compare's place, and the map only grows along the list)
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> ord_of;
   auto pair = [](uint32_t a, uint32_t b) { return a < b ? std::make_pair(a, b) : std::make_pair(b, a); };
   for (size_t k = 0; k < code.size(); k++) {
     const VInstr& c = code[k];
@@ -266,17 +274,24 @@ std::vector<VInstr> push_eq_into_lookup(const std::vector<VInstr>& code, std::ve
       for (size_t q = 0; q + 1 < c.prior.size(); q += 2) eq_of.emplace(pair(c.a, c.prior[q]), NONE);
   }
   std::vector<char> drop(code.size(), 0);
-  std::vector<std::vector<VInstr>> at(code.size());  // replacement of an EQ
+  std::vector<std::vector<VInstr>> at(code.size());  // replacement of a compare
+  auto literal = [&](uint32_t v) { return v < nv && defk[v] >= 0 && code[(size_t)defk[v]].op == K_CONST; };
   for (size_t k = 0; k < code.size(); k++) {
     const VInstr& e = code[k];
-    if (e.op != K_EQ || e.dst == NONE) continue;
+    // EQ, and the ordered compares against a literal (LASER's bounds checks of a storage read:
+    // ULE(ITE(EQ(key, k1), v1, ... LOOKUP ...), 21)); their operand order is kept
+    const bool ordered = e.op == K_ULT || e.op == K_ULE || e.op == K_SLT || e.op == K_SLE;
+    if ((e.op != K_EQ && !ordered) || e.dst == NONE) continue;
+    if (ordered && !literal(e.a) && !literal(e.b)) continue;
     uint32_t lk = NONE, x = NONE;
+    int lside = 0;  // the lookup is operand a (0) or b (1)
     for (int side = 0; side < 2 && lk == NONE; side++) {
       const uint32_t s = side ? e.b : e.a, o = side ? e.a : e.b;
       if (s < nv && defk[s] >= 0 && (code[(size_t)defk[s]].op == K_LOOKUP || code[(size_t)defk[s]].op == K_ITE) &&
           !drop[(size_t)defk[s]]) {
         lk = s;
         x = o;
+        lside = side;
       }
     }
     if (lk == NONE) continue;
@@ -289,12 +304,15 @@ std::vector<VInstr> push_eq_into_lookup(const std::vector<VInstr>& code, std::ve
     else
       for (uint32_t q = 0; q < n; q++) vals.push_back(L.prior[2 * q + 1]);
     vals.push_back(dflt);
+    // a compare of two literals folds in both tiers (the ITE's literal arm against a literal x); an
+    // ordered compare is a borrow chain (one instruction per limb), an EQ a XOR and an OR per limb
+    const uint64_t per = ordered ? (uint64_t)Lw : 2ull * Lw;
     uint64_t cost_new = n;
     for (uint32_t v : vals)
-      if (v != x && !eq_of.count(pair(v, x))) cost_new += 2ull * Lw;
+      if (v != x && !(!ordered && eq_of.count(pair(v, x))) && !(literal(v) && literal(x))) cost_new += per;
     // a lookup read elsewhere too stays: then only the compare goes
     const bool single = uses[lk] == 1;
-    const uint64_t cost_old = (single ? (uint64_t)n * Lw : 0ull) + 2ull * Lw;
+    const uint64_t cost_old = (single ? (uint64_t)n * Lw : 0ull) + per;
     // where the default is x itself (EQ(d, x) a literal 1) the rewrite is kept even against the cost
     // estimate, which counts every limb as live: the priors' values there are CONCATs with literal
     // tails, whose compares fold (C4 on the O3 kernel: 89.4 -> 97.7 G/s; the first tier -2.7 %,
@@ -303,18 +321,58 @@ std::vector<VInstr> push_eq_into_lookup(const std::vector<VInstr>& code, std::ve
       const char* g = getenv("MYTHGPU_EQ_PUSHDOWN");
       return !(g && g[0] == '1');
     }();
-    if (cost_new >= cost_old && !(force && dflt == x)) continue;
+    // Against a literal, a compare goes through selects whose other arms fold (LLVM's compare-of-select
+    // folding does the same to the O3 kernels): the compares left to compute along the pushed chains —
+    // through ITEs and LOOKUPs, however many readers they have, as each reader is pushed in turn — are
+    // counted, and up to six are taken for the wide selects that die once every reader is pushed
+    // (C4's storage reads: ITE(EQ(k, k1), 21, ITE(EQ(k, k2), 29, LOOKUP(...))) compared with 13 and 21).
+    // the distinct values left to compare (a leaf reached along several chains is compared once)
+    std::set<uint32_t> leaves;
+    std::function<void(uint32_t, int)> left = [&](uint32_t v, int depth) {
+      if (leaves.size() > 6) return;
+      if (v == x || (literal(v) && literal(x)) || (!ordered && eq_of.count(pair(v, x)))) return;
+      if (depth > 0 && v < nv && defk[v] >= 0 && !drop[(size_t)defk[v]]) {
+        const VInstr& D = code[(size_t)defk[v]];
+        if (D.op == K_ITE) {
+          left(D.b, depth - 1);
+          left(D.c, depth - 1);
+          return;
+        }
+        if (D.op == K_LOOKUP) {
+          left(D.p0, depth - 1);
+          for (uint32_t q = 0; q < D.c; q++) left(D.prior[2 * q + 1], depth - 1);
+          return;
+        }
+      }
+      leaves.insert(v);
+    };
+    if (literal(x))
+      for (uint32_t v : vals) left(v, 8);
+    if (cost_new >= cost_old && !(force && dflt == x) && !(literal(x) && leaves.size() <= 6)) continue;
     std::vector<VInstr> rep;
     uint32_t one = NONE;
+    uint32_t zero = NONE;
     auto eq_id = [&](uint32_t v) -> uint32_t {
-      if (v == x) {
-        if (one == NONE) {
-          one = (uint32_t)vwidth.size();
+      if (v == x) {  // x = x, x <= x: 1; x < x: 0
+        const bool t = e.op == K_EQ || e.op == K_ULE || e.op == K_SLE;
+        uint32_t& c = t ? one : zero;
+        if (c == NONE) {
+          c = (uint32_t)vwidth.size();
           vwidth.push_back(1);
-          rep.push_back(VInstr{K_CONST, 1, one, NONE, NONE, NONE, (uint32_t)consts.size(), 0, {}});
-          consts.push_back(1u);
+          rep.push_back(VInstr{K_CONST, 1, c, NONE, NONE, NONE, (uint32_t)consts.size(), 0, {}});
+          consts.push_back(t ? 1u : 0u);
         }
-        return one;
+        return c;
+      }
+      if (ordered) {
+        const uint32_t ca = lside ? x : v, cb = lside ? v : x;
+        auto it = ord_of.find({e.op, ca, cb});
+        if (it != ord_of.end()) return it->second;  // the same compare, pushed along another chain
+        const uint32_t id = (uint32_t)vwidth.size();
+        vwidth.push_back(1);
+        rep.push_back(VInstr{e.op, 1, id, ca, cb, NONE, e.p0, e.p1, {}});
+        ord_of[{e.op, ca, cb}] = id;
+        return id;
       }
       auto it = eq_of.find(pair(v, x));
       if (it != eq_of.end() && it->second != NONE && defk[it->second] >= 0 && (size_t)defk[it->second] < k)

@@ -571,6 +571,9 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                 else:
                     idx, nh = engine.search(prog, gh, seed, start, n, early_exit=True, assign=assign)
                 dt = time.perf_counter() - tl
+                if ticket_asm is not None:  # the launches the first tier's compile waited behind
+                    timing["asm_wait_launches"] = timing.get("asm_wait_launches", 0) + 1
+                    timing["asm_wait_launch_max_ms"] = max(timing.get("asm_wait_launch_max_ms", 0.0), dt * 1e3)
                 rate = n / dt if dt > 0 else None
                 scanned += n
                 start += n

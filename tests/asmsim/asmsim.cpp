@@ -3,6 +3,7 @@
 #include "asmsim.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <deque>
 #include <sstream>
@@ -21,8 +22,11 @@ namespace {
   X(s_orn2_b64) X(s_nor_b64) X(s_xnor_b64) X(s_not_b32) X(s_not_b64) X(s_min_u32) X(s_max_u32) X(s_cselect_b32)   \
   X(s_cselect_b64) X(s_cmp_eq_u32) X(s_cmp_lg_u32) X(s_cmp_lt_u32) X(s_cmp_le_u32) X(s_cmp_gt_u32)                 \
   X(s_cmp_ge_u32) X(s_cmp_eq_u64) X(s_cmp_lg_u64) X(s_ff1_i32_b64) X(s_bcnt1_i32_b64) X(s_ff1_i32_b32)           \
-  X(s_flbit_i32_b32) X(s_bfe_u32)                                                                                 \
-  X(s_cbranch_scc0) X(s_cbranch_scc1) X(s_cbranch_vccz) X(s_cbranch_vccnz) X(s_cbranch_execz) X(s_branch)         \
+  X(s_flbit_i32_b32) X(s_brev_b32) X(s_bfe_i32) X(s_cmpk_eq_i32) X(s_cmpk_lg_i32) X(s_cmpk_eq_u32) X(s_cmpk_lg_u32) X(s_getpc_b64) X(s_movk_i32) X(s_and_saveexec_b64) X(s_or_saveexec_b64) X(s_andn2_saveexec_b64)            \
+  X(s_bitcmp0_b32) X(s_bitcmp1_b32) X(s_cmp_eq_i32) X(s_cmp_lg_i32) X(s_cmp_lt_i32) X(s_cmp_gt_i32)               \
+  X(s_cmp_le_i32) X(s_cmp_ge_i32) X(s_min_i32) X(s_max_i32) X(s_sext_i32_i16) X(s_mul_hi_i32) X(s_bfe_u32)        \
+  X(s_cbranch_scc0) X(s_cbranch_scc1) X(s_cbranch_vccz) X(s_cbranch_vccnz) X(s_cbranch_execz)                     \
+  X(s_cbranch_execnz) X(s_branch)                                                                                 \
   X(s_nop) X(s_waitcnt) X(s_barrier) X(s_endpgm)                                                                  \
   X(s_load_dword) X(s_load_dwordx2) X(s_load_dwordx4) X(s_load_dwordx8)                                           \
   X(v_mov_b32) X(v_add_u32) X(v_sub_u32) X(v_subrev_u32) X(v_add_co_u32) X(v_addc_co_u32) X(v_sub_co_u32)        \
@@ -35,9 +39,14 @@ namespace {
   X(v_and_or_b32) X(v_lshl_add_u32) X(v_add_lshl_u32) X(v_bitop3_b32) X(v_readfirstlane_b32) X(v_lshlrev_b64)     \
   X(v_lshrrev_b64) X(v_ffbh_u32) X(v_ffbl_b32) X(v_perm_b32) X(v_mad_u32_u24) X(v_mad_u64_u32) X(v_bfi_b32)       \
   X(v_cvt_f32_u32) X(v_rcp_iflag_f32) X(v_cvt_u32_f32) X(v_mul_f32) X(v_readlane_b32) X(v_writelane_b32)          \
+  X(v_mov_b64) X(v_mbcnt_lo_u32_b32) X(v_mbcnt_hi_u32_b32) X(v_lshl_add_u64) X(v_rcp_f32) X(v_fmamk_f32)          \
+  X(v_ldexp_f32) X(v_cvt_f32_ubyte0) X(v_trunc_f32) X(v_sub_f32) X(v_add_f32) X(v_fma_f32) X(v_fmac_f32)          \
+  X(v_madak_f32) X(v_cvt_f32_ubyte1) X(v_cvt_f32_ubyte2) X(v_cvt_f32_ubyte3) X(v_bcnt_u32_b32) X(v_max_i32)       \
+  X(v_min_i32) X(v_bfrev_b32) X(v_alignbyte_b32) X(v_xor3_b32) X(v_ashrrev_i64) X(v_mul_hi_i32) X(v_add_i32) X(v_sub_i32)                      \
   X(global_load_dword) X(global_load_dwordx2) X(global_load_dwordx4) X(global_store_byte) X(global_store_dword)  \
-  X(global_atomic_umin_x2) X(global_atomic_add_x2) X(ds_read_b32) X(ds_write_b32) X(ds_read_b64) X(ds_write_b64)  \
-  X(ds_read2_b32)
+  X(global_atomic_umin_x2) X(global_atomic_add_x2) X(flat_atomic_umin_x2) X(flat_atomic_add_x2)                  \
+  X(ds_read_b32) X(ds_write_b32) X(ds_read_b64) X(ds_write_b64)                                                   \
+  X(ds_read2_b32) X(ds_read_b128) X(ds_write_b128) X(ds_min_u64) X(ds_add_u64) X(ds_add_rtn_u32) X(ds_write2_b32)
 
 enum Op {
 #define X_ENUM(n) OP_##n,
@@ -130,11 +139,30 @@ Opd operand(const std::string& t0) {
     o.n = 2;
     return o;
   }
+  if (t == "exec_lo" || t == "exec_hi") {
+    o.k = O_EXEC;
+    o.r = t == "exec_hi";
+    o.n = 1;
+    return o;
+  }
   if (t == "off") {
     o.k = O_OFF;
     return o;
   }
   if (reg('v', O_V) || reg('s', O_S)) return o;
+  // floating-point inline constants (their f32 bit patterns, as 32-bit operands read them)
+  static const std::pair<const char*, uint32_t> kF[] = {{"0.5", 0x3F000000u},  {"-0.5", 0xBF000000u},
+                                                        {"1.0", 0x3F800000u},  {"-1.0", 0xBF800000u},
+                                                        {"2.0", 0x40000000u},  {"-2.0", 0xC0000000u},
+                                                        {"4.0", 0x40800000u},  {"-4.0", 0xC0800000u},
+                                                        {"0.15915494", 0x3E22F983u}};
+  for (const auto& f : kF)
+    if (t == f.first) {
+      o.k = O_IMM;
+      o.imm = f.second;
+      o.inl = true;
+      return o;
+    }
   int64_t v;
   if (parse_int(t, v)) {
     o.k = O_IMM;
@@ -154,6 +182,7 @@ Module parse(const std::string& text) {
   std::istringstream in(text);
   std::string line;
   bool meta = false;
+  int64_t pending_pc = -1;
   std::string cur_kd;
   int cur_tag = -1;
   while (std::getline(in, line)) {
@@ -176,6 +205,21 @@ Module parse(const std::string& text) {
     }
     if (meta) continue;
     if (t[0] == '.') {
+      if (t.rfind(".asmsim_pc ", 0) == 0) {
+        int64_t v;
+        if (!parse_int(trim(t.substr(11)), v)) err("bad .asmsim_pc " + t);
+        pending_pc = v;
+        continue;
+      }
+      if (t.rfind(".asmsim_image ", 0) == 0) {
+        FILE* f = fopen(trim(t.substr(14)).c_str(), "rb");
+        if (!f) err("cannot read " + t);
+        uint8_t buf[65536];
+        size_t n;
+        while ((n = fread(buf, 1, sizeof buf, f)) > 0) m.image.insert(m.image.end(), buf, buf + n);
+        fclose(f);
+        continue;
+      }
       if (t.rfind(".amdhsa_kernel ", 0) == 0) cur_kd = trim(t.substr(15));
       if (t.rfind(".amdhsa_group_segment_fixed_size", 0) == 0 && !cur_kd.empty())
         m.kernels[cur_kd].lds_bytes = (uint32_t)atol(trim(t.substr(32)).c_str());
@@ -192,6 +236,8 @@ Module parse(const std::string& text) {
     Ins ins;
     ins.text = trim(raw);
     ins.tag = cur_tag;
+    ins.pc = pending_pc;
+    pending_pc = -1;
     const size_t sp = t.find_first_of(" \t");
     std::string mn = sp == std::string::npos ? t : t.substr(0, sp);
     std::string rest = sp == std::string::npos ? "" : trim(t.substr(sp));
@@ -226,7 +272,8 @@ Module parse(const std::string& text) {
       continue;
     }
     if (ins.op == OP_s_cbranch_scc0 || ins.op == OP_s_cbranch_scc1 || ins.op == OP_s_branch ||
-        ins.op == OP_s_cbranch_vccz || ins.op == OP_s_cbranch_vccnz || ins.op == OP_s_cbranch_execz) {
+        ins.op == OP_s_cbranch_vccz || ins.op == OP_s_cbranch_vccnz || ins.op == OP_s_cbranch_execz ||
+        ins.op == OP_s_cbranch_execnz) {
       fix.push_back({m.code.size(), rest});
       m.code.push_back(ins);
       continue;
@@ -260,10 +307,19 @@ Module parse(const std::string& text) {
           ins.offset = v;
         } else if (md == "sc0" || md == "sc1" || md == "nt") {
           // cache policy bits: no effect on a single-device simulation
-        } else if (md.rfind("src1_sel:", 0) == 0) {
+        } else if (md.rfind("offset0:", 0) == 0 || md.rfind("offset1:", 0) == 0) {
+          int64_t v;
+          if (!parse_int(md.substr(8), v)) err("bad offset " + ins.text);
+          (md[6] == '0' ? ins.offset0 : ins.offset1) = (int)v;
+        } else if (md.rfind("src0_sel:", 0) == 0 || md.rfind("src1_sel:", 0) == 0) {
           const std::string s = md.substr(9);
-          if (s == "WORD_1") ins.sdwa_src1_word1 = 1;
-          else if (s != "DWORD") err("unsupported sdwa select " + ins.text);
+          static const char* kSel[] = {"DWORD", "WORD_0", "WORD_1", "BYTE_0", "BYTE_1", "BYTE_2", "BYTE_3"};
+          int k = -1;
+          for (int q = 0; q < 7; q++)
+            if (s == kSel[q]) k = q;
+          if (k < 0) err("unsupported sdwa select " + ins.text);
+          ins.sdwa_sel[md[3] - '0'] = k;
+          if (md[3] == '1' && k == 2) ins.sdwa_src1_word1 = 1;
         } else if (md.rfind("bitop3:", 0) == 0) {
           int64_t v;
           if (!parse_int(md.substr(7), v) || v < 0 || v > 255) err("bad bitop3 table " + ins.text);
@@ -349,6 +405,7 @@ struct Ctx {
   std::vector<uint8_t> lds;
   Stats* st;
   int block = 0;
+  uint64_t image_base = 0;
 };
 
 [[noreturn]] void fail(const Wave& w, const Ctx& c, const Ins& in, const std::string& what) {
@@ -381,7 +438,7 @@ uint32_t sread(Wave& w, const Ctx& c, const Ins& in, const Opd& o) {
   switch (o.k) {
     case O_S: chk_s_read(w, c, in, o.r); return w.s[o.r];
     case O_IMM: return (uint32_t)o.imm;
-    case O_EXEC: return (uint32_t)w.exec;
+    case O_EXEC: return (uint32_t)(o.r ? w.exec >> 32 : w.exec);
     default: fail(w, c, in, "bad scalar operand");
   }
 }
@@ -393,7 +450,9 @@ uint64_t sread64(Wave& w, const Ctx& c, const Ins& in, const Opd& o) {
       chk_s_read(w, c, in, o.r + 1);
       return (uint64_t)w.s[o.r] | ((uint64_t)w.s[o.r + 1] << 32);
     case O_IMM:
-      if (!o.inl) fail(w, c, in, "32-bit literal in a 64-bit scalar operand");
+      // a 32-bit literal below 2^31 reads the same zero- or sign-extended (the only kind the tier
+      // emits none of; the O3 tier's compiler does, e.g. s_mov_b64 s[4:5], 0x248)
+      if (!o.inl && (o.imm >> 31) != 0) fail(w, c, in, "32-bit literal with bit 31 set in a 64-bit scalar operand");
       return (uint64_t)(int64_t)(int32_t)(uint32_t)o.imm;
     case O_EXEC: return w.exec;
     default: fail(w, c, in, "bad scalar operand");
@@ -401,7 +460,8 @@ uint64_t sread64(Wave& w, const Ctx& c, const Ins& in, const Opd& o) {
 }
 void swrite(Wave& w, const Ctx& c, const Ins& in, const Opd& o, uint32_t v) {
   if (o.k == O_EXEC) {
-    w.exec = (w.exec & ~0xFFFFFFFFull) | v;
+    if (o.r) w.exec = (w.exec & 0xFFFFFFFFull) | ((uint64_t)v << 32);
+    else w.exec = (w.exec & ~0xFFFFFFFFull) | v;
     return;
   }
   if (o.k != O_S) fail(w, c, in, "bad scalar destination");
@@ -478,7 +538,8 @@ Src vsrc(Wave& w, const Ctx& c, const Ins& in, const Opd& o, bool wide, ValuChec
       s.k = wide && o.inl ? (uint64_t)(int64_t)(int32_t)(uint32_t)o.imm : (uint32_t)o.imm;
       return s;
     case O_EXEC:
-      s.k = wide ? w.exec : (uint32_t)w.exec;
+      vc.sg(126);
+      s.k = wide ? w.exec : (uint32_t)(o.r ? w.exec >> 32 : w.exec);
       return s;
     default:
       fail(w, c, in, "bad VALU operand");
@@ -534,6 +595,26 @@ void retire(Wave& w, std::deque<Pend>& q, int keep) {
   }
 }
 
+// an SDWA source select (Ins::sdwa_sel)
+uint32_t sdwa(uint32_t x, int sel) {
+  switch (sel) {
+    case 0: return x;
+    case 1: return x & 0xFFFFu;
+    case 2: return x >> 16;
+    default: return (x >> (8 * (sel - 3))) & 0xFFu;
+  }
+}
+float f32(uint32_t x) {
+  float f;
+  memcpy(&f, &x, 4);
+  return f;
+}
+uint32_t u32f(float f) {
+  uint32_t x;
+  memcpy(&x, &f, 4);
+  return x;
+}
+
 uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c, uint32_t t) {
   uint32_t r = 0;
   for (int i = 0; i < 32; i++) {
@@ -557,7 +638,10 @@ bool step(Wave& w, Ctx& c) {
   const int op = in.op;
   // ---- scalar ------------------------------------------------------------------------------
   if (op <= OP_s_bfe_u32) {
-    if (c.st) c.st->salu++;
+    if (c.st) {
+      c.st->salu++;
+      if (in.tag >= 0) c.st->salu_by_tag[in.tag]++;
+    }
     uint64_t r = 0;
     switch (op) {
       case OP_s_mov_b32: need(2); swrite(w, c, in, a[0], sread(w, c, in, a[1])); break;
@@ -658,6 +742,83 @@ bool step(Wave& w, Ctx& c) {
       case OP_s_ff1_i32_b32: { need(2); const uint32_t x = sread(w, c, in, a[1]); swrite(w, c, in, a[0], x ? (uint32_t)__builtin_ctz(x) : 0xFFFFFFFFu); break; }
       case OP_s_flbit_i32_b32: { need(2); const uint32_t x = sread(w, c, in, a[1]); swrite(w, c, in, a[0], x ? (uint32_t)__builtin_clz(x) : 0xFFFFFFFFu); break; }
       case OP_s_bcnt1_i32_b64: { need(2); r = (uint32_t)__builtin_popcountll(sread64(w, c, in, a[1])); w.scc = r != 0; swrite(w, c, in, a[0], (uint32_t)r); break; }
+      case OP_s_bfe_i32: {
+        need(3);
+        const uint32_t x = sread(w, c, in, a[1]), f = sread(w, c, in, a[2]);
+        const uint32_t off = f & 31, wd = (f >> 16) & 127;
+        int32_t v = 0;
+        if (wd) {
+          const uint32_t u = wd >= 32 ? (x >> off) : ((x >> off) & ((1u << wd) - 1u));
+          v = wd >= 32 ? (int32_t)u : (int32_t)(u << (32 - wd)) >> (32 - wd);
+        }
+        w.scc = v != 0;
+        swrite(w, c, in, a[0], (uint32_t)v);
+        break;
+      }
+      case OP_s_cmpk_eq_i32: case OP_s_cmpk_lg_i32: case OP_s_cmpk_eq_u32: case OP_s_cmpk_lg_u32: {
+        // SOPK: a 16-bit immediate, sign-extended for the _i32 forms
+        need(2);
+        const uint32_t x = sread(w, c, in, a[0]), k16 = (uint32_t)a[1].imm & 0xFFFFu;
+        const uint32_t k = (op == OP_s_cmpk_eq_i32 || op == OP_s_cmpk_lg_i32) ? (uint32_t)(int32_t)(int16_t)k16 : k16;
+        w.scc = (op == OP_s_cmpk_eq_i32 || op == OP_s_cmpk_eq_u32) ? x == k : x != k;
+        break;
+      }
+      case OP_s_brev_b32: {
+        need(2);
+        uint32_t x = sread(w, c, in, a[1]), y = 0;
+        for (int i = 0; i < 32; i++) y |= ((x >> i) & 1u) << (31 - i);
+        swrite(w, c, in, a[0], y);
+        break;
+      }
+      case OP_s_getpc_b64:
+        // the address of the next instruction, in the image's buffer
+        need(1);
+        if (in.pc < 0 || !c.image_base) fail(w, c, in, "s_getpc_b64 without .asmsim_pc / .asmsim_image");
+        swrite64(w, c, in, a[0], c.image_base + (uint64_t)in.pc + 4);
+        break;
+      case OP_s_movk_i32: need(2); swrite(w, c, in, a[0], (uint32_t)(int32_t)(int16_t)(uint16_t)sread(w, c, in, a[1])); break;
+      case OP_s_and_saveexec_b64: case OP_s_or_saveexec_b64: case OP_s_andn2_saveexec_b64: {
+        need(2);
+        const uint64_t x = sread64(w, c, in, a[1]), e = w.exec;
+        swrite64(w, c, in, a[0], e);
+        r = op == OP_s_and_saveexec_b64 ? (x & e) : op == OP_s_or_saveexec_b64 ? (x | e) : (x & ~e);
+        w.exec = r;
+        w.scc = r != 0;
+        break;
+      }
+      case OP_s_bitcmp0_b32: case OP_s_bitcmp1_b32: {
+        need(2);
+        const uint32_t bit = sread(w, c, in, a[0]) >> (sread(w, c, in, a[1]) & 31) & 1u;
+        w.scc = op == OP_s_bitcmp0_b32 ? bit == 0 : bit == 1;
+        break;
+      }
+      case OP_s_cmp_eq_i32: case OP_s_cmp_lg_i32: case OP_s_cmp_lt_i32: case OP_s_cmp_gt_i32: case OP_s_cmp_le_i32:
+      case OP_s_cmp_ge_i32: {
+        need(2);
+        const int32_t x = (int32_t)sread(w, c, in, a[0]), y = (int32_t)sread(w, c, in, a[1]);
+        switch (op) {
+          case OP_s_cmp_eq_i32: w.scc = x == y; break;
+          case OP_s_cmp_lg_i32: w.scc = x != y; break;
+          case OP_s_cmp_lt_i32: w.scc = x < y; break;
+          case OP_s_cmp_gt_i32: w.scc = x > y; break;
+          case OP_s_cmp_le_i32: w.scc = x <= y; break;
+          default: w.scc = x >= y; break;
+        }
+        break;
+      }
+      case OP_s_min_i32: case OP_s_max_i32: {
+        need(3);
+        const int32_t x = (int32_t)sread(w, c, in, a[1]), y = (int32_t)sread(w, c, in, a[2]);
+        const bool first = op == OP_s_min_i32 ? x < y : x > y;
+        w.scc = first;
+        swrite(w, c, in, a[0], (uint32_t)(first ? x : y));
+        break;
+      }
+      case OP_s_sext_i32_i16: need(2); swrite(w, c, in, a[0], (uint32_t)(int32_t)(int16_t)(uint16_t)sread(w, c, in, a[1])); break;
+      case OP_s_mul_hi_i32:
+        need(3);
+        swrite(w, c, in, a[0], (uint32_t)(((int64_t)(int32_t)sread(w, c, in, a[1]) * (int32_t)sread(w, c, in, a[2])) >> 32));
+        break;
       case OP_s_bfe_u32: {
         need(3);
         const uint32_t x = sread(w, c, in, a[1]), f = sread(w, c, in, a[2]);
@@ -684,6 +845,7 @@ bool step(Wave& w, Ctx& c) {
       return true;
     }
     case OP_s_cbranch_execz: if (!w.exec) next = in.target; w.pc = next; return true;
+    case OP_s_cbranch_execnz: if (w.exec) next = in.target; w.pc = next; return true;
     case OP_s_branch: w.pc = in.target; return true;
     case OP_s_nop: {
       need(1);
@@ -735,35 +897,121 @@ bool step(Wave& w, Ctx& c) {
         if ((uint64_t)addr + n > c.lds.size()) fail(w, c, in, "LDS access past the kernel's allocation");
         return c.lds.data() + addr;
       };
-      if (op == OP_ds_read_b32 || op == OP_ds_read_b64) {
+      // bank conflicts: per lane group, the most distinct dword addresses on one bank, less one
+      auto conflicts = [&](const Src& ad, int nd, int group, int banks, const int* order, int64_t off) {
+        if (!c.st) return;
+        for (int g0 = 0; g0 < 64; g0 += group) {
+          std::unordered_map<uint32_t, std::vector<uint32_t>> bank;
+          for (int k = 0; k < group; k++) {
+            const int l = order ? order[g0 + k] : g0 + k;
+            if (!(w.exec >> l & 1)) continue;
+            for (int q = 0; q < nd; q++) {
+              const uint32_t dw = (uint32_t)((ad.lo(l) + off) / 4) + (uint32_t)q;
+              auto& v = bank[dw % (uint32_t)banks];
+              if (std::find(v.begin(), v.end(), dw) == v.end()) v.push_back(dw);
+            }
+          }
+          size_t worst = 1;
+          for (auto& kv : bank) worst = std::max(worst, kv.second.size());
+          c.st->lds_conflict += worst - 1;
+        }
+      };
+      // ds_read_b128's lane groups (MI355X_MICROARCH.md §LDS)
+      static const int kB128[64] = {0,  1,  2,  3,  12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27,
+                                    4,  5,  6,  7,  8,  9,  10, 11, 16, 17, 18, 19, 28, 29, 30, 31,
+                                    32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59,
+                                    36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63};
+      if (op == OP_ds_read_b32 || op == OP_ds_read_b64 || op == OP_ds_read_b128 || op == OP_ds_read2_b32) {
         need(2);
-        const int nw = op == OP_ds_read_b32 ? 1 : 2;
+        const int nw = op == OP_ds_read_b32 ? 1 : op == OP_ds_read_b64 || op == OP_ds_read2_b32 ? 2 : 4;
         ValuCheck vc;
         const Src ad = vsrc(w, c, in, a[1], false, vc, true);
+        if (a[0].k != O_V || a[0].n != nw) fail(w, c, in, "LDS load destination width");
+        if (op == OP_ds_read_b32) conflicts(ad, 1, 32, 32, nullptr, in.offset);
+        else if (op == OP_ds_read_b64) conflicts(ad, 2, 32, 64, nullptr, in.offset);
+        else if (op == OP_ds_read_b128) conflicts(ad, 4, 16, 64, kB128, in.offset);
+        else {
+          conflicts(ad, 1, 32, 32, nullptr, 4 * (int64_t)in.offset0);
+          conflicts(ad, 1, 32, 32, nullptr, 4 * (int64_t)in.offset1);
+        }
+        uint32_t adr[64];  // the destination may overlap the address register
+        for (int l = 0; l < 64; l++) adr[l] = ad.lo(l);
         Pend pd;
         for (int q = 0; q < nw; q++) {
           uint32_t* d = vdst(w, c, in, a[0], q);
+          const uint32_t o = op == OP_ds_read2_b32 ? 4u * (uint32_t)(q ? in.offset1 : in.offset0)
+                                                   : (uint32_t)in.offset + 4u * q;
           for (int l = 0; l < 64; l++)
-            if (w.exec >> l & 1) memcpy(&d[l], lds_at(ad.lo(l) + (uint32_t)in.offset + 4 * q, 4), 4);
+            if (w.exec >> l & 1) memcpy(&d[l], lds_at(adr[l] + o, 4), 4);
           pd.v.push_back(a[0].r + q);
           w.vpend[a[0].r + q]++;
         }
         w.lgkm.push_back(pd);
-      } else if (op == OP_ds_write_b32 || op == OP_ds_write_b64) {
-        need(2);
-        const int nw = op == OP_ds_write_b32 ? 1 : 2;
+      } else if (op == OP_ds_write_b32 || op == OP_ds_write_b64 || op == OP_ds_write_b128 || op == OP_ds_write2_b32) {
+        const int nw = op == OP_ds_write_b32 ? 1 : op == OP_ds_write_b64 ? 2 : op == OP_ds_write2_b32 ? 2 : 4;
+        need(op == OP_ds_write2_b32 ? 3 : 2);
         ValuCheck vc;
         const Src ad = vsrc(w, c, in, a[0], false, vc, true);
-        const Src dv = vsrc(w, c, in, a[1], nw == 2, vc, true);
+        std::vector<const uint32_t*> dv;
+        if (op == OP_ds_write2_b32) {
+          for (int q = 0; q < 2; q++) {
+            const Src x = vsrc(w, c, in, a[1 + q], false, vc, true);
+            if (x.scalar) fail(w, c, in, "LDS store data is not a VGPR");
+            dv.push_back(x.vec);
+          }
+        } else {
+          if (a[1].k != O_V || a[1].n != nw) fail(w, c, in, "LDS store data width");
+          for (int q = 0; q < nw; q++) {
+            chk_v_read(w, c, in, a[1].r + q);
+            dv.push_back(w.v[a[1].r + q]);
+          }
+        }
         for (int l = 0; l < 64; l++) {
           if (!(w.exec >> l & 1)) continue;
-          const uint64_t x = dv.v64(l);
           for (int q = 0; q < nw; q++) {
-            const uint32_t y = (uint32_t)(x >> (32 * q));
-            memcpy(lds_at(ad.lo(l) + (uint32_t)in.offset + 4 * q, 4), &y, 4);
+            const uint32_t o = op == OP_ds_write2_b32 ? 4u * (uint32_t)(q ? in.offset1 : in.offset0)
+                                                      : (uint32_t)in.offset + 4u * q;
+            memcpy(lds_at(ad.lo(l) + o, 4), &dv[q][l], 4);
           }
         }
         w.lgkm.push_back(Pend{});
+      } else if (op == OP_ds_min_u64 || op == OP_ds_add_u64) {
+        need(2);
+        ValuCheck vc;
+        const Src ad = vsrc(w, c, in, a[0], false, vc, true);
+        const Src dv = vsrc(w, c, in, a[1], true, vc, true);
+        for (int l = 0; l < 64; l++) {
+          if (!(w.exec >> l & 1)) continue;
+          uint8_t* p = lds_at(ad.lo(l) + (uint32_t)in.offset, 8);
+          if ((ad.lo(l) + (uint32_t)in.offset) & 7) fail(w, c, in, "misaligned 64-bit LDS atomic");
+          uint64_t cur;
+          memcpy(&cur, p, 8);
+          cur = op == OP_ds_min_u64 ? std::min(cur, dv.v64(l)) : cur + dv.v64(l);
+          memcpy(p, &cur, 8);
+        }
+        w.lgkm.push_back(Pend{});
+      } else if (op == OP_ds_add_rtn_u32) {
+        need(3);
+        ValuCheck vc;
+        const Src ad = vsrc(w, c, in, a[1], false, vc, true);
+        const Src dv = vsrc(w, c, in, a[2], false, vc, true);
+        std::vector<uint32_t> old(64);
+        for (int l = 0; l < 64; l++) {
+          if (!(w.exec >> l & 1)) continue;
+          uint8_t* p = lds_at(ad.lo(l) + (uint32_t)in.offset, 4);
+          uint32_t cur;
+          memcpy(&cur, p, 4);
+          old[l] = cur;
+          cur += dv.lo(l);
+          memcpy(p, &cur, 4);
+        }
+        uint32_t* d = vdst(w, c, in, a[0]);
+        for (int l = 0; l < 64; l++)
+          if (w.exec >> l & 1) d[l] = old[l];
+        Pend pd;
+        pd.v.push_back(a[0].r);
+        w.vpend[a[0].r]++;
+        w.lgkm.push_back(pd);
       } else {
         fail(w, c, in, "unsupported LDS instruction");
       }
@@ -772,6 +1020,27 @@ bool step(Wave& w, Ctx& c) {
     }
     // global: vaddr + saddr (32-bit lane offsets) or a 64-bit vaddr with "off"
     const bool store = op == OP_global_store_byte || op == OP_global_store_dword;
+    if (op == OP_flat_atomic_umin_x2 || op == OP_flat_atomic_add_x2) {
+      // flat address = the buffer's address (no LDS aperture in this simulation)
+      need(2);
+      ValuCheck vc;
+      const Src av = vsrc(w, c, in, a[0], true, vc, true);
+      const Src dv = vsrc(w, c, in, a[1], true, vc, true);
+      for (int l = 0; l < 64; l++) {
+        if (!(w.exec >> l & 1)) continue;
+        const uint64_t ad = av.v64(l) + (uint64_t)in.offset;
+        if (ad & 7) fail(w, c, in, "misaligned 64-bit atomic");
+        uint64_t cur;
+        uint8_t* p = c.mem.at(ad, 8);
+        memcpy(&cur, p, 8);
+        cur = op == OP_flat_atomic_umin_x2 ? std::min(cur, dv.v64(l)) : cur + dv.v64(l);
+        memcpy(p, &cur, 8);
+      }
+      w.vm.push_back(Pend{});
+      w.lgkm.push_back(Pend{});  // a flat access counts on both counters
+      w.pc = next;
+      return true;
+    }
     const bool atomic = op == OP_global_atomic_umin_x2 || op == OP_global_atomic_add_x2;
     const bool load = !store && !atomic;
     need(3);
@@ -876,7 +1145,7 @@ bool step(Wave& w, Ctx& c) {
       uint32_t* d = vdst(w, c, in, a[0]);
       const bool sd = enc == 3;
       lanes([&](int l) {
-        const uint32_t p = x.lo(l), q = sd && in.sdwa_src1_word1 ? (y.lo(l) >> 16) : y.lo(l);
+        const uint32_t p = sd ? sdwa(x.lo(l), in.sdwa_sel[0]) : x.lo(l), q = sd ? sdwa(y.lo(l), in.sdwa_sel[1]) : y.lo(l);
         uint32_t r = 0;
         switch (op) {
           case OP_v_add_u32: r = p + q; break;
@@ -899,16 +1168,20 @@ bool step(Wave& w, Ctx& c) {
       break;
     }
     case OP_v_not_b32: case OP_v_ffbh_u32: case OP_v_ffbl_b32: case OP_v_cvt_f32_u32: case OP_v_rcp_iflag_f32:
-    case OP_v_cvt_u32_f32: {
+    case OP_v_cvt_u32_f32: case OP_v_bfrev_b32: {
       need(2);
       const Src x = vsrc(w, c, in, a[1], false, vc, vop3);
       uint32_t* d = vdst(w, c, in, a[0]);
       lanes([&](int l) {
-        const uint32_t p = x.lo(l);
+        const uint32_t p = enc == 3 ? sdwa(x.lo(l), in.sdwa_sel[0]) : x.lo(l);
         uint32_t r;
         float f;
         switch (op) {
           case OP_v_not_b32: r = ~p; break;
+          case OP_v_bfrev_b32:
+            r = 0;
+            for (int i = 0; i < 32; i++) r |= ((p >> i) & 1u) << (31 - i);
+            break;
           case OP_v_ffbh_u32: r = p ? (uint32_t)__builtin_clz(p) : 0xFFFFFFFFu; break;
           case OP_v_ffbl_b32: r = p ? (uint32_t)__builtin_ctz(p) : 0xFFFFFFFFu; break;
           case OP_v_cvt_f32_u32: f = (float)p; memcpy(&r, &f, 4); break;
@@ -1031,7 +1304,7 @@ bool step(Wave& w, Ctx& c) {
     }
     case OP_v_bfe_u32: case OP_v_bfe_i32: case OP_v_alignbit_b32: case OP_v_lshl_or_b32: case OP_v_add3_u32:
     case OP_v_or3_b32: case OP_v_xad_u32: case OP_v_and_or_b32: case OP_v_lshl_add_u32: case OP_v_add_lshl_u32:
-    case OP_v_perm_b32: case OP_v_mad_u32_u24: case OP_v_bfi_b32: {
+    case OP_v_perm_b32: case OP_v_mad_u32_u24: case OP_v_bfi_b32: case OP_v_alignbyte_b32: case OP_v_xor3_b32: {
       need(4);
       const Src x = vsrc(w, c, in, a[1], false, vc, true), y = vsrc(w, c, in, a[2], false, vc, true),
                 z = vsrc(w, c, in, a[3], false, vc, true);
@@ -1065,6 +1338,8 @@ bool step(Wave& w, Ctx& c) {
           case OP_v_add_lshl_u32: r = (p + q) << (s & 31); break;
           case OP_v_mad_u32_u24: r = (p & 0xFFFFFFu) * (q & 0xFFFFFFu) + s; break;
           case OP_v_bfi_b32: r = (p & q) | (~p & s); break;
+          case OP_v_alignbyte_b32: r = (uint32_t)((((uint64_t)p << 32) | q) >> (8 * (s & 3))); break;
+          case OP_v_xor3_b32: r = p ^ q ^ s; break;
           default: {  // v_perm_b32: byte selects from {p, q}
             const uint64_t cat = ((uint64_t)p << 32) | q;
             for (int b = 0; b < 4; b++) {
@@ -1126,6 +1401,154 @@ bool step(Wave& w, Ctx& c) {
       mask_write(w, c, in, a[1], m);
       break;
     }
+    case OP_v_readlane_b32: {
+      need(3);
+      const Src x = vsrc(w, c, in, a[1], false, vc, true);
+      const uint32_t lane = sread(w, c, in, a[2]) & 63;
+      if (a[0].k != O_S) fail(w, c, in, "readlane destination");
+      chk_s_write(w, c, in, a[0].r);
+      w.s[a[0].r] = x.lo((int)lane);
+      w.sinit[a[0].r] = true;
+      w.sw[a[0].r] = w.slot;
+      break;
+    }
+    case OP_v_writelane_b32: {
+      need(3);
+      const Src x = vsrc(w, c, in, a[1], false, vc, true);
+      const uint32_t lane = sread(w, c, in, a[2]) & 63;
+      if (a[0].k != O_V) fail(w, c, in, "writelane destination");
+      chk_v_write(w, c, in, a[0].r);
+      w.v[a[0].r][lane] = x.lo((int)lane);
+      break;
+    }
+    case OP_v_mov_b64: {
+      need(2);
+      const Src x = vsrc(w, c, in, a[1], true, vc, vop3);
+      if (a[0].k != O_V || a[0].n != 2) fail(w, c, in, "64-bit move destination");
+      uint32_t* d0 = vdst(w, c, in, a[0], 0);
+      uint32_t* d1 = vdst(w, c, in, a[0], 1);
+      lanes([&](int l) {
+        const uint64_t v = x.v64(l);
+        d0[l] = (uint32_t)v;
+        d1[l] = (uint32_t)(v >> 32);
+      });
+      break;
+    }
+    case OP_v_lshl_add_u64: {
+      need(4);
+      const Src x = vsrc(w, c, in, a[1], true, vc, true), y = vsrc(w, c, in, a[2], false, vc, true),
+                z = vsrc(w, c, in, a[3], true, vc, true);
+      if (a[0].k != O_V || a[0].n != 2) fail(w, c, in, "64-bit destination");
+      uint32_t* d0 = vdst(w, c, in, a[0], 0);
+      uint32_t* d1 = vdst(w, c, in, a[0], 1);
+      lanes([&](int l) {
+        const uint64_t v = (x.v64(l) << (y.lo(l) & 63)) + z.v64(l);
+        d0[l] = (uint32_t)v;
+        d1[l] = (uint32_t)(v >> 32);
+      });
+      break;
+    }
+    case OP_v_ashrrev_i64: {
+      need(3);
+      const Src x = vsrc(w, c, in, a[1], false, vc, true), y = vsrc(w, c, in, a[2], true, vc, true);
+      uint32_t* d0 = vdst(w, c, in, a[0], 0);
+      uint32_t* d1 = vdst(w, c, in, a[0], 1);
+      lanes([&](int l) {
+        const uint64_t v = (uint64_t)((int64_t)y.v64(l) >> (x.lo(l) & 63));
+        d0[l] = (uint32_t)v;
+        d1[l] = (uint32_t)(v >> 32);
+      });
+      break;
+    }
+    case OP_v_mbcnt_lo_u32_b32: case OP_v_mbcnt_hi_u32_b32: {
+      need(3);
+      const Src x = vsrc(w, c, in, a[1], false, vc, vop3), y = vsrc(w, c, in, a[2], false, vc, vop3);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      lanes([&](int l) {
+        const int below = op == OP_v_mbcnt_lo_u32_b32 ? std::min(l, 32) : std::max(l - 32, 0);
+        const uint32_t m = below >= 32 ? 0xFFFFFFFFu : ((1u << below) - 1u);
+        d[l] = (uint32_t)__builtin_popcount(x.lo(l) & m) + y.lo(l);
+      });
+      break;
+    }
+    case OP_v_bcnt_u32_b32: {
+      need(3);
+      const Src x = vsrc(w, c, in, a[1], false, vc, vop3), y = vsrc(w, c, in, a[2], false, vc, vop3);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      lanes([&](int l) { d[l] = (uint32_t)__builtin_popcount(x.lo(l)) + y.lo(l); });
+      break;
+    }
+    case OP_v_max_i32: case OP_v_min_i32: case OP_v_mul_hi_i32: case OP_v_add_i32: case OP_v_sub_i32: {
+      need(3);
+      e32_src1(a[2]);
+      const Src x = vsrc(w, c, in, a[1], false, vc, vop3), y = vsrc(w, c, in, a[2], false, vc, vop3);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      lanes([&](int l) {
+        const int32_t p = (int32_t)x.lo(l), q = (int32_t)y.lo(l);
+        switch (op) {
+          case OP_v_max_i32: d[l] = (uint32_t)std::max(p, q); break;
+          case OP_v_min_i32: d[l] = (uint32_t)std::min(p, q); break;
+          case OP_v_mul_hi_i32: d[l] = (uint32_t)(((int64_t)p * q) >> 32); break;
+          case OP_v_add_i32: d[l] = (uint32_t)p + (uint32_t)q; break;
+          default: d[l] = (uint32_t)p - (uint32_t)q; break;
+        }
+      });
+      break;
+    }
+    case OP_v_rcp_f32: case OP_v_trunc_f32: case OP_v_cvt_f32_ubyte0: case OP_v_cvt_f32_ubyte1:
+    case OP_v_cvt_f32_ubyte2: case OP_v_cvt_f32_ubyte3: {
+      need(2);
+      const Src x = vsrc(w, c, in, a[1], false, vc, vop3);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      lanes([&](int l) {
+        const uint32_t p = x.lo(l);
+        switch (op) {
+          case OP_v_rcp_f32: d[l] = u32f(1.0f / f32(p)); break;
+          case OP_v_trunc_f32: d[l] = u32f(std::trunc(f32(p))); break;
+          default: d[l] = u32f((float)((p >> (8 * (op - OP_v_cvt_f32_ubyte0))) & 0xFFu)); break;
+        }
+      });
+      break;
+    }
+    case OP_v_add_f32: case OP_v_sub_f32: case OP_v_ldexp_f32: case OP_v_fmac_f32: {
+      need(3);
+      const Src x = vsrc(w, c, in, a[1], false, vc, vop3), y = vsrc(w, c, in, a[2], false, vc, vop3);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      lanes([&](int l) {
+        const float p = f32(x.lo(l)), q = f32(y.lo(l));
+        switch (op) {
+          case OP_v_add_f32: d[l] = u32f(p + q); break;
+          case OP_v_sub_f32: d[l] = u32f(p - q); break;
+          case OP_v_ldexp_f32: d[l] = u32f(std::ldexp(p, (int)(int32_t)y.lo(l))); break;
+          default: d[l] = u32f(std::fma(p, q, f32(d[l]))); break;
+        }
+      });
+      break;
+    }
+    case OP_v_fma_f32: {
+      need(4);
+      const Src x = vsrc(w, c, in, a[1], false, vc, true), y = vsrc(w, c, in, a[2], false, vc, true),
+                z = vsrc(w, c, in, a[3], false, vc, true);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      lanes([&](int l) { d[l] = u32f(std::fma(f32(x.lo(l)), f32(y.lo(l)), f32(z.lo(l)))); });
+      break;
+    }
+    case OP_v_fmamk_f32: case OP_v_madak_f32: {
+      // VOP2 with an inline 32-bit constant K: fmamk d = s0 * K + s1, madak d = s0 * s1 + K
+      need(4);
+      const Opd& ko = op == OP_v_fmamk_f32 ? a[2] : a[3];
+      if (ko.k != O_IMM) fail(w, c, in, "K operand");
+      const Src x = vsrc(w, c, in, a[1], false, vc, false),
+                y = vsrc(w, c, in, op == OP_v_fmamk_f32 ? a[3] : a[2], false, vc, false);
+      vc.literals++;
+      const float K = f32((uint32_t)ko.imm);
+      uint32_t* d = vdst(w, c, in, a[0]);
+      lanes([&](int l) {
+        d[l] = op == OP_v_fmamk_f32 ? u32f(std::fma(f32(x.lo(l)), K, f32(y.lo(l))))
+                                    : u32f(std::fma(f32(x.lo(l)), f32(y.lo(l)), K));
+      });
+      break;
+    }
     case OP_v_mul_f32: {
       need(3);
       const Src x = vsrc(w, c, in, a[1], false, vc, vop3), y = vsrc(w, c, in, a[2], false, vc, vop3);
@@ -1156,8 +1579,9 @@ void launch(const Module& m, const std::string& kernel, Memory& mem, uint64_t ke
   if (kit == m.kernels.end()) err("no kernel " + kernel);
   uint64_t steps = 0;
   std::vector<Wave> waves(4);
+  const uint64_t image_base = m.image.empty() ? 0 : mem.add(m.image.size(), m.image.data());
   for (uint32_t b = 0; b < nblk; b++) {
-    Ctx c{m, mem, std::vector<uint8_t>(kit->second.lds_bytes, 0), stats, (int)b};
+    Ctx c{m, mem, std::vector<uint8_t>(kit->second.lds_bytes, 0), stats, (int)b, image_base};
     for (int q = 0; q < 4; q++) {
       Wave& w = waves[q];
       memset(w.vinit, 0, sizeof w.vinit);

@@ -1,5 +1,6 @@
 // A CPU simulator of the gfx950 instruction subset the first JIT tier emits
-// (mythril_amd/csrc/jit_asm.cpp) — test infrastructure only, never linked into the product.
+// (mythril_amd/csrc/jit_asm.cpp) and the O3 tier's compiler output uses (disassembled by
+// tools/o3dis.py) — test infrastructure only, never linked into the product.
 //
 // It runs the emitted kernels (mgj_search, mgj_gen, mgj_eval) wave by wave on the host, 64 lanes
 // per wave, four waves per 256-lane block, with a flat 64-bit memory of the buffers the engine
@@ -42,11 +43,14 @@ struct Ins {
   int64_t offset = 0;   // offset:N
   int vmcnt = -1, lgkmcnt = -1;  // s_waitcnt
   int sdwa_src1_word1 = 0;
+  int sdwa_sel[2] = {0, 0};  // SDWA source selects: 0 DWORD, 1 WORD_0, 2 WORD_1, 3..6 BYTE_0..3
+  int offset0 = 0, offset1 = 0;  // ds_read2 / ds_write2 (dwords)
   int enc = 0;          // 0 VOP3-only / none, 1 _e32, 2 _e64, 3 _sdwa
   int bitop3 = -1;      // v_bitop3_b32's table
   int target = -1;      // branch target (instruction index)
   std::string text;     // the source line (diagnostics)
   int tag = -1;         // the "; vcode ..." annotation region it belongs to (MYTHGPU_JIT_ASM_ANNOTATE)
+  int64_t pc = -1;      // code address (".asmsim_pc A" before it; s_getpc_b64 of compiled code)
 };
 
 struct Kernel {
@@ -58,6 +62,9 @@ struct Module {
   std::vector<Ins> code;
   std::map<std::string, Kernel> kernels;
   std::vector<std::string> tags;  // annotation texts, by Ins::tag
+  // ".asmsim_image <file>": the code object's loaded image (vaddr 0 up), mapped at a buffer of its
+  // own so that s_getpc_b64-relative reads of baked tables (the O3 tier's mg_gd) find their data
+  std::vector<uint8_t> image;
 };
 
 // parse the emitter's assembly text (throws SimError on anything unknown)
@@ -77,7 +84,11 @@ struct Memory {
 
 struct Stats {
   uint64_t insts = 0, valu = 0, salu = 0, vmem = 0, lds = 0, waves = 0;
+  // extra LDS cycles from bank conflicts (the gfx950 lane groups and banks of
+  // docs MI355X_MICROARCH.md §LDS; what SQ_LDS_BANK_CONFLICT counts)
+  uint64_t lds_conflict = 0;
   std::map<int, uint64_t> valu_by_tag;  // VALU wave-instructions per annotation region
+  std::map<int, uint64_t> salu_by_tag;  // SALU instructions per annotation region
 };
 
 // run `kernel` over `nblk` 256-lane blocks; kernarg: the argument block's address

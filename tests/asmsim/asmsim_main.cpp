@@ -17,7 +17,10 @@
 #include <cstdlib>
 #include <cstdio>
 #include <chrono>
+#include <fstream>
+#include <sstream>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -94,7 +97,17 @@ std::string check_search(uint64_t rec, const std::vector<uint8_t>& prog, const s
   if (specialize_program(low, &specs, &consts, sp, err, /*keep_watch=*/false)) return "specialise: " + err;
   std::string src;
   int rc;
-  {
+  // ASMSIM_SEARCH_SOURCE=<file>: run this kernel text instead of the first tier's (the O3 tier's
+  // code object through tools/o3dis.py: its instruction counts, LDS bank conflicts and verdicts)
+  const char* ext = getenv("ASMSIM_SEARCH_SOURCE");
+  if (ext) {
+    std::ifstream f(ext, std::ios::binary);
+    if (!f) return std::string("cannot read ") + ext;
+    std::stringstream ss;
+    ss << f.rdbuf();
+    src = ss.str();
+    rc = 0;
+  } else {
     Tm tm(0);
     rc = jit_asm_source(sp, specs, consts, JIT_SEARCH | JIT_GEN, src, err);
   }
@@ -141,7 +154,7 @@ std::string check_search(uint64_t rec, const std::vector<uint8_t>& prog, const s
     const uint64_t lanes = (start + count) - (start & ~63ull);
     const uint32_t nblk = grid(lanes);
     // mgj_gen: verdict bytes
-    {
+    if (m.kernels.count("mgj_gen") && !getenv("ASMSIM_NO_GEN")) {  // ASMSIM_NO_GEN: counts of diagnostic builds
       asmsim::Memory mem;
       const uint64_t g = mem.add(std::max<size_t>(4, consts.size() * 4), consts.data());
       const uint64_t ver = mem.add(count);
@@ -198,10 +211,15 @@ std::string check_search(uint64_t rec, const std::vector<uint8_t>& prog, const s
         // ASMSIM_COUNT=1: the full-evaluation search launch's instructions per candidate (lane-
         // instructions, as SQ_INSTS_VALU x 64 / candidates)
         if (getenv("ASMSIM_COUNT")) {
-          printf("count record %llu: valu %.1f salu %.1f lds %.2f vmem %.2f per candidate\n", (unsigned long long)rec,
-                 64.0 * sst.valu / count, 64.0 * sst.salu / count, 64.0 * sst.lds / count, 64.0 * sst.vmem / count);
-          for (const auto& kv : sst.valu_by_tag)  // MYTHGPU_JIT_ASM_ANNOTATE=1: per program instruction
-            printf("count tag %s: %.2f\n", m.tags[kv.first].c_str(), 64.0 * kv.second / count);
+          printf("count record %llu: valu %.1f salu %.1f lds %.2f vmem %.2f lds_conflict %.2f per candidate\n",
+                 (unsigned long long)rec, 64.0 * sst.valu / count, 64.0 * sst.salu / count, 64.0 * sst.lds / count,
+                 64.0 * sst.vmem / count, 64.0 * sst.lds_conflict / count);
+          std::map<int, std::pair<uint64_t, uint64_t>> by;  // MYTHGPU_JIT_ASM_ANNOTATE=1: per program instruction
+          for (const auto& kv : sst.valu_by_tag) by[kv.first].first = kv.second;
+          for (const auto& kv : sst.salu_by_tag) by[kv.first].second = kv.second;
+          for (const auto& kv : by)
+            printf("count tag %s: %.2f salu %.2f\n", m.tags[kv.first].c_str(), 64.0 * kv.second.first / count,
+                   64.0 * kv.second.second / count);
         }
       }
       uint64_t r[kHitU64];

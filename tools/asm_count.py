@@ -34,8 +34,21 @@ def main():
         P, blob = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
         rec = record(0, P.to_bytes(), blob, 7, 1 << 40, 64 * 64)
         r = subprocess.run([str(exe)], input=rec, capture_output=True, env=env)
-        line = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("count")]
-        print(name, line[0].split(":", 1)[1].strip() if line else r.stdout.decode()[-300:] + r.stderr.decode()[-300:])
+        line = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("count record")]
+        summ = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("records=")]
+        ok = bool(summ) and " ok=1 " in summ[0]
+        print(name, line[0].split(":", 1)[1].strip() if line else r.stdout.decode()[-300:] + r.stderr.decode()[-300:],
+              "" if ok else "(DIFFERS from the C port: %s)" % (r.stdout.decode()[-400:]))
+        # MYTHGPU_JIT_ASM_ANNOTATE=1: the program instructions costing the most VALU per candidate
+        tags = []
+        for ln in r.stdout.decode().splitlines():
+            if ln.startswith("count tag "):
+                t, v = ln[len("count tag "):].rsplit(":", 1)
+                va, _, sa = v.strip().partition(" salu ")
+                tags.append((float(va), float(sa or 0), t.strip()))
+        key = (lambda x: x[1]) if env.get("ASMSIM_SORT") == "salu" else (lambda x: x[0])
+        for v, sv, t in sorted(tags, key=key, reverse=True)[:int(env.get("ASMSIM_TOP", "40"))]:
+            print(f"  {v:8.2f} {sv:8.2f}  {t}")
 
 
 if __name__ == "__main__":
