@@ -2686,7 +2686,7 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
   Engine& e = *ep;
   (void)hipSetDevice(device);
   std::unique_lock<std::mutex> lk(e.jit_mu);
-  auto& queue = e.jit_queue[lane];
+  auto& queue = e.jit_queue[lane ? 1 : 0];
   for (;;) {
     e.jit_cv.wait(lk, [&] { return e.jit_stop || !queue.empty(); });
     if (e.jit_stop) {
@@ -2870,8 +2870,10 @@ static int submit_jit(Engine& e, uint64_t prog, uint64_t gen, uint32_t flags, ui
       std::atexit(jit_atexit);
     });
     if (const char* c = getenv("MYTHGPU_JIT_CACHE")) e.code_cache.cap = std::max(1, atoi(c));
-    for (int lane = 0; lane < 2; lane++) std::thread(jit_worker_main, &e, e.device, lane).detach();
-    e.jit_workers = 2;
+    // lane 0: O3 compiles; lanes 1 and 2 share the first tier's queue (and its two assembly helpers), so
+    // a new search's assembly does not wait for one a finished search left in flight
+    for (int lane = 0; lane < 3; lane++) std::thread(jit_worker_main, &e, e.device, lane).detach();
+    e.jit_workers = 3;
   }
   e.tickets[h] = t;
   e.jit_queue[(t->flags & MG_JIT_ASM) ? 1 : 0].push_back(t);

@@ -537,7 +537,16 @@ struct Gen {
             for (uint32_t j = 0; j < L; j++) o << "    " << lim(j) << " = cv" << c << "_" << j << ";\n";
           } else {
             o << "    " << hdecl << "\n";
-            o << "    const uint32_t e = ((h >> 16) * " << sp.p[1] << "u) >> 16;\n";
+            // MYTHGPU_JIT_DICT_SPREAD=1 (diagnostic: WRONG verdicts): lane l of a 32-lane LDS group reads
+            // entry l, so the dictionary reads have no bank conflicts — what the conflicts cost
+            static const bool spread = [] {
+              const char* g = getenv("MYTHGPU_JIT_DICT_SPREAD");
+              return g && g[0] == '1';
+            }();
+            if (spread && sp.p[1] >= 32 && dict_lds.count(sp.p[0]))
+              o << "    const uint32_t e = lane & 31u; (void)h;\n";
+            else
+              o << "    const uint32_t e = ((h >> 16) * " << sp.p[1] << "u) >> 16;\n";
             dict_limbs(sp.p[0], sp.p[1], width, "e", lim, "    ");
           }
           delta(true);
@@ -1611,11 +1620,14 @@ struct Helper {
   std::string why;
 };
 
-// two helper processes: [0] compiles (clang + LLVM), [1] assembles the first tier — an assembly
-// request never queues behind a ~140 ms compile in the other
+// three helper processes: [0] compiles (clang + LLVM), [1] and [2] assemble the first tier — an
+// assembly request never queues behind a ~140 ms compile, nor behind the assembly of a search that
+// has already ended (a cancelled request in flight runs to its end: C5's hard query waited 8.3 ms
+// behind the easy query's, profiles/r05e_bench_c5.err)
+constexpr int kHelpers = 3;
 Helper& helper(int lane = 0) {
-  static Helper* h[2] = {new Helper, new Helper};  // leaked: usable from exit handlers
-  return *h[lane & 1];
+  static Helper* h[kHelpers] = {new Helper, new Helper, new Helper};  // leaked: usable from exit handlers
+  return *h[lane < 0 || lane >= kHelpers ? 0 : lane];
 }
 
 bool send_all(int fd, const void* p, size_t n) {
@@ -1710,9 +1722,32 @@ std::string env_snapshot() {
   return env;
 }
 
-int helper_compile(const std::string& src, std::vector<char>& code, std::string& log, bool& available) {
-  Helper& h = helper(src.compare(0, std::strlen(kAsmMarker), kAsmMarker) == 0 ? 1 : 0);
-  std::lock_guard<std::mutex> g(h.mu);
+int helper_compile_on(Helper& h, std::unique_lock<std::mutex>& g, const std::string& src, std::vector<char>& code,
+                      std::string& log, bool& available);
+
+// lane: -1 picks one (an assembly goes to whichever of its two helpers is free)
+int helper_compile(const std::string& src, std::vector<char>& code, std::string& log, bool& available, int lane = -1) {
+  const bool is_asm = src.compare(0, std::strlen(kAsmMarker), kAsmMarker) == 0;
+  if (!is_asm) {
+    std::unique_lock<std::mutex> g(helper(0).mu);
+    return helper_compile_on(helper(0), g, src, code, log, available);
+  }
+  if (lane == 1 || lane == 2) {
+    std::unique_lock<std::mutex> g(helper(lane).mu);
+    return helper_compile_on(helper(lane), g, src, code, log, available);
+  }
+  for (int l = 1; l <= 2; l++) {
+    std::unique_lock<std::mutex> g(helper(l).mu, std::try_to_lock);
+    if (g.owns_lock() && !helper(l).dead) return helper_compile_on(helper(l), g, src, code, log, available);
+  }
+  std::unique_lock<std::mutex> g(helper(1).mu);  // both busy: wait for the first
+  return helper_compile_on(helper(1), g, src, code, log, available);
+}
+
+// caller holds h.mu (g)
+int helper_compile_on(Helper& h, std::unique_lock<std::mutex>& g, const std::string& src, std::vector<char>& code,
+                      std::string& log, bool& available) {
+  (void)g;
   available = true;
   if (h.dead) {
     log = h.why;
@@ -1748,7 +1783,7 @@ int helper_compile(const std::string& src, std::vector<char>& code, std::string&
 }  // namespace
 
 void jit_helper_stop() {
-  for (int lane = 0; lane < 2; lane++) {
+  for (int lane = 0; lane < kHelpers; lane++) {
     Helper& h = helper(lane);
     std::lock_guard<std::mutex> g(h.mu);
     if (h.fd >= 0) {
@@ -1782,10 +1817,12 @@ void jit_helper_warm(const std::string& asm_src) {
   // not by the first query's first-tier compile (cold 11.9 ms against ~4.6 ms warm on the box,
   // profiles/r04h_bench.json)
   if (!asm_src.empty()) {
-    std::vector<char> code;
-    std::string log;
-    bool available = true;
-    (void)helper_compile(asm_src, code, log, available);
+    for (int lane = 1; lane <= 2; lane++) {  // both assembly helpers
+      std::vector<char> code;
+      std::string log;
+      bool available = true;
+      (void)helper_compile(asm_src, code, log, available, lane);
+    }
   }
   // the compiler's helper: started only (its first compile loads comgr)
   Helper& h = helper(0);

@@ -545,7 +545,9 @@ struct Gen {
       const GenSpec& sp = specs[c];
       const uint32_t kind = sp.kind & 0xFFu, n = sp.p[1], off = sp.p[0], w = P.coord_width[c], Lc = Lw(w);
       const bool dict = kind == MG_GEN_DICT || (kind == MG_GEN_MIXED && n && (sp.p[2] >> 16));
-      if (!dict || n <= 4 || Lc > 16 || lds_base.count(off)) continue;
+      // small dictionaries too (the actor / sender addresses: 3 entries): a select chain is two VALU
+      // per entry and limb, the LDS read none (its few addresses fall in distinct banks)
+      if (!dict || n < 2 || Lc > 16 || lds_base.count(off)) continue;
       if (w <= 32 && (uint64_t)n * w <= 32) continue;  // packed into one literal
       if ((size_t)off + (size_t)n * Lc > G.size() || lds_words + n * Lc > kLdsWords) continue;
       lds_base[off] = lds_words;
@@ -1561,7 +1563,7 @@ struct Gen {
       r[0] = d;
       return r;
     }
-    if (n <= 4) {  // selects over the entries' literals
+    if (n <= 4 && !lds_base.count(off)) {  // selects over the entries' literals
       std::vector<Mask> ms;
       for (uint32_t e2 = 0; e2 + 1 < n; e2++) {
         Mask m;
