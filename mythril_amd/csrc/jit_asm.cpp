@@ -172,15 +172,32 @@ class Emitter {
     }
     o << "  " << s << "\n";
   }
-  void ctl(const std::string& s) { o << "  " << s << "\n"; }
+  void ctl(const std::string& s) {
+    // a pending dictionary read does not cross a branch or a label: the waits are placed along one path
+    if (!lds_pending.empty()) {
+      if (s.compare(0, 9, "s_branch ") == 0 || s.compare(0, 10, "s_cbranch_") == 0) lds_flush();
+      else if (s.compare(0, 9, "s_waitcnt") == 0 && s.find("lgkmcnt(0)") != std::string::npos) lds_pending.clear();
+    }
+    o << "  " << s << "\n";
+  }
   std::string newlab() { return ".Lm" + std::to_string(nlab++); }
   void label(const std::string& L) {
+    lds_flush();
     o << L << ":\n";
     for (auto& kv : vw) kv.second = std::max(kv.second, pos - 1);
   }
   static std::initializer_list<int> none() { return {}; }
 
   // --- VGPRs ---------------------------------------------------------------------------------
+  // VGPRs a dictionary's LDS reads are still filling: the wave waits (s_waitcnt lgkmcnt(0)) only when
+  // one of them is next named — read, written or reallocated — not right after the reads, so the LDS
+  // latency overlaps the generator's other work (Gen::VL, valloc, lds_flush at the body's end)
+  std::set<int> lds_pending;
+  void lds_flush() {
+    if (lds_pending.empty()) return;
+    ctl("s_waitcnt lgkmcnt(0)");
+    lds_pending.clear();
+  }
   std::function<bool()> on_pressure;  // drop cached values (value numbering); true if any went
   // The value caches may not raise the kernel's VGPR count past the occupancy step the kernel
   // reaches without them (jit_asm_source): an allocation at or above vsoft first drops the caches.
@@ -194,9 +211,26 @@ class Emitter {
       // is free or the caches are empty
       if ((r >= 256 || r >= vsoft) && on_pressure && on_pressure()) continue;
       if (r >= 256) fail("out of VGPRs");
+      if (lds_pending.count(r)) lds_flush();  // a register whose load is still in flight
       vref[r] = 1;
       vgen[r] = ++gen_ctr;
       vhigh = std::max(vhigh, r + 1);
+      return (uint32_t)r;
+    }
+  }
+  // an even-aligned register pair (64-bit VGPR operands), each half with its own reference
+  uint32_t valloc2() {
+    for (;;) {
+      int r = (vfirst + 1) & ~1;
+      while (r + 1 < 256 && (vref[r] || vref[r + 1])) r += 2;
+      if ((r + 1 >= 256 || r + 1 >= vsoft) && on_pressure && on_pressure()) continue;
+      if (r + 1 >= 256) fail("out of VGPRs");
+      if (lds_pending.count(r) || lds_pending.count(r + 1)) lds_flush();
+      for (int q = 0; q < 2; q++) {
+        vref[r + q] = 1;
+        vgen[r + q] = ++gen_ctr;
+      }
+      vhigh = std::max(vhigh, r + 2);
       return (uint32_t)r;
     }
   }
@@ -243,7 +277,7 @@ struct Gen {
   const Lowered& P;
   const std::vector<GenSpec>& specs;
   const std::vector<uint32_t>& G;  // generator constants
-  Emitter E;
+  mutable Emitter E;  // (mutable: naming a register may first wait for its pending LDS read)
   std::vector<Val> val;
   std::vector<uint64_t> need;        // demanded limbs per value id (bit j = limb j)
   std::vector<int32_t> last;         // last vcode index reading each value id
@@ -394,7 +428,12 @@ struct Gen {
           fail("op " + std::to_string(in.op) + " outside the assembly tier");
       }
     }
-    if (!eval_kernel) plan_lds();
+    // MYTHGPU_JIT_ASM_NO_LDS=1: dictionaries gathered from global memory (diagnostic)
+    static const bool no_lds = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_LDS");
+      return g && g[0] == '1';
+    }();
+    if (!eval_kernel && !no_lds) plan_lds();
     // uses (for liveness) and demanded limbs (backward)
     auto use = [&](uint32_t id, size_t k) {
       if (id != MG_NONE && id < last.size()) last[id] = std::max(last[id], (int32_t)k);
@@ -681,9 +720,48 @@ struct Gen {
     const uint32_t r = E.valloc();
     return Limb{LR, r, E.vgen[r]};
   }
+  // x * y (x a VGPR, y a VGPR or an operand string `so`: an inline constant or s41) as (lo, hi): one
+  // v_mad_u64_u32 into a register pair when both halves are wanted — one instruction for what
+  // v_mul_lo_u32 + v_mul_hi_u32 take two (LLVM's choice for the O3 kernels' products too);
+  // MYTHGPU_JIT_ASM_NO_MAD=1: the two multiplies
+  static bool no_mad() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_MAD");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
+  void product(const Limb& vx, const std::string& so, bool s41, bool want_lo, bool want_hi, Limb& lo, Limb& hi) {
+    std::initializer_list<int> none{};
+    if (want_lo && want_hi && !no_mad()) {
+      const uint32_t r = E.valloc2();
+      lo = Limb{LR, r, E.vgen[r]};
+      hi = Limb{LR, r + 1, E.vgen[r + 1]};
+      Mask c;  // the carry-out pair the encoding names (always 0: the addend is 0)
+      c.k = 2;
+      c.s = E.salloc();
+      const std::string ins = "v_mad_u64_u32 v[" + std::to_string(r) + ":" + std::to_string(r + 1) + "], " + SP(c.s) +
+                              ", " + VL(vx) + ", " + so + ", 0";
+      if (s41) E.valu(ins, {41}, {c.s, c.s + 1});
+      else E.valu(ins, none, {c.s, c.s + 1});
+      E.srelease(c);
+      return;
+    }
+    if (want_lo) {
+      lo = fresh();
+      if (s41) E.valu("v_mul_lo_u32 " + VL(lo) + ", " + VL(vx) + ", " + so, {41});
+      else E.valu("v_mul_lo_u32 " + VL(lo) + ", " + VL(vx) + ", " + so);
+    }
+    if (want_hi) {
+      hi = fresh();
+      if (s41) E.valu("v_mul_hi_u32 " + VL(hi) + ", " + VL(vx) + ", " + so, {41});
+      else E.valu("v_mul_hi_u32 " + VL(hi) + ", " + VL(vx) + ", " + so);
+    }
+  }
   // the register name of a limb, checked against its allocation (MYTHGPU_JIT_ASM_CHECK)
   std::string VL(const Limb& l) const {
     E.check(l);
+    if (!E.lds_pending.empty() && l.reg() && E.lds_pending.count((int)l.v)) E.lds_flush();
     return V(l.v);
   }
 
@@ -1174,6 +1252,12 @@ struct Gen {
   // value read latest, and not by the instruction being emitted, moves to its VGPR form (one
   // v_cndmask; a later reader compares it back)
   size_t cur_k = 0;
+  // MYTHGPU_JIT_ASM_ANNOTATE: a phase of the instruction being emitted, a tag of its own in the
+  // simulator's per-tag counts (tools/asm_count.py)
+  void note(const char* phase) {
+    static const bool annotate = getenv("MYTHGPU_JIT_ASM_ANNOTATE") != nullptr;
+    if (annotate) E.o << "  ; vcode " << cur_k << " " << phase << "\n";
+  }
   bool spill_mask() {
     if (cur_k >= code.size()) return false;
     const Instr& in = code[cur_k];
@@ -1638,9 +1722,10 @@ struct Gen {
         E.mem("ds_read_b32 " + VL(d) + ", " + VL(va) + " offset:" + std::to_string((lb->second + j * n) * 4));
         r[j] = d;
         any = true;
+        if (!no_lds_defer()) E.lds_pending.insert((int)d.v);
       }
-      if (any) E.ctl("s_waitcnt lgkmcnt(0)");
-      drop(va);
+      if (any && no_lds_defer()) E.ctl("s_waitcnt lgkmcnt(0)");
+      drop(va);  // (the address register may be reused at once: a load read its address at issue)
       return r;
     }
     // gathers from the generator constants (s[4:5]): byte offset (off + idx * Lc + j) * 4
@@ -2331,16 +2416,10 @@ struct Gen {
         const bool via_s41 = ly.lit() && !inl(ly.v);
         if (via_s41) E.salu("s_mov_b32 s41, " + hexs(ly.v), {41});
         const std::string so = via_s41 ? std::string("s41") : src(ly);
-        const Limb dl = fresh();
-        if (via_s41) E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so, {41});
-        else E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so);
+        Limb dl, dh;
+        product(vx, so, via_s41, true, i + j + 1 < n, dl, dh);
         lo[i + j] = dl;
-        if (i + j + 1 < n) {
-          const Limb dh = fresh();
-          if (via_s41) E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so, {41});
-          else E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so);
-          hi[i + j + 1] = dh;
-        }
+        if (i + j + 1 < n) hi[i + j + 1] = dh;
       }
       std::vector<Limb> s1 = add_chain(acc, lo, n, false);
       for (auto& t : acc) drop(t);
@@ -2351,6 +2430,79 @@ struct Gen {
       acc = s2;
     }
     return acc;
+  }
+  // low n limbs of a * a: the cross products a_i a_j (i < j) once, doubled by a one-bit shift, then
+  // the squares a_i^2 added (bv_device.h sqr8): 16 products for 256 bits where mul_lo takes 36
+  std::vector<Limb> sqr_lo(const std::vector<Limb>& a, uint32_t n) {
+    auto at = [&](uint32_t i) { return i < a.size() ? a[i] : Lit(0); };
+    std::vector<Limb> acc(n, Lit(0));  // owned
+    for (uint32_t i = 0; 2 * i + 1 < n; i++) {
+      const Limb x = at(i);
+      if (x.lit() && x.v == 0) continue;
+      std::vector<Limb> lo(n, Lit(0)), hi(n, Lit(0));
+      for (uint32_t j = i + 1; i + j < n; j++) {
+        const Limb y = at(j);
+        if (y.lit() && y.v == 0) continue;
+        if (x.lit() && y.lit()) {
+          const uint64_t p = (uint64_t)x.v * y.v;
+          lo[i + j] = Lit((uint32_t)p);
+          if (i + j + 1 < n) hi[i + j + 1] = Lit((uint32_t)(p >> 32));
+          continue;
+        }
+        const Limb vx = x.reg() ? x : y, ly = x.reg() ? y : x;
+        const bool via_s41 = ly.lit() && !inl(ly.v);
+        if (via_s41) E.salu("s_mov_b32 s41, " + hexs(ly.v), {41});
+        const std::string so = via_s41 ? std::string("s41") : src(ly);
+        Limb dl, dh;
+        product(vx, so, via_s41, true, i + j + 1 < n, dl, dh);
+        lo[i + j] = dl;
+        if (i + j + 1 < n) hi[i + j + 1] = dh;
+      }
+      std::vector<Limb> s1 = add_chain(acc, lo, n, false);
+      drop_all(acc);
+      drop_all(lo);
+      acc = add_chain(s1, hi, n, false);
+      drop_all(s1);
+      drop_all(hi);
+    }
+    // acc <<= 1 (limb n-1's top bit drops out)
+    std::vector<Limb> dbl(n, Lit(0));
+    for (int j = (int)n - 1; j >= 0; j--) {
+      const Limb hi = acc[j], lo = j ? acc[j - 1] : Lit(0);
+      if (hi.lit() && lo.lit()) {
+        dbl[j] = Lit((hi.v << 1) | (lo.v >> 31));
+        continue;
+      }
+      const Limb d = fresh();
+      if (lo.lit() && lo.v == 0) E.valu("v_lshlrev_b32_e32 " + VL(d) + ", 1, " + VL(hi.reg() ? hi : vreg(hi)));
+      else {
+        const Limb h = v3(hi), l = v3(lo);
+        E.valu("v_alignbit_b32 " + VL(d) + ", " + src(h) + ", " + src(l) + ", 31");
+        drop(h);
+        drop(l);
+      }
+      dbl[j] = d;
+    }
+    drop_all(acc);
+    // the squares at limbs 2i, 2i + 1
+    std::vector<Limb> sq(n, Lit(0));
+    for (uint32_t i = 0; 2 * i < n; i++) {
+      const Limb x = at(i);
+      if (x.lit()) {
+        const uint64_t p = (uint64_t)x.v * x.v;
+        sq[2 * i] = Lit((uint32_t)p);
+        if (2 * i + 1 < n) sq[2 * i + 1] = Lit((uint32_t)(p >> 32));
+        continue;
+      }
+      Limb dl, dh;
+      product(x, VL(x), false, true, 2 * i + 1 < n, dl, dh);
+      sq[2 * i] = dl;
+      if (2 * i + 1 < n) sq[2 * i + 1] = dh;
+    }
+    std::vector<Limb> r = add_chain(dbl, sq, n, false);
+    drop_all(dbl);
+    drop_all(sq);
+    return r;
   }
   // dst[j] = v[j] (moves into loop-state registers; v released)
   void assign(const std::vector<Limb>& dst, std::vector<Limb>& v) {
@@ -2375,6 +2527,7 @@ struct Gen {
     std::vector<Limb> a = a_in, b = b_in;
     a.resize(La, Lit(0));
     b.resize(La, Lit(0));
+    note("udivrem:bitlen");
     const Limb la = bitlen(a), lb = bitlen(b);
     // n = la >= lb ? la - lb + 1 : 0
     const Limb n = fresh();
@@ -2385,8 +2538,14 @@ struct Gen {
       E.valu("v_cmp_lt_u32_e64 " + SP(lt.s) + ", " + VL(la) + ", " + VL(lb), {}, {lt.s, lt.s + 1});
       vsel(n, n, Reg(6), lt);
       E.srelease(lt);
+      // b == 0: no steps either (the SMT-LIB result is substituted at the end) — a zero divisor would
+      // otherwise run the wave for la + 1 steps (up to 257)
+      const Mask z = vcmp("eq", lb, 0);
+      vsel(n, n, Reg(6), z);
+      E.srelease(z);
     }
     drop(la);
+    note("udivrem:shift");
     // rem = a >> n, quo = a << (C - n)
     std::vector<Limb> rem = own(a, La), quo = own(a, La);
     shift_limbs(rem, n, false, Reg(6));
@@ -2399,6 +2558,7 @@ struct Gen {
     // the divisor's limbs as registers for the subtraction
     std::vector<Limb> bv(La);
     for (uint32_t j = 0; j < La; j++) bv[j] = vreg(b[j]);
+    note("udivrem:onelimb");
     // lanes whose divisor is one non-zero limb (x / 10**k, x / n for a small n): limb-serial long
     // division instead (div_one_limb), and out of the bit-serial loop below (n = 0)
     {
@@ -2422,6 +2582,7 @@ struct Gen {
       }
       E.srelease(one);
     }
+    note("udivrem:loop");
     const int sN = sreg(), sIt = sreg();
     wave_max(n, 9, sN);
     // NB: the wave's widest divisor in limbs (ballots over the divisor's limbs)
@@ -2501,6 +2662,7 @@ struct Gen {
     sfree(sNB);
     drop(n);
     for (auto& x : bv) drop(x);
+    note("udivrem:zero");
     // b == 0 (lb == 0): q = ~0 (to the width), r = a
     {
       const Mask z = vcmp("eq", lb, 0);
@@ -2646,12 +2808,14 @@ struct Gen {
   std::vector<Limb> sdivrem(uint32_t op, const std::vector<Limb>& a_in, const std::vector<Limb>& b_in, uint32_t W) {
     const uint32_t La = Lw(W);
     std::vector<Limb> a = own(a_in, La), b = own(b_in, La);
+    note("sdivrem:abs");
     const Mask ma = sign_mask(a, W), mb = sign_mask(b, W);
     std::vector<Limb> aa = own(a, La), bb = own(b, La);
     neg_where(aa, ma, W);
     neg_where(bb, mb, W);
     std::vector<Limb> q, r;
     udivrem(aa, bb, W, q, r);
+    note("sdivrem:sign");
     drop_all(aa);
     drop_all(bb);
     std::vector<Limb> out;
@@ -2723,7 +2887,7 @@ struct Gen {
       r[j] = fresh();
       E.valu("v_mov_b32_e32 " + VL(r[j]) + ", " + (j ? "0" : "1"));
     }
-    std::vector<Limb> b2 = mul_lo(base, base, La), b3;
+    std::vector<Limb> b2 = sqr_lo(base, La), b3;
     {
       std::vector<Limb> t = mul_lo(b2, base, La);
       b3 = own(t, La);
@@ -2758,7 +2922,7 @@ struct Gen {
       E.valu("v_alignbit_b32 " + VL(ex[i]) + ", " + VL(ex[i]) + ", " + VL(ex[i - 1]) + ", 30");
     E.valu("v_lshlrev_b32_e32 " + VL(ex[0]) + ", 2, " + VL(ex[0]));
     for (int sq = 0; sq < 2; sq++) {
-      std::vector<Limb> t = mul_lo(r, r, La);
+      std::vector<Limb> t = sqr_lo(r, La);
       assign(r, t);
     }
     {
@@ -3069,16 +3233,10 @@ struct Gen {
             } else {
               so = src(ly);
             }
-            const Limb dl = fresh();
-            if (via_s41) E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so, {41});
-            else E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so);
+            Limb dl, dh;
+            product(vx, so, via_s41, true, i + j + 1 < n, dl, dh);
             lo[i + j] = dl;
-            if (i + j + 1 < n) {
-              const Limb dh = fresh();
-              if (via_s41) E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so, {41});
-              else E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so);
-              hi[i + j + 1] = dh;
-            }
+            if (i + j + 1 < n) hi[i + j + 1] = dh;
           }
           (void)anyv;
           std::vector<Limb> s1 = add_chain(acc, lo, n, false);
@@ -3123,14 +3281,8 @@ struct Gen {
             // the product's limb 0 is the low half of a0 * b0 alone: it carries nothing into the limbs
             // the test reads (at or above wa >= 32), so it is not computed
             const bool lo_dead = i + j == 0 && wa >= 32;
-            const Limb dl = lo_dead ? Lit(0) : fresh(), dh = fresh();
-            if (via_s41) {
-              if (!lo_dead) E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so, {41});
-              E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so, {41});
-            } else {
-              if (!lo_dead) E.valu("v_mul_lo_u32 " + VL(dl) + ", " + VL(vx) + ", " + so);
-              E.valu("v_mul_hi_u32 " + VL(dh) + ", " + VL(vx) + ", " + so);
-            }
+            Limb dl = Lit(0), dh;
+            product(vx, so, via_s41, !lo_dead, true, dl, dh);
             lo[i + j] = dl;
             hi[i + j + 1] = dh;
           }
@@ -3722,6 +3874,14 @@ struct Gen {
     return r;
   }
 
+  // MYTHGPU_JIT_ASM_NO_LDS_DEFER=1: wait for a dictionary's LDS reads right after them
+  static bool no_lds_defer() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_LDS_DEFER");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
   // MYTHGPU_JIT_ASM_NO_GEN_WANT=1: every MIXED coordinate generated whole
   static bool no_gen_want() {
     static const bool on = [] {

@@ -833,6 +833,8 @@ bool step(Wave& w, Ctx& c) {
     return true;
   }
   // ---- control ---------------------------------------------------------------------------
+  if (c.st && op >= OP_s_cbranch_scc0 && op <= OP_s_branch) c.st->branches++;
+  if (c.st && op == OP_s_waitcnt) c.st->waitcnts++;
   switch (op) {
     case OP_s_cbranch_scc0: if (!w.scc) next = in.target; w.pc = next; return true;
     case OP_s_cbranch_scc1: if (w.scc) next = in.target; w.pc = next; return true;
@@ -851,6 +853,7 @@ bool step(Wave& w, Ctx& c) {
       need(1);
       if (a[0].k != O_IMM || a[0].imm > 15) fail(w, c, in, "bad s_nop");
       w.slot += (int64_t)a[0].imm;  // N + 1 wait states in all
+      if (c.st) c.st->nop_slots += a[0].imm + 1;
       w.pc = next;
       return true;
     }

@@ -87,6 +87,7 @@ struct Stats {
   // extra LDS cycles from bank conflicts (the gfx950 lane groups and banks of
   // docs MI355X_MICROARCH.md §LDS; what SQ_LDS_BANK_CONFLICT counts)
   uint64_t lds_conflict = 0;
+  uint64_t nop_slots = 0, branches = 0, waitcnts = 0;  // s_nop wait states, branches, s_waitcnt
   std::map<int, uint64_t> valu_by_tag;  // VALU wave-instructions per annotation region
   std::map<int, uint64_t> salu_by_tag;  // SALU instructions per annotation region
 };

@@ -211,9 +211,11 @@ std::string check_search(uint64_t rec, const std::vector<uint8_t>& prog, const s
         // ASMSIM_COUNT=1: the full-evaluation search launch's instructions per candidate (lane-
         // instructions, as SQ_INSTS_VALU x 64 / candidates)
         if (getenv("ASMSIM_COUNT")) {
-          printf("count record %llu: valu %.1f salu %.1f lds %.2f vmem %.2f lds_conflict %.2f per candidate\n",
+          printf("count record %llu: valu %.1f salu %.1f lds %.2f vmem %.2f lds_conflict %.2f nop %.1f branch %.1f "
+                 "waitcnt %.1f per candidate\n",
                  (unsigned long long)rec, 64.0 * sst.valu / count, 64.0 * sst.salu / count, 64.0 * sst.lds / count,
-                 64.0 * sst.vmem / count, 64.0 * sst.lds_conflict / count);
+                 64.0 * sst.vmem / count, 64.0 * sst.lds_conflict / count, 64.0 * sst.nop_slots / count,
+                 64.0 * sst.branches / count, 64.0 * sst.waitcnts / count);
           std::map<int, std::pair<uint64_t, uint64_t>> by;  // MYTHGPU_JIT_ASM_ANNOTATE=1: per program instruction
           for (const auto& kv : sst.valu_by_tag) by[kv.first].first = kv.second;
           for (const auto& kv : sst.salu_by_tag) by[kv.first].second = kv.second;
