@@ -5,7 +5,7 @@
 # conflict-free dictionary reads (MYTHGPU_JIT_DICT_SPREAD=1, wrong verdicts: what LDS bank conflicts cost)
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_asm.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r5f_pytest.log 2>&1 || { tail -40 gpurun_out/r5f_pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_asm.py tests/test_gpu_jit.py -m gpu -x -q --durations=12 --timeout 300 --timeout-method thread > gpurun_out/r5f_pytest.log 2>&1 || { tail -40 gpurun_out/r5f_pytest.log; exit 1; }
 tail -2 gpurun_out/r5f_pytest.log
 : > gpurun_out/r5f_rates.jsonl
 rate() {  # workload engine candidates tag [env...]
