@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--engine", choices=["jit", "asm", "interp"], default="jit",
                     help="jit: the O3 query kernel (clang + LLVM through comgr); asm: the JIT's first tier "
                          "(gfx950 assembly emitted by the engine); interp: the generic interpreter kernel")
+    ap.add_argument("--o3-only", action="store_true",
+                    help="--engine jit: time the O3 kernel even where the first tier is faster")
     ap.add_argument("--pmc-dir", default=str(ROOT / "profiles"),
                     help="where tools/profile.sh summaries (pmc_<workload>*.json) are looked up by kernel SHA")
     return ap.parse_args()
@@ -175,6 +177,38 @@ def main():
 
     from mythril_amd.distributed import chunk_start, first_hit_allreduce
 
+    # --engine jit: the engine's faster compiled tier for this query, as search.search races them (the
+    # first tier beats the O3 kernel on some queries): one untimed step of each after the warm-up
+    tier = "o3" if args.engine == "jit" else ("asm" if args.engine == "asm" else None)
+    tier_rates = None
+    jit_o3 = None
+    if args.engine == "jit" and not args.o3_only:
+        try:
+            ja_h = eng.jit_compile(prog, gh, asm=True)
+        except native.EngineUnsupported:
+            ja_h = None
+        if ja_h is not None:
+            cc0 = C * inproc
+            rates = {}
+            for name, h in (("o3", jit), ("asm", ja_h)):
+                for _ in range(max(1, args.warmup)):
+                    eng.jit_search(h, args.seed, chunk_start(0, rank, world, cc0), cc0, early_exit=False)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                eng.jit_search(h, args.seed, chunk_start(1, rank, world, cc0), cc0, early_exit=False)
+                torch.cuda.synchronize()
+                rates[name] = cc0 / (time.perf_counter() - t1)
+            r_t = torch.tensor([rates["o3"], rates["asm"]], dtype=torch.float64, device="cuda")
+            if distributed:  # every rank takes the same tier: the slowest rank's view decides
+                dist.all_reduce(r_t, op=dist.ReduceOp.MIN)
+            tier_rates = {"o3": float(r_t[0].item()), "asm": float(r_t[1].item())}
+            if tier_rates["asm"] > tier_rates["o3"]:
+                jit_o3 = jit  # kept for the first tier's agreement check below
+                jit, tier = ja_h, "asm"
+                sha = hashlib.sha256(native.jit_asm(P.to_bytes(), blob).encode()).hexdigest()[:16]
+            else:
+                eng.jit_free(ja_h)
+
     # in-process multi-GPU: one call sweeps inproc x C candidates, split over the devices in the shim
     CC = C * inproc
 
@@ -238,7 +272,8 @@ def main():
                 eng.jit_search(ja, args.seed, (s_ + 1) * na, na, early_exit=False)
             st_a = eng.stats()
             km_a = st_a.kernel_ms_total / max(st_a.launches, 1)
-            o3 = eng.jit_search(jit, args.seed, na, na, early_exit=False) if jit is not None else None
+            o3h = jit_o3 if jit_o3 is not None else jit
+            o3 = eng.jit_search(o3h, args.seed, na, na, early_exit=False) if o3h is not None else None
             asm_tier.update({"candidates_per_launch": na, "kernel_ms": km_a, "candidates_per_s": na / (km_a * 1e-3),
                              "agrees_with_o3_on_a_launch": o3 == eng.jit_search(ja, args.seed, na, na,
                                                                                 early_exit=False)})
@@ -403,6 +438,8 @@ def main():
                 "coords": int(info.n_coords),
                 "engine": args.engine,
                 "jit_source_sha16": sha,
+                "jit_tier": tier,
+                "jit_tier_rates": tier_rates,
                 "jit_compile_ms_cold": compile_ms,
                 "parallelism": f"inproc{inproc}" if inproc > 1 else f"shard{world}",
             },

@@ -28,6 +28,7 @@
 #include <string>
 #include <map>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/mythgpu.h"
@@ -1178,6 +1179,9 @@ struct Engine {
   std::deque<std::shared_ptr<JitTicket>> jit_queue[2];
   std::unordered_map<uint64_t, std::shared_ptr<JitTicket>> tickets;
   std::condition_variable jit_cv, jit_done_cv;
+  // sources being compiled right now: a second request for one waits for the first's code object
+  // (LASER re-asks a query while its first compile, cancelled with its search, still runs)
+  std::unordered_set<std::string> jit_inflight;
   bool init = false;
   int device = -1;
   hipStream_t stream = nullptr;
@@ -2726,6 +2730,8 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
     std::unique_ptr<DevJit> j;
     std::vector<char> code;
     lk.lock();
+    // the same source compiling on the other lane: wait for it, then take it from the cache
+    e.jit_done_cv.wait(lk, [&] { return e.jit_stop || !e.jit_inflight.count(src); });
     if (CodeCache::Entry* en = e.code_cache.find_entry(src)) {
       code = en->code;
       if (en->hold) {  // resident module: no load
@@ -2745,13 +2751,25 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
         j->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       }
     }
+    // a search that ended while this request waited: nothing to compile for it
+    const bool skip = !j && code.empty() && t->cancelled;
+    const bool owner = !j && code.empty() && !skip;
+    if (owner) e.jit_inflight.insert(src);
     lk.unlock();
     int rc = MG_OK;
     std::string log;
     bool compiled = false, from_disk = false;
-    if (!j && code.empty()) {
+    if (owner) {
       rc = jit_compile(src, code, log, &from_disk);
       compiled = rc == MG_OK;
+    }
+    if (skip) {
+      lk.lock();
+      t->state = JitTicket::FAILED;
+      t->rc = MG_E_INVALID;
+      t->err = "cancelled";
+      e.jit_done_cv.notify_all();
+      continue;
     }
     std::string err;
     const auto t_comp = std::chrono::steady_clock::now();
@@ -2797,6 +2815,7 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
       }
     }
     lk.lock();
+    if (owner) e.jit_inflight.erase(src);  // (waiters wake on the notify below)
     if (rc != MG_OK) {
       t->rc = rc;
       t->err = err;

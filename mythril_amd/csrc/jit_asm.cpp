@@ -2037,8 +2037,10 @@ struct Gen {
             E.ctl("s_cbranch_scc0 " + next);
           }
         };
+        note("mixed:key");
         if (pc) {
           branch(pc);
+          note("mixed:copy");
           std::vector<Limb> s;
           // the source's value when it is still live and whole (a copy chain's inner source may
           // have been generated earlier and released after its last analysed use)
@@ -2062,6 +2064,7 @@ struct Gen {
         }
         if (pd) {
           branch(pc + pd);
+          note("mixed:dict");
           const Limb h = grnd(c, 0xFFFFu);
           const Limb ix = dict_index(h, sp.p[1]);
           std::vector<Limb> dv = dict(sp.p[0], sp.p[1], width, ix, &out, Lg);
@@ -2083,6 +2086,7 @@ struct Gen {
         };
         if (ps) {
           branch(pc + pd + ps);
+          note("mixed:small");
           uni(small_bits);
           finish(out, width, sp.p[6], zeros(small_bits));
         }
@@ -2090,9 +2094,11 @@ struct Gen {
           E.ctl("s_branch " + end);
           E.label(next);
         }
+        note("mixed:uniform");
         uni(width);
         finish(out, width, sp.p[6], zeros(width));
         E.label(end);
+        note("mixed:join");
         Mask wsm;
         wsm.k = 2;
         wsm.s = ws;

@@ -488,6 +488,8 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
         tier = None        # "asm" / "o3": the compiled kernel in use
         asm_tried = o3_tried = False
         rate = None  # candidates/s of the kernel in use (last launch)
+        last_n = 0   # candidates of the last launch
+        race = None  # first tier vs O3: the first tier's handle and rate until the O3 kernel's first launch
         try:
             if jit == "always":
                 tc = time.perf_counter()
@@ -529,8 +531,11 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                             jit = "never"
                     if h is not None:
                         ticket = None
-                        if jh is not None:  # the O3 kernel replaces the first tier's on the same stream
-                            engine.jit_free(jh)
+                        if jh is not None:
+                            # the O3 kernel takes over the same stream; the first tier's stays until one
+                            # launch of the same size on the O3 kernel has shown which is faster (the first
+                            # tier beats O3 on some queries: C2, profiles/r05f_tier_rates.jsonl)
+                            race = {"asm_rate": rate, "n": last_n, "asm": jh}
                         else:
                             timing["jit_switch_ms"] = (now - t0) * 1e3
                             timing["interp_candidates"] = scanned
@@ -554,6 +559,8 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                         ticket = engine.jit_compile_async(prog, gh)
                         o3_tried = True
                 n = min(chunk, max_candidates - scanned)
+                if race is not None and race["n"]:
+                    n = min(n, race["n"])  # the race launch: as large as the first tier's last one
                 if rate:
                     cap_s = left
                     if ticket is not None or ticket_asm is not None:
@@ -571,6 +578,18 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                 else:
                     idx, nh = engine.search(prog, gh, seed, start, n, early_exit=True, assign=assign)
                 dt = time.perf_counter() - tl
+                last_n = n
+                if race is not None and jh is not None and tier == "o3":
+                    o3_rate = n / dt if dt > 0 else 0.0
+                    keep_asm = bool(race["asm_rate"]) and o3_rate < race["asm_rate"]
+                    timing["tier_race"] = {"asm_rate": race["asm_rate"], "o3_rate": o3_rate, "n": n,
+                                           "kept": "asm" if keep_asm else "o3"}
+                    if keep_asm:
+                        engine.jit_free(jh)
+                        jh, tier = race["asm"], "asm"
+                    else:
+                        engine.jit_free(race["asm"])
+                    race = None
                 if ticket_asm is not None:  # the launches the first tier's compile waited behind
                     timing["asm_wait_launches"] = timing.get("asm_wait_launches", 0) + 1
                     timing["asm_wait_launch_max_ms"] = max(timing.get("asm_wait_launch_max_ms", 0.0), dt * 1e3)
@@ -586,6 +605,8 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                 # (x16 after the 2^12 capture launch: a query that misses there is not an easy one)
                 chunk = min(chunk * (16 if chunk < (1 << 16) else 4), 1 << 26 if jh is None else 1 << 30)
         finally:
+            if race is not None:
+                engine.jit_free(race["asm"])
             if ticket_asm is not None:
                 engine.jit_cancel(ticket_asm)
             if ticket is not None:

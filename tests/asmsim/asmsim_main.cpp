@@ -362,6 +362,17 @@ std::string check_eval(const std::vector<uint8_t>& prog, uint64_t seed, uint32_t
                  got[i], want[i]);
         return b;
       }
+    if (getenv("ASMSIM_COUNT")) {  // as for the search launch: per candidate, and per program instruction
+      printf("count eval: valu %.1f salu %.1f vmem %.2f nop %.1f branch %.1f waitcnt %.1f per candidate\n",
+             64.0 * st.valu / n, 64.0 * st.salu / n, 64.0 * st.vmem / n, 64.0 * st.nop_slots / n,
+             64.0 * st.branches / n, 64.0 * st.waitcnts / n);
+      std::map<int, std::pair<uint64_t, uint64_t>> by;
+      for (const auto& kv : st.valu_by_tag) by[kv.first].first = kv.second;
+      for (const auto& kv : st.salu_by_tag) by[kv.first].second = kv.second;
+      for (const auto& kv : by)
+        printf("count tag %s: %.2f salu %.2f\n", m.tags[kv.first].c_str(), 64.0 * kv.second.first / n,
+               64.0 * kv.second.second / n);
+    }
   } catch (const asmsim::SimError& e) {
     C.simerror++;
     return "simulator: " + e.what;

@@ -11,10 +11,13 @@ from mythril_amd import search, workloads
 
 
 class FakeEngine:
-    def __init__(self, asm_raises=True, o3_ready_after=None, launch_s=0.0005):
+    def __init__(self, asm_raises=True, o3_ready_after=None, launch_s=0.0005, asm_ready_after=None,
+                 jit_launch_s=None):
         self.asm_raises = asm_raises
         self.o3_ready_after = o3_ready_after
+        self.asm_ready_after = asm_ready_after
         self.launch_s = launch_s
+        self.jit_launch_s = jit_launch_s or {}  # handle kind -> seconds per candidate
         self.submits = {"asm": 0, "o3": 0}
         self.polls = {"asm": 0, "o3": 0}
         self.launches = {"interp": 0, "jit": 0}
@@ -48,6 +51,8 @@ class FakeEngine:
         self.polls[kind] += 1
         if kind == "asm" and self.asm_raises:
             raise RuntimeError("JIT assembly tier: op 16 outside the assembly tier")
+        if kind == "asm" and self.asm_ready_after is not None and time.perf_counter() - at >= self.asm_ready_after:
+            return 700 + t
         if kind == "o3" and self.o3_ready_after is not None and time.perf_counter() - at >= self.o3_ready_after:
             return 500 + t
         return None
@@ -66,7 +71,9 @@ class FakeEngine:
 
     def jit_search(self, jh, seed, start, n, early_exit=True, assign=None):
         self.launches["jit"] += 1
-        time.sleep(self.launch_s)
+        kind = "asm" if jh >= 700 else "o3"
+        per = self.jit_launch_s.get(kind)
+        time.sleep(n * per if per else self.launch_s)
         return None, 0
 
 
@@ -94,3 +101,27 @@ def test_o3_still_replaces_interpreter_after_refused_first_tier():
     assert eng.launches["jit"] > 0
     assert res.timing.get("jit_tier") == "o3"
     assert ("jit", 500 + 101) in eng.freed  # the O3 kernel's module released at the end
+
+
+def test_tier_race_keeps_the_faster_first_tier():
+    """When the O3 kernel arrives, one launch as large as the first tier's last decides which
+    compiled kernel the search keeps: here the first tier is twice as fast, so it stays and the O3
+    kernel is released at once."""
+    eng = FakeEngine(asm_raises=False, asm_ready_after=0.005, o3_ready_after=0.03,
+                     jit_launch_s={"asm": 1e-9, "o3": 2e-9})
+    res = search.search(eng, _roots(), timeout_s=0.2, max_candidates=1 << 40, jit_cost_s=0.02)
+    race = res.timing.get("tier_race")
+    assert race is not None and race["kept"] == "asm", res.timing
+    assert race["asm_rate"] > race["o3_rate"]
+    assert res.timing.get("jit_tier") == "asm"
+    assert ("jit", 500 + 101) in eng.freed  # the O3 kernel's module
+
+
+def test_tier_race_switches_to_a_faster_o3():
+    eng = FakeEngine(asm_raises=False, asm_ready_after=0.005, o3_ready_after=0.03,
+                     jit_launch_s={"asm": 2e-9, "o3": 1e-9})
+    res = search.search(eng, _roots(), timeout_s=0.2, max_candidates=1 << 40, jit_cost_s=0.02)
+    race = res.timing.get("tier_race")
+    assert race is not None and race["kept"] == "o3", res.timing
+    assert res.timing.get("jit_tier") == "o3"
+    assert ("jit", 700 + 100) in eng.freed  # the first tier's module
