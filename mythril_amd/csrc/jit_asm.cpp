@@ -558,7 +558,63 @@ struct Gen {
         default: break;
       }
     }
+    plan_views();
   }
+
+  // Views: a CONCAT / EXTRACT / ZEXT value whose one reader is a CONCAT or an EXTRACT is never
+  // materialised — its reader takes the bits it needs from the view's operands (field()).  A chain
+  // of byte CONCATs building a word (calldata, storage keys) then costs a v_lshl_or per byte of the
+  // word's low limb and aliases the rest, where materialising every link re-aligned every limb at
+  // every link (C4's eval program: 1,565 VALU per candidate in CONCATs).  The view's operands live
+  // until its reader (last[] extended).  MYTHGPU_JIT_ASM_NO_VIEWS=1 materialises every value.
+  std::vector<uint8_t> view;  // value id -> a view
+  void plan_views() {
+    const size_t nv = P.vwidth.size();
+    view.assign(nv, 0);
+    static const bool off = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_VIEWS");
+      return g && g[0] == '1';
+    }();
+    if (off) return;
+    std::vector<uint32_t> nuse(nv, 0);
+    std::vector<uint8_t> field_only(nv, 1);
+    auto reader = [&](uint32_t id, uint32_t op) {
+      if (id == MG_NONE || id >= nv) return;
+      nuse[id]++;
+      if (op != K_CONCAT && op != K_EXTRACT) field_only[id] = 0;
+    };
+    for (size_t k = 0; k < code.size(); k++) {
+      const Instr& in = code[k];
+      switch (in.op) {
+        case K_CONST: break;
+        case K_WATCH: if (eval_kernel) reader(in.a, in.op); break;
+        case K_COORD: if (copysrc[k] != MG_NONE) reader(copysrc[k], in.op); break;
+        case K_LOOKUP:
+          reader(in.a, in.op);
+          reader(in.p0, in.op);
+          for (uint32_t q = 0; q < 2 * in.c; q++) reader(P.vaux[in.p1 + q], in.op);
+          break;
+        default:
+          reader(in.a, in.op);
+          if (in.op != K_NOT && in.op != K_NEG && in.op != K_EXTRACT && in.op != K_ZEXT && in.op != K_SEXT &&
+              in.op != K_ASSERT && in.op != K_COPY)
+            reader(in.b, in.op);
+          if (in.op == K_ITE) reader(in.c, in.op);
+          break;
+      }
+    }
+    for (size_t k = code.size(); k-- > 0;) {  // readers before their operands: chains extend in one pass
+      const Instr& in = code[k];
+      const uint32_t d = in.dst;
+      if (d == MG_NONE || d >= nv || def[d] != (int32_t)k) continue;
+      if (in.op != K_CONCAT && in.op != K_EXTRACT && in.op != K_ZEXT) continue;
+      if (in.wd <= 1 || nuse[d] != 1 || !field_only[d] || last[d] < 0) continue;
+      view[d] = 1;
+      for (uint32_t o : {in.a, in.op == K_CONCAT ? in.b : MG_NONE})
+        if (o != MG_NONE && o < nv) last[o] = std::max(last[o], last[d]);
+    }
+  }
+  bool is_view(uint32_t id) const { return id != MG_NONE && id < view.size() && view[id]; }
 
   void plan_lds() {
     // coordinates a search reads: the program's K_COORDs and, transitively, their COPY sources
@@ -971,6 +1027,35 @@ struct Gen {
     return c;
   }
 
+  // bits [p, p+n) (n <= 32) of value id at bit 0, zero above n (owned): through views (plan_views)
+  // to the materialised limbs they are made of
+  Limb field(uint32_t id, uint32_t p, uint32_t n) {
+    const uint32_t w = P.vwidth[id];
+    if (p >= w || n == 0) return Lit(0);
+    n = std::min(n, w - p);
+    if (!is_view(id)) return bits(limbs(id, Lw(w)), w, p, n);
+    return field_of(code[def[id]], p, n);
+  }
+  // the same of the value instruction `in` (a CONCAT, EXTRACT or ZEXT) defines
+  Limb field_of(const Instr& in, uint32_t p, uint32_t n) {
+    switch (in.op) {
+      case K_EXTRACT: return field(in.a, in.p0 + p, n);
+      case K_ZEXT: return field(in.a, p, n);  // bits above the operand: zero
+      case K_CONCAT: {  // a (high) : b (low, p1 bits)
+        const uint32_t wb = in.p1;
+        if (p + n <= wb) return field(in.b, p, n);
+        if (p >= wb) return field(in.a, p - wb, n);
+        const Limb lo = field(in.b, p, wb - p), hi = field(in.a, 0, p + n - wb);
+        const Limb r = shl_or(hi, wb - p, lo);
+        drop(lo);
+        drop(hi);
+        return r;
+      }
+      default: fail("internal: a view of op " + std::to_string(in.op));
+    }
+    return Lit(0);
+  }
+
   // (hi << s) | lo, lo < 2^s
   Limb shl_or(const Limb& hi, uint32_t s, const Limb& lo) {
     if (hi.lit() && lo.lit()) return Lit((s < 32 ? hi.v << s : 0u) | lo.v);
@@ -1299,11 +1384,97 @@ struct Gen {
     }
   }
 
+  // MYTHGPU_JIT_ASM_NO_SIGNED_LIT=1: signed compares against literals through the borrow chain
+  static bool no_signed_lit() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_SIGNED_LIT");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
+  // x <s y where one side is a literal K whose limbs above k are its sign extension (LASER's signed
+  // bounds: 0 <s x, x <s 29, x <s -1): with neg = the register side's sign and hi = its limbs above k
+  // equal K's, x <s K = neg | (hi & x_lo <u K_lo) for K >= 0, neg & (~hi | x_lo <u K_lo) for K < 0,
+  // and K <s x the mirror image — a sign test, an equality over the high limbs and a compare of the
+  // low ones, where the borrow chain runs through every limb with two wait states per link.  False
+  // when no side qualifies (fewer than two register limbs above k)
+  bool slt_literal(const std::vector<Limb>& x, const std::vector<Limb>& y, uint32_t w, Mask& out) {
+    const uint32_t La = Lw(w), tb = (w - 1) & 31;
+    const uint32_t topmask = tb == 31 ? 0xFFFFFFFFu : ((2u << tb) - 1u);
+    for (int side = 0; side < 2; side++) {
+      const std::vector<Limb>& kv = side ? x : y;  // the literal side
+      const std::vector<Limb>& rv = side ? y : x;
+      bool lit_all = true;
+      for (uint32_t j = 0; j < La; j++) lit_all = lit_all && kv[j].lit();
+      if (!lit_all) continue;
+      const bool kneg = (kv[La - 1].v >> tb) & 1u;
+      auto ext = [&](uint32_t j) { return kneg ? (j == La - 1 ? topmask : 0xFFFFFFFFu) : 0u; };
+      int k = -1;  // highest limb of K that is not sign extension
+      for (uint32_t j = 0; j < La; j++)
+        if (kv[j].v != ext(j)) k = (int)j;
+      if (k >= (int)La - 1) continue;
+      std::vector<std::pair<Limb, Limb>> hi;
+      uint32_t regs = 0;
+      for (uint32_t j = (uint32_t)(k + 1); j < La; j++) {
+        hi.push_back({rv[j], Lit(ext(j))});
+        regs += rv[j].reg();
+      }
+      if (regs < 2 || !rv[La - 1].reg()) continue;
+      // the register side's sign: its top limb >= 2^tb
+      Mask neg;
+      if (tb == 31) {  // 0 >s top limb
+        neg.k = 2;
+        neg.s = E.salloc();
+        E.valu("v_cmp_gt_i32_e64 " + SP(neg.s) + ", 0, " + VL(rv[La - 1]), {}, {neg.s, neg.s + 1});
+      } else {
+        neg = lt_mask({Lit((1u << tb) - 1u)}, {rv[La - 1]}, 32, false);
+      }
+      const Mask eh = eq_mask(hi);
+      Mask lo;
+      if (k < 0) {
+        lo.k = 1;
+        lo.ones = false;  // equal high limbs and no low ones: equal
+      } else {
+        lo = lt_mask(std::vector<Limb>(x.begin(), x.begin() + (k + 1)),
+                     std::vector<Limb>(y.begin(), y.begin() + (k + 1)), 32u * (uint32_t)(k + 1), false);
+      }
+      Mask t, r;
+      if (side == 0 && !kneg) {         // x < K, K >= 0: neg | (eh & lo)
+        t = mop("and", eh, lo);
+        r = mop("or", neg, t);
+      } else if (side == 0) {           // x < K, K < 0: neg & ~(eh & ~lo)
+        t = mop_andn(eh, lo);
+        r = mop_andn(neg, t);
+      } else if (!kneg) {               // K < x, K >= 0: ~(neg | (eh & ~lo))
+        t = mop_andn(eh, lo);
+        const Mask u = mop("or", neg, t);
+        r = mnot(u);
+        E.srelease(u);
+      } else {                          // K < x, K < 0: ~(neg & ~(eh & lo))
+        t = mop("and", eh, lo);
+        const Mask u = mop_andn(neg, t);
+        r = mnot(u);
+        E.srelease(u);
+      }
+      E.srelease(t);
+      E.srelease(neg);
+      E.srelease(eh);
+      E.srelease(lo);
+      out = r;
+      return true;
+    }
+    return false;
+  }
+
   // x < y (unsigned) over La limbs, as a mask; sgn: the top limbs' bit (w-1)&31 flipped first
   Mask lt_mask(std::vector<Limb> x, std::vector<Limb> y, uint32_t w, bool sgn) {
     const uint32_t La = Lw(w);
     x.resize(La, Lit(0));
     y.resize(La, Lit(0));
+    if (sgn && La > 1 && !no_signed_lit()) {
+      Mask r;
+      if (slt_literal(x, y, w, r)) return r;
+    }
     std::vector<Limb> own;
     if (sgn) {
       const uint32_t f = 1u << ((w - 1) & 31);
@@ -3596,40 +3767,10 @@ struct Gen {
         }
         break;
       }
-      case K_CONCAT: {
-        const uint32_t wb = in.p1, wa = W - wb;
-        const std::vector<Limb> a = limbs(in.a, Lw(wa)), b = limbs(in.b, Lw(wb));
+      case K_CONCAT: case K_EXTRACT: {  // limb by limb through field_of (operands may be views)
         std::vector<Limb> r(Ld);
-        for (uint32_t j = 0; j < Ld; j++) {
-          if (!(need[d] >> j & 1)) continue;
-          const uint32_t p = 32 * j, e2 = std::min(W, p + 32);
-          if (e2 <= wb) {
-            r[j] = bits(b, wb, p, e2 - p);
-          } else if (p >= wb) {
-            r[j] = bits(a, wa, p - wb, e2 - p);
-          } else {
-            const uint32_t nb = wb - p;
-            const Limb lo = bits(b, wb, p, nb), hi = bits(a, wa, 0, e2 - wb);
-            r[j] = shl_or(hi, nb, lo);
-            drop(lo);
-            drop(hi);
-          }
-        }
-        set(d, r);
-        break;
-      }
-      case K_EXTRACT: {
-        const uint32_t wa = in.p1;
-        const std::vector<Limb> a = limbs(in.a, Lw(wa));
-        std::vector<Limb> r(Ld);
-        for (uint32_t j = 0; j < Ld; j++) {
-          if (!(need[d] >> j & 1)) continue;
-          r[j] = bits(a, wa, in.p0 + 32 * j, std::min(32u, W - 32 * j));
-        }
-        if (W == 1) {
-          set(d, r);
-          break;
-        }
+        for (uint32_t j = 0; j < Ld; j++)
+          if (need[d] >> j & 1) r[j] = field_of(in, 32 * j, std::min(32u, W - 32 * j));
         set(d, r);
         break;
       }
@@ -3946,6 +4087,7 @@ struct Gen {
     for (size_t k = 0; k < code.size(); k++) {
       const Instr& in = code[k];
       cur_k = k;
+      if (is_view(in.dst)) continue;  // read through by its one reader (field_of)
       if (annotate)
         E.o << "  ; vcode " << k << " op " << in.op << " w " << in.wd << " dst " << in.dst << " a " << in.a << " b " << in.b
             << "\n";
@@ -3992,6 +4134,20 @@ struct Gen {
           done(in.a);
           if (in.b != MG_NONE) done(in.b);
           if (in.op == K_ITE) done(in.c);
+          if (in.op == K_CONCAT || in.op == K_EXTRACT) {  // the operands of the views it read through
+            std::function<void(uint32_t)> through = [&](uint32_t id) {
+              if (!is_view(id)) return;
+              const Instr& vi = code[def[id]];
+              done(vi.a);
+              through(vi.a);
+              if (vi.op == K_CONCAT) {
+                done(vi.b);
+                through(vi.b);
+              }
+            };
+            through(in.a);
+            if (in.op == K_CONCAT) through(in.b);
+          }
           break;
       }
     }

@@ -272,6 +272,59 @@ def test_asm_tier_workloads_sim(sim):
     assert int(summary["ok"]) >= len(recs) - 5
 
 
+def test_asm_signed_literal_compares_and_views_sim(sim):
+    """Signed compares against literals (the sign test + high-limb equality path) at every shape of
+    literal — zero, small, at 2^31, multi-limb, -1, small negative, the extremes — on both sides,
+    over operands whose high limbs are sign or zero extensions (so the high-limb equality is often
+    true), and byte CONCAT chains read through by EXTRACTs and CONCATs (views): eval (row-major and
+    tiled) and search kernels against the C port."""
+    from mythril_amd import search
+    from mythril_amd.smt import terms as T
+
+    rng = random.Random(11)
+    recs = []
+    for w in (40, 64, 72, 96, 160, 256):
+        x = T.BitVecVar(f"sx{w}", w)
+        n8 = T.BitVecVar(f"n8_{w}", 8)
+        n32 = T.BitVecVar(f"n32_{w}", 32)
+        ops = [x, T.sign_extend(w - 8, n8), T.sign_extend(w - 32, n32), T.zero_extend(w - 32, n32)]
+        lits = {0, 1, 29, (1 << 31) - 1, 1 << 31, (1 << 32) + 5, (1 << (w - 1)) - 1, 1 << (w - 1),
+                (1 << w) - 1, (1 << w) - 2, (1 << w) - (1 << 33), (1 << w) - 200, (1 << w) - (1 << 31)}
+        for k in sorted(lits):
+            K = T.BitVecVal(k % (1 << w), w)
+            for op in ("bvslt", "bvsle", "bvsgt", "bvsge"):
+                a = rng.choice(ops)
+                c1, c2 = T.bvcmp(op, a, K), T.bvcmp(op, K, rng.choice(ops))
+                roots = [T.or_(c1, T.not_(c2)) if rng.random() < 0.5 else c1]
+                P, blob = search.prepare(roots)
+                recs.append(record(0, P.to_bytes(), blob, rng.getrandbits(32), rng.getrandbits(63), 128))
+                prev = P.watch
+                P.set_watch([])
+                pe = P.to_bytes()
+                P.set_watch(prev)
+                recs.append(record(1 + (k & 1), pe, None, rng.getrandbits(32), 0, 64 * 3 + 5))
+    # byte chains: a word built from 32 bytes, read through by extracts and a wider concat
+    bs = [T.BitVecVar(f"cb{i}", 8) for i in range(32)]
+    word = bs[0]
+    for b in bs[1:]:
+        word = T.concat(word, b)
+    for lo, hi in ((0, 255), (8, 263 - 8), (3, 40), (100, 131), (248, 255)):
+        ex = T.extract(hi, lo, word)
+        wide = T.concat(T.BitVecVar("cw", 24), T.concat(ex, T.BitVecVal(5, 8)))
+        roots = [T.or_(T.bvcmp("bvult", T.extract(hi - lo, 0, wide), T.BitVecVal(1 << min(hi - lo, 200), hi - lo + 1)),
+                       T.eq(T.extract(7, 0, wide), T.BitVecVal(5, 8)))]
+        roots.append(T.not_(T.eq(T.extract(hi - lo + 8, 8, wide), T.BitVecVal(0, hi - lo + 1))))
+        P, blob = search.prepare(roots)
+        recs.append(record(0, P.to_bytes(), blob, rng.getrandbits(32), rng.getrandbits(63), 192))
+        P.set_watch([])
+        for kind in (1, 2):
+            recs.append(record(kind, P.to_bytes(), None, rng.getrandbits(32), 0, 64 * 4 + 9))
+    rc, summary, bad, err = run_sim(sim, b"".join(recs), {"MYTHGPU_JIT_ASM_CHECK": "1"})
+    assert rc == 0, f"{summary}\n" + "\n".join(bad) + "\n" + err[-3000:]
+    assert int(summary["ok"]) == len(recs), summary
+    print("signed literal compares / views:", summary)
+
+
 def _full_worker(args):
     exe, lo, hi, cfg, kind = args
     recs = _fuzz_records(lo, hi, full=True) if kind == "laser" else _tier_records(lo, hi, full=True)
