@@ -153,6 +153,14 @@ class Emitter {
     pos++;
     for (int r : wr) vw[r] = pos - 1;
   }
+  // SGPR pair s..s+1 written by a VALU within the last two instructions (a VALU read would wait)
+  bool fresh_valu_write(int s) const {
+    for (int r : {s, s + 1}) {
+      auto it = vw.find(r);
+      if (it != vw.end() && it->second + 3 - pos > 0) return true;
+    }
+    return false;
+  }
   void salu(const std::string& s, std::initializer_list<int> wr = {}) {
     o << "  " << s << "\n";
     pos++;
@@ -378,11 +386,100 @@ struct Gen {
         opl.pop_back();
       }
     };
-    for (size_t k = 0; k < v.size(); k++)
-      if (v[k].op == K_ASSERT || v[k].op == K_WATCH) visit((int32_t)k);
+    if (eval_kernel && !no_greedy()) {
+      greedy_roots(v, operands, done, visit);
+    } else {
+      for (size_t k = 0; k < v.size(); k++)
+        if (v[k].op == K_ASSERT || v[k].op == K_WATCH) visit((int32_t)k);
+    }
     for (size_t k = 0; k < v.size(); k++)
       if (!done[k]) visit((int32_t)k);
     code.swap(out);
+  }
+  // MYTHGPU_JIT_ASM_NO_GREEDY=1: the eval kernel's constraints in program order
+  static bool no_greedy() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_GREEDY");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
+  // The eval kernel evaluates every constraint (no early exit), so their order is free: each step
+  // emits the constraint whose not-yet-emitted cone leaves the fewest limbs live — the limbs of
+  // cone values still read outside it, less the limbs of live values whose last readers are in it
+  // (C4: coordinate rows and storage keys loaded early were held across hundreds of constraints
+  // that did not read them; 246 live VGPRs in program order)
+  template <class Ops, class Visit>
+  void greedy_roots(const std::vector<Instr>& v, Ops& operands, const std::vector<char>& done, Visit& visit) {
+    const size_t n = v.size();
+    std::vector<std::vector<int32_t>> opl(n);
+    std::vector<int32_t> users(n, 0);  // readers not yet emitted
+    for (size_t k = 0; k < n; k++) {
+      operands(v[k], opl[k]);
+      std::sort(opl[k].begin(), opl[k].end());
+      opl[k].erase(std::unique(opl[k].begin(), opl[k].end()), opl[k].end());
+      for (int32_t o : opl[k]) users[o]++;
+    }
+    auto limbs_of = [&](int32_t k) -> int32_t {
+      const Instr& in = v[k];
+      if (in.op == K_CONST || in.dst == MG_NONE || in.dst >= P.vwidth.size()) return 0;
+      const uint32_t w = P.vwidth[in.dst];
+      return w <= 1 ? 0 : (int32_t)Lw(w);
+    };
+    std::vector<int32_t> roots;
+    for (size_t k = 0; k < n; k++)
+      if (v[k].op == K_ASSERT || v[k].op == K_WATCH) roots.push_back((int32_t)k);
+    std::vector<int32_t> mark(n, -1), inner(n, 0);  // cone membership stamp; readers inside the cone
+    std::vector<int32_t> cone, st;
+    int32_t stamp = 0;
+    auto gather = [&](int32_t r) {  // the not-yet-emitted cone of r into `cone`, reader counts into inner
+      cone.clear();
+      st.assign(1, r);
+      mark[r] = ++stamp;
+      while (!st.empty()) {
+        const int32_t x = st.back();
+        st.pop_back();
+        cone.push_back(x);
+        for (int32_t o : opl[x]) {
+          if (done[o]) continue;
+          if (mark[o] != stamp) {
+            mark[o] = stamp;
+            st.push_back(o);
+          }
+        }
+      }
+      for (int32_t x : cone)
+        for (int32_t o : opl[x]) inner[o] = 0;
+      for (int32_t x : cone)
+        for (int32_t o : opl[x]) inner[o]++;
+    };
+    std::vector<char> taken(roots.size(), 0);
+    for (size_t step = 0; step < roots.size(); step++) {
+      int64_t best = INT64_MIN;
+      size_t bi = 0;
+      for (size_t i = 0; i < roots.size(); i++) {
+        if (taken[i]) continue;
+        gather(roots[i]);
+        int64_t score = 0;
+        for (int32_t x : cone) {
+          if (users[x] > inner[x]) score -= limbs_of(x);  // read again later: stays live
+          for (int32_t o : opl[x])
+            if (done[o] && mark[o] != stamp && users[o] == inner[o]) {
+              score += limbs_of(o);  // its last readers: freed
+              inner[o] = 1 << 30;   // counted once
+            }
+        }
+        if (score > best) {
+          best = score;
+          bi = i;
+        }
+      }
+      taken[bi] = 1;
+      gather(roots[bi]);
+      for (int32_t x : cone)
+        for (int32_t o : opl[x]) users[o]--;
+      visit(roots[bi]);
+    }
   }
 
   // ---------------------------------------------------------------------------------------
@@ -1260,6 +1357,30 @@ struct Gen {
     xcache.clear();
     xby.clear();
     for (auto& d : held) drop(d);
+    for (auto& kv : hcache) drop(kv.second);
+    hcache.clear();
+    hby.clear();
+    h_last.clear();
+  }
+  // The reduced difference of a value's high limbs against a sign extension (slt_literal): LASER
+  // compares one value with many literals (x >s 0, x >s 1, ... one per switch arm), whose high limbs
+  // are the same registers each time — kept like the XOR cache, keyed by the limbs' allocation tags
+  std::map<std::vector<uint64_t>, Limb> hcache;
+  std::multimap<uint32_t, std::vector<uint64_t>> hby;
+  std::map<std::vector<uint64_t>, uint64_t> h_last;
+  void hcache_free(uint32_t g) {
+    auto r = hby.equal_range(g);
+    std::vector<std::vector<uint64_t>> keys;
+    for (auto it = r.first; it != r.second; ++it) keys.push_back(it->second);
+    hby.erase(r.first, r.second);
+    for (const auto& k : keys) {
+      auto it = hcache.find(k);
+      if (it == hcache.end()) continue;
+      const Limb d = it->second;
+      hcache.erase(it);
+      h_last.erase(k);
+      drop(d);
+    }
   }
 
   // a == b over the first Lk limbs of values a and b.  The reduced difference (OR of the limbs' XORs)
@@ -1320,6 +1441,14 @@ struct Gen {
       const Limb d = it->second;
       x_last.erase(it->first);
       xcache.erase(it);  // its xby entries go stale: xcache_free skips keys no longer cached
+      drop(d);
+      return true;
+    }
+    if (!hcache.empty()) {
+      auto it = lru(hcache, h_last);
+      const Limb d = it->second;
+      h_last.erase(it->first);
+      hcache.erase(it);  // its hby entries go stale: hcache_free skips keys no longer cached
       drop(d);
       return true;
     }
@@ -1429,7 +1558,37 @@ struct Gen {
       } else {
         neg = lt_mask({Lit((1u << tb) - 1u)}, {rv[La - 1]}, 32, false);
       }
-      const Mask eh = eq_mask(hi);
+      Mask eh;
+      {
+        const bool cacheable = lvn_on && caches && !cond && !no_lvn();
+        std::vector<uint64_t> key;
+        bool regs_ok = true;
+        for (const auto& pr : hi) {
+          key.push_back(lid(pr.first));
+          key.push_back(lid(pr.second));
+          if (pr.first.reg() && (int)pr.first.v >= E.vfirst && !pr.first.g) regs_ok = false;
+        }
+        auto it = cacheable && regs_ok ? hcache.find(key) : hcache.end();
+        if (it != hcache.end()) {
+          h_last[key] = ++tick;
+          eh.k = 2;
+          eh.s = E.salloc();
+          E.valu("v_cmp_eq_u32_e64 " + SP(eh.s) + ", 0, " + VL(it->second), {}, {eh.s, eh.s + 1});
+        } else {
+          Limb keep{};
+          eh = eq_mask(hi, cacheable && regs_ok ? &keep : nullptr);
+          bool alias = false;  // an operand limb itself: a cached reference would pin its register
+          for (const auto& pr : hi) alias = alias || (pr.first.reg() && pr.first.v == keep.v);
+          if (keep.reg() && alias) {
+            drop(keep);
+          } else if (keep.reg()) {
+            hcache[key] = keep;  // the reference eq_mask handed over
+            h_last[key] = ++tick;
+            for (const auto& pr : hi)
+              if (pr.first.reg() && (int)pr.first.v >= E.vfirst) hby.insert({pr.first.g, key});
+          }
+        }
+      }
       Mask lo;
       if (k < 0) {
         lo.k = 1;
@@ -1680,6 +1839,36 @@ struct Gen {
     }
     const Limb d = fresh();
     E.valu("v_cndmask_b32_e32 " + VL(d) + ", " + src(ff) + ", " + VL(tt) + ", vcc", {kVCC, kVCC + 1});
+    drop(tmp);
+    drop(tmp2);
+    return d;
+  }
+  // m ? t : f with the mask in an SGPR pair (VOP3: the mask is the one constant-bus operand, so a
+  // literal that is not an inline constant comes through a VGPR)
+  static bool no_ite_e64() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_ITE_E64");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
+  Limb sel_mask(const Limb& t, const Limb& f, const Mask& m) {
+    if (t == f) {
+      E.retain(t);
+      return t;
+    }
+    if (t.k == LU || f.k == LU) fail("internal: a limb the demand analysis dropped was read");
+    Limb tt = t, ff = f, tmp, tmp2;
+    if (tt.lit() && !inl(tt.v)) {
+      tmp = vreg(tt);
+      tt = tmp;
+    }
+    if (ff.lit() && !inl(ff.v)) {
+      tmp2 = vreg(ff);
+      ff = tmp2;
+    }
+    const Limb d = fresh();
+    E.valu("v_cndmask_b32_e64 " + VL(d) + ", " + src(ff) + ", " + src(tt) + ", " + SP(m.s), {m.s, m.s + 1});
     drop(tmp);
     drop(tmp2);
     return d;
@@ -3720,6 +3909,14 @@ struct Gen {
           set(d, r);
           break;
         }
+        if (c.k == 2 && !no_ite_e64() && !E.fresh_valu_write(c.s)) {  // the mask straight from its SGPR pair
+          for (uint32_t j = 0; j < Ld; j++) {
+            if (!(need[d] >> j & 1)) continue;
+            r[j] = sel_mask(limb(in.b, j), limb(in.c, j), c);
+          }
+          set(d, r);
+          break;
+        }
         mask_to_vcc(c);
         for (uint32_t j = 0; j < Ld; j++) {
           if (!(need[d] >> j & 1)) continue;
@@ -4075,11 +4272,17 @@ struct Gen {
     eqdiff.clear();  // a kernel abandoned midway (AsmFail: out of VGPRs at this depth) left its entries
     xcache.clear();
     xby.clear();
+    hcache.clear();
+    hby.clear();
+    h_last.clear();
     litcache.clear();
     lit_last.clear();
     x_last.clear();
     eq_last.clear();
-    E.on_free = [this](uint32_t g) { xcache_free(g); };
+    E.on_free = [this](uint32_t g) {
+      xcache_free(g);
+      hcache_free(g);
+    };
     E.on_pressure = [this]() { return evict_one(); };
     E.on_spressure = [this]() { return spill_mask(); };
     lvn_on = true;
@@ -4288,12 +4491,92 @@ struct Gen {
       row_reg[rows_issued++] = d;
     }
   }
+  // --- LDS-staged rows (tiled SoA): the row queue in LDS instead of VGPRs ---------------------
+  // Each row is fetched by global_load_lds_dword (LDS-DMA: no VGPR while in flight) `gdepth` rows
+  // ahead of its use into a per-wave LDS slot, and read into a VGPR by ds_read_b32 `sdepth` rows
+  // ahead.  The queue's depth is then bounded by LDS (160 KiB per CU), not by the VGPRs the program
+  // leaves: C4's program holds ~200 VGPRs (2 waves per SIMD), which left the register queue ~12
+  // rows — 0.53 of HBM.  Slots: rows 0 .. D-1 of a group in slots 0 .. D-1 (the next group's are
+  // fetched there while this group's last D rows are consumed), rows >= D in D+1 rotating slots
+  // D + (p - D) % (D + 1): a slot is refilled only after the ds_read of its previous row was waited
+  // for.  s34 = the wave's slot base, glds_v its LDS address per lane.
+  bool glds = false;
+  uint32_t gdepth = 0, sdepth = 4;
+  Limb glds_v;
+  size_t gl_issued = 0, staged = 0;
+  long lgkm_n = 0;
+  std::vector<long> gseq, lseq;  // VMEM / LGKM issue index of each row's glds / ds_read
+  std::vector<Limb> stage_reg;
+  static bool glds_env() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_GLDS");
+      return !(g && g[0] == '0');
+    }();
+    return on;
+  }
+  static uint32_t glds_fixed() {
+    static const uint32_t n = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_GLDS");
+      const int v = g ? atoi(g) : 0;
+      return v > 1 ? (uint32_t)std::min(v, 60) : 0u;
+    }();
+    return n;
+  }
+  uint32_t glds_slot(size_t p) const { return p < gdepth ? (uint32_t)p : gdepth + (uint32_t)((p - gdepth) % (gdepth + 1)); }
+  uint32_t glds_slots() const { return gdepth + (rows.size() > gdepth ? gdepth + 1 : 0); }
+  // glds of row index idx: idx < M this group's row, else the next group's row idx - M
+  void glds_issue(size_t idx) {
+    const size_t M = rows.size();
+    const bool next = idx >= M;
+    const size_t p = next ? idx - M : idx;
+    const int b = next ? 28 : 26;
+    E.salu("s_add_u32 m0, s34, " + hexs(glds_slot(p) * 256u));
+    const uint64_t byte = (uint64_t)rows[p] * 256u;
+    std::string base = "s[" + std::to_string(b) + ":" + std::to_string(b + 1) + "]";
+    if (byte) {
+      E.salu("s_add_u32 s40, " + S(b) + ", " + hexs((uint32_t)byte), {40});
+      E.salu("s_addc_u32 s41, " + S(b + 1) + ", 0", {41});
+      base = "s[40:41]";
+    } else {
+      E.salu("s_nop 0");  // M0 -> LDS-DMA: one wait state
+    }
+    E.mem("global_load_lds_dword v2, " + base + "  ; soa row " + std::to_string(rows[p]) + (next ? " (next group)" : ""));
+    if (!next) gseq[p] = loads;
+    loads++;
+  }
+  void glds_upto(size_t u) {
+    const size_t M = rows.size();
+    while (gl_issued <= u && gl_issued < M + gdepth) glds_issue(gl_issued++);
+  }
+  void stage_upto(size_t u) {
+    const size_t M = rows.size();
+    while (staged <= u && staged < M) {
+      const size_t t = staged++;
+      const long after = loads - gseq[t] - 1;
+      E.ctl("s_waitcnt vmcnt(" + std::to_string(std::min<long>(std::max<long>(after, 0), 63)) + ")");
+      const Limb dv = fresh();
+      E.mem("ds_read_b32 " + VL(dv) + ", " + VL(glds_v) + " offset:" + std::to_string(glds_slot(t) * 256u));
+      lseq[t] = lgkm_n++;
+      stage_reg[t] = dv;
+    }
+  }
+
   std::vector<Limb> soa_limbs(const Instr& in, uint32_t d) {
     const uint32_t Lc = Lw(in.wd);
     std::vector<Limb> r(Lc);
     for (uint32_t j = 0; j < Lc; j++) {
       if (!(need[d] >> j & 1)) continue;
       if (rows_used >= rows.size() || rows[rows_used] != in.p1 + j) fail("internal: SoA row order");
+      if (glds) {
+        const size_t p = rows_used++;
+        stage_upto(p);
+        E.ctl("s_waitcnt lgkmcnt(" + std::to_string(std::min<long>(std::max<long>(lgkm_n - lseq[p] - 1, 0), 15)) + ")");
+        r[j] = stage_reg[p];
+        stage_reg[p] = Limb{};
+        glds_upto(p + gdepth);  // refills the slot row p - 1 (region 2) or row p + D - M (region 1) held
+        stage_upto(p + sdepth);
+        continue;
+      }
       issue_rows(rows_used + 1);
       // loads return in order: wait until only the loads issued after this row are outstanding
       // (stores are not counted: the watch stores are conditional; an uncounted younger store only
@@ -4333,6 +4616,13 @@ struct Gen {
           if (in.dst < need.size() && (need[in.dst] >> j & 1)) rows.push_back(in.p1 + j);
     row_reg.assign(rows.size(), Limb{});
     row_seq.assign(rows.size(), 0);
+    glds = tiled && glds_env() && !rows.empty() && gdepth > 0;
+    if (glds) {
+      gdepth = std::min<uint32_t>(gdepth, (uint32_t)rows.size());
+      gseq.assign(rows.size(), 0);
+      lseq.assign(rows.size(), 0);
+      stage_reg.assign(rows.size(), Limb{});
+    }
     auto& o = E.o;
     o << "  .text\n  .globl " << name << "\n  .p2align 8\n  .type " << name << ",@function\n" << name << ":\n";
     // arguments (soa, n, verdict_out, watch, nblk): s[4:5] soa, s[8:9] n, s[10:11] verdict, s[12:13] watch, s14 nblk
@@ -4354,8 +4644,14 @@ struct Gen {
     const std::string loop = E.newlab(), exit_ = E.newlab();
     // the ring: the first rows of the wave's first group, loaded before the loop
     ring_reg.clear();
-    for (size_t q = 0; q < std::min<size_t>(prefetch_depth(), rows.size()); q++) ring_reg.push_back(fresh());
+    if (!glds)
+      for (size_t q = 0; q < std::min<size_t>(prefetch_depth(), rows.size()); q++) ring_reg.push_back(fresh());
     vnext = tiled ? Limb{} : fresh();
+    if (glds) {  // the wave's LDS slots: s34 = wave * slots * 256, glds_v = s34 + 4 * lane
+      glds_v = fresh();
+      E.salu("s_mul_i32 s34, s3, " + hexs(glds_slots() * 256u), {34});
+      E.valu("v_lshl_add_u32 " + VL(glds_v) + ", v1, 2, s34", {34});
+    }
     if (tiled) {  // s31 = last group index, s32 = the grid stride in groups
       E.salu("s_add_u32 s31, s8, 63", {31});
       E.salu("s_lshr_b32 s31, s31, 6", {31});
@@ -4374,6 +4670,8 @@ struct Gen {
       E.valu("v_lshlrev_b32_e32 v2, 2, v2");
     }
     for (size_t q = 0; q < ring_reg.size(); q++) load_row(ring_reg[q], rows[q], 26, "v2", " (first group)");
+    if (glds)
+      for (size_t q = 0; q < gdepth; q++) glds_issue(q);  // the first group's first rows
     E.label(loop);
     E.salu("s_cmp_lt_u32 s16, s8");
     E.ctl("s_cbranch_scc0 " + exit_);
@@ -4402,10 +4700,18 @@ struct Gen {
     rows_used = 0;
     loads = 0;
     for (size_t q = 0; q < ring_reg.size(); q++) row_seq[q] = (long)q - (long)ring_reg.size();
+    if (glds) {  // rows 0 .. D-1 came in the previous iteration, its last D VMEM loads
+      for (size_t q = 0; q < gdepth; q++) gseq[q] = (long)q - (long)gdepth;
+      gl_issued = gdepth;
+      staged = 0;
+      lgkm_n = 0;
+    }
     body("");
     if (rows_used != rows.size()) fail("internal: SoA rows left unread");
+    if (glds && (gl_issued != rows.size() + gdepth || staged != rows.size())) fail("internal: LDS row queue");
     for (const Limb& l : ring_reg) drop(l);
     if (!tiled) drop(vnext);
+    if (glds) drop(glds_v);
     ring_reg.clear();
     for (int r = E.vfirst; r < 256; r++)
       if (E.vref[r]) fail("internal: VGPR v" + std::to_string(r) + " still held after the body");
@@ -4422,7 +4728,7 @@ struct Gen {
     const int nv = std::max(E.vhigh, kV0), ns = std::max(E.shigh, 56);
     const int accum = (nv + 3) / 4 * 4;
     o << "  .section .rodata,\"a\",@progbits\n  .p2align 6, 0x0\n  .amdhsa_kernel " << name << "\n"
-      << "    .amdhsa_group_segment_fixed_size 0\n    .amdhsa_private_segment_fixed_size 0\n"
+      << "    .amdhsa_group_segment_fixed_size " << eval_lds_bytes() << "\n    .amdhsa_private_segment_fixed_size 0\n"
       << "    .amdhsa_kernarg_size 36\n"
       << "    .amdhsa_user_sgpr_count 2\n    .amdhsa_user_sgpr_kernarg_segment_ptr 1\n"
       << "    .amdhsa_system_sgpr_workgroup_id_x 1\n    .amdhsa_system_vgpr_workitem_id 0\n"
@@ -4435,6 +4741,9 @@ struct Gen {
     meta_sgpr[name] = ns + 6;
     return o.str();
   }
+
+  // the eval kernel's LDS: four waves' row slots (256 B each) when rows are LDS-staged
+  uint32_t eval_lds_bytes() const { return glds ? 4u * glds_slots() * 256u : 0u; }
 
   int labels = 0;  // label numbers continue across the kernels of one module
   std::string kernel(const std::string& name) {
@@ -4716,7 +5025,7 @@ std::string metadata(const std::map<std::string, int>& vg, const std::map<std::s
 
 }  // namespace
 
-std::string metadata_eval(int vg, int sg) {
+std::string metadata_eval(int vg, int sg, uint32_t lds) {
   std::ostringstream o;
   auto arg = [&](uint32_t off, uint32_t size, const char* kind, bool global) {
     o << "      - .offset: " << off << "\n        .size: " << size << "\n        .value_kind: " << kind << "\n";
@@ -4728,7 +5037,7 @@ std::string metadata_eval(int vg, int sg) {
   arg(16, 8, "global_buffer", true);
   arg(24, 8, "global_buffer", true);
   arg(32, 4, "by_value", false);
-  o << "    .group_segment_fixed_size: 0\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 36\n"
+  o << "    .group_segment_fixed_size: " << lds << "\n    .kernarg_segment_align: 8\n    .kernarg_segment_size: 36\n"
     << "    .max_flat_workgroup_size: 256\n    .name: mgj_eval\n    .private_segment_fixed_size: 0\n"
     << "    .sgpr_count: " << sg << "\n    .sgpr_spill_count: 0\n    .symbol: mgj_eval.kd\n"
     << "    .uniform_work_group_size: 1\n    .uses_dynamic_stack: false\n    .vgpr_count: " << vg
@@ -4794,6 +5103,42 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
           ks = g.kernel_eval("mgj_eval");
         }
       }
+      // LDS-staged rows (tiled SoA): the queue depth the LDS leaves at the kernel's occupancy (160 KiB
+      // per CU over `waves` four-wave workgroups, 2 D + 1 slots of 256 B per wave), taken when deeper
+      // than the register queue just sized.  MYTHGPU_JIT_ASM_GLDS=0 keeps the register queue, =N fixes D
+      if (g.tiled && Gen::glds_env()) {
+        const std::string vks = ks;
+        const uint32_t vdepth = g.depth;
+        const int vnv = g.meta_vgpr["mgj_eval"];
+        const uint32_t M = (uint32_t)g.rows.size();
+        auto depth_for = [&](int nv) {
+          if (Gen::glds_fixed()) return std::min<uint32_t>(Gen::glds_fixed(), M);
+          const int w = std::max(1, std::min(8, 512 / ((nv + 7) / 8 * 8)));
+          const int slots = 160 / w;
+          return std::min<uint32_t>({32u, M, (uint32_t)std::max(1, (slots - 1) / 2)});
+        };
+        g.gdepth = depth_for(vnv);
+        bool ok = true;
+        try {
+          g.labels = 0;
+          ks = g.kernel_eval("mgj_eval");
+          const uint32_t d2 = depth_for(g.meta_vgpr["mgj_eval"]);
+          if (d2 != g.gdepth) {
+            g.gdepth = d2;
+            g.labels = 0;
+            ks = g.kernel_eval("mgj_eval");
+          }
+        } catch (const AsmFail&) {
+          ok = false;
+        }
+        if (!ok || (!Gen::glds_fixed() && g.gdepth <= vdepth)) {  // the register queue is as deep
+          g.gdepth = 0;
+          g.depth = vdepth;
+          g.glds = false;
+          ks = vks;
+          g.meta_vgpr["mgj_eval"] = vnv;
+        }
+      }
       if (!getenv("MYTHGPU_JIT_ASM_NOPOOL")) {
         std::vector<std::pair<uint32_t, uint32_t>> by;
         for (const auto& kv : g.census)
@@ -4806,7 +5151,7 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
           ks = g.kernel_eval("mgj_eval");
         }
       }
-      o << ks << metadata_eval(g.meta_vgpr["mgj_eval"], g.meta_sgpr["mgj_eval"]);
+      o << ks << metadata_eval(g.meta_vgpr["mgj_eval"], g.meta_sgpr["mgj_eval"], g.eval_lds_bytes());
       out = o.str();
       return MG_OK;
     }

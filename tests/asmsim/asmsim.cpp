@@ -44,6 +44,7 @@ namespace {
   X(v_madak_f32) X(v_cvt_f32_ubyte1) X(v_cvt_f32_ubyte2) X(v_cvt_f32_ubyte3) X(v_bcnt_u32_b32) X(v_max_i32)       \
   X(v_min_i32) X(v_bfrev_b32) X(v_alignbyte_b32) X(v_xor3_b32) X(v_ashrrev_i64) X(v_mul_hi_i32) X(v_add_i32) X(v_sub_i32)                      \
   X(global_load_dword) X(global_load_dwordx2) X(global_load_dwordx4) X(global_store_byte) X(global_store_dword)  \
+  X(global_load_lds_dword)                                                                                          \
   X(global_atomic_umin_x2) X(global_atomic_add_x2) X(flat_atomic_umin_x2) X(flat_atomic_add_x2)                  \
   X(ds_read_b32) X(ds_write_b32) X(ds_read_b64) X(ds_write_b64)                                                   \
   X(ds_read2_b32) X(ds_read_b128) X(ds_write_b128) X(ds_min_u64) X(ds_add_u64) X(ds_add_rtn_u32) X(ds_write2_b32)
@@ -147,6 +148,11 @@ Opd operand(const std::string& t0) {
   }
   if (t == "off") {
     o.k = O_OFF;
+    return o;
+  }
+  if (t == "m0") {  // M0 as SGPR 108 (the LDS-DMA destination base)
+    o.k = O_S;
+    o.r = 108;
     return o;
   }
   if (reg('v', O_V) || reg('s', O_S)) return o;
@@ -376,10 +382,14 @@ Buffer& Memory::of(uint64_t base) {
 
 namespace {
 
-constexpr int kNS = 108;  // s0..s105, vcc = s106:107
+constexpr int kNS = 109;  // s0..s105, vcc = s106:107, m0 = s108
+constexpr int kM0 = 108;
 
 struct Pend {
   std::vector<int> v, s;
+  // LDS dwords a global_load_lds writes (on vmcnt) or a ds_read reads (on lgkmcnt) while in flight
+  std::vector<uint32_t> lds;
+  std::vector<uint16_t>* ldsp = nullptr;
 };
 
 struct Wave {
@@ -395,6 +405,7 @@ struct Wave {
   bool scc = false;
   size_t pc = 0;
   int64_t slot = 0;
+  int64_t m0slot = -1000;  // slot of the last M0 write
   bool done = false, barrier = false;
   int id = 0;
 };
@@ -406,6 +417,8 @@ struct Ctx {
   Stats* st;
   int block = 0;
   uint64_t image_base = 0;
+  // per LDS dword: global_load_lds writes in flight (ldsw) and ds_reads in flight (ldsr)
+  std::vector<uint16_t> ldsw = std::vector<uint16_t>(lds.size() / 4 + 1, 0), ldsr = ldsw;
 };
 
 [[noreturn]] void fail(const Wave& w, const Ctx& c, const Ins& in, const std::string& what) {
@@ -469,6 +482,7 @@ void swrite(Wave& w, const Ctx& c, const Ins& in, const Opd& o, uint32_t v) {
   w.s[o.r] = v;
   w.sinit[o.r] = true;
   w.sw[o.r] = -1000;  // an SALU write: no VALU hazard on the new value
+  if (o.r == kM0) w.m0slot = w.slot;
 }
 void swrite64(Wave& w, const Ctx& c, const Ins& in, const Opd& o, uint64_t v) {
   if (o.k == O_EXEC) {
@@ -591,6 +605,7 @@ void retire(Wave& w, std::deque<Pend>& q, int keep) {
   while ((int)q.size() > keep) {
     for (int r : q.front().v) w.vpend[r]--;
     for (int r : q.front().s) w.spend[r]--;
+    for (uint32_t d : q.front().lds) (*q.front().ldsp)[d]--;
     q.pop_front();
   }
 }
@@ -940,12 +955,19 @@ bool step(Wave& w, Ctx& c) {
         uint32_t adr[64];  // the destination may overlap the address register
         for (int l = 0; l < 64; l++) adr[l] = ad.lo(l);
         Pend pd;
+        pd.ldsp = &c.ldsr;
         for (int q = 0; q < nw; q++) {
           uint32_t* d = vdst(w, c, in, a[0], q);
           const uint32_t o = op == OP_ds_read2_b32 ? 4u * (uint32_t)(q ? in.offset1 : in.offset0)
                                                    : (uint32_t)in.offset + 4u * q;
           for (int l = 0; l < 64; l++)
-            if (w.exec >> l & 1) memcpy(&d[l], lds_at(adr[l] + o, 4), 4);
+            if (w.exec >> l & 1) {
+              memcpy(&d[l], lds_at(adr[l] + o, 4), 4);
+              const uint32_t dw = (adr[l] + o) / 4;
+              if (c.ldsw[dw]) fail(w, c, in, "LDS read while a global_load_lds into it is in flight");
+              c.ldsr[dw]++;
+              pd.lds.push_back(dw);
+            }
           pd.v.push_back(a[0].r + q);
           w.vpend[a[0].r + q]++;
         }
@@ -974,6 +996,7 @@ bool step(Wave& w, Ctx& c) {
           for (int q = 0; q < nw; q++) {
             const uint32_t o = op == OP_ds_write2_b32 ? 4u * (uint32_t)(q ? in.offset1 : in.offset0)
                                                       : (uint32_t)in.offset + 4u * q;
+            if (c.ldsw[(ad.lo(l) + o) / 4]) fail(w, c, in, "LDS write while a global_load_lds into it is in flight");
             memcpy(lds_at(ad.lo(l) + o, 4), &dv[q][l], 4);
           }
         }
@@ -1022,6 +1045,41 @@ bool step(Wave& w, Ctx& c) {
       return true;
     }
     // global: vaddr + saddr (32-bit lane offsets) or a 64-bit vaddr with "off"
+    if (op == OP_global_load_lds_dword) {
+      // LDS-DMA: lane l's dword at its global address lands in LDS at M0 + 4 l (vmcnt counts it)
+      need(2);
+      ValuCheck vc;
+      if (a[0].k != O_V) fail(w, c, in, "global address is not a VGPR");
+      const bool off = a[1].k == O_OFF;
+      const Src av = vsrc(w, c, in, a[0], off, vc, true);
+      if (off && a[0].n != 2) fail(w, c, in, "64-bit address is not a VGPR pair");
+      uint64_t sb = 0;
+      if (!off) {
+        if (a[1].k != O_S || a[1].n != 2) fail(w, c, in, "global base is not an SGPR pair");
+        vmem_sgpr(w, c, in, a[1]);
+        sb = (uint64_t)w.s[a[1].r] | ((uint64_t)w.s[a[1].r + 1] << 32);
+      }
+      if (in.offset != 0) fail(w, c, in, "global_load_lds with an instruction offset (not modelled)");
+      chk_s_read(w, c, in, kM0);
+      if (w.slot - w.m0slot < 2) fail(w, c, in, "global_load_lds within one wait state of an M0 write");
+      const uint32_t base = w.s[kM0];
+      Pend pd;
+      pd.ldsp = &c.ldsw;
+      for (int l = 0; l < 64; l++) {
+        if (!(w.exec >> l & 1)) continue;
+        const uint64_t ad = off ? av.v64(l) : sb + av.lo(l);
+        const uint32_t la = base + 4u * (uint32_t)l;
+        if ((la & 3) || (uint64_t)la + 4 > c.lds.size()) fail(w, c, in, "global_load_lds past the kernel's LDS");
+        if (c.ldsr[la / 4]) fail(w, c, in, "global_load_lds into LDS a ds_read in flight still reads");
+        if (c.ldsw[la / 4]) fail(w, c, in, "two global_load_lds in flight into the same LDS");
+        memcpy(c.lds.data() + la, c.mem.at(ad, 4), 4);
+        c.ldsw[la / 4]++;
+        pd.lds.push_back(la / 4);
+      }
+      w.vm.push_back(pd);
+      w.pc = next;
+      return true;
+    }
     const bool store = op == OP_global_store_byte || op == OP_global_store_dword;
     if (op == OP_flat_atomic_umin_x2 || op == OP_flat_atomic_add_x2) {
       // flat address = the buffer's address (no LDS aperture in this simulation)
