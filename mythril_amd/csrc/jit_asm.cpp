@@ -665,9 +665,19 @@ struct Gen {
   // every link (C4's eval program: 1,565 VALU per candidate in CONCATs).  The view's operands live
   // until its reader (last[] extended).  MYTHGPU_JIT_ASM_NO_VIEWS=1 materialises every value.
   std::vector<uint8_t> view;  // value id -> a view
+  std::vector<uint32_t> slt_lits;  // value id -> signed compares of it against a literal
+  bool slt_many = false;           // the compare being emitted reads such a value 3+ times
   void plan_views() {
     const size_t nv = P.vwidth.size();
     view.assign(nv, 0);
+    slt_lits.assign(nv, 0);
+    for (const Instr& in : code) {
+      if (in.op != K_SLT && in.op != K_SLE) continue;
+      const Instr* da = def_of(in.a);
+      const Instr* db = def_of(in.b);
+      if (da && da->op == K_CONST && in.b < nv) slt_lits[in.b]++;
+      if (db && db->op == K_CONST && in.a < nv) slt_lits[in.a]++;
+    }
     static const bool off = [] {
       const char* g = getenv("MYTHGPU_JIT_ASM_NO_VIEWS");
       return g && g[0] == '1';
@@ -1521,6 +1531,57 @@ struct Gen {
     }();
     return on;
   }
+  static bool no_slt_clamp() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_SLT_CLAMP");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
+  // the 32-bit clamp of x (La limbs, sign bit tb of the top limb): x_lo when the limbs above are
+  // zero, else 0 for a negative x and ~0 for a positive one; held in hcache (owned by the caller: a
+  // retained reference), or an unset limb when x's registers carry no allocation tags
+  Limb clamp32(const std::vector<Limb>& rv, uint32_t La, uint32_t tb) {
+    if (!(lvn_on && caches && !cond && !no_lvn())) return Limb{};
+    std::vector<uint64_t> key{0xC1A3Full, tb};
+    for (uint32_t j = 0; j < La; j++) {
+      if (rv[j].reg() && (int)rv[j].v >= E.vfirst && !rv[j].g) return Limb{};
+      key.push_back(lid(rv[j]));
+    }
+    auto it = hcache.find(key);
+    if (it != hcache.end()) {
+      h_last[key] = ++tick;
+      E.retain(it->second);
+      return it->second;
+    }
+    std::vector<std::pair<Limb, Limb>> hz;
+    for (uint32_t j = 1; j < La; j++) hz.push_back({rv[j], Lit(0)});
+    const Mask z = eq_mask(hz);
+    const Limb t = fresh();
+    if (tb == 31) E.valu("v_ashrrev_i32_e32 " + VL(t) + ", 31, " + VL(rv[La - 1]));
+    else E.valu("v_bfe_i32 " + VL(t) + ", " + VL(rv[La - 1]) + ", " + std::to_string(tb) + ", 1");
+    E.valu("v_not_b32_e32 " + VL(t) + ", " + VL(t));  // ~0 when x >= 0, else 0
+    Limb lo = rv[0], tmp;
+    if (lo.lit() && !inl(lo.v)) {
+      tmp = vreg(lo);
+      lo = tmp;
+    }
+    const Limb yv = fresh();
+    if (z.k == 2) {
+      E.valu("v_cndmask_b32_e64 " + VL(yv) + ", " + VL(t) + ", " + src(lo) + ", " + SP(z.s), {z.s, z.s + 1});
+    } else {
+      E.valu("v_mov_b32_e32 " + VL(yv) + ", " + (z.ones ? src(lo) : VL(t)));
+    }
+    E.srelease(z);
+    drop(t);
+    drop(tmp);
+    E.retain(yv);
+    hcache[key] = yv;
+    h_last[key] = ++tick;
+    for (uint32_t j = 0; j < La; j++)
+      if (rv[j].reg() && (int)rv[j].v >= E.vfirst) hby.insert({rv[j].g, key});
+    return yv;
+  }
   // x <s y where one side is a literal K whose limbs above k are its sign extension (LASER's signed
   // bounds: 0 <s x, x <s 29, x <s -1): with neg = the register side's sign and hi = its limbs above k
   // equal K's, x <s K = neg | (hi & x_lo <u K_lo) for K >= 0, neg & (~hi | x_lo <u K_lo) for K < 0,
@@ -1549,6 +1610,26 @@ struct Gen {
         regs += rv[j].reg();
       }
       if (regs < 2 || !rv[La - 1].reg()) continue;
+      // a value compared with many nonnegative literals below 2^32 - 1 (LASER's calldata reads: byte i
+      // is ITE(i <s size, ..., 0) for every i): its 32-bit clamp y = (x < 2^32 ? x : x < 0 ? 0 : ~0)
+      // once (cached), then K <s x = K <u y and x <s K = ~(K - 1 <u y), one compare each
+      if (!kneg && k <= 0 && slt_many && !no_slt_clamp()) {
+        const uint32_t K = kv[0].v;
+        if (side == 1 ? K != 0xFFFFFFFFu : K != 0) {
+          const Limb yc = clamp32(rv, La, tb);
+          if (yc.reg()) {
+            const Mask m = lt_mask({Lit(side == 1 ? K : K - 1)}, {yc}, 32, false);
+            drop(yc);
+            if (side == 1) {
+              out = m;
+            } else {
+              out = mnot(m);
+              E.srelease(m);
+            }
+            return true;
+          }
+        }
+      }
       // the register side's sign: its top limb >= 2^tb
       Mask neg;
       if (tb == 31) {  // 0 >s top limb
@@ -3955,6 +4036,7 @@ struct Gen {
           set_mask(d, lt);
           break;
         }
+        slt_many = sgn && ((in.a < slt_lits.size() && slt_lits[in.a] >= 3) || (in.b < slt_lits.size() && slt_lits[in.b] >= 3));
         if (in.op == K_ULT || in.op == K_SLT) {
           set_mask(d, lt_mask(limbs(in.a, La), limbs(in.b, La), in.p1, sgn));
         } else {

@@ -303,6 +303,24 @@ def test_asm_signed_literal_compares_and_views_sim(sim):
                 pe = P.to_bytes()
                 P.set_watch(prev)
                 recs.append(record(1 + (k & 1), pe, None, rng.getrandbits(32), 0, 64 * 3 + 5))
+    # one value against many literals (the 32-bit clamp path): a sum of random weights over the compares
+    # that hold, its low bits tested, so a single wrong compare changes the verdict more often than not
+    for w in (40, 64, 96, 256):
+        n8, n32 = T.BitVecVar(f"m8_{w}", 8), T.BitVecVar(f"m32_{w}", 32)
+        for x in (T.BitVecVar(f"mx{w}", w), T.sign_extend(w - 8, n8), T.sign_extend(w - 32, n32),
+                  T.zero_extend(w - 32, n32)):
+            cs = []
+            for k in (0, 1, 2, 3, 5, 29, 127, 128, 255, 1 << 31, 0xFFFFFFFE, 0xFFFFFFFF, 1 << 32, 1 << 38):
+                K = T.BitVecVal(k % (1 << w), w)
+                cs += [T.bvcmp("bvslt", K, x), T.bvcmp("bvslt", x, K), T.bvcmp("bvsle", x, K), T.bvcmp("bvsge", x, K)]
+            acc = T.BitVecVal(0, 32)
+            for c in cs:
+                acc = T.bvbin("bvadd", acc, T.ite(c, T.BitVecVal(rng.getrandbits(32), 32), T.BitVecVal(0, 32)))
+            P, blob = search.prepare([T.eq(T.extract(2, 0, acc), T.BitVecVal(rng.randrange(8), 3))])
+            recs.append(record(0, P.to_bytes(), blob, rng.getrandbits(32), rng.getrandbits(63), 128))
+            P.set_watch([])
+            for kind in (1, 2):
+                recs.append(record(kind, P.to_bytes(), None, rng.getrandbits(32), 0, 64 * 4 + 9))
     # byte chains: a word built from 32 bytes, read through by extracts and a wider concat
     bs = [T.BitVecVar(f"cb{i}", 8) for i in range(32)]
     word = bs[0]
