@@ -207,18 +207,21 @@ class Emitter {
     lds_pending.clear();
   }
   std::function<bool()> on_pressure;  // drop cached values (value numbering); true if any went
+  std::function<bool()> on_hard;      // all 256 taken and no cache entry left: spill a value (eval)
   // The value caches may not raise the kernel's VGPR count past the occupancy step the kernel
   // reaches without them (jit_asm_source): an allocation at or above vsoft first drops the caches.
   // (C4: the literal cache alone took the search kernel from 98 to 134 VGPRs, 4 to 3 waves per SIMD.)
   int vsoft = 256;
+  int vhard = 256;  // the register file's end (MYTHGPU_JIT_ASM_SPILL_TEST lowers it to exercise spills)
   uint32_t valloc() {
     for (;;) {
       int r = vfirst;
-      while (r < 256 && vref[r]) r++;
+      while (r < vhard && vref[r]) r++;
       // cache entries go one at a time (least recently used first) until a register below the limit
       // is free or the caches are empty
       if ((r >= 256 || r >= vsoft) && on_pressure && on_pressure()) continue;
-      if (r >= 256) fail("out of VGPRs");
+      if (r >= vhard && on_hard && on_hard()) continue;
+      if (r >= vhard) fail("out of VGPRs");
       if (lds_pending.count(r)) lds_flush();  // a register whose load is still in flight
       vref[r] = 1;
       vgen[r] = ++gen_ctr;
@@ -230,9 +233,10 @@ class Emitter {
   uint32_t valloc2() {
     for (;;) {
       int r = (vfirst + 1) & ~1;
-      while (r + 1 < 256 && (vref[r] || vref[r + 1])) r += 2;
+      while (r + 1 < vhard && (vref[r] || vref[r + 1])) r += 2;
       if ((r + 1 >= 256 || r + 1 >= vsoft) && on_pressure && on_pressure()) continue;
-      if (r + 1 >= 256) fail("out of VGPRs");
+      if (r + 1 >= vhard && on_hard && on_hard()) continue;
+      if (r + 1 >= vhard) fail("out of VGPRs");
       if (lds_pending.count(r) || lds_pending.count(r + 1)) lds_flush();
       for (int q = 0; q < 2; q++) {
         vref[r + q] = 1;
@@ -386,7 +390,7 @@ struct Gen {
         opl.pop_back();
       }
     };
-    if (eval_kernel && !no_greedy()) {
+    if (eval_kernel && greedy_on()) {
       greedy_roots(v, operands, done, visit);
     } else {
       for (size_t k = 0; k < v.size(); k++)
@@ -396,10 +400,13 @@ struct Gen {
       if (!done[k]) visit((int32_t)k);
     code.swap(out);
   }
-  // MYTHGPU_JIT_ASM_NO_GREEDY=1: the eval kernel's constraints in program order
-  static bool no_greedy() {
+  // MYTHGPU_JIT_ASM_GREEDY=1: the eval kernel's constraints in greedy order (below).  Opt-in: it lowers
+  // C4's cache-free peak (238 -> 208 VGPRs) but the kernel's time did not move (the caches fill the
+  // occupancy step either way; profiles/r05i_eval_glds.jsonl), and with the model watch rows as roots
+  // it ran C4's read-back kernel out of registers
+  static bool greedy_on() {
     static const bool on = [] {
-      const char* g = getenv("MYTHGPU_JIT_ASM_NO_GREEDY");
+      const char* g = getenv("MYTHGPU_JIT_ASM_GREEDY");
       return g && g[0] == '1';
     }();
     return on;
@@ -963,6 +970,7 @@ struct Gen {
   // limb j of value id (Bools through their limb form)
   Limb limb(uint32_t id, uint32_t j) {
     if (P.vwidth[id] == 1 && j == 0) return limb_of_bool(id);
+    if (is_spilled(id)) reload(id);
     const Val& x = val[id];
     if (j >= x.l.size()) return Lit(0);
     return x.l[j];
@@ -1399,6 +1407,7 @@ struct Gen {
   // conditions), and a repeat then costs one compare
   std::map<std::pair<uint32_t, uint32_t>, Limb> eqdiff;  // each entry holds one reference
   Mask eq_ids(uint32_t a, uint32_t b, uint32_t Lk) {
+    PinScope pin_(*this, {a, b});
     const auto key = std::minmax(a, b);
     auto it = eqdiff.find(key);
     if (it != eqdiff.end()) {
@@ -2647,8 +2656,103 @@ struct Gen {
     x.w = 1;
     x.def = true;
   }
+  // ---- spills (eval kernels that do not fit 256 VGPRs otherwise) -----------------------------
+  // A model read-back with many array reads at distinct symbolic keys (VMTests' calldata bytes: 32
+  // canonicalising LOOKUPs, each comparing its key with every earlier one) keeps every key live to
+  // the last lookup — 8 limbs each.  When the 256 VGPRs are taken and no cache entry is left, a live
+  // value (width > 32, every register limb held by it alone, not read by the instruction being
+  // emitted nor pinned by a key test in progress; the one whose last reader comes latest) goes to
+  // LDS (ds_write per limb, the wave's slots at s35) and comes back on its next read (ds_read).
+  // Spills happen outside branches only; a read of a spilled value under a branch fails the
+  // kernel (the O3 kernel then).  Off unless the kernel fails without (jit_asm_source).
+  bool spill_on = false;
+  int vhard = 256;
+  std::vector<std::vector<int>> spill_at;  // value id -> LDS slot of each register limb (-1 none); empty: resident
+  std::vector<uint8_t> slot_busy;
+  uint32_t spill_hwm = 0;
+  Limb spill_v;                            // s35 + 4 * lane
+  std::vector<uint32_t> pinned;            // the instruction's operands, and values pinned by PinScope
+  struct PinScope {
+    Gen& g;
+    size_t n;
+    PinScope(Gen& g_, std::initializer_list<uint32_t> ids) : g(g_), n(ids.size()) {
+      for (uint32_t id : ids) g.pinned.push_back(id);
+    }
+    ~PinScope() { g.pinned.resize(g.pinned.size() - n); }
+  };
+  bool is_spilled(uint32_t id) const { return id < spill_at.size() && !spill_at[id].empty(); }
+  bool spill_one() {
+    if (!spill_on || cond) return false;
+    int best = -1;
+    int32_t bl = -1;
+    for (uint32_t id = 0; id < val.size(); id++) {
+      const Val& x = val[id];
+      if (!x.def || is_spilled(id) || is_view(id) || P.vwidth[id] <= 32) continue;
+      if (std::find(pinned.begin(), pinned.end(), id) != pinned.end()) continue;
+      int regs = 0;
+      bool own = true;
+      for (const Limb& l : x.l)
+        if (l.reg()) {
+          regs++;
+          own = own && (int)l.v >= E.vfirst && E.vref[l.v] == 1;
+        }
+      if (regs < 2 || !own) continue;
+      const int32_t lu = id < last.size() ? last[id] : -1;
+      if (lu > bl) {
+        bl = lu;
+        best = (int)id;
+      }
+    }
+    if (best < 0) return false;
+    Val& x = val[best];
+    std::vector<int> at(x.l.size(), -1);
+    for (size_t j = 0; j < x.l.size(); j++) {
+      if (!x.l[j].reg()) continue;
+      uint32_t sl = 0;
+      while (sl < slot_busy.size() && slot_busy[sl]) sl++;
+      if (sl >= 255) fail("out of VGPRs (spill slots)");
+      if (sl == slot_busy.size()) slot_busy.push_back(0);
+      slot_busy[sl] = 1;
+      spill_hwm = std::max(spill_hwm, sl + 1);
+      E.mem("ds_write_b32 " + VL(spill_v) + ", " + VL(x.l[j]) + " offset:" + std::to_string(sl * 256u));
+      at[j] = (int)sl;
+    }
+    E.ctl("s_waitcnt lgkmcnt(0)");  // the stores have read their registers
+    for (size_t j = 0; j < x.l.size(); j++)
+      if (at[j] >= 0) {
+        drop(x.l[j]);
+        x.l[j] = Limb{};
+      }
+    spill_at[best] = at;
+    spills++;
+    return true;
+  }
+  uint32_t spills = 0;
+  void reload(uint32_t id) {
+    if (cond) fail("a spilled value read under a branch");
+    if (std::find(pinned.begin(), pinned.end(), id) == pinned.end())
+      fail("internal: a spilled value read where it is not pinned");
+    Val& x = val[id];
+    const std::vector<int> at = spill_at[id];
+    spill_at[id].clear();  // (pinned: not a victim of the allocations below)
+    for (size_t j = 0; j < at.size(); j++) {
+      if (at[j] < 0) continue;
+      const Limb d = fresh();
+      E.mem("ds_read_b32 " + VL(d) + ", " + VL(spill_v) + " offset:" + std::to_string((uint32_t)at[j] * 256u));
+      x.l[j] = d;
+    }
+    E.ctl("s_waitcnt lgkmcnt(0)");
+    for (int sl : at)
+      if (sl >= 0) slot_busy[sl] = 0;
+  }
+
   void kill(uint32_t id) {
     Val& x = val[id];
+    if (is_spilled(id)) {
+      for (int sl : spill_at[id])
+        if (sl >= 0) slot_busy[sl] = 0;
+      spill_at[id].clear();
+    }
     for (auto& l : x.l) drop(l);
     x.l.clear();
     E.srelease(x.m);
@@ -3957,6 +4061,7 @@ struct Gen {
           E.sretain(val[in.a].m);
           val[d].m = val[in.a].m;
         }
+        if (is_spilled(in.a)) reload(in.a);
         std::vector<Limb> r = val[in.a].l;
         for (auto& x : r) E.retain(x);
         set(d, r);
@@ -4350,6 +4455,35 @@ struct Gen {
     static const bool on = getenv("MYTHGPU_JIT_ASM_DEBUG") != nullptr;
     return on;
   }
+  // the values instruction `in` reads directly (a LOOKUP's prior keys excepted: each is pinned by its
+  // key test only) and through the views it reads
+  void operands_of(const Instr& in, size_t k, std::vector<uint32_t>& out) {
+    std::function<void(uint32_t)> add = [&](uint32_t id) {
+      if (id == MG_NONE || id >= val.size()) return;
+      out.push_back(id);
+      if (is_view(id)) {
+        const Instr& vi = code[def[id]];
+        add(vi.a);
+        if (vi.op == K_CONCAT) add(vi.b);
+      }
+    };
+    switch (in.op) {
+      case K_CONST: break;
+      case K_COORD: if (copysrc[k] != MG_NONE) add(copysrc[k]); break;
+      case K_LOOKUP:
+        add(in.a);
+        add(in.p0);
+        for (uint32_t q = 0; q < in.c; q++) add(P.vaux[in.p1 + 2 * q + 1]);
+        break;
+      default:
+        add(in.a);
+        if (in.op != K_NOT && in.op != K_NEG && in.op != K_EXTRACT && in.op != K_ZEXT && in.op != K_SEXT &&
+            in.op != K_ASSERT && in.op != K_COPY && in.op != K_WATCH)
+          add(in.b);
+        if (in.op == K_ITE) add(in.c);
+        break;
+    }
+  }
   void body(const std::string& next) {
     eqdiff.clear();  // a kernel abandoned midway (AsmFail: out of VGPRs at this depth) left its entries
     xcache.clear();
@@ -4366,6 +4500,10 @@ struct Gen {
       hcache_free(g);
     };
     E.on_pressure = [this]() { return evict_one(); };
+    E.on_hard = [this]() { return spill_one(); };
+    spill_at.assign(val.size(), {});
+    slot_busy.clear();
+    pinned.clear();
     E.on_spressure = [this]() { return spill_mask(); };
     lvn_on = true;
     static const bool annotate = getenv("MYTHGPU_JIT_ASM_ANNOTATE") != nullptr;
@@ -4376,7 +4514,14 @@ struct Gen {
       if (annotate)
         E.o << "  ; vcode " << k << " op " << in.op << " w " << in.wd << " dst " << in.dst << " a " << in.a << " b " << in.b
             << "\n";
+      if (spill_on) {  // the values this instruction reads stay in registers while it is emitted
+        pinned.clear();
+        operands_of(in, k, pinned);
+        for (size_t q = 0; q < pinned.size(); q++)
+          if (is_spilled(pinned[q])) reload(pinned[q]);
+      }
       emit(in, k, next);
+      if (spill_on) pinned.clear();
       if (debug_live()) {
         int used = 0;
         for (int r = E.vfirst; r < 256; r++) used += E.vref[r] > 0;
@@ -4443,6 +4588,7 @@ struct Gen {
     lvn_on = false;
     E.on_free = nullptr;
     E.on_pressure = nullptr;
+    E.on_hard = nullptr;
     E.on_spressure = nullptr;
   }
 
@@ -4685,6 +4831,7 @@ struct Gen {
 
   std::string kernel_eval(const std::string& name) {
     E = Emitter();
+    E.vhard = vhard;
     E.nlab = labels;
     E.vsoft = vsoft;
     census.clear();
@@ -4698,7 +4845,7 @@ struct Gen {
           if (in.dst < need.size() && (need[in.dst] >> j & 1)) rows.push_back(in.p1 + j);
     row_reg.assign(rows.size(), Limb{});
     row_seq.assign(rows.size(), 0);
-    glds = tiled && glds_env() && !rows.empty() && gdepth > 0;
+    glds = tiled && glds_env() && !rows.empty() && gdepth > 0 && !spill_on;
     if (glds) {
       gdepth = std::min<uint32_t>(gdepth, (uint32_t)rows.size());
       gseq.assign(rows.size(), 0);
@@ -4729,6 +4876,13 @@ struct Gen {
     if (!glds)
       for (size_t q = 0; q < std::min<size_t>(prefetch_depth(), rows.size()); q++) ring_reg.push_back(fresh());
     vnext = tiled ? Limb{} : fresh();
+    spill_hwm = 0;
+    spills = 0;
+    if (spill_on) {  // the wave's spill slots: s35 = wave * slots * 256 (patched below), spill_v = s35 + 4 * lane
+      spill_v = fresh();
+      E.salu("s_mul_i32 s35, s3, __MG_SPILL_BYTES__", {35});
+      E.valu("v_lshl_add_u32 " + VL(spill_v) + ", v1, 2, s35", {35});
+    }
     if (glds) {  // the wave's LDS slots: s34 = wave * slots * 256, glds_v = s34 + 4 * lane
       glds_v = fresh();
       E.salu("s_mul_i32 s34, s3, " + hexs(glds_slots() * 256u), {34});
@@ -4794,6 +4948,7 @@ struct Gen {
     for (const Limb& l : ring_reg) drop(l);
     if (!tiled) drop(vnext);
     if (glds) drop(glds_v);
+    if (spill_on) drop(spill_v);
     ring_reg.clear();
     for (int r = E.vfirst; r < 256; r++)
       if (E.vref[r]) fail("internal: VGPR v" + std::to_string(r) + " still held after the body");
@@ -4821,11 +4976,20 @@ struct Gen {
     labels = E.nlab;
     meta_vgpr[name] = nv;
     meta_sgpr[name] = ns + 6;
-    return o.str();
+    std::string res = o.str();
+    if (spill_on) {
+      // the spill slots' wave stride: the ds offsets stay below the LDS-staged rows' slots' end
+      const size_t at = res.find("__MG_SPILL_BYTES__");
+      if (at != std::string::npos) res.replace(at, 18, hexs(spill_hwm * 256u));
+    }
+    return res;
   }
 
-  // the eval kernel's LDS: four waves' row slots (256 B each) when rows are LDS-staged
-  uint32_t eval_lds_bytes() const { return glds ? 4u * glds_slots() * 256u : 0u; }
+  // the eval kernel's LDS: four waves' row slots (256 B each) when rows are LDS-staged, and four
+  // waves' spill slots
+  uint32_t eval_lds_bytes() const {
+    return (glds ? 4u * glds_slots() * 256u : 0u) + (spill_on ? 4u * spill_hwm * 256u : 0u);
+  }
 
   int labels = 0;  // label numbers continue across the kernels of one module
   std::string kernel(const std::string& name) {
@@ -5141,7 +5305,9 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
     Gen g(P, specs, gconsts);
     std::ostringstream o;
     o << kAsmMarker << "\n  .amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"\n  .amdhsa_code_object_version 6\n";
-    if (kernels & JIT_EVAL) {  // the eval kernel alone (no generator)
+    if (kernels & JIT_EVAL) try {  // the eval kernel alone (no generator)
+      // MYTHGPU_JIT_ASM_SPILL_TEST=N (tests): straight to the spilling kernel with only N VGPRs
+      if (const char* st = getenv("MYTHGPU_JIT_ASM_SPILL_TEST")) throw AsmFail{"out of VGPRs (spill test " + std::string(st) + ")"};
       g.eval_kernel = true;
       g.tiled = (kernels & JIT_EVAL_TILED) || getenv("MYTHGPU_JIT_ASM_TILED");
       g.analyse();
@@ -5234,6 +5400,26 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
         }
       }
       o << ks << metadata_eval(g.meta_vgpr["mgj_eval"], g.meta_sgpr["mgj_eval"], g.eval_lds_bytes());
+      out = o.str();
+      return MG_OK;
+    } catch (const AsmFail& f) {
+      // out of VGPRs at every queue depth: once more with spills to LDS (Gen::spill_one), a depth-8
+      // register queue and the caches bounded by all 256 registers.  MYTHGPU_JIT_ASM_NO_SPILL=1: refuse
+      const char* ns = getenv("MYTHGPU_JIT_ASM_NO_SPILL");
+      if ((ns && ns[0] == '1') || f.why.find("out of VGPRs") == std::string::npos) throw;
+      Gen g2(P, specs, gconsts);
+      g2.eval_kernel = true;
+      g2.tiled = (kernels & JIT_EVAL_TILED) || getenv("MYTHGPU_JIT_ASM_TILED");
+      g2.analyse();
+      g2.spill_on = true;
+      g2.depth = 8;
+      g2.gdepth = 0;
+      g2.caches = true;
+      g2.vsoft = 256;
+      if (const char* st = getenv("MYTHGPU_JIT_ASM_SPILL_TEST")) g2.vhard = g2.vsoft = std::max(24, std::min(256, atoi(st)));
+      g2.labels = 0;
+      const std::string ks = g2.kernel_eval("mgj_eval");
+      o << ks << metadata_eval(g2.meta_vgpr["mgj_eval"], g2.meta_sgpr["mgj_eval"], g2.eval_lds_bytes());
       out = o.str();
       return MG_OK;
     }

@@ -343,6 +343,49 @@ def test_asm_signed_literal_compares_and_views_sim(sim):
     print("signed literal compares / views:", summary)
 
 
+def test_asm_eval_spills_sim(sim, monkeypatch):
+    """Eval kernels that spill values to LDS (Gen::spill_one / reload): random tier programs, the
+    workloads and a many-key array read (canonicalising LOOKUPs over 64-bit keys, so keys collide)
+    under an artificial 72-register file (MYTHGPU_JIT_ASM_SPILL_TEST), verdicts against the C port
+    with the simulator's LDS, wait-count and lifetime checks; a kernel the spiller cannot fit is
+    refused (the O3 kernel then), never wrong."""
+    from mythril_amd import native, search, workloads
+    from mythril_amd.smt import terms as T
+    from tests.helpers import random_tier_program
+
+    progs = []
+    for s_ in range(80):
+        P, _ = search.prepare(random_tier_program(30_000 + s_, full=bool(s_ & 1)))
+        P.set_watch([])
+        progs.append((P.to_bytes(), 1 + (s_ & 1)))
+    for name in ("walletlibrary_kill", "token_transfer_underflow", "etherstore_reentrancy"):
+        P, _ = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
+        P.set_watch([])
+        progs += [(P.to_bytes(), 1), (P.to_bytes(), 2)]
+    arr = T.ArrayVar("Cd", 64, 8)
+    keys = [T.BitVecVar(f"k{i}", 64) for i in range(48)]
+    acc = T.BitVecVal(0, 32)
+    rng = random.Random(3)
+    for k in keys:
+        acc = T.bvbin("bvadd", acc, T.bvbin("bvmul", T.zero_extend(24, T.select(arr, k)), T.BitVecVal(rng.getrandbits(32), 32)))
+    P, _ = search.prepare([T.eq(T.extract(2, 0, acc), T.BitVecVal(5, 3))])
+    P.set_watch([])
+    progs += [(P.to_bytes(), 1), (P.to_bytes(), 2)]
+    monkeypatch.setenv("MYTHGPU_JIT_ASM_SPILL_TEST", "72")
+    spilled = 0
+    for pb, kind in progs:
+        try:
+            spilled += native.jit_asm(pb, None, tiled=kind == 2).count("ds_write_b32") > 0
+        except native.EngineUnsupported:
+            pass
+    recs = [record(kind, pb, None, rng.getrandbits(32), 0, 64 * rng.randint(1, 3) + rng.randrange(64)) for pb, kind in progs]
+    rc, summary, bad, err = run_sim(sim, b"".join(recs), {"MYTHGPU_JIT_ASM_CHECK": "1", "MYTHGPU_JIT_ASM_SPILL_TEST": "72"})
+    assert rc == 0 and summary, err[-3000:]
+    assert summary["mismatch"] == "0" and summary["simerror"] == "0" and summary["asmerror"] == "0", (summary, bad[:5])
+    assert int(summary["ok"]) >= len(recs) // 2 and spilled >= 5, (summary, spilled)
+    print("spills:", summary, "kernels with spills:", spilled)
+
+
 def _full_worker(args):
     exe, lo, hi, cfg, kind = args
     recs = _fuzz_records(lo, hi, full=True) if kind == "laser" else _tier_records(lo, hi, full=True)
