@@ -671,6 +671,10 @@ struct Gen {
   // word's low limb and aliases the rest, where materialising every link re-aligned every limb at
   // every link (C4's eval program: 1,565 VALU per candidate in CONCATs).  The view's operands live
   // until its reader (last[] extended).  MYTHGPU_JIT_ASM_NO_VIEWS=1 materialises every value.
+  // K_MUL by operand pair (unordered) and width -> its vcode index: an UMUL_NOOVF of the same pair
+  // before it computes the low limbs of the same product (mulshare)
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t>, size_t> mul_at;
+  std::map<std::pair<uint32_t, uint32_t>, std::vector<Limb>> mulshare;  // owned limbs, until the MUL
   std::vector<uint8_t> view;  // value id -> a view
   std::vector<uint32_t> slt_lits;  // value id -> signed compares of it against a literal
   bool slt_many = false;           // the compare being emitted reads such a value 3+ times
@@ -678,6 +682,12 @@ struct Gen {
     const size_t nv = P.vwidth.size();
     view.assign(nv, 0);
     slt_lits.assign(nv, 0);
+    mul_at.clear();
+    for (size_t k = 0; k < code.size(); k++) {
+      const Instr& in = code[k];
+      if (in.op == K_MUL && !mul_at.count({std::min(in.a, in.b), std::max(in.a, in.b), in.wd}))
+        mul_at[{std::min(in.a, in.b), std::max(in.a, in.b), in.wd}] = k;
+    }
     for (const Instr& in : code) {
       if (in.op != K_SLT && in.op != K_SLE) continue;
       const Instr* da = def_of(in.a);
@@ -1536,6 +1546,13 @@ struct Gen {
   static bool no_signed_lit() {
     static const bool on = [] {
       const char* g = getenv("MYTHGPU_JIT_ASM_NO_SIGNED_LIT");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
+  static bool no_mulshare() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_MULSHARE");
       return g && g[0] == '1';
     }();
     return on;
@@ -3756,6 +3773,16 @@ struct Gen {
         break;
       }
       case K_MUL: {
+        {
+          auto ms = mulshare.find({std::min(in.a, in.b), std::max(in.a, in.b)});
+          if (ms != mulshare.end() && ms->second.size() == Ld) {  // an UMUL_NOOVF's product
+            std::vector<Limb> r = ms->second;
+            mulshare.erase(ms);
+            mask_top(r, W);
+            set(d, r);
+            break;
+          }
+        }
         const uint32_t n = std::min(Ld, demanded(d));
         std::vector<Limb> a = limbs(in.a, n), b = limbs(in.b, n), acc(n, Lit(0));  // acc owns
         for (uint32_t i = 0; i < n; i++) {
@@ -3805,8 +3832,13 @@ struct Gen {
       }
       case K_UMUL_NOOVF: {
         // the full 2La-limb product (schoolbook; zero literal limbs skipped: LASER's overflow checks
-        // multiply a small count by a word), then "no bit at or above wa" as one zero test
+        // multiply a small count by a word), then "no bit at or above wa" as one zero test.  A MUL of
+        // the same operands later in the program (batchOverflow: require(cnt * value / cnt == value)
+        // next to amount = cnt * value) takes the product's low limbs from here (mulshare)
         const uint32_t wa = in.p1, La = Lw(wa), n = 2 * La;
+        const auto mk = std::make_tuple(std::min(in.a, in.b), std::max(in.a, in.b), wa);
+        auto mi = mul_at.find(mk);
+        const bool share = !cond && !no_mulshare() && mi != mul_at.end() && mi->second > k;
         std::vector<Limb> a = limbs(in.a, La), b = limbs(in.b, La), acc(n, Lit(0));  // acc owns
         for (uint32_t i = 0; i < La; i++) {
           if (a[i].lit() && a[i].v == 0) continue;
@@ -3831,7 +3863,7 @@ struct Gen {
             }
             // the product's limb 0 is the low half of a0 * b0 alone: it carries nothing into the limbs
             // the test reads (at or above wa >= 32), so it is not computed
-            const bool lo_dead = i + j == 0 && wa >= 32;
+            const bool lo_dead = i + j == 0 && wa >= 32 && !share;
             Limb dl = Lit(0), dh;
             product(vx, so, via_s41, !lo_dead, true, dl, dh);
             lo[i + j] = dl;
@@ -3863,7 +3895,15 @@ struct Gen {
         }
         set_mask(d, eq_mask(prs));
         for (auto& t : tmp) drop(t);
-        for (auto& t : acc) drop(t);
+        if (share) {
+          std::vector<Limb> low(acc.begin(), acc.begin() + La);  // the references move to mulshare
+          for (uint32_t q = La; q < n; q++) drop(acc[q]);
+          auto& slot = mulshare[{std::min(in.a, in.b), std::max(in.a, in.b)}];
+          for (auto& t : slot) drop(t);
+          slot = low;
+        } else {
+          for (auto& t : acc) drop(t);
+        }
         break;
       }
       case K_SHL: case K_LSHR: case K_ASHR: {
@@ -4486,6 +4526,7 @@ struct Gen {
   }
   void body(const std::string& next) {
     eqdiff.clear();  // a kernel abandoned midway (AsmFail: out of VGPRs at this depth) left its entries
+    mulshare.clear();
     xcache.clear();
     xby.clear();
     hcache.clear();
@@ -4581,6 +4622,9 @@ struct Gen {
           break;
       }
     }
+    for (auto& kv : mulshare)
+      for (auto& t : kv.second) drop(t);
+    mulshare.clear();
     for (auto& kv : eqdiff) drop(kv.second);  // values live to the end of the body
     eqdiff.clear();
     xcache_clear();

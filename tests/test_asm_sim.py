@@ -321,6 +321,20 @@ def test_asm_signed_literal_compares_and_views_sim(sim):
             P.set_watch([])
             for kind in (1, 2):
                 recs.append(record(kind, P.to_bytes(), None, rng.getrandbits(32), 0, 64 * 4 + 9))
+    # an overflow check and the product it guards (batchOverflow): the MUL takes the UMUL_NOOVF's limbs
+    for w in (64, 96, 256):
+        for nb in (8, 32, w):
+            cnt = T.zero_extend(w - nb, T.BitVecVar(f"c{w}_{nb}", nb)) if nb < w else T.BitVecVar(f"c{w}", w)
+            val = T.BitVecVar(f"v{w}_{nb}", w)
+            prod = T.bvbin("bvmul", cnt, val)
+            for lo in (0, 3, w - 9):
+                roots = [T.or_(T.not_(T.bvcmp("bvumul_noovfl", cnt, val)),
+                               T.eq(T.extract(lo + 7, lo, prod), T.BitVecVal(rng.getrandbits(8), 8)),
+                               T.bvcmp("bvult", prod, T.BitVecVal(rng.getrandbits(w - 2), w)))]
+                P, blob = search.prepare(roots)
+                recs.append(record(0, P.to_bytes(), blob, rng.getrandbits(32), rng.getrandbits(63), 128))
+                P.set_watch([])
+                recs.append(record(1 + (lo & 1), P.to_bytes(), None, rng.getrandbits(32), 0, 64 * 2 + 9))
     # byte chains: a word built from 32 bytes, read through by extracts and a wider concat
     bs = [T.BitVecVar(f"cb{i}", 8) for i in range(32)]
     word = bs[0]
