@@ -4731,14 +4731,21 @@ struct Gen {
   }
   // the load of SoA row `row` of the group whose block base is s[b:b+1] (tiled) or of the candidates
   // at offsets `voff` (row-major: s[4:5] + row * n * 4)
+  // the 4-KiB page base of the last row loaded from each block (this group's in s[36:37], the next
+  // group's in s[18:19]; -1: none): a row in the same page needs no address arithmetic
+  int64_t page_at[2] = {-1, -1};
   void load_row(const Limb& d, uint32_t row, int b, const std::string& voff, const std::string& note) {
     if (tiled) {
       const uint64_t byte = (uint64_t)row * 256u, hi = byte & ~4095ull;
       std::string base = "s[" + std::to_string(b) + ":" + std::to_string(b + 1) + "]";
       if (hi) {
-        E.salu("s_add_u32 s40, " + S(b) + ", " + hexs((uint32_t)hi), {40});
-        E.salu("s_addc_u32 s41, " + S(b + 1) + ", 0", {41});
-        base = "s[40:41]";
+        const int w = b == 26 ? 0 : 1, pr = w ? 18 : 36;
+        if (page_at[w] != (int64_t)hi) {
+          E.salu("s_add_u32 " + S(pr) + ", " + S(b) + ", " + hexs((uint32_t)hi), {pr});
+          E.salu("s_addc_u32 " + S(pr + 1) + ", " + S(b + 1) + ", 0", {pr + 1});
+          page_at[w] = (int64_t)hi;
+        }
+        base = "s[" + std::to_string(pr) + ":" + std::to_string(pr + 1) + "]";
       }
       E.mem("global_load_dword " + VL(d) + ", v2, " + base + " offset:" + std::to_string(byte & 4095u) +
             "  ; soa row " + std::to_string(row) + note);
@@ -4779,10 +4786,14 @@ struct Gen {
   long lgkm_n = 0;
   std::vector<long> gseq, lseq;  // VMEM / LGKM issue index of each row's glds / ds_read
   std::vector<Limb> stage_reg;
+  // MYTHGPU_JIT_ASM_GLDS: 1 = the LDS queue where it is deeper than the register queue, N > 1 = the LDS
+  // queue at depth N; unset / 0 = the register queue.  Opt-in: measured within +-3 % of the register
+  // queue on C2 and C4 (profiles/r05i_eval_glds.jsonl) at ~2x its SALU and waits per row (M0, the
+  // address pair, a vmcnt and an lgkmcnt wait), and the kernel is issue-bound
   static bool glds_env() {
     static const bool on = [] {
       const char* g = getenv("MYTHGPU_JIT_ASM_GLDS");
-      return !(g && g[0] == '0');
+      return g && g[0] && g[0] != '0';
     }();
     return on;
   }
@@ -4945,6 +4956,7 @@ struct Gen {
       E.valu("v_lshlrev_b32_e32 v2, 2, v1");  // lane * 4 inside the group's 256-byte row
       E.salu("s_lshr_b32 s30, s16, 6", {30});
       block_base(26, 30);
+      page_at[0] = page_at[1] = -1;
     } else {
       E.valu("v_min_u32_e32 v2, s23, v3", {23});
       E.valu("v_lshlrev_b32_e32 v2, 2, v2");
@@ -4966,6 +4978,7 @@ struct Gen {
       E.salu("s_add_u32 s33, s30, s32", {33});
       E.salu("s_min_u32 s33, s33, s31", {33});
       block_base(28, 33);
+      page_at[0] = page_at[1] = -1;
     } else {
       E.valu("v_min_u32_e32 v2, s23, v3", {23});
       E.valu("v_lshlrev_b32_e32 v2, 2, v2");

@@ -1,6 +1,6 @@
 # round 5, run N: the GPU suite's JIT and first-tier files (spills to LDS, -O0 read-back fallbacks,
-# UMUL_NOOVF/MUL product sharing), the VMTests replay per phase on the default tier, then blocks per CU
-# for the first tier's search kernels against O3 (C3, C1, C4 at 2^28)
+# UMUL_NOOVF/MUL product sharing, row page bases cached), blocks per CU for the first tier's search
+# kernels against O3 (C3, C1, C4 at 2^28), the eval kernels' queue modes, the VMTests replay per phase
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_jit.py tests/test_gpu_asm.py -m gpu -x -q --durations=6 --timeout 300 --timeout-method thread > gpurun_out/r5n_pytest.log 2>&1 || { tail -40 gpurun_out/r5n_pytest.log; exit 1; }
@@ -21,5 +21,7 @@ for w in suicide_kill walletlibrary_kill; do
   for b in 32 64 128; do rate $w asm 268435456 bpc$b MYTHGPU_JIT_BPC=$b || exit 1; done
 done
 cat gpurun_out/r5n_rates.jsonl
+timeout -k 10 600 python tools/eval_glds_sweep.py > gpurun_out/r5n_eval.jsonl 2> gpurun_out/r5n_eval.err || { tail -20 gpurun_out/r5n_eval.err; exit 1; }
+cat gpurun_out/r5n_eval.jsonl
 MYTHGPU_JIT_TIMING=1 timeout -k 10 300 python tools/vmtests_timing.py 400 > gpurun_out/r5n_vmt.json 2> gpurun_out/r5n_vmt.err || { tail -5 gpurun_out/r5n_vmt.err; exit 0; }
 cat gpurun_out/r5n_vmt.json
