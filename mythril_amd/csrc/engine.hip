@@ -2711,11 +2711,11 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
       // the first tier: assembly straight from the specialised program (jit_asm.cpp)
       asm_rc = jit_asm_source(t->low, t->specs, t->consts, kernels, src, asm_err);
       if (asm_rc != MG_OK && t->asm_fallback) {  // chosen by default: the O3 kernel instead
-        // (a read-back kernel evaluates a few candidates: compiled without optimisation — LLVM took
-        // 20-70 s at -O3 on VMTests' many-lookup read-back kernels, 5x less at -O0)
+        // (not at -O0: LLVM's -O0 kernel for a VMTests read-back kept 52 KB of stack per lane in a
+        // dynamic stack and faulted on the GPU; -O1 compiled no faster than -O3)
         t->flags &= ~MG_JIT_ASM;
         asm_rc = MG_OK;
-        src = std::string(kJitOptO0) + jit_source(t->low, nullptr, nullptr, kernels);
+        src = jit_source(t->low, nullptr, nullptr, kernels);
       }
     } else {
       src = t->has_gen ? jit_source(t->low, &t->specs, &t->consts, kernels) : jit_source(t->low, nullptr, nullptr, kernels);

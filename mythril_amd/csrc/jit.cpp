@@ -1422,7 +1422,7 @@ std::string opt_level() { return std::string("-O") + (getenv("MYTHGPU_JIT_OPT") 
 int comgr_compile(const std::string& src, std::vector<char>& code, std::string& log) {
   Comgr& c = comgr();
   const std::string full = std::string(kComgrShim) + src;
-  const std::string optlvl = src.compare(0, std::strlen(kJitOptO0), kJitOptO0) == 0 ? std::string("-O0") : opt_level();
+  const std::string optlvl = opt_level();
   std::vector<const char*> opts = {optlvl.c_str(), "-std=c++17", "-nogpuinc", "-nogpulib", "-Wno-unused-variable",
                                    "-Wno-uninitialized", "-Wno-sometimes-uninitialized"};
   for (const auto& t : extra_options()) opts.push_back(t.c_str());

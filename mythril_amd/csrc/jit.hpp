@@ -11,8 +11,6 @@ namespace mg {
 // (per-candidate verdicts of generated candidates) and mgj_eval (SoA inputs).
 // `specs`/`gconsts` (nullable) specialise the generator at codegen time.
 enum : uint32_t { JIT_SEARCH = 1, JIT_EVAL = 2, JIT_GEN = 4, JIT_EVAL_TILED = 8 };
-// a first line that compiles the O3 tier's source at -O0 (read-back kernels the first tier refused)
-constexpr const char* kJitOptO0 = "// mythgpu: -O0\n";
 std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
                        uint32_t kernels);
 
