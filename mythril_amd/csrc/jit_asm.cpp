@@ -775,9 +775,31 @@ struct Gen {
     }
   }
 
-  // prologue: every lane of the block copies words of the planned tables, then a barrier
+  // prologue: every lane of the block copies words of the planned tables, then a barrier.  The loads
+  // of up to stage_batch() (table, word) steps go out before one wait and their stores (a wait per step had
+  // serialised one memory latency per table and step in every block's start-up: C3's first tier ran
+  // 283 G/s at 64 blocks per CU and 424 at 32, profiles/r05p_rates_c3_bpc.jsonl)
+  // MYTHGPU_JIT_ASM_STAGE_BATCH: steps per wait (default 1 until measured on the box; 16 batched)
+  static size_t stage_batch() {
+    static const size_t n = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_STAGE_BATCH");
+      return g ? (size_t)std::max(1, std::min(32, atoi(g))) : (size_t)1;
+    }();
+    return n;
+  }
   void emit_lds_prologue() {
     if (!lds_words) return;
+    std::vector<std::pair<Limb, Limb>> pend;  // (loaded word, LDS address)
+    auto flush = [&]() {
+      if (pend.empty()) return;
+      E.ctl("s_waitcnt vmcnt(0)");
+      for (auto& pr : pend) {
+        E.mem("ds_write_b32 " + VL(pr.second) + ", " + VL(pr.first));
+        drop(pr.first);
+        drop(pr.second);
+      }
+      pend.clear();
+    };
     for (const auto& kv : lds_base) {
       const uint32_t off = kv.first, base = kv.second, n = lds_shape[off].first, Lc = lds_shape[off].second;
       const uint32_t nL = n * Lc, M = (65536u + Lc - 1) / Lc;  // i / Lc = (i * M) >> 16 for i * Lc < 2^16
@@ -801,14 +823,13 @@ struct Gen {
         if (!inl(base)) E.salu("s_mov_b32 s41, " + hexs(base), {41});
         E.valu("v_add3_u32 " + VL(vj) + ", " + VL(vj) + ", " + VL(ve) + ", " + (inl(base) ? imm(base) : "s41"), {41});
         E.valu("v_lshlrev_b32_e32 " + VL(vj) + ", 2, " + VL(vj));
-        E.ctl("s_waitcnt vmcnt(0)");
-        E.mem("ds_write_b32 " + VL(vj) + ", " + VL(vt));
         drop(vi);
-        drop(vt);
         drop(ve);
-        drop(vj);
+        pend.push_back({vt, vj});
+        if (pend.size() >= stage_batch()) flush();
       }
     }
+    flush();
     E.ctl("s_waitcnt lgkmcnt(0)");
     E.ctl("s_barrier");
   }
