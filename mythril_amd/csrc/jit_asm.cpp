@@ -1578,6 +1578,14 @@ struct Gen {
     }();
     return on;
   }
+  // MYTHGPU_JIT_ASM_EXIT_SKIP=1: a wave reads the hit word before its end-of-wave atomicMin (measuring)
+  static bool exit_skip() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_EXIT_SKIP");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
   static bool no_slt_clamp() {
     static const bool on = [] {
       const char* g = getenv("MYTHGPU_JIT_ASM_NO_SLT_CLAMP");
@@ -5271,6 +5279,21 @@ struct Gen {
       const std::string nobest = E.newlab(), end = E.newlab();
       E.salu("s_cmp_eq_u64 s[30:31], -1");
       E.ctl("s_cbranch_scc1 " + nobest);
+      if (exit_skip()) {
+        // every wave's atomicMin on the one hit word serialises at the L2 (C3: most waves hit, 65,536
+        // waves at 64 blocks per CU): read the word first and skip the atomic when this wave's best
+        // cannot lower it (a stale read is larger than the word, never smaller: at worst one atomic
+        // too many)
+        E.salu("s_mov_b64 exec, 1");
+        E.mem("global_load_dwordx2 v[8:9], v6, s[16:17]", {16, 17});
+        E.ctl("s_waitcnt vmcnt(0)");
+        E.valu("v_readfirstlane_b32 s46, v8", {}, {46});
+        E.valu("v_readfirstlane_b32 s47, v9", {}, {47});
+        E.salu("s_mov_b64 exec, -1");
+        E.salu("s_sub_u32 s44, s30, s46", {44});
+        E.salu("s_subb_u32 s44, s31, s47", {44});  // SCC: best < word
+        E.ctl("s_cbranch_scc0 " + nobest);
+      }
       E.salu("s_mov_b64 exec, 1");
       E.valu("v_mov_b32_e32 v8, s30", {30});
       E.valu("v_mov_b32_e32 v9, s31", {31});
