@@ -1578,11 +1578,12 @@ struct Gen {
     }();
     return on;
   }
-  // MYTHGPU_JIT_ASM_EXIT_SKIP=1: a wave reads the hit word before its end-of-wave atomicMin (measuring)
+  // a wave reads the hit word before its end-of-wave atomicMin (MYTHGPU_JIT_ASM_EXIT_SKIP=0: always
+  // the atomic; profiles/r05s_rates_exit_skip.jsonl: C3's first tier 282 -> 435 G/s)
   static bool exit_skip() {
     static const bool on = [] {
       const char* g = getenv("MYTHGPU_JIT_ASM_EXIT_SKIP");
-      return g && g[0] == '1';
+      return !(g && g[0] == '0');
     }();
     return on;
   }

@@ -43,7 +43,7 @@ WORKERS = max(1, min(8, os.cpu_count() or 1))
 CONFIGS = [
     {},
     {"MYTHGPU_EQ_PUSHDOWN": "0", "MYTHGPU_ITE_PRUNE": "0"},
-    {"MYTHGPU_JIT_ASM_NO_EQ_CACHE": "1", "MYTHGPU_JIT_ASM_NO_BOOL_LOOKUP": "1", "MYTHGPU_JIT_ASM_EXIT_SKIP": "1"},
+    {"MYTHGPU_JIT_ASM_NO_EQ_CACHE": "1", "MYTHGPU_JIT_ASM_NO_BOOL_LOOKUP": "1", "MYTHGPU_JIT_ASM_EXIT_SKIP": "0"},
     {"MYTHGPU_JIT_ASM_NOPOOL": "1", "MYTHGPU_EQ_PUSHDOWN": "1", "MYTHGPU_JIT_ASM_GLDS": "1"},
 ]
 
