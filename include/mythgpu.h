@@ -222,6 +222,7 @@ typedef struct mg_stats {
   uint32_t cu_count;
   uint32_t clock_mhz;
   uint32_t n_devices;  /* logical devices mg_init opened (the mask's GPUs) */
+  uint64_t jit_refused;  /* JIT code objects the load gate refused (mg_code_object_check) */
 } mg_stats_t;
 
 /* device_mask: every set bit d opens GPU d (0 = GPU 0); all or nothing (a device that fails
@@ -301,6 +302,16 @@ int mg_program_jit_source(const uint8_t* ssa, size_t len, const uint32_t* gen_bl
  * kernel), optionally assembled */
 int mg_program_jit_asm(const uint8_t* ssa, size_t len, const uint32_t* gen_blob, size_t gen_words, int compile,
                        char* buf, size_t cap, size_t* out_len);
+/* host-only: the load gate every JIT code object passes before hipModuleLoadData (compiled or from
+ * the disk cache).  It reads the AMDHSA kernel descriptors: *kernels, the largest private segment
+ * per lane and LDS size over them, and whether any uses a dynamic stack (kernel_code_properties bit
+ * 11).  Returns MG_OK if the object would load, MG_E_UNSUPPORTED if the gate refuses it (a dynamic
+ * stack, more than MYTHGPU_JIT_PRIVATE_CAP bytes of private segment per lane — default 16 KiB — or
+ * more than 160 KiB of LDS), MG_E_INVALID if it is not a code object.  Out pointers may be null.
+ * A refused compile fails its JIT request with MG_E_UNSUPPORTED (search stays on the interpreter,
+ * the get_model hook on z3); mg_stats counts refusals in jit_refused. */
+int mg_code_object_check(const void* code, size_t len, uint32_t* kernels, uint32_t* max_private_bytes,
+                         uint32_t* max_group_bytes, uint32_t* dynamic_stack);
 int mg_jit_compile(uint64_t prog, uint64_t gen, uint64_t* jit_handle);
 /* flags: MG_JIT_GEN_VERDICTS also builds mgj_gen (per-candidate verdicts, mg_jit_verdicts);
  * MG_JIT_ASM builds the first tier instead: the same kernels emitted as gfx950 assembly with the

@@ -1216,6 +1216,7 @@ struct Engine {
   hipStream_t xs[4] = {};
   hipEvent_t xev[4] = {};
   mg_stats_t stats{};
+  uint64_t refused_base = 0;  // jit_refused_total() at the last mg_stats_reset
 };
 
 Engine& E() {
@@ -2449,6 +2450,7 @@ int mg_stats(mg_stats_t* out) {
   std::lock_guard<std::mutex> g(e.mu);
   OnDevice od_(e);
   *out = e.stats;
+  out->jit_refused = jit_refused_total() - e.refused_base;
   return MG_OK;
 }
 
@@ -2462,6 +2464,7 @@ int mg_stats_reset(void) {
   e.stats.cu_count = keep.cu_count;
   e.stats.clock_mhz = keep.clock_mhz;
   e.stats.n_devices = keep.n_devices;
+  e.refused_base = jit_refused_total();
   return MG_OK;
 }
 
@@ -2628,6 +2631,21 @@ int mg_program_jit_asm(const uint8_t* ssa, size_t len, const uint32_t* gen_blob,
     rc = jit_compile(src, code, log);
     if (rc) return set_err(rc, "JIT assembly failed: " + log.substr(0, 4000));
   }
+  return MG_OK;
+}
+
+int mg_code_object_check(const void* code, size_t len, uint32_t* kernels, uint32_t* max_private_bytes,
+                         uint32_t* max_group_bytes, uint32_t* dynamic_stack) {
+  CodeObjectInfo ci;
+  std::string err;
+  if (int rc = code_object_info(code, len, ci, err)) return set_err(rc, err);
+  if (kernels) *kernels = ci.kernels;
+  if (max_private_bytes) *max_private_bytes = ci.max_private_bytes;
+  if (max_group_bytes) *max_group_bytes = ci.max_group_bytes;
+  if (dynamic_stack) *dynamic_stack = ci.dynamic_stack ? 1u : 0u;
+  // the gate's verdict, not counted as a refusal of a JIT request
+  std::string why;
+  if (int rc = code_object_gate(ci, why)) return set_err(rc, why);
   return MG_OK;
 }
 

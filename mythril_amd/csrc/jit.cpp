@@ -6,6 +6,7 @@
 #include "jit.hpp"
 
 #include <dlfcn.h>
+#include <elf.h>
 #include <signal.h>
 #include <spawn.h>
 #include <sys/socket.h>
@@ -1941,6 +1942,127 @@ std::string disk_path(const std::string& dir, const std::string& key) {
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// Load gate: read the AMDHSA kernel descriptors of a code object (ELF64, EM_AMDGPU).  Each kernel
+// `k` has a 64-byte descriptor at symbol `k.kd`: group_segment_fixed_size at +0,
+// private_segment_fixed_size at +4, kernel_code_properties (u16) at +56, whose bit 11 is
+// USES_DYNAMIC_STACK.  These are the fields the runtime sizes scratch from, so they are what a
+// load has to be judged by (the msgpack metadata note only restates them).
+// ---------------------------------------------------------------------------
+namespace {
+std::atomic<uint64_t> g_refused{0};
+
+template <typename T>
+bool read_at(const std::vector<uint8_t>& b, size_t off, T& v) {
+  if (off > b.size() || b.size() - off < sizeof(T)) return false;
+  std::memcpy(&v, b.data() + off, sizeof(T));
+  return true;
+}
+}  // namespace
+
+int code_object_info(const void* code, size_t len, CodeObjectInfo& out, std::string& err) {
+  out = CodeObjectInfo{};
+  if (!code || len < sizeof(Elf64_Ehdr)) {
+    err = "code object too short";
+    return MG_E_INVALID;
+  }
+  const std::vector<uint8_t> b((const uint8_t*)code, (const uint8_t*)code + len);
+  Elf64_Ehdr eh;
+  std::memcpy(&eh, b.data(), sizeof eh);
+  if (std::memcmp(eh.e_ident, ELFMAG, SELFMAG) || eh.e_ident[EI_CLASS] != ELFCLASS64 || eh.e_machine != EM_AMDGPU ||
+      eh.e_shentsize != sizeof(Elf64_Shdr)) {
+    err = "not an AMDGPU ELF64 code object";
+    return MG_E_INVALID;
+  }
+  std::vector<Elf64_Shdr> sh(eh.e_shnum);
+  for (size_t i = 0; i < sh.size(); i++)
+    if (!read_at(b, eh.e_shoff + i * sizeof(Elf64_Shdr), sh[i])) {
+      err = "section headers out of range";
+      return MG_E_INVALID;
+    }
+  // prefer .symtab (every symbol); a stripped object still has .dynsym with the .kd symbols
+  int symi = -1;
+  for (size_t i = 0; i < sh.size(); i++)
+    if (sh[i].sh_type == SHT_SYMTAB) symi = (int)i;
+  if (symi < 0)
+    for (size_t i = 0; i < sh.size(); i++)
+      if (sh[i].sh_type == SHT_DYNSYM) symi = (int)i;
+  if (symi < 0 || sh[symi].sh_link >= sh.size() || sh[symi].sh_entsize != sizeof(Elf64_Sym)) {
+    err = "no symbol table";
+    return MG_E_INVALID;
+  }
+  const Elf64_Shdr& st = sh[symi];
+  const Elf64_Shdr& strs = sh[st.sh_link];
+  for (uint64_t k = 0; k < st.sh_size / sizeof(Elf64_Sym); k++) {
+    Elf64_Sym s;
+    if (!read_at(b, st.sh_offset + k * sizeof(Elf64_Sym), s)) break;
+    if (s.st_name >= strs.sh_size || s.st_shndx == SHN_UNDEF || s.st_shndx >= sh.size()) continue;
+    const size_t noff = strs.sh_offset + s.st_name;
+    if (noff >= b.size()) continue;
+    const char* nm = (const char*)b.data() + noff;
+    const size_t nl = strnlen(nm, b.size() - noff);
+    if (nl < 4 || std::strncmp(nm + nl - 3, ".kd", 3)) continue;
+    const Elf64_Shdr& sec = sh[s.st_shndx];
+    if (s.st_value < sec.sh_addr || s.st_value + 64 > sec.sh_addr + sec.sh_size) {
+      err = "kernel descriptor outside its section";
+      return MG_E_INVALID;
+    }
+    const size_t off = sec.sh_offset + (s.st_value - sec.sh_addr);
+    uint32_t group = 0, priv = 0;
+    uint16_t props = 0;
+    if (!read_at(b, off, group) || !read_at(b, off + 4, priv) || !read_at(b, off + 56, props)) {
+      err = "kernel descriptor out of range";
+      return MG_E_INVALID;
+    }
+    out.kernels++;
+    out.max_private_bytes = std::max(out.max_private_bytes, priv);
+    out.max_group_bytes = std::max(out.max_group_bytes, group);
+    if (props & (1u << 11)) out.dynamic_stack = true;
+  }
+  if (!out.kernels) {
+    err = "no kernel descriptors";
+    return MG_E_INVALID;
+  }
+  return MG_OK;
+}
+
+int code_object_gate(const CodeObjectInfo& ci, std::string& why) {
+  static const uint32_t cap = [] {
+    const char* c = getenv("MYTHGPU_JIT_PRIVATE_CAP");
+    return c ? (uint32_t)strtoul(c, nullptr, 0) : 16384u;
+  }();
+  if (ci.dynamic_stack) {
+    why = "code object refused: a kernel uses a dynamic stack";
+    return MG_E_UNSUPPORTED;
+  }
+  if (ci.max_private_bytes > cap) {
+    why = "code object refused: " + std::to_string(ci.max_private_bytes) + " B of private segment per lane (cap " +
+          std::to_string(cap) + ", MYTHGPU_JIT_PRIVATE_CAP)";
+    return MG_E_UNSUPPORTED;
+  }
+  if (ci.max_group_bytes > 160u * 1024u) {
+    why = "code object refused: " + std::to_string(ci.max_group_bytes) + " B of LDS (gfx950 has 160 KiB per CU)";
+    return MG_E_UNSUPPORTED;
+  }
+  return MG_OK;
+}
+
+int jit_check_code_object(const std::vector<char>& code, std::string& why) {
+  CodeObjectInfo ci;
+  std::string err;
+  int rc = code_object_info(code.data(), code.size(), ci, err);
+  if (rc == MG_OK) {
+    rc = code_object_gate(ci, why);
+  } else {
+    why = "code object refused: " + err;
+    rc = MG_E_UNSUPPORTED;
+  }
+  if (rc != MG_OK) g_refused++;
+  return rc;
+}
+
+uint64_t jit_refused_total() { return g_refused.load(); }
+
 void jit_disk_evict(const std::string& src) {
   const std::string dir = disk_cache_dir();
   if (dir.empty()) return;
@@ -1960,6 +2082,11 @@ int jit_compile(const std::string& src, std::vector<char>& code, std::string& lo
     path = disk_path(dir, key);
     if (disk_load(path, klen, h1, code)) {
       if (timing) fprintf(stderr, "mythgpu: JIT code object from the disk cache %s\n", path.c_str());
+      if (int rc = jit_check_code_object(code, log)) {  // written by a build without the gate
+        (void)unlink(path.c_str());
+        code.clear();
+        return rc;
+      }
       if (from_disk) *from_disk = true;
       return MG_OK;
     }
@@ -1976,6 +2103,14 @@ int jit_compile(const std::string& src, std::vector<char>& code, std::string& lo
     }
   }
   if (!done) rc = jit_compile_local(src, code, log);
+  if (rc == MG_OK) {
+    rc = jit_check_code_object(code, log);
+    if (rc != MG_OK) {
+      if (timing) fprintf(stderr, "mythgpu: %s\n", log.c_str());
+      code.clear();
+      return rc;
+    }
+  }
   if (rc == MG_OK && !path.empty()) {
     disk_store(dir, path, klen, h1, code);
     if (timing) fprintf(stderr, "mythgpu: JIT code object stored in the disk cache %s\n", path.c_str());

@@ -38,6 +38,27 @@ int jit_compile(const std::string& src, std::vector<char>& code, std::string& lo
 void jit_disk_evict(const std::string& src);
 int jit_compile_local(const std::string& src, std::vector<char>& code, std::string& log);
 
+// What a code object asks of the runtime, read from its AMDHSA kernel descriptors (every `*.kd`
+// symbol): the largest private (scratch) segment per lane, whether any kernel uses a dynamic stack
+// (kernel_code_properties bit 11), and how many kernels it holds.  MG_OK, or MG_E_INVALID for a
+// blob that is not a gfx950 ELF code object with kernel descriptors.
+struct CodeObjectInfo {
+  uint32_t kernels = 0;
+  uint32_t max_private_bytes = 0;
+  uint32_t max_group_bytes = 0;
+  bool dynamic_stack = false;
+};
+int code_object_info(const void* code, size_t len, CodeObjectInfo& out, std::string& err);
+// The load gate jit_compile applies to every code object, compiled or from the disk cache: a kernel
+// with a dynamic stack, or with more than MYTHGPU_JIT_PRIVATE_CAP bytes (default 16 KiB) of private
+// segment per lane, or more than 160 KiB of LDS, is refused with MG_E_UNSUPPORTED before anything
+// loads it (round 5's -O0 read-back kernel kept 52 KB per lane on a dynamic stack and faulted:
+// profiles/r05n_gpu_pytest_O0_fault.log).  jit_refused_total counts refusals for mg_stats.
+int jit_check_code_object(const std::vector<char>& code, std::string& why);
+// the gate's verdict on descriptors already read (MG_OK or MG_E_UNSUPPORTED with `why`), uncounted
+int code_object_gate(const CodeObjectInfo& ci, std::string& why);
+uint64_t jit_refused_total();
+
 // the helper process: stop it (end of input; it exits), and its pid (-1 none yet, -2 died)
 void jit_helper_stop();
 int jit_helper_pid();

@@ -2712,7 +2712,15 @@ struct Gen {
   // LDS (ds_write per limb, the wave's slots at s35) and comes back on its next read (ds_read).
   // Spills happen outside branches only; a read of a spilled value under a branch fails the
   // kernel (the O3 kernel then).  Off unless the kernel fails without (jit_asm_source).
+  // Slot layout, lane-major: lane l's slot k at s35 + 4 (S l + k), S = spill_stride() (odd, so the
+  // 64 lanes of one access fall in distinct banks), one 16-bit ds offset of 4 k reaching every slot.
+  // The slots of a workgroup's waves must fit the 160 KiB of LDS: at most 159 per wave with four
+  // working waves; a read-back that needs more (VMTests' expXY: 63 live 256-bit keys) runs `solo` —
+  // one working wave per 256-lane workgroup, the other three exit at once — with up to 639.
   bool spill_on = false;
+  bool solo = false;
+  uint32_t spill_stride() const { return spill_hwm | 1u; }
+  uint32_t spill_cap() const { return ((160u * 1024u) / ((solo ? 1u : 4u) * 256u) - 1u) | 1u; }
   int vhard = 256;
   std::vector<std::vector<int>> spill_at;  // value id -> LDS slot of each register limb (-1 none); empty: resident
   std::vector<uint8_t> slot_busy;
@@ -2757,11 +2765,11 @@ struct Gen {
       if (!x.l[j].reg()) continue;
       uint32_t sl = 0;
       while (sl < slot_busy.size() && slot_busy[sl]) sl++;
-      if (sl >= 255) fail("out of VGPRs (spill slots)");
+      if ((sl | 1u) > spill_cap()) fail("out of VGPRs (spill slots)");
       if (sl == slot_busy.size()) slot_busy.push_back(0);
       slot_busy[sl] = 1;
       spill_hwm = std::max(spill_hwm, sl + 1);
-      E.mem("ds_write_b32 " + VL(spill_v) + ", " + VL(x.l[j]) + " offset:" + std::to_string(sl * 256u));
+      E.mem("ds_write_b32 " + VL(spill_v) + ", " + VL(x.l[j]) + " offset:" + std::to_string(sl * 4u));
       at[j] = (int)sl;
     }
     E.ctl("s_waitcnt lgkmcnt(0)");  // the stores have read their registers
@@ -2785,7 +2793,7 @@ struct Gen {
     for (size_t j = 0; j < at.size(); j++) {
       if (at[j] < 0) continue;
       const Limb d = fresh();
-      E.mem("ds_read_b32 " + VL(d) + ", " + VL(spill_v) + " offset:" + std::to_string((uint32_t)at[j] * 256u));
+      E.mem("ds_read_b32 " + VL(d) + ", " + VL(spill_v) + " offset:" + std::to_string((uint32_t)at[j] * 4u));
       x.l[j] = d;
     }
     E.ctl("s_waitcnt lgkmcnt(0)");
@@ -4949,13 +4957,23 @@ struct Gen {
     E.ctl("s_waitcnt lgkmcnt(0)");
     for (const auto& kv : pool) E.valu("v_mov_b32_e32 " + V((uint32_t)kv.second) + ", " + imm(kv.first));
     // n * 4 (64-bit) in s[20:21]; the wave's first candidate s16 = block * 256 + wave * 64; stride s17
+    // (solo: s16 = block * 64, stride 64 per block, and waves 1..3 leave at once)
     E.salu("s_lshl_b64 s[20:21], s[8:9], 2", {20, 21});
-    E.salu("s_lshl_b32 s16, s2, 8", {16});
-    E.salu("s_lshl_b32 s22, s3, 6", {22});
-    E.salu("s_add_u32 s16, s16, s22", {16});
-    E.salu("s_lshl_b32 s17, s14, 8", {17});
+    if (solo) {
+      E.salu("s_lshl_b32 s16, s2, 6", {16});
+      E.salu("s_lshl_b32 s17, s14, 6", {17});
+    } else {
+      E.salu("s_lshl_b32 s16, s2, 8", {16});
+      E.salu("s_lshl_b32 s22, s3, 6", {22});
+      E.salu("s_add_u32 s16, s16, s22", {16});
+      E.salu("s_lshl_b32 s17, s14, 8", {17});
+    }
     E.salu("s_add_u32 s23, s8, -1", {23});  // n - 1
     const std::string loop = E.newlab(), exit_ = E.newlab();
+    if (solo) {
+      E.salu("s_cmp_lg_u32 s3, 0");
+      E.ctl("s_cbranch_scc1 " + exit_);
+    }
     // the ring: the first rows of the wave's first group, loaded before the loop
     ring_reg.clear();
     if (!glds)
@@ -4963,10 +4981,11 @@ struct Gen {
     vnext = tiled ? Limb{} : fresh();
     spill_hwm = 0;
     spills = 0;
-    if (spill_on) {  // the wave's spill slots: s35 = wave * slots * 256 (patched below), spill_v = s35 + 4 * lane
+    if (spill_on) {  // the wave's spill slots: s35 = wave * 256 S, spill_v = s35 + 4 S lane (S patched below)
       spill_v = fresh();
       E.salu("s_mul_i32 s35, s3, __MG_SPILL_BYTES__", {35});
-      E.valu("v_lshl_add_u32 " + VL(spill_v) + ", v1, 2, s35", {35});
+      E.valu("v_mul_u32_u24_e32 " + VL(spill_v) + ", __MG_SPILL_STRIDE_, v1");
+      E.valu("v_lshl_add_u32 " + VL(spill_v) + ", " + VL(spill_v) + ", 2, s35", {35});
     }
     if (glds) {  // the wave's LDS slots: s34 = wave * slots * 256, glds_v = s34 + 4 * lane
       glds_v = fresh();
@@ -5067,7 +5086,9 @@ struct Gen {
     if (spill_on) {
       // the spill slots' wave stride: the ds offsets stay below the LDS-staged rows' slots' end
       const size_t at = res.find("__MG_SPILL_BYTES__");
-      if (at != std::string::npos) res.replace(at, 18, hexs(spill_hwm * 256u));
+      if (at != std::string::npos) res.replace(at, 18, hexs(spill_stride() * 256u));
+      const size_t st = res.find("__MG_SPILL_STRIDE_");
+      if (st != std::string::npos) res.replace(st, 18, hexs(spill_stride()));
     }
     return res;
   }
@@ -5075,7 +5096,7 @@ struct Gen {
   // the eval kernel's LDS: four waves' row slots (256 B each) when rows are LDS-staged, and four
   // waves' spill slots
   uint32_t eval_lds_bytes() const {
-    return (glds ? 4u * glds_slots() * 256u : 0u) + (spill_on ? 4u * spill_hwm * 256u : 0u);
+    return (glds ? 4u * glds_slots() * 256u : 0u) + (spill_on ? (solo ? 1u : 4u) * spill_stride() * 256u : 0u);
   }
 
   int labels = 0;  // label numbers continue across the kernels of one module
@@ -5520,7 +5541,16 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
       g2.vsoft = 256;
       if (const char* st = getenv("MYTHGPU_JIT_ASM_SPILL_TEST")) g2.vhard = g2.vsoft = std::max(24, std::min(256, atoi(st)));
       g2.labels = 0;
-      const std::string ks = g2.kernel_eval("mgj_eval");
+      std::string ks;
+      try {
+        ks = g2.kernel_eval("mgj_eval");
+      } catch (const AsmFail& f2) {
+        // more slots than four waves' LDS holds: one working wave per workgroup (Gen::solo)
+        if (f2.why.find("spill slots") == std::string::npos) throw;
+        g2.solo = true;
+        g2.labels = 0;
+        ks = g2.kernel_eval("mgj_eval");
+      }
       o << ks << metadata_eval(g2.meta_vgpr["mgj_eval"], g2.meta_sgpr["mgj_eval"], g2.eval_lds_bytes());
       out = o.str();
       return MG_OK;

@@ -52,7 +52,7 @@ EXPORTS = [
     "mg_program_specialized", "mg_program_load",
     "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_info", "mg_gen_free", "mg_eval", "mg_eval_dev",
     "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
-    "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_program_jit_asm", "mg_jit_compile", "mg_jit_compile_ex", "mg_jit_verdicts", "mg_jit_info", "mg_jit_layout",
+    "mg_dev_free", "mg_dev_upload", "mg_dev_download", "mg_program_jit_source", "mg_program_jit_asm", "mg_code_object_check", "mg_jit_compile", "mg_jit_compile_ex", "mg_jit_verdicts", "mg_jit_info", "mg_jit_layout",
     "mg_jit_compile_async", "mg_jit_poll", "mg_jit_cancel", "mg_jit_helper_pid", "mg_cache_clear", "mg_split_range",
     "mg_jit_free", "mg_jit_search", "mg_jit_search_many", "mg_jit_eval", "mg_jit_eval_dev",
 ]
@@ -82,7 +82,7 @@ class Stats(C.Structure):
         ("programs_loaded", C.c_uint64), ("launches", C.c_uint64), ("candidates", C.c_uint64),
         ("hits", C.c_uint64), ("kernel_ms_total", C.c_double), ("last_kernel_ms", C.c_double),
         ("last_candidates", C.c_uint64), ("device", C.c_uint32), ("cu_count", C.c_uint32),
-        ("clock_mhz", C.c_uint32), ("n_devices", C.c_uint32),
+        ("clock_mhz", C.c_uint32), ("n_devices", C.c_uint32), ("jit_refused", C.c_uint64),
     ]
 
 
@@ -139,6 +139,7 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
             "mg_dev_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
             "mg_program_jit_source": (C.c_int, [u8p, C.c_size_t, u32p, C.c_size_t, C.c_int, C.c_char_p,
                                                 C.c_size_t, C.POINTER(C.c_size_t)]),
+            "mg_code_object_check": (C.c_int, [C.c_void_p, C.c_size_t, u32p, u32p, u32p, u32p]),
             "mg_program_jit_asm": (C.c_int, [u8p, C.c_size_t, u32p, C.c_size_t, C.c_int, C.c_char_p,
                                              C.c_size_t, C.POINTER(C.c_size_t)]),
             "mg_jit_compile": (C.c_int, [C.c_uint64, C.c_uint64, u64p]),
@@ -362,6 +363,11 @@ class Engine:
     def eval(self, prog: int, soa: np.ndarray, n: int, watch_words: int = 0):
         """Evaluate n candidates given as a [coord_words][n] uint32 SoA."""
         soa = np.ascontiguousarray(soa, dtype=np.uint32)
+        info = self.info(prog)  # mg_eval reads coord_words x n words and writes watch_words x n
+        if soa.size < info.coord_words * n:
+            raise ValueError(f"eval: SoA of {soa.size} words, the program reads {info.coord_words} x {n}")
+        if watch_words and watch_words < info.watch_words:
+            raise ValueError(f"eval: program stores {info.watch_words} watch rows, caller asked for {watch_words}")
         ver = np.zeros(n, dtype=np.uint8)
         watch = np.zeros((max(watch_words, 1), n), dtype=np.uint32) if watch_words else None
         _check(self.lib.mg_eval(prog, _ptr(soa, C.c_uint32), n, _ptr(ver, C.c_uint8),
@@ -467,7 +473,11 @@ class Engine:
         """Verdicts (and watch rows) of n explicit candidates.  The SoA is checked against the kernel's
         layout first: [coord_words][n] row-major, or tile_soa's (blocks, coord_words, 64) for a kernel
         compiled ``tiled`` — mg_jit_eval copies coord_words x n (tiled: x ceil(n/64) x 64) words from it."""
-        flags, cw, _ = self.jit_layout(jit)
+        flags, cw, ww = self.jit_layout(jit)
+        # mg_jit_eval copies the kernel's own watch_words rows into watch_out: a buffer sized from a
+        # smaller count would be overrun
+        if watch_words and watch_words < ww:
+            raise ValueError(f"eval kernel stores {ww} watch rows, caller asked for {watch_words}")
         if flags & MG_JIT_SOA_TILED:
             blocks = (n + 63) // 64
             if getattr(soa, "ndim", 0) != 3 or tuple(soa.shape[1:]) != (cw, 64) or soa.shape[0] < blocks:

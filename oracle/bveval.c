@@ -45,6 +45,8 @@ typedef struct {
   const uint32_t* coords; /* 4 words each */
   const uint32_t* tables;
   const uint32_t* consts;
+  uint32_t n_watch;
+  const uint32_t* watch; /* node ids whose values a model read-back returns */
   /* generator */
   uint32_t gen_n;
   const uint32_t* specs; /* 8 words each */
@@ -670,6 +672,7 @@ static int parse(prog_t* P, const uint32_t* w, size_t n, const uint32_t* gen, si
   P->n_tables = w[5];
   P->n_consts = w[6];
   uint32_t n_watch = w[7];
+  P->n_watch = n_watch;
   size_t pos = 16;
   P->nodes = (const node_t*)(w + pos);
   pos += 8ull * P->n_nodes;
@@ -679,6 +682,7 @@ static int parse(prog_t* P, const uint32_t* w, size_t n, const uint32_t* gen, si
   pos += 4ull * P->n_coords;
   P->tables = w + pos;
   pos += 4ull * P->n_tables;
+  P->watch = w + pos;
   pos += n_watch;
   P->consts = w + pos;
   pos += P->n_consts;
@@ -746,7 +750,18 @@ int bv_search(const uint32_t* prog, size_t prog_words, const uint32_t* gen, size
 
 /* Evaluate explicit assignments (SoA [row][n], as mg_eval); optional per-node dump
  * of node `watch_node` values (dump: n x MAXW 64-bit words). */
+int bv_eval_watch(const uint32_t* prog, size_t prog_words, const uint32_t* soa, uint64_t n, uint8_t* verdicts,
+                  uint32_t* watch_out);
+
 int bv_eval(const uint32_t* prog, size_t prog_words, const uint32_t* soa, uint64_t n, uint8_t* verdicts) {
+  return bv_eval_watch(prog, prog_words, soa, n, verdicts, NULL);
+}
+
+/* ... and (watch_out non-null) the model read-back mg_eval returns: watch node k's value as
+ * ceil(width/32) little-endian limb rows of n uint32, the watch list in order
+ * (laser/smt/model.py:45-59, Model.eval of each watched term). */
+int bv_eval_watch(const uint32_t* prog, size_t prog_words, const uint32_t* soa, uint64_t n, uint8_t* verdicts,
+                  uint32_t* watch_out) {
   prog_t P;
   int rc = parse(&P, prog, prog_words, NULL, 0);
   if (rc) return rc;
@@ -770,6 +785,16 @@ int bv_eval(const uint32_t* prog, size_t prog_words, const uint32_t* soa, uint64
     int v = eval_candidate(&X);
     if (v < 0) bad = 1;
     verdicts[i] = (uint8_t)(v > 0);
+    if (watch_out) {
+      uint64_t row = 0;
+      for (uint32_t k = 0; k < P.n_watch; k++) {
+        const uint32_t id = P.watch[k];
+        if (id >= P.n_nodes) { bad = 1; break; }
+        const uint32_t L = (P.nodes[id].width + 31) / 32;
+        for (uint32_t j = 0; j < L; j++) watch_out[(row + j) * n + i] = get_limb32(&X.vals[id], j);
+        row += L;
+      }
+    }
   }
   free(X.vals);
   free(X.entries);

@@ -32,6 +32,8 @@ extern "C" {
 int bv_search(const uint32_t* prog, size_t prog_words, const uint32_t* gen, size_t gen_words, uint64_t seed,
               uint64_t start, uint64_t count, int threads, uint64_t* first_hit, uint64_t* n_hits, uint8_t* verdicts);
 int bv_eval(const uint32_t* prog, size_t prog_words, const uint32_t* soa, uint64_t n, uint8_t* verdicts);
+int bv_eval_watch(const uint32_t* prog, size_t prog_words, const uint32_t* soa, uint64_t n, uint8_t* verdicts,
+                  uint32_t* watch_out);
 }
 
 using namespace mg;
@@ -326,7 +328,11 @@ std::string check_eval(const std::vector<uint8_t>& prog, uint64_t seed, uint32_t
     }
   }
   std::vector<uint8_t> want(n);
-  if (bv_eval((const uint32_t*)prog.data(), prog.size() / 4, soa.data(), n, want.data())) return "C port eval failed";
+  // the model read-back rows too (watch list kept: the kernel stores them, mg_jit_eval's watch_out)
+  std::vector<uint32_t> want_w((size_t)sp.watch_words * n, 0);
+  if (bv_eval_watch((const uint32_t*)prog.data(), prog.size() / 4, soa.data(), n, want.data(),
+                    sp.watch_words ? want_w.data() : nullptr))
+    return "C port eval failed";
   asmsim::Stats st;
   try {
     const asmsim::Module m = asmsim::parse(src);
@@ -362,6 +368,17 @@ std::string check_eval(const std::vector<uint8_t>& prog, uint64_t seed, uint32_t
                  got[i], want[i]);
         return b;
       }
+    if (sp.watch_words) {
+      const uint32_t* gw = (const uint32_t*)mem.of(wb).data.data();
+      for (size_t k = 0; k < want_w.size(); k++)
+        if (gw[k] != want_w[k]) {
+          C.mismatch++;
+          char b[200];
+          snprintf(b, sizeof b, "mgj_eval%s watch row %zu of candidate %zu: asm %08x, C port %08x", tiled ? " (tiled)" : "",
+                   k / n, k % n, gw[k], want_w[k]);
+          return b;
+        }
+    }
     if (getenv("ASMSIM_COUNT")) {  // as for the search launch: per candidate, and per program instruction
       printf("count eval: valu %.1f salu %.1f vmem %.2f nop %.1f branch %.1f waitcnt %.1f per candidate\n",
              64.0 * st.valu / n, 64.0 * st.salu / n, 64.0 * st.vmem / n, 64.0 * st.nop_slots / n,

@@ -401,6 +401,57 @@ def test_asm_eval_spills_sim(sim, monkeypatch):
     print("spills:", summary, "kernels with spills:", spilled)
 
 
+def _vmtest_readbacks(names=None, every=1):
+    """VMTests model read-backs as eval programs (watch rows kept), the shape
+    ``test_jit_vmtests_literals_as_runtime_inputs`` runs on the GPU: post-state storage words with
+    every PUSH literal lifted into a runtime coordinate
+    (``tests/laser/evm_testsuite/evm_test.py:109-188``)."""
+    from mythril_amd import ssa
+    from mythril_amd.smt import terms as T
+    from tests.helpers import lift_literals, vmtest_cases
+
+    out = []
+    for ci, (name, v, r) in enumerate(vmtest_cases()):
+        keys = [int(k, 16) for k in v["post_storage"]]
+        if not keys or (names is not None and name not in names) or (names is None and ci % every):
+            continue
+        lifted, _ = lift_literals([r.storage_word(k).raw for k in keys])
+        P = ssa.flatten([T.BoolVal(True)], extra=lifted)
+        P.set_watch([P.term_node[w.id] for w in lifted])
+        out.append((name, P.to_bytes()))
+    return out
+
+
+READBACK_SOLO = ("TestNameRegistrator", "expXY", "expXY_success")
+
+
+def test_asm_eval_readbacks_sim(sim):
+    """Model read-back kernels (watch rows stored) against the C port's values row by row — every
+    eleventh VMTests read-back plus the three whose 63 live 256-bit calldata keys need more LDS
+    spill slots than four waves of a workgroup can hold (160 KiB): those run `solo`, one working
+    wave per workgroup with up to 639 lane-major slots (jit_asm.cpp, Gen::solo).  Until round 6
+    they went to the O3 tier (20-160 s of LLVM each)."""
+    from mythril_amd import native
+
+    progs = _vmtest_readbacks(every=11) + _vmtest_readbacks(names=READBACK_SOLO)
+    assert len(progs) >= 30
+    solo = 0
+    for name, pb in progs:
+        src = native.jit_asm(pb, None)  # inside the tier: no EngineUnsupported
+        if name in READBACK_SOLO:
+            assert "s_cmp_lg_u32 s3, 0" in src and "ds_write_b32" in src, name
+            lds = int(src.split(".amdhsa_group_segment_fixed_size ")[1].split()[0])
+            assert 160 * 256 < lds <= 160 * 1024, (name, lds)  # past four waves' share, inside the CU's LDS
+            solo += 1
+    assert solo == 3
+    rng = random.Random(17)
+    recs = [record(1 + (i & 1), pb, None, rng.getrandbits(32), 0, 64 * 2 + 5) for i, (_, pb) in enumerate(progs)]
+    rc, summary, bad, err = run_sim(sim, b"".join(recs), {"MYTHGPU_JIT_ASM_CHECK": "1"})
+    assert rc == 0 and summary, f"{summary}\n" + "\n".join(bad[:5]) + "\n" + err[-3000:]
+    assert int(summary["ok"]) == len(recs), (summary, bad[:5])
+    print("read-backs:", summary)
+
+
 def _full_worker(args):
     exe, lo, hi, cfg, kind = args
     recs = _fuzz_records(lo, hi, full=True) if kind == "laser" else _tier_records(lo, hi, full=True)

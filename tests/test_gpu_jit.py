@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from helpers import RandomProgram, load_json, random_assignments, vmtest_cases
-from mythril_amd import search, ssa, workloads
+from mythril_amd import native, search, ssa, workloads
 from mythril_amd.replay import replay_assignment
 from mythril_amd.smt import terms as T
 from oracle.bv import OracleModel, evaluate
@@ -196,6 +196,10 @@ def _vmtests_replay(engine, o3):
             info = engine.info(prog)
             jh = engine.jit_compile(prog, 0, o3=o3)
             try:
+                flags, _, _ = engine.jit_layout(jh)
+                # round 6: every read-back is inside the first tier (the three with 63 live keys run
+                # `solo`), so none pays the O3 compile; the O3 sample asks for O3 explicitly
+                assert bool(flags & native.MG_JIT_ASM) == (not o3), (name, flags)
                 _, w_j = engine.jit_eval(jh, soa, 1, watch_words=info.watch_words)
             finally:
                 engine.jit_free(jh)
