@@ -385,13 +385,17 @@ def main():
         evals = []
         # the O3 and first-tier (jit_asm.cpp) eval kernels, each on the [row][candidate] SoA and on the
         # tiled SoA (MG_JIT_SOA_TILED: a group's rows in one block)
-        for asm in (False, True):
+        # (tiled SoA: a group's rows in one block); then the tier the engine picks when none is named
+        # (mg_jit_compile_ex without MG_JIT_ASM / MG_JIT_O3: what batched Model.eval gets by default)
+        for tier in ("o3", "asm", "default"):
             for tiled in (False, True):
                 for w in EVAL_WORKLOADS:
                     try:
-                        evals.append(eval_roofline(eng, torch, w, args.eval_candidates, args.pmc_dir, asm=asm, tiled=tiled))
+                        evals.append(eval_roofline(eng, torch, w, args.eval_candidates, args.pmc_dir, tiled=tiled,
+                                                   tier=tier))
                     except native.EngineUnsupported as e:
-                        evals.append({"workload": CONFIG_OF[w], "kernel": eval_kernel_name(asm, tiled), "unsupported": str(e)})
+                        evals.append({"workload": CONFIG_OF[w], "tier_requested": tier,
+                                      "kernel": eval_kernel_name(tier == "asm", tiled), "unsupported": str(e)})
 
     # CPU baseline: the C restatement over a bounded sample of the same candidates
     cpu = None
@@ -476,14 +480,18 @@ def eval_kernel_name(asm, tiled):
     return ("mgj_eval first tier (asm)" if asm else "mgj_eval (unspecialised program)") + (", tiled SoA" if tiled else "")
 
 
-def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5, asm=False, tiled=False):
+def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5, asm=False, tiled=False, tier=None):
     """``Model.eval`` batched (``laser/smt/model.py:45-59``): the compiled eval kernel
     (``mg_jit_eval_dev``) of the UNSPECIALISED program — no generator, no value ranges, every
     instruction evaluated — over n candidates whose coordinates are already in HBM as a
     ``[coord limb row][candidate]`` uint32 SoA (uniform random, masked to each coordinate's
     width), one verdict byte out per candidate.  Algorithmic bytes per candidate: 4 x the SoA
     rows the program reads (a coordinate the program never reads — an AUX word whose bytes
-    it reads through its sites, a lazy site — is not fetched) + 1 verdict byte out."""
+    it reads through its sites, a lazy site — is not fetched) + 1 verdict byte out.
+
+    ``tier``: "o3" / "asm" ask for a tier (MG_JIT_O3 / MG_JIT_ASM), "default" asks for none — the
+    engine then picks per program (engine.hip eval_tier_pick_asm) and the entry says which it built;
+    None: ``asm`` decides, as before."""
     from mythril_amd import native, search, ssa, workloads
 
     cs = workloads.WORKLOADS[workload]()
@@ -496,8 +504,11 @@ def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5, asm=False, tiled=Fal
     P.set_watch(prev)
     prog = eng.load(blob)
     info = eng.info(prog)
+    if tier is None:
+        tier = "asm" if asm else "o3"
     try:
-        jh = eng.jit_compile(prog, 0, asm=asm, tiled=tiled)
+        jh = eng.jit_compile(prog, 0, asm=tier == "asm", o3=tier == "o3", tiled=tiled)
+        asm = bool(eng.jit_layout(jh)[0] & native.MG_JIT_ASM)
     except Exception:
         eng.free(prog)
         raise
@@ -531,7 +542,7 @@ def eval_roofline(eng, torch, workload, n, pmc_dir, reps=5, asm=False, tiled=Fal
     del soa, ver
     bpc = 4 * rows_read + 1
     gbs = n * bpc / (kernel_ms * 1e-3) / 1e9
-    out = {"workload": CONFIG_OF[workload],
+    out = {"workload": CONFIG_OF[workload], "tier_requested": tier, "tier_built": "asm" if asm else "o3",
            "kernel": eval_kernel_name(asm, tiled), "soa_layout": "tiled" if tiled else "row-major", "candidates_per_launch": n,
            "program_instrs": int(info.n_instrs), "coord_words": cw, "soa_rows_read": rows_read,
            "bytes_per_candidate": bpc,

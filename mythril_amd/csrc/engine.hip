@@ -927,14 +927,15 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
       // EVAL: SoA row; GEN: output row (only written by active lanes)
       i[g] = (MODE == MODE_EVAL) ? (active[g] ? off : total - 1) : (idx - k.start);
     }
+    uint64_t cur_u = ~0ull;  // the hit word as this group starts (early exit only)
     if (early) {
       // every candidate below the current first hit is still evaluated, so the
       // final minimum is exact; waves entirely above it stop
       const unsigned long long cur = read_first_hit(k.first_hit, k.flags);
       // readfirstlane returns int: widen through uint32_t, or a low word with bit 31 set would
       // sign-extend over the high word
-      const uint64_t cur_u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) |
-                             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cur);
+      cur_u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) |
+              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cur);
       if (a0 + base >= cur_u) break;
     }
     // each group's key from its base (a0 + base + 64 g, a multiple of 64: idx >> 6 is the same for
@@ -954,7 +955,8 @@ __global__ void __launch_bounds__(kWave) k_run(KArgs k) {
           wave_hits += (uint64_t)__popcll(m);
           if (first < wave_best) {
             wave_best = first;
-            if (early && threadIdx.x == 0) {
+            // (a hit at or above the word read as the group started cannot lower it: no atomic)
+            if (early && threadIdx.x == 0 && first < cur_u) {
               atomicMin(k.first_hit, (unsigned long long)first);
               publish_peers(k.first_hit, (unsigned long long)first);
             }
@@ -1081,6 +1083,10 @@ struct DevJit {
   double compile_ms = 0;
   bool asm_tier = false;  // the first tier's kernels (jit_asm.cpp): an eval launch takes n < 2^30
   bool tiled = false;     // eval kernel compiled for the tiled SoA (MG_JIT_SOA_TILED)
+  // candidates per workgroup of a loop-free eval kernel (the first tier's `solo` read-backs: one
+  // 64-candidate group per workgroup, launched ceil(n / 64) wide); 0: the kernel loops over groups;
+  // -1: not read yet from the code object (code_object_info, mgj_meta_eval_cpb)
+  int eval_cpb = -1;
 };
 
 // unload (or let go of) a JIT kernel's module
@@ -1149,6 +1155,7 @@ struct JitTicket {
   std::vector<uint32_t> consts;
   bool cancelled = false;
   bool asm_fallback = false;  // the first tier was chosen by default (watch rows): O3 if it refuses
+  bool auto_eval = false;     // verdict-only eval, no tier asked for: the worker picks (eval_tier_pick)
   std::unique_ptr<DevJit> ready;  // loaded module, handed to Engine::jits by the poll
   int rc = MG_OK;
   std::string err;
@@ -2704,6 +2711,33 @@ static int load_jit(const std::vector<char>& code, const JitTicket& t, double co
   return MG_OK;
 }
 
+// The tier of a verdict-only eval kernel (batched Model.eval) when the caller names none.  Both tiers
+// are HBM-bound at different occupancies: on a small program LLVM's O3 kernel runs 8 waves per SIMD
+// and beats the first tier's 4 (C2 token_transfer_underflow: O3 0.80 of HBM against 0.72), on a
+// large one both run 2 waves and the first tier's row queue and instruction count win (C4
+// walletlibrary_kill: first tier 0.71-0.73 against O3 0.49-0.52; BENCH_r05 roofline_eval,
+// profiles/r06_eval_tiers.jsonl).  So the first tier's own register count decides: its kernel is
+// kept when it runs at most 3 waves per SIMD (more than 128 VGPRs), else the O3 kernel is compiled.
+// MYTHGPU_JIT_EVAL_TIER=o3|asm fixes the tier; MYTHGPU_JIT_EVAL_AUTO_VGPRS moves the threshold.
+static int eval_tier_env() {
+  static const int v = [] {
+    const char* w = getenv("MYTHGPU_JIT_EVAL_TIER");
+    if (!w) return 0;
+    return std::string(w) == "o3" ? 1 : std::string(w) == "asm" ? 2 : 0;
+  }();
+  return v;
+}
+
+static bool eval_tier_pick_asm(const std::string& asm_src) {
+  static const int thr = [] {
+    const char* c = getenv("MYTHGPU_JIT_EVAL_AUTO_VGPRS");
+    return c ? atoi(c) : 128;
+  }();
+  const size_t at = asm_src.find(".amdhsa_next_free_vgpr ");
+  if (at == std::string::npos) return true;
+  return atoi(asm_src.c_str() + at + 23) > thr;
+}
+
 static void jit_worker_main(Engine* ep, int device, int lane) {
   Engine& e = *ep;
   (void)hipSetDevice(device);
@@ -2728,6 +2762,10 @@ static void jit_worker_main(Engine* ep, int device, int lane) {
     if (t->flags & MG_JIT_ASM) {
       // the first tier: assembly straight from the specialised program (jit_asm.cpp)
       asm_rc = jit_asm_source(t->low, t->specs, t->consts, kernels, src, asm_err);
+      if (asm_rc == MG_OK && t->auto_eval && !eval_tier_pick_asm(src)) {
+        t->flags &= ~MG_JIT_ASM;
+        src = jit_source(t->low, nullptr, nullptr, kernels);
+      }
       if (asm_rc != MG_OK && t->asm_fallback) {  // chosen by default: the O3 kernel instead
         // (not at -O0: LLVM's -O0 kernel for a VMTests read-back kept 52 KB of stack per lane in a
         // dynamic stack and faulted on the GPU; -O1 compiled no faster than -O3)
@@ -2898,6 +2936,13 @@ static int submit_jit(Engine& e, uint64_t prog, uint64_t gen, uint32_t flags, ui
     if (t->low.watch_words && !(flags & (MG_JIT_ASM | MG_JIT_O3)) && !o3_env) {
       t->flags |= MG_JIT_ASM;
       t->asm_fallback = true;
+    }
+    // verdicts only (batched Model.eval): the worker emits the first tier and keeps it for a program
+    // whose kernel runs at <= 3 waves per SIMD, else compiles the O3 kernel (eval_tier_pick)
+    if (!t->low.watch_words && !(flags & (MG_JIT_ASM | MG_JIT_O3)) && eval_tier_env() != 1) {
+      t->flags |= MG_JIT_ASM;
+      t->asm_fallback = true;
+      t->auto_eval = eval_tier_env() == 0;
     }
   }
   const uint64_t h = e.next_handle++;
@@ -3240,6 +3285,20 @@ int mg_jit_eval_dev(uint64_t jit, const uint32_t* d_soa, uint64_t n, uint8_t* d_
     return set_err(MG_E_UNSUPPORTED, "the first tier's eval kernel takes fewer than 2^30 candidates per call");
   uint32_t nblk = 0;
   void* args[] = {&d_soa, &n, &d_verdict, &d_watch, &nblk};
+  if (j.eval_cpb < 0) {
+    CodeObjectInfo ci;
+    std::string err;
+    j.eval_cpb = (!j.code.empty() && code_object_info(j.code.data(), j.code.size(), ci, err) == MG_OK) ? (int)ci.eval_cpb : 0;
+  }
+  if (j.eval_cpb > 0) {  // one group per workgroup, no loop: the grid covers every candidate
+    const uint64_t blocks = (n + (uint64_t)j.eval_cpb - 1) / (uint64_t)j.eval_cpb;
+    if (blocks > 0xFFFFFFFFull) return set_err(MG_E_UNSUPPORTED, "eval launch too wide for a loop-free kernel");
+    nblk = (uint32_t)blocks;
+    HIPCHK(hipEventRecord(e.ev0, e.stream));
+    HIPCHK(hipModuleLaunchKernel(j.feval, nblk, 1, 1, 256, 1, 1, 0, e.stream, args, nullptr));
+    HIPCHK(hipEventRecord(e.ev1, e.stream));
+    return launch_wait(e, e.stats, n);
+  }
   return jit_launch(e, j.feval, j.nb_eval, n, args, nblk);
 }
 

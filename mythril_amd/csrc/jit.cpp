@@ -539,10 +539,19 @@ struct Gen {
           } else {
             o << "    " << hdecl << "\n";
             // MYTHGPU_JIT_DICT_SPREAD=1 (diagnostic: WRONG verdicts): lane l of a 32-lane LDS group reads
-            // entry l, so the dictionary reads have no bank conflicts — what the conflicts cost
+            // entry l, so the dictionary reads have no bank conflicts — what the conflicts cost.  Taken
+            // only together with MYTHGPU_UNSAFE_DIAGNOSTICS=1 (a profiling run's explicit opt-in); the
+            // switch alone is ignored with a warning, so it cannot leak into a user's searches
             static const bool spread = [] {
               const char* g = getenv("MYTHGPU_JIT_DICT_SPREAD");
-              return g && g[0] == '1';
+              if (!(g && g[0] == '1')) return false;
+              const char* u = getenv("MYTHGPU_UNSAFE_DIAGNOSTICS");
+              if (u && u[0] == '1') {
+                fprintf(stderr, "mythgpu: MYTHGPU_JIT_DICT_SPREAD=1: O3 search kernels give WRONG verdicts (timing only)\n");
+                return true;
+              }
+              fprintf(stderr, "mythgpu: MYTHGPU_JIT_DICT_SPREAD ignored (needs MYTHGPU_UNSAFE_DIAGNOSTICS=1)\n");
+              return false;
             }();
             if (spread && sp.p[1] >= 32 && dict_lds.count(sp.p[0]))
               o << "    const uint32_t e = lane & 31u; (void)h;\n";
@@ -1141,11 +1150,12 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
     g.emit_prefetch("Gn");
   }
   o << "  for (uint32_t kk = 0u; kk < nk; kk++, gbase += gstride << 6) {\n"
+       "  uint64_t cu = ~0ull;  // the hit word as this group starts (early exit only)\n"
        "  if (early) {\n"
        "    // system scope when peers on other GPUs lower this word (MG_SEARCH_SYSTEM_SCOPE, mg_init)\n"
        "    const unsigned long long cur = (flags & 2u) ? __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)\n"
        "                                               : __hip_atomic_load(hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
-       "    const uint64_t cu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) | "
+       "    cu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cur >> 32)) << 32) | "
        "(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cur);\n"
        "    if (gbase >= cu) break;\n"
        "  }\n"
@@ -1178,7 +1188,8 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
        "        wave_best = first;\n"
        "        // publish at once when waves stop early on it (and to the devices whose slices lie above\n"
        "        // this one's: the peer line at hit + 272, engine.hip kPeerWord); else once per wave at the end\n"
-       "        if (early && lane == 0u) {\n"
+       "        // (a hit at or above the word read as the group started cannot lower it: no atomic)\n"
+       "        if (early && lane == 0u && first < cu) {\n"
        "          atomicMin(hit, (unsigned long long)first);\n"
        "          const uint32_t np = (uint32_t)hit[272];\n"
        "          for (uint32_t q = 0u; q < np && q < 15u; q++)\n"
@@ -2001,8 +2012,16 @@ int code_object_info(const void* code, size_t len, CodeObjectInfo& out, std::str
     if (noff >= b.size()) continue;
     const char* nm = (const char*)b.data() + noff;
     const size_t nl = strnlen(nm, b.size() - noff);
-    if (nl < 4 || std::strncmp(nm + nl - 3, ".kd", 3)) continue;
     const Elf64_Shdr& sec = sh[s.st_shndx];
+    if (nl == 17 && !std::strncmp(nm, "mgj_meta_eval_cpb", 17)) {  // jit_asm.cpp: the solo eval kernel's grid
+      if (s.st_value < sec.sh_addr || s.st_value + 4 > sec.sh_addr + sec.sh_size ||
+          !read_at(b, sec.sh_offset + (s.st_value - sec.sh_addr), out.eval_cpb)) {
+        err = "mgj_meta_eval_cpb outside its section";
+        return MG_E_INVALID;
+      }
+      continue;
+    }
+    if (nl < 4 || std::strncmp(nm + nl - 3, ".kd", 3)) continue;
     if (s.st_value < sec.sh_addr || s.st_value + 64 > sec.sh_addr + sec.sh_size) {
       err = "kernel descriptor outside its section";
       return MG_E_INVALID;

@@ -47,6 +47,7 @@ struct CodeObjectInfo {
   uint32_t max_private_bytes = 0;
   uint32_t max_group_bytes = 0;
   bool dynamic_stack = false;
+  uint32_t eval_cpb = 0;  // mgj_meta_eval_cpb: candidates per workgroup of a loop-free eval kernel (0: loops)
 };
 int code_object_info(const void* code, size_t len, CodeObjectInfo& out, std::string& err);
 // The load gate jit_compile applies to every code object, compiled or from the disk cache: a kernel

@@ -4956,12 +4956,20 @@ struct Gen {
     E.salu("s_lshr_b32 s3, s3, 6", {3});
     E.ctl("s_waitcnt lgkmcnt(0)");
     for (const auto& kv : pool) E.valu("v_mov_b32_e32 " + V((uint32_t)kv.second) + ", " + imm(kv.first));
-    // n * 4 (64-bit) in s[20:21]; the wave's first candidate s16 = block * 256 + wave * 64; stride s17
-    // (solo: s16 = block * 64, stride 64 per block, and waves 1..3 leave at once)
+    // n * 4 (64-bit) in s[20:21]; the wave's first candidate s16 = block * 256 + wave * 64; stride s17.
+    // Solo: waves 1..3 leave at once and wave 0 evaluates the ONE group s16 = block * 64 — no group
+    // loop: a solo kernel is tens of thousands of instructions (VMTests' expXY: 58 k), past the +-128 KiB
+    // a branch reaches — so the engine launches ceil(n / 64) blocks for it (mgj_meta_eval_cpb below,
+    // read by code_object_info); lanes past n store nothing, as in the loop
     E.salu("s_lshl_b64 s[20:21], s[8:9], 2", {20, 21});
     if (solo) {
+      const std::string go = E.newlab();
+      E.salu("s_cmp_eq_u32 s3, 0");
+      E.ctl("s_cbranch_scc1 " + go);
+      E.ctl("s_endpgm");
+      E.label(go);
       E.salu("s_lshl_b32 s16, s2, 6", {16});
-      E.salu("s_lshl_b32 s17, s14, 6", {17});
+      E.salu("s_mov_b32 s17, 64", {17});
     } else {
       E.salu("s_lshl_b32 s16, s2, 8", {16});
       E.salu("s_lshl_b32 s22, s3, 6", {22});
@@ -4970,10 +4978,6 @@ struct Gen {
     }
     E.salu("s_add_u32 s23, s8, -1", {23});  // n - 1
     const std::string loop = E.newlab(), exit_ = E.newlab();
-    if (solo) {
-      E.salu("s_cmp_lg_u32 s3, 0");
-      E.ctl("s_cbranch_scc1 " + exit_);
-    }
     // the ring: the first rows of the wave's first group, loaded before the loop
     ring_reg.clear();
     if (!glds)
@@ -4998,12 +5002,15 @@ struct Gen {
       E.salu("s_add_u32 s31, s31, -1", {31});
       E.salu("s_lshr_b32 s32, s17, 6", {32});
     }
-    E.salu("s_cmp_lt_u32 s16, s8");
-    E.ctl("s_cbranch_scc0 " + exit_);
+    if (!solo) {
+      E.salu("s_cmp_lt_u32 s16, s8");
+      E.ctl("s_cbranch_scc0 " + exit_);
+    }
     E.valu("v_add_u32_e32 v3, s16, v1", {16});
     if (tiled) {
       E.valu("v_lshlrev_b32_e32 v2, 2, v1");  // lane * 4 inside the group's 256-byte row
       E.salu("s_lshr_b32 s30, s16, 6", {30});
+      if (solo) E.salu("s_min_u32 s30, s30, s31", {30});  // a block past n reads the last group
       block_base(26, 30);
       page_at[0] = page_at[1] = -1;
     } else {
@@ -5013,9 +5020,11 @@ struct Gen {
     for (size_t q = 0; q < ring_reg.size(); q++) load_row(ring_reg[q], rows[q], 26, "v2", " (first group)");
     if (glds)
       for (size_t q = 0; q < gdepth; q++) glds_issue(q);  // the first group's first rows
-    E.label(loop);
-    E.salu("s_cmp_lt_u32 s16, s8");
-    E.ctl("s_cbranch_scc0 " + exit_);
+    if (!solo) {
+      E.label(loop);
+      E.salu("s_cmp_lt_u32 s16, s8");
+      E.ctl("s_cbranch_scc0 " + exit_);
+    }
     // i = s16 + lane; v3 = i (store offset), v2 = 4 * min(i, n - 1) (load offset: lanes past n reread
     // the last candidate and store nothing); s[24:25] = lanes with i < n; vnext: the same for i + stride
     // (tiled: v2 = 4 * lane, the blocks of this group and the next in s[26:27] / s[28:29]; the last
@@ -5023,6 +5032,7 @@ struct Gen {
     E.valu("v_add_u32_e32 v3, s16, v1", {16});
     if (tiled) {
       E.salu("s_lshr_b32 s30, s16, 6", {30});
+      if (solo) E.salu("s_min_u32 s30, s30, s31", {30});
       block_base(26, 30);
       E.salu("s_add_u32 s33, s30, s32", {33});
       E.salu("s_min_u32 s33, s33, s31", {33});
@@ -5063,8 +5073,10 @@ struct Gen {
     E.salu("s_mov_b64 exec, s[24:25]");
     E.mem("global_store_byte v3, v7, s[10:11]");
     E.salu("s_mov_b64 exec, -1");
-    E.salu("s_add_u32 s16, s16, s17", {16});
-    E.ctl("s_branch " + loop);
+    if (!solo) {
+      E.salu("s_add_u32 s16, s16, s17", {16});
+      E.ctl("s_branch " + loop);
+    }
     E.label(exit_);
     E.ctl("s_waitcnt vmcnt(0)");  // the last iteration's loads for a group past n
     E.ctl("s_endpgm");
@@ -5078,7 +5090,11 @@ struct Gen {
       << "    .amdhsa_next_free_vgpr " << nv << "\n    .amdhsa_next_free_sgpr " << ns << "\n"
       << "    .amdhsa_accum_offset " << accum << "\n    .amdhsa_reserve_vcc 1\n"
       << "    .amdhsa_float_denorm_mode_32 3\n    .amdhsa_float_denorm_mode_16_64 3\n"
-      << "  .end_amdhsa_kernel\n  .text\n";
+      << "  .end_amdhsa_kernel\n";
+    if (solo)  // candidates per workgroup of the loop-free solo kernel (engine: eval launch grid)
+      o << "  .globl mgj_meta_eval_cpb\n  .p2align 2\n  .type mgj_meta_eval_cpb,@object\nmgj_meta_eval_cpb:\n"
+           "  .long 64\n  .size mgj_meta_eval_cpb, 4\n";
+    o << "  .text\n";
     labels = E.nlab;
     meta_vgpr[name] = nv;
     meta_sgpr[name] = ns + 6;

@@ -384,14 +384,19 @@ def replay(code_hex: str, calldata: bytes = b"", pre_storage: Optional[Dict[int,
             if dest not in jumpdests:
                 raise ExceptionalHalt("bad jump")
             k = pc_index[dest]
-        elif op == 0x57:                             # JUMPI (:1523-1585)
-            target = _pop(stack)
-            c = branch(_pop(stack))
-            if c:  # the target is a decision only on the taken branch
-                dest = decide(target, "JUMPI target")
-                if dest not in jumpdests:
-                    raise ExceptionalHalt("bad jump")
-                k = pc_index[dest]
+        elif op == 0x57:                             # JUMPI (:1537-1585)
+            target = _as_bv(_pop(stack))
+            cond = _pop(stack)
+            # LASER reads the target with get_concrete_int first: a symbolic one raises TypeError and
+            # the JUMPI is skipped — pc + 1, no branch constraint, the condition never looked at
+            # ("Skipping JUMPI to invalid destination.", :1549-1555)
+            if target.value is not None:
+                c = branch(cond)
+                if c:
+                    dest = int(target.value)
+                    if dest not in jumpdests:
+                        raise ExceptionalHalt("bad jump")
+                    k = pc_index[dest]
         elif op == 0x58:                             # PC
             stack.append(BVV(pc, 256))
         elif op == 0x59:                             # MSIZE

@@ -440,6 +440,9 @@ JIT_ASM = os.environ.get("MYTHGPU_JIT_ASM", "1") != "0"
 # constraint sets) is picked up at once instead of after a full 10 ms interpreter launch
 JIT_POLL_S = 0.010
 JIT_FIRST_POLL_S = 0.001
+# the tier race (first tier against the O3 kernel on the same query): the first tier is kept only when
+# it is faster by more than this fraction
+RACE_TIE = 0.03
 # kernel that produced the last search's result ("interp" / "jit") and that result, for
 # stream statistics (tools/stream_bench.py)
 LAST_ENGINE = None
@@ -579,21 +582,27 @@ def search(engine, roots: Sequence[T.Term], seed: int = 0x6D797468, chunk: int =
                     idx, nh = engine.search(prog, gh, seed, start, n, early_exit=True, assign=assign)
                 dt = time.perf_counter() - tl
                 last_n = n
+                race_kept_asm = False
                 if race is not None and jh is not None and tier == "o3":
                     o3_rate = n / dt if dt > 0 else 0.0
-                    keep_asm = bool(race["asm_rate"]) and o3_rate < race["asm_rate"]
+                    # the O3 rate is its module's first launch (start-up costs in it) and the first tier's
+                    # came from another range: near-equal rates (within RACE_TIE) go to O3
+                    keep_asm = bool(race["asm_rate"]) and o3_rate * (1.0 + RACE_TIE) < race["asm_rate"]
                     timing["tier_race"] = {"asm_rate": race["asm_rate"], "o3_rate": o3_rate, "n": n,
                                            "kept": "asm" if keep_asm else "o3"}
                     if keep_asm:
                         engine.jit_free(jh)
                         jh, tier = race["asm"], "asm"
+                        race_kept_asm = True
                     else:
                         engine.jit_free(race["asm"])
                     race = None
                 if ticket_asm is not None:  # the launches the first tier's compile waited behind
                     timing["asm_wait_launches"] = timing.get("asm_wait_launches", 0) + 1
                     timing["asm_wait_launch_max_ms"] = max(timing.get("asm_wait_launch_max_ms", 0.0), dt * 1e3)
-                rate = n / dt if dt > 0 else None
+                # the next launch is sized by the kernel that runs it: the first tier's own rate when the
+                # race kept it (this launch's rate is the O3 kernel's)
+                rate = timing["tier_race"]["asm_rate"] if race_kept_asm else (n / dt if dt > 0 else None)
                 scanned += n
                 start += n
                 if idx is not None:

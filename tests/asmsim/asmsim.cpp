@@ -236,7 +236,8 @@ Module parse(const std::string& text) {
     if (t.back() == ':' && t.find(' ') == std::string::npos) {
       const std::string L = t.substr(0, t.size() - 1);
       labels[L] = (int)m.code.size();
-      if (L[0] != '.') m.kernels[L].entry = m.code.size();
+      // kernel entries; mgj_meta_* are data objects the engine reads (jit_asm.cpp: mgj_meta_eval_cpb)
+      if (L[0] != '.' && L.rfind("mgj_meta_", 0) != 0) m.kernels[L].entry = m.code.size();
       continue;
     }
     Ins ins;

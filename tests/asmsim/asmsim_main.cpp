@@ -350,7 +350,9 @@ std::string check_eval(const std::vector<uint8_t>& prog, uint64_t seed, uint32_t
     const uint64_t sb = mem.add(lay.size() * 4, lay.data());
     const uint64_t ver = mem.add(n);
     const uint64_t wb = sp.watch_words ? mem.add((size_t)sp.watch_words * n * 4) : 0;
-    const uint32_t nblk = grid(n);
+    // a loop-free solo kernel evaluates one 64-candidate group per workgroup (engine.hip mg_jit_eval_dev)
+    const bool one_group = src.find("mgj_meta_eval_cpb:") != std::string::npos;
+    const uint32_t nblk = one_group ? (uint32_t)((n + 63) / 64) : grid(n);
     std::vector<uint8_t> ka(64, 0);
     put64(ka, 0, sb);
     put64(ka, 8, n);

@@ -429,23 +429,27 @@ def test_asm_eval_readbacks_sim(sim):
     """Model read-back kernels (watch rows stored) against the C port's values row by row — every
     eleventh VMTests read-back plus the three whose 63 live 256-bit calldata keys need more LDS
     spill slots than four waves of a workgroup can hold (160 KiB): those run `solo`, one working
-    wave per workgroup with up to 639 lane-major slots (jit_asm.cpp, Gen::solo).  Until round 6
-    they went to the O3 tier (20-160 s of LLVM each)."""
+    wave per workgroup with up to 639 lane-major slots and one 64-candidate group per workgroup, no
+    group loop (jit_asm.cpp, Gen::solo), assembled and linked by comgr as well.  Until round 6 they
+    went to the O3 tier (20-160 s of LLVM each)."""
     from mythril_amd import native
 
     progs = _vmtest_readbacks(every=11) + _vmtest_readbacks(names=READBACK_SOLO)
     assert len(progs) >= 30
     solo = 0
     for name, pb in progs:
-        src = native.jit_asm(pb, None)  # inside the tier: no EngineUnsupported
+        # inside the tier (no EngineUnsupported); the solo kernels also through comgr's assembler and
+        # linker and the load gate (a 58 k-instruction kernel: no branch may span it)
+        src = native.jit_asm(pb, None, compile=name in READBACK_SOLO)
         if name in READBACK_SOLO:
-            assert "s_cmp_lg_u32 s3, 0" in src and "ds_write_b32" in src, name
+            assert "mgj_meta_eval_cpb:" in src and "ds_write_b32" in src, name
             lds = int(src.split(".amdhsa_group_segment_fixed_size ")[1].split()[0])
             assert 160 * 256 < lds <= 160 * 1024, (name, lds)  # past four waves' share, inside the CU's LDS
             solo += 1
     assert solo == 3
     rng = random.Random(17)
-    recs = [record(1 + (i & 1), pb, None, rng.getrandbits(32), 0, 64 * 2 + 5) for i, (_, pb) in enumerate(progs)]
+    recs = [record(1 + (i & 1), pb, None, rng.getrandbits(32), 0, 64 * 2 + 5, flags=int(name in READBACK_SOLO))
+            for i, (name, pb) in enumerate(progs)]
     rc, summary, bad, err = run_sim(sim, b"".join(recs), {"MYTHGPU_JIT_ASM_CHECK": "1"})
     assert rc == 0 and summary, f"{summary}\n" + "\n".join(bad[:5]) + "\n" + err[-3000:]
     assert int(summary["ok"]) == len(recs), (summary, bad[:5])

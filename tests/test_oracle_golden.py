@@ -101,3 +101,21 @@ def test_jumpi_path_constraint_is_lasers():
         assert evaluate(c, m) == 1
         other = OracleModel({"calldatasize": 32}, {"calldata": ({31: 0 if taken else 9}, 0)})
         assert evaluate(c, other) == 0  # the constraint is the branch, not the concrete value
+
+
+def test_jumpi_symbolic_target_is_skipped_as_laser_does():
+    """A JUMPI whose target is input-dependent is skipped with no branch constraint, as LASER's
+    ``jumpi_`` does when ``get_concrete_int`` raises (``instructions.py:1549-1555``): execution
+    falls through whatever the condition.  Code: CALLDATALOAD(0) as the target, condition 1, then
+    SSTORE(0, 1) on the fall-through path, and a JUMPDEST at 12 that the target would reach."""
+    from mythril_amd.replay import replay
+
+    # PUSH1 1 PUSH1 0 CALLDATALOAD JUMPI PUSH1 1 PUSH1 0 SSTORE STOP JUMPDEST STOP
+    code = "6001600035576001600055005b00"
+    for word in (12, 0, 7):
+        data = word.to_bytes(32, "big")
+        arrs = {"calldata": ({i: b for i, b in enumerate(data)}, 0)}
+        m = OracleModel({"calldatasize": 32}, arrs)
+        r = replay(code, data, follow=lambda t, m=m: evaluate(t, m))
+        assert r.path == [], r.path
+        assert evaluate(r.storage_word(0).raw, m) == 1  # fell through to the SSTORE
