@@ -23,8 +23,11 @@
 //    write of every such SGPR;
 //  * no scalar stores and no scalar-cache writes anywhere: results leave through vector atomics.
 //
-// Programs outside this tier (division, EXP, Keccak, variable shifts, UMUL_NOOVF, values wider
-// than 2048 bits) get MG_E_UNSUPPORTED and stay with the interpreter until the O3 kernel is ready.
+// The tier covers LASER's whole vocabulary (round 5: symbolic UDIV/UREM/SDIV/SREM/SMOD, variable
+// shifts, EXP, Keccak-256, UMUL_NOOVF).  What it still refuses (MG_E_UNSUPPORTED: the search stays
+// on the interpreter until the O3 kernel is ready, an eval goes to the O3 kernel) is a kernel whose
+// live values do not fit 256 VGPRs plus the LDS spill slots of one wave (Gen::spill_one, `solo`),
+// and values wider than the limb bound (kMaxLimbs).
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
