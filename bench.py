@@ -391,15 +391,15 @@ def main():
         # tiled SoA (MG_JIT_SOA_TILED: a group's rows in one block)
         # (tiled SoA: a group's rows in one block); then the tier the engine picks when none is named
         # (mg_jit_compile_ex without MG_JIT_ASM / MG_JIT_O3: what batched Model.eval gets by default)
-        for tier in ("o3", "asm", "default"):
+        for etier in ("o3", "asm", "default"):
             for tiled in (False, True):
                 for w in EVAL_WORKLOADS:
                     try:
                         evals.append(eval_roofline(eng, torch, w, args.eval_candidates, args.pmc_dir, tiled=tiled,
-                                                   tier=tier))
+                                                   tier=etier))
                     except native.EngineUnsupported as e:
-                        evals.append({"workload": CONFIG_OF[w], "tier_requested": tier,
-                                      "kernel": eval_kernel_name(tier == "asm", tiled), "unsupported": str(e)})
+                        evals.append({"workload": CONFIG_OF[w], "tier_requested": etier,
+                                      "kernel": eval_kernel_name(etier == "asm", tiled), "unsupported": str(e)})
 
     # CPU baseline: the C restatement over a bounded sample of the same candidates
     cpu = None
