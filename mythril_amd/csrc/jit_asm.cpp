@@ -395,6 +395,8 @@ struct Gen {
     };
     if (eval_kernel && greedy_on()) {
       greedy_roots(v, operands, done, visit);
+    } else if (!eval_kernel && heavy_last_on()) {
+      heavy_last_roots(v, operands, done, visit);
     } else {
       for (size_t k = 0; k < v.size(); k++)
         if (v[k].op == K_ASSERT || v[k].op == K_WATCH) visit((int32_t)k);
@@ -402,6 +404,82 @@ struct Gen {
     for (size_t k = 0; k < v.size(); k++)
       if (!done[k]) visit((int32_t)k);
     code.swap(out);
+  }
+  // Search kernels: constraints whose not-yet-emitted cone is heavy (Keccak, EXP, division: hundreds
+  // to thousands of VALU per candidate) go after the light ones.  The early exit after each ASSERT
+  // (an early-exit search's wave leaves once all 64 of its candidates failed) then skips the heavy
+  // work of most rejected groups: a query whose cheap constraint rejects most candidates ahead of a
+  // Keccak (bench's C5 hard query: the ~2^-8 needle behind two Keccak-f[1600]) no longer pays the
+  // Keccaks for them.  Light constraints keep program order; the heavy ones follow, cheapest
+  // remaining cone first.  Verdicts do not depend on the order; a full-evaluation launch (no early
+  // exit) does the same work in another order.  MYTHGPU_JIT_ASM_HEAVY_LAST=0: program order.
+  static bool heavy_last_on() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_HEAVY_LAST");
+      return !(g && g[0] == '0');
+    }();
+    return on;
+  }
+  // rough VALU per candidate of one instruction (only to tell heavy cones from light ones)
+  uint32_t op_weight(const Instr& in) const {
+    const uint32_t w = (in.dst != MG_NONE && in.dst < P.vwidth.size()) ? P.vwidth[in.dst] : 32u;
+    const uint32_t L = std::max(1u, Lw(std::max(w, in.op >= K_EQ && in.op <= K_UMUL_NOOVF ? in.p1 : w)));
+    switch (in.op) {
+      case K_KECCAK: return 2500u * (in.p0 / 136u + 1u);
+      case K_EXP: return 1500u;
+      case K_UDIV: case K_UREM: case K_SDIV: case K_SREM: case K_SMOD: return 600u;
+      case K_MUL: return 4u * L * L;
+      case K_UMUL_NOOVF: return 8u * L * L;
+      case K_SHL: case K_LSHR: case K_ASHR: return 4u * L;
+      case K_LOOKUP: return 2u * Lw(in.b) * std::max(1u, in.c);
+      case K_COORD: return 8u * L;
+      default: return L;
+    }
+  }
+  static constexpr uint32_t kHeavyCone = 400;
+  template <class Ops, class Visit>
+  void heavy_last_roots(const std::vector<Instr>& v, Ops& operands, const std::vector<char>& done, Visit& visit) {
+    std::vector<int32_t> roots;
+    for (size_t k = 0; k < v.size(); k++)
+      if (v[k].op == K_ASSERT) roots.push_back((int32_t)k);
+    std::vector<int32_t> mark(v.size(), -1), st, ops;
+    int32_t stamp = 0;
+    auto cone_cost = [&](int32_t r) -> uint64_t {  // the not-yet-emitted cone of r
+      uint64_t c = 0;
+      st.assign(1, r);
+      mark[r] = ++stamp;
+      while (!st.empty()) {
+        const int32_t x = st.back();
+        st.pop_back();
+        c += op_weight(v[x]);
+        operands(v[x], ops);
+        for (int32_t o : ops)
+          if (!done[o] && mark[o] != stamp) {
+            mark[o] = stamp;
+            st.push_back(o);
+          }
+      }
+      return c;
+    };
+    std::vector<char> taken(roots.size(), 0);
+    for (size_t step = 0; step < roots.size(); step++) {
+      size_t pick = roots.size();
+      uint64_t best = UINT64_MAX;
+      for (size_t i = 0; i < roots.size(); i++) {
+        if (taken[i]) continue;
+        const uint64_t c = cone_cost(roots[i]);
+        if (c < kHeavyCone) {  // the first light constraint in program order
+          pick = i;
+          break;
+        }
+        if (c < best) {
+          best = c;
+          pick = i;
+        }
+      }
+      taken[pick] = 1;
+      visit(roots[pick]);
+    }
   }
   // MYTHGPU_JIT_ASM_GREEDY=1: the eval kernel's constraints in greedy order (below).  Opt-in: it lowers
   // C4's cache-free peak (238 -> 208 VGPRs) but the kernel's time did not move (the caches fill the
