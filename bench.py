@@ -404,7 +404,7 @@ def main():
     # CPU baseline: the C restatement over a bounded sample of the same candidates
     cpu = None
     if rank == 0 and world == 1 and inproc == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(P, blob, args, eng, prog, gh, jit)
+        cpu = cpu_baseline(P, blob, args, eng, prog, gh, jit, tier)
 
     if rank == 0:
         total = world * inproc * C * args.steps
@@ -584,7 +584,7 @@ def hard_query(cs, bits: int = 24):
     return [c.raw for c in cs] + [needle.raw]
 
 
-def cpu_baseline(P, blob, args, eng, prog, gh, jit=None):
+def cpu_baseline(P, blob, args, eng, prog, gh, jit=None, tier=None):
     from oracle import cport
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
@@ -600,6 +600,19 @@ def cpu_baseline(P, blob, args, eng, prog, gh, jit=None):
     g_first, g_hits = eng.search(prog, gh, args.seed, start, n, early_exit=False)
     if jit is not None:
         assert eng.jit_search(jit, args.seed, start, n, early_exit=False) == (g_first, g_hits)
+    # per-candidate verdicts on the first 2^16 of the window: the timed tier's own kernels built with
+    # mgj_gen (one verdict byte per candidate) against the C port's, byte for byte
+    nv = min(n, 1 << 16)
+    _, _, want = cport.search(P.to_bytes(), blob, args.seed, start, nv, threads=threads, verdicts=True)
+    if tier in ("asm", "o3"):
+        jv = eng.jit_compile(prog, gh, gen_verdicts=True, asm=tier == "asm")
+        try:
+            got = eng.jit_verdicts(jv, args.seed, start, nv)
+        finally:
+            eng.jit_free(jv)
+    else:
+        got, _ = eng.eval_generated(prog, gh, args.seed, start, nv)
+    per_candidate = bool(np.array_equal(np.asarray(got, dtype=np.uint8), np.asarray(want, dtype=np.uint8)))
     return {
         "value": n / dt,
         "unit": "candidate assignments/s",
@@ -607,6 +620,9 @@ def cpu_baseline(P, blob, args, eng, prog, gh, jit=None):
         "kind": "port",
         "sample": f"{n} candidates [{start}, {start + n}) of the same workload/seed; {dt:.1f} s",
         "agrees_with_gpu": bool(first == g_first and hits == g_hits),
+        "verdicts_checked": nv,
+        "verdicts_agree": per_candidate,
+        "verdicts_kernel": f"mgj_gen ({tier} tier)" if tier in ("asm", "o3") else "k_run (interpreter)",
     }
 
 

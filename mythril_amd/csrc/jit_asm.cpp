@@ -405,8 +405,8 @@ struct Gen {
       if (!done[k]) visit((int32_t)k);
     code.swap(out);
   }
-  // Search kernels: constraints whose not-yet-emitted cone is heavy (Keccak, EXP, division: hundreds
-  // to thousands of VALU per candidate) go after the light ones.  The early exit after each ASSERT
+  // Search kernels: constraints whose not-yet-emitted cone holds a heavy operator (Keccak, EXP,
+  // division: hundreds to thousands of VALU per candidate) go after the light ones.  The early exit after each ASSERT
   // (an early-exit search's wave leaves once all 64 of its candidates failed) then skips the heavy
   // work of most rejected groups: a query whose cheap constraint rejects most candidates ahead of a
   // Keccak (bench's C5 hard query: the ~2^-8 needle behind two Keccak-f[1600]) no longer pays the
@@ -420,7 +420,7 @@ struct Gen {
     }();
     return on;
   }
-  // rough VALU per candidate of one instruction (only to tell heavy cones from light ones)
+  // rough VALU per candidate of one instruction (to order the heavy cones, cheapest first)
   uint32_t op_weight(const Instr& in) const {
     const uint32_t w = (in.dst != MG_NONE && in.dst < P.vwidth.size()) ? P.vwidth[in.dst] : 32u;
     const uint32_t L = std::max(1u, Lw(std::max(w, in.op >= K_EQ && in.op <= K_UMUL_NOOVF ? in.p1 : w)));
@@ -436,7 +436,9 @@ struct Gen {
       default: return L;
     }
   }
-  static constexpr uint32_t kHeavyCone = 400;
+  static bool heavy_op(uint32_t op) {
+    return op == K_KECCAK || op == K_EXP || op == K_UDIV || op == K_UREM || op == K_SDIV || op == K_SREM || op == K_SMOD;
+  }
   template <class Ops, class Visit>
   void heavy_last_roots(const std::vector<Instr>& v, Ops& operands, const std::vector<char>& done, Visit& visit) {
     std::vector<int32_t> roots;
@@ -444,14 +446,16 @@ struct Gen {
       if (v[k].op == K_ASSERT) roots.push_back((int32_t)k);
     std::vector<int32_t> mark(v.size(), -1), st, ops;
     int32_t stamp = 0;
-    auto cone_cost = [&](int32_t r) -> uint64_t {  // the not-yet-emitted cone of r
+    auto cone_cost = [&](int32_t r, bool& heavy) -> uint64_t {  // the not-yet-emitted cone of r
       uint64_t c = 0;
+      heavy = false;
       st.assign(1, r);
       mark[r] = ++stamp;
       while (!st.empty()) {
         const int32_t x = st.back();
         st.pop_back();
         c += op_weight(v[x]);
+        heavy = heavy || heavy_op(v[x].op);
         operands(v[x], ops);
         for (int32_t o : ops)
           if (!done[o] && mark[o] != stamp) {
@@ -467,8 +471,9 @@ struct Gen {
       uint64_t best = UINT64_MAX;
       for (size_t i = 0; i < roots.size(); i++) {
         if (taken[i]) continue;
-        const uint64_t c = cone_cost(roots[i]);
-        if (c < kHeavyCone) {  // the first light constraint in program order
+        bool heavy = false;
+        const uint64_t c = cone_cost(roots[i], heavy);
+        if (!heavy) {  // the first light constraint in program order
           pick = i;
           break;
         }
