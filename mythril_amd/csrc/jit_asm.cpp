@@ -105,7 +105,8 @@ std::string VP(uint32_t r) { return "v[" + std::to_string(r) + ":" + std::to_str
 //        s[12:13] sk, s[14:15] sg, s[16:17] hit / verdict_out, s18 flags, s19 nblk, s[20:21] a0,
 //        s[22:23] end, s[24:25] ngroups, s[26:27] g, s28 gstride, s29 early, s[30:31] wave best,
 //        s[32:33] wave hits, s[34:35] gbase, s[36:37] G, s[38:39] verdict, s[40:41] temps,
-//        s[42:43] ~0 unless the launch stops early, s6 the group is full, s7 temp; pairs s[44:45] ..
+//        s[42:43] ~0 unless the launch stops early, s[10:11] / s[12:13] the call's partial first / last
+//        group base (after the prologue), s7 temp; pairs s[44:45] ..
 //        s[98:99] allocated
 constexpr int kV0 = 10;
 constexpr int kS0 = 44, kS1 = 100;
@@ -5254,6 +5255,18 @@ struct Gen {
     E.valu("v_xor_b32_e32 v2, s12, v1", {12});
     E.valu("v_mov_b32_e32 v3, s13", {13});
     vfmix(2, 3);
+    // the call's partial groups, by base (count and sk are dead from here): s[10:11] = the first group's
+    // base when start is not group-aligned, s[12:13] = the last group's when end is not, else ~0 — a
+    // group is partial iff its base equals one of them (two 64-bit compares at its end instead of nine
+    // SALU of bounds arithmetic per group)
+    E.salu("s_and_b32 s12, s22, 0xffffffc0", {12});
+    E.salu("s_mov_b32 s13, s23", {13});
+    E.salu("s_and_b32 s40, s22, 63", {40});
+    E.salu("s_cmp_lg_u32 s40, 0");
+    E.salu("s_cselect_b64 s[12:13], s[12:13], -1", {12, 13});
+    E.salu("s_and_b32 s40, s8, 63", {40});
+    E.salu("s_cmp_lg_u32 s40, 0");
+    E.salu("s_cselect_b64 s[10:11], s[20:21], -1", {10, 11});
     const std::string loop = E.newlab(), exit_ = E.newlab(), next = E.newlab(), cont = E.newlab();
     E.label(loop);
     // g < ngroups ?
@@ -5288,16 +5301,6 @@ struct Gen {
       E.ctl("s_cbranch_scc0 " + exit_);
       E.label(noearly);
     }
-    // full group (s6): gbase >= start and gbase + 64 <= end
-    E.salu("s_sub_u32 s40, s34, s8", {40});
-    E.salu("s_subb_u32 s40, s35, s9", {40});
-    E.salu("s_cselect_b32 s41, 0, 1", {41});
-    E.salu("s_add_u32 s40, s34, 64", {40});
-    E.salu("s_addc_u32 s7, s35, 0", {7});
-    E.salu("s_sub_u32 s40, s22, s40", {40});
-    E.salu("s_subb_u32 s40, s23, s7", {40});
-    E.salu("s_cselect_b32 s40, 0, 1", {40});
-    E.salu("s_and_b32 s6, s41, s40", {6});
     // G = fmix64((gbase >> 6) ^ sg)
     E.salu("s_lshr_b64 s[36:37], s[34:35], 6", {36, 37});
     E.salu("s_xor_b64 s[36:37], s[36:37], s[14:15]", {36, 37});
@@ -5312,9 +5315,12 @@ struct Gen {
     // m = verdict, restricted to [start, end) in a partial group
     E.salu("s_mov_b64 s[40:41], s[38:39]", {40, 41});
     {
-      const std::string fullg = E.newlab();
-      E.salu("s_cmp_eq_u32 s6, 0");
-      E.ctl("s_cbranch_scc0 " + fullg);
+      const std::string fullg = E.newlab(), part = E.newlab();
+      E.salu("s_cmp_eq_u64 s[34:35], s[10:11]");
+      E.ctl("s_cbranch_scc1 " + part);
+      E.salu("s_cmp_lg_u64 s[34:35], s[12:13]");
+      E.ctl("s_cbranch_scc1 " + fullg);
+      E.label(part);
       E.valu("v_add_co_u32_e32 v8, vcc, s34, v1", {34}, {kVCC, kVCC + 1});
       E.valu("v_mov_b32_e32 v9, s35", {35});
       E.valu("v_addc_co_u32_e32 v9, vcc, 0, v9, vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
@@ -5347,17 +5353,18 @@ struct Gen {
       E.mem("global_store_byte v[8:9], v7, off");
       E.salu("s_mov_b64 exec, -1");
     } else {
+      // a wave sweeps its groups in increasing index order, so its first group with a hit holds its
+      // best: later groups only count (bcnt) — no first-lane search and no 64-bit compare with the best
       E.salu("s_cmp_eq_u64 s[40:41], 0");
       E.ctl("s_cbranch_scc1 " + cont);
-      E.salu("s_ff1_i32_b64 s44, s[40:41]", {44});
       E.salu("s_bcnt1_i32_b64 s45, s[40:41]", {45});
       E.salu("s_add_u32 s32, s32, s45", {32});
       E.salu("s_addc_u32 s33, s33, 0", {33});
+      E.salu("s_cmp_lg_u64 s[30:31], -1");
+      E.ctl("s_cbranch_scc1 " + cont);
+      E.salu("s_ff1_i32_b64 s44, s[40:41]", {44});
       E.salu("s_add_u32 s46, s34, s44", {46});
       E.salu("s_addc_u32 s47, s35, 0", {47});
-      E.salu("s_sub_u32 s44, s46, s30", {44});
-      E.salu("s_subb_u32 s44, s47, s31", {44});
-      E.ctl("s_cbranch_scc0 " + cont);
       E.salu("s_mov_b64 s[30:31], s[46:47]", {30, 31});
       E.salu("s_cmp_eq_u32 s29, 0");
       E.ctl("s_cbranch_scc1 " + cont);
