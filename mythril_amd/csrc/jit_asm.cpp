@@ -193,8 +193,10 @@ class Emitter {
     o << "  " << s << "\n";
   }
   std::string newlab() { return ".Lm" + std::to_string(nlab++); }
+  int label_events = 0;  // labels emitted so far: SGPR state tracked at emission time is void past one
   void label(const std::string& L) {
     lds_flush();
+    label_events++;
     o << L << ":\n";
     for (auto& kv : vw) kv.second = std::max(kv.second, pos - 1);
   }
@@ -4845,14 +4847,41 @@ struct Gen {
   std::vector<long> row_seq;
   long loads = 0;
 
-  // s[dst:dst+1] (here s[40:41]) = base s[b:b+1] + row * n * 4 (n * 4 in s[14:15]... kept as s20 low / s21 high)
+  // s[40:41] = base s[b:b+1] + row * n * 4 (n * 4 in s[20:21]: below 2^32, the first tier's eval kernel
+  // takes n < 2^30, so s21 = 0 and one 32 x 32 -> 64 product is the whole offset)
   void row_ptr(uint32_t row, int b) {
     E.salu("s_mul_i32 s40, s20, " + hexs(row), {40});
     E.salu("s_mul_hi_u32 s41, s20, " + hexs(row), {41});
-    E.salu("s_mul_i32 s42, s21, " + hexs(row), {42});
-    E.salu("s_add_u32 s41, s41, s42", {41});
     E.salu("s_add_u32 s40, s40, " + S(b), {40});
     E.salu("s_addc_u32 s41, s41, " + S(b + 1), {41});
+  }
+  // Row-major loads keep the last loaded row's pointer (soa + row * n * 4, the same for every group) in
+  // s[100:101]: the next row is one add away when it follows it (rows are mostly read in order), two
+  // products and an add otherwise.  Valid until a label (a loop head or a join) is emitted.
+  int64_t rp_row = -1;
+  int rp_lab = -1;
+  bool rp_used = false;
+  void row_ptr_rm(uint32_t row) {
+    const bool have = rp_row >= 0 && rp_lab == E.label_events;
+    if (have && (int64_t)row == rp_row) {
+    } else if (have && (int64_t)row == rp_row + 1) {
+      E.salu("s_add_u32 s100, s100, s20", {100});
+      E.salu("s_addc_u32 s101, s101, 0", {101});
+    } else if (have && (int64_t)row > rp_row) {
+      const uint32_t dl = (uint32_t)(row - rp_row);
+      E.salu("s_mul_i32 s40, s20, " + hexs(dl), {40});
+      E.salu("s_mul_hi_u32 s41, s20, " + hexs(dl), {41});
+      E.salu("s_add_u32 s100, s100, s40", {100});
+      E.salu("s_addc_u32 s101, s101, s41", {101});
+    } else {
+      E.salu("s_mul_i32 s100, s20, " + hexs(row), {100});
+      E.salu("s_mul_hi_u32 s101, s20, " + hexs(row), {101});
+      E.salu("s_add_u32 s100, s100, s4", {100});
+      E.salu("s_addc_u32 s101, s101, s5", {101});
+    }
+    rp_row = row;
+    rp_lab = E.label_events;
+    rp_used = true;
   }
   // the load of SoA row `row` of the group whose block base is s[b:b+1] (tiled) or of the candidates
   // at offsets `voff` (row-major: s[4:5] + row * n * 4)
@@ -4875,8 +4904,8 @@ struct Gen {
       E.mem("global_load_dword " + VL(d) + ", v2, " + base + " offset:" + std::to_string(byte & 4095u) +
             "  ; soa row " + std::to_string(row) + note);
     } else {
-      row_ptr(row, 4);
-      E.mem("global_load_dword " + VL(d) + ", " + voff + ", s[40:41]  ; soa row " + std::to_string(row) + note);
+      row_ptr_rm(row);
+      E.mem("global_load_dword " + VL(d) + ", " + voff + ", s[100:101]  ; soa row " + std::to_string(row) + note);
     }
   }
   // s[d:d+1] = soa + g * coord_words * 256 for the group index in s[g]
@@ -5011,6 +5040,9 @@ struct Gen {
 
   std::string kernel_eval(const std::string& name) {
     E = Emitter();
+    rp_row = -1;
+    rp_lab = -1;
+    rp_used = false;
     E.vhard = vhard;
     E.nlab = labels;
     E.vsoft = vsoft;
@@ -5167,7 +5199,7 @@ struct Gen {
     E.label(exit_);
     E.ctl("s_waitcnt vmcnt(0)");  // the last iteration's loads for a group past n
     E.ctl("s_endpgm");
-    const int nv = std::max(E.vhigh, kV0), ns = std::max(E.shigh, 56);
+    const int nv = std::max(E.vhigh, kV0), ns = std::max(E.shigh, rp_used ? 102 : 56);
     const int accum = (nv + 3) / 4 * 4;
     o << "  .section .rodata,\"a\",@progbits\n  .p2align 6, 0x0\n  .amdhsa_kernel " << name << "\n"
       << "    .amdhsa_group_segment_fixed_size " << eval_lds_bytes() << "\n    .amdhsa_private_segment_fixed_size 0\n"

@@ -1,7 +1,8 @@
 """Instructions per candidate of the first tier's eval kernel (mgj_eval, tiled SoA, no watch rows: the
 kernel bench.py's roofline_eval runs) on the CPU simulator, optionally per program instruction.
 
-  python tools/eval_count.py [workload ...] [K=V ...]     (MYTHGPU_JIT_ASM_ANNOTATE=1: per instruction)"""
+  python tools/eval_count.py [workload ...] [K=V ...]     (MYTHGPU_JIT_ASM_ANNOTATE=1: per instruction;
+                                                          EVAL_LAYOUT=rowmajor: the [row][candidate] SoA)"""
 import os
 import subprocess
 import sys
@@ -32,7 +33,8 @@ def main():
     for name in names or ["token_transfer_underflow", "walletlibrary_kill"]:
         P, _ = search.prepare([c.raw for c in workloads.WORKLOADS[name]()])
         P.set_watch([])
-        r = subprocess.run([str(exe)], input=record(2, P.to_bytes(), None, 7, 0, 64 * 32), capture_output=True,
+        kind = 1 if env.get("EVAL_LAYOUT") == "rowmajor" else 2  # record kind 1: row-major SoA, 2: tiled
+        r = subprocess.run([str(exe)], input=record(kind, P.to_bytes(), None, 7, 0, 64 * 32), capture_output=True,
                            env=env)
         out = r.stdout.decode()
         tags = []
