@@ -100,15 +100,16 @@ std::string VP(uint32_t r) { return "v[" + std::to_string(r) + ":" + std::to_str
 
 // fixed registers
 // VGPRs: v0 tid, v1 lane, v2/v3 lane key (lo/hi), v4/v5 group-lane key K (lo/hi), v6 zero, v7 scratch,
-//        v[8:9] 64-bit scratch; the allocator hands out v10 and up
+//        v[8:9] 64-bit scratch, v10/v11 the group keys of the wave's next 64 groups (search kernels:
+//        lane l holds G of the l-th, lo/hi); the allocator hands out v12 and up
 // SGPRs: s[0:1] kernarg, s2 block id, s3 wave in block, s[4:5] gconsts, s[8:9] start, s[10:11] count,
 //        s[12:13] sk, s[14:15] sg, s[16:17] hit / verdict_out, s18 flags, s19 nblk, s[20:21] a0,
 //        s[22:23] end, s[24:25] ngroups, s[26:27] g, s28 gstride, s29 early, s[30:31] wave best,
 //        s[32:33] wave hits, s[34:35] gbase, s[36:37] G, s[38:39] verdict, s[40:41] temps,
 //        s[42:43] ~0 unless the launch stops early, s[10:11] / s[12:13] the call's partial first / last
-//        group base (after the prologue), s7 temp; pairs s[44:45] ..
+//        group base (after the prologue), s7 the next group's lane in v10/v11; pairs s[44:45] ..
 //        s[98:99] allocated
-constexpr int kV0 = 10;
+constexpr int kV0 = 12;
 constexpr int kS0 = 44, kS1 = 100;
 
 class Emitter {
@@ -5299,6 +5300,7 @@ struct Gen {
     E.salu("s_and_b32 s40, s8, 63", {40});
     E.salu("s_cmp_lg_u32 s40, 0");
     E.salu("s_cselect_b64 s[10:11], s[20:21], -1", {10, 11});
+    E.salu("s_movk_i32 s7, 0x40", {7});  // the group-key table is due at the first group
     const std::string loop = E.newlab(), exit_ = E.newlab(), next = E.newlab(), cont = E.newlab();
     E.label(loop);
     // g < ngroups ?
@@ -5333,10 +5335,30 @@ struct Gen {
       E.ctl("s_cbranch_scc0 " + exit_);
       E.label(noearly);
     }
-    // G = fmix64((gbase >> 6) ^ sg)
-    E.salu("s_lshr_b64 s[36:37], s[34:35], 6", {36, 37});
-    E.salu("s_xor_b64 s[36:37], s[36:37], s[14:15]", {36, 37});
-    sfmix(36);
+    // G = fmix64((gbase >> 6) ^ sg), gbase >> 6 = (a0 >> 6) + g.  Every 64 groups the wave computes the
+    // keys of its next 64 on the VALU (lane l: group g + l * gstride) into v10/v11, and each group reads
+    // its own with two v_readlane: 18 SALU per group (fmix64 on the scalar unit, 8 of them multiplies)
+    // become 2 VALU + ~0.4 amortised
+    {
+      const std::string have = E.newlab();
+      E.salu("s_cmp_lt_u32 s7, 64");
+      E.ctl("s_cbranch_scc1 " + have);
+      E.valu("v_mul_u32_u24_e32 v10, s28, v1", {28});
+      E.valu("v_lshrrev_b64 v[8:9], 6, s[20:21]", {20, 21});
+      E.valu("v_add_co_u32_e32 v10, vcc, s26, v10", {26}, {kVCC, kVCC + 1});
+      E.valu("v_mov_b32_e32 v11, s27", {27});
+      E.valu("v_addc_co_u32_e32 v11, vcc, 0, v11, vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
+      E.valu("v_add_co_u32_e32 v10, vcc, v8, v10", {}, {kVCC, kVCC + 1});
+      E.valu("v_addc_co_u32_e32 v11, vcc, v9, v11, vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
+      E.valu("v_xor_b32_e32 v10, s14, v10", {14});
+      E.valu("v_xor_b32_e32 v11, s15, v11", {15});
+      vfmix(10, 11);
+      E.salu("s_mov_b32 s7, 0", {7});
+      E.label(have);
+      E.valu("v_readlane_b32 s36, v10, s7", {7}, {36});
+      E.valu("v_readlane_b32 s37, v11, s7", {7}, {37});
+      E.salu("s_add_u32 s7, s7, 1", {7});
+    }
     E.valu("v_xor_b32_e32 v4, s36, v2", {36});
     E.valu("v_xor_b32_e32 v5, s37, v3", {37});
     E.salu("s_mov_b64 s[38:39], -1", {38, 39});
