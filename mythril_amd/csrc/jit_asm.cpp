@@ -4244,12 +4244,22 @@ struct Gen {
             set_mask(d, x);
             break;
           }
+          // (c & b) | (e & ~c): the else side in one s_andn2_b64 (a literal else folds)
           const Mask t = mop("and", c, mask_of(in.b));
-          const Mask nc = mnot(c);
-          const Mask f = mop("and", nc, mask_of(in.c));
+          const Mask e = mask_of(in.c);
+          Mask f;
+          if (e.k == 1) {
+            if (e.ones) {
+              f = mnot(c);
+            } else {
+              f.k = 1;
+              f.ones = false;
+            }
+          } else {
+            f = mop_andn(e, c);
+          }
           set_mask(d, mop("or", t, f));
           E.srelease(t);
-          E.srelease(nc);
           E.srelease(f);
           break;
         }
@@ -4397,11 +4407,32 @@ struct Gen {
               }
               continue;
             }
-            const Mask t = mop("and", h, mask_of(vv));
-            const Mask f = mop_andn(cur, h);
-            const Mask nc = mop("or", t, f);
-            E.srelease(t);
-            E.srelease(f);
+            // nc = h ? v : cur = (h & v) | (cur & ~h), one SALU when either side is a literal (the first
+            // select of the compare pushdown's chain meets its default 1: v | ~h, one s_orn2_b64)
+            const Mask vm = mask_of(vv);
+            Mask nc;
+            if (cur.k == 1 && !cur.ones) {
+              nc = mop("and", h, vm);
+            } else if (cur.k == 1 && vm.k == 2) {
+              nc.k = 2;
+              nc.s = E.salloc();
+              E.salu("s_orn2_b64 " + SP(nc.s) + ", " + SP(vm.s) + ", " + SP(h.s), {nc.s, nc.s + 1});
+            } else if (cur.k == 1) {  // both literal, cur true: v ? 1 : ~h
+              if (vm.ones) {
+                nc.k = 1;
+                nc.ones = true;
+              } else {
+                nc = mnot(h);
+              }
+            } else if (vm.k == 1) {
+              nc = vm.ones ? mop("or", h, cur) : mop_andn(cur, h);
+            } else {
+              const Mask t = mop("and", h, vm);
+              const Mask f = mop_andn(cur, h);
+              nc = mop("or", t, f);
+              E.srelease(t);
+              E.srelease(f);
+            }
             E.srelease(cur);
             E.srelease(h);
             cur = nc;
