@@ -4798,6 +4798,15 @@ struct Gen {
   // ---------------------------------------------------------------------------------------
   // the kernel around the body
   // ---------------------------------------------------------------------------------------
+  // MYTHGPU_JIT_ASM_SGKEY=1: the group key on the scalar unit per group (fmix64, 18 SALU) instead of the
+  // VALU table of the next 64 groups
+  static bool salu_group_key() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_SGKEY");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
   // 64-bit fmix64 of s[x:x+1] in place (SALU; s40/s41 scratch)
   void sfmix(int x) {
     auto xs = [&]() {
@@ -5370,7 +5379,11 @@ struct Gen {
     // keys of its next 64 on the VALU (lane l: group g + l * gstride) into v10/v11, and each group reads
     // its own with two v_readlane: 18 SALU per group (fmix64 on the scalar unit, 8 of them multiplies)
     // become 2 VALU + ~0.4 amortised
-    {
+    if (salu_group_key()) {
+      E.salu("s_lshr_b64 s[36:37], s[34:35], 6", {36, 37});
+      E.salu("s_xor_b64 s[36:37], s[36:37], s[14:15]", {36, 37});
+      sfmix(36);
+    } else {
       const std::string have = E.newlab();
       E.salu("s_cmp_lt_u32 s7, 64");
       E.ctl("s_cbranch_scc1 " + have);
