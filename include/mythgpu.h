@@ -233,6 +233,10 @@ typedef struct mg_stats {
  * smaller, latency-bound calls and every other call run on the first device.  Programs, generators and JIT kernels are mirrored under the same
  * handles and uploaded to a device on first use there. */
 int mg_init(uint32_t device_mask);
+/* the exchange step of a split search: 0 = host reduction (default), 1 = ONE RCCL all-reduce(min) of
+ * the devices' first-hit words over xGMI (MYTHGPU_COLLECTIVE=rccl and a mask of distinct physical
+ * GPUs; =rccl-force also on one device).  librccl is dlopen'ed; any failure keeps the host reduction. */
+int mg_collective_kind(void);
 /* host-only: the slice of [start, start+count) device d of n_dev sweeps */
 int mg_split_range(uint64_t start, uint64_t count, uint32_t n_dev, uint64_t* starts, uint64_t* counts);
 void mg_shutdown(void);

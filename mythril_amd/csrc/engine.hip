@@ -11,6 +11,7 @@
 // Modes: EVAL (coordinates from a SoA buffer in HBM), GEN (coordinates from the
 // counter-based generator, for model materialisation), SEARCH (generator + wave
 // ballot + atomicMin first hit).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -1585,6 +1586,120 @@ static bool split_over_devices(uint64_t count) {
   return g_devs.size() > 1 && count / g_devs.size() >= split_min_per_device();
 }
 
+// ---------------------------------------------------------------------------------------------
+// The split search's exchange step as ONE RCCL all-reduce(min) over xGMI: after the
+// devices' launches are queued, each device's first-hit word (d_hit[0]) is reduced in place on its
+// own stream in one ncclGroupStart / ncclGroupEnd, so every device holds the global first hit and
+// the host reads it back with the counts.  MYTHGPU_COLLECTIVE=rccl turns it on for a device mask
+// that spans distinct physical GPUs (logical devices on one GPU cannot form an RCCL communicator and
+// keep the host reduction); =rccl-force also for one device (a one-rank communicator: the plumbing
+// on a one-GPU box).  Default: the host reduction (one 2 KiB read per device, which the counts need
+// anyway).  librccl is dlopen'ed on first use: no link-time dependency, and a failure to load or to
+// build the communicators leaves the host reduction in place (mg_collective_kind says which).
+// ---------------------------------------------------------------------------------------------
+struct Rccl {
+  bool tried = false, ok = false;
+  std::string why;
+  int (*init_all)(void** comms, int ndev, const int* devlist) = nullptr;
+  int (*all_reduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
+  int (*group_start)() = nullptr;
+  int (*group_end)() = nullptr;
+  int (*destroy)(void*) = nullptr;
+  const char* (*err_str)(int) = nullptr;
+  std::vector<void*> comms;  // one per g_devs entry
+};
+static Rccl g_rccl;
+constexpr int kNcclUint64 = 5, kNcclMin = 3;  // rccl.h ncclDataType_t / ncclRedOp_t
+
+static int collective_mode() {  // 0 host, 1 rccl (distinct physical GPUs), 2 rccl-force
+  static const int m = [] {
+    const char* c = getenv("MYTHGPU_COLLECTIVE");
+    if (!c) return 0;
+    const std::string v(c);
+    return v == "rccl" ? 1 : v == "rccl-force" ? 2 : 0;
+  }();
+  return m;
+}
+
+// caller holds E().mu: the communicators over g_devs, built once; false = host reduction
+static bool rccl_ready() {
+  Rccl& r = g_rccl;
+  if (r.tried) return r.ok;
+  r.tried = true;
+  const int mode = collective_mode();
+  if (!mode) return false;
+  std::vector<int> devlist;
+  for (Engine* d : g_devs) devlist.push_back(d->device);
+  std::vector<int> uniq(devlist);
+  std::sort(uniq.begin(), uniq.end());
+  if (std::unique(uniq.begin(), uniq.end()) != uniq.end()) {
+    r.why = "logical devices share a GPU";
+    return false;
+  }
+  if (devlist.size() < 2 && mode != 2) {
+    r.why = "one device";
+    return false;
+  }
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    r.why = "librccl not found";
+    return false;
+  }
+  r.init_all = (decltype(r.init_all))dlsym(h, "ncclCommInitAll");
+  r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
+  r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+  r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+  r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+  r.err_str = (decltype(r.err_str))dlsym(h, "ncclGetErrorString");
+  if (!r.init_all || !r.all_reduce || !r.group_start || !r.group_end || !r.destroy) {
+    r.why = "librccl lacks the symbols";
+    return false;
+  }
+  r.comms.assign(devlist.size(), nullptr);
+  const int rc = r.init_all(r.comms.data(), (int)devlist.size(), devlist.data());
+  (void)hipSetDevice(E().device);
+  if (rc != 0) {
+    r.why = std::string("ncclCommInitAll: ") + (r.err_str ? r.err_str(rc) : std::to_string(rc));
+    r.comms.clear();
+    return false;
+  }
+  r.ok = true;
+  return true;
+}
+
+// caller holds E().mu; every device's launch is queued on its stream: d_hit[0] of each device becomes
+// the minimum over all of them (in place), ordered before the read-back fetch_hits queues after it
+static int rccl_first_hit_min() {
+  Rccl& r = g_rccl;
+  if (r.group_start() != 0) return set_err(MG_E_HIP, "ncclGroupStart failed");
+  int rc = 0;
+  for (size_t d = 0; d < g_devs.size() && rc == 0; d++) {
+    Engine& de = *g_devs[d];
+    rc = r.all_reduce(de.d_hit, de.d_hit, 1, kNcclUint64, kNcclMin, r.comms[d], de.stream);
+  }
+  const int rc2 = r.group_end();
+  (void)hipSetDevice(E().device);
+  if (rc != 0 || rc2 != 0)
+    return set_err(MG_E_HIP, std::string("ncclAllReduce: ") + (r.err_str ? r.err_str(rc ? rc : rc2) : "error"));
+  return MG_OK;
+}
+
+static int fetch_hits(Engine& e);
+
+// the split search's exchange (every device takes part: its word is ~0 when it had no slice), then the
+// read-back of each device's hit buffer (the counts; word 0 now the global first hit on every device)
+static int rccl_fetch(const std::vector<uint64_t>& ct) {
+  (void)ct;
+  if (int rc = rccl_first_hit_min()) return rc;
+  for (Engine* d : g_devs) {
+    HIPCHK(hipSetDevice(d->device));
+    if (int rc = fetch_hits(*d)) return rc;
+  }
+  HIPCHK(hipSetDevice(E().device));
+  return MG_OK;
+}
+
 // One empty launch of every interpreter variant the engine launches by default (and of the capture
 // gather and Keccak kernels) at initialisation: the runtime loads a kernel's code on its first launch,
 // ~2 ms that the first query of the process paid inside its time to first model (the first k_run
@@ -1812,6 +1927,11 @@ void mg_shutdown(void) {
     e.code_cache.idx.clear();
     return;
   }
+  if (g_rccl.ok) {  // the communicators before the streams and buffers they use
+    for (void* c : g_rccl.comms) (void)g_rccl.destroy(c);
+    g_rccl.comms.clear();
+  }
+  g_rccl.tried = g_rccl.ok = false;
   for (size_t i = g_devs.size(); i-- > 0;) {
     Engine* d = g_devs[i];
     (void)hipSetDevice(d->device);
@@ -2298,6 +2418,7 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
     std::vector<uint64_t> st(nd), ct(nd);
     mg_split_range(start, count, nd, st.data(), ct.data());
     int rc = MG_OK;
+    const bool coll = rccl_ready();  // the exchange as one RCCL all-reduce(min) (MYTHGPU_COLLECTIVE)
     for (uint32_t d = 0; d < nd && rc == MG_OK; d++) {
       if (!ct[d]) continue;
       Engine& de = *g_devs[d];
@@ -2315,8 +2436,9 @@ int mg_search(uint64_t prog, uint64_t gen, uint64_t seed, uint64_t start, uint64
       k.seed = seed;
       k.flags = flags | (de.sys_scope ? MG_SEARCH_SYSTEM_SCOPE : 0u);
       rc = launch_async<MODE_SEARCH>(de, dg.spec, k, ct[d]);
-      if (rc == MG_OK) rc = fetch_hits(de);
+      if (rc == MG_OK && !coll) rc = fetch_hits(de);
     }
+    if (rc == MG_OK && coll) rc = rccl_fetch(ct);
     for (uint32_t d = 0; d < nd; d++) {
       if (!ct[d]) continue;
       Engine& de = *g_devs[d];
@@ -2639,6 +2761,15 @@ int mg_program_jit_asm(const uint8_t* ssa, size_t len, const uint32_t* gen_blob,
     if (rc) return set_err(rc, "JIT assembly failed: " + log.substr(0, 4000));
   }
   return MG_OK;
+}
+
+int mg_collective_kind(void) {
+  Engine& e = E();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.init) return set_err(MG_E_NOTINIT, "mg_init first");
+  OnDevice od_(e);
+  if (!collective_mode()) return 0;
+  return rccl_ready() ? 1 : 0;
 }
 
 int mg_code_object_check(const void* code, size_t len, uint32_t* kernels, uint32_t* max_private_bytes,
@@ -3109,6 +3240,7 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
     };
     std::vector<A> a(nd);
     int rc = MG_OK;
+    const bool coll = rccl_ready();  // the exchange as one RCCL all-reduce(min) (MYTHGPU_COLLECTIVE)
     for (uint32_t d = 0; d < nd && rc == MG_OK; d++) {
       if (!ct[d]) continue;
       Engine& de = *g_devs[d];
@@ -3123,8 +3255,9 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
       const uint64_t lanes = (st[d] + ct[d]) - (st[d] & ~63ull);
       // hipModuleLaunchKernel copies the argument values at the call (nblk is set before it)
       rc = jit_launch_async(de, dj->fsearch, dj->nb_search, lanes, args, a[d].nblk);
-      if (rc == MG_OK) rc = fetch_hits(de);
+      if (rc == MG_OK && !coll) rc = fetch_hits(de);
     }
+    if (rc == MG_OK && coll) rc = rccl_fetch(ct);
     for (uint32_t d = 0; d < nd; d++) {
       if (!ct[d]) continue;
       Engine& de = *g_devs[d];
@@ -3147,6 +3280,8 @@ int mg_jit_search(uint64_t jit, uint64_t seed, uint64_t start, uint64_t count, u
     const uint64_t lanes = (start + count) - (start & ~63ull);
     int rc = arm_hits(e);
     if (!rc) rc = jit_launch_async(e, j.fsearch, j.nb_search, lanes, args, nblk);
+    // MYTHGPU_COLLECTIVE=rccl-force on one device: the same all-reduce over a one-rank communicator
+    if (!rc && collective_mode() == 2 && g_devs.size() == 1 && rccl_ready()) rc = rccl_first_hit_min();
     if (!rc) rc = fetch_hits(e);
     if (!rc) rc = collect_hits(e, e.stats, count, res);
     if (rc) return rc;

@@ -48,7 +48,7 @@ def tile_soa(soa):
 NO_HIT = (1 << 64) - 1
 
 EXPORTS = [
-    "mg_init", "mg_shutdown", "mg_last_error", "mg_version", "mg_program_check", "mg_program_check_gen",
+    "mg_init", "mg_collective_kind", "mg_shutdown", "mg_last_error", "mg_version", "mg_program_check", "mg_program_check_gen",
     "mg_program_specialized", "mg_program_load",
     "mg_program_info", "mg_program_free", "mg_gen_load", "mg_gen_info", "mg_gen_free", "mg_eval", "mg_eval_dev",
     "mg_eval_generated", "mg_search", "mg_keccak256", "mg_stats", "mg_stats_reset", "mg_dev_alloc",
@@ -112,6 +112,7 @@ def load_library(path: Optional[Path] = None) -> C.CDLL:
         u8p, u32p, u64p = C.POINTER(C.c_uint8), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
         sig = {
             "mg_init": (C.c_int, [C.c_uint32]),
+            "mg_collective_kind": (C.c_int, []),
             "mg_shutdown": (None, []),
             "mg_last_error": (C.c_char_p, []),
             "mg_version": (C.c_int, []),
