@@ -53,7 +53,10 @@ def test_rccl_first_hit_equals_host_reduction():
     rccl = _run(MYTHGPU_COLLECTIVE="rccl-force")
     assert host["kind"] == 0
     assert rccl["kind"] == 1, "librccl did not load or the one-rank communicator failed"
-    assert rccl["rows"] == host["rows"]
+    # first hits everywhere; counts only for full sweeps (an early-exit search's count depends on when
+    # the waves above the first hit saw it)
+    for a, b in zip(rccl["rows"], host["rows"]):
+        assert a[:4] == b[:4] and a[4][0] == b[4][0] and (a[3] or a[4][1] == b[4][1]), (a, b)
     for w, start, n, early, (first, hits) in rccl["rows"]:
         if early:
             continue
@@ -68,4 +71,5 @@ def test_logical_devices_keep_the_host_reduction():
     virt = _run(MYTHGPU_COLLECTIVE="rccl", MYTHGPU_VIRTUAL_DEVICES="2", MYTHGPU_SPLIT_MIN="4096")
     host = _run()
     assert virt["kind"] == 0
-    assert [r[4] for r in virt["rows"]] == [r[4] for r in host["rows"]]
+    for a, b in zip(virt["rows"], host["rows"]):
+        assert a[4][0] == b[4][0] and (a[3] or a[4][1] == b[4][1]), (a, b)
