@@ -4798,15 +4798,21 @@ struct Gen {
   // ---------------------------------------------------------------------------------------
   // the kernel around the body
   // ---------------------------------------------------------------------------------------
-  // MYTHGPU_JIT_ASM_SGKEY=1: the group key on the scalar unit per group (fmix64, 18 SALU) instead of the
-  // VALU table of the next 64 groups
-  static bool salu_group_key() {
-    static const bool on = [] {
+  // The group key on the scalar unit per group (fmix64, 18 SALU, 8 of them multiplies) or from the VALU
+  // table of the wave's next 64 groups (2 v_readlane per group + ~0.4 VALU amortised): the table pays
+  // where the scalar unit is the busier one.  jit_asm_source decides per kernel from the first pass's
+  // static SALU : VALU ratio (kSgkeyRatio); MYTHGPU_JIT_ASM_SGKEY=1 / =0 fixes the scalar / VALU key.
+  // Measured (profiles/r06f_group_key_ab.jsonl, profiles/r06h_bench_*): C3 515 vs 482 G/s with the
+  // table, C1 / etherstore / C4 +0.7-0.9 %, the C2 headline at 2^30 233 vs 229.6 with the scalar key.
+  bool sgkey = false;
+  static int sgkey_env() {
+    static const int v = [] {
       const char* g = getenv("MYTHGPU_JIT_ASM_SGKEY");
-      return g && g[0] == '1';
+      return g ? (g[0] == '1' ? 1 : 0) : -1;
     }();
-    return on;
+    return v;
   }
+  bool salu_group_key() const { return sgkey; }
   // 64-bit fmix64 of s[x:x+1] in place (SALU; s40/s41 scratch)
   void sfmix(int x) {
     auto xs = [&]() {
@@ -5622,6 +5628,11 @@ std::string metadata_eval(int vg, int sg, uint32_t lds) {
   return o.str();
 }
 
+// SALU : VALU lines of a search kernel's first pass (VALU group key, no caches) below which the group
+// key stays on the scalar unit (whole kernel: C2 0.24, C5 0.16: scalar; C1 0.26, etherstore 0.27, C4 0.32,
+// C3 0.41: the VALU table)
+constexpr double kSgkeyRatio = 0.25;
+
 // the most VGPRs a kernel of `v` VGPRs may use and keep its waves per SIMD (512 per lane, in
 // granules of 8), and never below 96 (5 waves)
 static int occupancy_step(int v) {
@@ -5780,6 +5791,20 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
     }
     g.caches = true;
     g.vsoft = occupancy_step(v0);
+    // the group key's unit (Gen::sgkey): the scalar unit unless the first pass's body leans on it
+    if (Gen::sgkey_env() >= 0) {
+      g.sgkey = Gen::sgkey_env() == 1;
+    } else if (!ks.empty()) {
+      size_t sa = 0, va = 0;
+      std::istringstream in(ks);
+      for (std::string ln; std::getline(in, ln);) {
+        if (ln.rfind("  v_", 0) == 0) va++;
+        else if (ln.rfind("  s_", 0) == 0 && ln.rfind("  s_waitcnt", 0) && ln.rfind("  s_nop", 0) &&
+                 ln.rfind("  s_branch", 0) && ln.rfind("  s_cbranch", 0) && ln.rfind("  s_endpgm", 0))
+          sa++;
+      }
+      g.sgkey = va && (double)sa < kSgkeyRatio * (double)va;
+    }
     {
       std::vector<std::pair<uint32_t, uint32_t>> by;  // (count, literal)
       if (!getenv("MYTHGPU_JIT_ASM_NOPOOL"))
