@@ -2389,6 +2389,140 @@ std::vector<uint32_t> narrow_literal_tails(std::vector<VInstr>& code, std::vecto
 
 }  // namespace
 
+// A search program's constraints, heavy ones last (the interpreter's and the O3 kernel's order; the
+// first tier orders its own the same way, jit_asm.cpp heavy_last_roots).  Each ASSERT is emitted
+// right after the cone it needs, so a wave that leaves at the first ASSERT all its lanes failed skips
+// every later cone.  A constraint whose not-yet-emitted cone holds Keccak, EXP or a division goes
+// after the light ones (which keep program order); the heavy ones follow cheapest remaining cone
+// first.  A program without such an operator is returned unchanged.  MYTHGPU_HEAVY_LAST=0: off.
+static void heavy_last(std::vector<VInstr>& list) {
+  static const bool on = [] {
+    const char* g = getenv("MYTHGPU_HEAVY_LAST");
+    return !(g && g[0] == '0');
+  }();
+  auto heavy = [](uint32_t op) {
+    return op == K_KECCAK || op == K_EXP || op == K_UDIV || op == K_UREM || op == K_SDIV || op == K_SREM || op == K_SMOD;
+  };
+  if (!on || std::none_of(list.begin(), list.end(), [&](const VInstr& c) { return heavy(c.op); })) return;
+  // rough VALU per candidate on the compiled kernels (the first tier's op_weight): which heavy cone is
+  // cheapest (a Keccak-f[1600] ~2,500, EXP ~1,500, a division ~600)
+  auto weight = [](const VInstr& in) -> uint64_t {
+    const uint64_t L = std::max<uint32_t>(1, Lw(std::max(in.wd, in.op >= K_EQ && in.op <= K_UMUL_NOOVF ? in.p1 : in.wd)));
+    switch (in.op) {
+      case K_KECCAK: return 2500ull * (in.p0 / 136u + 1u);
+      case K_EXP: return 1500;
+      case K_UDIV: case K_UREM: case K_SDIV: case K_SREM: case K_SMOD: return 600;
+      case K_MUL: return 4 * L * L;
+      case K_UMUL_NOOVF: return 8 * L * L;
+      case K_SHL: case K_LSHR: case K_ASHR: return 4 * L;
+      case K_LOOKUP: return 2ull * Lw(in.b) * std::max<uint32_t>(1, in.c);
+      case K_COORD: return 8 * L;
+      default: return L;
+    }
+  };
+  std::map<uint32_t, int32_t> def;
+  for (size_t k = 0; k < list.size(); k++)
+    if (list[k].dst != MG_NONE && !def.count(list[k].dst)) def[list[k].dst] = (int32_t)k;
+  auto operands = [&](const VInstr& c, std::vector<int32_t>& out) {
+    out.clear();
+    auto add = [&](uint32_t x) {
+      auto it = x == MG_NONE ? def.end() : def.find(x);
+      if (it != def.end()) out.push_back(it->second);
+    };
+    if (c.op == K_LOOKUP) {
+      add(c.a);
+      add(c.p0);
+      for (uint32_t x : c.prior) add(x);
+    } else if (c.op == K_CONCAT || c.op == K_EXTRACT || c.op == K_ZEXT || c.op == K_SEXT || c.op == K_KECCAK ||
+               c.op == K_ASSERT || c.op == K_WATCH || c.op == K_COPY) {
+      add(c.a);
+      add(c.b);
+    } else if (c.op != K_CONST && c.op != K_COORD) {
+      add(c.a);
+      add(c.b);
+      add(c.c);
+    }
+  };
+  std::vector<char> done(list.size(), 0);
+  std::vector<int32_t> order, ops, st, mark(list.size(), -1);
+  int32_t stamp = 0;
+  auto visit = [&](int32_t root) {  // operands first, depth-first
+    std::vector<std::pair<int32_t, std::vector<int32_t>>> stk;
+    stk.push_back({root, {}});
+    operands(list[root], stk.back().second);
+    std::reverse(stk.back().second.begin(), stk.back().second.end());
+    while (!stk.empty()) {
+      auto& top = stk.back();
+      if (done[top.first]) {
+        stk.pop_back();
+        continue;
+      }
+      if (!top.second.empty()) {
+        const int32_t o = top.second.back();
+        top.second.pop_back();
+        if (!done[o]) {
+          stk.push_back({o, {}});
+          operands(list[o], stk.back().second);
+          std::reverse(stk.back().second.begin(), stk.back().second.end());
+        }
+        continue;
+      }
+      done[top.first] = 1;
+      order.push_back(top.first);
+      stk.pop_back();
+    }
+  };
+  auto cone = [&](int32_t r, bool& hv) -> uint64_t {
+    uint64_t c = 0;
+    hv = false;
+    st.assign(1, r);
+    mark[r] = ++stamp;
+    while (!st.empty()) {
+      const int32_t x = st.back();
+      st.pop_back();
+      const VInstr& in = list[x];
+      c += weight(in);
+      hv = hv || heavy(in.op);
+      operands(in, ops);
+      for (int32_t o : ops)
+        if (!done[o] && mark[o] != stamp) {
+          mark[o] = stamp;
+          st.push_back(o);
+        }
+    }
+    return c;
+  };
+  std::vector<int32_t> roots;
+  for (size_t k = 0; k < list.size(); k++)
+    if (list[k].op == K_ASSERT || list[k].op == K_WATCH) roots.push_back((int32_t)k);
+  std::vector<char> taken(roots.size(), 0);
+  for (size_t step = 0; step < roots.size(); step++) {
+    size_t pick = roots.size();
+    uint64_t best = UINT64_MAX;
+    for (size_t i = 0; i < roots.size(); i++) {
+      if (taken[i]) continue;
+      bool hv = false;
+      const uint64_t c = cone(roots[i], hv);
+      if (!hv) {
+        pick = i;
+        break;
+      }
+      if (c < best) {
+        best = c;
+        pick = i;
+      }
+    }
+    taken[pick] = 1;
+    visit(roots[pick]);
+  }
+  for (size_t k = 0; k < list.size(); k++)
+    if (!done[k]) visit((int32_t)k);
+  std::vector<VInstr> out;
+  out.reserve(list.size());
+  for (int32_t k : order) out.push_back(std::move(list[k]));
+  list.swap(out);
+}
+
 int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, const std::vector<uint32_t>* gconsts,
                        Lowered& out, std::string& err, bool keep_watch, bool keep_asserts) {
   try {
@@ -2517,11 +2651,16 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
       }
       return r;
     };
+    // a search program (a generator: early exit) with heavy operators: heavy constraints last
+    const bool order = specs != nullptr;
+    if (order) heavy_last(kept);
     if (narrowed) {
       std::vector<VInstr> kept_wide = jit_rewrites(dce(wide));
+      if (order) heavy_last(kept_wide);
       allocate(kept_wide, vwidth, out, &kept);
     } else {
       std::vector<VInstr> jit_list = jit_rewrites(kept);
+      if (order) heavy_last(jit_list);
       if (pushed || pruned)
         allocate(jit_list, vwidth, out, &kept);
       else
