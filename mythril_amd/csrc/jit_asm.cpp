@@ -858,10 +858,13 @@ struct Gen {
       // per entry and limb, the LDS read none (its few addresses fall in distinct banks)
       if (!dict || n < 2 || Lc > 16 || lds_base.count(off)) continue;
       if (w <= 32 && (uint64_t)n * w <= 32) continue;  // packed into one literal
-      if ((size_t)off + (size_t)n * Lc > G.size() || lds_words + n * Lc > kLdsWords) continue;
-      lds_base[off] = lds_words;
+      // pair layout (lds_pairs): limbs (2p, 2p+1) of entry e side by side at word base + 2pn + 2e, an odd
+      // top limb padded, the base even (8-byte aligned for ds_read_b64)
+      const uint32_t Ls = lds_pairs() ? Lc + (Lc & 1u) : Lc, at = lds_pairs() ? (lds_words + 1u) & ~1u : lds_words;
+      if ((size_t)off + (size_t)n * Lc > G.size() || at + n * Ls > kLdsWords) continue;
+      lds_base[off] = at;
       lds_shape[off] = {n, Lc};
-      lds_words += n * Lc;
+      lds_words = at + n * Ls;
     }
   }
 
@@ -870,6 +873,16 @@ struct Gen {
   // serialised one memory latency per table and step in every block's start-up: C3's first tier ran
   // 283 G/s at 64 blocks per CU and 424 at 32, profiles/r05p_rates_c3_bpc.jsonl)
   // MYTHGPU_JIT_ASM_STAGE_BATCH: steps per wait (default 1 until measured on the box; 16 batched)
+  // Staged dictionaries in pairs of limbs, read by ds_read_b64: 8 bytes per lane in the LDS cycles and
+  // lane groups a ds_read_b32 moves 4 in (64 banks instead of 32), so a lookup costs half the LDS
+  // array cycles, bank conflicts included.  MYTHGPU_JIT_ASM_LDS_B32=1: one limb per read (limb-major)
+  static bool lds_pairs() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_LDS_B32");
+      return !(g && g[0] == '1');
+    }();
+    return on;
+  }
   static size_t stage_batch() {
     static const size_t n = [] {
       const char* g = getenv("MYTHGPU_JIT_ASM_STAGE_BATCH");
@@ -909,7 +922,16 @@ struct Gen {
         E.valu("v_lshrrev_b32_e32 " + VL(ve) + ", 16, " + VL(ve));       // entry e
         E.valu("v_mul_u32_u24_e32 " + VL(vj) + ", " + imm(Lc) + ", " + VL(ve));
         E.valu("v_sub_u32_e32 " + VL(vj) + ", " + VL(vi) + ", " + VL(vj));  // limb j
-        E.valu("v_mul_u32_u24_e32 " + VL(vj) + ", " + imm(n) + ", " + VL(vj));
+        if (lds_pairs()) {  // word base + (j & ~1) n + 2e + (j & 1)
+          const Limb vo = fresh();
+          E.valu("v_and_b32_e32 " + VL(vo) + ", 1, " + VL(vj));
+          E.valu("v_and_b32_e32 " + VL(vj) + ", -2, " + VL(vj));
+          E.valu("v_mul_u32_u24_e32 " + VL(vj) + ", " + imm(n) + ", " + VL(vj));
+          E.valu("v_lshl_add_u32 " + VL(ve) + ", " + VL(ve) + ", 1, " + VL(vo));
+          drop(vo);
+        } else {
+          E.valu("v_mul_u32_u24_e32 " + VL(vj) + ", " + imm(n) + ", " + VL(vj));
+        }
         if (!inl(base)) E.salu("s_mov_b32 s41, " + hexs(base), {41});
         E.valu("v_add3_u32 " + VL(vj) + ", " + VL(vj) + ", " + VL(ve) + ", " + (inl(base) ? imm(base) : "s41"), {41});
         E.valu("v_lshlrev_b32_e32 " + VL(vj) + ", 2, " + VL(vj));
@@ -2294,6 +2316,57 @@ struct Gen {
       return r;
     }
     auto lb = lds_base.find(off);
+    if (lb != lds_base.end() && lds_pairs()) {  // pairs: limbs (2p, 2p+1) at word base + 2pn + 2 idx
+      const Limb va = fresh();
+      E.valu("v_lshlrev_b32_e32 " + VL(va) + ", 3, " + VL(idx));
+      auto varies = [&](uint32_t j) {
+        if (j >= Lu) return false;
+        for (uint32_t e2 = 1; e2 < n; e2++)
+          if (G[off + e2 * Lc + j] != G[off + j]) return true;
+        return false;
+      };
+      bool any = false;
+      for (uint32_t j = 0; j < Lu; j += 2) {
+        const bool a0 = varies(j), a1 = j + 1 < Lc && varies(j + 1);
+        if (!a0) r[j] = Lit(G[off + j]);
+        if (j + 1 < Lc && !a1) r[j + 1] = Lit(G[off + j + 1]);
+        if (!a0 && !a1) continue;
+        const uint32_t byte = (lb->second + j * n) * 4;
+        any = true;
+        if (a0 && a1) {
+          Limb d0, d1;
+          if (tgt) {
+            d0 = (*tgt)[j];
+            d1 = (*tgt)[j + 1];
+          } else {
+            const uint32_t rr = E.valloc2();
+            d0 = Limb{LR, rr, E.vgen[rr]};
+            d1 = Limb{LR, rr + 1, E.vgen[rr + 1]};
+          }
+          if ((d0.v & 1u) == 0 && d1.v == d0.v + 1) {
+            E.mem("ds_read_b64 " + VP(d0.v) + ", " + VL(va) + " offset:" + std::to_string(byte));
+          } else {  // a target pair the allocator could not align
+            E.mem("ds_read_b32 " + VL(d0) + ", " + VL(va) + " offset:" + std::to_string(byte));
+            E.mem("ds_read_b32 " + VL(d1) + ", " + VL(va) + " offset:" + std::to_string(byte + 4));
+          }
+          r[j] = d0;
+          r[j + 1] = d1;
+          if (!no_lds_defer()) {
+            E.lds_pending.insert((int)d0.v);
+            E.lds_pending.insert((int)d1.v);
+          }
+        } else {
+          const uint32_t q = a0 ? j : j + 1;
+          const Limb d = dst(q);
+          E.mem("ds_read_b32 " + VL(d) + ", " + VL(va) + " offset:" + std::to_string(byte + 4 * (q - j)));
+          r[q] = d;
+          if (!no_lds_defer()) E.lds_pending.insert((int)d.v);
+        }
+      }
+      if (any && no_lds_defer()) E.ctl("s_waitcnt lgkmcnt(0)");
+      drop(va);
+      return r;
+    }
     if (lb != lds_base.end()) {  // from the LDS copy: word base + j * n + idx
       const Limb va = fresh();
       E.valu("v_lshlrev_b32_e32 " + VL(va) + ", 2, " + VL(idx));
@@ -2588,7 +2661,20 @@ struct Gen {
         }
         CondScope cs_(*this);
         std::vector<Limb> out(Lg);
-        for (auto& x : out) x = fresh();
+        if (lds_pairs() && sp.p[1] && (sp.p[2] >> 16) && lds_base.count(sp.p[0])) {
+          // the dictionary alternative reads limb pairs straight into these: even-aligned pairs
+          for (uint32_t j = 0; j < Lg; j += 2) {
+            if (j + 1 < Lg) {
+              const uint32_t rr = E.valloc2();
+              out[j] = Limb{LR, rr, E.vgen[rr]};
+              out[j + 1] = Limb{LR, rr + 1, E.vgen[rr + 1]};
+            } else {
+              out[j] = fresh();
+            }
+          }
+        } else {
+          for (auto& x : out) x = fresh();
+        }
         const uint32_t pc = sp.p[3] != MG_NONE ? (sp.p[2] & 0xFFFFu) : 0u;
         const uint32_t pd = sp.p[1] ? (sp.p[2] >> 16) : 0u;
         const uint32_t ps = sp.p[4] & 0xFFFFu;
@@ -4551,7 +4637,9 @@ struct Gen {
         } else {
           E.salu("s_and_b64 s[38:39], s[38:39], " + SP(m.s), {38, 39});
         }
-        if (!gen_kernel && !eval_kernel) {
+        bool later = false;  // the last ASSERT falls through to the group's end anyway
+        for (size_t q = k + 1; q < code.size() && !later; q++) later = code[q].op == K_ASSERT;
+        if (!gen_kernel && !eval_kernel && later) {
           // early exit: s[42:43] is ~0 when the launch does not stop early, so the OR is zero only
           // when every lane failed and the wave may leave
           E.salu("s_or_b64 s[40:41], s[38:39], s[42:43]", {40, 41});
@@ -5636,8 +5724,13 @@ constexpr double kSgkeyRatio = 0.25;
 // the most VGPRs a kernel of `v` VGPRs may use and keep its waves per SIMD (512 per lane, in
 // granules of 8), and never below 96 (5 waves)
 static int occupancy_step(int v) {
+  // MYTHGPU_JIT_ASM_VMIN=N: the floor instead of 96 (diagnostic)
+  static const int floor_v = [] {
+    const char* g = getenv("MYTHGPU_JIT_ASM_VMIN");
+    return g ? std::max(24, std::min(256, atoi(g))) : 96;
+  }();
   const int waves = std::max(1, std::min(8, 512 / ((std::max(v, 1) + 7) / 8 * 8)));
-  return std::max(96, std::min(256, 512 / waves / 8 * 8));
+  return std::max(floor_v, std::min(256, 512 / waves / 8 * 8));
 }
 
 int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const std::vector<uint32_t>& gconsts,
@@ -5784,6 +5877,7 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
     try {
       ks = g.kernel("mgj_search");
       v0 = g.meta_vgpr["mgj_search"];
+      if (getenv("MYTHGPU_JIT_ASM_VREPORT")) fprintf(stderr, "mythgpu asm: pass-1 VGPRs %d\n", v0);
     } catch (const AsmFail&) {
       // out of VGPRs without the caches (shared XOR limbs relieve pressure): no soft limit then
       v0 = 256;

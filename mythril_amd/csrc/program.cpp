@@ -411,6 +411,46 @@ std::vector<VInstr> push_eq_into_lookup(const std::vector<VInstr>& code, std::ve
 }
 
 // K_COORD / K_CONST moved to just before their first use (order among them kept)
+// The compiled kernels' list: a Bool NOT whose operand is an ordering compare read only by it becomes
+// the complementary compare of the swapped operands — not (a <u b) = b <=u a, not (a <=u b) = b <u a,
+// signed alike — defined at the compare's place under the NOT's value id (EQ keeps its NOT).  The first
+// tier computes ULE / SLE as the negated borrow, so NOT(ULE) had cost two scalar NOTs.
+std::vector<VInstr> fold_not_compares(const std::vector<VInstr>& code, size_t nv, bool* changed) {
+  std::vector<uint32_t> uses(nv, 0);
+  std::vector<int64_t> def(nv, -1);
+  for (size_t k = 0; k < code.size(); k++) {
+    for_each_use(code[k], [&](uint32_t v) {
+      if (v < nv) uses[v]++;
+    });
+    if (code[k].dst != MG_NONE && code[k].dst < nv) def[code[k].dst] = (int64_t)k;
+  }
+  std::vector<VInstr> out = code;
+  std::vector<char> drop(code.size(), 0);
+  for (size_t k = 0; k < code.size(); k++) {
+    const VInstr& n = code[k];
+    if (n.op != K_NOT || n.wd != 1 || n.a >= nv || uses[n.a] != 1 || def[n.a] < 0) continue;
+    VInstr& c = out[def[n.a]];
+    uint32_t op;
+    switch (c.op) {
+      case K_ULT: op = K_ULE; break;
+      case K_ULE: op = K_ULT; break;
+      case K_SLT: op = K_SLE; break;
+      case K_SLE: op = K_SLT; break;
+      default: continue;
+    }
+    c.op = op;
+    std::swap(c.a, c.b);
+    c.dst = n.dst;
+    drop[k] = 1;
+    *changed = true;
+  }
+  std::vector<VInstr> r;
+  r.reserve(out.size());
+  for (size_t k = 0; k < out.size(); k++)
+    if (!drop[k]) r.push_back(std::move(out[k]));
+  return r;
+}
+
 std::vector<VInstr> sink_inputs(const std::vector<VInstr>& code, size_t nv) {
   std::vector<int64_t> first(nv, -1);
   for (size_t k = 0; k < code.size(); k++)
@@ -2635,7 +2675,13 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
     out.limb_ops = 0;
     // the compiled kernels' list also takes the lookup-compare pushdown; the interpreter's slot code
     // does not (each pushed compare is one more dispatch there)
-    bool pushed = false, pruned = false;
+    bool pushed = false, pruned = false, folded = false;
+    // MYTHGPU_FOLD_NOT=0: keep NOT(compare) as two instructions (diagnostic)
+    static const bool fold_on = [] {
+      const char* g = getenv("MYTHGPU_FOLD_NOT");
+      return !(g && g[0] == '0');
+    }();
+    auto fold_nots = [&] { return fold_on; };
     auto jit_rewrites = [&](const std::vector<VInstr>& list) {
       std::vector<VInstr> r = prune_guarded_lookups(list, vwidth.size(), &pruned);
       if (pruned) r = dce(r);
@@ -2649,6 +2695,7 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
         pushed = true;
         r = dce(r);
       }
+      if (fold_nots()) r = fold_not_compares(r, vwidth.size(), &folded);
       return r;
     };
     // a search program (a generator: early exit) with heavy operators: heavy constraints last
@@ -2661,7 +2708,7 @@ int specialize_program(const Lowered& in, const std::vector<GenSpec>* specs, con
     } else {
       std::vector<VInstr> jit_list = jit_rewrites(kept);
       if (order) heavy_last(jit_list);
-      if (pushed || pruned)
+      if (pushed || pruned || folded)
         allocate(jit_list, vwidth, out, &kept);
       else
         allocate(kept, vwidth, out);

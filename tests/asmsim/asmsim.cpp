@@ -946,6 +946,11 @@ bool step(Wave& w, Ctx& c) {
         ValuCheck vc;
         const Src ad = vsrc(w, c, in, a[1], false, vc, true);
         if (a[0].k != O_V || a[0].n != nw) fail(w, c, in, "LDS load destination width");
+        if (nw > 1 && op != OP_ds_read2_b32 && (a[0].r & 1)) fail(w, c, in, "odd-aligned VGPR tuple");
+        if (op == OP_ds_read_b64)
+          for (int l = 0; l < 64; l++)
+            if ((w.exec >> l & 1) && ((ad.lo(l) + (uint32_t)in.offset) & 7u))
+              fail(w, c, in, "ds_read_b64 address not 8-byte aligned");
         if (op == OP_ds_read_b32) conflicts(ad, 1, 32, 32, nullptr, in.offset);
         else if (op == OP_ds_read_b64) conflicts(ad, 2, 32, 64, nullptr, in.offset);
         else if (op == OP_ds_read_b128) conflicts(ad, 4, 16, 64, kB128, in.offset);
