@@ -1340,7 +1340,159 @@ struct Gen {
     }();
     return on;
   }
+  // Dictionary limbs: a register that holds limb j of entry `idx` of a pure DICT coordinate's table
+  // (gen_value), keyed by its allocation tag, with the entry index register (one reference each).
+  // A compare of such limbs with literals, or with the same limbs of another coordinate drawn from an
+  // equal table, is decided by the indices: C4's key tests of caller-keyed mappings (the caller
+  // against the three actor literals) cost one compare of the index instead of an XOR-OR reduction
+  // over five limbs — what LLVM finds in the O3 kernel from its select chains.
+  // MYTHGPU_JIT_ASM_NO_DICT_EQ=1: off
+  struct DLimb {
+    uint32_t off = 0, n = 0, Lc = 0, j = 0;
+    Limb idx;
+  };
+  std::map<uint32_t, DLimb> dlimb;
+  static bool no_dict_eq() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_DICT_EQ");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
+  void dlimb_free(uint32_t g) {
+    auto it = dlimb.find(g);
+    if (it == dlimb.end()) return;
+    const Limb ix = it->second.idx;
+    dlimb.erase(it);
+    drop(ix);
+  }
+  bool dict_limb(const Limb& l, DLimb& out) const {
+    if (!l.reg() || !l.g || (int)l.v < E.vfirst || E.vgen[l.v] != l.g) return false;
+    auto it = dlimb.find(l.g);
+    if (it == dlimb.end()) return false;
+    out = it->second;
+    return true;
+  }
+  // the lane mask of idx in the entry set S (bit e), n entries; false when it takes more than two VALU
+  bool idx_in_set(const Limb& idx, const std::vector<char>& S, uint32_t n, Mask& m) {
+    uint32_t cnt = 0, first = 0, miss = 0;
+    for (uint32_t e = 0; e < n; e++) {
+      if (S[e]) {
+        if (!cnt) first = e;
+        cnt++;
+      } else {
+        miss = e;
+      }
+    }
+    if (cnt == 0 || cnt == n) {
+      m.k = 1;
+      m.ones = cnt == n;
+      return true;
+    }
+    if (cnt != 1 && cnt != n - 1 && n > 32) return false;
+    m.k = 2;
+    m.s = E.salloc();
+    if (cnt == 1 || cnt == n - 1) {
+      const uint32_t e = cnt == 1 ? first : miss;
+      const std::string op = cnt == 1 ? "v_cmp_eq_u32" : "v_cmp_ne_u32";
+      if (inl(e)) {
+        E.valu(op + "_e64 " + SP(m.s) + ", " + imm(e) + ", " + VL(idx), {}, {m.s, m.s + 1});
+      } else {
+        E.valu(op + "_e32 vcc, " + hexs(e) + ", " + VL(idx), {}, {kVCC, kVCC + 1});
+        E.salu("s_mov_b64 " + SP(m.s) + ", vcc", {m.s, m.s + 1});
+      }
+      return true;
+    }
+    uint32_t bits = 0;
+    for (uint32_t e = 0; e < n; e++)
+      if (S[e]) bits |= 1u << e;
+    const Limb t = fresh();
+    E.salu("s_mov_b32 s41, " + hexs(bits), {41});
+    E.valu("v_bfe_u32 " + VL(t) + ", s41, " + VL(idx) + ", 1", {41});
+    E.valu("v_cmp_ne_u32_e64 " + SP(m.s) + ", 0, " + VL(t), {}, {m.s, m.s + 1});
+    drop(t);
+    return true;
+  }
+  // a == b over limb pairs decided by dictionary indices (above); false: the general reduction
+  bool dict_eq(const std::vector<std::pair<Limb, Limb>>& prs, Mask& m) {
+    if (no_dict_eq() || dlimb.empty()) return false;
+    bool haveA = false, haveB = false;
+    DLimb A, B;
+    std::vector<std::pair<uint32_t, uint32_t>> lits;  // (limb of A, literal)
+    std::vector<std::pair<uint32_t, uint32_t>> regs;  // (limb of A, limb of B)
+    auto same_src = [](const DLimb& x, const DLimb& y) {
+      return x.off == y.off && x.n == y.n && x.Lc == y.Lc && x.idx == y.idx && x.idx.g == y.idx.g;
+    };
+    for (const auto& pr : prs) {
+      const Limb a = pr.first, b = pr.second;
+      if (a.lit() && b.lit()) {
+        if (a.v != b.v) {
+          m.k = 1;
+          m.ones = false;
+          return true;
+        }
+        continue;
+      }
+      if (a == b) continue;
+      DLimb da, db;
+      const bool ia = dict_limb(a, da), ib = dict_limb(b, db);
+      if ((ia && b.lit()) || (ib && a.lit())) {
+        const DLimb& d = ia ? da : db;
+        if (!haveA) {
+          A = d;
+          haveA = true;
+        } else if (!same_src(A, d)) {
+          return false;
+        }
+        lits.push_back({d.j, ia ? b.v : a.v});
+      } else if (ia && ib) {
+        if (!haveA) {
+          A = da;
+          haveA = true;
+        }
+        if (!haveB) {
+          B = db;
+          haveB = true;
+        }
+        const bool fwd = same_src(A, da) && same_src(B, db), rev = same_src(A, db) && same_src(B, da);
+        if (!fwd && !rev) return false;
+        const DLimb& x = fwd ? da : db;
+        const DLimb& y = fwd ? db : da;
+        regs.push_back({x.j, y.j});
+      } else {
+        return false;
+      }
+    }
+    if (!haveA) return false;  // (only literal pairs: the general path folds them)
+    if (!lits.empty() && !regs.empty()) return false;
+    if (!lits.empty()) {
+      std::vector<char> S(A.n, 0);
+      for (uint32_t e = 0; e < A.n; e++) {
+        bool ok = true;
+        for (const auto& lj : lits) ok = ok && G[A.off + e * A.Lc + lj.first] == lj.second;
+        S[e] = ok;
+      }
+      return idx_in_set(A.idx, S, A.n, m);
+    }
+    // two coordinates' entries: equal exactly when their indices are, if entry e of A matches entry e
+    // of B and no other on the compared limbs
+    if (!haveB || A.n != B.n || A.n > 256) return false;
+    for (uint32_t e = 0; e < A.n; e++)
+      for (uint32_t f = 0; f < B.n; f++) {
+        bool eq = true;
+        for (const auto& jj : regs) eq = eq && G[A.off + e * A.Lc + jj.first] == G[B.off + f * B.Lc + jj.second];
+        if (eq != (e == f)) return false;
+      }
+    m.k = 2;
+    m.s = E.salloc();
+    E.valu("v_cmp_eq_u32_e64 " + SP(m.s) + ", " + VL(A.idx) + ", " + VL(B.idx), {}, {m.s, m.s + 1});
+    return true;
+  }
   Mask eq_mask(const std::vector<std::pair<Limb, Limb>>& prs, Limb* keep = nullptr) {
+    {
+      Mask dm;
+      if (dict_eq(prs, dm)) return dm;
+    }
     std::vector<Limb> diff;  // owned
     std::vector<std::pair<Limb, Limb>> raw;  // pairs for the bitop3 accumulation
     for (const auto& pr : prs) {
@@ -2802,8 +2954,24 @@ struct Gen {
         const Limb ix = dict_index(h, sp.p[1]);
         drop(h);
         r = dict(sp.p[0], sp.p[1], width, ix);
+        std::vector<Limb> rd = r;
+        if (width & 31) mask_top(r, width);
+        if (fix) fixbits(r, fix, false);
+        // limbs still the entries' registers (not masked or fixed anew): dictionary limbs
+        if (!no_dict_eq() && caches)
+          for (uint32_t j = 0; j < r.size() && j < rd.size(); j++)
+            if (r[j].reg() && r[j] == rd[j] && r[j].g == rd[j].g && !dlimb.count(r[j].g)) {
+              DLimb dl;
+              dl.off = sp.p[0];
+              dl.n = sp.p[1];
+              dl.Lc = Lc;
+              dl.j = j;
+              dl.idx = ix;
+              E.retain(ix);
+              dlimb[r[j].g] = dl;
+            }
         drop(ix);
-        break;
+        return r;
       }
       case MG_GEN_RANGE: {
         const Limb rr = grnd(c, 0);
@@ -4783,9 +4951,11 @@ struct Gen {
     lit_last.clear();
     x_last.clear();
     eq_last.clear();
+    dlimb.clear();
     E.on_free = [this](uint32_t g) {
       xcache_free(g);
       hcache_free(g);
+      dlimb_free(g);
     };
     E.on_pressure = [this]() { return evict_one(); };
     E.on_hard = [this]() { return spill_one(); };
@@ -5901,9 +6071,14 @@ int jit_asm_source(const Lowered& P, const std::vector<GenSpec>& specs, const st
     }
     {
       std::vector<std::pair<uint32_t, uint32_t>> by;  // (count, literal)
+      // MYTHGPU_JIT_ASM_POOL_MIN=N: pool literals materialised at least N times (default 2)
+      static const uint32_t pool_min = [] {
+        const char* g = getenv("MYTHGPU_JIT_ASM_POOL_MIN");
+        return g ? (uint32_t)std::max(1, atoi(g)) : 2u;
+      }();
       if (!getenv("MYTHGPU_JIT_ASM_NOPOOL"))
         for (const auto& kv : g.census)
-          if (kv.second >= 2) by.push_back({kv.second, kv.first});
+          if (kv.second >= pool_min) by.push_back({kv.second, kv.first});
       std::sort(by.begin(), by.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
       const int room = std::max(0, std::min(96, g.vsoft) - v0);
       for (size_t i = 0; i < by.size() && (int)i < room; i++) g.pool[by[i].second] = kV0 + (int)i;
