@@ -5249,6 +5249,14 @@ struct Gen {
   // queue at depth N; unset / 0 = the register queue.  Opt-in: measured within +-3 % of the register
   // queue on C2 and C4 (profiles/r05i_eval_glds.jsonl) at ~2x its SALU and waits per row (M0, the
   // address pair, a vmcnt and an lgkmcnt wait), and the kernel is issue-bound
+  // MYTHGPU_JIT_ASM_XCD=1: the eval kernel's XCD-aware block order (above; diagnostic until measured)
+  static bool xcd_swizzle() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_XCD");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
   static bool glds_env() {
     static const bool on = [] {
       const char* g = getenv("MYTHGPU_JIT_ASM_GLDS");
@@ -5394,6 +5402,25 @@ struct Gen {
       E.label(go);
       E.salu("s_lshl_b32 s16, s2, 6", {16});
       E.salu("s_mov_b32 s17, 64", {17});
+    } else if (xcd_swizzle()) {
+      // blocks b and b + 8 share an XCD (MI355X_MICROARCH.md): with the block count a multiple of 8,
+      // block b takes candidates at (b % 8) * (nblk / 8) + b / 8, so the blocks of one XCD sweep one
+      // contiguous stretch of every SoA row (a bijection; otherwise the identity)
+      const std::string keep = E.newlab();
+      E.salu("s_mov_b32 s40, s2", {40});
+      E.salu("s_and_b32 s41, s14, 7", {41});
+      E.salu("s_cmp_eq_u32 s41, 0");
+      E.ctl("s_cbranch_scc0 " + keep);
+      E.salu("s_lshr_b32 s41, s14, 3", {41});
+      E.salu("s_and_b32 s40, s2, 7", {40});
+      E.salu("s_mul_i32 s40, s40, s41", {40});
+      E.salu("s_lshr_b32 s41, s2, 3", {41});
+      E.salu("s_add_u32 s40, s40, s41", {40});
+      E.label(keep);
+      E.salu("s_lshl_b32 s16, s40, 8", {16});
+      E.salu("s_lshl_b32 s22, s3, 6", {22});
+      E.salu("s_add_u32 s16, s16, s22", {16});
+      E.salu("s_lshl_b32 s17, s14, 8", {17});
     } else {
       E.salu("s_lshl_b32 s16, s2, 8", {16});
       E.salu("s_lshl_b32 s22, s3, 6", {22});
