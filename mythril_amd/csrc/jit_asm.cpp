@@ -5697,6 +5697,17 @@ struct Gen {
     E.valu("v_xor_b32_e32 v4, s36, v2", {36});
     E.valu("v_xor_b32_e32 v5, s37, v3", {37});
     E.salu("s_mov_b64 s[38:39], -1", {38, 39});
+    {  // MYTHGPU_JIT_ASM_DIAG_PAD=S,V: S scalar and V vector no-op moves per group (issue-sensitivity
+       // timing builds; results unchanged)
+      static const std::pair<int, int> pad = [] {
+        const char* g = getenv("MYTHGPU_JIT_ASM_DIAG_PAD");
+        int a = 0, b = 0;
+        if (g) sscanf(g, "%d,%d", &a, &b);
+        return std::make_pair(std::max(0, std::min(a, 200)), std::max(0, std::min(b, 200)));
+      }();
+      for (int q = 0; q < pad.first; q++) E.salu("s_mov_b32 s40, s40", {40});
+      for (int q = 0; q < pad.second; q++) E.valu("v_mov_b32_e32 v7, 0");
+    }
     body(next);
     for (int r = E.vfirst; r < 256; r++)
       if (E.vref[r]) fail("internal: VGPR v" + std::to_string(r) + " still held after the body");
