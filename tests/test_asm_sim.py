@@ -18,7 +18,8 @@ the simulator and the C port, test infrastructure, at -O2).  Programs: ``MYTHGPU
 mappings with many-prior inverse lookups and literal-slot tails, Store chains, wrap predicates, ITE
 guards, symbol equalities that make MIXED coordinates copy each other in chains), split over four
 emitter configurations (the lookup-compare pushdown and the guarded-lookup pruning on and off, the
-difference cache and Bool lookups off, no literal pool with the LDS-staged eval row queue), plus
+difference cache, Bool lookups, limb-pair dictionary reads, index compares and NOT folding off, no
+literal pool with the LDS-staged eval row queue), plus
 random programs over the tier's
 operators and the workloads at several windows.
 
@@ -43,7 +44,8 @@ WORKERS = max(1, min(8, os.cpu_count() or 1))
 CONFIGS = [
     {},
     {"MYTHGPU_EQ_PUSHDOWN": "0", "MYTHGPU_ITE_PRUNE": "0"},
-    {"MYTHGPU_JIT_ASM_NO_EQ_CACHE": "1", "MYTHGPU_JIT_ASM_NO_BOOL_LOOKUP": "1", "MYTHGPU_JIT_ASM_EXIT_SKIP": "0"},
+    {"MYTHGPU_JIT_ASM_NO_EQ_CACHE": "1", "MYTHGPU_JIT_ASM_NO_BOOL_LOOKUP": "1", "MYTHGPU_JIT_ASM_EXIT_SKIP": "0",
+     "MYTHGPU_JIT_ASM_LDS_B32": "1", "MYTHGPU_JIT_ASM_NO_DICT_EQ": "1", "MYTHGPU_FOLD_NOT": "0"},
     {"MYTHGPU_JIT_ASM_NOPOOL": "1", "MYTHGPU_EQ_PUSHDOWN": "1", "MYTHGPU_JIT_ASM_GLDS": "1"},
 ]
 
