@@ -92,6 +92,18 @@ struct Gen {
     return n;
   }
 
+  // Staged tables in quads of limbs: limbs 4q .. 4q+3 of entry e at word base + 4qn + 4e (the top quad
+  // padded), read as one 16-byte load where two or more of its limbs vary — ds_read_b128 moves 16
+  // bytes per lane in 4 LDS cycles, four times a ds_read_b32's bytes per cycle (MI355X_MICROARCH.md
+  // §LDS).  (Pairs were tried first: LLVM merges two 8-byte loads into ds_read2_b64, which takes twice
+  // a ds_read_b64's cycles.)  MYTHGPU_JIT_DICT_PAIRS=0: limb-major ([limb][entry])
+  static bool dict_pairs() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_DICT_PAIRS");
+      return !(g && g[0] == '0');
+    }();
+    return on;
+  }
   void plan_dict_lds() {
     dict_lds.clear();
     dict_n.clear();
@@ -123,7 +135,7 @@ struct Gen {
       if (!dict || n == 0 || c >= P.coord_width.size() || coord_dead(c)) continue;
       const uint32_t w = P.coord_width[c], L = Lw(w);
       if (!packed_dict(off, n, w, "e").empty() || dict_lds.count(off) || n <= select_dict_max()) continue;
-      const uint32_t need = (n * L + 3u) & ~3u;  // 16-B aligned tables (ds_read_b128)
+      const uint32_t need = dict_pairs() ? n * ((L + 3u) & ~3u) : (n * L + 3u) & ~3u;  // 16-B aligned tables
       if (lds_words + need > kDictLdsWords) continue;
       dict_lds[off] = lds_words;
       dict_n[off] = n;
@@ -180,7 +192,7 @@ struct Gen {
   // kernel prologue: copy the planned tables into LDS (all 256 lanes), then a block barrier
   void emit_dict_prologue() {
     if (!lds_words) return;
-    o << "  __shared__ uint32_t mg_dict[" << lds_words << "];\n";
+    o << "  __shared__ __attribute__((aligned(16))) uint32_t mg_dict[" << lds_words << "];\n";
     std::map<uint32_t, uint32_t> len;  // table -> words (n * L)
     for (uint32_t c = 0; c < specs->size(); c++) {
       const GenSpec& sp = (*specs)[c];
@@ -194,8 +206,13 @@ struct Gen {
     // a 256-bit table put every lane's limb j in one of 4 banks: 16-way conflicts)
     for (const auto& kv : len) {
       const uint32_t n = dict_n.at(kv.first), L = kv.second / std::max(n, 1u);
-      o << "  for (uint32_t i = tid; i < " << kv.second << "u; i += 256u) mg_dict[" << dict_lds.at(kv.first)
-        << "u + (i % " << L << "u) * " << n << "u + i / " << L << "u] = gconsts[" << kv.first << "u + i];\n";
+      if (dict_pairs())
+        o << "  for (uint32_t i = tid; i < " << kv.second << "u; i += 256u) mg_dict[" << dict_lds.at(kv.first)
+          << "u + ((i % " << L << "u) & ~3u) * " << n << "u + 4u * (i / " << L << "u) + ((i % " << L
+          << "u) & 3u)] = gconsts[" << kv.first << "u + i];\n";
+      else
+        o << "  for (uint32_t i = tid; i < " << kv.second << "u; i += 256u) mg_dict[" << dict_lds.at(kv.first)
+          << "u + (i % " << L << "u) * " << n << "u + i / " << L << "u] = gconsts[" << kv.first << "u + i];\n";
     }
     o << "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"workgroup\");\n"
          "  __builtin_amdgcn_s_barrier();\n"
@@ -229,6 +246,23 @@ struct Gen {
         for (uint32_t j = b; j < std::min(L, b + q); j++) gvl[j] = t + "." + comp[j - b];
       }
     }
+    auto varies = [&](uint32_t j) {
+      for (uint32_t e = 1; e < n; e++)
+        if (G[off + e * L + j] != G[off + j]) return true;
+      return false;
+    };
+    std::vector<std::string> pl(L);  // limb j from a quad load of the LDS copy
+    if (lds != dict_lds.end() && dict_pairs() && n > select_dict_max())
+      for (uint32_t b = 0; b < L; b += 4) {
+        uint32_t k = 0;
+        for (uint32_t j = b; j < std::min(L, b + 4); j++) k += varies(j) && gvl[j].empty();
+        if (k < 2) continue;
+        const std::string t = "mg_gq" + std::to_string(gv_tmp++);
+        o << ind << "const u32x4 " << t << " = *(const u32x4*)(mg_dict + " << lds->second + b * n << "u + 4u * " << idx
+          << ");\n";
+        static const char* comp = "xyzw";
+        for (uint32_t j = b; j < std::min(L, b + 4); j++) pl[j] = t + "." + comp[j - b];
+      }
     for (uint32_t j = 0; j < L; j++) {
       bool same = true;
       for (uint32_t e = 1; e < n && same; e++) same = G[off + e * L + j] == G[off + j];
@@ -243,6 +277,9 @@ struct Gen {
         for (int32_t e = (int32_t)n - 2; e >= 0; e--)
           v = "(" + idx + " == " + std::to_string(e) + "u ? " + hex(G[off + e * L + j]) + " : " + v + ")";
       } else if (!gvl[j].empty()) v = gvl[j];
+      else if (!pl[j].empty()) v = pl[j];
+      else if (lds != dict_lds.end() && dict_pairs())
+        v = "mg_dict[" + std::to_string(lds->second + (j & ~3u) * n + (j & 3u)) + "u + 4u * " + idx + "]";
       else if (lds != dict_lds.end()) v = "mg_dict[" + std::to_string(lds->second + j * n) + "u + " + idx + "]";
       else v = "gconsts[" + std::to_string(off + j) + "u + " + idx + " * " + std::to_string(L) + "u]";
       o << ind << lim(j) << " = " << v << ";\n";
