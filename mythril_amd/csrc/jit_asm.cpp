@@ -5712,8 +5712,11 @@ struct Gen {
     for (int r = E.vfirst; r < 256; r++)
       if (E.vref[r]) fail("internal: VGPR v" + std::to_string(r) + " still held after the body");
     E.label(next);
-    // m = verdict, restricted to [start, end) in a partial group
-    E.salu("s_mov_b64 s[40:41], s[38:39]", {40, 41});
+    // m = verdict, restricted to [start, end) in a partial group: in place in s[38:39] (search kernels:
+    // dead after the group), a copy in s[40:41] (the gen kernel stores the verdict as well)
+    const std::string M = gen_kernel ? "s[40:41]" : "s[38:39]";
+    const int m0 = gen_kernel ? 40 : 38;
+    if (gen_kernel) E.salu("s_mov_b64 s[40:41], s[38:39]", {40, 41});
     {
       const std::string fullg = E.newlab(), part = E.newlab();
       E.salu("s_cmp_eq_u64 s[34:35], s[10:11]");
@@ -5726,8 +5729,8 @@ struct Gen {
       E.valu("v_addc_co_u32_e32 v9, vcc, 0, v9, vcc", {kVCC, kVCC + 1}, {kVCC, kVCC + 1});
       E.valu("v_cmp_le_u64_e64 s[44:45], s[8:9], v[8:9]", {8, 9}, {44, 45});
       E.valu("v_cmp_gt_u64_e64 s[46:47], s[22:23], v[8:9]", {22, 23}, {46, 47});
-      E.salu("s_and_b64 s[40:41], s[40:41], s[44:45]", {40, 41});
-      E.salu("s_and_b64 s[40:41], s[40:41], s[46:47]", {40, 41});
+      E.salu("s_and_b64 " + M + ", " + M + ", s[44:45]", {m0, m0 + 1});
+      E.salu("s_and_b64 " + M + ", " + M + ", s[46:47]", {m0, m0 + 1});
       E.label(fullg);
     }
     if (gen_kernel) {
@@ -5755,14 +5758,13 @@ struct Gen {
     } else {
       // a wave sweeps its groups in increasing index order, so its first group with a hit holds its
       // best: later groups only count (bcnt) — no first-lane search and no 64-bit compare with the best
-      E.salu("s_cmp_eq_u64 s[40:41], 0");
-      E.ctl("s_cbranch_scc1 " + cont);
-      E.salu("s_bcnt1_i32_b64 s45, s[40:41]", {45});
+      E.salu("s_bcnt1_i32_b64 s45, s[38:39]", {45});  // SCC: any hit
+      E.ctl("s_cbranch_scc0 " + cont);
       E.salu("s_add_u32 s32, s32, s45", {32});
       E.salu("s_addc_u32 s33, s33, 0", {33});
       E.salu("s_cmp_lg_u64 s[30:31], -1");
       E.ctl("s_cbranch_scc1 " + cont);
-      E.salu("s_ff1_i32_b64 s44, s[40:41]", {44});
+      E.salu("s_ff1_i32_b64 s44, s[38:39]", {44});
       E.salu("s_add_u32 s46, s34, s44", {46});
       E.salu("s_addc_u32 s47, s35, 0", {47});
       E.salu("s_mov_b64 s[30:31], s[46:47]", {30, 31});
