@@ -29,6 +29,7 @@
 // live values do not fit 256 VGPRs plus the LDS spill slots of one wave (Gen::spill_one, `solo`),
 // and values wider than the limb bound (kMaxLimbs).
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -5699,14 +5700,20 @@ struct Gen {
     E.salu("s_mov_b64 s[38:39], -1", {38, 39});
     {  // MYTHGPU_JIT_ASM_DIAG_PAD=S,V: S scalar and V vector no-op moves per group (issue-sensitivity
        // timing builds; results unchanged)
-      static const std::pair<int, int> pad = [] {
+      // ,B: B taken branches to the next instruction
+      static const std::array<int, 3> pad = [] {
         const char* g = getenv("MYTHGPU_JIT_ASM_DIAG_PAD");
-        int a = 0, b = 0;
-        if (g) sscanf(g, "%d,%d", &a, &b);
-        return std::make_pair(std::max(0, std::min(a, 200)), std::max(0, std::min(b, 200)));
+        int a = 0, b = 0, c = 0;
+        if (g) sscanf(g, "%d,%d,%d", &a, &b, &c);
+        return std::array<int, 3>{std::max(0, std::min(a, 200)), std::max(0, std::min(b, 200)), std::max(0, std::min(c, 200))};
       }();
-      for (int q = 0; q < pad.first; q++) E.salu("s_mov_b32 s40, s40", {40});
-      for (int q = 0; q < pad.second; q++) E.valu("v_mov_b32_e32 v7, 0");
+      for (int q = 0; q < pad[0]; q++) E.salu("s_mov_b32 s40, s40", {40});
+      for (int q = 0; q < pad[1]; q++) E.valu("v_mov_b32_e32 v7, 0");
+      for (int q = 0; q < pad[2]; q++) {
+        const std::string l = E.newlab();
+        E.ctl("s_branch " + l);
+        E.label(l);
+      }
     }
     body(next);
     for (int r = E.vfirst; r < 256; r++)
@@ -5848,8 +5855,13 @@ struct Gen {
       E.label(end);
     }
     E.ctl("s_endpgm");
-    // descriptor
-    const int nv = std::max(E.vhigh, kV0), ns = std::max(E.shigh, 56);
+    // descriptor (MYTHGPU_JIT_ASM_DIAG_VGPRS=N: at least N VGPRs reserved — fewer waves per SIMD, for
+    // occupancy-sensitivity timing builds)
+    static const int diag_vgprs = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_DIAG_VGPRS");
+      return g ? std::max(0, std::min(256, atoi(g))) : 0;
+    }();
+    const int nv = std::max({E.vhigh, kV0, diag_vgprs}), ns = std::max(E.shigh, 56);
     const int accum = (nv + 3) / 4 * 4;
     o << "  .section .rodata,\"a\",@progbits\n  .p2align 6, 0x0\n  .amdhsa_kernel " << name << "\n"
       << "    .amdhsa_group_segment_fixed_size " << lds_words * 4 << "\n    .amdhsa_private_segment_fixed_size 0\n"
