@@ -2285,11 +2285,26 @@ struct Gen {
   // jit.cpp, engine.hip and oracle/bveval.c)
   // ---------------------------------------------------------------------------------------
   // per-lane hash grnd(c, j) into a fresh VGPR
+  // (x ^ salt) ^ ((x ^ salt) >> 16) = (x ^ (x >> 16)) ^ (salt ^ (salt >> 16)): v4 holds the group-lane
+  // key's x ^ (x >> 16), folded once per group (kernel()), so each draw XORs in its salt's fold — one
+  // VALU per draw instead of two.  MYTHGPU_JIT_ASM_NO_KFOLD=1: the fold per draw
+  static bool no_kfold() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_KFOLD");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
   Limb grnd(uint32_t c, uint32_t j, const Limb* into = nullptr) {
     const Limb d = into ? *into : fresh(), t = fresh();
-    E.valu("v_xor_b32_e32 " + VL(d) + ", " + imm(gsalt(c, j)) + ", v4");
-    E.valu("v_xor_b32_sdwa " + VL(d) + ", " + VL(d) + ", " + VL(d) +
-           " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1");
+    const uint32_t salt = gsalt(c, j);
+    if (no_kfold()) {
+      E.valu("v_xor_b32_e32 " + VL(d) + ", " + imm(salt) + ", v4");
+      E.valu("v_xor_b32_sdwa " + VL(d) + ", " + VL(d) + ", " + VL(d) +
+             " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1");
+    } else {
+      E.valu("v_xor_b32_e32 " + VL(d) + ", " + imm(salt ^ (salt >> 16)) + ", v4");
+    }
     E.valu("v_mul_u32_u24_e32 " + VL(d) + ", 0x9e3779, " + VL(d));
     E.valu("v_lshrrev_b32_e32 " + VL(t) + ", 15, " + VL(d));
     E.valu("v_xad_u32 " + VL(d) + ", " + VL(t) + ", " + VL(d) + ", v5");
@@ -5696,6 +5711,8 @@ struct Gen {
       E.salu("s_add_u32 s7, s7, 1", {7});
     }
     E.valu("v_xor_b32_e32 v4, s36, v2", {36});
+    if (!no_kfold())  // v4 ^= v4 >> 16 (grnd)
+      E.valu("v_xor_b32_sdwa v4, v4, v4 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1");
     E.valu("v_xor_b32_e32 v5, s37, v3", {37});
     E.salu("s_mov_b64 s[38:39], -1", {38, 39});
     {  // MYTHGPU_JIT_ASM_DIAG_PAD=S,V: S scalar and V vector no-op moves per group (issue-sensitivity
