@@ -2586,9 +2586,22 @@ struct Gen {
   }
 
   // e = ((h >> 16) * n) >> 16
+  // entry ((h >> 16) * n) >> 16: for n < 256 the high half of the 24-bit product (h >> 16) * (n << 16),
+  // one v_mul_hi_u32_u24 for the multiply and the shift (MYTHGPU_JIT_ASM_NO_MULHI24=1: three VALU)
+  static bool no_mulhi24() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_NO_MULHI24");
+      return g && g[0] == '1';
+    }();
+    return on;
+  }
   Limb dict_index(const Limb& h, uint32_t n) {
     const Limb e2 = fresh();
     E.valu("v_lshrrev_b32_e32 " + VL(e2) + ", 16, " + VL(h));
+    if (n < 256 && !no_mulhi24()) {
+      E.valu("v_mul_hi_u32_u24_e32 " + VL(e2) + ", " + imm(n << 16) + ", " + VL(e2));
+      return e2;
+    }
     E.valu("v_mul_u32_u24_e32 " + VL(e2) + ", " + imm(n) + ", " + VL(e2));
     E.valu("v_lshrrev_b32_e32 " + VL(e2) + ", 16, " + VL(e2));
     return e2;

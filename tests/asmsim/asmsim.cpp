@@ -31,7 +31,7 @@ namespace {
   X(s_load_dword) X(s_load_dwordx2) X(s_load_dwordx4) X(s_load_dwordx8)                                           \
   X(v_mov_b32) X(v_add_u32) X(v_sub_u32) X(v_subrev_u32) X(v_add_co_u32) X(v_addc_co_u32) X(v_sub_co_u32)        \
   X(v_subrev_co_u32) X(v_subb_co_u32) X(v_subbrev_co_u32) X(v_and_b32) X(v_or_b32) X(v_xor_b32) X(v_not_b32)     \
-  X(v_lshlrev_b32) X(v_lshrrev_b32) X(v_ashrrev_i32) X(v_min_u32) X(v_max_u32) X(v_mul_u32_u24) X(v_mul_lo_u32)  \
+  X(v_lshlrev_b32) X(v_lshrrev_b32) X(v_ashrrev_i32) X(v_min_u32) X(v_max_u32) X(v_mul_u32_u24) X(v_mul_hi_u32_u24) X(v_mul_lo_u32)  \
   X(v_mul_hi_u32) X(v_cndmask_b32) X(v_cmp_eq_u32) X(v_cmp_ne_u32) X(v_cmp_lt_u32) X(v_cmp_le_u32)                \
   X(v_cmp_gt_u32) X(v_cmp_ge_u32) X(v_cmp_eq_i32) X(v_cmp_ne_i32) X(v_cmp_lt_i32) X(v_cmp_le_i32) X(v_cmp_gt_i32) \
   X(v_cmp_ge_i32) X(v_cmp_eq_u64) X(v_cmp_ne_u64) X(v_cmp_lt_u64) X(v_cmp_le_u64) X(v_cmp_gt_u64) X(v_cmp_ge_u64) \
@@ -1205,7 +1205,7 @@ bool step(Wave& w, Ctx& c) {
     }
     case OP_v_add_u32: case OP_v_sub_u32: case OP_v_subrev_u32: case OP_v_and_b32: case OP_v_or_b32:
     case OP_v_xor_b32: case OP_v_lshlrev_b32: case OP_v_lshrrev_b32: case OP_v_ashrrev_i32: case OP_v_min_u32:
-    case OP_v_max_u32: case OP_v_mul_u32_u24: case OP_v_mul_lo_u32: case OP_v_mul_hi_u32: {
+    case OP_v_max_u32: case OP_v_mul_u32_u24: case OP_v_mul_hi_u32_u24: case OP_v_mul_lo_u32: case OP_v_mul_hi_u32: {
       need(3);
       e32_src1(a[2]);
       const Src x = vsrc(w, c, in, a[1], false, vc, vop3), y = vsrc(w, c, in, a[2], false, vc, vop3);
@@ -1227,6 +1227,7 @@ bool step(Wave& w, Ctx& c) {
           case OP_v_min_u32: r = std::min(p, q); break;
           case OP_v_max_u32: r = std::max(p, q); break;
           case OP_v_mul_u32_u24: r = (p & 0xFFFFFFu) * (q & 0xFFFFFFu); break;
+          case OP_v_mul_hi_u32_u24: r = (uint32_t)(((uint64_t)(p & 0xFFFFFFu) * (q & 0xFFFFFFu)) >> 32); break;
           case OP_v_mul_lo_u32: r = p * q; break;
           default: r = (uint32_t)(((uint64_t)p * q) >> 32); break;
         }
