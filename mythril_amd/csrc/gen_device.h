@@ -46,8 +46,11 @@ __host__ __device__ __forceinline__ uint32_t gext(uint32_t a, uint32_t b, uint32
   return (uint32_t)(((((uint64_t)a) << 32) | b) >> s) + b;
 }
 
+// kf = klo ^ (klo >> 16): gfin's first xor-shift is linear, so (klo ^ salt) ^ ((klo ^ salt) >> 16) =
+// kf ^ (salt ^ (salt >> 16)) — the key's half folded once per group, each draw XORs in its salt's
+// fold (a constant in the compiled kernels, a scalar in the interpreter): one vector op per draw
 struct GKeys {
-  uint32_t klo, khi, glo, ghi;
+  uint32_t klo, khi, glo, ghi, kf;
 };
 
 // lk = gen_lane_key(idx & 63, sk), computed once per lane by kernels whose lanes keep their slot
@@ -59,6 +62,7 @@ __device__ __forceinline__ GKeys gen_keys_lk(uint64_t idx, uint64_t lk, uint64_t
   GKeys k;
   k.klo = (uint32_t)K;
   k.khi = (uint32_t)(K >> 32);
+  k.kf = k.klo ^ (k.klo >> 16);
   k.glo = (uint32_t)G;
   k.ghi = (uint32_t)(G >> 32);
   return k;
@@ -70,7 +74,11 @@ __device__ __forceinline__ GKeys gen_keys(uint64_t idx, uint64_t sk, uint64_t sg
 
 // per-lane random limb j of coordinate c; h(c) = grnd(k, c, 0xFFFF)
 __device__ __forceinline__ uint32_t grnd(const GKeys& k, uint32_t c, uint32_t j) {
-  return gfin(k.klo ^ gsalt(c, j)) + k.khi;
+  const uint32_t s = gsalt(c, j);
+  uint32_t x = k.kf ^ (s ^ (s >> 16));  // = (klo ^ s) ^ ((klo ^ s) >> 16), gfin's first step
+  x = (x & 0xFFFFFFu) * 0x9E3779u;
+  x ^= x >> 15;
+  return x + k.khi;
 }
 
 // per-group choice bits of coordinate c (high 16: alternative, low 16: delta).  Wave-uniform,

@@ -396,7 +396,7 @@ struct Gen {
   void emit_prefetch(const char* Gn) {
     if (pf.empty()) return;
     o << "  { GKeys kn; { const uint64_t K = " << Gn << " ^ LK;\n"
-         "    kn.klo = (uint32_t)K; kn.khi = (uint32_t)(K >> 32); kn.glo = (uint32_t)" << Gn
+         "    kn.klo = (uint32_t)K; kn.khi = (uint32_t)(K >> 32); kn.kf = kn.klo ^ (kn.klo >> 16); kn.glo = (uint32_t)" << Gn
       << "; kn.ghi = (uint32_t)(" << Gn << " >> 32); }\n";
     for (uint32_t c : pf) {
       const GenSpec& sp = (*specs)[c];
@@ -1209,7 +1209,8 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   }
   o << "  GKeys ky;\n"
        "  { const uint64_t K = G ^ LK;\n"
-       "    ky.klo = (uint32_t)K; ky.khi = (uint32_t)(K >> 32); ky.glo = (uint32_t)G; ky.ghi = (uint32_t)(G >> 32); }\n"
+       "    ky.klo = (uint32_t)K; ky.khi = (uint32_t)(K >> 32); ky.kf = ky.klo ^ (ky.klo >> 16); ky.glo = (uint32_t)G;\n"
+       "    ky.ghi = (uint32_t)(G >> 32); }\n"
        "  uint32_t verdict = 1u;\n";
   g.decls();
   g.pf_active = true;
@@ -1274,7 +1275,8 @@ std::string jit_source(const Lowered& P, const std::vector<GenSpec>* specs, cons
   g.emit_group_keys("kk", "g", "gstride");
   o << "  GKeys ky;\n"
        "  { const uint64_t K = G ^ LK;\n"
-       "    ky.klo = (uint32_t)K; ky.khi = (uint32_t)(K >> 32); ky.glo = (uint32_t)G; ky.ghi = (uint32_t)(G >> 32); }\n"
+       "    ky.klo = (uint32_t)K; ky.khi = (uint32_t)(K >> 32); ky.kf = ky.klo ^ (ky.klo >> 16); ky.glo = (uint32_t)G;\n"
+       "    ky.ghi = (uint32_t)(G >> 32); }\n"
        "  uint32_t verdict = 1u;\n";
   g.decls();
   g.body(true);
