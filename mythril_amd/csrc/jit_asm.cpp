@@ -2588,6 +2588,13 @@ struct Gen {
   // e = ((h >> 16) * n) >> 16
   // entry ((h >> 16) * n) >> 16: for n < 256 the high half of the 24-bit product (h >> 16) * (n << 16),
   // one v_mul_hi_u32_u24 for the multiply and the shift (MYTHGPU_JIT_ASM_NO_MULHI24=1: three VALU)
+  static bool aligned_mad() {
+    static const bool on = [] {
+      const char* g = getenv("MYTHGPU_JIT_ASM_ALIGNED_MAD");
+      return !(g && g[0] == '0');
+    }();
+    return on;
+  }
   static bool no_mulhi24() {
     static const bool on = [] {
       const char* g = getenv("MYTHGPU_JIT_ASM_NO_MULHI24");
@@ -3027,6 +3034,26 @@ struct Gen {
         }
         const int32_t sh = (int32_t)sp.p[1];
         const uint32_t k = reach_limbs(&G[sp.p[0]], Lc, sp.p[2] ? sp.p[2] - 1u : 0xFFFFFFFFull, (uint32_t)sh);
+        if (aligned_mad() && k == 2 && Lc >= 2 && sh > 0 && sh <= 6 && m.reg()) {
+          // base + (m << sh) over two limbs as one m * 2^sh + base (v_mad_u64_u32, the base in s[40:41])
+          // instead of two shifts and a carry pair (MYTHGPU_JIT_ASM_ALIGNED_MAD=0: those)
+          const uint32_t rp = E.valloc2();
+          E.salu("s_mov_b32 s40, " + hexs(G[sp.p[0]]), {40});
+          E.salu("s_mov_b32 s41, " + hexs(G[sp.p[0] + 1]), {41});
+          Mask cm;
+          cm.k = 2;
+          cm.s = E.salloc();
+          E.valu("v_mad_u64_u32 v[" + std::to_string(rp) + ":" + std::to_string(rp + 1) + "], " + SP(cm.s) + ", " + VL(m) +
+                     ", " + std::to_string(1 << sh) + ", s[40:41]",
+                 {40, 41}, {cm.s, cm.s + 1});
+          E.srelease(cm);
+          drop(m);
+          r.assign(Lc, Lit(0));
+          r[0] = Limb{LR, rp, E.vgen[rp]};
+          r[1] = Limb{LR, rp + 1, E.vgen[rp + 1]};
+          for (uint32_t j = 2; j < Lc; j++) r[j] = Lit(G[sp.p[0] + j]);
+          break;
+        }
         std::vector<Limb> mw(Lc, Lit(0));
         for (uint32_t j = 0; j < Lc; j++) {
           const int32_t bit0 = (int32_t)(j * 32) - sh;

@@ -45,7 +45,8 @@ CONFIGS = [
     {},
     {"MYTHGPU_EQ_PUSHDOWN": "0", "MYTHGPU_ITE_PRUNE": "0"},
     {"MYTHGPU_JIT_ASM_NO_EQ_CACHE": "1", "MYTHGPU_JIT_ASM_NO_BOOL_LOOKUP": "1", "MYTHGPU_JIT_ASM_EXIT_SKIP": "0",
-     "MYTHGPU_JIT_ASM_LDS_B32": "1", "MYTHGPU_JIT_ASM_NO_DICT_EQ": "1", "MYTHGPU_FOLD_NOT": "0"},
+     "MYTHGPU_JIT_ASM_LDS_B32": "1", "MYTHGPU_JIT_ASM_NO_DICT_EQ": "1", "MYTHGPU_FOLD_NOT": "0",
+     "MYTHGPU_JIT_ASM_NO_KFOLD": "1", "MYTHGPU_JIT_ASM_NO_MULHI24": "1", "MYTHGPU_JIT_ASM_ALIGNED_MAD": "0"},
     {"MYTHGPU_JIT_ASM_NOPOOL": "1", "MYTHGPU_EQ_PUSHDOWN": "1", "MYTHGPU_JIT_ASM_GLDS": "1"},
 ]
 

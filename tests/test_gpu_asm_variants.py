@@ -1,7 +1,8 @@
 """The first tier's round-6 code paths against their predecessors on the GPU: limb-pair dictionary
 reads (``ds_read_b64``) vs one limb per read (``MYTHGPU_JIT_ASM_LDS_B32=1``), dictionary-index
-compares vs the XOR/OR reduction (``MYTHGPU_JIT_ASM_NO_DICT_EQ=1``), and the specialiser's
-NOT(compare) folding vs the two instructions (``MYTHGPU_FOLD_NOT=0``).  Each variant runs in its own
+compares vs the XOR/OR reduction (``MYTHGPU_JIT_ASM_NO_DICT_EQ=1``), the specialiser's
+NOT(compare) folding vs the two instructions (``MYTHGPU_FOLD_NOT=0``), and the generator's folded
+key, one-multiply dictionary index and one-instruction ALIGNED offset vs their first forms.  Each variant runs in its own
 process (the switches are read once) over the same full-sweep windows; every first hit and hit
 count equals the C port's (``oracle/bveval.c``), so each variant is checked, not only compared.
 
@@ -52,7 +53,8 @@ def _run(env):
     {"MYTHGPU_JIT_ASM_LDS_B32": "1"},
     {"MYTHGPU_JIT_ASM_NO_DICT_EQ": "1"},
     {"MYTHGPU_FOLD_NOT": "0"},
-], ids=["default", "lds_b32", "no_dict_eq", "no_fold_not"])
+    {"MYTHGPU_JIT_ASM_NO_KFOLD": "1", "MYTHGPU_JIT_ASM_NO_MULHI24": "1", "MYTHGPU_JIT_ASM_ALIGNED_MAD": "0"},
+], ids=["default", "lds_b32", "no_dict_eq", "no_fold_not", "generator_v1"])
 def test_first_tier_variant_matches_c_port(variant):
     from mythril_amd import search, workloads
     from oracle import cport
