@@ -640,6 +640,19 @@ struct Gen {
           << "; uint32_t cy = 0u;\n";
         const int32_t sh = (int32_t)sp.p[1];
         const uint32_t k = reach_limbs(&G[sp.p[0]], L, sp.p[2] ? sp.p[2] - 1u : 0xFFFFFFFFull, (uint32_t)sh);
+        static const bool wide = [] {  // MYTHGPU_JIT_ALIGNED64=0: the limb-wise carry chain
+          const char* g = getenv("MYTHGPU_JIT_ALIGNED64");
+          return !(g && g[0] == '0');
+        }();
+        if (wide && k == 2 && L >= 2 && sh >= 0 && sh < 32) {
+          // the offset reaches two limbs: one 64-bit (m << sh) + base (v_lshl_add_u64 / v_mad_u64_u32)
+          const uint64_t base = ((uint64_t)G[sp.p[0] + 1] << 32) | G[sp.p[0]];
+          o << "  { const uint64_t s64 = (m << " << sh << ") + " << base << "ull;\n";
+          o << "  " << lim(0) << " = (uint32_t)s64;\n  " << lim(1) << " = (uint32_t)(s64 >> 32); }\n";
+          for (uint32_t j = 2; j < L; j++) o << "  " << lim(j) << " = " << hex(G[sp.p[0] + j]) << ";\n";
+          o << "  (void)cy;\n";
+          break;
+        }
         for (uint32_t j = 0; j < L; j++) {
           const int32_t bit0 = (int32_t)(j * 32) - sh;
           std::string mw;
